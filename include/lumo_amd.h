@@ -1,0 +1,261 @@
+/* lumo_amd: MI355X (gfx950) wavefront path tracer behind a C ABI.
+ *
+ * This header is the drop-in boundary for lumo's render hot path (ekarpp/lumo v0.6.1).
+ * Every entry point names the reference interface it replaces (paths relative to the
+ * lumo source tree).  Plain C: fixed-width integers, doubles, pointers and sizes only.
+ * All calls return lumo_status (0 = OK); no exceptions cross the ABI.  A context is
+ * bound to one GPU and is thread-compatible (one host thread per context; contexts on
+ * different GPUs may be driven concurrently).
+ */
+#ifndef LUMO_AMD_H
+#define LUMO_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LUMO_ABI_VERSION 1
+
+typedef int32_t lumo_status;
+enum {
+    LUMO_OK = 0,
+    LUMO_ERR_INVALID = 1,     /* bad argument / malformed scene            */
+    LUMO_ERR_NO_DEVICE = 2,   /* HIP device missing or not gfx950           */
+    LUMO_ERR_HIP = 3,         /* HIP runtime error                          */
+    LUMO_ERR_NO_SCENE = 4,    /* render/trace before lumo_scene_upload      */
+    LUMO_ERR_NO_CAMERA = 5,   /* render before lumo_camera_set              */
+    LUMO_ERR_UNSUPPORTED = 6, /* feature outside the implemented scope      */
+    LUMO_ERR_OOM = 7
+};
+
+/* ---------------------------------------------------------------------------------
+ * Flattened scene (the device image of lumo's Scene, src/tracer/scene.rs:17-29).
+ * Produced on the host by lumo_amd's scene builder (or by lumo's own Rust Scene after
+ * build(): the arrays below are exactly its BVH / kd-tree node arrays), copied to HBM
+ * by lumo_scene_upload.  The caller owns all host arrays.
+ * ------------------------------------------------------------------------------- */
+
+/* Spectrum as sigmoid polynomial, f32 (spectrum.rs:14-19). */
+typedef struct {
+    float c0, c1, c2, scale;
+} lumo_spectrum;
+
+enum {
+    LUMO_MAT_BLANK = 0,
+    LUMO_MAT_LAMBERTIAN = 1,   /* BxDF::Lambertian (bxdf/scatter.rs:3-27)          */
+    LUMO_MAT_LIGHT = 2,        /* Material::Light (material.rs:15, 223-234)         */
+    LUMO_MAT_MF_DIFFUSE = 3,   /* BxDF::MfDiffuse   (not yet on the GPU path)       */
+    LUMO_MAT_MF_CONDUCTOR = 4, /* BxDF::MfConductor (not yet on the GPU path)       */
+    LUMO_MAT_MF_DIELECTRIC = 5 /* BxDF::MfDielectric(not yet on the GPU path)       */
+};
+
+typedef struct {
+    int32_t kind;       /* LUMO_MAT_*                                           */
+    int32_t two_sided;  /* Light: emits from the back face too                   */
+    int32_t illuminant; /* Light: index into dense_spectra                       */
+    int32_t eta_idx;    /* microfacet: dense_spectra index of eta                */
+    int32_t k_idx;      /* microfacet: dense_spectra index of k                  */
+    int32_t pad0;
+    double scale;       /* Light: emission scale                                 */
+    double roughness;   /* microfacet: max(roughness, 1e-5)                      */
+    lumo_spectrum albedo; /* Lambertian spectrum / Light texture / kd             */
+    lumo_spectrum ks;
+    lumo_spectrum tf;
+} lumo_material;
+
+/* lumo BVH node (object/bvh.rs:18-26, bvh/node.rs:8-14), depth-first layout:
+ * left child = index + 1, `right` = index of the right child or -1.
+ * A leaf has count > 0: items[first .. first+count) are object indices. */
+typedef struct {
+    double bmin[3], bmax[3];
+    int32_t right;
+    int32_t first;
+    int32_t count;
+    int32_t pad0;
+} lumo_bvh_node;
+
+/* lumo kd-tree node (object/kdtree/node.rs:24-31), pre-order layout:
+ * left child = index + 1; leaf: items[first .. first+count) are triangle indices
+ * local to the owning object. */
+typedef struct {
+    double point;
+    int32_t axis;
+    int32_t right;
+    int32_t leaf;
+    int32_t first;
+    int32_t count;
+    int32_t pad0;
+} lumo_kd_node;
+
+enum {
+    LUMO_OBJ_KDMESH = 0,   /* KdTree<Triangle> (TriangleMesh::new, triangle_mesh.rs:46-60) */
+    LUMO_OBJ_RECTANGLE = 1 /* Rectangle (object/rectangle.rs): 2-triangle kd mesh + uv/sampling */
+};
+
+typedef struct {
+    int32_t type;      /* LUMO_OBJ_*                                     */
+    int32_t material;  /* material of the mesh (KdTree::material)        */
+    int32_t kd_root;   /* index of the root in kd_nodes                  */
+    int32_t tri_base;  /* first triangle of this object in triangles[]   */
+    int32_t item_base; /* kd leaf item lists live in kd_items[item_base..] */
+    int32_t num_tris;
+    double bmin[3], bmax[3]; /* kd boundary (KdTree::boundary)             */
+    double origin[3], b0[3], b1[3]; /* Rectangle parameters (rectangle.rs:6-13) */
+    double area;       /* Sampleable::area                              */
+} lumo_object;
+
+typedef struct {
+    int32_t v[3];   /* vertex indices into vertices[]                 */
+    int32_t n[3];   /* shading-normal indices or -1                   */
+    int32_t t[3];   /* uv indices or -1                               */
+    int32_t material;
+} lumo_triangle;
+
+typedef struct {
+    /* geometry */
+    int32_t num_vertices, num_normals, num_uvs, num_triangles;
+    const double* vertices; /* xyz f64 */
+    const double* normals;  /* xyz f64 */
+    const double* uvs;      /* uv f64  */
+    const lumo_triangle* triangles;
+    /* per-object kd-trees */
+    int32_t num_kd_nodes, num_kd_items;
+    const lumo_kd_node* kd_nodes;
+    const int32_t* kd_items;
+    /* objects BVH (Scene::objects) */
+    int32_t num_objects, num_object_nodes, num_object_items;
+    const lumo_object* objects;
+    const lumo_bvh_node* object_nodes;
+    const int32_t* object_items;
+    /* lights BVH (Scene::lights) + power alias table (bvh.rs:105-191) */
+    int32_t num_lights, num_light_nodes, num_light_items;
+    const lumo_object* lights;
+    const lumo_bvh_node* light_nodes;
+    const int32_t* light_items;
+    const double* alias_prob;  /* alias_table[i].0 */
+    const int32_t* alias_idx;  /* alias_table[i].1 */
+    const double* alias_pdf;   /* alias_pdf[i]     */
+    /* materials and 95-bin dense spectra (dense_spectrum.rs) */
+    int32_t num_materials, num_dense_spectra;
+    const lumo_material* materials;
+    const double* dense_spectra; /* num_dense_spectra x 95 */
+} lumo_scene_desc;
+
+/* Camera (camera.rs:17-38, CameraConfig): world_to_camera, screen_to_raster and
+ * camera_to_screen transforms as (m, inv) row-major 4x4 pairs. Perspective only. */
+typedef struct {
+    double world_to_camera[2][16];
+    double screen_to_raster[2][16];
+    double camera_to_screen[2][16];
+    double lens_radius, focal_length;
+    int64_t width, height;
+    int32_t orthographic; /* 0 = Perspective */
+    int32_t illuminant;   /* dense_spectra index used for white balance */
+    double white_balance[9];   /* ColorSpace::wb_matrix (space.rs:144-151), row-major */
+    double xyz_to_rgb[9];      /* colour space XYZ->RGB (default DCI-P3, space.rs:51-54) */
+    double filter_radius, filter_sigma; /* PixelFilter::Gaussian (filter.rs:20-24) */
+} lumo_camera_desc;
+
+/* RenderTask (renderer/task.rs:86-104): one tile x one sample batch. */
+typedef struct {
+    uint64_t px_min[2], px_max[2]; /* tile [px_min, px_max) in raster space */
+    uint64_t batch;                /* sample batch index (256 spp per batch) */
+    uint64_t samples;              /* samples in this batch                  */
+    uint64_t total_samples;        /* Renderer::num_samples                  */
+    uint64_t seed;                 /* task seed from the renderer stream     */
+} lumo_tile_task;
+
+/* RenderTaskResult (renderer/task.rs:106-116) + its FilmTile pixels (film/tile.rs).
+ * `rgb_w` is caller-allocated: 4 doubles (sum w*r, w*g, w*b, sum w) per pixel of the
+ * tile, row-major over [px_min, px_max). */
+typedef struct {
+    double* rgb_w;
+    uint64_t num_camera_rays;
+    uint64_t num_rays;       /* sum of FilmSample.cost (path depth), task.rs:65 */
+    uint64_t num_queries;    /* closest-hit + shadow visibility queries issued  */
+} lumo_tile_result;
+
+enum { LUMO_RNG_WAVEFRONT = 0, LUMO_RNG_LUMO_ORDER = 1 };
+enum { LUMO_INTEGRATOR_PATH_TRACE = 0 };
+
+typedef struct {
+    int32_t integrator; /* LUMO_INTEGRATOR_*                              */
+    int32_t rng_mode;   /* LUMO_RNG_WAVEFRONT (GPU); lumo-order: oracle only */
+    int32_t max_paths;  /* cap on paths in flight (0 = all pixels of the call) */
+    int32_t pad0;
+} lumo_render_cfg;
+
+/* Ray batch for traversal-only queries (parity + micro-benchmarks). */
+typedef struct {
+    const double* origin; /* n x 3 */
+    const double* dir;    /* n x 3 */
+    const double* t_max;  /* n (closest: ignored, INF) */
+    const int32_t* light; /* n: light index for visibility queries (any_hit mode) */
+} lumo_ray_soa;
+
+typedef struct {
+    double* t;       /* closest: hit t (INF on miss); visibility: light t or INF if occluded */
+    int32_t* kind;   /* 0 miss, 1 object, 2 light                                      */
+    int32_t* object; /* object / light index                                           */
+    int32_t* prim;   /* triangle index (global)                                        */
+} lumo_hit_soa;
+
+/* Per-stage device time (HIP events; only with LUMO_TIMING=1 in the environment), launch
+ * counts, query counts and traversal counters (AABB slab tests, kd split-node visits,
+ * triangle tests) of the closest-hit [0] and shadow [1] kernels, summed over renders. */
+enum { LUMO_STAGE_CAMERA = 0, LUMO_STAGE_CLOSEST, LUMO_STAGE_SHADE, LUMO_STAGE_SHADOW, LUMO_STAGE_RESOLVE,
+       LUMO_STAGE_FINISH, LUMO_STAGE_FILM, LUMO_STAGE_RING };
+typedef struct {
+    double kernel_ms[8];
+    uint64_t launches[8];
+    uint64_t closest_queries, shadow_queries, bounces;
+    uint64_t aabb_tests[2], kd_nodes[2], tri_tests[2];
+} lumo_stats;
+
+/* Per-path dump of one task (test hook for per-path parity): arrays sized samples x pixels
+ * (pass-major, pixel raster order within the tile); delta has one entry per pass. */
+typedef struct {
+    double* radiance;  /* 4 per path */
+    double* lambda_;   /* 4 per path */
+    double* raster;    /* 2 per path */
+    uint64_t* depth;
+    double* delta;
+} lumo_path_dump;
+
+/* --- context ---------------------------------------------------------------------- */
+/* Replaces: ThreadPool::new + RenderTaskExecutor::new (pool.rs:17-38, task.rs:12-21). */
+lumo_status lumo_create(int device, void** ctx_out);
+void lumo_destroy(void* ctx);
+const char* lumo_status_str(lumo_status st);
+int lumo_abi_version(void);
+/* Number of visible GPUs (0 when the HIP runtime has none). */
+int lumo_device_count(void);
+
+/* Replaces: Renderer::new(scene, ...) -> scene.build() + Arc<Scene> (renderer.rs:40-63). */
+lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* scene);
+/* Replaces: Arc<Camera> shared with the executor (task.rs:4-10). */
+lumo_status lumo_camera_set(void* ctx, const lumo_camera_desc* camera);
+
+/* Replaces: Executor<RenderTask, RenderTaskResult>::exec (pool.rs:6-8, task.rs:24-82),
+ * batched: all n tasks are rendered as one wavefront. */
+lumo_status lumo_render_tiles(void* ctx, const lumo_tile_task* tasks, size_t n,
+                              const lumo_render_cfg* cfg, lumo_tile_result* out);
+
+/* Replaces: Scene::hit (scene.rs:119-147) when any_hit == 0, and
+ * Scene::hit_light (scene.rs:165-189) when any_hit != 0.  Host buffers in and out. */
+lumo_status lumo_trace(void* ctx, const lumo_ray_soa* rays, size_t n, lumo_hit_soa* hits,
+                       int any_hit);
+
+lumo_status lumo_stats_get(void* ctx, lumo_stats* stats);
+lumo_status lumo_stats_reset(void* ctx);
+
+/* Test hook: render one task in the wavefront order and dump every path. */
+lumo_status lumo_debug_paths(void* ctx, const lumo_tile_task* task, lumo_path_dump* dump);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LUMO_AMD_H */

@@ -1,0 +1,70 @@
+/* lumo_amd host API: scene / camera construction mirroring lumo's builder API
+ * (Scene, Material, Spectrum, TriangleMesh, Rectangle, Camera::builder, Renderer task
+ * generation, Film).  Produces the lumo_scene_desc / lumo_camera_desc / lumo_tile_task
+ * records that the device boundary (lumo_amd.h) consumes.  CPU only; part of the product.
+ */
+#ifndef LUMO_HOST_H
+#define LUMO_HOST_H
+#include "lumo_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Spectrum constructors (spectrum.rs:38-93) */
+lumo_spectrum lumo_spectrum_from_rgb(double r, double g, double b);
+lumo_spectrum lumo_spectrum_from_srgb(int r, int g, int b);
+lumo_spectrum lumo_spectrum_from_pts(const char* pts);
+/* rgb2spec table cell (maxc, z, y, x) -> c0,c1,c2 (tables.rs data) */
+void lumo_rgb2spec_cell(int l, int k, int j, int i, float out[3]);
+int lumo_rgb2spec_write(const char* path, int threads);
+
+/* Scene builder (scene.rs add / add_light, material.rs constructors) */
+void* lumo_builder_new(void);
+void lumo_builder_free(void* b);
+int lumo_builder_material_lambertian(void* b, lumo_spectrum spec);
+/* Material::Light(texture, illuminant, scale, two_sided); illuminant = builtin dense id */
+int lumo_builder_material_light(void* b, lumo_spectrum tex, int illuminant, double scale, int two_sided);
+/* TriangleMesh::new: vertices (nv x 3), faces as concatenated index lists with sizes. */
+int lumo_builder_add_mesh(void* b, const double* vertices, int64_t nv, const int64_t* face_idx,
+                          const int64_t* face_sizes, int64_t nfaces, int material, int as_light);
+/* Rectangle::new(Mat3(a, b, c), material) */
+int lumo_builder_add_rectangle(void* b, const double* a, const double* bb, const double* c, int material,
+                               int as_light);
+/* Scene::cornell_box() */
+void* lumo_builder_cornell_box(void);
+/* Scene::build + flatten; returns an owning flat scene (free with lumo_scene_free). */
+void* lumo_builder_build(void* b);
+int lumo_scene_get_desc(void* scene, lumo_scene_desc* out);
+void lumo_scene_free(void* scene);
+
+/* Builtin dense spectra ids (color/illuminants, color/materials) */
+enum {
+    LUMO_DENSE_CIE_X = 0, LUMO_DENSE_CIE_Y, LUMO_DENSE_CIE_Z, LUMO_DENSE_A, LUMO_DENSE_D50, LUMO_DENSE_D65,
+    LUMO_DENSE_F2, LUMO_DENSE_F7, LUMO_DENSE_CORNELL, LUMO_DENSE_GLASS_ETA, LUMO_DENSE_DIAMOND_ETA,
+    LUMO_DENSE_MIRROR_ETA, LUMO_DENSE_MIRROR_K
+};
+
+/* Camera::builder() (camera/builder.rs) */
+typedef struct {
+    double origin[3], towards[3], up[3];
+    double zoom, lens_radius, focal_length, vfov;
+    int64_t width, height;
+    int32_t illuminant;  /* LUMO_DENSE_* */
+    int32_t color_space; /* 0 sRGB, 1 DCI-P3 (default), 2 Rec. 2020 */
+    double filter_radius, filter_sigma;
+} lumo_camera_params;
+void lumo_camera_params_default(lumo_camera_params* p);
+void lumo_camera_params_cornell_box(lumo_camera_params* p);
+int lumo_camera_build(const lumo_camera_params* p, lumo_camera_desc* out);
+
+/* Renderer::render task list (renderer.rs:179-204): batches of 256 spp x 16^2 tiles, each
+ * task seeded by the renderer's Xorshift stream.  Returns the number of tasks (writes at
+ * most `cap` of them when tasks != NULL). */
+int64_t lumo_make_tasks(int64_t width, int64_t height, uint64_t samples, uint64_t seed, lumo_tile_task* tasks,
+                        int64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

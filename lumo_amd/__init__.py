@@ -1,0 +1,353 @@
+"""lumo_amd — MI355X (gfx950) wavefront path tracer with lumo's API.
+
+Python mirror of lumo's builder API (ekarpp/lumo v0.6.1) over the C ABI in include/:
+    Spectrum.from_rgb / from_srgb / from_pts          (src/tracer/color/spectrum.rs)
+    Material.lambertian / Material.light               (src/tracer/material.rs)
+    Scene() .add_mesh / .add_rectangle / cornell_box() (src/tracer/scene.rs, scene/cornell_box.rs)
+    Camera.builder() ... .build(), Camera.cornell_box()(src/tracer/camera*.rs)
+    Renderer(scene, camera).samples(n).seed(s).render() -> Film   (src/renderer.rs)
+
+Scene construction runs in the C++ host library; rendering runs only on the GPU through
+lumo_render_tiles (the replacement of lumo's RenderTaskExecutor::exec).  There is no CPU
+fallback: without a gfx950 device, Renderer.render raises.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _ffi
+from ._ffi import check
+
+__all__ = ["Spectrum", "Material", "Scene", "Camera", "Renderer", "Integrator", "Film", "Device",
+           "DENSE", "TILE_SIZE", "SAMPLES_INCREMENT", "make_tasks"]
+
+TILE_SIZE = 16          # renderer.rs:15
+SAMPLES_INCREMENT = 256  # renderer.rs:17
+DENSE = {"CIE_X": 0, "CIE_Y": 1, "CIE_Z": 2, "A": 3, "D50": 4, "D65": 5, "F2": 6, "F7": 7, "CORNELL": 8,
+         "GLASS_ETA": 9, "DIAMOND_ETA": 10, "MIRROR_ETA": 11, "MIRROR_K": 12}
+
+
+def lib():
+    return _ffi.load()
+
+
+class Spectrum:
+    """Sigmoid-polynomial spectrum (spectrum.rs:14-19): c0, c1, c2 (f32) and scale."""
+
+    def __init__(self, s):
+        self._s = s
+
+    @staticmethod
+    def from_rgb(r, g, b):
+        return Spectrum(lib().lumo_spectrum_from_rgb(r, g, b))
+
+    @staticmethod
+    def from_srgb(r, g, b):
+        return Spectrum(lib().lumo_spectrum_from_srgb(r, g, b))
+
+    @staticmethod
+    def from_pts(pts):
+        return Spectrum(lib().lumo_spectrum_from_pts(pts.encode()))
+
+    @property
+    def coeffs(self):
+        return (self._s.c0, self._s.c1, self._s.c2)
+
+    @property
+    def scale(self):
+        return self._s.scale
+
+    def is_black(self):
+        return self._s.scale == 0.0
+
+
+Spectrum.WHITE = None  # filled lazily (needs the library)
+
+
+class Material:
+    def __init__(self, kind, **kw):
+        self.kind = kind
+        self.kw = kw
+
+    @staticmethod
+    def lambertian(spec):
+        return Material("lambertian", spec=spec)
+
+    @staticmethod
+    def light(tex, illuminant="D65", scale=1.0, two_sided=False):
+        """Material::Light(texture, illuminant, scale, two_sided); Material::light uses D65."""
+        return Material("light", spec=tex, illuminant=illuminant, scale=scale, two_sided=two_sided)
+
+    def _add(self, b):
+        L = lib()
+        if self.kind == "lambertian":
+            return L.lumo_builder_material_lambertian(b, self.kw["spec"]._s)
+        ill = self.kw["illuminant"]
+        ill = DENSE[ill] if isinstance(ill, str) else int(ill)
+        return L.lumo_builder_material_light(b, self.kw["spec"]._s, ill, float(self.kw["scale"]),
+                                             int(bool(self.kw["two_sided"])))
+
+
+class Scene:
+    """lumo Scene: objects + lights; build() produces the flattened device image."""
+
+    def __init__(self, _builder=None):
+        L = lib()
+        self._b = _builder if _builder is not None else L.lumo_builder_new()
+        self._flat = None
+
+    @staticmethod
+    def cornell_box():
+        return Scene(lib().lumo_builder_cornell_box())
+
+    def _mat(self, m):
+        idx = m._add(self._b)
+        if idx < 0:
+            raise ValueError("invalid material")
+        return idx
+
+    def add_mesh(self, vertices, faces, material, light=False):
+        """TriangleMesh::new(vertices, faces, [], [], material) added with Scene::add."""
+        v = np.ascontiguousarray(np.asarray(vertices, dtype=np.float64).reshape(-1, 3))
+        sizes = np.asarray([len(f) for f in faces], dtype=np.int64)
+        idx = np.asarray([i for f in faces for i in f], dtype=np.int64)
+        m = self._mat(material)
+        st = lib().lumo_builder_add_mesh(self._b, v.ctypes.data_as(_ffi.c_double_p), len(v),
+                                         idx.ctypes.data_as(_ffi.c_int64_p), sizes.ctypes.data_as(_ffi.c_int64_p),
+                                         len(sizes), m, int(light))
+        check(st, "add_mesh")
+        self._flat = None
+
+    def add_rectangle(self, a, b, c, material, light=False):
+        """Rectangle::new(Mat3::new(a, b, c), material) via Scene::add / Scene::add_light."""
+        arr = [np.ascontiguousarray(np.asarray(x, dtype=np.float64)) for x in (a, b, c)]
+        m = self._mat(material)
+        st = lib().lumo_builder_add_rectangle(self._b, *[x.ctypes.data_as(_ffi.c_double_p) for x in arr], m,
+                                              int(light))
+        check(st, "add_rectangle")
+        self._flat = None
+
+    def build(self):
+        if self._flat is None:
+            p = lib().lumo_builder_build(self._b)
+            if not p:
+                raise ValueError("scene build failed (no lights?)")
+            self._flat = C.c_void_p(p)
+        return self
+
+    def desc(self):
+        self.build()
+        d = _ffi.SceneDesc()
+        check(lib().lumo_scene_get_desc(self._flat, C.byref(d)), "scene desc")
+        return d
+
+    def __del__(self):
+        try:
+            L = _ffi._lib
+            if L is not None:
+                if self._flat is not None:
+                    L.lumo_scene_free(self._flat)
+                L.lumo_builder_free(self._b)
+        except Exception:
+            pass
+
+
+class Camera:
+    class Builder:
+        def __init__(self, params):
+            self.p = params
+
+        def origin(self, x, y, z):
+            self.p.origin[:] = [x, y, z]
+            return self
+
+        def towards(self, x, y, z):
+            self.p.towards[:] = [x, y, z]
+            return self
+
+        def up(self, x, y, z):
+            self.p.up[:] = [x, y, z]
+            return self
+
+        def zoom(self, z):
+            self.p.zoom = z
+            return self
+
+        def lens_radius(self, r):
+            self.p.lens_radius = r
+            return self
+
+        def focal_length(self, f):
+            self.p.focal_length = f
+            return self
+
+        def resolution(self, wh):
+            self.p.width, self.p.height = int(wh[0]), int(wh[1])
+            return self
+
+        def vfov(self, v):
+            self.p.vfov = v
+            return self
+
+        def illuminant(self, name):
+            self.p.illuminant = DENSE[name] if isinstance(name, str) else int(name)
+            return self
+
+        def build(self):
+            d = _ffi.CameraDesc()
+            check(lib().lumo_camera_build(C.byref(self.p), C.byref(d)), "camera build")
+            return Camera(d, (self.p.width, self.p.height))
+
+    def __init__(self, desc, resolution):
+        self.desc = desc
+        self.resolution = resolution
+
+    @staticmethod
+    def builder():
+        p = _ffi.CameraParams()
+        lib().lumo_camera_params_default(C.byref(p))
+        return Camera.Builder(p)
+
+    @staticmethod
+    def cornell_box_builder():
+        p = _ffi.CameraParams()
+        lib().lumo_camera_params_cornell_box(C.byref(p))
+        return Camera.Builder(p)
+
+    @staticmethod
+    def cornell_box(resolution=(512, 512)):
+        return Camera.cornell_box_builder().resolution(resolution).build()
+
+
+class Integrator:
+    PathTrace = 0
+
+
+def make_tasks(width, height, samples, seed):
+    """renderer.rs:179-204: (batch, tile) tasks in publish order with their stream seeds."""
+    L = lib()
+    n = L.lumo_make_tasks(width, height, samples, seed, None, 0)
+    arr = (_ffi.TileTask * n)()
+    L.lumo_make_tasks(width, height, samples, seed, arr, n)
+    return arr
+
+
+class Film:
+    """Film pixels (film.rs:57-92): per pixel sum of w*rgb and sum of w (PIXEL_BUFFERS = 1)."""
+
+    def __init__(self, width, height):
+        self.width, self.height = width, height
+        self.pixels = np.zeros((height, width, 4), dtype=np.float64)
+
+    def add_tile(self, task, rgb_w):
+        """Film::add_tile (film.rs:155-171)."""
+        x0, y0 = task.px_min[0], task.px_min[1]
+        x1, y1 = task.px_max[0], task.px_max[1]
+        self.pixels[y0:y1, x0:x1, :] += rgb_w.reshape(y1 - y0, x1 - x0, 4)
+
+    def rgb(self):
+        """Pixel::value (film.rs:82-91): sum(w*rgb) / sum(w), linear colour-space RGB."""
+        with np.errstate(invalid="ignore", divide="ignore"):
+            return self.pixels[..., :3] / self.pixels[..., 3:4]
+
+
+class Device:
+    """One lumo_amd context bound to one GPU (lumo_create)."""
+
+    def __init__(self, device=0):
+        L = lib()
+        ctx = C.c_void_p()
+        st = L.lumo_create(device, C.byref(ctx))
+        if st != _ffi.LUMO_OK:
+            raise RuntimeError(f"lumo_create(device={device}) failed: {L.lumo_status_str(st).decode()}")
+        self.ctx = ctx
+        self.scene = None
+
+    def upload(self, scene, camera):
+        L = lib()
+        self._scene_desc = scene.desc()
+        check(L.lumo_scene_upload(self.ctx, C.byref(self._scene_desc)), "scene upload")
+        check(L.lumo_camera_set(self.ctx, C.byref(camera.desc)), "camera set")
+        self.scene = scene
+
+    def render_tasks(self, tasks, max_paths=0):
+        """lumo_render_tiles over `tasks`; returns per-task (rgb_w array, result)."""
+        L = lib()
+        n = len(tasks)
+        bufs, res = [], (_ffi.TileResult * n)()
+        for i, t in enumerate(tasks):
+            P = (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1])
+            b = np.zeros(4 * P, dtype=np.float64)
+            bufs.append(b)
+            res[i].rgb_w = b.ctypes.data_as(_ffi.c_double_p)
+        arr = tasks if isinstance(tasks, C.Array) else (_ffi.TileTask * n)(*tasks)
+        cfg = _ffi.RenderCfg(0, 0, max_paths, 0)
+        check(L.lumo_render_tiles(self.ctx, arr, n, C.byref(cfg), res), "render_tiles")
+        return bufs, res
+
+    def stats(self):
+        s = _ffi.Stats()
+        check(lib().lumo_stats_get(self.ctx, C.byref(s)), "stats")
+        return s
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            lib().lumo_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Renderer:
+    """Renderer::new(scene, camera) builder (renderer.rs:24-100); GPU tile dispatch."""
+
+    def __init__(self, scene, camera):
+        self.scene = scene.build()
+        self.camera = camera
+        self._samples = 1
+        self._seed = None
+        self._integrator = Integrator.PathTrace
+        self._device = 0
+
+    def samples(self, n):
+        self._samples = int(n)
+        return self
+
+    def seed(self, s):
+        self._seed = int(s)
+        return self
+
+    def integrator(self, i):
+        if i != Integrator.PathTrace:
+            raise NotImplementedError("only Integrator.PathTrace is on the GPU path")
+        self._integrator = i
+        return self
+
+    def device(self, d):
+        self._device = int(d)
+        return self
+
+    def render(self, rank=0, world_size=1):
+        """Render all (batch, tile) tasks; with world_size > 1 this rank renders the tiles
+        with tile_index % world_size == rank and returns its partial film."""
+        import time
+        if self._seed is None:
+            self._seed = time.time_ns() & 0xFFFFFFFFFFFFFFFF or 1
+        w, h = self.camera.resolution
+        tasks = make_tasks(w, h, self._samples, self._seed)
+        tiles_per_batch = ((w + TILE_SIZE - 1) // TILE_SIZE) * ((h + TILE_SIZE - 1) // TILE_SIZE)
+        mine = [t for i, t in enumerate(tasks) if (i % tiles_per_batch) % world_size == rank]
+        dev = Device(self._device)
+        dev.upload(self.scene, self.camera)
+        film = Film(w, h)
+        bufs, res = dev.render_tasks(mine)
+        for t, b in zip(mine, bufs):
+            film.add_tile(t, b)
+        self.num_rays = sum(r.num_rays for r in res)
+        self.num_camera_rays = sum(r.num_camera_rays for r in res)
+        dev.close()
+        return film

@@ -1,0 +1,191 @@
+"""ctypes mirror of include/lumo_amd.h and include/lumo_host.h (the C-ABI boundary).
+
+Only plain C types cross the boundary; no torch types.  `load()` loads the in-tree
+liblumo_amd.so built by `make` (or __graft_entry__.build()).  The product raises if the
+library is missing: there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblumo_amd.so")
+
+c_double_p = C.POINTER(C.c_double)
+c_int32_p = C.POINTER(C.c_int32)
+c_int64_p = C.POINTER(C.c_int64)
+c_uint64_p = C.POINTER(C.c_uint64)
+
+LUMO_OK = 0
+STATUS = {0: "OK", 1: "INVALID", 2: "NO_DEVICE", 3: "HIP", 4: "NO_SCENE", 5: "NO_CAMERA",
+          6: "UNSUPPORTED", 7: "OOM"}
+
+
+class Spectrum(C.Structure):
+    _fields_ = [("c0", C.c_float), ("c1", C.c_float), ("c2", C.c_float), ("scale", C.c_float)]
+
+
+class Material(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("two_sided", C.c_int32), ("illuminant", C.c_int32),
+                ("eta_idx", C.c_int32), ("k_idx", C.c_int32), ("pad0", C.c_int32),
+                ("scale", C.c_double), ("roughness", C.c_double),
+                ("albedo", Spectrum), ("ks", Spectrum), ("tf", Spectrum)]
+
+
+class BvhNode(C.Structure):
+    _fields_ = [("bmin", C.c_double * 3), ("bmax", C.c_double * 3), ("right", C.c_int32),
+                ("first", C.c_int32), ("count", C.c_int32), ("pad0", C.c_int32)]
+
+
+class KdNode(C.Structure):
+    _fields_ = [("point", C.c_double), ("axis", C.c_int32), ("right", C.c_int32), ("leaf", C.c_int32),
+                ("first", C.c_int32), ("count", C.c_int32), ("pad0", C.c_int32)]
+
+
+class Object(C.Structure):
+    _fields_ = [("type", C.c_int32), ("material", C.c_int32), ("kd_root", C.c_int32), ("tri_base", C.c_int32),
+                ("item_base", C.c_int32), ("num_tris", C.c_int32), ("bmin", C.c_double * 3),
+                ("bmax", C.c_double * 3), ("origin", C.c_double * 3), ("b0", C.c_double * 3),
+                ("b1", C.c_double * 3), ("area", C.c_double)]
+
+
+class Triangle(C.Structure):
+    _fields_ = [("v", C.c_int32 * 3), ("n", C.c_int32 * 3), ("t", C.c_int32 * 3), ("material", C.c_int32)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [
+        ("num_vertices", C.c_int32), ("num_normals", C.c_int32), ("num_uvs", C.c_int32),
+        ("num_triangles", C.c_int32),
+        ("vertices", c_double_p), ("normals", c_double_p), ("uvs", c_double_p),
+        ("triangles", C.POINTER(Triangle)),
+        ("num_kd_nodes", C.c_int32), ("num_kd_items", C.c_int32),
+        ("kd_nodes", C.POINTER(KdNode)), ("kd_items", c_int32_p),
+        ("num_objects", C.c_int32), ("num_object_nodes", C.c_int32), ("num_object_items", C.c_int32),
+        ("objects", C.POINTER(Object)), ("object_nodes", C.POINTER(BvhNode)), ("object_items", c_int32_p),
+        ("num_lights", C.c_int32), ("num_light_nodes", C.c_int32), ("num_light_items", C.c_int32),
+        ("lights", C.POINTER(Object)), ("light_nodes", C.POINTER(BvhNode)), ("light_items", c_int32_p),
+        ("alias_prob", c_double_p), ("alias_idx", c_int32_p), ("alias_pdf", c_double_p),
+        ("num_materials", C.c_int32), ("num_dense_spectra", C.c_int32),
+        ("materials", C.POINTER(Material)), ("dense_spectra", c_double_p),
+    ]
+
+
+class CameraDesc(C.Structure):
+    _fields_ = [
+        ("world_to_camera", (C.c_double * 16) * 2), ("screen_to_raster", (C.c_double * 16) * 2),
+        ("camera_to_screen", (C.c_double * 16) * 2),
+        ("lens_radius", C.c_double), ("focal_length", C.c_double),
+        ("width", C.c_int64), ("height", C.c_int64),
+        ("orthographic", C.c_int32), ("illuminant", C.c_int32),
+        ("white_balance", C.c_double * 9), ("xyz_to_rgb", C.c_double * 9),
+        ("filter_radius", C.c_double), ("filter_sigma", C.c_double),
+    ]
+
+
+class TileTask(C.Structure):
+    _fields_ = [("px_min", C.c_uint64 * 2), ("px_max", C.c_uint64 * 2), ("batch", C.c_uint64),
+                ("samples", C.c_uint64), ("total_samples", C.c_uint64), ("seed", C.c_uint64)]
+
+
+class TileResult(C.Structure):
+    _fields_ = [("rgb_w", c_double_p), ("num_camera_rays", C.c_uint64), ("num_rays", C.c_uint64),
+                ("num_queries", C.c_uint64)]
+
+
+class RenderCfg(C.Structure):
+    _fields_ = [("integrator", C.c_int32), ("rng_mode", C.c_int32), ("max_paths", C.c_int32),
+                ("pad0", C.c_int32)]
+
+
+class RaySoA(C.Structure):
+    _fields_ = [("origin", c_double_p), ("dir", c_double_p), ("t_max", c_double_p), ("light", c_int32_p)]
+
+
+class HitSoA(C.Structure):
+    _fields_ = [("t", c_double_p), ("kind", c_int32_p), ("object", c_int32_p), ("prim", c_int32_p)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("kernel_ms", C.c_double * 8), ("launches", C.c_uint64 * 8), ("closest_queries", C.c_uint64),
+                ("shadow_queries", C.c_uint64), ("bounces", C.c_uint64), ("aabb_tests", C.c_uint64 * 2),
+                ("kd_nodes", C.c_uint64 * 2), ("tri_tests", C.c_uint64 * 2)]
+
+
+class CameraParams(C.Structure):
+    _fields_ = [("origin", C.c_double * 3), ("towards", C.c_double * 3), ("up", C.c_double * 3),
+                ("zoom", C.c_double), ("lens_radius", C.c_double), ("focal_length", C.c_double),
+                ("vfov", C.c_double), ("width", C.c_int64), ("height", C.c_int64),
+                ("illuminant", C.c_int32), ("color_space", C.c_int32),
+                ("filter_radius", C.c_double), ("filter_sigma", C.c_double)]
+
+
+class PathDump(C.Structure):
+    _fields_ = [("radiance", c_double_p), ("lambda_", c_double_p), ("raster", c_double_p),
+                ("depth", c_uint64_p), ("delta", c_double_p)]
+
+
+# (name, restype, argtypes) of every exported symbol declared in include/*.h
+DEVICE_API = [
+    ("lumo_create", C.c_int32, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("lumo_destroy", None, [C.c_void_p]),
+    ("lumo_status_str", C.c_char_p, [C.c_int32]),
+    ("lumo_abi_version", C.c_int, []),
+    ("lumo_device_count", C.c_int, []),
+    ("lumo_scene_upload", C.c_int32, [C.c_void_p, C.POINTER(SceneDesc)]),
+    ("lumo_camera_set", C.c_int32, [C.c_void_p, C.POINTER(CameraDesc)]),
+    ("lumo_render_tiles", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.c_size_t, C.POINTER(RenderCfg),
+                                      C.POINTER(TileResult)]),
+    ("lumo_trace", C.c_int32, [C.c_void_p, C.POINTER(RaySoA), C.c_size_t, C.POINTER(HitSoA), C.c_int]),
+    ("lumo_stats_get", C.c_int32, [C.c_void_p, C.POINTER(Stats)]),
+    ("lumo_stats_reset", C.c_int32, [C.c_void_p]),
+    ("lumo_debug_trace", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.c_int, C.c_int, c_double_p, C.POINTER(C.c_int)]),
+    ("lumo_debug_paths", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.POINTER(PathDump)]),
+]
+HOST_API = [
+    ("lumo_spectrum_from_rgb", Spectrum, [C.c_double, C.c_double, C.c_double]),
+    ("lumo_spectrum_from_srgb", Spectrum, [C.c_int, C.c_int, C.c_int]),
+    ("lumo_spectrum_from_pts", Spectrum, [C.c_char_p]),
+    ("lumo_rgb2spec_cell", None, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]),
+    ("lumo_rgb2spec_write", C.c_int, [C.c_char_p, C.c_int]),
+    ("lumo_builder_new", C.c_void_p, []),
+    ("lumo_builder_free", None, [C.c_void_p]),
+    ("lumo_builder_material_lambertian", C.c_int, [C.c_void_p, Spectrum]),
+    ("lumo_builder_material_light", C.c_int, [C.c_void_p, Spectrum, C.c_int, C.c_double, C.c_int]),
+    ("lumo_builder_add_mesh", C.c_int, [C.c_void_p, c_double_p, C.c_int64, c_int64_p, c_int64_p, C.c_int64,
+                                        C.c_int, C.c_int]),
+    ("lumo_builder_add_rectangle", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p, C.c_int, C.c_int]),
+    ("lumo_builder_cornell_box", C.c_void_p, []),
+    ("lumo_builder_build", C.c_void_p, [C.c_void_p]),
+    ("lumo_scene_get_desc", C.c_int32, [C.c_void_p, C.POINTER(SceneDesc)]),
+    ("lumo_scene_free", None, [C.c_void_p]),
+    ("lumo_camera_params_default", None, [C.POINTER(CameraParams)]),
+    ("lumo_camera_params_cornell_box", None, [C.POINTER(CameraParams)]),
+    ("lumo_camera_build", C.c_int32, [C.POINTER(CameraParams), C.POINTER(CameraDesc)]),
+    ("lumo_make_tasks", C.c_int64, [C.c_int64, C.c_int64, C.c_uint64, C.c_uint64, C.POINTER(TileTask),
+                                    C.c_int64]),
+]
+
+_lib = None
+
+
+def load(path=None):
+    """Load liblumo_amd.so (raises OSError if it has not been built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise OSError(f"lumo_amd: {p} not built; run `make` (or __graft_entry__.build())")
+    lib = C.CDLL(p)
+    for name, res, args in DEVICE_API + HOST_API:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(st, what=""):
+    if st != LUMO_OK:
+        raise RuntimeError(f"lumo_amd: {what} failed: {STATUS.get(st, st)}")

@@ -1,0 +1,211 @@
+// Deterministic f64 transcendentals for the render path (exp, log1p, cosh, sin, cos).
+//
+// lumo calls Rust std (`f64::exp/cos/sin/cosh`, `atanh` = 0.5*ln_1p(..)), i.e. the platform
+// libm.  Device libm (ROCm ocml) and glibc differ by an ulp on some inputs, and in the Cornell
+// box such an ulp decides geometric ties (the light is coplanar with the ceiling; walls share
+// edges).  These functions are built only from IEEE +,-,*,/ and exponent-bit manipulation
+// (no FMA; compiled with -ffp-contract=off), so the GPU kernels and the CPU oracle evaluate
+// them bit-identically.  Algorithms: Sun fdlibm (e_exp.c, e_log.c, k_sin.c, k_cos.c;
+// Cody-Waite argument reduction), accuracy < 1 ulp; tests/test_lmath.py bounds the distance
+// to glibc and tests/test_oracle.py quantifies what an ulp of libm changes in an image.
+#pragma once
+#include "vec.h"
+
+namespace lumo {
+
+LUMO_HD double lm_scalbn(double x, int k) {
+    // x in [0.5, 2] normal; k in [-1070, 1030]: multiply by 2^k in <= 3 exact steps
+    while (k > 1000) {
+        x *= f64_from_bits((uint64_t)(1023 + 1000) << 52);
+        k -= 1000;
+    }
+    while (k < -1000) {
+        x *= f64_from_bits((uint64_t)(1023 - 1000) << 52);
+        k += 1000;
+    }
+    if (k >= -1022) return x * f64_from_bits((uint64_t)(1023 + k) << 52);
+    // subnormal result: two steps so that only the last multiply rounds
+    x *= f64_from_bits((uint64_t)(1023 - 1022) << 52);
+    k += 1022;
+    return x * f64_from_bits((uint64_t)(1023 + k) << 52);
+}
+
+// fdlibm e_exp.c
+LUMO_HD double lm_exp(double x) {
+    const double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10,
+                 invln2 = 1.44269504088896338700e+00, P1 = 1.66666666666666019037e-01,
+                 P2 = -2.77777777770155933842e-03, P3 = 6.61375632143793436117e-05,
+                 P4 = -1.65339022054652515390e-06, P5 = 4.13813679705723846039e-08;
+    if (x != x) return x;
+    if (x > 709.782712893383973096) return f64_from_bits(0x7ff0000000000000ull);
+    if (x < -745.13321910194110842) return 0.0;
+    const double ax = fabs(x);
+    double hi = x, lo = 0.0;
+    int k = 0;
+    if (ax > 0.5 * 0.6931471805599453) {
+        if (ax < 1.5 * 0.6931471805599453) {
+            k = x < 0.0 ? -1 : 1;
+            hi = x < 0.0 ? x + ln2HI : x - ln2HI;
+            lo = x < 0.0 ? -ln2LO : ln2LO;
+        } else {
+            k = (int)(invln2 * x + (x < 0.0 ? -0.5 : 0.5));
+            const double t = (double)k;
+            hi = x - t * ln2HI;
+            lo = t * ln2LO;
+        }
+        x = hi - lo;
+    } else if (ax < 3.725290298461914e-09) {
+        return 1.0 + x;
+    }
+    const double t = x * x;
+    const double c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
+    const double y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
+    return lm_scalbn(y, k);
+}
+
+// fdlibm e_log.c for finite x > 0
+LUMO_HD double lm_log(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                 Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+                 Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                 Lg7 = 1.479819860511658591e-01;
+    if (x != x) return x;
+    if (x < 0.0) return f64_from_bits(0x7ff8000000000000ull);
+    if (x == 0.0) return -f64_from_bits(0x7ff0000000000000ull);
+    if (x > 1.7976931348623157e308) return x;
+    int k = 0;
+    uint64_t bits = f64_bits(x);
+    if ((bits >> 52) == 0) {  // subnormal
+        x *= 18014398509481984.0;  // 2^54
+        k -= 54;
+        bits = f64_bits(x);
+    }
+    int hx = (int)(bits >> 32);
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    int i = (hx + 0x95f64) & 0x100000;
+    // normalize x or x/2 into [sqrt(2)/2, sqrt(2))
+    x = f64_from_bits(((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (bits & 0xffffffffull));
+    k += (i >> 20);
+    const double f = x - 1.0;
+    const double dk = (double)k;
+    if ((0x000fffff & (2 + hx)) < 3) {  // |f| < 2^-20
+        if (f == 0.0) return k == 0 ? 0.0 : dk * ln2_hi + dk * ln2_lo;
+        const double R = f * f * (0.5 - 0.33333333333333333 * f);
+        return k == 0 ? f - R : dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    i = hx - 0x6147a;
+    const double w = z * z;
+    const int j = 0x6b851 - hx;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    const double R = t2 + t1;
+    if (i > 0) {
+        const double hfsq = 0.5 * f * f;
+        if (k == 0) return f - (hfsq - s * (hfsq + R));
+        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    if (k == 0) return f - s * (f - R);
+    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+// log1p(x) = log(u) * x / (u - 1), u = 1 + x (Goldberg); exact for u == 1
+LUMO_HD double lm_log1p(double x) {
+    const double u = 1.0 + x;
+    if (u == 1.0) return x;
+    if (!(u > 0.0)) return lm_log(u);
+    return lm_log(u) * (x / (u - 1.0));
+}
+
+LUMO_HD double lm_cosh(double x) {
+    const double e = lm_exp(fabs(x));
+    return 0.5 * e + 0.5 / e;
+}
+
+// fdlibm k_sin.c / k_cos.c kernels on |x| <= pi/4 with tail y (x + y = reduced argument)
+LUMO_HD double lm_ksin(double x, double y) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double z = x * x;
+    const double v = z * x;
+    const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    if (y == 0.0) return x + v * (S1 + z * r);
+    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+LUMO_HD double lm_kcos(double x, double y) {
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double z = x * x;
+    const double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+// Cody-Waite reduction by pi/2 (fdlibm e_rem_pio2.c medium path), |x| < 2^19 * pi/2.
+// Returns n and x - n*pi/2 = y0 + y1.
+LUMO_HD int lm_rem_pio2(double x, double& y0, double& y1) {
+    const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+                 pio2_1t = 6.07710050650619224932e-11, pio2_2 = 6.07710050630396597660e-11,
+                 pio2_2t = 2.02226624879595063154e-21, pio2_3 = 2.02226624871116645580e-21,
+                 pio2_3t = 8.47842766036889956997e-32;
+    const double t = fabs(x);
+    const int n = (int)(t * invpio2 + 0.5);
+    const double fn = (double)n;
+    double r = t - fn * pio2_1;
+    double w = fn * pio2_1t;
+    y0 = r - w;
+    const int j = (int)((f64_bits(t) >> 52) & 0x7ff);
+    int i = j - (int)((f64_bits(y0) >> 52) & 0x7ff);
+    if (i > 16) {  // 2nd iteration, good to 118 bits
+        double tt = r;
+        w = fn * pio2_2;
+        r = tt - w;
+        w = fn * pio2_2t - ((tt - r) - w);
+        y0 = r - w;
+        i = j - (int)((f64_bits(y0) >> 52) & 0x7ff);
+        if (i > 49) {  // 3rd iteration, 151 bits
+            tt = r;
+            w = fn * pio2_3;
+            r = tt - w;
+            w = fn * pio2_3t - ((tt - r) - w);
+            y0 = r - w;
+        }
+    }
+    y1 = (r - y0) - w;
+    if (x < 0.0) {
+        y0 = -y0;
+        y1 = -y1;
+        return -n;
+    }
+    return n;
+}
+LUMO_HD double lm_sin(double x) {
+    if (fabs(x) <= 0.7853981633974483) return lm_ksin(x, 0.0);
+    double y0, y1;
+    const int n = lm_rem_pio2(x, y0, y1);
+    switch (n & 3) {
+        case 0: return lm_ksin(y0, y1);
+        case 1: return lm_kcos(y0, y1);
+        case 2: return -lm_ksin(y0, y1);
+        default: return -lm_kcos(y0, y1);
+    }
+}
+LUMO_HD double lm_cos(double x) {
+    if (fabs(x) <= 0.7853981633974483) return lm_kcos(x, 0.0);
+    double y0, y1;
+    const int n = lm_rem_pio2(x, y0, y1);
+    switch (n & 3) {
+        case 0: return lm_kcos(y0, y1);
+        case 1: return -lm_ksin(y0, y1);
+        case 2: return -lm_kcos(y0, y1);
+        default: return lm_ksin(y0, y1);
+    }
+}
+
+}  // namespace lumo

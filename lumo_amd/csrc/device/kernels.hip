@@ -1,0 +1,1145 @@
+// MI355X wavefront path tracer: HIP kernels for gfx950 + host orchestration + C ABI.
+//
+// One path slot per (tile task, pixel).  Per sample pass:
+//   k_camera   MultiJittered sample + camera ray + hero wavelengths  (integrator.rs:45-70)
+//   repeat until no path is alive:
+//     k_closest  Scene::hit for the active queue                     (scene.rs:119-147)
+//     k_shade    BSDF sample, NEE shadow-ray records, spawn, RR       (path_trace.rs:18-77,
+//                                                                      integrator.rs:87-137)
+//     k_shadow   Scene::hit_light + MIS for every shadow record        (integrator.rs:139-184)
+//     k_resolve  radiance += sum(gathered * single) / n_shadow         (integrator.rs:74-85)
+//   k_finish   per-sample XYZ -> white balance -> RGB, luminance, cost (film/tile.rs:65-66, task.rs:64-69)
+//   k_film     tile-clipped Gaussian splat as a deterministic gather   (film/tile.rs:65-111)
+//   k_ring     adaptive-RR ring buffer + delta of the next pass        (task.rs:28-69)
+// Active-path queues are compacted with wave64 ballot + mbcnt prefix sums and one atomic per
+// wavefront.  All arithmetic is IEEE f64 without contraction (-ffp-contract=off).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstddef>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../../include/lumo_amd.h"
+#include "dscene.h"
+
+using namespace lumo;
+using namespace lumo::dev;
+
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr uint64_t SAMPLES_INCREMENT = 256;
+constexpr int RR_DEPTH = 5;
+
+enum Stage { ST_CAMERA = 0, ST_CLOSEST, ST_SHADE, ST_SHADOW, ST_RESOLVE, ST_FINISH, ST_FILM, ST_RING, ST_COUNT };
+enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_N };
+enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
+
+struct DCam {
+    Xform wtc, sctr, cts;
+    double lens_radius, focal_length;
+    M3 wb, x2r;
+    double fr, fsig;
+};
+
+// Path state (SoA)
+struct Paths {
+    double *ro, *rd, *gath, *rad, *lam, *raster;
+    uint64_t *rng;  // 2 per slot: hi, lo
+    uint32_t *depth, *flags, *queries;
+    int32_t *task, *pix;
+    uint64_t *pseed, *mj_rng, *mj_state;
+    uint16_t* perm;  // 2 * dim per slot
+    double* hit_t;
+    int32_t *hit_kind, *hit_obj, *hit_tri;
+    // shadow records, R = N * 2 * n_shadow (fixed slot-major layout)
+    double *sh_o, *sh_d, *sh_f, *sh_psct, *sh_cos, *sh_out;
+    int32_t *sh_light, *sh_flags;
+    double *g_sh, *pdf_l;
+    // per-pass outputs
+    double *p_rgb, *p_lum;
+    uint32_t *p_cost, *p_valid;
+    double* film;
+    int32_t *q0, *q1, *sq, *rq;
+    uint32_t* counts;
+    unsigned long long* tcount;  // [2][TC_N]
+};
+
+struct Tasks {
+    lumo_tile_task* t;
+    int32_t* first;  // first slot of each task (n_tasks + 1)
+    uint64_t* ring_cost;
+    double* ring_lum;
+    uint32_t* ring_ptr;
+    double* delta;
+    unsigned long long *num_rays, *queries;
+};
+
+// Per-bounce trace of one path (diagnostics; lumo_debug_trace).
+struct DebugLog {
+    int slot, pass, cur_pass, n;
+    double rec[64][20];
+};
+__device__ DebugLog g_dbg;
+
+struct Dump {
+    double *rad, *lam, *raster, *delta;
+    unsigned long long* depth;
+};
+
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)); }
+
+// Wave64 stream compaction: every lane of the wave must call this.
+__device__ __forceinline__ void wave_append(bool pred, int32_t value, int32_t* queue, uint32_t* counter) {
+    const uint64_t mask = __ballot(pred);
+    if (mask == 0) return;
+    const int lane = lane_id();
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    const uint32_t prefix =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader);
+    if (pred) queue[base + prefix] = value;
+}
+
+// Wave-reduced traversal counters (one atomic per wavefront).
+__device__ __forceinline__ void flush_counters(const Counters& C, unsigned long long* dst) {
+    unsigned long long a = C.aabb, k = C.kd, t = C.tri;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_down(a, off);
+        k += __shfl_down(k, off);
+        t += __shfl_down(t, off);
+    }
+    if (lane_id() == 0) {
+        if (a) atomicAdd(dst + TC_AABB, a);
+        if (k) atomicAdd(dst + TC_KD, k);
+        if (t) atomicAdd(dst + TC_TRI, t);
+    }
+}
+
+__device__ __forceinline__ V3 ldv3(const double* p, int i) { return V3{p[3 * i], p[3 * i + 1], p[3 * i + 2]}; }
+__device__ __forceinline__ void stv3(double* p, int i, V3 v) {
+    p[3 * i] = v.x;
+    p[3 * i + 1] = v.y;
+    p[3 * i + 2] = v.z;
+}
+__device__ __forceinline__ DColor ldc(const double* p, int i) {
+    return DColor{{p[4 * i], p[4 * i + 1], p[4 * i + 2], p[4 * i + 3]}};
+}
+__device__ __forceinline__ void stc(double* p, int i, const DColor& c) {
+    p[4 * i] = c.s[0];
+    p[4 * i + 1] = c.s[1];
+    p[4 * i + 2] = c.s[2];
+    p[4 * i + 3] = c.s[3];
+}
+
+// ------------------------------------------------------------------ init
+// Pixel sampler seeds: the tile stream's first P outputs.
+__global__ void k_init_seeds(Tasks T, Paths S, int n_tasks) {
+    const int ti = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ti >= n_tasks) return;
+    Xorshift r = xs_new(T.t[ti].seed);
+    for (int s = T.first[ti]; s < T.first[ti + 1]; ++s) S.pseed[s] = xs_u64(r);
+}
+
+// MultiJitteredSampler::new (samplers.rs:148-171): two Fisher-Yates permutations per pixel.
+__global__ void k_init_mj(Tasks T, Paths S, int n, int dim_stride) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const lumo_tile_task& t = T.t[S.task[s]];
+    const uint64_t dim = (uint64_t)ceil(sqrt((double)t.total_samples));
+    Xorshift r = xs_new(S.pseed[s]);
+    uint16_t* px = S.perm + (size_t)s * 2 * dim_stride;
+    uint16_t* py = px + dim_stride;
+    for (int which = 0; which < 2; ++which) {
+        uint16_t* p = which == 0 ? px : py;
+        for (uint64_t i = 0; i < dim; ++i) p[i] = (uint16_t)i;
+        for (uint64_t i = 0; i + 1 < dim; ++i) {
+            const uint64_t rnd = xs_u64(r);
+            const uint64_t j = i + rnd % (dim - i);
+            const uint16_t tmp = p[i];
+            p[i] = p[j];
+            p[j] = tmp;
+        }
+    }
+    S.mj_rng[2 * s] = r.hi;
+    S.mj_rng[2 * s + 1] = r.lo;
+    S.mj_state[s] = t.batch * SAMPLES_INCREMENT;
+}
+
+__device__ __forceinline__ uint64_t wf_path_seed(uint64_t pixel_seed, uint64_t k) {
+    return splitmix64(pixel_seed ^ splitmix64(k + 1));
+}
+
+// ------------------------------------------------------------------ camera (pass `pass`)
+__global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, int n, int dim_stride, uint32_t pass) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    bool active = false;
+    if (s < n) {
+        const lumo_tile_task& t = T.t[S.task[s]];
+        active = pass < t.samples;
+        S.p_valid[s] = active ? 1u : 0u;
+        if (active) {
+            // MultiJitteredSampler::next (samplers.rs:174-193)
+            const uint64_t dim = (uint64_t)ceil(sqrt((double)t.total_samples));
+            const V2 scale0 = V2{1.0 / (double)dim, (double)dim / (double)t.total_samples};
+            const V2 scale1 = scale0 / (double)dim;
+            Xorshift mr{S.mj_rng[2 * s], S.mj_rng[2 * s + 1]};
+            const uint64_t st = S.mj_state[s];
+            const uint64_t x0 = st % dim, y0 = st / dim;
+            const uint16_t* px = S.perm + (size_t)s * 2 * dim_stride;
+            const uint16_t* py = px + dim_stride;
+            const V2 offset0 = scale0 * V2{(double)x0, (double)y0};
+            const V2 offset1 = scale1 * V2{(double)px[y0], (double)py[x0]};
+            const V2 rsq = scale1 * xs_vec2(mr);
+            S.mj_state[s] = st + 1;
+            S.mj_rng[2 * s] = mr.hi;
+            S.mj_rng[2 * s + 1] = mr.lo;
+            const int j = S.pix[s];
+            const uint64_t W = t.px_max[0] - t.px_min[0];
+            const V2 xy = V2{(double)(t.px_min[0] + (uint64_t)j % W), (double)(t.px_min[1] + (uint64_t)j / W)};
+            const V2 raster = xy + (offset0 + offset1 + rsq);
+            // Integrator::integrate: lens sample (2 draws), then wavelengths (1 draw)
+            Xorshift r = xs_new(wf_path_seed(S.pseed[s], pass));
+            const V2 lens = xs_vec2(r);
+            const V3 screen = xf_pt_inv(cam.sctr, V3{raster.x, raster.y, 0.0});
+            const V3 wl0 = normalize(xf_pt_inv(cam.cts, screen));
+            V3 xo_local = V3{0, 0, 0}, wi_local = wl0;
+            if (cam.lens_radius != 0.0) {  // camera.rs:221-243
+                const V2 lxy = cam.lens_radius * square_to_disk(lens);
+                const V3 lz = V3{lxy.x, lxy.y, 0.0};
+                const V3 focus = (cam.focal_length / wl0.z) * wl0;
+                xo_local = xo_local + lz;
+                wi_local = focus - lz;
+            }
+            const Ray ray = ray_new(xf_pt_inv(cam.wtc, xo_local), xf_dir_inv(cam.wtc, wi_local));
+            double L[NS];
+            wl_sample(xs_float(r), L);
+            stv3(S.ro, s, ray.o);
+            stv3(S.rd, s, ray.d);
+            stc(S.gath, s, cfill(1.0));
+            stc(S.rad, s, cfill(0.0));
+            for (int i = 0; i < NS; ++i) S.lam[4 * s + i] = L[i];
+            S.raster[2 * s] = raster.x;
+            S.raster[2 * s + 1] = raster.y;
+            S.rng[2 * s] = r.hi;
+            S.rng[2 * s + 1] = r.lo;
+            S.depth[s] = 0;
+            S.flags[s] = 1u;  // last_specular
+            S.queries[s] = 0;
+        }
+    }
+    wave_append(active, s, S.q0, S.counts + CNT_NEXT);
+}
+
+// ------------------------------------------------------------------ closest hit
+__global__ __launch_bounds__(BLOCK) void k_closest(DScene sc, Paths S, const int32_t* queue, uint32_t count) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    Counters C{0, 0, 0};
+    if (q < count) {
+        const int s = queue[q];
+        const Ray r{ldv3(S.ro, s), ldv3(S.rd, s)};
+        const HitRef h = scene_hit(sc, r, C);
+        S.hit_t[s] = h.t;
+        S.hit_kind[s] = h.kind;
+        S.hit_obj[s] = h.obj;
+        S.hit_tri[s] = h.tri;
+        S.queries[s] += 1;
+    }
+    flush_counters(C, S.tcount);
+}
+
+// ------------------------------------------------------------------ shade
+__global__ __launch_bounds__(BLOCK) void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue, uint32_t count,
+                                                  int32_t* next_queue) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    bool alive = false, resolve = false;
+    int s = -1;
+    const int ns = sc.n_shadow;
+    int n_sh = 0;
+    if (q < count) {
+        s = queue[q];
+        const int kind = S.hit_kind[s];
+        if (kind != 0) {
+            const Ray ro{ldv3(S.ro, s), ldv3(S.rd, s)};
+            const HitRef hr{S.hit_t[s], kind, S.hit_obj[s], S.hit_tri[s]};
+            DHit ho;
+            hit_record(sc, hr, ro, ho);
+            const lumo_material m = sc.mats[ho.material];
+            Xorshift rng{S.rng[2 * s], S.rng[2 * s + 1]};
+            if (s == g_dbg.slot && g_dbg.pass == g_dbg.cur_pass && g_dbg.n < 64) {
+                double* d = g_dbg.rec[g_dbg.n++];
+                d[0] = S.depth[s]; d[1] = hr.kind; d[2] = hr.obj; d[3] = hr.tri; d[4] = hr.t;
+                d[5] = ro.o.x; d[6] = ro.o.y; d[7] = ro.o.z; d[8] = ro.d.x; d[9] = ro.d.y; d[10] = ro.d.z;
+                d[11] = ho.p.x; d[12] = ho.p.y; d[13] = ho.p.z; d[14] = ho.ng.x; d[15] = ho.ng.y; d[16] = ho.ng.z;
+                d[17] = (double)(rng.hi >> 11); d[18] = ho.backface; d[19] = S.gath[4 * s];
+            }
+            double L[NS];
+            for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
+            DColor gathered = ldc(S.gath, s);
+            DColor radiance = ldc(S.rad, s);
+            const V3 wo = -ro.d;
+            (void)xs_float(rng);  // rand_u (unused by Lambertian, drawn in order)
+            const V2 sq = xs_vec2(rng);
+            V3 wi;
+            if (!bsdf_sample(m, ho, wo, sq, wi)) {
+                if (S.flags[s] & 1u) radiance = radiance + gathered * emit(sc, m, L, ho.backface);
+                stc(S.rad, s, radiance);
+            } else {
+                // NEE: n_shadow x [light pick, light direction, BSDF sample] (integrator.rs:87-137)
+                const bool delta_mat = false;  // Lambertian / Light
+                if (!delta_mat) {
+                    const int base = s * 2 * ns;
+                    for (int i = 0; i < ns; ++i) {
+                        const int li = sample_light(sc, xs_float(rng));
+                        const lumo_object& Lo = sc.lights[li];
+                        S.pdf_l[s * ns + i] = sc.alias_pdf[li];
+                        {
+                            const V2 rs = xs_vec2(rng);
+                            const V3 w = light_sample_towards(Lo, ho.p, rs);
+                            const Ray ri = spawn(ho, w);
+                            const int rec = base + 2 * i;
+                            stv3(S.sh_o, rec, ri.o);
+                            stv3(S.sh_d, rec, ri.d);
+                            stc(S.sh_f, rec, bsdf_f(m, ho, wo, w, L));
+                            S.sh_psct[rec] = bsdf_pdf(m, ho, wo, w);
+                            S.sh_cos[rec] = shading_cosine(m, w, ho.ns);
+                            S.sh_light[rec] = li;
+                            S.sh_flags[rec] = 1 | 2;  // valid | light-sampled
+                            n_sh++;
+                        }
+                        {
+                            (void)xs_float(rng);
+                            const V2 rsq = xs_vec2(rng);
+                            V3 w;
+                            const int rec = base + 2 * i + 1;
+                            if (bsdf_sample(m, ho, wo, rsq, w)) {
+                                const Ray ri = spawn(ho, w);
+                                stv3(S.sh_o, rec, ri.o);
+                                stv3(S.sh_d, rec, ri.d);
+                                stc(S.sh_f, rec, bsdf_f(m, ho, wo, w, L));
+                                S.sh_psct[rec] = bsdf_pdf(m, ho, wo, w);
+                                S.sh_cos[rec] = shading_cosine(m, w, ho.ns);
+                                S.sh_light[rec] = li;
+                                S.sh_flags[rec] = 1;
+                                n_sh++;
+                            } else {
+                                S.sh_flags[rec] = 0;
+                            }
+                        }
+                    }
+                    stc(S.g_sh, s, gathered);
+                    resolve = true;
+                }
+                // spawn the continuation (path_trace.rs:42-77)
+                const Ray ri = spawn(ho, wi);
+                const V3 wi2 = ri.d;
+                const double p_scatter = bsdf_pdf(m, ho, wo, wi2);
+                if (p_scatter > 0.0) {
+                    const DColor bsdf = bsdf_f(m, ho, wo, wi2, L);
+                    gathered = gathered * (bsdf * shading_cosine(m, wi2, ho.ns) / p_scatter);
+                    bool cont = true;
+                    const uint32_t depth = S.depth[s];
+                    if ((int)depth >= RR_DEPTH) {
+                        const double lum = luminance(sc, gathered, L);
+                        const double rr_prob = rmin(lum / T.delta[S.task[s]], 1.0);
+                        if (xs_float(rng) > rr_prob)
+                            cont = false;
+                        else
+                            gathered = gathered / rr_prob;
+                    }
+                    if (cont) {
+                        S.flags[s] = 0u;  // last_specular = is_specular() = false (Lambertian)
+                        S.depth[s] = depth + 1;
+                        stv3(S.ro, s, ri.o);
+                        stv3(S.rd, s, ri.d);
+                        stc(S.gath, s, gathered);
+                        alive = true;
+                    }
+                }
+            }
+            S.rng[2 * s] = rng.hi;
+            S.rng[2 * s + 1] = rng.lo;
+            S.queries[s] += (uint32_t)n_sh;
+        }
+    }
+    wave_append(alive, s, next_queue, S.counts + CNT_NEXT);
+    wave_append(resolve, s, S.rq, S.counts + CNT_RESOLVE);
+}
+
+// Shadow-record queue: all valid records of the resolve queue's slots.
+__global__ __launch_bounds__(BLOCK) void k_shadow_queue(DScene sc, Paths S, uint32_t count) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int per = 2 * sc.n_shadow;
+    const uint32_t total = count * (uint32_t)per;
+    bool valid = false;
+    int rec = -1;
+    if (q < total) {
+        const int s = S.rq[q / per];
+        rec = s * per + (int)(q % per);
+        valid = (S.sh_flags[rec] & 1) != 0;
+        if (!valid) stc(S.sh_out, rec, cfill(0.0));
+    }
+    wave_append(valid, rec, S.sq, S.counts + CNT_SHADOW);
+}
+
+// ------------------------------------------------------------------ shadow (hit_light + MIS)
+__global__ __launch_bounds__(BLOCK) void k_shadow(DScene sc, Paths S, uint32_t count) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    Counters C{0, 0, 0};
+    if (q < count) {
+        const int rec = S.sq[q];
+        const int s = rec / (2 * sc.n_shadow);
+        const Ray ri{ldv3(S.sh_o, rec), ldv3(S.sh_d, rec)};
+        const int li = S.sh_light[rec];
+        DHit hi;
+        DColor out = cfill(0.0);
+        if (scene_hit_light(sc, ri, li, hi, C)) {
+            const lumo_object& Lo = sc.lights[li];
+            const double p_lig = light_pdf(Lo, ri, hi.p, hi.ng);
+            const double p_sct = S.sh_psct[rec];
+            if (!(p_lig == 0.0 || p_sct == 0.0)) {  // mis_sample (integrator.rs:139-184)
+                double L[NS];
+                for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
+                const bool li_mode = (S.sh_flags[rec] & 2) != 0;
+                const double denom = p_lig * p_lig + p_sct * p_sct;
+                const double weight = li_mode ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
+                const double p_denom = li_mode ? p_lig : p_sct;
+                const lumo_material hm = sc.mats[hi.material];
+                out = ldc(S.sh_f, rec) * cfill(1.0) * emit(sc, hm, L, hi.backface) * S.sh_cos[rec] * weight / p_denom;
+            }
+        }
+        stc(S.sh_out, rec, out);
+    }
+    flush_counters(C, S.tcount + TC_N);
+}
+
+// ------------------------------------------------------------------ resolve (shadow_rays fold)
+__global__ __launch_bounds__(BLOCK) void k_resolve(DScene sc, Paths S, uint32_t count) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= count) return;
+    const int s = S.rq[q];
+    const int ns = sc.n_shadow;
+    const DColor g = ldc(S.g_sh, s);
+    DColor acc = cfill(0.0);
+    for (int i = 0; i < ns; ++i) {
+        const int rec = s * 2 * ns + 2 * i;
+        const DColor single = (cfill(0.0) + ldc(S.sh_out, rec) + ldc(S.sh_out, rec + 1)) / S.pdf_l[s * ns + i];
+        acc = acc + g * single;
+    }
+    stc(S.rad, s, ldc(S.rad, s) + acc / (double)ns);
+}
+
+// ------------------------------------------------------------------ finish + film + ring
+__global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, int n, uint32_t pass, Dump dump,
+                                                   int dump_p) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n || !S.p_valid[s]) return;
+    double L[NS];
+    for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
+    const DColor c = ldc(S.rad, s);
+    const V3 rgb = m3_mul_vec(cam.x2r, m3_mul_vec(cam.wb, color_xyz(sc, c, L)));
+    stv3(S.p_rgb, s, rgb);
+    S.p_lum[s] = luminance(sc, c, L);
+    S.p_cost[s] = S.depth[s];
+    if (dump.rad) {
+        const size_t o = (size_t)pass * dump_p + S.pix[s];
+        for (int i = 0; i < NS; ++i) {
+            dump.rad[4 * o + i] = c.s[i];
+            dump.lam[4 * o + i] = L[i];
+        }
+        dump.raster[2 * o] = S.raster[2 * s];
+        dump.raster[2 * o + 1] = S.raster[2 * s + 1];
+        dump.depth[o] = S.depth[s];
+    }
+}
+
+__device__ __forceinline__ double gauss(double x, double sigma) {
+    return lm_exp(-(x * x) / (2.0 * sigma * sigma)) / sqrt(rmax(2.0 * PI * sigma * sigma, 0.0));
+}
+
+// FilmTile::add_sample as a gather: destination pixel d receives, in source raster order, the
+// samples whose (tile-clipped) 3x3 footprint contains d.  Sources farther than 2 px cannot.
+__global__ __launch_bounds__(BLOCK) void k_film(Paths S, Tasks T, DCam cam, int n) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const int ti = S.task[s];
+    const lumo_tile_task& t = T.t[ti];
+    const int W = (int)(t.px_max[0] - t.px_min[0]), H = (int)(t.px_max[1] - t.px_min[1]);
+    const int j = S.pix[s];
+    const int dx = j % W, dy = j / W;
+    const uint64_t gx = t.px_min[0] + dx, gy = t.px_min[1] + dy;
+    const int first = T.first[ti];
+    const uint64_t r = (uint64_t)ceil(cam.fr - 0.5);
+    double acc[4] = {S.film[4 * s], S.film[4 * s + 1], S.film[4 * s + 2], S.film[4 * s + 3]};
+    const double gr = gauss(cam.fr, cam.fsig);
+    for (int sy = dy - 2; sy <= dy + 1; ++sy) {
+        if (sy < 0 || sy >= H) continue;
+        for (int sx = dx - 2; sx <= dx + 1; ++sx) {
+            if (sx < 0 || sx >= W) continue;
+            const int src = first + sy * W + sx;
+            if (!S.p_valid[src]) continue;
+            const double rx = S.raster[2 * src], ry = S.raster[2 * src + 1];
+            const uint64_t px = rx > 0.0 ? (uint64_t)floor(rx) : 0, py = ry > 0.0 ? (uint64_t)floor(ry) : 0;
+            const uint64_t mix = std::max(px >= r ? px - r : 0, t.px_min[0]);
+            const uint64_t miy = std::max(py >= r ? py - r : 0, t.px_min[1]);
+            const uint64_t mxx = std::min(px + r, t.px_max[0] - 1), mxy = std::min(py + r, t.px_max[1] - 1);
+            if (gx < mix || gx > mxx || gy < miy || gy > mxy) continue;
+            const double vx = rx - (0.5 + (double)gx), vy = ry - (0.5 + (double)gy);
+            const double w = rmax(gauss(vx, cam.fsig) - gr, 0.0) * rmax(gauss(vy, cam.fsig) - gr, 0.0);
+            if (w != 0.0) {
+                const V3 c = ldv3(S.p_rgb, src) * w;
+                acc[0] += c.x;
+                acc[1] += c.y;
+                acc[2] += c.z;
+                acc[3] += w;
+            }
+        }
+    }
+    for (int i = 0; i < 4; ++i) S.film[4 * s + i] = acc[i];
+}
+
+// task.rs:42-53 + 64-69: ring update in pixel order, then delta for the next pass.
+__global__ void k_ring(Paths S, Tasks T, int n_tasks, int update) {
+    const int ti = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ti >= n_tasks) return;
+    const lumo_tile_task& t = T.t[ti];
+    const uint64_t n = t.samples;
+    uint64_t* rc = T.ring_cost + (size_t)ti * SAMPLES_INCREMENT;
+    double* rl = T.ring_lum + (size_t)ti * SAMPLES_INCREMENT;
+    if (update) {
+        uint32_t ptr = T.ring_ptr[ti];
+        unsigned long long rays = 0, queries = 0;
+        for (int s = T.first[ti]; s < T.first[ti + 1]; ++s) {
+            if (!S.p_valid[s]) continue;
+            rays += S.p_cost[s];
+            queries += S.queries[s];
+            rc[ptr] = S.p_cost[s];
+            rl[ptr] = S.p_lum[s];
+            ptr = (uint32_t)((ptr + 1) % n);
+        }
+        T.ring_ptr[ti] = ptr;
+        T.num_rays[ti] += rays;
+        T.queries[ti] += queries;
+    }
+    double f = 0.0, f2 = 0.0;
+    for (uint64_t i = 0; i < n; ++i) f = f + rl[i];
+    for (uint64_t i = 0; i < n; ++i) f2 = f2 + rl[i] * rl[i];
+    const double var = f2 - f * f / (double)n;
+    double delta = 1e-5;
+    if (!(var <= 0.0)) {
+        uint64_t cost = 0;
+        for (uint64_t i = 0; i < n; ++i) cost += rc[i];
+        delta = sqrt(var / (double)cost);
+    }
+    T.delta[ti] = delta;
+}
+
+// ------------------------------------------------------------------ traversal-only entry (lumo_trace)
+__global__ void k_trace(DScene sc, const double* o, const double* d, const int32_t* light, int n, int any_hit,
+                        double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
+                        unsigned long long* tcount) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    Counters C{0, 0, 0};
+    if (i < n) {
+        const Ray r{ldv3(o, i), ldv3(d, i)};
+        if (!any_hit) {
+            const HitRef h = scene_hit(sc, r, C);
+            t_out[i] = h.t;
+            kind_out[i] = h.kind;
+            obj_out[i] = h.obj;
+            prim_out[i] = h.tri;
+        } else {
+            DHit lh;
+            const int li = light[i];
+            const bool vis = scene_hit_light(sc, r, li, lh, C);
+            t_out[i] = vis ? lh.t : DINF;
+            kind_out[i] = vis ? 2 : 0;
+            obj_out[i] = vis ? li : -1;
+            prim_out[i] = -1;
+        }
+    }
+    flush_counters(C, tcount);
+}
+
+// ================================================================== host side
+#define HIPCHK(x)                                \
+    do {                                         \
+        hipError_t e__ = (x);                    \
+        if (e__ != hipSuccess) {                 \
+            last_hip_error() = e__;              \
+            return LUMO_ERR_HIP;                 \
+        }                                        \
+    } while (0)
+
+hipError_t& last_hip_error() {
+    static thread_local hipError_t e = hipSuccess;
+    return e;
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool has_scene = false, has_camera = false;
+    DScene sc{};
+    DCam cam{};
+    std::vector<DevBuf> scene_bufs;
+    std::vector<DevBuf> work;  // grown on demand
+    lumo_stats stats{};
+    hipEvent_t ev[2 * ST_COUNT];
+};
+
+lumo_status dev_alloc(DevBuf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return LUMO_OK;
+    if (b.p) hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    if (hipMalloc(&b.p, bytes) != hipSuccess) return LUMO_ERR_OOM;
+    b.bytes = bytes;
+    return LUMO_OK;
+}
+
+template <typename T>
+lumo_status upload(Ctx& c, const T* host, size_t count, const T** dptr) {
+    c.scene_bufs.emplace_back();
+    DevBuf& b = c.scene_bufs.back();
+    const lumo_status st = dev_alloc(b, sizeof(T) * count);
+    if (st) return st;
+    if (count && host) HIPCHK(hipMemcpy(b.p, host, sizeof(T) * count, hipMemcpyHostToDevice));
+    *dptr = static_cast<const T*>(b.p);
+    return LUMO_OK;
+}
+
+void free_scene(Ctx& c) {
+    for (DevBuf& b : c.scene_bufs)
+        if (b.p) hipFree(b.p);
+    c.scene_bufs.clear();
+    c.has_scene = false;
+}
+
+int ceil_div(uint64_t a, uint64_t b) { return (int)((a + b - 1) / b); }
+
+// Work-buffer carve-out (one allocation per field, grown on demand)
+enum WorkId {
+    W_RO, W_RD, W_GATH, W_RAD, W_LAM, W_RASTER, W_RNG, W_DEPTH, W_FLAGS, W_QUERIES, W_TASK, W_PIX, W_PSEED, W_MJRNG,
+    W_MJSTATE, W_PERM, W_HIT_T, W_HIT_KIND, W_HIT_OBJ, W_HIT_TRI, W_SH_O, W_SH_D, W_SH_F, W_SH_PSCT, W_SH_COS,
+    W_SH_OUT, W_SH_LIGHT, W_SH_FLAGS, W_G_SH, W_PDF_L, W_P_RGB, W_P_LUM, W_P_COST, W_P_VALID, W_FILM, W_Q0, W_Q1,
+    W_SQ, W_RQ, W_COUNTS, W_TCOUNT, W_TASKS, W_FIRST, W_RING_COST, W_RING_LUM, W_RING_PTR, W_DELTA, W_NUM_RAYS,
+    W_TQUERIES, W_DUMP_RAD, W_DUMP_LAM, W_DUMP_RASTER, W_DUMP_DEPTH, W_DUMP_DELTA, W_COUNT
+};
+
+template <typename T>
+T* wbuf(Ctx& c, int id, size_t count, lumo_status& st) {
+    if (c.work.size() < W_COUNT) c.work.resize(W_COUNT);
+    const lumo_status s = dev_alloc(c.work[id], sizeof(T) * count);
+    if (s) st = s;
+    return static_cast<T*>(c.work[id].p);
+}
+
+struct StageTimer {
+    Ctx& c;
+    bool on;
+    int stage;
+    StageTimer(Ctx& cc, bool enable, int st) : c(cc), on(enable), stage(st) {
+        if (on) hipEventRecord(c.ev[2 * stage], c.stream);
+    }
+    ~StageTimer() {
+        if (on) {
+            hipEventRecord(c.ev[2 * stage + 1], c.stream);
+            hipEventSynchronize(c.ev[2 * stage + 1]);
+            float ms = 0.f;
+            hipEventElapsedTime(&ms, c.ev[2 * stage], c.ev[2 * stage + 1]);
+            c.stats.kernel_ms[stage] += ms;
+            c.stats.launches[stage] += 1;
+        }
+    }
+};
+
+bool g_timing = false;
+
+lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lumo_tile_result* out, Dump* dump_host,
+                        uint64_t dump_samples) {
+    if (!c.has_scene) return LUMO_ERR_NO_SCENE;
+    if (!c.has_camera) return LUMO_ERR_NO_CAMERA;
+    if (n_tasks == 0) return LUMO_OK;
+    // slots
+    std::vector<int32_t> first(n_tasks + 1), task_of, pix_of;
+    uint64_t max_total = 1, max_samples = 0;
+    for (size_t i = 0; i < n_tasks; ++i) {
+        const lumo_tile_task& t = tasks[i];
+        if (!(t.px_max[0] > t.px_min[0] && t.px_max[1] > t.px_min[1]) || t.samples == 0 ||
+            t.samples > SAMPLES_INCREMENT || t.total_samples == 0 ||
+            t.px_max[0] > (uint64_t)1 << 31 || t.px_max[1] > (uint64_t)1 << 31)
+            return LUMO_ERR_INVALID;
+        const uint64_t P = (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1]);
+        first[i] = (int32_t)task_of.size();
+        for (uint64_t j = 0; j < P; ++j) {
+            task_of.push_back((int32_t)i);
+            pix_of.push_back((int32_t)j);
+        }
+        if (task_of.size() > (1u << 30)) return LUMO_ERR_INVALID;
+        max_total = std::max(max_total, t.total_samples);
+        max_samples = std::max(max_samples, t.samples);
+    }
+    first[n_tasks] = (int32_t)task_of.size();
+    const int N = (int)task_of.size();
+    const int ns = c.sc.n_shadow;
+    const size_t R = (size_t)N * 2 * ns;
+    const int dim_stride = (int)std::ceil(std::sqrt((double)max_total));
+    if (dim_stride > 65535) return LUMO_ERR_INVALID;
+
+    lumo_status st = LUMO_OK;
+    Paths S{};
+    S.ro = wbuf<double>(c, W_RO, 3 * (size_t)N, st);
+    S.rd = wbuf<double>(c, W_RD, 3 * (size_t)N, st);
+    S.gath = wbuf<double>(c, W_GATH, 4 * (size_t)N, st);
+    S.rad = wbuf<double>(c, W_RAD, 4 * (size_t)N, st);
+    S.lam = wbuf<double>(c, W_LAM, 4 * (size_t)N, st);
+    S.raster = wbuf<double>(c, W_RASTER, 2 * (size_t)N, st);
+    S.rng = wbuf<uint64_t>(c, W_RNG, 2 * (size_t)N, st);
+    S.depth = wbuf<uint32_t>(c, W_DEPTH, N, st);
+    S.flags = wbuf<uint32_t>(c, W_FLAGS, N, st);
+    S.queries = wbuf<uint32_t>(c, W_QUERIES, N, st);
+    S.task = wbuf<int32_t>(c, W_TASK, N, st);
+    S.pix = wbuf<int32_t>(c, W_PIX, N, st);
+    S.pseed = wbuf<uint64_t>(c, W_PSEED, N, st);
+    S.mj_rng = wbuf<uint64_t>(c, W_MJRNG, 2 * (size_t)N, st);
+    S.mj_state = wbuf<uint64_t>(c, W_MJSTATE, N, st);
+    S.perm = wbuf<uint16_t>(c, W_PERM, 2 * (size_t)dim_stride * N, st);
+    S.hit_t = wbuf<double>(c, W_HIT_T, N, st);
+    S.hit_kind = wbuf<int32_t>(c, W_HIT_KIND, N, st);
+    S.hit_obj = wbuf<int32_t>(c, W_HIT_OBJ, N, st);
+    S.hit_tri = wbuf<int32_t>(c, W_HIT_TRI, N, st);
+    S.sh_o = wbuf<double>(c, W_SH_O, 3 * R, st);
+    S.sh_d = wbuf<double>(c, W_SH_D, 3 * R, st);
+    S.sh_f = wbuf<double>(c, W_SH_F, 4 * R, st);
+    S.sh_psct = wbuf<double>(c, W_SH_PSCT, R, st);
+    S.sh_cos = wbuf<double>(c, W_SH_COS, R, st);
+    S.sh_out = wbuf<double>(c, W_SH_OUT, 4 * R, st);
+    S.sh_light = wbuf<int32_t>(c, W_SH_LIGHT, R, st);
+    S.sh_flags = wbuf<int32_t>(c, W_SH_FLAGS, R, st);
+    S.g_sh = wbuf<double>(c, W_G_SH, 4 * (size_t)N, st);
+    S.pdf_l = wbuf<double>(c, W_PDF_L, (size_t)ns * N, st);
+    S.p_rgb = wbuf<double>(c, W_P_RGB, 3 * (size_t)N, st);
+    S.p_lum = wbuf<double>(c, W_P_LUM, N, st);
+    S.p_cost = wbuf<uint32_t>(c, W_P_COST, N, st);
+    S.p_valid = wbuf<uint32_t>(c, W_P_VALID, N, st);
+    S.film = wbuf<double>(c, W_FILM, 4 * (size_t)N, st);
+    S.q0 = wbuf<int32_t>(c, W_Q0, N, st);
+    S.q1 = wbuf<int32_t>(c, W_Q1, N, st);
+    S.sq = wbuf<int32_t>(c, W_SQ, R, st);
+    S.rq = wbuf<int32_t>(c, W_RQ, N, st);
+    S.counts = wbuf<uint32_t>(c, W_COUNTS, 4, st);
+    S.tcount = wbuf<unsigned long long>(c, W_TCOUNT, 2 * TC_N, st);
+    Tasks T{};
+    T.t = wbuf<lumo_tile_task>(c, W_TASKS, n_tasks, st);
+    T.first = wbuf<int32_t>(c, W_FIRST, n_tasks + 1, st);
+    T.ring_cost = wbuf<uint64_t>(c, W_RING_COST, SAMPLES_INCREMENT * n_tasks, st);
+    T.ring_lum = wbuf<double>(c, W_RING_LUM, SAMPLES_INCREMENT * n_tasks, st);
+    T.ring_ptr = wbuf<uint32_t>(c, W_RING_PTR, n_tasks, st);
+    T.delta = wbuf<double>(c, W_DELTA, n_tasks, st);
+    T.num_rays = wbuf<unsigned long long>(c, W_NUM_RAYS, n_tasks, st);
+    T.queries = wbuf<unsigned long long>(c, W_TQUERIES, n_tasks, st);
+    Dump D{};
+    int dump_p = 0;
+    if (dump_host) {
+        dump_p = N;  // single task
+        const size_t m = (size_t)dump_samples * N;
+        D.rad = wbuf<double>(c, W_DUMP_RAD, 4 * m, st);
+        D.lam = wbuf<double>(c, W_DUMP_LAM, 4 * m, st);
+        D.raster = wbuf<double>(c, W_DUMP_RASTER, 2 * m, st);
+        D.depth = wbuf<unsigned long long>(c, W_DUMP_DEPTH, m, st);
+        D.delta = wbuf<double>(c, W_DUMP_DELTA, dump_samples, st);
+    }
+    if (st) return st;
+
+    hipStream_t sm = c.stream;
+    HIPCHK(hipMemcpyAsync(T.t, tasks, sizeof(lumo_tile_task) * n_tasks, hipMemcpyHostToDevice, sm));
+    HIPCHK(hipMemcpyAsync(T.first, first.data(), sizeof(int32_t) * (n_tasks + 1), hipMemcpyHostToDevice, sm));
+    HIPCHK(hipMemcpyAsync(S.task, task_of.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, sm));
+    HIPCHK(hipMemcpyAsync(S.pix, pix_of.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, sm));
+    HIPCHK(hipMemsetAsync(T.ring_cost, 0, sizeof(uint64_t) * SAMPLES_INCREMENT * n_tasks, sm));
+    HIPCHK(hipMemsetAsync(T.ring_lum, 0, sizeof(double) * SAMPLES_INCREMENT * n_tasks, sm));
+    HIPCHK(hipMemsetAsync(T.ring_ptr, 0, sizeof(uint32_t) * n_tasks, sm));
+    HIPCHK(hipMemsetAsync(T.num_rays, 0, sizeof(unsigned long long) * n_tasks, sm));
+    HIPCHK(hipMemsetAsync(T.queries, 0, sizeof(unsigned long long) * n_tasks, sm));
+    HIPCHK(hipMemsetAsync(S.film, 0, sizeof(double) * 4 * N, sm));
+    HIPCHK(hipMemsetAsync(S.tcount, 0, sizeof(unsigned long long) * 2 * TC_N, sm));
+
+    const int gT = ceil_div(n_tasks, BLOCK), gN = ceil_div(N, BLOCK);
+    k_init_seeds<<<gT, BLOCK, 0, sm>>>(T, S, (int)n_tasks);
+    k_init_mj<<<gN, BLOCK, 0, sm>>>(T, S, N, dim_stride);
+    k_ring<<<gT, BLOCK, 0, sm>>>(S, T, (int)n_tasks, 0);
+    HIPCHK(hipGetLastError());
+
+    uint64_t bounces = 0, closest_q = 0, shadow_q = 0;
+    uint32_t counts[4];
+    for (uint64_t pass = 0; pass < max_samples; ++pass) {
+        {
+            const int cp = (int)pass;
+            HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dbg), &cp, sizeof(int), offsetof(DebugLog, cur_pass),
+                                          hipMemcpyHostToDevice, sm));
+        }
+        if (dump_host) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, sm));
+        HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * 4, sm));
+        {
+            StageTimer tm(c, g_timing, ST_CAMERA);
+            k_camera<<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(counts, S.counts, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, sm));
+        HIPCHK(hipStreamSynchronize(sm));
+        uint32_t qn = counts[CNT_NEXT];
+        int32_t* qa = S.q0;
+        int32_t* qb = S.q1;
+        while (qn > 0) {
+            bounces++;
+            closest_q += qn;
+            HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * 4, sm));
+            {
+                StageTimer tm(c, g_timing, ST_CLOSEST);
+                k_closest<<<ceil_div(qn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, qa, qn);
+            }
+            {
+                StageTimer tm(c, g_timing, ST_SHADE);
+                k_shade<<<ceil_div(qn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qn, qb);
+            }
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(counts, S.counts, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, sm));
+            HIPCHK(hipStreamSynchronize(sm));
+            const uint32_t rn = counts[CNT_RESOLVE];
+            if (rn > 0) {
+                const uint64_t total = (uint64_t)rn * 2 * ns;
+                k_shadow_queue<<<ceil_div(total, BLOCK), BLOCK, 0, sm>>>(c.sc, S, rn);
+                HIPCHK(hipMemcpyAsync(counts + CNT_SHADOW, S.counts + CNT_SHADOW, sizeof(uint32_t),
+                                      hipMemcpyDeviceToHost, sm));
+                HIPCHK(hipStreamSynchronize(sm));
+                const uint32_t sn = counts[CNT_SHADOW];
+                shadow_q += sn;
+                if (sn > 0) {
+                    StageTimer tm(c, g_timing, ST_SHADOW);
+                    k_shadow<<<ceil_div(sn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, sn);
+                }
+                {
+                    StageTimer tm(c, g_timing, ST_RESOLVE);
+                    k_resolve<<<ceil_div(rn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, rn);
+                }
+                HIPCHK(hipGetLastError());
+            }
+            qn = counts[CNT_NEXT];
+            std::swap(qa, qb);
+        }
+        {
+            StageTimer tm(c, g_timing, ST_FINISH);
+            k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, S, c.cam, N, (uint32_t)pass, D, dump_p);
+        }
+        {
+            StageTimer tm(c, g_timing, ST_FILM);
+            k_film<<<gN, BLOCK, 0, sm>>>(S, T, c.cam, N);
+        }
+        {
+            StageTimer tm(c, g_timing, ST_RING);
+            k_ring<<<gT, BLOCK, 0, sm>>>(S, T, (int)n_tasks, 1);
+        }
+        HIPCHK(hipGetLastError());
+    }
+    // results
+    std::vector<double> film((size_t)4 * N);
+    std::vector<unsigned long long> rays(n_tasks), queries(n_tasks);
+    HIPCHK(hipMemcpyAsync(film.data(), S.film, sizeof(double) * 4 * N, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipMemcpyAsync(rays.data(), T.num_rays, sizeof(unsigned long long) * n_tasks, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipMemcpyAsync(queries.data(), T.queries, sizeof(unsigned long long) * n_tasks, hipMemcpyDeviceToHost,
+                          sm));
+    unsigned long long tc[2 * TC_N];
+    HIPCHK(hipMemcpyAsync(tc, S.tcount, sizeof(tc), hipMemcpyDeviceToHost, sm));
+    if (dump_host) {
+        const size_t m = (size_t)dump_samples * N;
+        HIPCHK(hipMemcpyAsync(dump_host->rad, D.rad, sizeof(double) * 4 * m, hipMemcpyDeviceToHost, sm));
+        HIPCHK(hipMemcpyAsync(dump_host->lam, D.lam, sizeof(double) * 4 * m, hipMemcpyDeviceToHost, sm));
+        HIPCHK(hipMemcpyAsync(dump_host->raster, D.raster, sizeof(double) * 2 * m, hipMemcpyDeviceToHost, sm));
+        HIPCHK(hipMemcpyAsync(dump_host->depth, D.depth, sizeof(unsigned long long) * m, hipMemcpyDeviceToHost, sm));
+        HIPCHK(hipMemcpyAsync(dump_host->delta, D.delta, sizeof(double) * dump_samples, hipMemcpyDeviceToHost, sm));
+    }
+    HIPCHK(hipStreamSynchronize(sm));
+    for (size_t i = 0; i < n_tasks; ++i) {
+        if (!out) break;
+        const lumo_tile_task& t = tasks[i];
+        const size_t P = (size_t)(first[i + 1] - first[i]);
+        if (out[i].rgb_w) std::memcpy(out[i].rgb_w, film.data() + 4 * (size_t)first[i], sizeof(double) * 4 * P);
+        out[i].num_camera_rays = P * t.samples;
+        out[i].num_rays = rays[i];
+        out[i].num_queries = queries[i];
+    }
+    c.stats.closest_queries += closest_q;
+    c.stats.shadow_queries += shadow_q;
+    c.stats.bounces += bounces;
+    for (int k = 0; k < 2; ++k) {
+        c.stats.aabb_tests[k] += tc[k * TC_N + TC_AABB];
+        c.stats.kd_nodes[k] += tc[k * TC_N + TC_KD];
+        c.stats.tri_tests[k] += tc[k * TC_N + TC_TRI];
+    }
+    return LUMO_OK;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+int lumo_abi_version(void) { return LUMO_ABI_VERSION; }
+
+int lumo_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* lumo_status_str(lumo_status st) {
+    switch (st) {
+        case LUMO_OK: return "ok";
+        case LUMO_ERR_INVALID: return "invalid argument";
+        case LUMO_ERR_NO_DEVICE: return "no gfx950 device";
+        case LUMO_ERR_HIP: return hipGetErrorString(last_hip_error());
+        case LUMO_ERR_NO_SCENE: return "no scene uploaded";
+        case LUMO_ERR_NO_CAMERA: return "no camera set";
+        case LUMO_ERR_UNSUPPORTED: return "unsupported";
+        case LUMO_ERR_OOM: return "out of device memory";
+        default: return "unknown";
+    }
+}
+
+lumo_status lumo_create(int device, void** ctx_out) {
+    if (!ctx_out) return LUMO_ERR_INVALID;
+    *ctx_out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return LUMO_ERR_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return LUMO_ERR_NO_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return LUMO_ERR_NO_DEVICE;
+    HIPCHK(hipSetDevice(device));
+    Ctx* c = new (std::nothrow) Ctx();
+    if (!c) return LUMO_ERR_OOM;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return LUMO_ERR_HIP;
+    }
+    for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventCreate(&c->ev[i]);
+    {
+        DebugLog h{};
+        h.slot = -1;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &h, sizeof(h));
+    }
+    const char* tm = std::getenv("LUMO_TIMING");
+    g_timing = tm && tm[0] == '1';
+    *ctx_out = c;
+    return LUMO_OK;
+}
+
+void lumo_destroy(void* ctx) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    free_scene(*c);
+    for (DevBuf& b : c->work)
+        if (b.p) hipFree(b.p);
+    for (int i = 0; i < 2 * ST_COUNT; ++i) hipEventDestroy(c->ev[i]);
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !d) return LUMO_ERR_INVALID;
+    if (d->num_lights <= 0 || d->num_light_nodes <= 0 || d->num_dense_spectra < 3 || !d->materials) return LUMO_ERR_INVALID;
+    for (int i = 0; i < d->num_materials; ++i) {
+        const int k = d->materials[i].kind;
+        if (k != LUMO_MAT_LAMBERTIAN && k != LUMO_MAT_LIGHT && k != LUMO_MAT_BLANK) return LUMO_ERR_UNSUPPORTED;
+    }
+    for (int i = 0; i < d->num_lights; ++i)
+        if (d->lights[i].type != LUMO_OBJ_RECTANGLE) return LUMO_ERR_UNSUPPORTED;
+    HIPCHK(hipSetDevice(c->device));
+    free_scene(*c);
+    DScene& s = c->sc;
+    lumo_status st = LUMO_OK;
+    auto chk = [&](lumo_status x) {
+        if (x && !st) st = x;
+    };
+    chk(upload(*c, d->vertices, (size_t)3 * d->num_vertices, &s.vertices));
+    chk(upload(*c, d->normals, (size_t)3 * d->num_normals, &s.normals));
+    chk(upload(*c, d->uvs, (size_t)2 * d->num_uvs, &s.uvs));
+    chk(upload(*c, d->triangles, (size_t)d->num_triangles, &s.tris));
+    chk(upload(*c, d->kd_nodes, (size_t)d->num_kd_nodes, &s.kd));
+    chk(upload(*c, d->kd_items, (size_t)d->num_kd_items, &s.kd_items));
+    chk(upload(*c, d->objects, (size_t)d->num_objects, &s.objs));
+    chk(upload(*c, d->object_nodes, (size_t)d->num_object_nodes, &s.onodes));
+    chk(upload(*c, d->object_items, (size_t)d->num_object_items, &s.oitems));
+    chk(upload(*c, d->lights, (size_t)d->num_lights, &s.lights));
+    chk(upload(*c, d->light_nodes, (size_t)d->num_light_nodes, &s.lnodes));
+    chk(upload(*c, d->light_items, (size_t)d->num_light_items, &s.litems));
+    chk(upload(*c, d->alias_prob, (size_t)d->num_lights, &s.alias_prob));
+    chk(upload(*c, d->alias_idx, (size_t)d->num_lights, &s.alias_idx));
+    chk(upload(*c, d->alias_pdf, (size_t)d->num_lights, &s.alias_pdf));
+    chk(upload(*c, d->materials, (size_t)d->num_materials, &s.mats));
+    chk(upload(*c, d->dense_spectra, (size_t)95 * d->num_dense_spectra, &s.dense));
+    if (st) {
+        free_scene(*c);
+        return st;
+    }
+    s.n_onodes = d->num_object_nodes;
+    s.n_lnodes = d->num_light_nodes;
+    s.n_lights = d->num_lights;
+    int n = d->num_lights, lg = 0;
+    while (n > 1) {
+        n >>= 1;
+        lg++;
+    }
+    s.n_shadow = lg > 1 ? lg : 1;  // scene.rs:90-92
+    c->has_scene = true;
+    return LUMO_OK;
+}
+
+lumo_status lumo_camera_set(void* ctx, const lumo_camera_desc* d) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !d) return LUMO_ERR_INVALID;
+    if (d->orthographic) return LUMO_ERR_UNSUPPORTED;
+    if (d->width <= 0 || d->height <= 0 || !(d->filter_radius > 0.0) || !(d->filter_sigma > 0.0)) return LUMO_ERR_INVALID;
+    auto get = [](const double (&a)[2][16]) {
+        Xform x;
+        M4* ms[2] = {&x.m, &x.inv};
+        for (int q = 0; q < 2; ++q) {
+            V4* rows[4] = {&ms[q]->y0, &ms[q]->y1, &ms[q]->y2, &ms[q]->y3};
+            for (int r = 0; r < 4; ++r) *rows[r] = V4{a[q][4 * r], a[q][4 * r + 1], a[q][4 * r + 2], a[q][4 * r + 3]};
+        }
+        return x;
+    };
+    auto m3 = [](const double* a) { return M3{V3{a[0], a[1], a[2]}, V3{a[3], a[4], a[5]}, V3{a[6], a[7], a[8]}}; };
+    c->cam.wtc = get(d->world_to_camera);
+    c->cam.sctr = get(d->screen_to_raster);
+    c->cam.cts = get(d->camera_to_screen);
+    c->cam.lens_radius = d->lens_radius;
+    c->cam.focal_length = d->focal_length;
+    c->cam.wb = m3(d->white_balance);
+    c->cam.x2r = m3(d->xyz_to_rgb);
+    c->cam.fr = d->filter_radius;
+    c->cam.fsig = d->filter_sigma;
+    if ((uint64_t)std::ceil(d->filter_radius - 0.5) != 1) return LUMO_ERR_UNSUPPORTED;  // 3x3 gather footprint
+    c->has_camera = true;
+    return LUMO_OK;
+}
+
+lumo_status lumo_render_tiles(void* ctx, const lumo_tile_task* tasks, size_t n, const lumo_render_cfg* cfg,
+                              lumo_tile_result* out) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || (!tasks && n) || (!out && n)) return LUMO_ERR_INVALID;
+    if (cfg && cfg->rng_mode != LUMO_RNG_WAVEFRONT) return LUMO_ERR_UNSUPPORTED;
+    if (cfg && cfg->integrator != LUMO_INTEGRATOR_PATH_TRACE) return LUMO_ERR_UNSUPPORTED;
+    HIPCHK(hipSetDevice(c->device));
+    const size_t max_paths = (cfg && cfg->max_paths > 0) ? (size_t)cfg->max_paths : (size_t)1 << 30;
+    size_t i = 0;
+    while (i < n) {  // chunk the task list so that at most max_paths slots are in flight
+        size_t j = i, paths = 0;
+        while (j < n) {
+            const size_t P = (tasks[j].px_max[0] - tasks[j].px_min[0]) * (tasks[j].px_max[1] - tasks[j].px_min[1]);
+            if (j > i && paths + P > max_paths) break;
+            paths += P;
+            ++j;
+        }
+        const lumo_status st = render_impl(*c, tasks + i, j - i, out + i, nullptr, 0);
+        if (st) return st;
+        i = j;
+    }
+    return LUMO_OK;
+}
+
+lumo_status lumo_trace(void* ctx, const lumo_ray_soa* rays, size_t n, lumo_hit_soa* hits, int any_hit) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !rays || !hits || !rays->origin || !rays->dir || (any_hit && !rays->light)) return LUMO_ERR_INVALID;
+    if (!c->has_scene) return LUMO_ERR_NO_SCENE;
+    if (n == 0) return LUMO_OK;
+    HIPCHK(hipSetDevice(c->device));
+    if (any_hit)
+        for (size_t i = 0; i < n; ++i)
+            if (rays->light[i] < 0 || rays->light[i] >= c->sc.n_lights) return LUMO_ERR_INVALID;
+    lumo_status st = LUMO_OK;
+    double* o = wbuf<double>(*c, W_SH_O, 3 * n, st);
+    double* d = wbuf<double>(*c, W_SH_D, 3 * n, st);
+    int32_t* light = wbuf<int32_t>(*c, W_SH_LIGHT, n, st);
+    double* t = wbuf<double>(*c, W_HIT_T, n, st);
+    int32_t* kind = wbuf<int32_t>(*c, W_HIT_KIND, n, st);
+    int32_t* obj = wbuf<int32_t>(*c, W_HIT_OBJ, n, st);
+    int32_t* prim = wbuf<int32_t>(*c, W_HIT_TRI, n, st);
+    unsigned long long* tc = wbuf<unsigned long long>(*c, W_TCOUNT, 2 * TC_N, st);
+    if (st) return st;
+    hipStream_t sm = c->stream;
+    HIPCHK(hipMemcpyAsync(o, rays->origin, sizeof(double) * 3 * n, hipMemcpyHostToDevice, sm));
+    HIPCHK(hipMemcpyAsync(d, rays->dir, sizeof(double) * 3 * n, hipMemcpyHostToDevice, sm));
+    if (any_hit) HIPCHK(hipMemcpyAsync(light, rays->light, sizeof(int32_t) * n, hipMemcpyHostToDevice, sm));
+    HIPCHK(hipMemsetAsync(tc, 0, sizeof(unsigned long long) * 2 * TC_N, sm));
+    k_trace<<<ceil_div(n, BLOCK), BLOCK, 0, sm>>>(c->sc, o, d, light, (int)n, any_hit, t, kind, obj, prim, tc);
+    HIPCHK(hipGetLastError());
+    if (hits->t) HIPCHK(hipMemcpyAsync(hits->t, t, sizeof(double) * n, hipMemcpyDeviceToHost, sm));
+    if (hits->kind) HIPCHK(hipMemcpyAsync(hits->kind, kind, sizeof(int32_t) * n, hipMemcpyDeviceToHost, sm));
+    if (hits->object) HIPCHK(hipMemcpyAsync(hits->object, obj, sizeof(int32_t) * n, hipMemcpyDeviceToHost, sm));
+    if (hits->prim) HIPCHK(hipMemcpyAsync(hits->prim, prim, sizeof(int32_t) * n, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipStreamSynchronize(sm));
+    return LUMO_OK;
+}
+
+lumo_status lumo_stats_get(void* ctx, lumo_stats* stats) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !stats) return LUMO_ERR_INVALID;
+    *stats = c->stats;
+    return LUMO_OK;
+}
+
+lumo_status lumo_stats_reset(void* ctx) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return LUMO_ERR_INVALID;
+    std::memset(&c->stats, 0, sizeof(c->stats));
+    return LUMO_OK;
+}
+
+// Diagnostics: trace one slot (pass, pixel of a single-task render) bounce by bounce.
+lumo_status lumo_debug_trace(void* ctx, const lumo_tile_task* task, int pass, int pixel, double* out, int* n_out) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !task || !out || !n_out) return LUMO_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    DebugLog h{};
+    h.slot = pixel;
+    h.pass = pass;
+    h.cur_pass = -1;
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &h, sizeof(h)));
+    const lumo_status st = render_impl(*c, task, 1, nullptr, nullptr, 0);
+    if (st) return st;
+    HIPCHK(hipMemcpyFromSymbol(&h, HIP_SYMBOL(g_dbg), sizeof(h)));
+    *n_out = h.n;
+    std::memcpy(out, h.rec, sizeof(double) * 20 * h.n);
+    h.slot = -1;
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &h, sizeof(h)));
+    return LUMO_OK;
+}
+
+lumo_status lumo_debug_paths(void* ctx, const lumo_tile_task* task, lumo_path_dump* dump) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !task || !dump || !dump->radiance || !dump->lambda_ || !dump->raster || !dump->depth || !dump->delta)
+        return LUMO_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    Dump D{dump->radiance, dump->lambda_, dump->raster, dump->delta,
+           reinterpret_cast<unsigned long long*>(dump->depth)};
+    return render_impl(*c, task, 1, nullptr, &D, task->samples);
+}
+
+}  // extern "C"

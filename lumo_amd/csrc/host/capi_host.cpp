@@ -1,0 +1,163 @@
+// C ABI over the host scene builder (include/lumo_host.h).
+#include <cstring>
+#include <exception>
+
+#include "../../../include/lumo_host.h"
+#include "../common/rng.h"
+#include "rgb2spec.h"
+#include "scene.h"
+
+using namespace lumo;
+
+namespace {
+V3 v3p(const double* p) { return V3{p[0], p[1], p[2]}; }
+}  // namespace
+
+extern "C" {
+
+lumo_spectrum lumo_spectrum_from_rgb(double r, double g, double b) { return spectrum_from_rgb(r, g, b); }
+lumo_spectrum lumo_spectrum_from_srgb(int r, int g, int b) { return spectrum_from_srgb(r, g, b); }
+lumo_spectrum lumo_spectrum_from_pts(const char* pts) { return spectrum_from_pts(pts ? pts : ""); }
+
+void lumo_rgb2spec_cell(int l, int k, int j, int i, float out[3]) {
+    const SpecCoeffs c = rgb2spec_cell(l, k, j, i);
+    out[0] = c.c0;
+    out[1] = c.c1;
+    out[2] = c.c2;
+}
+int lumo_rgb2spec_write(const char* path, int threads) { return rgb2spec_write_table(path, threads) ? 0 : 1; }
+
+void* lumo_builder_new(void) { return new SceneBuilder(); }
+void lumo_builder_free(void* b) { delete static_cast<SceneBuilder*>(b); }
+
+int lumo_builder_material_lambertian(void* b, lumo_spectrum spec) {
+    return static_cast<SceneBuilder*>(b)->add_material(material_lambertian(spec));
+}
+int lumo_builder_material_light(void* b, lumo_spectrum tex, int illuminant, double scale, int two_sided) {
+    if (illuminant < 0 || illuminant >= DENSE_BUILTIN_COUNT) return -1;
+    return static_cast<SceneBuilder*>(b)->add_material(material_light(tex, illuminant, scale, two_sided != 0));
+}
+int lumo_builder_add_mesh(void* b, const double* vertices, int64_t nv, const int64_t* face_idx,
+                          const int64_t* face_sizes, int64_t nfaces, int material, int as_light) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (material < 0 || material >= (int)sb->materials.size()) return LUMO_ERR_INVALID;
+    std::vector<V3> vs;
+    for (int64_t i = 0; i < nv; ++i) vs.push_back(v3p(vertices + 3 * i));
+    std::vector<Face> faces;
+    int64_t off = 0;
+    for (int64_t f = 0; f < nfaces; ++f) {
+        Face fc;
+        if (face_sizes[f] < 3) return LUMO_ERR_INVALID;
+        for (int64_t k = 0; k < face_sizes[f]; ++k) {
+            const int64_t v = face_idx[off + k];
+            if (v < 0 || v >= nv) return LUMO_ERR_INVALID;
+            fc.vidx.push_back(v);
+        }
+        off += face_sizes[f];
+        faces.push_back(fc);
+    }
+    sb->add_mesh(vs, faces, {}, {}, material, as_light != 0);
+    return LUMO_OK;
+}
+int lumo_builder_add_rectangle(void* b, const double* a, const double* bb, const double* c, int material,
+                               int as_light) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (material < 0 || material >= (int)sb->materials.size()) return LUMO_ERR_INVALID;
+    sb->add_rectangle(v3p(a), v3p(bb), v3p(c), material, as_light != 0);
+    return LUMO_OK;
+}
+void* lumo_builder_cornell_box(void) { return new SceneBuilder(SceneBuilder::cornell_box()); }
+
+void* lumo_builder_build(void* b) {
+    try {
+        return build_scene(*static_cast<SceneBuilder*>(b)).release();
+    } catch (const std::exception&) {
+        return nullptr;
+    }
+}
+int lumo_scene_get_desc(void* scene, lumo_scene_desc* out) {
+    if (!scene || !out) return LUMO_ERR_INVALID;
+    *out = static_cast<FlatScene*>(scene)->desc();
+    return LUMO_OK;
+}
+void lumo_scene_free(void* scene) { delete static_cast<FlatScene*>(scene); }
+
+static void params_from(const CameraParams& c, lumo_camera_params* p) {
+    p->origin[0] = c.origin.x; p->origin[1] = c.origin.y; p->origin[2] = c.origin.z;
+    p->towards[0] = c.towards.x; p->towards[1] = c.towards.y; p->towards[2] = c.towards.z;
+    p->up[0] = c.up.x; p->up[1] = c.up.y; p->up[2] = c.up.z;
+    p->zoom = c.zoom;
+    p->lens_radius = c.lens_radius;
+    p->focal_length = c.focal_length;
+    p->vfov = c.vfov;
+    p->width = c.width;
+    p->height = c.height;
+    p->illuminant = c.illuminant;
+    p->color_space = c.color_space;
+    p->filter_radius = c.filter_radius;
+    p->filter_sigma = c.filter_sigma;
+}
+void lumo_camera_params_default(lumo_camera_params* p) { params_from(CameraParams{}, p); }
+void lumo_camera_params_cornell_box(lumo_camera_params* p) { params_from(CameraParams::cornell_box(), p); }
+
+int lumo_camera_build(const lumo_camera_params* p, lumo_camera_desc* out) {
+    if (!p || !out) return LUMO_ERR_INVALID;
+    if (p->width <= 0 || p->height <= 0 || !(p->zoom > 0.0) || !(p->vfov > 0.0 && p->vfov < 180.0) ||
+        p->lens_radius < 0.0 || p->illuminant < 0 || p->illuminant >= DENSE_BUILTIN_COUNT ||
+        !(p->filter_radius > 0.0) || !(p->filter_sigma > 0.0))
+        return LUMO_ERR_INVALID;
+    CameraParams c;
+    c.origin = v3p(p->origin);
+    c.towards = v3p(p->towards);
+    c.up = v3p(p->up);
+    if (!(distance_squared(c.towards, c.origin) > EPSILON) || length(c.up) == 0.0) return LUMO_ERR_INVALID;
+    c.zoom = p->zoom;
+    c.lens_radius = p->lens_radius;
+    c.focal_length = p->focal_length;
+    c.vfov = p->vfov;
+    c.width = p->width;
+    c.height = p->height;
+    c.illuminant = p->illuminant;
+    c.color_space = p->color_space;
+    c.filter_radius = p->filter_radius;
+    c.filter_sigma = p->filter_sigma;
+    *out = build_camera(c);
+    return LUMO_OK;
+}
+
+int64_t lumo_make_tasks(int64_t width, int64_t height, uint64_t samples, uint64_t seed, lumo_tile_task* tasks,
+                        int64_t cap) {
+    const uint64_t TILE = 16, INC = 256;  // renderer.rs:15-17
+    if (width <= 0 || height <= 0 || samples == 0) return 0;
+    Xorshift rng = xs_new(seed);
+    const uint64_t tiles_x = ((uint64_t)width + TILE - 1) / TILE, tiles_y = ((uint64_t)height + TILE - 1) / TILE;
+    int64_t count = 0;
+    uint64_t taken = 0;
+    while (taken < samples) {
+        const uint64_t prev = taken;
+        const uint64_t batch = taken / INC;
+        taken += INC;
+        if (taken > samples) taken = samples;
+        const uint64_t s = taken - prev;
+        for (uint64_t y = 0; y < tiles_y; ++y) {
+            for (uint64_t x = 0; x < tiles_x; ++x) {
+                const uint64_t task_seed = xs_u64(rng);
+                if (tasks && count < cap) {
+                    lumo_tile_task& t = tasks[count];
+                    t.px_min[0] = x * TILE;
+                    t.px_min[1] = y * TILE;
+                    t.px_max[0] = std::min(x * TILE + TILE, (uint64_t)width);
+                    t.px_max[1] = std::min(y * TILE + TILE, (uint64_t)height);
+                    t.batch = batch;
+                    t.samples = s;
+                    t.total_samples = samples;
+                    t.seed = task_seed;
+                }
+                count++;
+            }
+        }
+    }
+    return count;
+}
+
+}  // extern "C"

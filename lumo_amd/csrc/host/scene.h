@@ -1,0 +1,110 @@
+// Host scene model mirroring lumo's builder API (Scene / Material / TriangleMesh / Rectangle /
+// Camera::builder) and the build step that produces the flattened device image
+// (lumo_scene_desc).  Acceleration structures are built with lumo's own algorithms so the
+// GPU walks exactly the nodes lumo walks:
+//   * per-mesh SAH kd-tree: object/kdtree.rs:43-89, kdtree/node.rs:125-336
+//   * objects / lights BVH: object/bvh.rs:232-313, bvh/node.rs:26-211
+//   * light power alias table: object/bvh.rs:105-191
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../../include/lumo_amd.h"
+#include "color.h"
+
+namespace lumo {
+
+struct HostMaterial {
+    lumo_material m{};
+    const Dense* illum = nullptr;  // light illuminant (dense)
+    Dense illum_owned;
+    bool has_owned = false;
+};
+
+HostMaterial material_lambertian(lumo_spectrum spec);
+HostMaterial material_light(lumo_spectrum tex, int illuminant_builtin, double scale, bool two_sided);
+
+struct Face {
+    std::vector<int64_t> vidx, nidx, tidx;
+};
+
+// One lumo `Object` / `Sampleable` before flattening.
+struct HostObject {
+    int type = LUMO_OBJ_KDMESH;
+    int material = 0;               // index into SceneBuilder::materials
+    std::vector<V3> vertices;
+    std::vector<V3> normals;
+    std::vector<V2> uvs;
+    struct Tri {
+        int64_t v[3], n[3], t[3];
+    };
+    std::vector<Tri> tris;
+    V3 origin{}, b0{}, b1{};        // Rectangle
+};
+
+struct KdBuilt {
+    std::vector<lumo_kd_node> nodes;
+    std::vector<int32_t> items;
+    V3 bmin, bmax;
+};
+// Build lumo's SAH kd-tree over the triangles of `obj` (exactly KdTree::new).
+KdBuilt build_kdtree(const HostObject& obj);
+
+struct BvhBuilt {
+    std::vector<lumo_bvh_node> nodes;
+    std::vector<int32_t> items;
+};
+// Build lumo's BVH over objects with the given bounding boxes (BVH::_build).
+BvhBuilt build_bvh(const std::vector<V3>& bmin, const std::vector<V3>& bmax);
+
+class SceneBuilder {
+   public:
+    std::vector<HostMaterial> materials;
+    std::vector<HostObject> objects;
+    std::vector<HostObject> lights;
+
+    int add_material(const HostMaterial& m);
+    // TriangleMesh::new (triangle_mesh.rs:46-60): fan-triangulated faces, degenerate dropped.
+    void add_mesh(const std::vector<V3>& vertices, const std::vector<Face>& faces,
+                  const std::vector<V3>& normals, const std::vector<V2>& uvs, int material, bool as_light = false);
+    // Rectangle::new(Mat3(a, b, c), material) (rectangle.rs:23-45)
+    void add_rectangle(V3 a, V3 b, V3 c, int material, bool as_light);
+
+    // Scene::cornell_box (scene/cornell_box.rs:8-193)
+    static SceneBuilder cornell_box();
+};
+
+// Owning flattened scene; desc() points into the vectors.
+struct FlatScene {
+    std::vector<double> vertices, normals, uvs;
+    std::vector<lumo_triangle> triangles;
+    std::vector<lumo_kd_node> kd_nodes;
+    std::vector<int32_t> kd_items;
+    std::vector<lumo_object> objects, lights;
+    std::vector<lumo_bvh_node> object_nodes, light_nodes;
+    std::vector<int32_t> object_items, light_items;
+    std::vector<double> alias_prob, alias_pdf;
+    std::vector<int32_t> alias_idx;
+    std::vector<lumo_material> materials;
+    std::vector<double> dense;
+    lumo_scene_desc desc() const;
+};
+
+// Scene::build (scene.rs:33-52) + flattening.
+std::unique_ptr<FlatScene> build_scene(const SceneBuilder& sb);
+
+// Camera::builder() (camera/builder.rs) -> lumo_camera_desc
+struct CameraParams {
+    V3 origin{0, 0, 0}, towards{0, 0, -1}, up{0, 1, 0};
+    double zoom = 1.0, lens_radius = 0.0, focal_length = 0.0, vfov = 90.0;
+    int64_t width = 1024, height = 768;
+    int illuminant = DENSE_D65;
+    int color_space = CS_DCI_P3;
+    double filter_radius = 1.5, filter_sigma = 1.5 / 4.0;
+    static CameraParams cornell_box();  // camera.rs:139-148
+};
+lumo_camera_desc build_camera(const CameraParams& p);
+Xform xf_desc_get(const double (&a)[2][16]);
+
+}  // namespace lumo

@@ -1,0 +1,66 @@
+/* ORACLE — test infrastructure only.
+ *
+ * CPU restatement (f64, scalar C++) of lumo's render hot path, used ONLY by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker / baseline.
+ * The product (lumo_amd) never links, loads or calls anything under oracle/.
+ *
+ * It consumes the same flattened scene and camera (include/lumo_amd.h) the GPU path
+ * consumes, and restates, function by function, with file:line citations in oracle.cpp:
+ *   renderer.rs / renderer/task.rs   tile tasks, per-pixel samplers, adaptive-RR delta
+ *   samplers.rs, rng.rs, rng/maps.rs  MultiJittered sampler, Xorshiftr128+, disk maps
+ *   integrator.rs, path_trace.rs      path tracing with NEE + MIS + Russian roulette
+ *   scene.rs, object/{bvh,kdtree,triangle,rectangle,aabb}.rs  traversal + intersection
+ *   hit.rs, ray.rs, onb.rs, efloat.rs robust spawning, shading frame
+ *   material.rs, bsdf.rs, bxdf.rs, bxdf/scatter.rs  Lambertian + Light
+ *   color/{color,wavelength,spectrum,dense_spectrum,xyz,space}.rs  hero wavelengths
+ *   camera.rs, film.rs, film/tile.rs, filter.rs, tone_mapping.rs
+ *
+ * Parity pins: lumo's Rust crate cannot be built here (no cargo; srgb.coeff missing), so
+ * the oracle is pinned by the reference's own known-answer vectors (spectrum_tests.rs)
+ * and property tests (kd-tree reachability, hit/hit_t consistency, scene visibility,
+ * filter integrals) — see tests/ and DESIGN.md §Oracle.
+ *
+ * Two sample-stream orders:
+ *   ORACLE_LUMO_ORDER  exactly lumo's tile-serial Xorshift stream (task.rs:27-76);
+ *   ORACLE_WAVEFRONT   the per-path stream order the GPU implements.
+ */
+#ifndef LUMO_ORACLE_H
+#define LUMO_ORACLE_H
+#include "../include/lumo_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORACLE_WAVEFRONT = 0, ORACLE_LUMO_ORDER = 1 };
+
+typedef struct {
+    uint64_t aabb_tests;   /* BVH node + kd boundary slab tests */
+    uint64_t kd_nodes;     /* kd interior node visits           */
+    uint64_t tri_tests;    /* triangle tests (any kind)         */
+    uint64_t closest_queries, shadow_queries;
+} oracle_counters;
+
+/* Render `n` tile tasks; `threads` worker threads (tasks are independent). */
+int oracle_render_tiles(const lumo_scene_desc* scene, const lumo_camera_desc* camera,
+                        const lumo_tile_task* tasks, size_t n, int mode, int threads,
+                        lumo_tile_result* out, oracle_counters* counters);
+
+/* Per-path record of the wavefront order for one task (for per-path parity tests):
+ * out arrays sized (pixels * samples), pixel-major within each pass (pass s, pixel j). */
+int oracle_trace_paths(const lumo_scene_desc* scene, const lumo_camera_desc* camera,
+                       const lumo_tile_task* task, double* radiance4, double* lambda4,
+                       double* raster2, uint64_t* depth, double* delta_per_pass);
+
+/* Diagnostics: per-bounce record of path (pass, pixel) of one task (20 doubles each). */
+int oracle_debug_trace(const lumo_scene_desc* scene, const lumo_camera_desc* camera,
+                       const lumo_tile_task* task, int pass, int pixel, double* out, int* n_out);
+
+/* Scene::hit (any_hit = 0) or Scene::hit_light (any_hit != 0) for a batch of rays. */
+int oracle_trace(const lumo_scene_desc* scene, const lumo_ray_soa* rays, size_t n,
+                 lumo_hit_soa* hits, int any_hit, oracle_counters* counters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

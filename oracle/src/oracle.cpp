@@ -1,0 +1,1030 @@
+// ORACLE (test infrastructure only; see oracle/oracle.h).  Scalar f64 restatement of
+// lumo's render path.  Shares only the plain vector algebra and the Xorshift generator
+// (lumo_amd/csrc/common/{vec,rng}.h, themselves restatements of math/*.rs and rng.rs);
+// every algorithm below is restated here independently of the HIP kernels.
+#include "../oracle.h"
+
+#ifdef LUMO_ORACLE_GLIBC  // sensitivity build: platform libm as Rust std would call it
+#include <cmath>
+#define LUMO_COS std::cos
+#define LUMO_SIN std::sin
+#define O_LOG1P std::log1p
+#define O_COSH std::cosh
+#define O_EXP std::exp
+#else
+#define O_LOG1P lumo::lm_log1p
+#define O_COSH lumo::lm_cosh
+#define O_EXP lumo::lm_exp
+#endif
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <thread>
+#include <vector>
+
+#include "../../lumo_amd/csrc/common/lmath.h"
+#include "../../lumo_amd/csrc/common/rng.h"
+#include "../../lumo_amd/csrc/common/vec.h"
+
+using namespace lumo;
+
+namespace {
+
+constexpr double INF = std::numeric_limits<double>::infinity();
+constexpr int NS = 4;  // SPECTRUM_SAMPLES (color.rs:60)
+constexpr double LMIN = 360.0, LMAX = 830.0;
+constexpr double Y_INTEGRAL = 106.856895;
+constexpr double SAMPLE_VISIBLE_INTEGRAL = 253.819;
+constexpr uint64_t SAMPLES_INCREMENT = 256;  // renderer.rs:17
+constexpr int RR_DEPTH = 5;                  // path_trace.rs:3
+
+struct Counters {
+    uint64_t aabb = 0, kd = 0, tri = 0, closest = 0, shadow = 0;
+};
+
+// ------------------------------------------------------------------ colour (color.rs)
+struct Color {
+    double s[NS];
+};
+Color cconst(double v) { return Color{{v, v, v, v}}; }
+Color operator+(Color a, Color b) {
+    for (int i = 0; i < NS; ++i) a.s[i] = a.s[i] + b.s[i];
+    return a;
+}
+Color operator*(Color a, Color b) {
+    for (int i = 0; i < NS; ++i) a.s[i] = a.s[i] * b.s[i];
+    return a;
+}
+Color operator*(Color a, double v) {
+    for (int i = 0; i < NS; ++i) a.s[i] = a.s[i] * v;
+    return a;
+}
+Color operator*(double v, Color a) {
+    for (int i = 0; i < NS; ++i) a.s[i] = v * a.s[i];
+    return a;
+}
+// color.rs:239-272: division by zero gives zero
+Color operator/(Color a, Color b) {
+    for (int i = 0; i < NS; ++i) a.s[i] = b.s[i] == 0.0 ? 0.0 : a.s[i] / b.s[i];
+    return a;
+}
+Color operator/(Color a, double v) {
+    for (int i = 0; i < NS; ++i) a.s[i] = v == 0.0 ? 0.0 : a.s[i] / v;
+    return a;
+}
+double cmean(const Color& c) {
+    double sum = 0.0;
+    for (int i = 0; i < NS; ++i) sum += c.s[i];
+    return sum / NS;
+}
+
+struct Lambda {
+    double l[NS];
+};
+// wavelength.rs:55-59; Rust atanh(x) = 0.5 * ln_1p(2x / (1 - x))
+double wl_sample_one(double v) {
+    const double x = 0.85691062 - SAMPLE_VISIBLE_INTEGRAL * v * 0.0072;
+    return 538.0 - 138.888889 * (0.5 * O_LOG1P((2.0 * x) / (1.0 - x)));
+}
+// wavelength.rs:36-47
+Lambda wl_sample(double rand_u) {
+    Lambda L;
+    for (int i = 0; i < NS; ++i) {
+        double v = rand_u + (double)i / (double)NS;
+        v = v > 1.0 ? v - 1.0 : v;
+        L.l[i] = wl_sample_one(v);
+    }
+    return L;
+}
+double wl_pdf_one(double l) {  // wavelength.rs:67-74
+    if (l < LMIN || l > LMAX) return 0.0;
+    const double c = O_COSH(0.0072 * (l - 538.05));
+    return 1.0 / (SAMPLE_VISIBLE_INTEGRAL * (c * c));
+}
+bool wl_terminated(const Lambda& L) {
+    for (int i = 1; i < NS; ++i)
+        if (L.l[i] != 0.0) return false;
+    return true;
+}
+Color wl_pdf(const Lambda& L) {  // wavelength.rs:24-32
+    Color c;
+    for (int i = 0; i < NS; ++i) c.s[i] = wl_pdf_one(L.l[i]);
+    if (wl_terminated(L)) c.s[0] /= (double)NS;
+    return c;
+}
+
+// dense_spectrum.rs:77-97
+double dense_one(const double* v, double lambda) {
+    const double STEP = (LMAX - LMIN) / (95.0 - 1.0);
+    const double fb = std::ceil((lambda - LMIN) / STEP);
+    size_t b1 = fb > 0.0 ? (size_t)fb : 0;  // Rust `as usize` saturates
+    const double l1 = LMIN + STEP * (double)b1;
+    if (lambda == 0.0) return 0.0;
+    if (b1 > 94) b1 = 94;  // out-of-range wavelengths would panic in Rust (unreachable)
+    if (lambda == l1) return v[b1];
+    const size_t b0 = b1 == 0 ? 0 : b1 - 1;
+    const double l0 = l1 - STEP;
+    const double x1 = (lambda - l0) / STEP;
+    const double x0 = 1.0 - x1;
+    return v[b0] * x0 + v[b1] * x1;
+}
+Color dense_sample(const double* v, const Lambda& L) {
+    Color c;
+    for (int i = 0; i < NS; ++i) c.s[i] = dense_one(v, L.l[i]);
+    return c;
+}
+// spectrum.rs:108-124 (f32 sigmoid polynomial)
+double spec_one(const lumo_spectrum& s, double lambda) {
+    const float l = (float)lambda;
+    const float x = s.c0 * l * l + s.c1 * l + s.c2;
+    const float sig = 0.5f + x / (2.0f * std::sqrt(1.0f + x * x));
+    return (double)(s.scale * sig);
+}
+Color spec_sample(const lumo_spectrum& s, const Lambda& L) {
+    Color c;
+    for (int i = 0; i < NS; ++i) c.s[i] = spec_one(s, L.l[i]);
+    return c;
+}
+
+// ------------------------------------------------------------------ scene access
+struct Scene {
+    const lumo_scene_desc* d;
+    const double* dense(int idx) const { return d->dense_spectra + 95 * idx; }
+    V3 vert(int i) const { return V3{d->vertices[3 * i], d->vertices[3 * i + 1], d->vertices[3 * i + 2]}; }
+    int num_shadow_rays() const {  // scene.rs:90-92
+        int n = d->num_lights, lg = 0;
+        while (n > 1) {
+            n >>= 1;
+            lg++;
+        }
+        return lg > 1 ? lg : 1;
+    }
+};
+double luminance(const Scene& sc, const Color& c, const Lambda& L) {  // color.rs:91-94
+    const Color pdf = wl_pdf(L);
+    return cmean(dense_sample(sc.dense(1), L) * c / pdf) / Y_INTEGRAL;
+}
+V3 color_xyz(const Scene& sc, const Color& c, const Lambda& L) {  // color.rs:97-105
+    const Color pdf = wl_pdf(L);
+    return V3{cmean(dense_sample(sc.dense(0), L) * c / pdf), cmean(dense_sample(sc.dense(1), L) * c / pdf),
+              cmean(dense_sample(sc.dense(2), L) * c / pdf)} /
+           Y_INTEGRAL;
+}
+
+struct Ray {
+    V3 origin, dir;
+};
+Ray ray_new(V3 o, V3 d) { return Ray{o, normalize(d)}; }  // ray.rs:14-19
+
+struct Hit {
+    double t;
+    int material;
+    V3 p, fp_error, ns, ng;
+    V2 uv;
+    bool backface;
+};
+
+V2 wrap_uv(V2 uv) {  // hit.rs:61-68
+    V2 f{rfract(uv.x), rfract(uv.y)};
+    return V2{f.x < 0.0 ? f.x + 1.0 : f.x, f.y < 0.0 ? f.y + 1.0 : f.y};
+}
+Hit hit_new(double t, int material, V3 wo, V3 xi, V3 err, V3 ns, V3 ng, V2 uv) {  // hit.rs:37-59
+    Hit h;
+    h.t = t;
+    h.material = material;
+    h.backface = dot(wo, ng) > 0.0;
+    h.p = xi;
+    h.fp_error = err;
+    h.ns = ns;
+    h.ng = ng;
+    h.uv = wrap_uv(uv);
+    return h;
+}
+// hit.rs:84-112
+V3 ray_origin(const Hit& h, bool outside) {
+    const V3 ne = h.ng;
+    const double scaled_err = dot(h.fp_error, vabs(ne));
+    const V3 offset = outside ? ne * scaled_err : (-ne) * scaled_err;
+    const V3 xi = h.p + offset;
+    auto mv = [](double v, double n) { return n > 0.0 ? next_float(v) : (n < 0.0 ? previous_float(v) : v); };
+    return V3{mv(xi.x, offset.x), mv(xi.y, offset.y), mv(xi.z, offset.z)};
+}
+Ray generate_ray(const Hit& h, V3 wi) { return ray_new(ray_origin(h, dot(wi, h.ng) >= 0.0), wi); }  // hit.rs:115-123
+
+// ------------------------------------------------------------------ intersection
+// aabb.rs:33-44
+void aabb_intersect(const double* bmin, const double* bmax, V3 o, V3 inv, double& ts, double& te) {
+    const V3 ro_min = (V3{bmin[0], bmin[1], bmin[2]} - o) * inv;
+    const V3 ro_max = (V3{bmax[0], bmax[1], bmax[2]} - o) * inv;
+    ts = max_element(vmin(ro_min, ro_max));
+    te = min_element(vmax(ro_max, ro_min)) * (1.0 + 2.0 * gamma_n(3));
+}
+
+// triangle.rs:63-187. Returns INF on miss; fills *out when geo.
+double triangle_hit(const Scene& sc, int ti, const Ray& r, double t_min, double t_max, bool geo, Hit* out,
+                    Counters& C) {
+    C.tri++;
+    const lumo_triangle& T = sc.d->triangles[ti];
+    const V3 A = sc.vert(T.v[0]), B = sc.vert(T.v[1]), Cv = sc.vert(T.v[2]);
+    const V3 xo = r.origin;
+    const V3 wa = vabs(r.dir);
+    const int kz = (wa.x > wa.y && wa.x > wa.z) ? 0 : (wa.y > wa.z ? 1 : 2);
+    auto permute = [kz](V3 v) { return kz == 0 ? V3{v.y, v.z, v.x} : (kz == 1 ? V3{v.z, v.x, v.y} : v); };
+    const V3 wi = permute(r.dir);
+    V3 at = permute(A - xo), bt = permute(B - xo), ct = permute(Cv - xo);
+    const V3 shear = V3{-wi.x, -wi.y, 0.0} / wi.z;
+    at = at + shear * at.z;
+    bt = bt + shear * bt.z;
+    ct = ct + shear * ct.z;
+    const V3 edges = V3{bt.x * ct.y - bt.y * ct.x, ct.x * at.y - ct.y * at.x, at.x * bt.y - at.y * bt.x};
+    if (min_element(edges) < 0.0 && max_element(edges) > 0.0) return INF;
+    const double det = dot(edges, V3{1.0, 1.0, 1.0});
+    if (det == 0.0) return INF;
+    const double t_scaled = dot(edges, V3{at.z, bt.z, ct.z}) / wi.z;
+    const bool b1 = det < 0.0 && (t_scaled > t_min * det || t_scaled < t_max * det);
+    const bool b2 = det > 0.0 && (t_scaled < t_min * det || t_scaled > t_max * det);
+    if (b1 || b2) return INF;
+    const double t = t_scaled / det;
+    if (!geo) return t;
+    const double max_z_v = rmax(rmax(fabs(at.z), fabs(bt.z)), fabs(ct.z));
+    const double delta_z = gamma_n(3) * max_z_v;
+    const double max_y_v = rmax(rmax(fabs(at.y), fabs(bt.y)), fabs(ct.y));
+    const double delta_y = gamma_n(5) * (max_y_v + max_z_v);
+    const double max_x_v = rmax(rmax(fabs(at.x), fabs(bt.x)), fabs(ct.x));
+    const double delta_x = gamma_n(5) * (max_x_v + max_z_v);
+    const double delta_e = 2.0 * (gamma_n(2) * max_x_v * max_y_v + delta_y * max_x_v + delta_x * max_y_v);
+    const double max_e = rmax(rmax(fabs(edges.x), fabs(edges.y)), fabs(edges.z));
+    const double delta_t = 3.0 * (gamma_n(3) * max_e * max_z_v + delta_e * max_z_v + delta_z * max_e) / fabs(det);
+    if (t <= t_min + delta_t) return INF;
+    const V3 bary = edges / det;
+    const double alpha = bary.x, beta = bary.y, gam = bary.z;
+    const V3 ng = normalize(cross(B - A, Cv - A));
+    V3 ns = ng;
+    if (T.n[0] >= 0) {
+        auto nv = [&](int i) {
+            return V3{sc.d->normals[3 * i], sc.d->normals[3 * i + 1], sc.d->normals[3 * i + 2]};
+        };
+        ns = normalize(bary.x * nv(T.n[0]) + bary.y * nv(T.n[1]) + bary.z * nv(T.n[2]));
+    }
+    const V3 xi = alpha * A + beta * B + gam * Cv;
+    V2 ta{0, 0}, tb{1, 0}, tc{1, 1};
+    if (T.t[0] >= 0) {
+        auto uv = [&](int i) { return V2{sc.d->uvs[2 * i], sc.d->uvs[2 * i + 1]}; };
+        ta = uv(T.t[0]);
+        tb = uv(T.t[1]);
+        tc = uv(T.t[2]);
+    }
+    const V2 uv = alpha * ta + beta * tb + gam * tc;
+    const V3 err = gamma_n(7) * V3{dot(vabs(bary * V3{A.x, B.x, Cv.x}), V3{1, 1, 1}),
+                                   dot(vabs(bary * V3{A.y, B.y, Cv.y}), V3{1, 1, 1}),
+                                   dot(vabs(bary * V3{A.z, B.z, Cv.z}), V3{1, 1, 1})};
+    *out = hit_new(t, T.material, r.dir, xi, err, ns, ng, uv);
+    return t;
+}
+
+// kdtree.rs:101-169.  geo: returns true + *out on hit; !geo: returns true, *t_out.
+bool kdtree_hit(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, bool geo, Hit* out,
+                double* t_out, Counters& C) {
+    const double origin[3] = {r.origin.x, r.origin.y, r.origin.z};
+    const double inv_dir[3] = {1.0 / r.dir.x, 1.0 / r.dir.y, 1.0 / r.dir.z};
+    struct Entry {
+        int node;
+        double ts, te;
+    } stack[64];
+    int sp = 0;
+    double t_hit = INF;
+    int curr = ob.kd_root;
+    int idx = -1;
+    double ts, te;
+    C.aabb++;
+    aabb_intersect(ob.bmin, ob.bmax, r.origin, 1.0 / r.dir, ts, te);
+    double t_start = rmax(ts, t_min), t_end = rmin(te, t_max);
+    for (;;) {
+        if (t_hit < t_start) break;
+        const lumo_kd_node& node = sc.d->kd_nodes[curr];
+        if (node.leaf) {
+            for (int k = 0; k < node.count; ++k) {
+                const int i = sc.d->kd_items[ob.item_base + node.first + k];
+                Hit dummy;
+                const double t = triangle_hit(sc, ob.tri_base + i, r, t_min, t_end, false, &dummy, C);
+                if (geo) {
+                    if (t < t_end) {
+                        t_end = t;
+                        t_hit = t;
+                        idx = i;
+                    }
+                } else if (t < t_end) {
+                    *t_out = t;
+                    return true;
+                }
+            }
+            if (sp == 0) break;
+            sp--;
+            curr = stack[sp].node;
+            t_start = stack[sp].ts;
+            t_end = stack[sp].te;
+        } else {
+            C.kd++;
+            const int ax = node.axis;
+            const double point = node.point;
+            const double t_split = (point - origin[ax]) * inv_dir[ax];
+            const bool left_first = origin[ax] < point || (origin[ax] == point && inv_dir[ax] <= 0.0);
+            const int first = left_first ? curr + 1 : node.right;
+            const int second = left_first ? node.right : curr + 1;
+            if (t_split > t_end || t_split <= 0.0) {
+                curr = first;
+            } else if (t_split < t_start) {
+                curr = second;
+            } else {
+                curr = first;
+                stack[sp] = Entry{second, t_split, t_end};
+                t_end = t_split;
+                sp++;
+            }
+        }
+    }
+    if (idx < 0) return false;
+    if (geo) {
+        const double t = triangle_hit(sc, ob.tri_base + idx, r, t_min, t_max, true, out, C);
+        return t != INF;
+    }
+    *t_out = INF;
+    return true;
+}
+
+// Object::hit / hit_t for the flattened object kinds
+bool object_hit(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, Hit* out,
+                Counters& C) {
+    if (!kdtree_hit(sc, ob, r, t_min, t_max, true, out, nullptr, C)) return false;
+    if (ob.type == LUMO_OBJ_RECTANGLE) {  // rectangle.rs:74-85
+        const V3 b0{ob.b0[0], ob.b0[1], ob.b0[2]}, b1{ob.b1[0], ob.b1[1], ob.b1[2]};
+        out->uv = wrap_uv(V2{dot(b0, out->p), dot(b1, out->p)});
+    }
+    return true;
+}
+double object_hit_t(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, Counters& C) {
+    double t = INF;
+    if (!kdtree_hit(sc, ob, r, t_min, t_max, false, nullptr, &t, C)) return INF;
+    return t;
+}
+
+// bvh.rs:315-362. Returns index or -1.
+int bvh_hit_idx(const Scene& sc, const lumo_bvh_node* nodes, int n_nodes, const int32_t* items,
+                const lumo_object* objs, const Ray& r, double t_min, double t_max, bool geo, Counters& C) {
+    if (n_nodes == 0) return -1;
+    const V3 origin = r.origin;
+    const V3 inv_dir = 1.0 / r.dir;
+    int stack[64];
+    int sp = 0, curr = 0, idx = -1;
+    double tt = t_max;
+    for (;;) {
+        const lumo_bvh_node& node = nodes[curr];
+        double ts, te;
+        C.aabb++;
+        aabb_intersect(node.bmin, node.bmax, origin, inv_dir, ts, te);
+        ts = rmax(ts, t_min);
+        te = rmin(te, tt);
+        if (ts <= te) {
+            if (node.count == 0) {
+                curr += 1;
+                if (node.right >= 0) stack[sp++] = node.right;
+                continue;
+            }
+            for (int k = 0; k < node.count; ++k) {
+                const int i = items[node.first + k];
+                const double t = object_hit_t(sc, objs[i], r, t_min, tt, C);
+                if (geo) {
+                    if (t < tt) {
+                        tt = t;
+                        idx = i;
+                    }
+                } else if (t < tt) {
+                    return i;
+                }
+            }
+        }
+        if (sp == 0) break;
+        curr = stack[--sp];
+    }
+    return idx;
+}
+
+struct BvhView {
+    const lumo_bvh_node* nodes;
+    int n;
+    const int32_t* items;
+    const lumo_object* objs;
+};
+BvhView objects_of(const Scene& sc) {
+    return BvhView{sc.d->object_nodes, sc.d->num_object_nodes, sc.d->object_items, sc.d->objects};
+}
+BvhView lights_of(const Scene& sc) {
+    return BvhView{sc.d->light_nodes, sc.d->num_light_nodes, sc.d->light_items, sc.d->lights};
+}
+bool bvh_hit(const Scene& sc, const BvhView& b, const Ray& r, double t_min, double t_max, Hit* out, int* which,
+             Counters& C) {
+    const int idx = bvh_hit_idx(sc, b.nodes, b.n, b.items, b.objs, r, t_min, t_max, true, C);
+    if (idx < 0) return false;
+    if (!object_hit(sc, b.objs[idx], r, t_min, t_max, out, C)) return false;
+    if (which) *which = idx;
+    return true;
+}
+double bvh_hit_t(const Scene& sc, const BvhView& b, const Ray& r, double t_min, double t_max, Counters& C) {
+    const int idx = bvh_hit_idx(sc, b.nodes, b.n, b.items, b.objs, r, t_min, t_max, false, C);
+    if (idx < 0) return INF;
+    return object_hit_t(sc, b.objs[idx], r, t_min, t_max, C);
+}
+
+// scene.rs:119-147. kind: 0 miss, 1 object, 2 light.
+bool scene_hit(const Scene& sc, const Ray& r, Hit* h, int* kind, int* which, Counters& C) {
+    C.closest++;
+    double t_max = INF;
+    bool found = false;
+    *kind = 0;
+    Hit tmp;
+    int w = -1;
+    if (bvh_hit(sc, objects_of(sc), r, 0.0, t_max, &tmp, &w, C)) {
+        *h = tmp;
+        found = true;
+        *kind = 1;
+        *which = w;
+        t_max = tmp.t;
+    }
+    if (bvh_hit(sc, lights_of(sc), r, 0.0, t_max, &tmp, &w, C)) {
+        *h = tmp;
+        found = true;
+        *kind = 2;
+        *which = w;
+    }
+    return found;
+}
+
+// scene.rs:165-189
+bool scene_hit_light(const Scene& sc, const Ray& r, int light, Hit* out, Counters& C) {
+    C.shadow++;
+    Hit lh;
+    if (!object_hit(sc, sc.d->lights[light], r, 0.0, INF, &lh, C)) return false;
+    const double t_max = lh.t - EPSILON;
+    if (bvh_hit_t(sc, objects_of(sc), r, 0.0, t_max, C) < t_max) return false;
+    if (bvh_hit_t(sc, lights_of(sc), r, 0.0, t_max, C) < t_max) return false;
+    *out = lh;
+    return true;
+}
+
+// ------------------------------------------------------------------ materials
+const lumo_material& mat(const Scene& sc, int m) { return sc.d->materials[m]; }
+
+struct Onb {
+    V3 u, v, w;
+};
+Onb onb_new(V3 w) {  // onb.rs:19-39 (Duff et al.)
+    const double sgn = rsignum(w.z);
+    const double a = -1.0 / (sgn + w.z);
+    const double b = w.x * w.y * a;
+    return Onb{V3{1.0 + sgn * w.x * w.x * a, sgn * b, -sgn * w.x}, V3{b, sgn + w.y * w.y * a, -w.y}, w};
+}
+V3 onb_to_world(const Onb& o, V3 v) { return v.x * o.u + v.y * o.v + v.z * o.w; }
+V3 onb_to_local(const Onb& o, V3 v) { return V3{dot(v, o.u), dot(v, o.v), dot(v, o.w)}; }
+
+bool is_reflection_bxdf(int kind) { return kind != LUMO_MAT_MF_DIELECTRIC; }
+
+// material.rs:273-289 -> bsdf.rs:51-67 -> bxdf.rs:104-124
+bool bsdf_sample(const Scene& sc, const Hit& h, V3 wo, double rand_u, V2 rand_sq, V3* wi) {
+    (void)rand_u;
+    const lumo_material& m = mat(sc, h.material);
+    if (m.kind != LUMO_MAT_LAMBERTIAN) return false;  // Light / Blank -> None
+    const Onb uvw = onb_new(h.ns);
+    (void)onb_to_local(uvw, wo);
+    if (h.backface && is_reflection_bxdf(m.kind)) return false;
+    *wi = onb_to_world(uvw, square_to_cos_hemisphere(rand_sq));
+    return true;
+}
+// material.rs:292-306 -> bsdf.rs:70-84 -> bxdf.rs:127-150 -> scatter.rs:16-26
+double bsdf_pdf(const Scene& sc, const Hit& h, V3 wo, V3 wi) {
+    const lumo_material& m = mat(sc, h.material);
+    if (m.kind != LUMO_MAT_LAMBERTIAN) return 0.0;
+    const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
+    const Onb uvw = onb_new(h.ns);
+    const V3 wol = onb_to_local(uvw, wo), wil = onb_to_local(uvw, wi);
+    if (!reflection) return 0.0;
+    if (!(wol.z * wil.z > 0.0)) return 0.0;
+    const double cos_theta = wil.z;
+    return cos_theta > 0.0 ? cos_theta / PI : 0.0;
+}
+// material.rs:254-270 -> bsdf.rs:28-48 -> bxdf.rs:71-100
+Color bsdf_f(const Scene& sc, const Hit& h, V3 wo, V3 wi, const Lambda& L) {
+    const lumo_material& m = mat(sc, h.material);
+    if (m.kind != LUMO_MAT_LAMBERTIAN) return cconst(0.0);
+    const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
+    if ((!reflection || h.backface) && is_reflection_bxdf(m.kind)) return cconst(0.0);
+    return spec_sample(m.albedo, L) / PI;
+}
+double shading_cosine(const Scene& sc, int material, V3 wi, V3 ns) {  // material.rs:315-320
+    return mat(sc, material).kind == LUMO_MAT_LIGHT || mat(sc, material).kind == LUMO_MAT_BLANK ? 1.0
+                                                                                                 : fabs(dot(ns, wi));
+}
+bool is_specular(const Scene& sc, int material) { (void)sc, (void)material; return false; }  // Lambertian/Light
+bool is_delta(const Scene& sc, int material) { (void)sc, (void)material; return false; }
+// material.rs:223-234
+Color emit(const Scene& sc, int material, const Lambda& L, const Hit& h) {
+    const lumo_material& m = mat(sc, material);
+    if (m.kind != LUMO_MAT_LIGHT) return cconst(0.0);
+    if (!m.two_sided && h.backface) return cconst(0.0);
+    return m.scale * spec_sample(m.albedo, L) * dense_sample(sc.dense(m.illuminant), L);
+}
+
+// lights (bvh.rs:51-86, rectangle.rs:113-134, object.rs:138-156)
+int sample_light(const Scene& sc, double rand_u) {
+    const double u = rand_u * (double)sc.d->num_lights;
+    const double fl = std::floor(u);
+    const size_t idx = fl > 0.0 ? (size_t)fl : 0;
+    const double fr = rfract(u);
+    return fr < sc.d->alias_prob[idx] ? (int)idx : sc.d->alias_idx[idx];
+}
+V3 light_sample_on(const lumo_object& L, V2 rs) {  // Rectangle::sample_on -> point only
+    const V3 o{L.origin[0], L.origin[1], L.origin[2]}, b0{L.b0[0], L.b0[1], L.b0[2]}, b1{L.b1[0], L.b1[1], L.b1[2]};
+    return o + rs.x * b0 + rs.y * b1;
+}
+V3 light_sample_towards(const lumo_object& L, V3 xo, V2 rs) { return normalize(light_sample_on(L, rs) - xo); }
+double light_sample_towards_pdf(const lumo_object& L, const Ray& ri, V3 xi, V3 ng) {
+    const double p_area = 1.0 / L.area;
+    return p_area * distance_squared(ri.origin, xi) / fabs(dot(ng, ri.dir));
+}
+
+// ------------------------------------------------------------------ integrator
+// integrator.rs:139-184
+Color mis_sample(const Scene& sc, V3 wo, V3 wi, const Hit& ho, const Hit& hi, const Lambda& L, bool li, double p_lig,
+                 double p_sct) {
+    if (p_lig == 0.0 || p_sct == 0.0) return cconst(0.0);
+    const Color bsdf = bsdf_f(sc, ho, wo, wi, L);
+    const double denom = p_lig * p_lig + p_sct * p_sct;
+    const double weight = li ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
+    const double p_denom = li ? p_lig : p_sct;
+    return bsdf * cconst(1.0) * emit(sc, hi.material, L, hi) * shading_cosine(sc, ho.material, wi, ho.ns) * weight /
+           p_denom;
+}
+
+// integrator.rs:87-137
+Color single_shadow_ray(const Scene& sc, V3 wo, const Lambda& L, const Hit& ho, Xorshift& rng, Counters& C) {
+    const V3 xo = ho.p;
+    const int li = sample_light(sc, xs_float(rng));
+    const lumo_object& light = sc.d->lights[li];
+    const double pdf_light = sc.d->alias_pdf[li];
+    Color radiance = cconst(0.0);
+    {
+        const V2 rs = xs_vec2(rng);
+        const V3 wi = light_sample_towards(light, xo, rs);
+        const Ray ri = generate_ray(ho, wi);
+        Hit hi;
+        Color add = cconst(0.0);
+        if (scene_hit_light(sc, ri, li, &hi, C)) {
+            const double p_lig = light_sample_towards_pdf(light, ri, hi.p, hi.ng);
+            const double p_sct = bsdf_pdf(sc, ho, wo, wi);
+            add = mis_sample(sc, wo, wi, ho, hi, L, true, p_lig, p_sct);
+        }
+        radiance = radiance + add;
+    }
+    {
+        const double rand_u = xs_float(rng);
+        const V2 rand_sq = xs_vec2(rng);
+        V3 wi;
+        Color add = cconst(0.0);
+        if (bsdf_sample(sc, ho, wo, rand_u, rand_sq, &wi)) {
+            const Ray ri = generate_ray(ho, wi);
+            Hit hi;
+            if (scene_hit_light(sc, ri, li, &hi, C)) {
+                const double p_lig = light_sample_towards_pdf(light, ri, hi.p, hi.ng);
+                const double p_sct = bsdf_pdf(sc, ho, wo, wi);
+                add = mis_sample(sc, wo, wi, ho, hi, L, false, p_lig, p_sct);
+            }
+        }
+        radiance = radiance + add;
+    }
+    return radiance / pdf_light;
+}
+
+struct Sample {
+    Color color;
+    Lambda lambda;
+    V2 raster;
+    uint64_t cost;
+};
+
+struct DbgLog {
+    bool on = false;
+    int n = 0;
+    double rec[64][20];
+};
+thread_local DbgLog* g_dbg = nullptr;
+
+// path_trace.rs:5-82
+Sample path_trace(const Scene& sc, Ray ro, Xorshift& rng, Lambda L, double delta, V2 raster, Counters& C) {
+    bool last_specular = true;
+    Color radiance = cconst(0.0), gathered = cconst(1.0);
+    uint64_t depth = 0;
+    for (;;) {
+        Hit ho;
+        int kind, which;
+        if (!scene_hit(sc, ro, &ho, &kind, &which, C)) break;
+        if (g_dbg && g_dbg->n < 64) {
+            double* d = g_dbg->rec[g_dbg->n++];
+            d[0] = (double)depth; d[1] = kind; d[2] = which; d[3] = -1; d[4] = ho.t;
+            d[5] = ro.origin.x; d[6] = ro.origin.y; d[7] = ro.origin.z; d[8] = ro.dir.x; d[9] = ro.dir.y; d[10] = ro.dir.z;
+            d[11] = ho.p.x; d[12] = ho.p.y; d[13] = ho.p.z; d[14] = ho.ng.x; d[15] = ho.ng.y; d[16] = ho.ng.z;
+            d[17] = (double)(rng.hi >> 11); d[18] = ho.backface; d[19] = gathered.s[0];
+        }
+        gathered = gathered * cconst(1.0);  // scene.transmittance (no medium)
+        const V3 wo = -ro.dir;
+        const double u = xs_float(rng);
+        const V2 sq = xs_vec2(rng);
+        V3 wi;
+        if (!bsdf_sample(sc, ho, wo, u, sq, &wi)) {
+            if (last_specular) radiance = radiance + gathered * emit(sc, ho.material, L, ho);
+            break;
+        }
+        if (!is_delta(sc, ho.material)) {
+            const int n = sc.num_shadow_rays();
+            Color acc = cconst(0.0);
+            for (int i = 0; i < n; ++i) acc = acc + gathered * single_shadow_ray(sc, -ro.dir, L, ho, rng, C);
+            radiance = radiance + acc / (double)n;
+        }
+        const Ray ri = generate_ray(ho, wi);
+        const V3 wi2 = ri.dir;
+        const double p_scatter = bsdf_pdf(sc, ho, wo, wi2);
+        if (p_scatter <= 0.0) break;
+        const Color bsdf = bsdf_f(sc, ho, wo, wi2, L);
+        gathered = gathered * (bsdf * shading_cosine(sc, ho.material, wi2, ho.ns) / p_scatter);
+        if ((int)depth >= RR_DEPTH) {
+            const double lum = luminance(sc, gathered, L);
+            const double rr_prob = rmin(lum / delta, 1.0);
+            if (xs_float(rng) > rr_prob) break;
+            gathered = gathered / rr_prob;
+        }
+        last_specular = is_specular(sc, ho.material);
+        depth += 1;
+        ro = ri;
+    }
+    return Sample{radiance, L, raster, depth};
+}
+
+// ------------------------------------------------------------------ camera (camera.rs)
+struct Cam {
+    Xform wtc, sctr, cts;
+    double lens_radius, focal_length;
+    M3 wb, x2r;
+    double fr, fsig;
+};
+Cam cam_of(const lumo_camera_desc* c) {
+    Cam k;
+    auto get = [](const double (&a)[2][16]) {
+        Xform x;
+        M4* ms[2] = {&x.m, &x.inv};
+        for (int q = 0; q < 2; ++q) {
+            V4* rows[4] = {&ms[q]->y0, &ms[q]->y1, &ms[q]->y2, &ms[q]->y3};
+            for (int r = 0; r < 4; ++r) *rows[r] = V4{a[q][4 * r], a[q][4 * r + 1], a[q][4 * r + 2], a[q][4 * r + 3]};
+        }
+        return x;
+    };
+    k.wtc = get(c->world_to_camera);
+    k.sctr = get(c->screen_to_raster);
+    k.cts = get(c->camera_to_screen);
+    k.lens_radius = c->lens_radius;
+    k.focal_length = c->focal_length;
+    auto m3 = [](const double* a) { return M3{V3{a[0], a[1], a[2]}, V3{a[3], a[4], a[5]}, V3{a[6], a[7], a[8]}}; };
+    k.wb = m3(c->white_balance);
+    k.x2r = m3(c->xyz_to_rgb);
+    k.fr = c->filter_radius;
+    k.fsig = c->filter_sigma;
+    return k;
+}
+// camera.rs:257-268 (Perspective) + add_dof :221-243
+Ray camera_ray(const Cam& k, V2 raster_xy, V2 rand_sq) {
+    const V3 screen = xf_pt_inv(k.sctr, V3{raster_xy.x, raster_xy.y, 0.0});
+    const V3 wi_local0 = normalize(xf_pt_inv(k.cts, screen));
+    V3 xo_local = V3{0, 0, 0}, wi_local = wi_local0;
+    if (k.lens_radius != 0.0) {
+        const V2 lxy = k.lens_radius * square_to_disk(rand_sq);
+        const V3 lens = V3{lxy.x, lxy.y, 0.0};
+        const double focus_distance = k.focal_length / wi_local0.z;
+        const V3 focus = focus_distance * wi_local0;
+        xo_local = xo_local + lens;
+        wi_local = focus - lens;
+    }
+    return ray_new(xf_pt_inv(k.wtc, xo_local), xf_dir_inv(k.wtc, wi_local));
+}
+
+// integrator.rs:45-70 (PathTrace)
+Sample integrate(const Scene& sc, const Cam& k, Xorshift& rng, double delta, V2 raster, Counters& C) {
+    const V2 lens = xs_vec2(rng);
+    const Ray r = camera_ray(k, raster, lens);
+    const Lambda L = wl_sample(xs_float(rng));
+    return path_trace(sc, r, rng, L, delta, raster, C);
+}
+
+// ------------------------------------------------------------------ sampler (samplers.rs:136-193)
+std::vector<size_t> gen_perm(Xorshift& rng, size_t n) {  // rng.rs:104-116
+    std::vector<size_t> p(n);
+    for (size_t i = 0; i < n; ++i) p[i] = i;
+    for (size_t i = 0; i + 1 < n; ++i) {
+        const uint64_t rnd = xs_u64(rng);
+        const size_t j = i + (size_t)(rnd % (uint64_t)(n - i));
+        std::swap(p[i], p[j]);
+    }
+    return p;
+}
+struct MJ {
+    uint64_t state, batch_end, dim;
+    std::vector<size_t> px, py;
+    V2 scale0, scale1;
+    Xorshift rng;
+};
+MJ mj_new(uint64_t batch, uint64_t samples, uint64_t seed) {  // SamplerType::new (samplers.rs:26-37)
+    const uint64_t s0 = batch * SAMPLES_INCREMENT;
+    uint64_t s1 = (batch + 1) * SAMPLES_INCREMENT;
+    s1 = std::min(s1, samples);
+    MJ m;
+    m.rng = xs_new(seed);
+    m.dim = (uint64_t)std::ceil(std::sqrt((double)samples));
+    const V2 scale = V2{1.0 / (double)m.dim, (double)m.dim / (double)samples};
+    m.px = gen_perm(m.rng, m.dim);
+    m.py = gen_perm(m.rng, m.dim);
+    m.state = s0;
+    m.batch_end = s1;
+    m.scale0 = scale;
+    m.scale1 = scale / (double)m.dim;
+    return m;
+}
+bool mj_next(MJ& m, V2* out) {
+    if (m.state == m.batch_end) return false;
+    const uint64_t x0 = m.state % m.dim, y0 = m.state / m.dim;
+    const V2 offset0 = m.scale0 * V2{(double)x0, (double)y0};
+    const V2 offset1 = m.scale1 * V2{(double)m.px[y0], (double)m.py[x0]};
+    const V2 rand_sq = m.scale1 * xs_vec2(m.rng);
+    m.state += 1;
+    *out = offset0 + offset1 + rand_sq;
+    return true;
+}
+
+// ------------------------------------------------------------------ film (film/tile.rs, filter.rs)
+double gauss(double x, double sigma) {
+    return O_EXP(-(x * x) / (2.0 * sigma * sigma)) / std::sqrt(rmax(2.0 * PI * sigma * sigma, 0.0));
+}
+struct Tile {
+    uint64_t x0, y0, x1, y1;
+    std::vector<double> px;  // 4 per pixel: w*r, w*g, w*b, w
+};
+void tile_add_sample(const Scene& sc, const Cam& k, Tile& T, const Sample& s) {
+    const V3 xyz = color_xyz(sc, s.color, s.lambda);
+    const V3 rgb = m3_mul_vec(k.x2r, m3_mul_vec(k.wb, xyz));
+    auto to_u64 = [](double v) -> uint64_t { return v > 0.0 ? (uint64_t)v : 0; };
+    const uint64_t pxx = to_u64(std::floor(s.raster.x)), pxy = to_u64(std::floor(s.raster.y));
+    const uint64_t r = (uint64_t)std::ceil(k.fr - 0.5);
+    const uint64_t mix = std::max(pxx >= r ? pxx - r : 0, T.x0), miy = std::max(pxy >= r ? pxy - r : 0, T.y0);
+    const uint64_t mxx = std::min(pxx + r, T.x1 - 1), mxy = std::min(pxy + r, T.y1 - 1);
+    const uint64_t w = T.x1 - T.x0;
+    for (uint64_t fy = miy; fy <= mxy; ++fy) {
+        for (uint64_t fx = mix; fx <= mxx; ++fx) {
+            const V2 v = V2{s.raster.x - (0.5 + (double)fx), s.raster.y - (0.5 + (double)fy)};
+            const double gx = gauss(v.x, k.fsig), gy = gauss(v.y, k.fsig), gr = gauss(k.fr, k.fsig);
+            const double wt = rmax(gx - gr, 0.0) * rmax(gy - gr, 0.0);
+            if (wt != 0.0) {
+                double* p = &T.px[4 * ((fy - T.y0) * w + (fx - T.x0))];
+                const V3 c = rgb * wt;
+                p[0] += c.x;
+                p[1] += c.y;
+                p[2] += c.z;
+                p[3] += wt;
+            }
+        }
+    }
+}
+
+double ring_delta(const uint64_t* ns, const double* fs, uint64_t n) {  // task.rs:42-53
+    double f = 0.0, f2 = 0.0;
+    for (uint64_t i = 0; i < n; ++i) f = f + fs[i];
+    for (uint64_t i = 0; i < n; ++i) f2 = f2 + fs[i] * fs[i];
+    const double var = f2 - f * f / (double)n;
+    if (var <= 0.0) return 1e-5;
+    uint64_t cost = 0;
+    for (uint64_t i = 0; i < n; ++i) cost += ns[i];
+    return std::sqrt(var / (double)cost);
+}
+
+// task.rs:24-82, exactly lumo's order
+void exec_lumo_order(const Scene& sc, const Cam& k, const lumo_tile_task& t, lumo_tile_result& res, Counters& C) {
+    Tile T{t.px_min[0], t.px_min[1], t.px_max[0], t.px_max[1], {}};
+    T.px.assign(4 * (T.x1 - T.x0) * (T.y1 - T.y0), 0.0);
+    Xorshift rng = xs_new(t.seed);
+    uint64_t ns[SAMPLES_INCREMENT] = {0};
+    double fs[SAMPLES_INCREMENT] = {0};
+    uint64_t ptr = 0, num_rays = 0;
+    for (uint64_t y = T.y0; y < T.y1; ++y) {
+        for (uint64_t x = T.x0; x < T.x1; ++x) {
+            const V2 xy{(double)x, (double)y};
+            MJ m = mj_new(t.batch, t.total_samples, xs_u64(rng));
+            V2 rs;
+            while (mj_next(m, &rs)) {
+                const V2 raster = xy + rs;
+                const double delta = ring_delta(ns, fs, t.samples);
+                Sample s = integrate(sc, k, rng, delta, raster, C);
+                num_rays += s.cost;
+                ns[ptr] = s.cost;
+                fs[ptr] = luminance(sc, s.color, s.lambda);
+                ptr = (ptr + 1) % t.samples;
+                tile_add_sample(sc, k, T, s);  // ToneMap::NoMap
+            }
+        }
+    }
+    std::memcpy(res.rgb_w, T.px.data(), T.px.size() * sizeof(double));
+    res.num_camera_rays = (T.x1 - T.x0) * (T.y1 - T.y0) * t.samples;
+    res.num_rays = num_rays;
+}
+
+}  // namespace
+
+namespace lumo_oracle_wavefront {
+// per-pixel sampler seeds are the tile stream's first P outputs; each path
+// (pixel j, sample k of the batch) owns Xorshift::new(path_seed(pixel_seed_j, k)); passes
+// are sample-major and the adaptive-RR ring is updated at the end of each pass.
+uint64_t path_seed(uint64_t pixel_seed, uint64_t k) { return splitmix64(pixel_seed ^ splitmix64(k + 1)); }
+}  // namespace lumo_oracle_wavefront
+
+namespace {
+struct WaveOut {
+    std::vector<Sample>* paths;
+    std::vector<double>* deltas;
+    int dbg_pass = -1, dbg_pixel = -1;
+    DbgLog* log = nullptr;
+};
+void exec_wavefront(const Scene& sc, const Cam& k, const lumo_tile_task& t, lumo_tile_result* res, Counters& C,
+                    WaveOut* dbg) {
+    Tile T{t.px_min[0], t.px_min[1], t.px_max[0], t.px_max[1], {}};
+    T.px.assign(4 * (T.x1 - T.x0) * (T.y1 - T.y0), 0.0);
+    const uint64_t W = T.x1 - T.x0, H = T.y1 - T.y0, P = W * H;
+    Xorshift trng = xs_new(t.seed);
+    std::vector<uint64_t> pseed(P);
+    std::vector<MJ> mj;
+    mj.reserve(P);
+    for (uint64_t j = 0; j < P; ++j) {
+        pseed[j] = xs_u64(trng);
+        mj.push_back(mj_new(t.batch, t.total_samples, pseed[j]));
+    }
+    uint64_t ns[SAMPLES_INCREMENT] = {0};
+    double fs[SAMPLES_INCREMENT] = {0};
+    uint64_t ptr = 0, num_rays = 0;
+    std::vector<Sample> pass(P);
+    for (uint64_t s = 0; s < t.samples; ++s) {
+        const double delta = ring_delta(ns, fs, t.samples);
+        if (dbg) dbg->deltas->push_back(delta);
+        for (uint64_t j = 0; j < P; ++j) {
+            V2 rs;
+            mj_next(mj[j], &rs);
+            const V2 raster = V2{(double)(T.x0 + j % W), (double)(T.y0 + j / W)} + rs;
+            Xorshift prng = xs_new(lumo_oracle_wavefront::path_seed(pseed[j], s));
+            if (dbg && dbg->log && (int)s == dbg->dbg_pass && (int)j == dbg->dbg_pixel) g_dbg = dbg->log;
+            pass[j] = integrate(sc, k, prng, delta, raster, C);
+            g_dbg = nullptr;
+            tile_add_sample(sc, k, T, pass[j]);
+            if (dbg) dbg->paths->push_back(pass[j]);
+        }
+        for (uint64_t j = 0; j < P; ++j) {
+            num_rays += pass[j].cost;
+            ns[ptr] = pass[j].cost;
+            fs[ptr] = luminance(sc, pass[j].color, pass[j].lambda);
+            ptr = (ptr + 1) % t.samples;
+        }
+    }
+    if (res) {
+        std::memcpy(res->rgb_w, T.px.data(), T.px.size() * sizeof(double));
+        res->num_camera_rays = P * t.samples;
+        res->num_rays = num_rays;
+    }
+}
+
+bool valid_task(const lumo_tile_task& t) {
+    return t.px_max[0] > t.px_min[0] && t.px_max[1] > t.px_min[1] && t.samples >= 1 &&
+           t.samples <= SAMPLES_INCREMENT && t.total_samples >= 1;
+}
+}  // namespace
+
+extern "C" int oracle_render_tiles(const lumo_scene_desc* scene, const lumo_camera_desc* camera,
+                                   const lumo_tile_task* tasks, size_t n, int mode, int threads,
+                                   lumo_tile_result* out, oracle_counters* counters) {
+    if (!scene || !camera || (!tasks && n) || (!out && n)) return LUMO_ERR_INVALID;
+    for (size_t i = 0; i < n; ++i)
+        if (!valid_task(tasks[i]) || !out[i].rgb_w) return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    const Cam k = cam_of(camera);
+    if (threads < 1) threads = 1;
+    std::atomic<size_t> next{0};
+    std::vector<Counters> cs(threads);
+    std::vector<std::thread> pool;
+    for (int w = 0; w < threads; ++w) {
+        pool.emplace_back([&, w]() {
+            for (;;) {
+                const size_t i = next++;
+                if (i >= n) return;
+                out[i].num_queries = 0;
+                const uint64_t q0 = cs[w].closest + cs[w].shadow;
+                if (mode == ORACLE_LUMO_ORDER)
+                    exec_lumo_order(sc, k, tasks[i], out[i], cs[w]);
+                else
+                    exec_wavefront(sc, k, tasks[i], &out[i], cs[w], nullptr);
+                out[i].num_queries = cs[w].closest + cs[w].shadow - q0;
+            }
+        });
+    }
+    for (auto& th : pool) th.join();
+    if (counters) {
+        std::memset(counters, 0, sizeof(*counters));
+        for (const Counters& c : cs) {
+            counters->aabb_tests += c.aabb;
+            counters->kd_nodes += c.kd;
+            counters->tri_tests += c.tri;
+            counters->closest_queries += c.closest;
+            counters->shadow_queries += c.shadow;
+        }
+    }
+    return LUMO_OK;
+}
+
+extern "C" int oracle_trace_paths(const lumo_scene_desc* scene, const lumo_camera_desc* camera,
+                                  const lumo_tile_task* task, double* radiance4, double* lambda4, double* raster2,
+                                  uint64_t* depth, double* delta_per_pass) {
+    if (!scene || !camera || !task || !valid_task(*task)) return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    const Cam k = cam_of(camera);
+    Counters C;
+    std::vector<Sample> paths;
+    std::vector<double> deltas;
+    WaveOut dbg{&paths, &deltas};
+    exec_wavefront(sc, k, *task, nullptr, C, &dbg);
+    for (size_t i = 0; i < paths.size(); ++i) {
+        for (int c = 0; c < NS; ++c) {
+            if (radiance4) radiance4[4 * i + c] = paths[i].color.s[c];
+            if (lambda4) lambda4[4 * i + c] = paths[i].lambda.l[c];
+        }
+        if (raster2) {
+            raster2[2 * i] = paths[i].raster.x;
+            raster2[2 * i + 1] = paths[i].raster.y;
+        }
+        if (depth) depth[i] = paths[i].cost;
+    }
+    if (delta_per_pass)
+        for (size_t i = 0; i < deltas.size(); ++i) delta_per_pass[i] = deltas[i];
+    return LUMO_OK;
+}
+
+extern "C" int oracle_trace(const lumo_scene_desc* scene, const lumo_ray_soa* rays, size_t n, lumo_hit_soa* hits,
+                            int any_hit, oracle_counters* counters) {
+    if (!scene || !rays || !hits) return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    Counters C;
+    for (size_t i = 0; i < n; ++i) {
+        const Ray r{V3{rays->origin[3 * i], rays->origin[3 * i + 1], rays->origin[3 * i + 2]},
+                    V3{rays->dir[3 * i], rays->dir[3 * i + 1], rays->dir[3 * i + 2]}};
+        Hit h;
+        if (!any_hit) {
+            int kind = 0, which = -1;
+            const bool f = scene_hit(sc, r, &h, &kind, &which, C);
+            hits->t[i] = f ? h.t : INF;
+            hits->kind[i] = f ? kind : 0;
+            hits->object[i] = f ? which : -1;
+            hits->prim[i] = -1;
+        } else {
+            const int light = rays->light[i];
+            const bool f = scene_hit_light(sc, r, light, &h, C);
+            hits->t[i] = f ? h.t : INF;
+            hits->kind[i] = f ? 2 : 0;
+            hits->object[i] = f ? light : -1;
+            hits->prim[i] = -1;
+        }
+    }
+    if (counters) {
+        counters->aabb_tests = C.aabb;
+        counters->kd_nodes = C.kd;
+        counters->tri_tests = C.tri;
+        counters->closest_queries = C.closest;
+        counters->shadow_queries = C.shadow;
+    }
+    return LUMO_OK;
+}
+
+extern "C" int oracle_debug_trace(const lumo_scene_desc* scene, const lumo_camera_desc* camera,
+                                  const lumo_tile_task* task, int pass, int pixel, double* out, int* n_out) {
+    if (!scene || !camera || !task || !valid_task(*task)) return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    const Cam k = cam_of(camera);
+    Counters C;
+    std::vector<Sample> paths;
+    std::vector<double> deltas;
+    DbgLog log;
+    WaveOut dbg{&paths, &deltas, pass, pixel, &log};
+    exec_wavefront(sc, k, *task, nullptr, C, &dbg);
+    *n_out = log.n;
+    std::memcpy(out, log.rec, sizeof(double) * 20 * log.n);
+    return LUMO_OK;
+}

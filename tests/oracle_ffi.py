@@ -1,0 +1,92 @@
+"""ctypes loader for the CPU oracle (test infrastructure only; see oracle/oracle.h)."""
+import ctypes as C
+import os
+
+import numpy as np
+
+from lumo_amd import _ffi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_PATH = os.path.join(ROOT, "oracle", "_build", "liblumo_oracle.so")
+
+WAVEFRONT, LUMO_ORDER = 0, 1
+
+
+class Counters(C.Structure):
+    _fields_ = [("aabb_tests", C.c_uint64), ("kd_nodes", C.c_uint64), ("tri_tests", C.c_uint64),
+                ("closest_queries", C.c_uint64), ("shadow_queries", C.c_uint64)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        lib = C.CDLL(ORACLE_PATH)
+        lib.oracle_render_tiles.restype = C.c_int
+        lib.oracle_render_tiles.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(_ffi.CameraDesc),
+                                            C.POINTER(_ffi.TileTask), C.c_size_t, C.c_int, C.c_int,
+                                            C.POINTER(_ffi.TileResult), C.POINTER(Counters)]
+        lib.oracle_trace_paths.restype = C.c_int
+        lib.oracle_trace_paths.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(_ffi.CameraDesc),
+                                           C.POINTER(_ffi.TileTask), _ffi.c_double_p, _ffi.c_double_p,
+                                           _ffi.c_double_p, _ffi.c_uint64_p, _ffi.c_double_p]
+        lib.oracle_trace.restype = C.c_int
+        lib.oracle_trace.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(_ffi.RaySoA), C.c_size_t,
+                                     C.POINTER(_ffi.HitSoA), C.c_int, C.POINTER(Counters)]
+        _lib = lib
+    return _lib
+
+
+def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1):
+    """Returns (list of rgb_w arrays, results array, counters)."""
+    lib = load()
+    n = len(tasks)
+    arr = tasks if isinstance(tasks, C.Array) else (_ffi.TileTask * n)(*tasks)
+    res = (_ffi.TileResult * n)()
+    bufs = []
+    for i, t in enumerate(arr):
+        P = (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1])
+        b = np.zeros(4 * P)
+        bufs.append(b)
+        res[i].rgb_w = b.ctypes.data_as(_ffi.c_double_p)
+    cnt = Counters()
+    st = lib.oracle_render_tiles(C.byref(scene_desc), C.byref(camera_desc), arr, n, mode, threads, res,
+                                 C.byref(cnt))
+    assert st == 0, st
+    return bufs, res, cnt
+
+
+def trace_paths(scene_desc, camera_desc, task):
+    lib = load()
+    P = (task.px_max[0] - task.px_min[0]) * (task.px_max[1] - task.px_min[1])
+    m = P * task.samples
+    rad, lam, ras = np.zeros(4 * m), np.zeros(4 * m), np.zeros(2 * m)
+    depth, delta = np.zeros(m, dtype=np.uint64), np.zeros(task.samples)
+    st = lib.oracle_trace_paths(C.byref(scene_desc), C.byref(camera_desc), C.byref(task),
+                                rad.ctypes.data_as(_ffi.c_double_p), lam.ctypes.data_as(_ffi.c_double_p),
+                                ras.ctypes.data_as(_ffi.c_double_p), depth.ctypes.data_as(_ffi.c_uint64_p),
+                                delta.ctypes.data_as(_ffi.c_double_p))
+    assert st == 0, st
+    return dict(radiance=rad.reshape(-1, 4), lam=lam.reshape(-1, 4), raster=ras.reshape(-1, 2), depth=depth,
+                delta=delta)
+
+
+def trace(scene_desc, origins, dirs, lights=None):
+    lib = load()
+    n = len(origins)
+    o = np.ascontiguousarray(origins, dtype=np.float64)
+    d = np.ascontiguousarray(dirs, dtype=np.float64)
+    li = np.ascontiguousarray(lights if lights is not None else np.zeros(n), dtype=np.int32)
+    rays = _ffi.RaySoA(o.ctypes.data_as(_ffi.c_double_p), d.ctypes.data_as(_ffi.c_double_p), None,
+                       li.ctypes.data_as(_ffi.c_int32_p))
+    t = np.zeros(n)
+    kind, obj, prim = (np.zeros(n, dtype=np.int32) for _ in range(3))
+    hits = _ffi.HitSoA(t.ctypes.data_as(_ffi.c_double_p), kind.ctypes.data_as(_ffi.c_int32_p),
+                       obj.ctypes.data_as(_ffi.c_int32_p), prim.ctypes.data_as(_ffi.c_int32_p))
+    cnt = Counters()
+    st = lib.oracle_trace(C.byref(scene_desc), C.byref(rays), n, C.byref(hits), int(lights is not None),
+                          C.byref(cnt))
+    assert st == 0
+    return t, kind, obj, cnt

@@ -1,0 +1,20 @@
+"""Helpers shared by the GPU parity tests and smoke()."""
+import ctypes as C
+
+import numpy as np
+
+from lumo_amd import _ffi
+
+
+def gpu_paths(dev, task):
+    """lumo_debug_paths: per-path radiance / wavelengths / raster / depth of one task."""
+    P = (task.px_max[0] - task.px_min[0]) * (task.px_max[1] - task.px_min[1])
+    m = P * task.samples
+    rad, lam, ras = np.zeros(4 * m), np.zeros(4 * m), np.zeros(2 * m)
+    depth, delta = np.zeros(m, dtype=np.uint64), np.zeros(task.samples)
+    dump = _ffi.PathDump(rad.ctypes.data_as(_ffi.c_double_p), lam.ctypes.data_as(_ffi.c_double_p),
+                         ras.ctypes.data_as(_ffi.c_double_p), depth.ctypes.data_as(_ffi.c_uint64_p),
+                         delta.ctypes.data_as(_ffi.c_double_p))
+    _ffi.check(_ffi.load().lumo_debug_paths(dev.ctx, C.byref(task), C.byref(dump)), "debug_paths")
+    return dict(radiance=rad.reshape(-1, 4), lam=lam.reshape(-1, 4), raster=ras.reshape(-1, 2), depth=depth,
+                delta=delta)
