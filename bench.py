@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: lumo's Cornell box, PathTrace, 1024x1024 @ 1024 spp (BASELINE.json configs[1]).
+
+One "step" = the full C1 render: every (256-spp batch, 16x16 tile) RenderTask of the frame
+(renderer.rs:179-204), 4 batches x 4096 tiles = 1.07e9 camera paths.  With N ranks (one per GPU,
+launched by torch.distributed.run) the tasks are sharded by tile index (tile % N == rank), the
+scene is replicated, and no collective touches the data path; only the timing barrier and the
+final max/sum reductions use the process group.
+
+Prints ONE JSON line (rank 0).  `value` is whole-job Mrays/s = (closest-hit + shadow-visibility
+queries of all ranks) / max-over-ranks wall time of the K timed steps.  Also reported:
+Msamples/s (camera paths), lumo's own "total rays" rate (sum of path depths, task.rs:65), the
+roofline of the dominant kernel (algorithmic bytes from the kernels' own traversal counters over
+live HIP-event kernel time), and the CPU baseline (the f64 oracle in lumo's tile-serial order on
+this host's cores, on a bounded sample of the same frame).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 0x5EED_1234
+# Algorithmic bytes per unit: f64 data touched by the algorithm.
+B_AABB, B_KD, B_TRI = 48, 16, 84           # slab test bounds; kd split node; 3 vertices + indices
+B_CLOSEST_IO, B_SHADOW_IO = 48 + 20, 104 + 32  # ray in + hit out; shadow record in + contribution out
+STAGES = ["camera", "closest", "shade", "shadow", "resolve", "finish", "film", "ring"]
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return ws, rank, local
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--max-paths", type=int, default=1 << 21, help="paths in flight per wavefront")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
+    ap.add_argument("--cpu-tile-stride", type=int, default=256, help="CPU sample: every k-th tile of each batch")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    import lumo_amd as L
+    from lumo_amd import _ffi
+
+    pg = None
+    if ws > 1:
+        import torch
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+        pg = dist
+
+    scene = L.Scene.cornell_box()
+    cam = L.Camera.cornell_box((args.res, args.res))
+    tasks = L.make_tasks(args.res, args.res, args.spp, SEED)
+    tiles = ((args.res + 15) // 16) ** 2
+    mine = [t for i, t in enumerate(tasks) if (i % tiles) % ws == rank]
+    mine_arr = (_ffi.TileTask * len(mine))(*mine)
+
+    dev = L.Device(local)
+    dev.upload(scene, cam)
+    lib = _ffi.load()
+
+    def step():
+        bufs, res = dev.render_tasks(mine_arr, max_paths=args.max_paths)
+        return sum(r.num_queries for r in res), sum(r.num_camera_rays for r in res), sum(r.num_rays for r in res)
+
+    def barrier():
+        if pg is not None:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            pg.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    lib.lumo_set_timing(1)
+    lib.lumo_stats_reset(dev.ctx)
+    barrier()
+    t0 = time.perf_counter()
+    q = cams = rays = 0
+    for _ in range(args.steps):
+        a, b, c = step()
+        q, cams, rays = q + a, cams + b, rays + c
+    barrier()  # lumo_render_tiles returns only after its stream has drained
+    elapsed = time.perf_counter() - t0
+    lib.lumo_set_timing(0)
+    st = dev.stats()
+
+    if pg is not None:
+        import torch
+        dev_t = "cuda" if torch.cuda.is_available() else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+        elapsed = float(t.item())
+        s = torch.tensor([q, cams, rays], dtype=torch.float64, device=dev_t)
+        pg.all_reduce(s, op=pg.ReduceOp.SUM)
+        q, cams, rays = (float(x) for x in s.tolist())
+
+    if rank == 0:
+        roof = roofline(st)
+        cpu = cpu_baseline(scene, cam, tasks, tiles, args) if (args.cpu_baseline and ws == 1) else None
+        value = q / elapsed / 1e6
+        out = {
+            "metric": "Mrays/s",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (Scene::cornell_box defined in code; no assets needed)",
+            "config": {
+                "workload": f"cornell_{args.res}x{args.res}_{args.spp}spp_pathtrace",
+                "scene": "Scene::cornell_box (32 triangles, 1 rectangle light)",
+                "camera": "Camera::cornell_box",
+                "resolution": [args.res, args.res],
+                "spp": args.spp,
+                "integrator": "PathTrace (NEE + MIS + RR)",
+                "seed": SEED,
+                "rng_mode": "wavefront (per-path Xorshiftr128+ streams; DESIGN.md §RNG)",
+                "parallelism": f"tiles sharded tile%{ws}",
+            },
+            "msamples_per_s": round(cams / elapsed / 1e6, 3),
+            "lumo_total_rays_per_s_M": round(rays / elapsed / 1e6, 3),
+            "queries_per_step": q / args.steps,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    dev.close()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+def roofline(st):
+    """Dominant-kernel roofline from live per-launch HIP-event times and traversal counters."""
+    ms = list(st.kernel_ms)
+    launches = list(st.launches)
+    per_stage = {STAGES[i]: {"ms": round(ms[i], 3), "launches": int(launches[i])} for i in range(8)}
+    dom = max(range(8), key=lambda i: ms[i])
+    name = STAGES[dom]
+    if name == "closest":
+        nbytes = (st.closest_queries * B_CLOSEST_IO + st.aabb_tests[0] * B_AABB + st.kd_nodes[0] * B_KD +
+                  st.tri_tests[0] * B_TRI)
+    elif name == "shadow":
+        nbytes = (st.shadow_queries * B_SHADOW_IO + st.aabb_tests[1] * B_AABB + st.kd_nodes[1] * B_KD +
+                  st.tri_tests[1] * B_TRI)
+    else:
+        nbytes = None
+    out = {"bound": "hbm", "kernel": f"k_{name}", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": pmc_traffic(name),
+           "stages": per_stage}
+    if nbytes is not None and ms[dom] > 0 and launches[dom] > 0:
+        achieved = nbytes / (ms[dom] * 1e-3) / 1e9
+        out.update({"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 5),
+                    "bytes_per_launch": nbytes / launches[dom],
+                    "avg_launch_us": ms[dom] * 1e3 / launches[dom]})
+    else:
+        out.update({"achieved": None, "frac": None})
+    return out
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(f"k_{kernel}", {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(scene, cam, tasks, tiles, args):
+    """The oracle (f64 restatement of lumo's CPU path, lumo's own tile-serial RNG order) on this
+    host: every k-th tile of every batch of the same frame, all spp; Mrays/s of that sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    try:
+        import oracle_ffi as O
+        O.load()
+    except OSError:
+        return None
+    sample = [t for i, t in enumerate(tasks) if (i % tiles) % args.cpu_tile_stride == 0]
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    bufs, res, cnt = O.render_tasks(scene.desc(), cam.desc, sample, O.LUMO_ORDER, threads)
+    dt = time.perf_counter() - t0
+    q = sum(r.num_queries for r in res)
+    paths = sum(r.num_camera_rays for r in res)
+    return {"value": round(q / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "msamples_per_s": round(paths / dt / 1e6, 4), "seconds": round(dt, 2),
+            "sample": f"{len(sample)} tasks = every {args.cpu_tile_stride}th 16x16 tile of each 256-spp batch of "
+                      f"the {args.res}^2 @ {args.spp} spp frame ({paths} paths), lumo tile-serial RNG order"}
+
+
+if __name__ == "__main__":
+    main()

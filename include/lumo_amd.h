@@ -251,6 +251,8 @@ lumo_status lumo_trace(void* ctx, const lumo_ray_soa* rays, size_t n, lumo_hit_s
 
 lumo_status lumo_stats_get(void* ctx, lumo_stats* stats);
 lumo_status lumo_stats_reset(void* ctx);
+/* Enable per-launch HIP-event timing of every stage (also LUMO_TIMING=1). */
+void lumo_set_timing(int on);
 
 /* Test hook: render one task in the wavefront order and dump every path. */
 lumo_status lumo_debug_paths(void* ctx, const lumo_tile_task* task, lumo_path_dump* dump);

@@ -138,6 +138,7 @@ DEVICE_API = [
     ("lumo_trace", C.c_int32, [C.c_void_p, C.POINTER(RaySoA), C.c_size_t, C.POINTER(HitSoA), C.c_int]),
     ("lumo_stats_get", C.c_int32, [C.c_void_p, C.POINTER(Stats)]),
     ("lumo_stats_reset", C.c_int32, [C.c_void_p]),
+    ("lumo_set_timing", None, [C.c_int]),
     ("lumo_debug_trace", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.c_int, C.c_int, c_double_p, C.POINTER(C.c_int)]),
     ("lumo_debug_paths", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.POINTER(PathDump)]),
 ]

@@ -647,24 +647,59 @@ T* wbuf(Ctx& c, int id, size_t count, lumo_status& st) {
     return static_cast<T*>(c.work[id].p);
 }
 
+// Per-launch HIP event pairs, resolved at the synchronisation points the host loop already
+// has (queue-count readbacks), so timing adds no extra stalls.
+struct Timing {
+    std::vector<hipEvent_t> free_ev;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    hipEvent_t get() {
+        if (free_ev.empty()) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            return e;
+        }
+        hipEvent_t e = free_ev.back();
+        free_ev.pop_back();
+        return e;
+    }
+};
+Timing& timing() {
+    static Timing t;
+    return t;
+}
+
 struct StageTimer {
     Ctx& c;
     bool on;
     int stage;
+    hipEvent_t a{}, b{};
     StageTimer(Ctx& cc, bool enable, int st) : c(cc), on(enable), stage(st) {
-        if (on) hipEventRecord(c.ev[2 * stage], c.stream);
+        if (on) {
+            a = timing().get();
+            b = timing().get();
+            (void)hipEventRecord(a, c.stream);
+        }
+        c.stats.launches[stage] += 1;
     }
     ~StageTimer() {
         if (on) {
-            hipEventRecord(c.ev[2 * stage + 1], c.stream);
-            hipEventSynchronize(c.ev[2 * stage + 1]);
-            float ms = 0.f;
-            hipEventElapsedTime(&ms, c.ev[2 * stage], c.ev[2 * stage + 1]);
-            c.stats.kernel_ms[stage] += ms;
-            c.stats.launches[stage] += 1;
+            (void)hipEventRecord(b, c.stream);
+            timing().pending.push_back({stage, {a, b}});
         }
     }
 };
+
+// Call after the stream has been synchronised.
+void resolve_timers(Ctx& c) {
+    Timing& t = timing();
+    for (auto& p : t.pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.second.first, p.second.second) == hipSuccess) c.stats.kernel_ms[p.first] += ms;
+        t.free_ev.push_back(p.second.first);
+        t.free_ev.push_back(p.second.second);
+    }
+    t.pending.clear();
+}
 
 bool g_timing = false;
 
@@ -800,6 +835,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(counts, S.counts, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, sm));
         HIPCHK(hipStreamSynchronize(sm));
+        if (g_timing) resolve_timers(c);
         uint32_t qn = counts[CNT_NEXT];
         int32_t* qa = S.q0;
         int32_t* qb = S.q1;
@@ -818,6 +854,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(counts, S.counts, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, sm));
             HIPCHK(hipStreamSynchronize(sm));
+            if (g_timing) resolve_timers(c);
             const uint32_t rn = counts[CNT_RESOLVE];
             if (rn > 0) {
                 const uint64_t total = (uint64_t)rn * 2 * ns;
@@ -872,6 +909,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         HIPCHK(hipMemcpyAsync(dump_host->delta, D.delta, sizeof(double) * dump_samples, hipMemcpyDeviceToHost, sm));
     }
     HIPCHK(hipStreamSynchronize(sm));
+    if (g_timing) resolve_timers(c);
     for (size_t i = 0; i < n_tasks; ++i) {
         if (!out) break;
         const lumo_tile_task& t = tasks[i];
@@ -1104,6 +1142,8 @@ lumo_status lumo_stats_get(void* ctx, lumo_stats* stats) {
     *stats = c->stats;
     return LUMO_OK;
 }
+
+void lumo_set_timing(int on) { g_timing = on != 0; }
 
 lumo_status lumo_stats_reset(void* ctx) {
     Ctx* c = static_cast<Ctx*>(ctx);

@@ -1,0 +1,46 @@
+"""Summarise rocprofv3 CSV output of tools/profile.sh: per-kernel launches, average duration
+(kernel trace) and HBM bytes per launch from the FETCH_SIZE / WRITE_SIZE passes.
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes of wide
+coalesced reads -> reported both raw and x2; WRITE_SIZE is taken as is. Units: KB -> bytes."""
+import csv, glob, json, os, sys
+from collections import defaultdict
+
+out = sys.argv[1]
+
+
+def rows(pattern):
+    for p in glob.glob(os.path.join(out, pattern), recursive=True):
+        with open(p) as f:
+            yield from csv.DictReader(f)
+
+
+def short(name):
+    for k in ("k_camera", "k_closest", "k_shade", "k_shadow_queue", "k_shadow", "k_resolve", "k_finish", "k_film",
+              "k_ring", "k_init_mj", "k_init_seeds", "k_trace"):
+        if k in name:
+            return k
+    return name[:60]
+
+
+res = defaultdict(lambda: {"launches": 0, "total_ns": 0})
+for r in rows("trace/**/*kernel_trace.csv"):
+    k = short(r.get("Kernel_Name", ""))
+    res[k]["launches"] += 1
+    res[k]["total_ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+for k, v in res.items():
+    v["avg_us"] = v["total_ns"] / max(v["launches"], 1) / 1e3
+for tag, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+    acc = defaultdict(lambda: [0.0, 0])
+    for r in rows(f"{tag}/**/*counter_collection.csv"):
+        if r.get("Counter_Name") != ctr:
+            continue
+        k = short(r.get("Kernel_Name", ""))
+        acc[k][0] += float(r["Counter_Value"]) * 1024.0
+        acc[k][1] += 1
+    for k, (b, n) in acc.items():
+        res[k][ctr.lower() + "_bytes_per_launch"] = b / max(n, 1)
+for k, v in res.items():
+    if "fetch_size_bytes_per_launch" in v and "write_size_bytes_per_launch" in v:
+        v["hbm_bytes_per_launch"] = 2 * v["fetch_size_bytes_per_launch"] + v["write_size_bytes_per_launch"]
+        v["hbm_bytes_per_launch_raw"] = v["fetch_size_bytes_per_launch"] + v["write_size_bytes_per_launch"]
+print(json.dumps(dict(res), indent=1, sort_keys=True))

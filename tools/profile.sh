@@ -1,0 +1,18 @@
+#!/bin/bash
+# rocprofv3 profile of the bench command (run ON the GPU box from the repo root):
+#   1. --kernel-trace --stats          per-kernel launch counts / average durations
+#   2. --pmc FETCH_SIZE  (own pass)    HBM read bytes per dispatch
+#   3. --pmc WRITE_SIZE  (own pass)    HBM write bytes per dispatch
+# PMC passes never combine with sys/runtime/hip traces.  Outputs under gpurun_out/prof/.
+# Usage: tools/profile.sh <tag> [bench args...]
+set -e
+TAG=${1:-r01}; shift || true
+REPO=$(pwd)
+OUT=$REPO/gpurun_out/prof/$TAG
+mkdir -p $OUT
+ARGS="$@"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $REPO/bench.py $ARGS > $OUT/bench_trace.json 2> $OUT/trace.err
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $REPO/bench.py $ARGS > $OUT/bench_fetch.json 2> $OUT/fetch.err
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $REPO/bench.py $ARGS > $OUT/bench_write.json 2> $OUT/write.err
+cd $REPO && python3 tools/parse_prof.py $OUT > $OUT/summary.json
