@@ -43,7 +43,15 @@ $(ORACLE_G): oracle/src/oracle.cpp oracle/oracle.h $(COMMON_H)
 	@mkdir -p oracle/_build
 	$(CXX) $(CXXFLAGS) -O2 -DLUMO_ORACLE_GLIBC -shared -o $@ oracle/src/oracle.cpp -lpthread
 
+# A/B variants of the device code (perf experiments): lumo_amd/liblumo_amd_<name>.so
+VARIANTS ?= lb4:-DLUMO_TRAVERSAL_WAVES=4 noinl:-DLUMO_NOINLINE_KD
+variants: $(HOST_OBJ)
+	@for v in $(VARIANTS); do n=$${v%%:*}; f=$${v#*:}; f=$$(echo $$f | tr ',' ' '); \
+	  echo "variant $$n: $$f"; \
+	  $(HIPCC) $(HIPFLAGS) $$f -c lumo_amd/csrc/device/kernels.hip -o build/device/kernels_$$n.o && \
+	  $(HIPCC) -shared --offload-arch=$(ARCH) -o lumo_amd/liblumo_amd_$$n.so $(HOST_OBJ) build/device/kernels_$$n.o -lpthread; done
+
 clean:
 	rm -rf build $(LIB) oracle/_build
 
-.PHONY: all clean
+.PHONY: all clean variants

@@ -45,9 +45,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--res", type=int, default=1024)
     ap.add_argument("--spp", type=int, default=1024)
-    ap.add_argument("--max-paths", type=int, default=1 << 21, help="paths in flight per wavefront")
+    ap.add_argument("--max-paths", type=int, default=1 << 23, help="paths in flight per wavefront")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
-    ap.add_argument("--cpu-tile-stride", type=int, default=256, help="CPU sample: every k-th tile of each batch")
+    ap.add_argument("--cpu-tile-stride", type=int, default=8, help="CPU sample: every k-th tile of each batch")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()

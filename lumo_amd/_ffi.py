@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblumo_amd.so")
+LIB_PATH = os.environ.get("LUMO_AMD_LIB") or os.path.join(_HERE, "liblumo_amd.so")
 
 c_double_p = C.POINTER(C.c_double)
 c_int32_p = C.POINTER(C.c_int32)

@@ -20,8 +20,9 @@ constexpr double DINF = __builtin_huge_val();
 constexpr int NS = 4;
 constexpr double Y_INTEGRAL = 106.856895;
 constexpr double SVI = 253.819;  // SAMPLE_VISIBLE_INTEGRAL
-constexpr int KD_STACK = 64;
-constexpr int BVH_STACK = 64;
+// Traversal stacks are sized per scene: the kernels are instantiated for STK in {8,16,32,64}
+// and the host picks the smallest class >= the deepest kd / BVH path (lumo itself uses 64,
+// kdtree.rs:110, bvh.rs:324; a scene needing more than 64 would panic there too).
 
 struct DScene {
     const double* vertices;
@@ -41,7 +42,7 @@ struct DScene {
     const double* alias_pdf;
     const lumo_material* mats;
     const double* dense;
-    int32_t n_onodes, n_lnodes, n_lights, n_shadow;
+    int32_t n_onodes, n_lnodes, n_lights, n_shadow, stack_class;
 };
 
 struct Counters {
@@ -52,6 +53,29 @@ struct Ray {
     V3 o, d;
 };
 __device__ __forceinline__ Ray ray_new(V3 o, V3 d) { return Ray{o, normalize(d)}; }
+
+// Per-ray setup hoisted out of the traversal: lumo recomputes 1/dir in every BVH / kd traversal
+// (bvh.rs:322, kdtree.rs:108-109) and the watertight permutation + shear in every triangle test
+// (triangle.rs:67-95).  They depend only on the ray, so computing them once yields the same
+// IEEE values.
+struct RayX {
+    V3 o, d, inv, wi, shear;
+    int kz;
+};
+__device__ __forceinline__ V3 perm_kz(int kz, V3 v) {
+    return kz == 0 ? V3{v.y, v.z, v.x} : (kz == 1 ? V3{v.z, v.x, v.y} : v);
+}
+__device__ __forceinline__ RayX rayx(const Ray& r) {
+    RayX x;
+    x.o = r.o;
+    x.d = r.d;
+    x.inv = 1.0 / r.d;
+    const V3 wa = vabs(r.d);
+    x.kz = (wa.x > wa.y && wa.x > wa.z) ? 0 : (wa.y > wa.z ? 1 : 2);
+    x.wi = perm_kz(x.kz, r.d);
+    x.shear = V3{-x.wi.x, -x.wi.y, 0.0} / x.wi.z;
+    return x;
+}
 
 struct DColor {
     double s[NS];
@@ -196,17 +220,15 @@ __device__ __forceinline__ void slab(const double* bmin, const double* bmax, V3 
 }
 
 // triangle.rs:63-187, GEO = false: returns t or INF
-__device__ __forceinline__ double tri_hit_t(const DScene& sc, int ti, const Ray& r, double t_min, double t_max,
+__device__ __forceinline__ double tri_hit_t(const DScene& sc, int ti, const RayX& r, double t_min, double t_max,
                                             Counters& C) {
     C.tri++;
     const lumo_triangle T = sc.tris[ti];
     const V3 A = ld3(sc.vertices + 3 * T.v[0]), B = ld3(sc.vertices + 3 * T.v[1]), Cv = ld3(sc.vertices + 3 * T.v[2]);
-    const V3 wa = vabs(r.d);
-    const int kz = (wa.x > wa.y && wa.x > wa.z) ? 0 : (wa.y > wa.z ? 1 : 2);
-    auto perm = [kz](V3 v) { return kz == 0 ? V3{v.y, v.z, v.x} : (kz == 1 ? V3{v.z, v.x, v.y} : v); };
-    const V3 wi = perm(r.d);
-    V3 at = perm(A - r.o), bt = perm(B - r.o), ct = perm(Cv - r.o);
-    const V3 shear = V3{-wi.x, -wi.y, 0.0} / wi.z;
+    const int kz = r.kz;
+    const V3 wi = r.wi;
+    V3 at = perm_kz(kz, A - r.o), bt = perm_kz(kz, B - r.o), ct = perm_kz(kz, Cv - r.o);
+    const V3 shear = r.shear;
     at = at + shear * at.z;
     bt = bt + shear * bt.z;
     ct = ct + shear * ct.z;
@@ -222,15 +244,13 @@ __device__ __forceinline__ double tri_hit_t(const DScene& sc, int ti, const Ray&
 }
 
 // triangle.rs:63-187, GEO = true: full hit record; returns false on miss / self-hit reject.
-__device__ bool tri_hit_geo(const DScene& sc, int ti, const Ray& r, double t_min, double t_max, DHit& out) {
+__device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_min, double t_max, DHit& out) {
     const lumo_triangle T = sc.tris[ti];
     const V3 A = ld3(sc.vertices + 3 * T.v[0]), B = ld3(sc.vertices + 3 * T.v[1]), Cv = ld3(sc.vertices + 3 * T.v[2]);
-    const V3 wa = vabs(r.d);
-    const int kz = (wa.x > wa.y && wa.x > wa.z) ? 0 : (wa.y > wa.z ? 1 : 2);
-    auto perm = [kz](V3 v) { return kz == 0 ? V3{v.y, v.z, v.x} : (kz == 1 ? V3{v.z, v.x, v.y} : v); };
-    const V3 wi = perm(r.d);
-    V3 at = perm(A - r.o), bt = perm(B - r.o), ct = perm(Cv - r.o);
-    const V3 shear = V3{-wi.x, -wi.y, 0.0} / wi.z;
+    const int kz = r.kz;
+    const V3 wi = r.wi;
+    V3 at = perm_kz(kz, A - r.o), bt = perm_kz(kz, B - r.o), ct = perm_kz(kz, Cv - r.o);
+    const V3 shear = r.shear;
     at = at + shear * at.z;
     bt = bt + shear * bt.z;
     ct = ct + shear * ct.z;
@@ -282,20 +302,25 @@ __device__ bool tri_hit_geo(const DScene& sc, int ti, const Ray& r, double t_min
 
 // kdtree.rs:101-169.  GEO: returns the winning local triangle index (or -1);
 // !GEO: returns t of the first hit found (or INF).
-template <bool GEO>
-__device__ double kd_traverse(const DScene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max,
+#ifdef LUMO_NOINLINE_KD
+#define KD_INLINE __noinline__
+#else
+#define KD_INLINE
+#endif
+template <bool GEO, int STK>
+__device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min, double t_max,
                               int* idx_out, Counters& C) {
     const double origin[3] = {r.o.x, r.o.y, r.o.z};
-    const double inv_dir[3] = {1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z};
-    int st_node[KD_STACK];
-    double st_ts[KD_STACK], st_te[KD_STACK];
+    const double inv_dir[3] = {r.inv.x, r.inv.y, r.inv.z};
+    int st_node[STK];
+    double st_ts[STK], st_te[STK];
     int sp = 0;
     double t_hit = DINF;
     int curr = ob.kd_root;
     int idx = -1;
     double ts, te;
     C.aabb++;
-    slab(ob.bmin, ob.bmax, r.o, 1.0 / r.d, ts, te);
+    slab(ob.bmin, ob.bmax, r.o, r.inv, ts, te);
     double t_start = rmax(ts, t_min), t_end = rmin(te, t_max);
     for (;;) {
         if (t_hit < t_start) break;
@@ -349,17 +374,19 @@ __device__ double kd_traverse(const DScene& sc, const lumo_object& ob, const Ray
 }
 
 // Object::hit_t for KdMesh / Rectangle (kdtree.rs:178-180, rectangle.rs:87-89)
-__device__ __forceinline__ double object_hit_t(const DScene& sc, const lumo_object& ob, const Ray& r, double t_min,
+template <int STK>
+__device__ __forceinline__ double object_hit_t(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                                double t_max, Counters& C) {
-    return kd_traverse<false>(sc, ob, r, t_min, t_max, nullptr, C);
+    return kd_traverse<false, STK>(sc, ob, r, t_min, t_max, nullptr, C);
 }
 
 // Object::hit: kd GEO traversal, then the winner's full GEO test.  Returns the global
 // triangle index or -1 (miss, or the GEO self-intersection rejection).
-__device__ __forceinline__ int object_hit_tri(const DScene& sc, const lumo_object& ob, const Ray& r, double t_min,
+template <int STK>
+__device__ __forceinline__ int object_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                               double t_max, Counters& C, DHit* out) {
     int idx = -1;
-    kd_traverse<true>(sc, ob, r, t_min, t_max, &idx, C);
+    kd_traverse<true, STK>(sc, ob, r, t_min, t_max, &idx, C);
     if (idx < 0) return -1;
     DHit h;
     if (!tri_hit_geo(sc, ob.tri_base + idx, r, t_min, t_max, h)) return -1;
@@ -373,12 +400,12 @@ __device__ __forceinline__ void object_fix_hit(const lumo_object& ob, DHit& h) {
 }
 
 // bvh.rs:315-362: returns object index or -1
-template <bool GEO>
+template <bool GEO, int STK>
 __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_nodes, const int32_t* items,
-                            const lumo_object* objs, const Ray& r, double t_min, double t_max, Counters& C) {
+                            const lumo_object* objs, const RayX& r, double t_min, double t_max, Counters& C) {
     if (n_nodes == 0) return -1;
-    const V3 inv_dir = 1.0 / r.d;
-    int stack[BVH_STACK];
+    const V3 inv_dir = r.inv;
+    int stack[STK];
     int sp = 0, curr = 0, idx = -1;
     double tt = t_max;
     for (;;) {
@@ -397,7 +424,7 @@ __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_
             }
             for (int k = 0; k < count; ++k) {
                 const int i = items[node.first + k];
-                const double t = object_hit_t(sc, objs[i], r, t_min, tt, C);
+                const double t = object_hit_t<STK>(sc, objs[i], r, t_min, tt, C);
                 if (GEO) {
                     if (t < tt) {
                         tt = t;
@@ -415,12 +442,13 @@ __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_
 }
 
 // BVH::hit_t (bvh.rs:371-374)
+template <int STK>
 __device__ __forceinline__ double bvh_hit_t(const DScene& sc, const lumo_bvh_node* nodes, int n, const int32_t* items,
-                                            const lumo_object* objs, const Ray& r, double t_min, double t_max,
+                                            const lumo_object* objs, const RayX& r, double t_min, double t_max,
                                             Counters& C) {
-    const int idx = bvh_traverse<false>(sc, nodes, n, items, objs, r, t_min, t_max, C);
+    const int idx = bvh_traverse<false, STK>(sc, nodes, n, items, objs, r, t_min, t_max, C);
     if (idx < 0) return DINF;
-    return object_hit_t(sc, objs[idx], r, t_min, t_max, C);
+    return object_hit_t<STK>(sc, objs[idx], r, t_min, t_max, C);
 }
 
 // Scene::hit (scene.rs:119-147).  kind: 0 miss, 1 object, 2 light.
@@ -428,41 +456,43 @@ struct HitRef {
     double t;
     int kind, obj, tri;
 };
-__device__ HitRef scene_hit(const DScene& sc, const Ray& r, Counters& C) {
+template <int STK>
+__device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     HitRef h{DINF, 0, -1, -1};
     double t_max = DINF;
     DHit g;
-    int oi = bvh_traverse<true>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C);
+    int oi = bvh_traverse<true, STK>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C);
     if (oi >= 0) {
-        const int tri = object_hit_tri(sc, sc.objs[oi], r, 0.0, t_max, C, &g);
+        const int tri = object_hit_tri<STK>(sc, sc.objs[oi], r, 0.0, t_max, C, &g);
         if (tri >= 0) {
             h = HitRef{g.t, 1, oi, tri};
             t_max = g.t;
         }
     }
-    const int li = bvh_traverse<true>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C);
+    const int li = bvh_traverse<true, STK>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C);
     if (li >= 0) {
-        const int tri = object_hit_tri(sc, sc.lights[li], r, 0.0, t_max, C, &g);
+        const int tri = object_hit_tri<STK>(sc, sc.lights[li], r, 0.0, t_max, C, &g);
         if (tri >= 0) h = HitRef{g.t, 2, li, tri};
     }
     return h;
 }
 
 // Rebuild the full hit record of a closest hit (the GEO test is deterministic).
-__device__ __forceinline__ void hit_record(const DScene& sc, const HitRef& hr, const Ray& r, DHit& h) {
+__device__ __forceinline__ void hit_record(const DScene& sc, const HitRef& hr, const RayX& r, DHit& h) {
     const lumo_object& ob = hr.kind == 1 ? sc.objs[hr.obj] : sc.lights[hr.obj];
     tri_hit_geo(sc, hr.tri, r, 0.0, DINF, h);
     object_fix_hit(ob, h);
 }
 
 // Scene::hit_light (scene.rs:165-189): returns true and the light hit if visible.
-__device__ bool scene_hit_light(const DScene& sc, const Ray& r, int light, DHit& lh, Counters& C) {
+template <int STK>
+__device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit& lh, Counters& C) {
     const lumo_object& L = sc.lights[light];
-    if (object_hit_tri(sc, L, r, 0.0, DINF, C, &lh) < 0) return false;
+    if (object_hit_tri<STK>(sc, L, r, 0.0, DINF, C, &lh) < 0) return false;
     object_fix_hit(L, lh);
     const double t_max = lh.t - EPSILON;
-    if (bvh_hit_t(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C) < t_max) return false;
-    if (bvh_hit_t(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C) < t_max) return false;
+    if (bvh_hit_t<STK>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C) < t_max) return false;
+    if (bvh_hit_t<STK>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C) < t_max) return false;
     return true;
 }
 
@@ -522,7 +552,7 @@ __device__ __forceinline__ V3 light_sample_towards(const lumo_object& L, V3 xo, 
     const V3 xi = ld3(L.origin) + rs.x * ld3(L.b0) + rs.y * ld3(L.b1);
     return normalize(xi - xo);
 }
-__device__ __forceinline__ double light_pdf(const lumo_object& L, const Ray& ri, V3 xi, V3 ng) {
+__device__ __forceinline__ double light_pdf(const lumo_object& L, const RayX& ri, V3 xi, V3 ng) {
     const double p_area = 1.0 / L.area;
     return p_area * distance_squared(ri.o, xi) / fabs(dot(ng, ri.d));
 }

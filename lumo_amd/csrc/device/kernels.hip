@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "../../../include/lumo_amd.h"
@@ -32,6 +33,10 @@ using namespace lumo::dev;
 namespace {
 
 constexpr int BLOCK = 256;
+#ifndef LUMO_TRAVERSAL_WAVES
+#define LUMO_TRAVERSAL_WAVES 1
+#endif
+#define TRAV_BOUNDS __launch_bounds__(BLOCK, LUMO_TRAVERSAL_WAVES)
 constexpr uint64_t SAMPLES_INCREMENT = 256;
 constexpr int RR_DEPTH = 5;
 
@@ -238,13 +243,14 @@ __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, in
 }
 
 // ------------------------------------------------------------------ closest hit
-__global__ __launch_bounds__(BLOCK) void k_closest(DScene sc, Paths S, const int32_t* queue, uint32_t count) {
+template <int STK>
+__global__ TRAV_BOUNDS void k_closest(DScene sc, Paths S, const int32_t* queue, uint32_t count) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     Counters C{0, 0, 0};
     if (q < count) {
         const int s = queue[q];
-        const Ray r{ldv3(S.ro, s), ldv3(S.rd, s)};
-        const HitRef h = scene_hit(sc, r, C);
+        const RayX r = rayx(Ray{ldv3(S.ro, s), ldv3(S.rd, s)});
+        const HitRef h = scene_hit<STK>(sc, r, C);
         S.hit_t[s] = h.t;
         S.hit_kind[s] = h.kind;
         S.hit_obj[s] = h.obj;
@@ -255,7 +261,7 @@ __global__ __launch_bounds__(BLOCK) void k_closest(DScene sc, Paths S, const int
 }
 
 // ------------------------------------------------------------------ shade
-__global__ __launch_bounds__(BLOCK) void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue, uint32_t count,
+__global__ TRAV_BOUNDS void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue, uint32_t count,
                                                   int32_t* next_queue) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     bool alive = false, resolve = false;
@@ -269,7 +275,7 @@ __global__ __launch_bounds__(BLOCK) void k_shade(DScene sc, Paths S, Tasks T, co
             const Ray ro{ldv3(S.ro, s), ldv3(S.rd, s)};
             const HitRef hr{S.hit_t[s], kind, S.hit_obj[s], S.hit_tri[s]};
             DHit ho;
-            hit_record(sc, hr, ro, ho);
+            hit_record(sc, hr, rayx(ro), ho);
             const lumo_material m = sc.mats[ho.material];
             Xorshift rng{S.rng[2 * s], S.rng[2 * s + 1]};
             if (s == g_dbg.slot && g_dbg.pass == g_dbg.cur_pass && g_dbg.n < 64) {
@@ -370,36 +376,28 @@ __global__ __launch_bounds__(BLOCK) void k_shade(DScene sc, Paths S, Tasks T, co
     }
     wave_append(alive, s, next_queue, S.counts + CNT_NEXT);
     wave_append(resolve, s, S.rq, S.counts + CNT_RESOLVE);
-}
-
-// Shadow-record queue: all valid records of the resolve queue's slots.
-__global__ __launch_bounds__(BLOCK) void k_shadow_queue(DScene sc, Paths S, uint32_t count) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    const int per = 2 * sc.n_shadow;
-    const uint32_t total = count * (uint32_t)per;
-    bool valid = false;
-    int rec = -1;
-    if (q < total) {
-        const int s = S.rq[q / per];
-        rec = s * per + (int)(q % per);
-        valid = (S.sh_flags[rec] & 1) != 0;
-        if (!valid) stc(S.sh_out, rec, cfill(0.0));
+    // shadow-record queue: every valid record of this slot, in record order (fused compaction)
+    for (int k = 0; k < 2 * ns; ++k) {
+        const int rec = s * 2 * ns + k;
+        const bool v = resolve && (S.sh_flags[rec] & 1) != 0;
+        if (resolve && !v) stc(S.sh_out, rec, cfill(0.0));
+        wave_append(v, rec, S.sq, S.counts + CNT_SHADOW);
     }
-    wave_append(valid, rec, S.sq, S.counts + CNT_SHADOW);
 }
 
 // ------------------------------------------------------------------ shadow (hit_light + MIS)
-__global__ __launch_bounds__(BLOCK) void k_shadow(DScene sc, Paths S, uint32_t count) {
+template <int STK>
+__global__ TRAV_BOUNDS void k_shadow(DScene sc, Paths S, uint32_t count) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     Counters C{0, 0, 0};
     if (q < count) {
         const int rec = S.sq[q];
         const int s = rec / (2 * sc.n_shadow);
-        const Ray ri{ldv3(S.sh_o, rec), ldv3(S.sh_d, rec)};
+        const RayX ri = rayx(Ray{ldv3(S.sh_o, rec), ldv3(S.sh_d, rec)});
         const int li = S.sh_light[rec];
         DHit hi;
         DColor out = cfill(0.0);
-        if (scene_hit_light(sc, ri, li, hi, C)) {
+        if (scene_hit_light<STK>(sc, ri, li, hi, C)) {
             const lumo_object& Lo = sc.lights[li];
             const double p_lig = light_pdf(Lo, ri, hi.p, hi.ng);
             const double p_sct = S.sh_psct[rec];
@@ -505,51 +503,81 @@ __global__ __launch_bounds__(BLOCK) void k_film(Paths S, Tasks T, DCam cam, int 
 }
 
 // task.rs:42-53 + 64-69: ring update in pixel order, then delta for the next pass.
-__global__ void k_ring(Paths S, Tasks T, int n_tasks, int update) {
-    const int ti = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per task.  The pass's samples land in ring slots (ptr + j) % n; when a tile has more
+// pixels than ring slots only the last writer of a slot (no j + n < P) stores.  The variance
+// sums stay sequential in slot order (lane 0, from LDS) so they round exactly like task.rs.
+__global__ __launch_bounds__(64) void k_ring(Paths S, Tasks T, int n_tasks, int update) {
+    const int ti = blockIdx.x;
     if (ti >= n_tasks) return;
+    const int lane = threadIdx.x;
+    __shared__ double lum[SAMPLES_INCREMENT];
+    __shared__ unsigned long long cst[SAMPLES_INCREMENT];
     const lumo_tile_task& t = T.t[ti];
-    const uint64_t n = t.samples;
+    const int n = (int)t.samples;
     uint64_t* rc = T.ring_cost + (size_t)ti * SAMPLES_INCREMENT;
     double* rl = T.ring_lum + (size_t)ti * SAMPLES_INCREMENT;
-    if (update) {
-        uint32_t ptr = T.ring_ptr[ti];
-        unsigned long long rays = 0, queries = 0;
-        for (int s = T.first[ti]; s < T.first[ti + 1]; ++s) {
-            if (!S.p_valid[s]) continue;
-            rays += S.p_cost[s];
-            queries += S.queries[s];
-            rc[ptr] = S.p_cost[s];
-            rl[ptr] = S.p_lum[s];
-            ptr = (uint32_t)((ptr + 1) % n);
+    for (int r = lane; r < n; r += 64) {
+        lum[r] = rl[r];
+        cst[r] = rc[r];
+    }
+    __syncthreads();
+    const int f0 = T.first[ti];
+    const int P = T.first[ti + 1] - f0;
+    if (update && S.p_valid[f0]) {
+        const uint32_t ptr = T.ring_ptr[ti];
+        unsigned long long rays = 0, q = 0;
+        for (int j = lane; j < P; j += 64) {
+            const int sl = f0 + j;
+            rays += S.p_cost[sl];
+            q += S.queries[sl];
+            if (j + n >= P) {
+                const int r = (int)((ptr + (uint32_t)j) % (uint32_t)n);
+                lum[r] = S.p_lum[sl];
+                cst[r] = S.p_cost[sl];
+            }
         }
-        T.ring_ptr[ti] = ptr;
-        T.num_rays[ti] += rays;
-        T.queries[ti] += queries;
+        for (int off = 32; off > 0; off >>= 1) {
+            rays += __shfl_down(rays, off);
+            q += __shfl_down(q, off);
+        }
+        if (lane == 0) {
+            T.num_rays[ti] += rays;
+            T.queries[ti] += q;
+            T.ring_ptr[ti] = (uint32_t)((ptr + (uint32_t)P) % (uint32_t)n);
+        }
+        __syncthreads();
+        for (int r = lane; r < n; r += 64) {
+            rl[r] = lum[r];
+            rc[r] = cst[r];
+        }
     }
-    double f = 0.0, f2 = 0.0;
-    for (uint64_t i = 0; i < n; ++i) f = f + rl[i];
-    for (uint64_t i = 0; i < n; ++i) f2 = f2 + rl[i] * rl[i];
-    const double var = f2 - f * f / (double)n;
-    double delta = 1e-5;
-    if (!(var <= 0.0)) {
-        uint64_t cost = 0;
-        for (uint64_t i = 0; i < n; ++i) cost += rc[i];
-        delta = sqrt(var / (double)cost);
+    __syncthreads();
+    if (lane == 0) {
+        double f = 0.0, f2 = 0.0;
+        for (int i = 0; i < n; ++i) f = f + lum[i];
+        for (int i = 0; i < n; ++i) f2 = f2 + lum[i] * lum[i];
+        const double var = f2 - f * f / (double)n;
+        double delta = 1e-5;
+        if (!(var <= 0.0)) {
+            uint64_t cost = 0;
+            for (int i = 0; i < n; ++i) cost += cst[i];
+            delta = sqrt(var / (double)cost);
+        }
+        T.delta[ti] = delta;
     }
-    T.delta[ti] = delta;
 }
 
 // ------------------------------------------------------------------ traversal-only entry (lumo_trace)
+template <int STK>
 __global__ void k_trace(DScene sc, const double* o, const double* d, const int32_t* light, int n, int any_hit,
                         double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
                         unsigned long long* tcount) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     Counters C{0, 0, 0};
     if (i < n) {
-        const Ray r{ldv3(o, i), ldv3(d, i)};
+        const RayX r = rayx(Ray{ldv3(o, i), ldv3(d, i)});
         if (!any_hit) {
-            const HitRef h = scene_hit(sc, r, C);
+            const HitRef h = scene_hit<STK>(sc, r, C);
             t_out[i] = h.t;
             kind_out[i] = h.kind;
             obj_out[i] = h.obj;
@@ -557,7 +585,7 @@ __global__ void k_trace(DScene sc, const double* o, const double* d, const int32
         } else {
             DHit lh;
             const int li = light[i];
-            const bool vis = scene_hit_light(sc, r, li, lh, C);
+            const bool vis = scene_hit_light<STK>(sc, r, li, lh, C);
             t_out[i] = vis ? lh.t : DINF;
             kind_out[i] = vis ? 2 : 0;
             obj_out[i] = vis ? li : -1;
@@ -703,6 +731,16 @@ void resolve_timers(Ctx& c) {
 
 bool g_timing = false;
 
+template <typename F>
+void by_stack_class(int cls, F&& f) {
+    switch (cls) {
+        case 8: f(std::integral_constant<int, 8>{}); break;
+        case 16: f(std::integral_constant<int, 16>{}); break;
+        case 32: f(std::integral_constant<int, 32>{}); break;
+        default: f(std::integral_constant<int, 64>{}); break;
+    }
+}
+
 lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lumo_tile_result* out, Dump* dump_host,
                         uint64_t dump_samples) {
     if (!c.has_scene) return LUMO_ERR_NO_SCENE;
@@ -815,7 +853,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     const int gT = ceil_div(n_tasks, BLOCK), gN = ceil_div(N, BLOCK);
     k_init_seeds<<<gT, BLOCK, 0, sm>>>(T, S, (int)n_tasks);
     k_init_mj<<<gN, BLOCK, 0, sm>>>(T, S, N, dim_stride);
-    k_ring<<<gT, BLOCK, 0, sm>>>(S, T, (int)n_tasks, 0);
+    k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 0);
     HIPCHK(hipGetLastError());
 
     uint64_t bounces = 0, closest_q = 0, shadow_q = 0;
@@ -845,7 +883,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * 4, sm));
             {
                 StageTimer tm(c, g_timing, ST_CLOSEST);
-                k_closest<<<ceil_div(qn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, qa, qn);
+                by_stack_class(c.sc.stack_class, [&](auto K) {
+                    k_closest<decltype(K)::value><<<ceil_div(qn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, qa, qn);
+                });
             }
             {
                 StageTimer tm(c, g_timing, ST_SHADE);
@@ -856,24 +896,19 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             HIPCHK(hipStreamSynchronize(sm));
             if (g_timing) resolve_timers(c);
             const uint32_t rn = counts[CNT_RESOLVE];
-            if (rn > 0) {
-                const uint64_t total = (uint64_t)rn * 2 * ns;
-                k_shadow_queue<<<ceil_div(total, BLOCK), BLOCK, 0, sm>>>(c.sc, S, rn);
-                HIPCHK(hipMemcpyAsync(counts + CNT_SHADOW, S.counts + CNT_SHADOW, sizeof(uint32_t),
-                                      hipMemcpyDeviceToHost, sm));
-                HIPCHK(hipStreamSynchronize(sm));
-                const uint32_t sn = counts[CNT_SHADOW];
-                shadow_q += sn;
-                if (sn > 0) {
-                    StageTimer tm(c, g_timing, ST_SHADOW);
-                    k_shadow<<<ceil_div(sn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, sn);
-                }
-                {
-                    StageTimer tm(c, g_timing, ST_RESOLVE);
-                    k_resolve<<<ceil_div(rn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, rn);
-                }
-                HIPCHK(hipGetLastError());
+            const uint32_t sn = counts[CNT_SHADOW];
+            shadow_q += sn;
+            if (sn > 0) {
+                StageTimer tm(c, g_timing, ST_SHADOW);
+                by_stack_class(c.sc.stack_class, [&](auto K) {
+                    k_shadow<decltype(K)::value><<<ceil_div(sn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, sn);
+                });
             }
+            if (rn > 0) {
+                StageTimer tm(c, g_timing, ST_RESOLVE);
+                k_resolve<<<ceil_div(rn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, rn);
+            }
+            HIPCHK(hipGetLastError());
             qn = counts[CNT_NEXT];
             std::swap(qa, qb);
         }
@@ -887,7 +922,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         }
         {
             StageTimer tm(c, g_timing, ST_RING);
-            k_ring<<<gT, BLOCK, 0, sm>>>(S, T, (int)n_tasks, 1);
+            k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 1);
         }
         HIPCHK(hipGetLastError());
     }
@@ -1045,6 +1080,43 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         lg++;
     }
     s.n_shadow = lg > 1 ? lg : 1;  // scene.rs:90-92
+    // deepest pending-stack use: BVH (right children pending on a root-leaf path) and kd trees
+    int need = 1;
+    auto bvh_need = [&](const lumo_bvh_node* nodes, int n) {
+        std::vector<int> pend(n > 0 ? n : 1, 0);
+        int mx = 0;
+        for (int i = 0; i < n; ++i) {  // parents precede children in lumo's layout
+            if (nodes[i].count == 0) {
+                const int p = pend[i] + (nodes[i].right >= 0 ? 1 : 0);
+                if (i + 1 < n) pend[i + 1] = std::max(pend[i + 1], p);
+                if (nodes[i].right >= 0 && nodes[i].right < n) pend[nodes[i].right] = std::max(pend[nodes[i].right], pend[i]);
+                mx = std::max(mx, p);
+            }
+        }
+        return mx;
+    };
+    need = std::max(need, bvh_need(d->object_nodes, d->num_object_nodes));
+    need = std::max(need, bvh_need(d->light_nodes, d->num_light_nodes));
+    {
+        std::vector<int> depth(d->num_kd_nodes > 0 ? d->num_kd_nodes : 1, 0);
+        for (int i = 0; i < d->num_kd_nodes; ++i) {
+            if (!d->kd_nodes[i].leaf) {
+                if (i + 1 < d->num_kd_nodes) depth[i + 1] = std::max(depth[i + 1], depth[i] + 1);
+                const int r = d->kd_nodes[i].right;
+                if (r >= 0 && r < d->num_kd_nodes) depth[r] = std::max(depth[r], depth[i] + 1);
+                need = std::max(need, depth[i] + 1);
+            }
+        }
+    }
+    if (need > 64) {
+        free_scene(*c);
+        return LUMO_ERR_UNSUPPORTED;  // lumo's fixed [_; 64] stacks would overflow too
+    }
+    s.stack_class = need <= 8 ? 8 : need <= 16 ? 16 : need <= 32 ? 32 : 64;
+    if (const char* e = std::getenv("LUMO_STACK_CLASS")) {  // A/B override (never below `need`)
+        const int f = std::atoi(e);
+        if (f >= need && (f == 8 || f == 16 || f == 32 || f == 64)) s.stack_class = f;
+    }
     c->has_scene = true;
     return LUMO_OK;
 }
@@ -1126,7 +1198,10 @@ lumo_status lumo_trace(void* ctx, const lumo_ray_soa* rays, size_t n, lumo_hit_s
     HIPCHK(hipMemcpyAsync(d, rays->dir, sizeof(double) * 3 * n, hipMemcpyHostToDevice, sm));
     if (any_hit) HIPCHK(hipMemcpyAsync(light, rays->light, sizeof(int32_t) * n, hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemsetAsync(tc, 0, sizeof(unsigned long long) * 2 * TC_N, sm));
-    k_trace<<<ceil_div(n, BLOCK), BLOCK, 0, sm>>>(c->sc, o, d, light, (int)n, any_hit, t, kind, obj, prim, tc);
+    by_stack_class(c->sc.stack_class, [&](auto K) {
+        k_trace<decltype(K)::value>
+            <<<ceil_div(n, BLOCK), BLOCK, 0, sm>>>(c->sc, o, d, light, (int)n, any_hit, t, kind, obj, prim, tc);
+    });
     HIPCHK(hipGetLastError());
     if (hits->t) HIPCHK(hipMemcpyAsync(hits->t, t, sizeof(double) * n, hipMemcpyDeviceToHost, sm));
     if (hits->kind) HIPCHK(hipMemcpyAsync(hits->kind, kind, sizeof(int32_t) * n, hipMemcpyDeviceToHost, sm));
