@@ -168,6 +168,10 @@ def roofline(st):
         nbytes = None
     out = {"bound": "hbm", "kernel": f"k_{name}", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": pmc_traffic(name),
            "stages": per_stage}
+    cq, sq = max(st.closest_queries, 1), max(st.shadow_queries, 1)
+    out["per_query"] = {
+        "closest": {"aabb": st.aabb_tests[0] / cq, "kd": st.kd_nodes[0] / cq, "tri": st.tri_tests[0] / cq},
+        "shadow": {"aabb": st.aabb_tests[1] / sq, "kd": st.kd_nodes[1] / sq, "tri": st.tri_tests[1] / sq}}
     if nbytes is not None and ms[dom] > 0 and launches[dom] > 0:
         achieved = nbytes / (ms[dom] * 1e-3) / 1e9
         out.update({"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 5),

@@ -43,7 +43,33 @@ struct DScene {
     const lumo_material* mats;
     const double* dense;
     int32_t n_onodes, n_lnodes, n_lights, n_shadow, stack_class;
+    // Traversal working set packed contiguously (16-B aligned sub-arrays) so that a small scene
+    // can be staged into LDS once per workgroup; hot_bytes == 0 disables staging.
+    const char* hot;
+    uint32_t hot_bytes;
+    uint32_t off_onodes, off_oitems, off_lnodes, off_litems, off_objs, off_lights, off_kd, off_kd_items, off_tris,
+        off_vertices;
 };
+
+// Copy the packed traversal set into LDS and point a scene view at it.
+__device__ __forceinline__ DScene stage_scene_lds(const DScene& sc, char* lds) {
+    const uint4* src = reinterpret_cast<const uint4*>(sc.hot);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    for (uint32_t i = threadIdx.x; i < sc.hot_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+    DScene v = sc;
+    v.onodes = reinterpret_cast<const lumo_bvh_node*>(lds + sc.off_onodes);
+    v.oitems = reinterpret_cast<const int32_t*>(lds + sc.off_oitems);
+    v.lnodes = reinterpret_cast<const lumo_bvh_node*>(lds + sc.off_lnodes);
+    v.litems = reinterpret_cast<const int32_t*>(lds + sc.off_litems);
+    v.objs = reinterpret_cast<const lumo_object*>(lds + sc.off_objs);
+    v.lights = reinterpret_cast<const lumo_object*>(lds + sc.off_lights);
+    v.kd = reinterpret_cast<const lumo_kd_node*>(lds + sc.off_kd);
+    v.kd_items = reinterpret_cast<const int32_t*>(lds + sc.off_kd_items);
+    v.tris = reinterpret_cast<const lumo_triangle*>(lds + sc.off_tris);
+    v.vertices = reinterpret_cast<const double*>(lds + sc.off_vertices);
+    return v;
+}
 
 struct Counters {
     uint32_t aabb, kd, tri;
@@ -243,7 +269,10 @@ __device__ __forceinline__ double tri_hit_t(const DScene& sc, int ti, const RayX
     return t_scaled / det;
 }
 
-// triangle.rs:63-187, GEO = true: full hit record; returns false on miss / self-hit reject.
+// triangle.rs:63-187, GEO = true: returns false on miss / self-hit reject.  FULL also builds the
+// hit record (point, normals, uv, error bounds); !FULL stops after the t <= t_min + delta_t
+// check (callers that only need acceptance and t; the record is rebuilt identically later).
+template <bool FULL>
 __device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_min, double t_max, DHit& out) {
     const lumo_triangle T = sc.tris[ti];
     const V3 A = ld3(sc.vertices + 3 * T.v[0]), B = ld3(sc.vertices + 3 * T.v[1]), Cv = ld3(sc.vertices + 3 * T.v[2]);
@@ -273,6 +302,8 @@ __device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_mi
     const double max_e = rmax(rmax(fabs(e.x), fabs(e.y)), fabs(e.z));
     const double delta_t = 3.0 * (gamma_n(3) * max_e * max_z_v + delta_e * max_z_v + delta_z * max_e) / fabs(det);
     if (t <= t_min + delta_t) return false;
+    out.t = t;
+    if (!FULL) return true;
     const V3 bary = e / det;
     const V3 ng = normalize(cross(B - A, Cv - A));
     V3 ns = ng;
@@ -382,15 +413,13 @@ __device__ __forceinline__ double object_hit_t(const DScene& sc, const lumo_obje
 
 // Object::hit: kd GEO traversal, then the winner's full GEO test.  Returns the global
 // triangle index or -1 (miss, or the GEO self-intersection rejection).
-template <int STK>
+template <int STK, bool FULL>
 __device__ __forceinline__ int object_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
-                                              double t_max, Counters& C, DHit* out) {
+                                              double t_max, Counters& C, DHit& out) {
     int idx = -1;
     kd_traverse<true, STK>(sc, ob, r, t_min, t_max, &idx, C);
     if (idx < 0) return -1;
-    DHit h;
-    if (!tri_hit_geo(sc, ob.tri_base + idx, r, t_min, t_max, h)) return -1;
-    if (out) *out = h;
+    if (!tri_hit_geo<FULL>(sc, ob.tri_base + idx, r, t_min, t_max, out)) return -1;
     return ob.tri_base + idx;
 }
 
@@ -402,7 +431,8 @@ __device__ __forceinline__ void object_fix_hit(const lumo_object& ob, DHit& h) {
 // bvh.rs:315-362: returns object index or -1
 template <bool GEO, int STK>
 __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_nodes, const int32_t* items,
-                            const lumo_object* objs, const RayX& r, double t_min, double t_max, Counters& C) {
+                            const lumo_object* objs, const RayX& r, double t_min, double t_max, Counters& C,
+                            double* t_found = nullptr) {
     if (n_nodes == 0) return -1;
     const V3 inv_dir = r.inv;
     int stack[STK];
@@ -431,6 +461,7 @@ __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_
                         idx = i;
                     }
                 } else if (t < tt) {
+                    if (t_found) *t_found = t;
                     return i;
                 }
             }
@@ -446,9 +477,12 @@ template <int STK>
 __device__ __forceinline__ double bvh_hit_t(const DScene& sc, const lumo_bvh_node* nodes, int n, const int32_t* items,
                                             const lumo_object* objs, const RayX& r, double t_min, double t_max,
                                             Counters& C) {
-    const int idx = bvh_traverse<false, STK>(sc, nodes, n, items, objs, r, t_min, t_max, C);
+    // bvh.rs:371-374 re-runs objects[idx].hit_t(r, t_min, t_max); in any-hit mode the traversal
+    // called exactly that (tt == t_max), so its value is reused.
+    double t = DINF;
+    const int idx = bvh_traverse<false, STK>(sc, nodes, n, items, objs, r, t_min, t_max, C, &t);
     if (idx < 0) return DINF;
-    return object_hit_t<STK>(sc, objs[idx], r, t_min, t_max, C);
+    return t;
 }
 
 // Scene::hit (scene.rs:119-147).  kind: 0 miss, 1 object, 2 light.
@@ -463,7 +497,7 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     DHit g;
     int oi = bvh_traverse<true, STK>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C);
     if (oi >= 0) {
-        const int tri = object_hit_tri<STK>(sc, sc.objs[oi], r, 0.0, t_max, C, &g);
+        const int tri = object_hit_tri<STK, false>(sc, sc.objs[oi], r, 0.0, t_max, C, g);
         if (tri >= 0) {
             h = HitRef{g.t, 1, oi, tri};
             t_max = g.t;
@@ -471,7 +505,7 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     }
     const int li = bvh_traverse<true, STK>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C);
     if (li >= 0) {
-        const int tri = object_hit_tri<STK>(sc, sc.lights[li], r, 0.0, t_max, C, &g);
+        const int tri = object_hit_tri<STK, false>(sc, sc.lights[li], r, 0.0, t_max, C, g);
         if (tri >= 0) h = HitRef{g.t, 2, li, tri};
     }
     return h;
@@ -480,7 +514,7 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
 // Rebuild the full hit record of a closest hit (the GEO test is deterministic).
 __device__ __forceinline__ void hit_record(const DScene& sc, const HitRef& hr, const RayX& r, DHit& h) {
     const lumo_object& ob = hr.kind == 1 ? sc.objs[hr.obj] : sc.lights[hr.obj];
-    tri_hit_geo(sc, hr.tri, r, 0.0, DINF, h);
+    tri_hit_geo<true>(sc, hr.tri, r, 0.0, DINF, h);
     object_fix_hit(ob, h);
 }
 
@@ -488,11 +522,14 @@ __device__ __forceinline__ void hit_record(const DScene& sc, const HitRef& hr, c
 template <int STK>
 __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit& lh, Counters& C) {
     const lumo_object& L = sc.lights[light];
-    if (object_hit_tri<STK>(sc, L, r, 0.0, DINF, C, &lh) < 0) return false;
-    object_fix_hit(L, lh);
+    const int tri = object_hit_tri<STK, false>(sc, L, r, 0.0, DINF, C, lh);
+    if (tri < 0) return false;
     const double t_max = lh.t - EPSILON;
     if (bvh_hit_t<STK>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C) < t_max) return false;
     if (bvh_hit_t<STK>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C) < t_max) return false;
+    // visible: build the light hit record (same GEO test, now in full)
+    tri_hit_geo<true>(sc, tri, r, 0.0, DINF, lh);
+    object_fix_hit(L, lh);
     return true;
 }
 

@@ -33,10 +33,16 @@ using namespace lumo::dev;
 namespace {
 
 constexpr int BLOCK = 256;
-#ifndef LUMO_TRAVERSAL_WAVES
-#define LUMO_TRAVERSAL_WAVES 1
+// Minimum waves per SIMD (register budget) per kernel, tuned by A/B on MI355X.
+#ifndef LUMO_CLOSEST_WAVES
+#define LUMO_CLOSEST_WAVES 4
 #endif
-#define TRAV_BOUNDS __launch_bounds__(BLOCK, LUMO_TRAVERSAL_WAVES)
+#ifndef LUMO_SHADOW_WAVES
+#define LUMO_SHADOW_WAVES 4
+#endif
+#ifndef LUMO_SHADE_WAVES
+#define LUMO_SHADE_WAVES 1
+#endif
 constexpr uint64_t SAMPLES_INCREMENT = 256;
 constexpr int RR_DEPTH = 5;
 
@@ -110,6 +116,33 @@ __device__ __forceinline__ void wave_append(bool pred, int32_t value, int32_t* q
     if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
     base = __shfl(base, leader);
     if (pred) queue[base + prefix] = value;
+}
+
+// Workgroup-aggregated stream compaction: ballot + mbcnt inside each wave, wave totals scanned
+// in LDS, ONE atomicAdd per workgroup on the queue counter (a single hot counter word
+// saturates near 88 M atomics/s on MI355X, MI355X_MICROARCH.md "dequeue").  Every thread of
+// the block must call it (it synchronises the block).
+__device__ __forceinline__ void block_append(bool pred, int32_t value, int32_t* queue, uint32_t* counter) {
+    __shared__ uint32_t wtot[BLOCK / 64];
+    __shared__ uint32_t base_s;
+    const uint64_t mask = __ballot(pred);
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t prefix =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+    if (lane == 0) wtot[w] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+            const uint32_t cnt = wtot[i];
+            wtot[i] = t;
+            t += cnt;
+        }
+        base_s = t ? atomicAdd(counter, t) : 0u;
+    }
+    __syncthreads();
+    if (pred) queue[base_s + wtot[w] + prefix] = value;
+    __syncthreads();
 }
 
 // Wave-reduced traversal counters (one atomic per wavefront).
@@ -239,15 +272,16 @@ __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, in
             S.queries[s] = 0;
         }
     }
-    wave_append(active, s, S.q0, S.counts + CNT_NEXT);
+    block_append(active, s, S.q0, S.counts + CNT_NEXT);
 }
 
 // ------------------------------------------------------------------ closest hit
-template <int STK>
-__global__ TRAV_BOUNDS void k_closest(DScene sc, Paths S, const int32_t* queue, uint32_t count) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+template <int STK, bool LDS>
+__global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc0, Paths S, const int32_t* queue, uint32_t count) {
+    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     Counters C{0, 0, 0};
-    if (q < count) {
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
         const int s = queue[q];
         const RayX r = rayx(Ray{ldv3(S.ro, s), ldv3(S.rd, s)});
         const HitRef h = scene_hit<STK>(sc, r, C);
@@ -261,7 +295,7 @@ __global__ TRAV_BOUNDS void k_closest(DScene sc, Paths S, const int32_t* queue, 
 }
 
 // ------------------------------------------------------------------ shade
-__global__ TRAV_BOUNDS void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue, uint32_t count,
+__global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue, uint32_t count,
                                                   int32_t* next_queue) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     bool alive = false, resolve = false;
@@ -374,25 +408,23 @@ __global__ TRAV_BOUNDS void k_shade(DScene sc, Paths S, Tasks T, const int32_t* 
             S.queries[s] += (uint32_t)n_sh;
         }
     }
-    wave_append(alive, s, next_queue, S.counts + CNT_NEXT);
-    wave_append(resolve, s, S.rq, S.counts + CNT_RESOLVE);
-    // shadow-record queue: every valid record of this slot, in record order (fused compaction)
-    for (int k = 0; k < 2 * ns; ++k) {
-        const int rec = s * 2 * ns + k;
-        const bool v = resolve && (S.sh_flags[rec] & 1) != 0;
-        if (resolve && !v) stc(S.sh_out, rec, cfill(0.0));
-        wave_append(v, rec, S.sq, S.counts + CNT_SHADOW);
-    }
+    block_append(alive, s, next_queue, S.counts + CNT_NEXT);
+    block_append(resolve, s, S.rq, S.counts + CNT_RESOLVE);
 }
 
 // ------------------------------------------------------------------ shadow (hit_light + MIS)
-template <int STK>
-__global__ TRAV_BOUNDS void k_shadow(DScene sc, Paths S, uint32_t count) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+// One thread per (resolve-queue slot, shadow record); `count` = resolve count x 2 n_shadow.
+// Records whose BSDF sample failed are skipped (k_resolve reads them as black).
+template <int STK, bool LDS>
+__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0, Paths S, uint32_t count) {
+    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     Counters C{0, 0, 0};
-    if (q < count) {
-        const int rec = S.sq[q];
-        const int s = rec / (2 * sc.n_shadow);
+    const uint32_t per = 2u * (uint32_t)sc.n_shadow;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
+        const int s = S.rq[q / per];
+        const int rec = s * (int)per + (int)(q % per);
+        if ((S.sh_flags[rec] & 1) == 0) continue;
         const RayX ri = rayx(Ray{ldv3(S.sh_o, rec), ldv3(S.sh_d, rec)});
         const int li = S.sh_light[rec];
         DHit hi;
@@ -427,7 +459,9 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(DScene sc, Paths S, uint32_t 
     DColor acc = cfill(0.0);
     for (int i = 0; i < ns; ++i) {
         const int rec = s * 2 * ns + 2 * i;
-        const DColor single = (cfill(0.0) + ldc(S.sh_out, rec) + ldc(S.sh_out, rec + 1)) / S.pdf_l[s * ns + i];
+        const DColor a = ldc(S.sh_out, rec);
+        const DColor b = (S.sh_flags[rec + 1] & 1) ? ldc(S.sh_out, rec + 1) : cfill(0.0);
+        const DColor single = (cfill(0.0) + a + b) / S.pdf_l[s * ns + i];
         acc = acc + g * single;
     }
     stc(S.rad, s, ldc(S.rad, s) + acc / (double)ns);
@@ -625,6 +659,7 @@ struct Ctx {
     std::vector<DevBuf> work;  // grown on demand
     lumo_stats stats{};
     hipEvent_t ev[2 * ST_COUNT];
+    int lds_grid_cap = 2048;
 };
 
 lumo_status dev_alloc(DevBuf& b, size_t bytes) {
@@ -739,6 +774,21 @@ void by_stack_class(int cls, F&& f) {
         case 32: f(std::integral_constant<int, 32>{}); break;
         default: f(std::integral_constant<int, 64>{}); break;
     }
+}
+
+// Traversal launch: stack class x LDS staging.  With LDS staging the grid is capped (persistent
+// grid-stride loop) so each workgroup copies the packed scene once per launch.
+bool g_lds = true;
+template <typename F>
+void launch_trav(Ctx& c, uint32_t count, F&& f) {
+    const bool lds = g_lds && c.sc.hot_bytes > 0;
+    const int grid_full = ceil_div(count, BLOCK);
+    by_stack_class(c.sc.stack_class, [&](auto K) {
+        if (lds)
+            f(K, std::true_type{}, std::min(grid_full, c.lds_grid_cap), (size_t)c.sc.hot_bytes);
+        else
+            f(K, std::false_type{}, grid_full, (size_t)0);
+    });
 }
 
 lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lumo_tile_result* out, Dump* dump_host,
@@ -883,8 +933,8 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * 4, sm));
             {
                 StageTimer tm(c, g_timing, ST_CLOSEST);
-                by_stack_class(c.sc.stack_class, [&](auto K) {
-                    k_closest<decltype(K)::value><<<ceil_div(qn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, qa, qn);
+                launch_trav(c, qn, [&](auto K, auto Lds, int grid, size_t shm) {
+                    k_closest<decltype(K)::value, decltype(Lds)::value><<<grid, BLOCK, shm, sm>>>(c.sc, S, qa, qn);
                 });
             }
             {
@@ -896,12 +946,11 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             HIPCHK(hipStreamSynchronize(sm));
             if (g_timing) resolve_timers(c);
             const uint32_t rn = counts[CNT_RESOLVE];
-            const uint32_t sn = counts[CNT_SHADOW];
-            shadow_q += sn;
+            const uint32_t sn = rn * 2u * (uint32_t)ns;
             if (sn > 0) {
                 StageTimer tm(c, g_timing, ST_SHADOW);
-                by_stack_class(c.sc.stack_class, [&](auto K) {
-                    k_shadow<decltype(K)::value><<<ceil_div(sn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, sn);
+                launch_trav(c, sn, [&](auto K, auto Lds, int grid, size_t shm) {
+                    k_shadow<decltype(K)::value, decltype(Lds)::value><<<grid, BLOCK, shm, sm>>>(c.sc, S, sn);
                 });
             }
             if (rn > 0) {
@@ -955,6 +1004,11 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         out[i].num_queries = queries[i];
     }
     c.stats.closest_queries += closest_q;
+    {
+        unsigned long long total_q = 0;
+        for (size_t i = 0; i < n_tasks; ++i) total_q += queries[i];
+        shadow_q = total_q - closest_q;  // per-slot query counters: 1 per closest + 1 per valid record
+    }
     c.stats.shadow_queries += shadow_q;
     c.stats.bounces += bounces;
     for (int k = 0; k < 2; ++k) {
@@ -1014,6 +1068,8 @@ lumo_status lumo_create(int device, void** ctx_out) {
         h.slot = -1;
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &h, sizeof(h));
     }
+    if (const char* e = std::getenv("LUMO_LDS")) g_lds = e[0] != '0';
+    if (const char* e = std::getenv("LUMO_LDS_GRID")) c->lds_grid_cap = std::max(1, std::atoi(e));
     const char* tm = std::getenv("LUMO_TIMING");
     g_timing = tm && tm[0] == '1';
     *ctx_out = c;
@@ -1074,6 +1130,36 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     s.n_onodes = d->num_object_nodes;
     s.n_lnodes = d->num_light_nodes;
     s.n_lights = d->num_lights;
+    {   // packed traversal set for LDS staging (scenes up to 48 KiB)
+        std::vector<char> hot;
+        auto put = [&](const void* p, size_t bytes) -> uint32_t {
+            const size_t off = (hot.size() + 15) & ~(size_t)15;
+            hot.resize(off + ((bytes + 15) & ~(size_t)15), 0);
+            if (bytes) std::memcpy(hot.data() + off, p, bytes);
+            return (uint32_t)off;
+        };
+        s.off_onodes = put(d->object_nodes, sizeof(lumo_bvh_node) * d->num_object_nodes);
+        s.off_oitems = put(d->object_items, sizeof(int32_t) * d->num_object_items);
+        s.off_lnodes = put(d->light_nodes, sizeof(lumo_bvh_node) * d->num_light_nodes);
+        s.off_litems = put(d->light_items, sizeof(int32_t) * d->num_light_items);
+        s.off_objs = put(d->objects, sizeof(lumo_object) * d->num_objects);
+        s.off_lights = put(d->lights, sizeof(lumo_object) * d->num_lights);
+        s.off_kd = put(d->kd_nodes, sizeof(lumo_kd_node) * d->num_kd_nodes);
+        s.off_kd_items = put(d->kd_items, sizeof(int32_t) * d->num_kd_items);
+        s.off_tris = put(d->triangles, sizeof(lumo_triangle) * d->num_triangles);
+        s.off_vertices = put(d->vertices, sizeof(double) * 3 * d->num_vertices);
+        s.hot_bytes = 0;
+        if (hot.size() <= 48 * 1024) {
+            const char* dp = nullptr;
+            chk(upload(*c, hot.data(), hot.size(), &dp));
+            if (st) {
+                free_scene(*c);
+                return st;
+            }
+            s.hot = dp;
+            s.hot_bytes = (uint32_t)hot.size();
+        }
+    }
     int n = d->num_lights, lg = 0;
     while (n > 1) {
         n >>= 1;
@@ -1219,6 +1305,7 @@ lumo_status lumo_stats_get(void* ctx, lumo_stats* stats) {
 }
 
 void lumo_set_timing(int on) { g_timing = on != 0; }
+void lumo_set_lds_staging(int on) { g_lds = on != 0; }
 
 lumo_status lumo_stats_reset(void* ctx) {
     Ctx* c = static_cast<Ctx*>(ctx);
