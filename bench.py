@@ -67,8 +67,9 @@ def main():
     scene = L.Scene.cornell_box()
     cam = L.Camera.cornell_box((args.res, args.res))
     tasks = L.make_tasks(args.res, args.res, args.spp, SEED)
-    tiles = ((args.res + 15) // 16) ** 2
-    mine = [t for i, t in enumerate(tasks) if (i % tiles) % ws == rank]
+    from lumo_amd.dist import shard_tasks, tiles_per_batch
+    tiles = tiles_per_batch(args.res, args.res)
+    mine = shard_tasks(tasks, args.res, args.res, rank, ws)
     mine_arr = (_ffi.TileTask * len(mine))(*mine)
 
     dev = L.Device(local)

@@ -256,6 +256,13 @@ void lumo_set_timing(int on);
 
 /* Test hook: render one task in the wavefront order and dump every path. */
 lumo_status lumo_debug_paths(void* ctx, const lumo_tile_task* task, lumo_path_dump* dump);
+/* Diagnostics: per-bounce record (20 doubles per bounce, at most 64 bounces) of the path of
+ * `pixel` in sample pass `pass` of `task`; *n_out = number of bounces recorded. */
+lumo_status lumo_debug_trace(void* ctx, const lumo_tile_task* task, int pass, int pixel, double* out,
+                             int* n_out);
+/* Perf switch: stage the packed scene in LDS inside the traversal kernels (default on; also
+ * LUMO_LDS=0 in the environment). */
+void lumo_set_lds_staging(int on);
 
 #ifdef __cplusplus
 }

@@ -64,6 +64,10 @@ int lumo_camera_build(const lumo_camera_params* p, lumo_camera_desc* out);
 int64_t lumo_make_tasks(int64_t width, int64_t height, uint64_t samples, uint64_t seed, lumo_tile_task* tasks,
                         int64_t cap);
 
+/* Test hook: evaluate the render path's deterministic transcendentals (lmath.h) on the host.
+ * which: 0 exp, 1 log1p, 2 cosh, 3 sin, 4 cos. */
+void lumo_lmath(int which, const double* x, double* y, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

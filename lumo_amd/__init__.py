@@ -139,6 +139,7 @@ class Scene:
         self.build()
         d = _ffi.SceneDesc()
         check(lib().lumo_scene_get_desc(self._flat, C.byref(d)), "scene desc")
+        d._owner = self  # the descriptor points into this scene's flat arrays
         return d
 
     def __del__(self):
@@ -263,11 +264,12 @@ class Device:
         self.ctx = ctx
         self.scene = None
 
-    def upload(self, scene, camera):
+    def upload(self, scene, camera=None):
         L = lib()
         self._scene_desc = scene.desc()
         check(L.lumo_scene_upload(self.ctx, C.byref(self._scene_desc)), "scene upload")
-        check(L.lumo_camera_set(self.ctx, C.byref(camera.desc)), "camera set")
+        if camera is not None:
+            check(L.lumo_camera_set(self.ctx, C.byref(camera.desc)), "camera set")
         self.scene = scene
 
     def render_tasks(self, tasks, max_paths=0):
@@ -284,6 +286,23 @@ class Device:
         cfg = _ffi.RenderCfg(0, 0, max_paths, 0)
         check(L.lumo_render_tiles(self.ctx, arr, n, C.byref(cfg), res), "render_tiles")
         return bufs, res
+
+    def trace(self, origins, dirs, lights=None):
+        """lumo_trace: closest hit (Scene::hit, scene.rs:119-147) of each ray, or with `lights`
+        the visibility of that light (Scene::hit_light, scene.rs:165-189).  Returns t, kind
+        (0 miss, 1 object, 2 light), object/light index, triangle index."""
+        n = len(origins)
+        o = np.ascontiguousarray(origins, dtype=np.float64).reshape(n, 3)
+        d = np.ascontiguousarray(dirs, dtype=np.float64).reshape(n, 3)
+        li = None if lights is None else np.ascontiguousarray(lights, dtype=np.int32)
+        rays = _ffi.RaySoA(o.ctypes.data_as(_ffi.c_double_p), d.ctypes.data_as(_ffi.c_double_p), None,
+                           None if li is None else li.ctypes.data_as(_ffi.c_int32_p))
+        t = np.zeros(n)
+        kind, obj, prim = (np.zeros(n, dtype=np.int32) for _ in range(3))
+        hits = _ffi.HitSoA(t.ctypes.data_as(_ffi.c_double_p), kind.ctypes.data_as(_ffi.c_int32_p),
+                           obj.ctypes.data_as(_ffi.c_int32_p), prim.ctypes.data_as(_ffi.c_int32_p))
+        check(lib().lumo_trace(self.ctx, C.byref(rays), n, C.byref(hits), int(li is not None)), "trace")
+        return t, kind, obj, prim
 
     def stats(self):
         s = _ffi.Stats()
@@ -339,8 +358,8 @@ class Renderer:
             self._seed = time.time_ns() & 0xFFFFFFFFFFFFFFFF or 1
         w, h = self.camera.resolution
         tasks = make_tasks(w, h, self._samples, self._seed)
-        tiles_per_batch = ((w + TILE_SIZE - 1) // TILE_SIZE) * ((h + TILE_SIZE - 1) // TILE_SIZE)
-        mine = [t for i, t in enumerate(tasks) if (i % tiles_per_batch) % world_size == rank]
+        from .dist import shard_tasks
+        mine = shard_tasks(tasks, w, h, rank, world_size)
         dev = Device(self._device)
         dev.upload(self.scene, self.camera)
         film = Film(w, h)

@@ -139,6 +139,7 @@ DEVICE_API = [
     ("lumo_stats_get", C.c_int32, [C.c_void_p, C.POINTER(Stats)]),
     ("lumo_stats_reset", C.c_int32, [C.c_void_p]),
     ("lumo_set_timing", None, [C.c_int]),
+    ("lumo_set_lds_staging", None, [C.c_int]),
     ("lumo_debug_trace", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.c_int, C.c_int, c_double_p, C.POINTER(C.c_int)]),
     ("lumo_debug_paths", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.POINTER(PathDump)]),
 ]
@@ -162,6 +163,7 @@ HOST_API = [
     ("lumo_camera_params_default", None, [C.POINTER(CameraParams)]),
     ("lumo_camera_params_cornell_box", None, [C.POINTER(CameraParams)]),
     ("lumo_camera_build", C.c_int32, [C.POINTER(CameraParams), C.POINTER(CameraDesc)]),
+    ("lumo_lmath", None, [C.c_int, c_double_p, c_double_p, C.c_int64]),
     ("lumo_make_tasks", C.c_int64, [C.c_int64, C.c_int64, C.c_uint64, C.c_uint64, C.POINTER(TileTask),
                                     C.c_int64]),
 ]

@@ -3,6 +3,7 @@
 #include <exception>
 
 #include "../../../include/lumo_host.h"
+#include "../common/lmath.h"
 #include "../common/rng.h"
 #include "rgb2spec.h"
 #include "scene.h"
@@ -158,6 +159,18 @@ int64_t lumo_make_tasks(int64_t width, int64_t height, uint64_t samples, uint64_
         }
     }
     return count;
+}
+
+void lumo_lmath(int which, const double* x, double* y, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) {
+        switch (which) {
+            case 0: y[i] = lm_exp(x[i]); break;
+            case 1: y[i] = lm_log1p(x[i]); break;
+            case 2: y[i] = lm_cosh(x[i]); break;
+            case 3: y[i] = lm_sin(x[i]); break;
+            default: y[i] = lm_cos(x[i]); break;
+        }
+    }
 }
 
 }  // extern "C"

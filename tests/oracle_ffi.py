@@ -8,6 +8,8 @@ from lumo_amd import _ffi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_PATH = os.path.join(ROOT, "oracle", "_build", "liblumo_oracle.so")
+# the same restatement built against the platform libm instead of lmath.h (sensitivity checks)
+ORACLE_GLIBC_PATH = os.path.join(ROOT, "oracle", "_build", "liblumo_oracle_glibc.so")
 
 WAVEFRONT, LUMO_ORDER = 0, 1
 
@@ -17,13 +19,13 @@ class Counters(C.Structure):
                 ("closest_queries", C.c_uint64), ("shadow_queries", C.c_uint64)]
 
 
-_lib = None
+_libs = {}
 
 
-def load():
-    global _lib
-    if _lib is None:
-        lib = C.CDLL(ORACLE_PATH)
+def load(path=None):
+    path = path or ORACLE_PATH
+    if path not in _libs:
+        lib = C.CDLL(path)
         lib.oracle_render_tiles.restype = C.c_int
         lib.oracle_render_tiles.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(_ffi.CameraDesc),
                                             C.POINTER(_ffi.TileTask), C.c_size_t, C.c_int, C.c_int,
@@ -35,13 +37,13 @@ def load():
         lib.oracle_trace.restype = C.c_int
         lib.oracle_trace.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(_ffi.RaySoA), C.c_size_t,
                                      C.POINTER(_ffi.HitSoA), C.c_int, C.POINTER(Counters)]
-        _lib = lib
-    return _lib
+        _libs[path] = lib
+    return _libs[path]
 
 
-def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1):
+def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path=None):
     """Returns (list of rgb_w arrays, results array, counters)."""
-    lib = load()
+    lib = load(path)
     n = len(tasks)
     arr = tasks if isinstance(tasks, C.Array) else (_ffi.TileTask * n)(*tasks)
     res = (_ffi.TileResult * n)()
@@ -58,8 +60,8 @@ def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1):
     return bufs, res, cnt
 
 
-def trace_paths(scene_desc, camera_desc, task):
-    lib = load()
+def trace_paths(scene_desc, camera_desc, task, path=None):
+    lib = load(path)
     P = (task.px_max[0] - task.px_min[0]) * (task.px_max[1] - task.px_min[1])
     m = P * task.samples
     rad, lam, ras = np.zeros(4 * m), np.zeros(4 * m), np.zeros(2 * m)

@@ -1,0 +1,71 @@
+"""GPU traversal parity: lumo_trace (closest hit = Scene::hit, visibility = Scene::hit_light)
+vs the oracle on the same rays.  Bar: bit-exact t, kind and object index."""
+import numpy as np
+import pytest
+
+import lumo_amd as L
+import oracle_ffi as O
+from test_oracle import disk_scene, sphere_points, unit_cube_scene
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    d = L.Device(0)
+    yield d
+    d.close()
+
+
+def _rays_in_box(n, seed):
+    rng = np.random.default_rng(seed)
+    o = rng.uniform([1, 1, 1], [555, 548, 558], size=(n, 3))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return o, d
+
+
+def _cmp(dev, scene, o, d, lights=None):
+    dev.upload(scene)
+    g = dev.trace(o, d, lights)
+    r = O.trace(scene.desc(), o, d, lights)
+    np.testing.assert_array_equal(g[0], r[0])
+    np.testing.assert_array_equal(g[1], r[1])
+    np.testing.assert_array_equal(g[2], r[2])
+    return g
+
+
+def test_closest_cornell(dev):
+    o, d = _rays_in_box(200000, 1)
+    t, kind, _, prim = _cmp(dev, L.Scene.cornell_box(), o, d)
+    assert np.mean(kind > 0) > 0.99  # closed box
+    assert np.all(prim[kind == 1] >= 0)
+
+
+def test_visibility_cornell(dev):
+    sc = L.Scene.cornell_box()
+    o, _ = _rays_in_box(100000, 2)
+    # aim at points on the light rectangle (cornell_box.rs: y = 548.8 ceiling light)
+    rng = np.random.default_rng(3)
+    tgt = np.stack([rng.uniform(213, 343, len(o)), np.full(len(o), 548.7), rng.uniform(227, 332, len(o))], 1)
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    t, kind, _, _ = _cmp(dev, sc, o, d, lights=np.zeros(len(o), dtype=np.int32))
+    assert 0.05 < np.mean(kind == 2) < 0.99
+
+
+def test_property_scenes(dev):
+    s = unit_cube_scene()
+    xo = sphere_points(10000, 3, 5.0)
+    xo = xo[xo[:, 1] > -0.1]
+    d = -xo / np.linalg.norm(xo, axis=1, keepdims=True)
+    _, kind, _, _ = _cmp(dev, s, xo, d)
+    assert np.all(kind == 1)
+    _cmp(dev, disk_scene(), np.array([(0.0, 0.0, 0.0), (0.0, 3.0, 0.0)]),
+         np.array([(0.0, 1.0, 0.0), (0.0, -1.0, 0.0)]), lights=np.array([0, 0]))
+
+
+def test_trace_rejects_bad_light(dev):
+    dev.upload(L.Scene.cornell_box())
+    with pytest.raises(Exception):
+        dev.trace(np.zeros((1, 3)), np.array([(0.0, 1.0, 0.0)]), lights=np.array([5]))
