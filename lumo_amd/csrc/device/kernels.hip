@@ -104,20 +104,6 @@ struct Dump {
 
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)); }
 
-// Wave64 stream compaction: every lane of the wave must call this.
-__device__ __forceinline__ void wave_append(bool pred, int32_t value, int32_t* queue, uint32_t* counter) {
-    const uint64_t mask = __ballot(pred);
-    if (mask == 0) return;
-    const int lane = lane_id();
-    const int leader = __ffsll((unsigned long long)mask) - 1;
-    const uint32_t prefix =
-        __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
-    base = __shfl(base, leader);
-    if (pred) queue[base + prefix] = value;
-}
-
 // Workgroup-aggregated stream compaction: ballot + mbcnt inside each wave, wave totals scanned
 // in LDS, ONE atomicAdd per workgroup on the queue counter (a single hot counter word
 // saturates near 88 M atomics/s on MI355X, MI355X_MICROARCH.md "dequeue").  Every thread of
@@ -665,7 +651,7 @@ struct Ctx {
 lumo_status dev_alloc(DevBuf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.bytes >= bytes) return LUMO_OK;
-    if (b.p) hipFree(b.p);
+    if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
     if (hipMalloc(&b.p, bytes) != hipSuccess) return LUMO_ERR_OOM;
@@ -686,7 +672,7 @@ lumo_status upload(Ctx& c, const T* host, size_t count, const T** dptr) {
 
 void free_scene(Ctx& c) {
     for (DevBuf& b : c.scene_bufs)
-        if (b.p) hipFree(b.p);
+        if (b.p) (void)hipFree(b.p);
     c.scene_bufs.clear();
     c.has_scene = false;
 }
@@ -1079,13 +1065,13 @@ lumo_status lumo_create(int device, void** ctx_out) {
 void lumo_destroy(void* ctx) {
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c) return;
-    hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
     free_scene(*c);
     for (DevBuf& b : c->work)
-        if (b.p) hipFree(b.p);
-    for (int i = 0; i < 2 * ST_COUNT; ++i) hipEventDestroy(c->ev[i]);
-    hipStreamDestroy(c->stream);
+        if (b.p) (void)hipFree(b.p);
+    for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventDestroy(c->ev[i]);
+    (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
