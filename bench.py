@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--max-paths", type=int, default=1 << 23, help="paths in flight per wavefront")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
-    ap.add_argument("--cpu-tile-stride", type=int, default=8, help="CPU sample: every k-th tile of each batch")
+    ap.add_argument("--cpu-tile-stride", type=int, default=32, help="CPU sample: every k-th tile of each batch")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -167,17 +167,22 @@ def roofline(st):
                   st.tri_tests[1] * B_TRI)
     else:
         nbytes = None
-    out = {"bound": "hbm", "kernel": f"k_{name}", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": pmc_traffic(name),
-           "stages": per_stage}
+    pmc = pmc_traffic(name)
+    out = {"bound": "hbm", "kernel": f"k_{name}", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "traffic": pmc.get("hbm_bytes_per_launch"), "traffic_raw": pmc.get("hbm_bytes_per_launch_raw"),
+           "traffic_source": "profiles/pmc_traffic.json" if pmc else None, "stages": per_stage}
     cq, sq = max(st.closest_queries, 1), max(st.shadow_queries, 1)
     out["per_query"] = {
         "closest": {"aabb": st.aabb_tests[0] / cq, "kd": st.kd_nodes[0] / cq, "tri": st.tri_tests[0] / cq},
         "shadow": {"aabb": st.aabb_tests[1] / sq, "kd": st.kd_nodes[1] / sq, "tri": st.tri_tests[1] / sq}}
     if nbytes is not None and ms[dom] > 0 and launches[dom] > 0:
         achieved = nbytes / (ms[dom] * 1e-3) / 1e9
+        avg_s = ms[dom] * 1e-3 / launches[dom]
         out.update({"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 5),
-                    "bytes_per_launch": nbytes / launches[dom],
-                    "avg_launch_us": ms[dom] * 1e3 / launches[dom]})
+                    "bytes_per_launch": nbytes / launches[dom], "avg_launch_us": avg_s * 1e6})
+        if out["traffic"]:
+            # measured DRAM-side rate of the same kernel: PMC bytes per launch over live launch time
+            out["hbm_gbs_measured"] = round(out["traffic"] / avg_s / 1e9, 2)
     else:
         out.update({"achieved": None, "frac": None})
     return out
@@ -189,9 +194,9 @@ def pmc_traffic(kernel):
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get(f"k_{kernel}", {}).get("hbm_bytes_per_launch")
+        return d.get(f"k_{kernel}", {})
     except (OSError, ValueError):
-        return None
+        return {}
 
 
 def cpu_baseline(scene, cam, tasks, tiles, args):

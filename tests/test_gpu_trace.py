@@ -38,7 +38,7 @@ def _cmp(dev, scene, o, d, lights=None):
 def test_closest_cornell(dev):
     o, d = _rays_in_box(200000, 1)
     t, kind, _, prim = _cmp(dev, L.Scene.cornell_box(), o, d)
-    assert np.mean(kind > 0) > 0.99  # closed box
+    assert np.mean(kind > 0) > 0.8  # the box is open towards the camera (z = 0)
     assert np.all(prim[kind == 1] >= 0)
 
 

@@ -1,0 +1,28 @@
+"""Copy a tools/profile.sh run into profiles/<round>/ and refresh profiles/pmc_traffic.json
+(HBM bytes per launch per kernel, read by bench.py's roofline).
+Usage: python tools/update_traffic.py gpurun_out/prof/<tag> <round>"""
+import json
+import os
+import shutil
+import sys
+
+src, rnd = sys.argv[1], sys.argv[2]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+dst = os.path.join(ROOT, "profiles", rnd)
+os.makedirs(dst, exist_ok=True)
+summary = json.load(open(os.path.join(src, "summary.json")))
+shutil.copy(os.path.join(src, "summary.json"), os.path.join(dst, "rocprof_summary.json"))
+shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+for name in ("bench_trace.json", "bench_fetch.json", "bench_write.json"):
+    p = os.path.join(src, name)
+    if os.path.exists(p):
+        shutil.copy(p, os.path.join(dst, name.replace("bench_", "bench_under_rocprof_")))
+out = {"source": f"profiles/{rnd}/rocprof_summary.json (tools/profile.sh: separate FETCH_SIZE and WRITE_SIZE "
+                  "passes, no traces)",
+       "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE counts half of wide coalesced reads, "
+                     "MI355X_MICROARCH.md HBM section); raw = FETCH_SIZE + WRITE_SIZE. Bytes per launch."}
+for k, v in summary.items():
+    if k.startswith("k_") and "hbm_bytes_per_launch" in v:
+        out[k] = {kk: v[kk] for kk in ("hbm_bytes_per_launch", "hbm_bytes_per_launch_raw", "avg_us", "launches")}
+json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1, sort_keys=True)
+print("updated", dst)
