@@ -47,10 +47,11 @@ enum {
     LUMO_MAT_BLANK = 0,
     LUMO_MAT_LAMBERTIAN = 1,   /* BxDF::Lambertian (bxdf/scatter.rs:3-27)          */
     LUMO_MAT_LIGHT = 2,        /* Material::Light (material.rs:15, 223-234)         */
-    LUMO_MAT_MF_DIFFUSE = 3,   /* BxDF::MfDiffuse   (not yet on the GPU path)       */
-    LUMO_MAT_MF_CONDUCTOR = 4, /* BxDF::MfConductor (not yet on the GPU path)       */
-    LUMO_MAT_MF_DIELECTRIC = 5 /* BxDF::MfDielectric(not yet on the GPU path)       */
+    LUMO_MAT_MF_DIFFUSE = 3,   /* BxDF::MfDiffuse    (bxdf/microfacet.rs:120-199)    */
+    LUMO_MAT_MF_CONDUCTOR = 4, /* BxDF::MfConductor  (bxdf/microfacet.rs:62-118)     */
+    LUMO_MAT_MF_DIELECTRIC = 5 /* BxDF::MfDielectric (bxdf/microfacet.rs:201-374)    */
 };
+enum { LUMO_MATF_CONSTANT_ETA = 1 /* DenseSpectrum::is_constant of eta (no dispersion) */ };
 
 typedef struct {
     int32_t kind;       /* LUMO_MAT_*                                           */
@@ -58,10 +59,10 @@ typedef struct {
     int32_t illuminant; /* Light: index into dense_spectra                       */
     int32_t eta_idx;    /* microfacet: dense_spectra index of eta                */
     int32_t k_idx;      /* microfacet: dense_spectra index of k                  */
-    int32_t pad0;
+    int32_t flags;      /* LUMO_MATF_*                                           */
     double scale;       /* Light: emission scale                                 */
     double roughness;   /* microfacet: max(roughness, 1e-5)                      */
-    lumo_spectrum albedo; /* Lambertian spectrum / Light texture / kd             */
+    lumo_spectrum albedo; /* Lambertian spectrum / Light texture / microfacet kd  */
     lumo_spectrum ks;
     lumo_spectrum tf;
 } lumo_material;

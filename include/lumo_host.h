@@ -25,6 +25,15 @@ void lumo_builder_free(void* b);
 int lumo_builder_material_lambertian(void* b, lumo_spectrum spec);
 /* Material::Light(texture, illuminant, scale, two_sided); illuminant = builtin dense id */
 int lumo_builder_material_light(void* b, lumo_spectrum tex, int illuminant, double scale, int two_sided);
+/* Microfacet materials (material.rs:26-187).  Return the material index, or -1 on invalid
+ * parameters (roughness outside [0, 1]). */
+int lumo_builder_material_microfacet(void* b, double roughness, double eta, double k, int is_transparent,
+                                     int fresnel_enabled, lumo_spectrum kd, lumo_spectrum ks, lumo_spectrum tf);
+int lumo_builder_material_diffuse(void* b, lumo_spectrum kd);
+int lumo_builder_material_metal(void* b, lumo_spectrum ks, double roughness, double eta, double k);
+int lumo_builder_material_transparent(void* b, lumo_spectrum tf, double roughness, double eta);
+int lumo_builder_material_mirror(void* b);
+int lumo_builder_material_glass(void* b);
 /* TriangleMesh::new: vertices (nv x 3), faces as concatenated index lists with sizes. */
 int lumo_builder_add_mesh(void* b, const double* vertices, int64_t nv, const int64_t* face_idx,
                           const int64_t* face_sizes, int64_t nfaces, int material, int as_light);
@@ -33,6 +42,9 @@ int lumo_builder_add_rectangle(void* b, const double* a, const double* bb, const
                                int as_light);
 /* Scene::cornell_box() */
 void* lumo_builder_cornell_box(void);
+/* Scene::empty_box(def_color, mat_left, mat_right) (scene/empty_box.rs:16-97) added to builder b;
+ * mat_left / mat_right are material indices returned by b.  Returns LUMO_OK or LUMO_ERR_INVALID. */
+int lumo_builder_empty_box(void* b, lumo_spectrum def_color, int mat_left, int mat_right);
 /* Scene::build + flatten; returns an owning flat scene (free with lumo_scene_free). */
 void* lumo_builder_build(void* b);
 int lumo_scene_get_desc(void* scene, lumo_scene_desc* out);
@@ -65,7 +77,7 @@ int64_t lumo_make_tasks(int64_t width, int64_t height, uint64_t samples, uint64_
                         int64_t cap);
 
 /* Test hook: evaluate the render path's deterministic transcendentals (lmath.h) on the host.
- * which: 0 exp, 1 log1p, 2 cosh, 3 sin, 4 cos. */
+ * which: 0 exp, 1 log1p, 2 cosh, 3 sin, 4 cos, 5 atan. */
 void lumo_lmath(int which, const double* x, double* y, int64_t n);
 
 #ifdef __cplusplus

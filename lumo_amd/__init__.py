@@ -61,7 +61,21 @@ class Spectrum:
         return self._s.scale == 0.0
 
 
-Spectrum.WHITE = None  # filled lazily (needs the library)
+    @staticmethod
+    def black():
+        return Spectrum(_ffi.Spectrum(0.0, 0.0, 0.0, 0.0))
+
+
+# spectrum.rs:22-38 constants, built on first use (they need the library's rgb2spec table)
+_NAMED = {"WHITE": (1.0, 1.0, 1.0), "RED": (1.0, 0.0, 0.0), "GREEN": (0.0, 1.0, 0.0), "BLUE": (0.0, 0.0, 1.0),
+          "YELLOW": (1.0, 1.0, 0.0), "MAGENTA": (1.0, 0.0, 1.0), "CYAN": (0.0, 1.0, 1.0)}
+
+
+def named_spectrum(name):
+    """Spectrum::WHITE / BLACK / RED / GREEN / BLUE / YELLOW / MAGENTA / CYAN."""
+    if name == "BLACK":
+        return Spectrum.black()
+    return Spectrum.from_rgb(*_NAMED[name])
 
 
 class Material:
@@ -78,10 +92,53 @@ class Material:
         """Material::Light(texture, illuminant, scale, two_sided); Material::light uses D65."""
         return Material("light", spec=tex, illuminant=illuminant, scale=scale, two_sided=two_sided)
 
+    @staticmethod
+    def microfacet(roughness, eta, k, is_transparent, fresnel_enabled, kd, ks, tf):
+        """Material::microfacet (material.rs:26-68), solid-colour textures."""
+        return Material("microfacet", roughness=roughness, eta=eta, k=k, is_transparent=is_transparent,
+                        fresnel_enabled=fresnel_enabled, kd=kd, ks=ks, tf=tf)
+
+    @staticmethod
+    def diffuse(kd):
+        """Material::diffuse: MfDiffuse, roughness 1 (material.rs:94-115)."""
+        return Material("diffuse", kd=kd)
+
+    @staticmethod
+    def metal(ks, roughness, eta, k):
+        """Material::metal: MfConductor (material.rs:71-91)."""
+        return Material("metal", ks=ks, roughness=roughness, eta=eta, k=k)
+
+    @staticmethod
+    def transparent(tf, roughness, eta):
+        """Material::transparent: MfDielectric (material.rs:123-143)."""
+        return Material("transparent", tf=tf, roughness=roughness, eta=eta)
+
+    @staticmethod
+    def mirror():
+        return Material("mirror")
+
+    @staticmethod
+    def glass():
+        return Material("glass")
+
     def _add(self, b):
         L = lib()
+        k = self.kw
         if self.kind == "lambertian":
-            return L.lumo_builder_material_lambertian(b, self.kw["spec"]._s)
+            return L.lumo_builder_material_lambertian(b, k["spec"]._s)
+        if self.kind == "microfacet":
+            return L.lumo_builder_material_microfacet(b, k["roughness"], k["eta"], k["k"], int(k["is_transparent"]),
+                                                      int(k["fresnel_enabled"]), k["kd"]._s, k["ks"]._s, k["tf"]._s)
+        if self.kind == "diffuse":
+            return L.lumo_builder_material_diffuse(b, k["kd"]._s)
+        if self.kind == "metal":
+            return L.lumo_builder_material_metal(b, k["ks"]._s, k["roughness"], k["eta"], k["k"])
+        if self.kind == "transparent":
+            return L.lumo_builder_material_transparent(b, k["tf"]._s, k["roughness"], k["eta"])
+        if self.kind == "mirror":
+            return L.lumo_builder_material_mirror(b)
+        if self.kind == "glass":
+            return L.lumo_builder_material_glass(b)
         ill = self.kw["illuminant"]
         ill = DENSE[ill] if isinstance(ill, str) else int(ill)
         return L.lumo_builder_material_light(b, self.kw["spec"]._s, ill, float(self.kw["scale"]),
@@ -99,6 +156,15 @@ class Scene:
     @staticmethod
     def cornell_box():
         return Scene(lib().lumo_builder_cornell_box())
+
+    @staticmethod
+    def empty_box(def_color, mat_left, mat_right):
+        """Scene::empty_box (scene/empty_box.rs): 2 x 1.6 x 2 box centred at (0, 0, -1), one
+        small ceiling light, MfDiffuse floor / roof / front wall of `def_color`."""
+        s = Scene()
+        ml, mr = s._mat(mat_left), s._mat(mat_right)
+        check(lib().lumo_builder_empty_box(s._b, def_color._s, ml, mr), "empty_box")
+        return s
 
     def _mat(self, m):
         idx = m._add(self._b)

@@ -26,7 +26,7 @@ class Spectrum(C.Structure):
 
 class Material(C.Structure):
     _fields_ = [("kind", C.c_int32), ("two_sided", C.c_int32), ("illuminant", C.c_int32),
-                ("eta_idx", C.c_int32), ("k_idx", C.c_int32), ("pad0", C.c_int32),
+                ("eta_idx", C.c_int32), ("k_idx", C.c_int32), ("flags", C.c_int32),
                 ("scale", C.c_double), ("roughness", C.c_double),
                 ("albedo", Spectrum), ("ks", Spectrum), ("tf", Spectrum)]
 
@@ -153,6 +153,14 @@ HOST_API = [
     ("lumo_builder_free", None, [C.c_void_p]),
     ("lumo_builder_material_lambertian", C.c_int, [C.c_void_p, Spectrum]),
     ("lumo_builder_material_light", C.c_int, [C.c_void_p, Spectrum, C.c_int, C.c_double, C.c_int]),
+    ("lumo_builder_material_microfacet", C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_double, C.c_int, C.c_int,
+                                                   Spectrum, Spectrum, Spectrum]),
+    ("lumo_builder_material_diffuse", C.c_int, [C.c_void_p, Spectrum]),
+    ("lumo_builder_material_metal", C.c_int, [C.c_void_p, Spectrum, C.c_double, C.c_double, C.c_double]),
+    ("lumo_builder_material_transparent", C.c_int, [C.c_void_p, Spectrum, C.c_double, C.c_double]),
+    ("lumo_builder_material_mirror", C.c_int, [C.c_void_p]),
+    ("lumo_builder_material_glass", C.c_int, [C.c_void_p]),
+    ("lumo_builder_empty_box", C.c_int, [C.c_void_p, Spectrum, C.c_int, C.c_int]),
     ("lumo_builder_add_mesh", C.c_int, [C.c_void_p, c_double_p, C.c_int64, c_int64_p, c_int64_p, C.c_int64,
                                         C.c_int, C.c_int]),
     ("lumo_builder_add_rectangle", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p, C.c_int, C.c_int]),

@@ -1,4 +1,4 @@
-// Deterministic f64 transcendentals for the render path (exp, log1p, cosh, sin, cos).
+// Deterministic f64 transcendentals for the render path (exp, log1p, cosh, sin, cos, atan2).
 //
 // lumo calls Rust std (`f64::exp/cos/sin/cosh`, `atanh` = 0.5*ln_1p(..)), i.e. the platform
 // libm.  Device libm (ROCm ocml) and glibc differ by an ulp on some inputs, and in the Cornell
@@ -205,6 +205,106 @@ LUMO_HD double lm_cos(double x) {
         case 1: return -lm_ksin(y0, y1);
         case 2: return -lm_kcos(y0, y1);
         default: return lm_ksin(y0, y1);
+    }
+}
+
+// musl / fdlibm s_atan.c (the Rust `libm` crate that lumo's Complex::arg calls is a musl port)
+LUMO_HD double lm_atan(double x) {
+    const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
+                              1.57079632679489655800e+00};
+    const double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
+                              6.12323399573676603587e-17};
+    const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+                 aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+                 aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+                 aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+                 aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+                 aT10 = 1.62858201153657823623e-02;
+    const uint64_t bits = f64_bits(x);
+    const uint32_t ix = (uint32_t)(bits >> 32) & 0x7fffffffu;
+    const bool neg = (bits >> 63) != 0;
+    int id;
+    if (ix >= 0x44100000u) {  // |x| >= 2^66
+        if (x != x) return x;
+        const double z = atanhi[3] + atanlo[3];
+        return neg ? -z : z;
+    }
+    if (ix < 0x3fdc0000u) {          // |x| < 0.4375
+        if (ix < 0x3e400000u) return x;  // |x| < 2^-27
+        id = -1;
+    } else {
+        x = fabs(x);
+        if (ix < 0x3ff30000u) {    // |x| < 1.1875
+            if (ix < 0x3fe60000u) {  // 7/16 <= |x| < 11/16
+                id = 0;
+                x = (2.0 * x - 1.0) / (2.0 + x);
+            } else {  // 11/16 <= |x| < 19/16
+                id = 1;
+                x = (x - 1.0) / (x + 1.0);
+            }
+        } else if (ix < 0x40038000u) {  // |x| < 2.4375
+            id = 2;
+            x = (x - 1.5) / (1.0 + 1.5 * x);
+        } else {
+            id = 3;
+            x = -1.0 / x;
+        }
+    }
+    const double z = x * x;
+    const double w = z * z;
+    const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    const double r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return neg ? -r : r;
+}
+
+// musl e_atan2.c
+LUMO_HD double lm_atan2(double y, double x) {
+    const double pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16;
+    if (x != x || y != y) return x + y;
+    const uint64_t bx = f64_bits(x), by = f64_bits(y);
+    const uint32_t ix = (uint32_t)(bx >> 32), lx = (uint32_t)bx;
+    const uint32_t iy = (uint32_t)(by >> 32), ly = (uint32_t)by;
+    if (((ix - 0x3ff00000u) | lx) == 0) return lm_atan(y);  // x = 1.0
+    const uint32_t m = ((iy >> 31) & 1u) | ((ix >> 30) & 2u);  // 2*sign(x) + sign(y)
+    const uint32_t ax = ix & 0x7fffffffu, ay = iy & 0x7fffffffu;
+    if ((ay | ly) == 0) {  // y = 0
+        switch (m) {
+            case 0:
+            case 1: return y;
+            case 2: return pi;
+            default: return -pi;
+        }
+    }
+    if ((ax | lx) == 0) return (m & 1u) ? -pi / 2 : pi / 2;  // x = 0
+    if (ax == 0x7ff00000u) {                                   // x = inf
+        if (ay == 0x7ff00000u) {
+            switch (m) {
+                case 0: return pi / 4;
+                case 1: return -pi / 4;
+                case 2: return 3 * pi / 4;
+                default: return -3 * pi / 4;
+            }
+        }
+        switch (m) {
+            case 0: return 0.0;
+            case 1: return -0.0;
+            case 2: return pi;
+            default: return -pi;
+        }
+    }
+    if (ax + (64u << 20) < ay || ay == 0x7ff00000u) return (m & 1u) ? -pi / 2 : pi / 2;  // |y/x| > 2^64
+    double z;
+    if ((m & 2u) && ay + (64u << 20) < ax)
+        z = 0.0;  // |y/x| < 2^-64, x < 0
+    else
+        z = lm_atan(fabs(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return -z;
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
     }
 }
 

@@ -112,6 +112,11 @@ __device__ __forceinline__ DColor operator+(DColor a, const DColor& b) {
     for (int i = 0; i < NS; ++i) a.s[i] = a.s[i] + b.s[i];
     return a;
 }
+__device__ __forceinline__ DColor operator-(DColor a, const DColor& b) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) a.s[i] = a.s[i] - b.s[i];
+    return a;
+}
 __device__ __forceinline__ DColor operator*(DColor a, const DColor& b) {
 #pragma unroll
     for (int i = 0; i < NS; ++i) a.s[i] = a.s[i] * b.s[i];
@@ -533,7 +538,7 @@ __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit
     return true;
 }
 
-// ---------------------------------------------------------------- materials (Lambertian + Light)
+// ---------------------------------------------------------------- materials
 struct Onb {
     V3 u, v, w;
 };
@@ -546,30 +551,303 @@ __device__ __forceinline__ Onb onb_new(V3 w) {  // onb.rs:19-39
 __device__ __forceinline__ V3 onb_world(const Onb& o, V3 v) { return v.x * o.u + v.y * o.v + v.z * o.w; }
 __device__ __forceinline__ V3 onb_local(const Onb& o, V3 v) { return V3{dot(v, o.u), dot(v, o.v), dot(v, o.w)}; }
 
-__device__ __forceinline__ bool bsdf_sample(const lumo_material& m, const DHit& h, V3 wo, V2 sq, V3& wi) {
-    if (m.kind != LUMO_MAT_LAMBERTIAN) return false;
-    const Onb uvw = onb_new(h.ns);
-    if (h.backface) return false;  // reflection BxDF on the back face (bxdf.rs:112-114)
-    wi = onb_world(uvw, square_to_cos_hemisphere(sq));
+// GGX microfacet model (microfacet.rs) evaluated in the shading frame (Z = ns).
+struct Mf {
+    double a;  // roughness (isotropic: roughness.x == roughness.y)
+    const double* eta;
+    const double* k;
+};
+__device__ __forceinline__ Mf mf_of(const DScene& sc, const lumo_material& m) {
+    return Mf{m.roughness, sc.dense + 95 * m.eta_idx, sc.dense + 95 * m.k_idx};
+}
+__device__ __forceinline__ bool mf_delta(const Mf& d) { return (d.a + d.a) / 2.0 < 1e-3; }
+__device__ __forceinline__ bool mf_specular(const Mf& d) { return (d.a + d.a) / 2.0 < 0.01; }
+__device__ __forceinline__ double sq(double x) { return x * x; }
+__device__ __forceinline__ double pow5(double x) {
+    const double x2 = x * x;
+    const double x4 = x2 * x2;
+    return x * x4;
+}
+__device__ __forceinline__ double clampd(double x, double lo, double hi) {
+    if (x < lo) x = lo;
+    if (x > hi) x = hi;
+    return x;
+}
+__device__ __forceinline__ double schlick(double f0, double f90, double c) { return f0 + (f90 - f0) * pow5(1.0 - c); }
+// cos/sin of the azimuth (spherical_utils.rs)
+__device__ __forceinline__ void cs_phi(V3 w, double& cp, double& sp) {
+    const double st = sqrt(rmax(1.0 - w.z * w.z, 0.0));
+    cp = st == 0.0 ? 1.0 : clampd(w.x / st, -1.0, 1.0);
+    sp = st == 0.0 ? 0.0 : clampd(w.y / st, -1.0, 1.0);
+}
+__device__ __forceinline__ double tan2_theta(V3 w) { return rmax(1.0 - w.z * w.z, 0.0) / (w.z * w.z); }
+__device__ __forceinline__ bool is_inf(double x) { return x == DINF || x == -DINF; }
+__device__ double mf_D(const Mf& d, V3 wh) {
+    const double tan2 = tan2_theta(wh);
+    if (is_inf(tan2)) return 0.0;
+    const double cos4 = sq(wh.z * wh.z);
+    if (cos4 < EPSILON * EPSILON) return 0.0;
+    double cp, sp;
+    cs_phi(wh, cp, sp);
+    const double e = tan2 * (sq(cp / d.a) + sq(sp / d.a));
+    return 1.0 / (PI * (d.a * d.a) * cos4 * sq(1.0 + e));
+}
+__device__ double mf_Lambda(const Mf& d, V3 w) {
+    const double tan2 = tan2_theta(w);
+    if (is_inf(tan2)) return 0.0;
+    double cp, sp;
+    cs_phi(w, cp, sp);
+    const double alpha2 = sq(d.a * cp) + sq(d.a * sp);
+    return (sqrt(rmax(1.0 + alpha2 * tan2, 0.0)) - 1.0) / 2.0;
+}
+__device__ __forceinline__ bool chi(V3 wo, V3 wh) { return rsignum(wh.z) * dot(wo, wh) * wo.z > EPSILON; }
+__device__ __forceinline__ double mf_G(const Mf& d, V3 wo, V3 wi, V3 wh) {
+    return chi(wo, wh) ? 1.0 / (1.0 + mf_Lambda(d, wo) + mf_Lambda(d, wi)) : 0.0;
+}
+__device__ __forceinline__ double mf_G1(const Mf& d, V3 wo, V3 wh) {
+    return chi(wo, wh) ? 1.0 / (1.0 + mf_Lambda(d, wo)) : 0.0;
+}
+__device__ __forceinline__ double mf_normal_pdf(const Mf& d, V3 wh, V3 wo) {
+    return rmax(mf_G1(d, wo, wh) * mf_D(d, wh) * fabs(dot(wh, wo)) / fabs(wo.z), 0.0);
+}
+__device__ V3 mf_sample_normal(const Mf& d, V3 wo, V2 u) {  // Heitz 2018 visible normals
+    V3 ws = normalize(V3{wo.x * d.a, wo.y * d.a, wo.z});
+    if (ws.z < 0.0) ws = -ws;
+    const V3 t1 = (1.0 - ws.z < EPSILON) ? V3{1.0, 0.0, 0.0} : normalize(cross(ws, V3{0.0, 0.0, 1.0}));
+    const V3 t2 = cross(t1, ws);
+    const double r = sqrt(u.x);
+    const double theta = 2.0 * PI * u.y;
+    const double x = r * lm_cos(theta);
+    const double h = sqrt(rmax(1.0 - x * x, 0.0));
+    const double lerp = (1.0 + ws.z) / 2.0;
+    const double y = (1.0 - lerp) * h + lerp * r * lm_sin(theta);
+    const V3 wm{x, y, sqrt(rmax(1.0 - x * x - y * y, 0.0))};
+    const V3 w = wm.x * t1 + wm.y * t2 + wm.z * ws;
+    return normalize(V3{d.a * w.x, d.a * w.y, rmax(w.z, EPSILON)});
+}
+// Fresnel (microfacet.rs:258-311): real index, or conductor with complex index eta + ik
+__device__ double fresnel_real(V3 wo, V3 wh, double eta) {
+    double c = dot(wo, wh);
+    const double e = c < 0.0 ? 1.0 / eta : eta;
+    c = fabs(c);
+    const double sin2_i = (1.0 - c * c) / (e * e);
+    if (sin2_i >= 1.0) return 1.0;
+    const double ci = sqrt(rmax(1.0 - sin2_i, 0.0));
+    const double rpa = (e * c - ci) / (e * c + ci);
+    const double rpe = (c - e * ci) / (c + e * ci);
+    return (rpa * rpa + rpe * rpe) / 2.0;
+}
+struct Cx {
+    double re, im;
+};
+__device__ __forceinline__ Cx cmul(Cx a, Cx b) { return Cx{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+__device__ __forceinline__ double cnorm2(Cx a) { return a.re * a.re + a.im * a.im; }
+__device__ __forceinline__ Cx cdivf(Cx a, double v) { return v == 0.0 ? Cx{NAN, NAN} : Cx{a.re / v, a.im / v}; }
+__device__ __forceinline__ Cx cdiv(Cx a, Cx b) {  // complex.rs: a * conj(b) / |b|^2
+    if (b.re == 0.0 && b.im == 0.0) return Cx{NAN, NAN};
+    return cdivf(cmul(a, Cx{b.re, -b.im}), cnorm2(b));
+}
+__device__ double fresnel_complex(V3 wo, V3 wh, double n, double k) {
+    const Cx eta{n, k};
+    const double c = clampd(dot(wo, wh), 0.0, 1.0);
+    const double sin2_o = 1.0 - c * c;
+    const Cx e2 = cmul(eta, eta);
+    const Cx sin2_i = (e2.re == 0.0 && e2.im == 0.0)
+                          ? Cx{NAN, NAN}
+                          : cdivf(Cx{sin2_o * e2.re, sin2_o * -e2.im}, cnorm2(e2));
+    const Cx z{1.0 - sin2_i.re, -sin2_i.im};
+    const double rn = sqrt(sqrt(cnorm2(z)));
+    const double half = lm_atan2(z.im, z.re) / 2.0;
+    const Cx ci{rn * lm_cos(half), rn * lm_sin(half)};
+    const Cx ec{eta.re * c, eta.im * c};
+    const Cx rpa = cdiv(Cx{ec.re - ci.re, ec.im - ci.im}, Cx{ec.re + ci.re, ec.im + ci.im});
+    const Cx eci = cmul(eta, ci);
+    const Cx rpe = cdiv(Cx{c - eci.re, -eci.im}, Cx{c + eci.re, eci.im});
+    return (cnorm2(rpa) + cnorm2(rpe)) / 2.0;
+}
+__device__ double fresnel_at(const Mf& d, V3 wo, V3 wh, double wl) {
+    const double eta = dense_one(d.eta, wl);
+    const double k = dense_one(d.k, wl);
+    if (k == 0.0) return eta == 0.0 ? 0.0 : fresnel_real(wo, wh, eta);
+    return fresnel_complex(wo, wh, eta, k);
+}
+__device__ __forceinline__ DColor fresnel(const Mf& d, V3 wo, V3 wh, const double* L) {
+    DColor c;
+    for (int i = 0; i < NS; ++i) c.s[i] = fresnel_at(d, wo, wh, L[i]);
+    return c;
+}
+__device__ __forceinline__ bool reflect_about(V3 wo, V3 n, V3& wi) {
+    const V3 w = 2.0 * (n * dot(wo, n) / length_squared(n)) - wo;
+    if (!(w.z * wo.z > 0.0)) return false;
+    wi = w;
     return true;
 }
-__device__ __forceinline__ double bsdf_pdf(const lumo_material& m, const DHit& h, V3 wo, V3 wi) {
-    if (m.kind != LUMO_MAT_LAMBERTIAN) return 0.0;
+__device__ __forceinline__ bool refract_about(double eta, V3 wo, V3 no, V3& wi) {
+    const bool flip = dot(no, wo) < 0.0;
+    const double cos_to = flip ? -dot(no, wo) : dot(no, wo);
+    const double er = flip ? 1.0 / eta : eta;
+    const V3 n = flip ? -no : no;
+    const double sin2_ti = (1.0 - cos_to * cos_to) / (er * er);
+    if (sin2_ti >= 1.0) return false;
+    const double cos_ti = sqrt(rmax(1.0 - sin2_ti, 0.0));
+    const V3 w = -wo / er + (cos_to / er - cos_ti) * n;
+    if (w.z * wo.z > 0.0) return false;
+    wi = w;
+    return true;
+}
+__device__ DColor reflect_coeff(const Mf& d, V3 wo, V3 wi, const double* L) {
+    const V3 wh = normalize(wi + wo);
+    return mf_D(d, wh) * fresnel(d, wo, wh, L) * mf_G(d, wo, wi, wh) / (4.0 * fabs(wo.z) * fabs(wi.z));
+}
+__device__ __forceinline__ double cos_hemisphere_pdf(V3 wo, V3 wi) {
+    if (!(wo.z * wi.z > 0.0)) return 0.0;
+    return wi.z > 0.0 ? wi.z / PI : 0.0;
+}
+__device__ __forceinline__ bool standard_kind(int k) {
+    return k == LUMO_MAT_LAMBERTIAN || k == LUMO_MAT_MF_DIFFUSE || k == LUMO_MAT_MF_CONDUCTOR ||
+           k == LUMO_MAT_MF_DIELECTRIC;
+}
+
+// Material::bsdf_sample (material.rs:273-289 -> bsdf.rs -> bxdf.rs:104-124); may terminate L
+__device__ bool bsdf_sample(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, double* L,
+                            double rand_u, V2 rs, V3& wi) {
+    if (!standard_kind(m.kind)) return false;
+    const Onb uvw = onb_new(h.ns);
+    const V3 o = onb_local(uvw, wo);
+    if (h.backface && m.kind != LUMO_MAT_MF_DIELECTRIC) return false;
+    V3 w;
+    if (m.kind == LUMO_MAT_LAMBERTIAN) {
+        w = square_to_cos_hemisphere(rs);
+    } else {
+        const Mf d = mf_of(sc, m);
+        if (m.kind == LUMO_MAT_MF_DIFFUSE) {
+            const double pr = schlick(0.04, 1.0, o.z);
+            const double ps = 1.0 - pr;
+            if (rand_u < pr / (pr + ps)) {
+                if (!reflect_about(o, mf_delta(d) ? V3{0.0, 0.0, 1.0} : mf_sample_normal(d, o, rs), w)) return false;
+            } else {
+                w = square_to_cos_hemisphere(rs);
+            }
+        } else if (m.kind == LUMO_MAT_MF_CONDUCTOR) {
+            if (mf_delta(d)) {
+                w = V3{-o.x, -o.y, o.z};
+            } else if (!reflect_about(o, mf_sample_normal(d, o, rs), w)) {
+                return false;
+            }
+        } else {
+            if (!(m.flags & LUMO_MATF_CONSTANT_ETA)) {  // ColorWavelength::terminate
+                L[1] = 0.0;
+                L[2] = 0.0;
+                L[3] = 0.0;
+            }
+            const double wl = L[0];
+            const double eta = dense_one(d.eta, wl);
+            const V3 wh = (eta == 1.0 || mf_delta(d)) ? V3{0.0, 0.0, 1.0} : mf_sample_normal(d, o, rs);
+            const double pr = fresnel_at(d, o, wh, wl);
+            const double pt = 1.0 - pr;
+            const bool ok = rand_u < pr / (pr + pt) ? reflect_about(o, wh, w) : refract_about(eta, o, wh, w);
+            if (!ok) return false;
+        }
+    }
+    wi = onb_world(uvw, w);
+    return true;
+}
+// Material::bsdf_pdf (material.rs:292-306 -> bsdf.rs:70-84 -> bxdf.rs:127-150)
+__device__ double bsdf_pdf(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, V3 wi, const double* L) {
+    if (!standard_kind(m.kind)) return 0.0;
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
     const Onb uvw = onb_new(h.ns);
-    const V3 wol = onb_local(uvw, wo), wil = onb_local(uvw, wi);
-    if (!reflection) return 0.0;
-    if (!(wol.z * wil.z > 0.0)) return 0.0;
-    return wil.z > 0.0 ? wil.z / PI : 0.0;
+    const V3 o = onb_local(uvw, wo), i = onb_local(uvw, wi);
+    if (!reflection && m.kind != LUMO_MAT_MF_DIELECTRIC) return 0.0;
+    if (m.kind == LUMO_MAT_LAMBERTIAN) return cos_hemisphere_pdf(o, i);
+    const Mf d = mf_of(sc, m);
+    if (m.kind == LUMO_MAT_MF_DIFFUSE) {
+        if (!(i.z * o.z > 0.0)) return 0.0;
+        const V3 wh = normalize(o + i);
+        const double pr = schlick(0.04, 1.0, o.z);
+        const double ps = 1.0 - pr;
+        const double p_ref = mf_delta(d) ? (1.0 - wh.z < EPSILON ? 1.0 : 0.0)
+                                         : mf_normal_pdf(d, wh, o) / (4.0 * fabs(dot(o, wh)));
+        return pr * p_ref + ps * cos_hemisphere_pdf(o, i);
+    }
+    if (m.kind == LUMO_MAT_MF_CONDUCTOR) {
+        if (!(i.z * o.z > 0.0)) return 0.0;
+        V3 wh = normalize(o + i);
+        if (wh.z < 0.0) wh = -wh;
+        if (mf_delta(d)) return 1.0 - wh.z < EPSILON ? 1.0 : 0.0;
+        return mf_normal_pdf(d, wh, o) / (4.0 * fabs(dot(o, wh)));
+    }
+    const double wl = L[0];
+    const double eta = dense_one(d.eta, wl);
+    const double er = reflection ? 1.0 : (o.z < 0.0 ? 1.0 / eta : eta);
+    V3 wh = eta == 1.0 ? V3{0.0, 0.0, 1.0} : normalize(o + i * er);
+    if (wh.z < 0.0) wh = -wh;
+    const double hwo = dot(o, wh), hwi = dot(i, wh);
+    if (hwo == 0.0 || hwi == 0.0) return 0.0;
+    if (hwo * o.z < 0.0 || hwi * i.z < 0.0) return 0.0;
+    const double pr = fresnel_at(d, o, wh, wl);
+    const double pt = 1.0 - pr;
+    const bool flat = eta == 1.0 || mf_delta(d);
+    if (reflection && flat) return 1.0 - wh.z < EPSILON ? pr / (pr + pt) : 0.0;
+    if (reflection) return mf_normal_pdf(d, wh, o) / (4.0 * fabs(hwo)) * pr / (pr + pt);
+    if (flat) return 1.0 - wh.z < EPSILON ? pt / (pr + pt) : 0.0;
+    return mf_normal_pdf(d, wh, o) * fabs(hwi) / sq(hwi + hwo / er) * pt / (pr + pt);
 }
-__device__ __forceinline__ DColor bsdf_f(const lumo_material& m, const DHit& h, V3 wo, V3 wi, const double* L) {
-    if (m.kind != LUMO_MAT_LAMBERTIAN) return cfill(0.0);
+// Material::bsdf_f, Transport::Radiance (material.rs:254-270 -> bsdf.rs:28-48 -> bxdf.rs:71-100)
+__device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, V3 wi, const double* L) {
+    if (!standard_kind(m.kind)) return cfill(0.0);
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
-    if (!reflection || h.backface) return cfill(0.0);
-    return spec_sample(m.albedo, L) / PI;
+    const Onb uvw = onb_new(h.ns);
+    const V3 o = onb_local(uvw, wo), i = onb_local(uvw, wi);
+    if ((!reflection || h.backface) && m.kind != LUMO_MAT_MF_DIELECTRIC) return cfill(0.0);
+    if (m.kind == LUMO_MAT_LAMBERTIAN) return spec_sample(m.albedo, L) / PI;
+    const Mf d = mf_of(sc, m);
+    if (m.kind == LUMO_MAT_MF_DIFFUSE) {
+        const V3 wh = normalize(o + i);
+        const DColor F = fresnel(d, o, wh, L);
+        const DColor fr = mf_D(d, wh) * F * mf_G(d, o, i, wh) / (4.0 * fabs(o.z) * fabs(i.z));
+        // Disney diffuse with Frostbite renormalisation (microfacet.rs:164-179)
+        const double r2 = sq(d.a);
+        const double fd90 = 0.5 * r2 + 2.0 * sq(wh.z) * r2;
+        const double fd = schlick(1.0, fd90, o.z) * schlick(1.0, fd90, i.z) * (1.0 + r2 * (1.0 / 1.51 - 1.0));
+        return fr * spec_sample(m.ks, L) + spec_sample(m.albedo, L) * (cfill(1.0) - F) * fd / PI;
+    }
+    if (m.kind == LUMO_MAT_MF_CONDUCTOR) {
+        const DColor ks = spec_sample(m.ks, L);
+        if (mf_delta(d)) return ks * fresnel(d, o, V3{0.0, 0.0, 1.0}, L) / fabs(i.z);
+        return ks * reflect_coeff(d, o, i, L);
+    }
+    const double eta = dense_one(d.eta, L[0]);
+    const double er = reflection ? 1.0 : (o.z < 0.0 ? 1.0 / eta : eta);
+    const bool flat = eta == 1.0 || mf_delta(d);
+    V3 wh = flat ? V3{0.0, 0.0, 1.0} : normalize(i * er + o);
+    if (reflection) {
+        const DColor ks = spec_sample(m.ks, L);
+        if (flat) return ks * fresnel(d, o, wh, L) / fabs(i.z);
+        return ks * reflect_coeff(d, o, i, L);
+    }
+    const DColor F = fresnel(d, o, wh, L);
+    if (wh.z < 0.0) wh = -wh;
+    const double scale = er * er;
+    const DColor tf = spec_sample(m.tf, L);
+    if (flat) return tf * (cfill(1.0) - F) / (scale * fabs(i.z));
+    const double hwo = dot(wh, o), hwi = dot(wh, i);
+    return tf * mf_D(d, wh) * (cfill(1.0) - F) * mf_G(d, o, i, wh) / scale * fabs(hwi * hwo / (i.z * o.z)) /
+           sq(er * hwi + hwo);
 }
 __device__ __forceinline__ double shading_cosine(const lumo_material& m, V3 wi, V3 ns) {
-    return (m.kind == LUMO_MAT_LIGHT || m.kind == LUMO_MAT_BLANK) ? 1.0 : fabs(dot(ns, wi));
+    return standard_kind(m.kind) ? fabs(dot(ns, wi)) : 1.0;
+}
+__device__ __forceinline__ bool mat_is_specular(const lumo_material& m) {  // bxdf.rs:33-40
+    if (m.kind == LUMO_MAT_MF_DIELECTRIC) return true;
+    if (m.kind == LUMO_MAT_MF_CONDUCTOR) return (m.roughness + m.roughness) / 2.0 < 0.01;
+    return false;
+}
+__device__ __forceinline__ bool mat_is_delta(const DScene& sc, const lumo_material& m, const double* L) {
+    if (m.kind == LUMO_MAT_MF_CONDUCTOR) return (m.roughness + m.roughness) / 2.0 < 1e-3;
+    if (m.kind == LUMO_MAT_MF_DIELECTRIC)
+        return (m.roughness + m.roughness) / 2.0 < 1e-3 || dense_one(sc.dense + 95 * m.eta_idx, L[0]) == 1.0;
+    return false;
 }
 __device__ __forceinline__ DColor emit(const DScene& sc, const lumo_material& m, const double* L, bool backface) {
     if (m.kind != LUMO_MAT_LIGHT) return cfill(0.0);
@@ -585,7 +863,7 @@ __device__ __forceinline__ int sample_light(const DScene& sc, double u) {
     const double fr = rfract(x);
     return fr < sc.alias_prob[idx] ? idx : sc.alias_idx[idx];
 }
-__device__ __forceinline__ V3 light_sample_towards(const lumo_object& L, V3 xo, V2 rs) {
+__device__ __forceinline__ V3 light_sample_towards(const DScene& sc, const lumo_object& L, V3 xo, V2 rs) {
     const V3 xi = ld3(L.origin) + rs.x * ld3(L.b0) + rs.y * ld3(L.b1);
     return normalize(xi - xo);
 }

@@ -310,16 +310,18 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
             DColor gathered = ldc(S.gath, s);
             DColor radiance = ldc(S.rad, s);
             const V3 wo = -ro.d;
-            (void)xs_float(rng);  // rand_u (unused by Lambertian, drawn in order)
+            const double rand_u = xs_float(rng);
             const V2 sq = xs_vec2(rng);
             V3 wi;
-            if (!bsdf_sample(m, ho, wo, sq, wi)) {
+            if (!bsdf_sample(sc, m, ho, wo, L, rand_u, sq, wi)) {
                 if (S.flags[s] & 1u) radiance = radiance + gathered * emit(sc, m, L, ho.backface);
                 stc(S.rad, s, radiance);
             } else {
+                if (m.kind == LUMO_MAT_MF_DIELECTRIC && !(m.flags & LUMO_MATF_CONSTANT_ETA)) {
+                    for (int i = 1; i < NS; ++i) S.lam[4 * s + i] = 0.0;  // lambda terminated
+                }
                 // NEE: n_shadow x [light pick, light direction, BSDF sample] (integrator.rs:87-137)
-                const bool delta_mat = false;  // Lambertian / Light
-                if (!delta_mat) {
+                if (!mat_is_delta(sc, m, L)) {
                     const int base = s * 2 * ns;
                     for (int i = 0; i < ns; ++i) {
                         const int li = sample_light(sc, xs_float(rng));
@@ -327,29 +329,29 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
                         S.pdf_l[s * ns + i] = sc.alias_pdf[li];
                         {
                             const V2 rs = xs_vec2(rng);
-                            const V3 w = light_sample_towards(Lo, ho.p, rs);
+                            const V3 w = light_sample_towards(sc, Lo, ho.p, rs);
                             const Ray ri = spawn(ho, w);
                             const int rec = base + 2 * i;
                             stv3(S.sh_o, rec, ri.o);
                             stv3(S.sh_d, rec, ri.d);
-                            stc(S.sh_f, rec, bsdf_f(m, ho, wo, w, L));
-                            S.sh_psct[rec] = bsdf_pdf(m, ho, wo, w);
+                            stc(S.sh_f, rec, bsdf_f(sc, m, ho, wo, w, L));
+                            S.sh_psct[rec] = bsdf_pdf(sc, m, ho, wo, w, L);
                             S.sh_cos[rec] = shading_cosine(m, w, ho.ns);
                             S.sh_light[rec] = li;
                             S.sh_flags[rec] = 1 | 2;  // valid | light-sampled
                             n_sh++;
                         }
                         {
-                            (void)xs_float(rng);
+                            const double ru = xs_float(rng);
                             const V2 rsq = xs_vec2(rng);
                             V3 w;
                             const int rec = base + 2 * i + 1;
-                            if (bsdf_sample(m, ho, wo, rsq, w)) {
+                            if (bsdf_sample(sc, m, ho, wo, L, ru, rsq, w)) {
                                 const Ray ri = spawn(ho, w);
                                 stv3(S.sh_o, rec, ri.o);
                                 stv3(S.sh_d, rec, ri.d);
-                                stc(S.sh_f, rec, bsdf_f(m, ho, wo, w, L));
-                                S.sh_psct[rec] = bsdf_pdf(m, ho, wo, w);
+                                stc(S.sh_f, rec, bsdf_f(sc, m, ho, wo, w, L));
+                                S.sh_psct[rec] = bsdf_pdf(sc, m, ho, wo, w, L);
                                 S.sh_cos[rec] = shading_cosine(m, w, ho.ns);
                                 S.sh_light[rec] = li;
                                 S.sh_flags[rec] = 1;
@@ -365,9 +367,9 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
                 // spawn the continuation (path_trace.rs:42-77)
                 const Ray ri = spawn(ho, wi);
                 const V3 wi2 = ri.d;
-                const double p_scatter = bsdf_pdf(m, ho, wo, wi2);
+                const double p_scatter = bsdf_pdf(sc, m, ho, wo, wi2, L);
                 if (p_scatter > 0.0) {
-                    const DColor bsdf = bsdf_f(m, ho, wo, wi2, L);
+                    const DColor bsdf = bsdf_f(sc, m, ho, wo, wi2, L);
                     gathered = gathered * (bsdf * shading_cosine(m, wi2, ho.ns) / p_scatter);
                     bool cont = true;
                     const uint32_t depth = S.depth[s];
@@ -380,7 +382,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
                             gathered = gathered / rr_prob;
                     }
                     if (cont) {
-                        S.flags[s] = 0u;  // last_specular = is_specular() = false (Lambertian)
+                        S.flags[s] = mat_is_specular(m) ? 1u : 0u;  // last_specular
                         S.depth[s] = depth + 1;
                         stv3(S.ro, s, ri.o);
                         stv3(S.rd, s, ri.d);

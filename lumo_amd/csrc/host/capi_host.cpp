@@ -38,6 +38,32 @@ int lumo_builder_material_light(void* b, lumo_spectrum tex, int illuminant, doub
     if (illuminant < 0 || illuminant >= DENSE_BUILTIN_COUNT) return -1;
     return static_cast<SceneBuilder*>(b)->add_material(material_light(tex, illuminant, scale, two_sided != 0));
 }
+int lumo_builder_material_microfacet(void* b, double roughness, double eta, double k, int is_transparent,
+                                     int fresnel_enabled, lumo_spectrum kd, lumo_spectrum ks, lumo_spectrum tf) {
+    HostMaterial h;
+    if (!material_microfacet(roughness, eta, k, is_transparent != 0, fresnel_enabled != 0, kd, ks, tf, h)) return -1;
+    return static_cast<SceneBuilder*>(b)->add_material(h);
+}
+int lumo_builder_material_diffuse(void* b, lumo_spectrum kd) {
+    return static_cast<SceneBuilder*>(b)->add_material(material_diffuse(kd));
+}
+int lumo_builder_material_metal(void* b, lumo_spectrum ks, double roughness, double eta, double k) {
+    HostMaterial h;
+    if (!material_microfacet(roughness, eta, k, false, true, spectrum_from_rgb(1.0, 1.0, 1.0), ks,
+                             lumo_spectrum{0.0f, 0.0f, 0.0f, 0.0f}, h))
+        return -1;
+    return static_cast<SceneBuilder*>(b)->add_material(h);
+}
+int lumo_builder_material_transparent(void* b, lumo_spectrum tf, double roughness, double eta) {
+    HostMaterial h;
+    if (!material_microfacet(roughness, eta, 0.0, true, true, lumo_spectrum{0.0f, 0.0f, 0.0f, 0.0f},
+                             spectrum_from_rgb(1.0, 1.0, 1.0), tf, h))
+        return -1;
+    return static_cast<SceneBuilder*>(b)->add_material(h);
+}
+int lumo_builder_material_mirror(void* b) { return static_cast<SceneBuilder*>(b)->add_material(material_mirror()); }
+int lumo_builder_material_glass(void* b) { return static_cast<SceneBuilder*>(b)->add_material(material_glass()); }
+
 int lumo_builder_add_mesh(void* b, const double* vertices, int64_t nv, const int64_t* face_idx,
                           const int64_t* face_sizes, int64_t nfaces, int material, int as_light) {
     SceneBuilder* sb = static_cast<SceneBuilder*>(b);
@@ -68,6 +94,13 @@ int lumo_builder_add_rectangle(void* b, const double* a, const double* bb, const
     return LUMO_OK;
 }
 void* lumo_builder_cornell_box(void) { return new SceneBuilder(SceneBuilder::cornell_box()); }
+int lumo_builder_empty_box(void* b, lumo_spectrum def_color, int mat_left, int mat_right) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    const int n = (int)sb->materials.size();
+    if (!sb || mat_left < 0 || mat_left >= n || mat_right < 0 || mat_right >= n) return LUMO_ERR_INVALID;
+    sb->empty_box(def_color, mat_left, mat_right);
+    return LUMO_OK;
+}
 
 void* lumo_builder_build(void* b) {
     try {
@@ -168,6 +201,7 @@ void lumo_lmath(int which, const double* x, double* y, int64_t n) {
             case 1: y[i] = lm_log1p(x[i]); break;
             case 2: y[i] = lm_cosh(x[i]); break;
             case 3: y[i] = lm_sin(x[i]); break;
+            case 5: y[i] = lm_atan(x[i]); break;
             default: y[i] = lm_cos(x[i]); break;
         }
     }

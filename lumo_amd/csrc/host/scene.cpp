@@ -503,6 +503,58 @@ HostMaterial material_light(lumo_spectrum tex, int illuminant_builtin, double sc
     return h;
 }
 
+bool material_microfacet(double roughness, double eta, double k, bool is_transparent, bool fresnel_enabled,
+                         lumo_spectrum kd, lumo_spectrum ks, lumo_spectrum tf, HostMaterial& out) {
+    if (!(roughness >= 0.0 && roughness <= 1.0)) return false;  // microfacet.rs:31 assert
+    HostMaterial h;
+    h.m.kind = is_transparent ? LUMO_MAT_MF_DIELECTRIC : (fresnel_enabled ? LUMO_MAT_MF_CONDUCTOR : LUMO_MAT_MF_DIFFUSE);
+    h.m.illuminant = -1;
+    h.m.roughness = rmax(roughness, 1e-5);
+    h.m.albedo = kd;
+    h.m.ks = ks;
+    h.m.tf = tf;
+    h.eta_const = eta;
+    if (is_transparent && eta == 1.5) h.eta_builtin = DENSE_GLASS_ETA;
+    if (is_transparent && eta == 2.5) h.eta_builtin = DENSE_DIAMOND_ETA;
+    h.k_const = k;
+    out = h;
+    return true;
+}
+namespace {
+lumo_spectrum spec_white() { return spectrum_from_rgb(1.0, 1.0, 1.0); }
+lumo_spectrum spec_black() { return lumo_spectrum{0.0f, 0.0f, 0.0f, 0.0f}; }
+}  // namespace
+HostMaterial material_diffuse(lumo_spectrum kd) {
+    HostMaterial h;
+    material_microfacet(1.0, 1.5, 0.0, false, false, kd, spec_white(), spec_black(), h);
+    return h;
+}
+HostMaterial material_metal(lumo_spectrum ks, double roughness, double eta, double k) {
+    HostMaterial h;
+    if (!material_microfacet(roughness, eta, k, false, true, spec_white(), ks, spec_black(), h))
+        throw std::runtime_error("metal: roughness outside [0, 1]");
+    return h;
+}
+HostMaterial material_transparent(lumo_spectrum tf, double roughness, double eta) {
+    HostMaterial h;
+    if (!material_microfacet(roughness, eta, 0.0, true, true, spec_black(), spec_white(), tf, h))
+        throw std::runtime_error("transparent: roughness outside [0, 1]");
+    return h;
+}
+HostMaterial material_mirror() {
+    HostMaterial h;
+    material_microfacet(0.0, 0.0, 0.0, false, true, spec_black(), spec_white(), spec_black(), h);
+    h.eta_builtin = DENSE_MIRROR_ETA;
+    h.k_builtin = DENSE_MIRROR_K;
+    return h;
+}
+HostMaterial material_glass() {
+    HostMaterial h;
+    material_microfacet(0.0, 1.5, 0.0, true, true, spec_black(), spec_white(), spec_white(), h);
+    h.eta_builtin = DENSE_GLASS_ETA;
+    return h;
+}
+
 int SceneBuilder::add_material(const HostMaterial& m) {
     materials.push_back(m);
     return (int)materials.size() - 1;
@@ -641,6 +693,22 @@ SceneBuilder SceneBuilder::cornell_box() {
     return s;
 }
 
+void SceneBuilder::empty_box(lumo_spectrum def_color, int mat_left, int mat_right) {
+    const double ground = -0.8, ceiling = 0.8, right = 1.0, left = -1.0, front = -2.0, back = 0.0;
+    const double l_dim = 0.1, eps = 0.001;  // Scene::LIGHT_EPS
+    const int light_m = add_material(material_light(spectrum_from_srgb(252, 201, 138), DENSE_D65, 1.0, false));
+    add_rectangle(V3{-l_dim, ceiling - eps, 0.6 * front + l_dim}, V3{-l_dim, ceiling - eps, 0.6 * front - l_dim},
+                  V3{l_dim, ceiling - eps, 0.6 * front - l_dim}, light_m, true);
+    add_rectangle(V3{left, ground, back}, V3{left, ground, front}, V3{left, ceiling, front}, mat_left, false);
+    add_rectangle(V3{right, ground, front}, V3{right, ground, back}, V3{right, ceiling, back}, mat_right, false);
+    const int floor_m = add_material(material_diffuse(def_color));
+    add_rectangle(V3{left, ground, back}, V3{right, ground, back}, V3{right, ground, front}, floor_m, false);
+    const int roof_m = add_material(material_diffuse(def_color));
+    add_rectangle(V3{left, ceiling, front}, V3{right, ceiling, front}, V3{right, ceiling, back}, roof_m, false);
+    const int front_m = add_material(material_diffuse(def_color));
+    add_rectangle(V3{left, ground, front}, V3{right, ground, front}, V3{right, ceiling, front}, front_m, false);
+}
+
 lumo_scene_desc FlatScene::desc() const {
     lumo_scene_desc d{};
     d.num_vertices = (int32_t)(vertices.size() / 3);
@@ -720,7 +788,27 @@ std::unique_ptr<FlatScene> build_scene(const SceneBuilder& sb) {
     // dense spectra: builtins first (indices = DenseId)
     for (int i = 0; i < DENSE_BUILTIN_COUNT; ++i)
         for (int k = 0; k < DENSE; ++k) fs->dense.push_back(builtin_dense(i).v[k]);
-    for (const HostMaterial& hm : sb.materials) fs->materials.push_back(hm.m);
+    // microfacet eta / k: builtin curves by id, constants appended once each
+    std::vector<double> consts;
+    auto dense_const = [&](double v) -> int32_t {
+        for (size_t i = 0; i < consts.size(); ++i)
+            if (consts[i] == v || (consts[i] != consts[i] && v != v)) return (int32_t)(DENSE_BUILTIN_COUNT + i);
+        consts.push_back(v);
+        for (int k = 0; k < DENSE; ++k) fs->dense.push_back(v);
+        return (int32_t)(DENSE_BUILTIN_COUNT + consts.size() - 1);
+    };
+    for (const HostMaterial& hm : sb.materials) {
+        lumo_material m = hm.m;
+        if (m.kind == LUMO_MAT_MF_DIFFUSE || m.kind == LUMO_MAT_MF_CONDUCTOR || m.kind == LUMO_MAT_MF_DIELECTRIC) {
+            m.eta_idx = hm.eta_builtin >= 0 ? hm.eta_builtin : dense_const(hm.eta_const);
+            m.k_idx = hm.k_builtin >= 0 ? hm.k_builtin : dense_const(hm.k_const);
+            const double* e = fs->dense.data() + (size_t)DENSE * m.eta_idx;
+            bool constant = true;
+            for (int k = 1; k < DENSE; ++k) constant = constant && e[k] == e[0];
+            m.flags = constant ? LUMO_MATF_CONSTANT_ETA : 0;
+        }
+        fs->materials.push_back(m);
+    }
 
     auto flatten_objects = [&](const std::vector<HostObject>& src, std::vector<lumo_object>& dst,
                                std::vector<V3>& bmins, std::vector<V3>& bmaxs) {

@@ -20,10 +20,23 @@ struct HostMaterial {
     const Dense* illum = nullptr;  // light illuminant (dense)
     Dense illum_owned;
     bool has_owned = false;
+    // microfacet eta / k: a builtin dense spectrum (>= 0) or DenseSpectrum::from_constant
+    int eta_builtin = -1, k_builtin = -1;
+    double eta_const = 0.0, k_const = 0.0;
 };
 
 HostMaterial material_lambertian(lumo_spectrum spec);
 HostMaterial material_light(lumo_spectrum tex, int illuminant_builtin, double scale, bool two_sided);
+// Material::microfacet (material.rs:26-68): GGX; MfDielectric if transparent, else MfConductor
+// if Fresnel is enabled, else MfDiffuse.  Transparent eta 1.5 / 2.5 use the glass / diamond
+// dispersion curves.  Returns false for roughness outside [0, 1].
+bool material_microfacet(double roughness, double eta, double k, bool is_transparent, bool fresnel_enabled,
+                         lumo_spectrum kd, lumo_spectrum ks, lumo_spectrum tf, HostMaterial& out);
+HostMaterial material_diffuse(lumo_spectrum kd);                                        // material.rs:94-115
+HostMaterial material_metal(lumo_spectrum ks, double roughness, double eta, double k);  // :71-91
+HostMaterial material_transparent(lumo_spectrum tf, double roughness, double eta);      // :123-143
+HostMaterial material_mirror();                                                          // :146-165
+HostMaterial material_glass();                                                           // :168-187
 
 struct Face {
     std::vector<int64_t> vidx, nidx, tidx;
@@ -73,6 +86,9 @@ class SceneBuilder {
 
     // Scene::cornell_box (scene/cornell_box.rs:8-193)
     static SceneBuilder cornell_box();
+    // Scene::empty_box (scene/empty_box.rs:16-97) added to this builder; mat_left / mat_right
+    // are material indices of this builder.
+    void empty_box(lumo_spectrum def_color, int mat_left, int mat_right);
 };
 
 // Owning flattened scene; desc() points into the vectors.

@@ -11,7 +11,8 @@
  *   integrator.rs, path_trace.rs      path tracing with NEE + MIS + Russian roulette
  *   scene.rs, object/{bvh,kdtree,triangle,rectangle,aabb}.rs  traversal + intersection
  *   hit.rs, ray.rs, onb.rs, efloat.rs robust spawning, shading frame
- *   material.rs, bsdf.rs, bxdf.rs, bxdf/scatter.rs  Lambertian + Light
+ *   material.rs, bsdf.rs, bxdf.rs, bxdf/{scatter,microfacet}.rs, microfacet.rs
+ *                                    Lambertian, MfDiffuse, MfConductor, MfDielectric, Light
  *   color/{color,wavelength,spectrum,dense_spectrum,xyz,space}.rs  hero wavelengths
  *   camera.rs, film.rs, film/tile.rs, filter.rs, tone_mapping.rs
  *
@@ -59,6 +60,18 @@ int oracle_debug_trace(const lumo_scene_desc* scene, const lumo_camera_desc* cam
 /* Scene::hit (any_hit = 0) or Scene::hit_light (any_hit != 0) for a batch of rays. */
 int oracle_trace(const lumo_scene_desc* scene, const lumo_ray_soa* rays, size_t n,
                  lumo_hit_soa* hits, int any_hit, oracle_counters* counters);
+
+/* BSDF probes at a surface point with ns = ng = +Z (front face), in world = shading space.
+ * oracle_bsdf_sample: n samples of bsdf_sample(wo, lambda(u0), rand_u, rand_sq) with rng
+ *   Xorshift::new(seed); ok[i] = 0 when the sample is None.
+ * oracle_bsdf_eval: pdf and f (4 wavelengths of lambda4) for each wi.
+ * oracle_furnace: white_furnace_tests.rs furnace_sample: mean f*cos/pdf over n samples. */
+int oracle_bsdf_sample(const lumo_scene_desc* scene, int material, const double* wo, const double* lambda4,
+                       size_t n, uint64_t seed, double* wi3, int* ok);
+int oracle_bsdf_eval(const lumo_scene_desc* scene, int material, const double* wo, const double* lambda4,
+                     const double* wi3, size_t n, double* pdf, double* f4);
+int oracle_furnace(const lumo_scene_desc* scene, int material, const double* wo, size_t n, uint64_t seed,
+                   double* out4);
 
 #ifdef __cplusplus
 }

@@ -11,10 +11,16 @@
 #define O_LOG1P std::log1p
 #define O_COSH std::cosh
 #define O_EXP std::exp
+#define O_ATAN2 std::atan2
+#define O_COS std::cos
+#define O_SIN std::sin
 #else
 #define O_LOG1P lumo::lm_log1p
 #define O_COSH lumo::lm_cosh
 #define O_EXP lumo::lm_exp
+#define O_ATAN2 lumo::lm_atan2
+#define O_COS lumo::lm_cos
+#define O_SIN lumo::lm_sin
 #endif
 
 #include <algorithm>
@@ -56,6 +62,10 @@ Color operator+(Color a, Color b) {
 }
 Color operator*(Color a, Color b) {
     for (int i = 0; i < NS; ++i) a.s[i] = a.s[i] * b.s[i];
+    return a;
+}
+Color operator-(Color a, const Color& b) {
+    for (int i = 0; i < NS; ++i) a.s[i] = a.s[i] - b.s[i];
     return a;
 }
 Color operator*(Color a, double v) {
@@ -489,45 +499,404 @@ Onb onb_new(V3 w) {  // onb.rs:19-39 (Duff et al.)
 V3 onb_to_world(const Onb& o, V3 v) { return v.x * o.u + v.y * o.v + v.z * o.w; }
 V3 onb_to_local(const Onb& o, V3 v) { return V3{dot(v, o.u), dot(v, o.v), dot(v, o.w)}; }
 
-bool is_reflection_bxdf(int kind) { return kind != LUMO_MAT_MF_DIELECTRIC; }
+// ---- spherical utilities (math/spherical_utils.rs), Z = shading normal
+double sph_cos2(V3 w) { return w.z * w.z; }
+double sph_sin2(V3 w) { return rmax(1.0 - sph_cos2(w), 0.0); }
+double sph_sin(V3 w) { return std::sqrt(sph_sin2(w)); }
+double sph_tan2(V3 w) { return sph_sin2(w) / sph_cos2(w); }
+double rclamp(double x, double lo, double hi) {  // f64::clamp
+    if (x < lo) x = lo;
+    if (x > hi) x = hi;
+    return x;
+}
+double sph_cos_phi(V3 w) {
+    const double st = sph_sin(w);
+    return st == 0.0 ? 1.0 : rclamp(w.x / st, -1.0, 1.0);
+}
+double sph_sin_phi(V3 w) {
+    const double st = sph_sin(w);
+    return st == 0.0 ? 0.0 : rclamp(w.y / st, -1.0, 1.0);
+}
+bool same_hemisphere(V3 v, V3 u) { return v.z * u.z > 0.0; }
+double powi2(double x) { return x * x; }
+double powi5(double x) {  // f64::powi(x, 5): square-and-multiply
+    const double x2 = x * x;
+    const double x4 = x2 * x2;
+    return x * x4;
+}
+V3 project_onto(V3 v, V3 n) { return n * dot(v, n) / length_squared(n); }  // vec3.rs:134-136
 
-// material.rs:273-289 -> bsdf.rs:51-67 -> bxdf.rs:104-124
-bool bsdf_sample(const Scene& sc, const Hit& h, V3 wo, double rand_u, V2 rand_sq, V3* wi) {
-    (void)rand_u;
-    const lumo_material& m = mat(sc, h.material);
-    if (m.kind != LUMO_MAT_LAMBERTIAN) return false;  // Light / Blank -> None
-    const Onb uvw = onb_new(h.ns);
-    (void)onb_to_local(uvw, wo);
-    if (h.backface && is_reflection_bxdf(m.kind)) return false;
-    *wi = onb_to_world(uvw, square_to_cos_hemisphere(rand_sq));
+// ---- complex numbers (math/complex.rs)
+struct Cx {
+    double re, im;
+};
+Cx cx_mul(Cx a, Cx b) { return Cx{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+Cx cx_scale(Cx a, double v) { return Cx{a.re * v, a.im * v}; }
+double cx_norm_sqr(Cx a) { return a.re * a.re + a.im * a.im; }
+Cx cx_co(Cx a) { return Cx{a.re, -a.im}; }
+Cx cx_div_f(Cx a, double v) {
+    if (v == 0.0) return Cx{NAN, NAN};
+    return Cx{a.re / v, a.im / v};
+}
+Cx cx_div(Cx a, Cx b) {
+    if (b.re == 0.0 && b.im == 0.0) return Cx{NAN, NAN};
+    return cx_div_f(cx_mul(a, cx_co(b)), cx_norm_sqr(b));
+}
+Cx f_div_cx(double a, Cx b) {  // Float / Complex
+    if (b.re == 0.0 && b.im == 0.0) return Cx{NAN, NAN};
+    return cx_div_f(Cx{a * cx_co(b).re, a * cx_co(b).im}, cx_norm_sqr(b));
+}
+Cx cx_sqrt(Cx a) {
+    const double norm = std::sqrt(cx_norm_sqr(a));
+    const double arg = O_ATAN2(a.im, a.re);
+    return Cx{std::sqrt(norm) * O_COS(arg / 2.0), std::sqrt(norm) * O_SIN(arg / 2.0)};
+}
+
+// ---- microfacet distribution (microfacet.rs); MfDistribution::new always builds GGX
+struct Mfd {
+    double rx, ry;
+    const double* eta;
+    const double* k;
+    bool constant_eta;
+    lumo_spectrum kd, ks, tf;
+};
+Mfd mfd_of(const Scene& sc, const lumo_material& m) {
+    return Mfd{m.roughness, m.roughness, sc.dense(m.eta_idx), sc.dense(m.k_idx), (m.flags & LUMO_MATF_CONSTANT_ETA) != 0,
+               m.albedo, m.ks, m.tf};
+}
+bool mfd_is_specular(const Mfd& d) { return (d.rx + d.ry) / 2.0 < 0.01; }   // microfacet.rs:73-77
+bool mfd_is_delta(const Mfd& d) { return (d.rx + d.ry) / 2.0 < 1e-3; }      // :80-84
+double eta_at(const Mfd& d, double wl) { return dense_one(d.eta, wl); }
+double k_at(const Mfd& d, double wl) { return dense_one(d.k, wl); }
+double f_schlick(double f0, double f90, double c) { return f0 + (f90 - f0) * powi5(1.0 - c); }
+
+double disney_diffuse(const Mfd& d, double cwo, double cwi, double cwh) {  // :164-179
+    const double r2 = powi2(d.rx);
+    const double energy_bias = 0.5 * r2;
+    const double fd90 = energy_bias + 2.0 * powi2(cwh) * r2;
+    const double view = f_schlick(1.0, fd90, cwo);
+    const double light = f_schlick(1.0, fd90, cwi);
+    const double energy_factor = 1.0 + r2 * (1.0 / 1.51 - 1.0);
+    return view * light * energy_factor;
+}
+double mf_d(const Mfd& d, V3 wh) {  // :189-213 (GGX)
+    const double tan2 = sph_tan2(wh);
+    if (std::isinf(tan2)) return 0.0;
+    const double cos4 = powi2(sph_cos2(wh));
+    if (cos4 < EPSILON * EPSILON) return 0.0;
+    const double cp = sph_cos_phi(wh), sp = sph_sin_phi(wh);
+    const double alpha2 = d.rx * d.ry;
+    const double e = tan2 * (powi2(cp / d.rx) + powi2(sp / d.ry));
+    return 1.0 / (PI * alpha2 * cos4 * powi2(1.0 + e));
+}
+double fr_real(V3 wo, V3 wh, double eta) {  // :291-311
+    double cos_o = dot(wo, wh);
+    const bool inside = cos_o < 0.0;
+    const double e = inside ? 1.0 / eta : eta;
+    cos_o = fabs(cos_o);
+    const double sin2_o = 1.0 - cos_o * cos_o;
+    const double sin2_i = sin2_o / (e * e);
+    if (sin2_i >= 1.0) return 1.0;
+    const double cos_i = std::sqrt(rmax(1.0 - sin2_i, 0.0));
+    const double r_par = (e * cos_o - cos_i) / (e * cos_o + cos_i);
+    const double r_per = (cos_o - e * cos_i) / (cos_o + e * cos_i);
+    return (r_par * r_par + r_per * r_per) / 2.0;
+}
+double fr_complex(V3 wo, V3 wh, double eta_re, double k) {  // :275-289
+    const Cx eta{eta_re, k};
+    const double cos_o = rclamp(dot(wo, wh), 0.0, 1.0);
+    const double sin2_o = 1.0 - cos_o * cos_o;
+    const Cx sin2_i = f_div_cx(sin2_o, cx_mul(eta, eta));
+    const Cx cos_i = cx_sqrt(Cx{1.0 - sin2_i.re, -sin2_i.im});
+    const Cx eco = cx_scale(eta, cos_o);
+    const Cx r_par = cx_div(Cx{eco.re - cos_i.re, eco.im - cos_i.im}, Cx{eco.re + cos_i.re, eco.im + cos_i.im});
+    const Cx eci = cx_mul(eta, cos_i);
+    const Cx r_per = cx_div(Cx{cos_o - eci.re, -eci.im}, Cx{cos_o + eci.re, eci.im});
+    return (cx_norm_sqr(r_par) + cx_norm_sqr(r_per)) / 2.0;
+}
+double f_at(const Mfd& d, V3 wo, V3 wh, double wl) {  // :258-271
+    const double eta = eta_at(d, wl);
+    const double k = k_at(d, wl);
+    if (k == 0.0) return eta == 0.0 ? 0.0 : fr_real(wo, wh, eta);
+    return fr_complex(wo, wh, eta, k);
+}
+Color f_fresnel(const Mfd& d, V3 wo, V3 wh, const Lambda& L) {
+    Color c;
+    for (int i = 0; i < NS; ++i) c.s[i] = f_at(d, wo, wh, L.l[i]);
+    return c;
+}
+bool chi_pass(V3 wo, V3 wh) {  // :314-320
+    const double chi = rsignum(wh.z) * dot(wo, wh) * wo.z;
+    return chi > EPSILON;
+}
+double mf_lambda(const Mfd& d, V3 w) {  // :357-372 (GGX)
+    const double tan2 = sph_tan2(w);
+    if (std::isinf(tan2)) return 0.0;
+    const double cp = sph_cos_phi(w), sp = sph_sin_phi(w);
+    const double alpha2 = powi2(d.rx * cp) + powi2(d.ry * sp);
+    return (std::sqrt(rmax(1.0 + alpha2 * tan2, 0.0)) - 1.0) / 2.0;
+}
+double mf_g(const Mfd& d, V3 wo, V3 wi, V3 wh) {
+    if (!chi_pass(wo, wh)) return 0.0;
+    return 1.0 / (1.0 + mf_lambda(d, wo) + mf_lambda(d, wi));
+}
+double mf_g1(const Mfd& d, V3 wo, V3 wh) {
+    if (!chi_pass(wo, wh)) return 0.0;
+    return 1.0 / (1.0 + mf_lambda(d, wo));
+}
+double sample_normal_pdf(const Mfd& d, V3 wh, V3 wo) {  // :394-412 (GGX)
+    const double pdf = mf_g1(d, wo, wh) * mf_d(d, wh) * fabs(dot(wh, wo)) / fabs(wo.z);
+    return rmax(pdf, 0.0);
+}
+V3 sample_normal(const Mfd& d, V3 wo, V2 sq) {  // :416-465 (GGX, Heitz 2018)
+    V3 ws = normalize(V3{wo.x * d.rx, wo.y * d.ry, wo.z});
+    if (ws.z < 0.0) ws = -ws;
+    const V3 u = (1.0 - ws.z < EPSILON) ? V3{1.0, 0.0, 0.0} : normalize(cross(ws, V3{0.0, 0.0, 1.0}));
+    const V3 v = cross(u, ws);
+    const double r = std::sqrt(sq.x);
+    const double theta = 2.0 * PI * sq.y;
+    const double x = r * O_COS(theta);
+    const double h = std::sqrt(rmax(1.0 - x * x, 0.0));
+    const double lerp = (1.0 + ws.z) / 2.0;
+    const double y = (1.0 - lerp) * h + lerp * r * O_SIN(theta);
+    const V3 wm{x, y, std::sqrt(rmax(1.0 - x * x - y * y, 0.0))};
+    const V3 w = wm.x * u + wm.y * v + wm.z * ws;
+    return normalize(V3{d.rx * w.x, d.ry * w.y, rmax(w.z, EPSILON)});
+}
+
+// ---- BxDFs (bxdf.rs, bxdf/scatter.rs, bxdf/microfacet.rs)
+bool mf_reflect(V3 wo, V3 no, V3* wi) {  // bxdf/microfacet.rs:7-15
+    const V3 w = 2.0 * project_onto(wo, no) - wo;
+    if (!same_hemisphere(w, wo)) return false;
+    *wi = w;
     return true;
 }
-// material.rs:292-306 -> bsdf.rs:70-84 -> bxdf.rs:127-150 -> scatter.rs:16-26
-double bsdf_pdf(const Scene& sc, const Hit& h, V3 wo, V3 wi) {
+bool mf_refract(double eta, V3 wo, V3 no, V3* wi) {  // :17-42
+    double cos_to, eta_ratio;
+    V3 n;
+    if (dot(no, wo) < 0.0) {
+        cos_to = -dot(no, wo);
+        eta_ratio = 1.0 / eta;
+        n = -no;
+    } else {
+        cos_to = dot(no, wo);
+        eta_ratio = eta;
+        n = no;
+    }
+    const double sin2_to = 1.0 - cos_to * cos_to;
+    const double sin2_ti = sin2_to / powi2(eta_ratio);
+    if (sin2_ti >= 1.0) return false;  // unreachable!() in lumo: TIR samples reflection
+    const double cos_ti = std::sqrt(rmax(1.0 - sin2_ti, 0.0));
+    const V3 w = -wo / eta_ratio + (cos_to / eta_ratio - cos_ti) * n;
+    if (same_hemisphere(w, wo)) return false;
+    *wi = w;
+    return true;
+}
+Color reflect_coeff(const Mfd& d, V3 wo, V3 wi, const Lambda& L) {  // :44-60
+    const double cwo = wo.z, cwi = wi.z;
+    const V3 wh = normalize(wi + wo);
+    const double D = mf_d(d, wh);
+    const Color F = f_fresnel(d, wo, wh, L);
+    const double G = mf_g(d, wo, wi, wh);
+    return D * F * G / (4.0 * fabs(cwo) * fabs(cwi));
+}
+double lambertian_pdf(V3 wo, V3 wi) {  // scatter.rs:14-26
+    if (!same_hemisphere(wo, wi)) return 0.0;
+    const double c = wi.z;
+    return c > 0.0 ? c / PI : 0.0;
+}
+Color spec_c(const lumo_spectrum& s, const Lambda& L) { return spec_sample(s, L); }
+const Color WHITE_C = Color{{1.0, 1.0, 1.0, 1.0}};
+
+// conductor (:66-118)
+Color conductor_f(const Mfd& d, V3 wo, V3 wi, const Lambda& L) {
+    const Color ks = spec_c(d.ks, L);
+    if (mfd_is_delta(d)) return ks * f_fresnel(d, wo, V3{0.0, 0.0, 1.0}, L) / fabs(wi.z);
+    return ks * reflect_coeff(d, wo, wi, L);
+}
+bool conductor_sample(const Mfd& d, V3 wo, V2 sq, V3* wi) {
+    if (mfd_is_delta(d)) {
+        *wi = V3{-wo.x, -wo.y, wo.z};
+        return true;
+    }
+    return mf_reflect(wo, sample_normal(d, wo, sq), wi);
+}
+double conductor_pdf(const Mfd& d, V3 wo, V3 wi) {
+    if (!same_hemisphere(wi, wo)) return 0.0;
+    V3 wh = normalize(wo + wi);
+    if (wh.z < 0.0) wh = -wh;
+    if (mfd_is_delta(d)) return 1.0 - wh.z < EPSILON ? 1.0 : 0.0;
+    return sample_normal_pdf(d, wh, wo) / (4.0 * fabs(dot(wo, wh)));
+}
+// diffuse (:120-199)
+Color diffuse_f(const Mfd& d, V3 wo, V3 wi, const Lambda& L) {
+    const V3 wh = normalize(wo + wi);
+    const double cwo = wo.z, cwi = wi.z, cwh = wh.z;
+    const double D = mf_d(d, wh);
+    const Color F = f_fresnel(d, wo, wh, L);
+    const double G = mf_g(d, wo, wi, wh);
+    const Color fr = D * F * G / (4.0 * fabs(cwo) * fabs(cwi));
+    const double fd = disney_diffuse(d, cwo, cwi, cwh);
+    const Color ks = spec_c(d.ks, L);
+    const Color kd = spec_c(d.kd, L);
+    return fr * ks + kd * (WHITE_C - F) * fd / PI;
+}
+bool diffuse_sample(const Mfd& d, V3 wo, double rand_u, V2 sq, V3* wi) {
+    const double pr = f_schlick(0.04, 1.0, wo.z);
+    const double ps = 1.0 - pr;
+    if (rand_u < pr / (pr + ps)) {
+        const V3 wh = mfd_is_delta(d) ? V3{0.0, 0.0, 1.0} : sample_normal(d, wo, sq);
+        return mf_reflect(wo, wh, wi);
+    }
+    *wi = square_to_cos_hemisphere(sq);
+    return true;
+}
+double diffuse_pdf(const Mfd& d, V3 wo, V3 wi) {
+    if (!same_hemisphere(wi, wo)) return 0.0;
+    const V3 wh = normalize(wo + wi);
+    const double pr = f_schlick(0.04, 1.0, wo.z);
+    const double ps = 1.0 - pr;
+    const double wh_dot_wo = dot(wo, wh);
+    const double p_ref = mfd_is_delta(d) ? (1.0 - wh.z < EPSILON ? 1.0 : 0.0)
+                                         : sample_normal_pdf(d, wh, wo) / (4.0 * fabs(wh_dot_wo));
+    const double p_sct = lambertian_pdf(wo, wi);
+    return pr * p_ref + ps * p_sct;
+}
+// dielectric (:201-374)
+Color dielectric_f(const Mfd& d, V3 wo, V3 wi, const Lambda& L, bool reflection) {
+    const double cwo = wo.z, cwi = wi.z;
+    const bool wo_inside = cwo < 0.0;
+    const double eta = eta_at(d, L.l[0]);
+    const double eta_ratio = reflection ? 1.0 : (wo_inside ? 1.0 / eta : eta);
+    const bool flat = eta == 1.0 || mfd_is_delta(d);
+    V3 wh = flat ? V3{0.0, 0.0, 1.0} : normalize(wi * eta_ratio + wo);
+    if (reflection) {
+        const Color ks = spec_c(d.ks, L);
+        if (flat) return ks * f_fresnel(d, wo, wh, L) / fabs(cwi);
+        return ks * reflect_coeff(d, wo, wi, L);
+    }
+    const Color F = f_fresnel(d, wo, wh, L);
+    if (wh.z < 0.0) wh = -wh;
+    const double scale = eta_ratio * eta_ratio;  // Transport::Radiance
+    const Color tf = spec_c(d.tf, L);
+    if (flat) return tf * (WHITE_C - F) / (scale * fabs(cwi));
+    const double D = mf_d(d, wh);
+    const double G = mf_g(d, wo, wi, wh);
+    const double wh_dot_wo = dot(wh, wo), wh_dot_wi = dot(wh, wi);
+    return tf * D * (WHITE_C - F) * G / scale * fabs(wh_dot_wi * wh_dot_wo / (cwi * cwo)) /
+           powi2(eta_ratio * wh_dot_wi + wh_dot_wo);
+}
+bool dielectric_sample(const Mfd& d, V3 wo, Lambda& L, double rand_u, V2 sq, V3* wi) {
+    double wl;
+    if (d.constant_eta) {
+        wl = L.l[0];
+    } else {  // ColorWavelength::terminate
+        for (int i = 1; i < NS; ++i) L.l[i] = 0.0;
+        wl = L.l[0];
+    }
+    const double eta = eta_at(d, wl);
+    const V3 wh = (eta == 1.0 || mfd_is_delta(d)) ? V3{0.0, 0.0, 1.0} : sample_normal(d, wo, sq);
+    const double pr = f_at(d, wo, wh, wl);
+    const double pt = 1.0 - pr;
+    if (rand_u < pr / (pr + pt)) return mf_reflect(wo, wh, wi);
+    return mf_refract(eta, wo, wh, wi);
+}
+double dielectric_pdf(const Mfd& d, V3 wo, V3 wi, bool reflection, const Lambda& L) {
+    const double cwo = wo.z, cwi = wi.z;
+    const bool wo_inside = cwo < 0.0;
+    const double wl = L.l[0];
+    const double eta = eta_at(d, wl);
+    const double eta_ratio = reflection ? 1.0 : (wo_inside ? 1.0 / eta : eta);
+    V3 wh = eta == 1.0 ? V3{0.0, 0.0, 1.0} : normalize(wo + wi * eta_ratio);
+    if (wh.z < 0.0) wh = -wh;
+    const double wh_dot_wo = dot(wo, wh), wh_dot_wi = dot(wi, wh);
+    if (wh_dot_wo == 0.0 || wh_dot_wi == 0.0) return 0.0;
+    if (wh_dot_wo * cwo < 0.0 || wh_dot_wi * cwi < 0.0) return 0.0;
+    const double pr = f_at(d, wo, wh, wl);
+    const double pt = 1.0 - pr;
+    const bool flat = eta == 1.0 || mfd_is_delta(d);
+    if (reflection && flat) return 1.0 - wh.z < EPSILON ? pr / (pr + pt) : 0.0;
+    if (reflection) return sample_normal_pdf(d, wh, wo) / (4.0 * fabs(wh_dot_wo)) * pr / (pr + pt);
+    if (flat) return 1.0 - wh.z < EPSILON ? pt / (pr + pt) : 0.0;
+    return sample_normal_pdf(d, wh, wo) * fabs(wh_dot_wi) / powi2(wh_dot_wi + wh_dot_wo / eta_ratio) * pt / (pr + pt);
+}
+
+bool is_standard(int kind) {
+    return kind == LUMO_MAT_LAMBERTIAN || kind == LUMO_MAT_MF_DIFFUSE || kind == LUMO_MAT_MF_CONDUCTOR ||
+           kind == LUMO_MAT_MF_DIELECTRIC;
+}
+bool is_reflection_bxdf(int kind) { return kind != LUMO_MAT_MF_DIELECTRIC; }  // bxdf.rs:46-54
+
+// material.rs:273-289 -> bsdf.rs:51-67 -> bxdf.rs:104-124
+bool bsdf_sample(const Scene& sc, const Hit& h, V3 wo, Lambda& L, double rand_u, V2 rand_sq, V3* wi) {
     const lumo_material& m = mat(sc, h.material);
-    if (m.kind != LUMO_MAT_LAMBERTIAN) return 0.0;
+    if (!is_standard(m.kind)) return false;  // Light / Blank -> None
+    const Onb uvw = onb_new(h.ns);
+    const V3 wol = onb_to_local(uvw, wo);
+    if (h.backface && is_reflection_bxdf(m.kind)) return false;
+    V3 w;
+    bool ok;
+    switch (m.kind) {
+        case LUMO_MAT_LAMBERTIAN:
+            w = square_to_cos_hemisphere(rand_sq);
+            ok = true;
+            break;
+        case LUMO_MAT_MF_DIFFUSE: ok = diffuse_sample(mfd_of(sc, m), wol, rand_u, rand_sq, &w); break;
+        case LUMO_MAT_MF_CONDUCTOR: ok = conductor_sample(mfd_of(sc, m), wol, rand_sq, &w); break;
+        default: ok = dielectric_sample(mfd_of(sc, m), wol, L, rand_u, rand_sq, &w); break;
+    }
+    if (!ok) return false;
+    *wi = onb_to_world(uvw, w);
+    return true;
+}
+// material.rs:292-306 -> bsdf.rs:70-84 -> bxdf.rs:127-150
+double bsdf_pdf(const Scene& sc, const Hit& h, V3 wo, V3 wi, const Lambda& L) {
+    const lumo_material& m = mat(sc, h.material);
+    if (!is_standard(m.kind)) return 0.0;
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
     const Onb uvw = onb_new(h.ns);
     const V3 wol = onb_to_local(uvw, wo), wil = onb_to_local(uvw, wi);
-    if (!reflection) return 0.0;
-    if (!(wol.z * wil.z > 0.0)) return 0.0;
-    const double cos_theta = wil.z;
-    return cos_theta > 0.0 ? cos_theta / PI : 0.0;
+    if (!reflection && is_reflection_bxdf(m.kind)) return 0.0;
+    switch (m.kind) {
+        case LUMO_MAT_LAMBERTIAN: return lambertian_pdf(wol, wil);
+        case LUMO_MAT_MF_DIFFUSE: return diffuse_pdf(mfd_of(sc, m), wol, wil);
+        case LUMO_MAT_MF_CONDUCTOR: return conductor_pdf(mfd_of(sc, m), wol, wil);
+        default: return dielectric_pdf(mfd_of(sc, m), wol, wil, reflection, L);
+    }
 }
 // material.rs:254-270 -> bsdf.rs:28-48 -> bxdf.rs:71-100
 Color bsdf_f(const Scene& sc, const Hit& h, V3 wo, V3 wi, const Lambda& L) {
     const lumo_material& m = mat(sc, h.material);
-    if (m.kind != LUMO_MAT_LAMBERTIAN) return cconst(0.0);
+    if (!is_standard(m.kind)) return cconst(0.0);
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
+    const Onb uvw = onb_new(h.ns);
+    const V3 wol = onb_to_local(uvw, wo), wil = onb_to_local(uvw, wi);
     if ((!reflection || h.backface) && is_reflection_bxdf(m.kind)) return cconst(0.0);
-    return spec_sample(m.albedo, L) / PI;
+    switch (m.kind) {
+        case LUMO_MAT_LAMBERTIAN: return spec_sample(m.albedo, L) / PI;
+        case LUMO_MAT_MF_DIFFUSE: return diffuse_f(mfd_of(sc, m), wol, wil, L);
+        case LUMO_MAT_MF_CONDUCTOR: return conductor_f(mfd_of(sc, m), wol, wil, L);
+        default: return dielectric_f(mfd_of(sc, m), wol, wil, L, reflection);
+    }
 }
 double shading_cosine(const Scene& sc, int material, V3 wi, V3 ns) {  // material.rs:315-320
-    return mat(sc, material).kind == LUMO_MAT_LIGHT || mat(sc, material).kind == LUMO_MAT_BLANK ? 1.0
-                                                                                                 : fabs(dot(ns, wi));
+    return is_standard(mat(sc, material).kind) ? fabs(dot(ns, wi)) : 1.0;
 }
-bool is_specular(const Scene& sc, int material) { (void)sc, (void)material; return false; }  // Lambertian/Light
-bool is_delta(const Scene& sc, int material) { (void)sc, (void)material; return false; }
+bool is_specular(const Scene& sc, int material) {  // material.rs:196-203, bxdf.rs:33-40
+    const lumo_material& m = mat(sc, material);
+    if (m.kind == LUMO_MAT_MF_DIELECTRIC) return true;
+    if (m.kind == LUMO_MAT_MF_CONDUCTOR) return mfd_is_specular(mfd_of(sc, m));
+    return false;
+}
+bool is_delta(const Scene& sc, int material, const Lambda& L) {  // material.rs:207-213, bxdf.rs:57-66
+    const lumo_material& m = mat(sc, material);
+    if (m.kind == LUMO_MAT_MF_CONDUCTOR) return mfd_is_delta(mfd_of(sc, m));
+    if (m.kind == LUMO_MAT_MF_DIELECTRIC) {
+        const Mfd d = mfd_of(sc, m);
+        return mfd_is_delta(d) || eta_at(d, L.l[0]) == 1.0;
+    }
+    return false;
+}
 // material.rs:223-234
 Color emit(const Scene& sc, int material, const Lambda& L, const Hit& h) {
     const lumo_material& m = mat(sc, material);
@@ -568,7 +937,7 @@ Color mis_sample(const Scene& sc, V3 wo, V3 wi, const Hit& ho, const Hit& hi, co
 }
 
 // integrator.rs:87-137
-Color single_shadow_ray(const Scene& sc, V3 wo, const Lambda& L, const Hit& ho, Xorshift& rng, Counters& C) {
+Color single_shadow_ray(const Scene& sc, V3 wo, Lambda& L, const Hit& ho, Xorshift& rng, Counters& C) {
     const V3 xo = ho.p;
     const int li = sample_light(sc, xs_float(rng));
     const lumo_object& light = sc.d->lights[li];
@@ -582,7 +951,7 @@ Color single_shadow_ray(const Scene& sc, V3 wo, const Lambda& L, const Hit& ho, 
         Color add = cconst(0.0);
         if (scene_hit_light(sc, ri, li, &hi, C)) {
             const double p_lig = light_sample_towards_pdf(light, ri, hi.p, hi.ng);
-            const double p_sct = bsdf_pdf(sc, ho, wo, wi);
+            const double p_sct = bsdf_pdf(sc, ho, wo, wi, L);
             add = mis_sample(sc, wo, wi, ho, hi, L, true, p_lig, p_sct);
         }
         radiance = radiance + add;
@@ -592,12 +961,12 @@ Color single_shadow_ray(const Scene& sc, V3 wo, const Lambda& L, const Hit& ho, 
         const V2 rand_sq = xs_vec2(rng);
         V3 wi;
         Color add = cconst(0.0);
-        if (bsdf_sample(sc, ho, wo, rand_u, rand_sq, &wi)) {
+        if (bsdf_sample(sc, ho, wo, L, rand_u, rand_sq, &wi)) {
             const Ray ri = generate_ray(ho, wi);
             Hit hi;
             if (scene_hit_light(sc, ri, li, &hi, C)) {
                 const double p_lig = light_sample_towards_pdf(light, ri, hi.p, hi.ng);
-                const double p_sct = bsdf_pdf(sc, ho, wo, wi);
+                const double p_sct = bsdf_pdf(sc, ho, wo, wi, L);
                 add = mis_sample(sc, wo, wi, ho, hi, L, false, p_lig, p_sct);
             }
         }
@@ -641,11 +1010,11 @@ Sample path_trace(const Scene& sc, Ray ro, Xorshift& rng, Lambda L, double delta
         const double u = xs_float(rng);
         const V2 sq = xs_vec2(rng);
         V3 wi;
-        if (!bsdf_sample(sc, ho, wo, u, sq, &wi)) {
+        if (!bsdf_sample(sc, ho, wo, L, u, sq, &wi)) {
             if (last_specular) radiance = radiance + gathered * emit(sc, ho.material, L, ho);
             break;
         }
-        if (!is_delta(sc, ho.material)) {
+        if (!is_delta(sc, ho.material, L)) {
             const int n = sc.num_shadow_rays();
             Color acc = cconst(0.0);
             for (int i = 0; i < n; ++i) acc = acc + gathered * single_shadow_ray(sc, -ro.dir, L, ho, rng, C);
@@ -653,7 +1022,7 @@ Sample path_trace(const Scene& sc, Ray ro, Xorshift& rng, Lambda L, double delta
         }
         const Ray ri = generate_ray(ho, wi);
         const V3 wi2 = ri.dir;
-        const double p_scatter = bsdf_pdf(sc, ho, wo, wi2);
+        const double p_scatter = bsdf_pdf(sc, ho, wo, wi2, L);
         if (p_scatter <= 0.0) break;
         const Color bsdf = bsdf_f(sc, ho, wo, wi2, L);
         gathered = gathered * (bsdf * shading_cosine(sc, ho.material, wi2, ho.ns) / p_scatter);
@@ -1026,5 +1395,86 @@ extern "C" int oracle_debug_trace(const lumo_scene_desc* scene, const lumo_camer
     exec_wavefront(sc, k, *task, nullptr, C, &dbg);
     *n_out = log.n;
     std::memcpy(out, log.rec, sizeof(double) * 20 * log.n);
+    return LUMO_OK;
+}
+
+// ------------------------------------------------------------------ BSDF probes (tests only)
+namespace {
+Hit probe_hit(int material) {
+    Hit h{};
+    h.t = 1.0;
+    h.material = material;
+    h.p = V3{0.0, 0.0, 0.0};
+    h.ns = V3{0.0, 0.0, 1.0};
+    h.ng = V3{0.0, 0.0, 1.0};
+    h.backface = false;
+    return h;
+}
+}  // namespace
+
+extern "C" int oracle_bsdf_sample(const lumo_scene_desc* scene, int material, const double* wo, const double* lambda4,
+                                  size_t n, uint64_t seed, double* wi3, int* ok) {
+    if (!scene || !wo || !lambda4 || !wi3 || !ok || material < 0 || material >= scene->num_materials)
+        return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    const Hit h = probe_hit(material);
+    Xorshift rng = xs_new(seed);
+    const V3 o{wo[0], wo[1], wo[2]};
+    for (size_t i = 0; i < n; ++i) {
+        Lambda L;
+        for (int k = 0; k < NS; ++k) L.l[k] = lambda4[k];
+        const double u = xs_float(rng);
+        const V2 sq = xs_vec2(rng);
+        V3 w{0.0, 0.0, 0.0};
+        ok[i] = bsdf_sample(sc, h, o, L, u, sq, &w) ? 1 : 0;
+        wi3[3 * i] = w.x;
+        wi3[3 * i + 1] = w.y;
+        wi3[3 * i + 2] = w.z;
+    }
+    return LUMO_OK;
+}
+
+extern "C" int oracle_bsdf_eval(const lumo_scene_desc* scene, int material, const double* wo, const double* lambda4,
+                                const double* wi3, size_t n, double* pdf, double* f4) {
+    if (!scene || !wo || !lambda4 || !wi3 || !pdf || !f4 || material < 0 || material >= scene->num_materials)
+        return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    const Hit h = probe_hit(material);
+    Lambda L;
+    for (int k = 0; k < NS; ++k) L.l[k] = lambda4[k];
+    const V3 o{wo[0], wo[1], wo[2]};
+    for (size_t i = 0; i < n; ++i) {
+        const V3 w{wi3[3 * i], wi3[3 * i + 1], wi3[3 * i + 2]};
+        pdf[i] = bsdf_pdf(sc, h, o, w, L);
+        const Color f = bsdf_f(sc, h, o, w, L);
+        for (int k = 0; k < NS; ++k) f4[4 * i + k] = f.s[k];
+    }
+    return LUMO_OK;
+}
+
+// white_furnace_tests.rs:111-129
+extern "C" int oracle_furnace(const lumo_scene_desc* scene, int material, const double* wo, size_t n, uint64_t seed,
+                              double* out4) {
+    if (!scene || !wo || !out4 || material < 0 || material >= scene->num_materials) return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    const Hit h = probe_hit(material);
+    Xorshift rng = xs_new(seed);
+    const V3 o{wo[0], wo[1], wo[2]};
+    Lambda L = wl_sample(xs_float(rng));
+    size_t misses = 0;
+    Color radiance = cconst(0.0);
+    for (size_t i = 0; i < n; ++i) {
+        const double u = xs_float(rng);
+        const V2 sq = xs_vec2(rng);
+        V3 w;
+        if (!bsdf_sample(sc, h, o, L, u, sq, &w)) {
+            misses++;
+            continue;
+        }
+        radiance = radiance + bsdf_f(sc, h, o, w, L) * shading_cosine(sc, material, w, h.ns) / bsdf_pdf(sc, h, o, w, L);
+    }
+    const Color pdf = wl_pdf(L);
+    const Color r = radiance * pdf / (pdf * (double)(n - misses));
+    for (int k = 0; k < NS; ++k) out4[k] = r.s[k];
     return LUMO_OK;
 }

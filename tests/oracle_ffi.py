@@ -37,6 +37,14 @@ def load(path=None):
         lib.oracle_trace.restype = C.c_int
         lib.oracle_trace.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(_ffi.RaySoA), C.c_size_t,
                                      C.POINTER(_ffi.HitSoA), C.c_int, C.POINTER(Counters)]
+        dp = _ffi.c_double_p
+        lib.oracle_bsdf_sample.restype = C.c_int
+        lib.oracle_bsdf_sample.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, dp, C.c_size_t, C.c_uint64, dp,
+                                           C.POINTER(C.c_int)]
+        lib.oracle_bsdf_eval.restype = C.c_int
+        lib.oracle_bsdf_eval.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, dp, dp, C.c_size_t, dp, dp]
+        lib.oracle_furnace.restype = C.c_int
+        lib.oracle_furnace.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, C.c_size_t, C.c_uint64, dp]
         _libs[path] = lib
     return _libs[path]
 
@@ -92,3 +100,36 @@ def trace(scene_desc, origins, dirs, lights=None):
                           C.byref(cnt))
     assert st == 0
     return t, kind, obj, cnt
+
+
+def _dp(a):
+    return a.ctypes.data_as(_ffi.c_double_p)
+
+
+def bsdf_sample(scene_desc, material, wo, lam, n, seed):
+    wo = np.ascontiguousarray(wo, dtype=np.float64)
+    lam = np.ascontiguousarray(lam, dtype=np.float64)
+    wi = np.zeros((n, 3))
+    ok = np.zeros(n, dtype=np.int32)
+    st = load().oracle_bsdf_sample(C.byref(scene_desc), material, _dp(wo), _dp(lam), n, seed, _dp(wi),
+                                   ok.ctypes.data_as(C.POINTER(C.c_int)))
+    assert st == 0
+    return wi, ok.astype(bool)
+
+
+def bsdf_eval(scene_desc, material, wo, lam, wi):
+    wo = np.ascontiguousarray(wo, dtype=np.float64)
+    lam = np.ascontiguousarray(lam, dtype=np.float64)
+    wi = np.ascontiguousarray(wi, dtype=np.float64).reshape(-1, 3)
+    pdf = np.zeros(len(wi))
+    f = np.zeros((len(wi), 4))
+    st = load().oracle_bsdf_eval(C.byref(scene_desc), material, _dp(wo), _dp(lam), _dp(wi), len(wi), _dp(pdf), _dp(f))
+    assert st == 0
+    return pdf, f
+
+
+def furnace(scene_desc, material, wo, n, seed):
+    wo = np.ascontiguousarray(wo, dtype=np.float64)
+    out = np.zeros(4)
+    assert load().oracle_furnace(C.byref(scene_desc), material, _dp(wo), n, seed, _dp(out)) == 0
+    return out
