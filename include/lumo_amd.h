@@ -92,20 +92,33 @@ typedef struct {
 } lumo_kd_node;
 
 enum {
-    LUMO_OBJ_KDMESH = 0,   /* KdTree<Triangle> (TriangleMesh::new, triangle_mesh.rs:46-60) */
-    LUMO_OBJ_RECTANGLE = 1 /* Rectangle (object/rectangle.rs): 2-triangle kd mesh + uv/sampling */
+    LUMO_OBJ_KDMESH = 0,    /* KdTree<Triangle> (TriangleMesh::new, triangle_mesh.rs:46-60) */
+    LUMO_OBJ_RECTANGLE = 1, /* Rectangle (object/rectangle.rs): 2-triangle kd mesh + uv/sampling */
+    LUMO_OBJ_TRIANGLE = 2   /* a single Triangle (object/triangle.rs), e.g. an emissive OBJ face
+                               added as a light (parser/obj.rs:93-103)                       */
 };
 
+/* Instance transform (object/instance.rs, math/transform.rs): row-major 4x4 local->world `m`,
+ * its inverse `inv`, and the normal transform (transpose of inv's 3x3, Transform::to_normal). */
 typedef struct {
-    int32_t type;      /* LUMO_OBJ_*                                     */
+    double m[16];
+    double inv[16];
+    double nrm[9];
+    double pad0;
+} lumo_transform;
+
+typedef struct {
+    int32_t type;      /* LUMO_OBJ_* of the shape                        */
     int32_t material;  /* material of the mesh (KdTree::material)        */
-    int32_t kd_root;   /* index of the root in kd_nodes                  */
+    int32_t kd_root;   /* index of the root in kd_nodes (-1: TRIANGLE)   */
     int32_t tri_base;  /* first triangle of this object in triangles[]   */
     int32_t item_base; /* kd leaf item lists live in kd_items[item_base..] */
     int32_t num_tris;
-    double bmin[3], bmax[3]; /* kd boundary (KdTree::boundary)             */
+    int32_t xform;     /* Instance: index into transforms[], else -1     */
+    int32_t material_override; /* Instance material (instance.rs:96-98) or -1 */
+    double bmin[3], bmax[3]; /* kd boundary in the shape's own space (KdTree::boundary) */
     double origin[3], b0[3], b1[3]; /* Rectangle parameters (rectangle.rs:6-13) */
-    double area;       /* Sampleable::area                              */
+    double area;       /* Sampleable::area of the shape (own space)      */
 } lumo_object;
 
 typedef struct {
@@ -143,6 +156,9 @@ typedef struct {
     int32_t num_materials, num_dense_spectra;
     const lumo_material* materials;
     const double* dense_spectra; /* num_dense_spectra x 95 */
+    /* instance transforms referenced by lumo_object.xform */
+    int32_t num_transforms, pad1;
+    const lumo_transform* transforms;
 } lumo_scene_desc;
 
 /* Camera (camera.rs:17-38, CameraConfig): world_to_camera, screen_to_raster and

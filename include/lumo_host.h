@@ -40,6 +40,16 @@ int lumo_builder_add_mesh(void* b, const double* vertices, int64_t nv, const int
 /* Rectangle::new(Mat3(a, b, c), material) */
 int lumo_builder_add_rectangle(void* b, const double* a, const double* bb, const double* c, int material,
                                int as_light);
+/* Instanceable / Instance transformations (object/instance.rs:203-299, kdtree.rs:93-99) applied to
+ * object `index` of builder b (lights if is_light).  Each op composes AFTER the current transform;
+ * rotations take the angle in x (radians).  Returns LUMO_OK or LUMO_ERR_INVALID. */
+enum {
+    LUMO_INST_TRANSLATE = 0, LUMO_INST_SCALE, LUMO_INST_ROTATE_X, LUMO_INST_ROTATE_Y, LUMO_INST_ROTATE_Z,
+    LUMO_INST_TO_UNIT_SIZE, LUMO_INST_TO_ORIGIN, LUMO_INST_SET_X, LUMO_INST_SET_Y, LUMO_INST_SET_Z
+};
+int lumo_builder_instance_op(void* b, int is_light, int64_t index, int op, double x, double y, double z);
+/* Number of objects (is_light = 0) or lights (is_light != 0) added so far. */
+int64_t lumo_builder_count(void* b, int is_light);
 /* Scene::cornell_box() */
 void* lumo_builder_cornell_box(void);
 /* Scene::empty_box(def_color, mat_left, mat_right) (scene/empty_box.rs:16-97) added to builder b;

@@ -145,6 +145,55 @@ class Material:
                                              int(bool(self.kw["two_sided"])))
 
 
+class ObjectRef:
+    """Handle to an object added to a Scene; Instanceable transformations compose in call order
+    (object/instance.rs:203-299): mesh.to_unit_size().to_origin().rotate_y(a).translate(x, y, z)."""
+    _OPS = {"translate": 0, "scale": 1, "rotate_x": 2, "rotate_y": 3, "rotate_z": 4, "to_unit_size": 5,
+            "to_origin": 6, "set_x": 7, "set_y": 8, "set_z": 9}
+
+    def __init__(self, scene, index, light=False):
+        self.scene, self.index, self.light = scene, index, light
+
+    def _op(self, name, x=0.0, y=0.0, z=0.0):
+        check(lib().lumo_builder_instance_op(self.scene._b, int(self.light), self.index, self._OPS[name], x, y, z),
+              name)
+        self.scene._flat = None
+        return self
+
+    def translate(self, x, y, z):
+        return self._op("translate", x, y, z)
+
+    def scale(self, x, y, z):
+        return self._op("scale", x, y, z)
+
+    def scale_uniform(self, s):
+        return self._op("scale", s, s, s)
+
+    def rotate_x(self, r):
+        return self._op("rotate_x", r)
+
+    def rotate_y(self, r):
+        return self._op("rotate_y", r)
+
+    def rotate_z(self, r):
+        return self._op("rotate_z", r)
+
+    def to_unit_size(self):
+        return self._op("to_unit_size")
+
+    def to_origin(self):
+        return self._op("to_origin")
+
+    def set_x(self, v):
+        return self._op("set_x", v)
+
+    def set_y(self, v):
+        return self._op("set_y", v)
+
+    def set_z(self, v):
+        return self._op("set_z", v)
+
+
 class Scene:
     """lumo Scene: objects + lights; build() produces the flattened device image."""
 
@@ -175,14 +224,21 @@ class Scene:
     def add_mesh(self, vertices, faces, material, light=False):
         """TriangleMesh::new(vertices, faces, [], [], material) added with Scene::add."""
         v = np.ascontiguousarray(np.asarray(vertices, dtype=np.float64).reshape(-1, 3))
-        sizes = np.asarray([len(f) for f in faces], dtype=np.int64)
-        idx = np.asarray([i for f in faces for i in f], dtype=np.int64)
+        if isinstance(faces, np.ndarray) and faces.ndim == 2:  # uniform polygons, fast path
+            idx = np.ascontiguousarray(faces, dtype=np.int64).reshape(-1)
+            sizes = np.full(len(faces), faces.shape[1], dtype=np.int64)
+        else:
+            sizes = np.asarray([len(f) for f in faces], dtype=np.int64)
+            idx = np.asarray([i for f in faces for i in f], dtype=np.int64)
         m = self._mat(material)
         st = lib().lumo_builder_add_mesh(self._b, v.ctypes.data_as(_ffi.c_double_p), len(v),
                                          idx.ctypes.data_as(_ffi.c_int64_p), sizes.ctypes.data_as(_ffi.c_int64_p),
                                          len(sizes), m, int(light))
         check(st, "add_mesh")
         self._flat = None
+        if light:  # one Triangle light per face triangle (parser/obj.rs:93-103)
+            return None
+        return ObjectRef(self, lib().lumo_builder_count(self._b, 0) - 1)
 
     def add_rectangle(self, a, b, c, material, light=False):
         """Rectangle::new(Mat3::new(a, b, c), material) via Scene::add / Scene::add_light."""
@@ -192,6 +248,7 @@ class Scene:
                                               int(light))
         check(st, "add_rectangle")
         self._flat = None
+        return ObjectRef(self, lib().lumo_builder_count(self._b, int(light)) - 1, light)
 
     def build(self):
         if self._flat is None:

@@ -41,9 +41,14 @@ class KdNode(C.Structure):
                 ("first", C.c_int32), ("count", C.c_int32), ("pad0", C.c_int32)]
 
 
+class Transform(C.Structure):
+    _fields_ = [("m", C.c_double * 16), ("inv", C.c_double * 16), ("nrm", C.c_double * 9), ("pad0", C.c_double)]
+
+
 class Object(C.Structure):
     _fields_ = [("type", C.c_int32), ("material", C.c_int32), ("kd_root", C.c_int32), ("tri_base", C.c_int32),
-                ("item_base", C.c_int32), ("num_tris", C.c_int32), ("bmin", C.c_double * 3),
+                ("item_base", C.c_int32), ("num_tris", C.c_int32), ("xform", C.c_int32),
+                ("material_override", C.c_int32), ("bmin", C.c_double * 3),
                 ("bmax", C.c_double * 3), ("origin", C.c_double * 3), ("b0", C.c_double * 3),
                 ("b1", C.c_double * 3), ("area", C.c_double)]
 
@@ -67,6 +72,7 @@ class SceneDesc(C.Structure):
         ("alias_prob", c_double_p), ("alias_idx", c_int32_p), ("alias_pdf", c_double_p),
         ("num_materials", C.c_int32), ("num_dense_spectra", C.c_int32),
         ("materials", C.POINTER(Material)), ("dense_spectra", c_double_p),
+        ("num_transforms", C.c_int32), ("pad1", C.c_int32), ("transforms", C.POINTER(Transform)),
     ]
 
 
@@ -161,6 +167,9 @@ HOST_API = [
     ("lumo_builder_material_mirror", C.c_int, [C.c_void_p]),
     ("lumo_builder_material_glass", C.c_int, [C.c_void_p]),
     ("lumo_builder_empty_box", C.c_int, [C.c_void_p, Spectrum, C.c_int, C.c_int]),
+    ("lumo_builder_instance_op", C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_double, C.c_double,
+                                           C.c_double]),
+    ("lumo_builder_count", C.c_int64, [C.c_void_p, C.c_int]),
     ("lumo_builder_add_mesh", C.c_int, [C.c_void_p, c_double_p, C.c_int64, c_int64_p, c_int64_p, C.c_int64,
                                         C.c_int, C.c_int]),
     ("lumo_builder_add_rectangle", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p, C.c_int, C.c_int]),

@@ -42,13 +42,14 @@ struct DScene {
     const double* alias_pdf;
     const lumo_material* mats;
     const double* dense;
+    const lumo_transform* xforms;
     int32_t n_onodes, n_lnodes, n_lights, n_shadow, stack_class;
     // Traversal working set packed contiguously (16-B aligned sub-arrays) so that a small scene
     // can be staged into LDS once per workgroup; hot_bytes == 0 disables staging.
     const char* hot;
     uint32_t hot_bytes;
     uint32_t off_onodes, off_oitems, off_lnodes, off_litems, off_objs, off_lights, off_kd, off_kd_items, off_tris,
-        off_vertices;
+        off_vertices, off_xforms;
 };
 
 // Copy the packed traversal set into LDS and point a scene view at it.
@@ -68,6 +69,7 @@ __device__ __forceinline__ DScene stage_scene_lds(const DScene& sc, char* lds) {
     v.kd_items = reinterpret_cast<const int32_t*>(lds + sc.off_kd_items);
     v.tris = reinterpret_cast<const lumo_triangle*>(lds + sc.off_tris);
     v.vertices = reinterpret_cast<const double*>(lds + sc.off_vertices);
+    v.xforms = reinterpret_cast<const lumo_transform*>(lds + sc.off_xforms);
     return v;
 }
 
@@ -409,28 +411,83 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
     return DINF;
 }
 
-// Object::hit_t for KdMesh / Rectangle (kdtree.rs:178-180, rectangle.rs:87-89)
+// ---- Instance (object/instance.rs:81-105): the shape is hit with the ray in its own space
+__device__ __forceinline__ V3 xrow3(const double* m, int r, V3 v) { return V3{m[4 * r], m[4 * r + 1], m[4 * r + 2]}; }
+__device__ __forceinline__ V3 xf_apply(const double* m, V3 v, double w) {  // project(m * (v, w))
+    const V4 in{v.x, v.y, v.z, w};
+    const V4 o{dot4(V4{m[0], m[1], m[2], m[3]}, in), dot4(V4{m[4], m[5], m[6], m[7]}, in),
+               dot4(V4{m[8], m[9], m[10], m[11]}, in), dot4(V4{m[12], m[13], m[14], m[15]}, in)};
+    return project(o);
+}
+__device__ __forceinline__ V3 xf_abs_apply(const double* m, V3 v, double w) {
+    const V4 in{v.x, v.y, v.z, w};
+    auto r = [&](int i) { return V4{fabs(m[4 * i]), fabs(m[4 * i + 1]), fabs(m[4 * i + 2]), fabs(m[4 * i + 3])}; };
+    return project(V4{dot4(r(0), in), dot4(r(1), in), dot4(r(2), in), dot4(r(3), in)});
+}
+__device__ __forceinline__ V3 m3_apply(const double* n, V3 v) {
+    return V3{dot(V3{n[0], n[1], n[2]}, v), dot(V3{n[3], n[4], n[5]}, v), dot(V3{n[6], n[7], n[8]}, v)};
+}
+// Ray::transform::<false> (ray.rs:24-31): direction left unnormalised
+__device__ __forceinline__ RayX ray_local(const lumo_transform& T, const RayX& r) {
+    return rayx(Ray{xf_apply(T.inv, r.o, 1.0), xf_apply(T.inv, r.d, 0.0)});
+}
+// hit record of an instance hit back to world space (instance.rs:88-102)
+__device__ void instance_fix_hit(const lumo_transform& T, int material_override, DHit& h) {
+    h.ns = normalize(m3_apply(T.nrm, h.ns));
+    h.ng = normalize(m3_apply(T.nrm, h.ng));
+    const V3 e3 = vabs(h.err), p3 = vabs(h.p);
+    V3 err = gamma_n(3) * xf_abs_apply(T.m, p3, 1.0);
+    if (!(e3.x == 0.0 && e3.y == 0.0 && e3.z == 0.0))
+        err = err + (gamma_n(3) + 1.0) * xf_abs_apply(T.m, e3, 0.0);
+    h.err = err;
+    if (material_override >= 0) h.material = material_override;
+    h.p = xf_apply(T.m, h.p, 1.0);
+}
+
+// Object::hit_t of the shape (kdtree.rs:178-180, rectangle.rs:87-89, triangle.rs:195-197)
+template <int STK>
+__device__ __forceinline__ double shape_hit_t(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
+                                              double t_max, Counters& C) {
+    if (ob.type == LUMO_OBJ_TRIANGLE) return tri_hit_t(sc, ob.tri_base, r, t_min, t_max, C);
+    return kd_traverse<false, STK>(sc, ob, r, t_min, t_max, nullptr, C);
+}
 template <int STK>
 __device__ __forceinline__ double object_hit_t(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                                double t_max, Counters& C) {
-    return kd_traverse<false, STK>(sc, ob, r, t_min, t_max, nullptr, C);
+    if (ob.xform < 0) return shape_hit_t<STK>(sc, ob, r, t_min, t_max, C);
+    return shape_hit_t<STK>(sc, ob, ray_local(sc.xforms[ob.xform], r), t_min, t_max, C);
 }
 
-// Object::hit: kd GEO traversal, then the winner's full GEO test.  Returns the global
-// triangle index or -1 (miss, or the GEO self-intersection rejection).
-template <int STK, bool FULL>
-__device__ __forceinline__ int object_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
-                                              double t_max, Counters& C, DHit& out) {
+// Object::hit: kd GEO traversal, then the winner's GEO test (acceptance + t only; the record is
+// rebuilt by object_record).  Returns the global triangle index or -1.
+template <int STK>
+__device__ __forceinline__ int shape_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
+                                             double t_max, Counters& C, DHit& out) {
+    if (ob.type == LUMO_OBJ_TRIANGLE) return tri_hit_geo<false>(sc, ob.tri_base, r, t_min, t_max, out) ? ob.tri_base : -1;
     int idx = -1;
     kd_traverse<true, STK>(sc, ob, r, t_min, t_max, &idx, C);
     if (idx < 0) return -1;
-    if (!tri_hit_geo<FULL>(sc, ob.tri_base + idx, r, t_min, t_max, out)) return -1;
+    if (!tri_hit_geo<false>(sc, ob.tri_base + idx, r, t_min, t_max, out)) return -1;
     return ob.tri_base + idx;
 }
+template <int STK>
+__device__ __forceinline__ int object_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
+                                              double t_max, Counters& C, DHit& out) {
+    if (ob.xform < 0) return shape_hit_tri<STK>(sc, ob, r, t_min, t_max, C, out);
+    return shape_hit_tri<STK>(sc, ob, ray_local(sc.xforms[ob.xform], r), t_min, t_max, C, out);
+}
 
-// Rectangle uv override (rectangle.rs:74-85)
-__device__ __forceinline__ void object_fix_hit(const lumo_object& ob, DHit& h) {
+// Full hit record of triangle `tri` of object `ob` for world ray r (the GEO test is
+// deterministic, so re-running it reproduces the accepted hit), incl. Rectangle uv
+// (rectangle.rs:74-85) and the instance transform.
+__device__ void object_record(const DScene& sc, const lumo_object& ob, int tri, const RayX& r, DHit& h) {
+    if (ob.xform < 0) {
+        tri_hit_geo<true>(sc, tri, r, 0.0, DINF, h);
+    } else {
+        tri_hit_geo<true>(sc, tri, ray_local(sc.xforms[ob.xform], r), 0.0, DINF, h);
+    }
     if (ob.type == LUMO_OBJ_RECTANGLE) h.uv = wrap_uv(V2{dot(ld3(ob.b0), h.p), dot(ld3(ob.b1), h.p)});
+    if (ob.xform >= 0) instance_fix_hit(sc.xforms[ob.xform], ob.material_override, h);
 }
 
 // bvh.rs:315-362: returns object index or -1
@@ -502,7 +559,7 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     DHit g;
     int oi = bvh_traverse<true, STK>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C);
     if (oi >= 0) {
-        const int tri = object_hit_tri<STK, false>(sc, sc.objs[oi], r, 0.0, t_max, C, g);
+        const int tri = object_hit_tri<STK>(sc, sc.objs[oi], r, 0.0, t_max, C, g);
         if (tri >= 0) {
             h = HitRef{g.t, 1, oi, tri};
             t_max = g.t;
@@ -510,7 +567,7 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     }
     const int li = bvh_traverse<true, STK>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C);
     if (li >= 0) {
-        const int tri = object_hit_tri<STK, false>(sc, sc.lights[li], r, 0.0, t_max, C, g);
+        const int tri = object_hit_tri<STK>(sc, sc.lights[li], r, 0.0, t_max, C, g);
         if (tri >= 0) h = HitRef{g.t, 2, li, tri};
     }
     return h;
@@ -519,22 +576,20 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
 // Rebuild the full hit record of a closest hit (the GEO test is deterministic).
 __device__ __forceinline__ void hit_record(const DScene& sc, const HitRef& hr, const RayX& r, DHit& h) {
     const lumo_object& ob = hr.kind == 1 ? sc.objs[hr.obj] : sc.lights[hr.obj];
-    tri_hit_geo<true>(sc, hr.tri, r, 0.0, DINF, h);
-    object_fix_hit(ob, h);
+    object_record(sc, ob, hr.tri, r, h);
 }
 
 // Scene::hit_light (scene.rs:165-189): returns true and the light hit if visible.
 template <int STK>
 __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit& lh, Counters& C) {
     const lumo_object& L = sc.lights[light];
-    const int tri = object_hit_tri<STK, false>(sc, L, r, 0.0, DINF, C, lh);
+    const int tri = object_hit_tri<STK>(sc, L, r, 0.0, DINF, C, lh);
     if (tri < 0) return false;
     const double t_max = lh.t - EPSILON;
     if (bvh_hit_t<STK>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C) < t_max) return false;
     if (bvh_hit_t<STK>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C) < t_max) return false;
     // visible: build the light hit record (same GEO test, now in full)
-    tri_hit_geo<true>(sc, tri, r, 0.0, DINF, lh);
-    object_fix_hit(L, lh);
+    object_record(sc, L, tri, r, lh);
     return true;
 }
 
@@ -863,13 +918,47 @@ __device__ __forceinline__ int sample_light(const DScene& sc, double u) {
     const double fr = rfract(x);
     return fr < sc.alias_prob[idx] ? idx : sc.alias_idx[idx];
 }
-__device__ __forceinline__ V3 light_sample_towards(const DScene& sc, const lumo_object& L, V3 xo, V2 rs) {
-    const V3 xi = ld3(L.origin) + rs.x * ld3(L.b0) + rs.y * ld3(L.b1);
-    return normalize(xi - xo);
+// Sampleable::sample_on -> point (rectangle.rs:113-125, triangle.rs:214-240)
+__device__ __forceinline__ V3 shape_sample_on(const DScene& sc, const lumo_object& L, V2 rs) {
+    if (L.type == LUMO_OBJ_TRIANGLE) {
+        const lumo_triangle T = sc.tris[L.tri_base];
+        const V3 A = ld3(sc.vertices + 3 * T.v[0]), B = ld3(sc.vertices + 3 * T.v[1]),
+                 Cv = ld3(sc.vertices + 3 * T.v[2]);
+        const double gam = 1.0 - sqrt(1.0 - rs.x);
+        const double beta = rs.y * (1.0 - gam);
+        return A + beta * (B - A) + gam * (Cv - A);
+    }
+    return ld3(L.origin) + rs.x * ld3(L.b0) + rs.y * ld3(L.b1);
 }
-__device__ __forceinline__ double light_pdf(const lumo_object& L, const RayX& ri, V3 xi, V3 ng) {
+__device__ __forceinline__ double shape_pdf(const lumo_object& L, V3 xo, V3 wi, V3 xi, V3 ng) {
     const double p_area = 1.0 / L.area;
-    return p_area * distance_squared(ri.o, xi) / fabs(dot(ng, ri.d));
+    return p_area * distance_squared(xo, xi) / fabs(dot(ng, wi));
+}
+// Sampleable::sample_towards (object.rs:138-141; Instance: instance.rs:162-167)
+__device__ V3 light_sample_towards(const DScene& sc, const lumo_object& L, V3 xo, V2 rs) {
+    if (L.xform < 0) return normalize(shape_sample_on(sc, L, rs) - xo);
+    const lumo_transform& T = sc.xforms[L.xform];
+    const V3 xl = xf_apply(T.inv, xo, 1.0);
+    const V3 dl = normalize(shape_sample_on(sc, L, rs) - xl);
+    return normalize(xf_apply(T.m, dl, 0.0));
+}
+// Sampleable::sample_towards_pdf (object.rs:149-156; Instance: instance.rs:169-199)
+__device__ double light_pdf(const DScene& sc, const lumo_object& L, const RayX& ri, V3 xi, V3 ng) {
+    if (L.xform < 0) return shape_pdf(L, ri.o, ri.d, xi, ng);
+    const lumo_transform& T = sc.xforms[L.xform];
+    const M3 N{V3{T.nrm[0], T.nrm[1], T.nrm[2]}, V3{T.nrm[3], T.nrm[4], T.nrm[5]}, V3{T.nrm[6], T.nrm[7], T.nrm[8]}};
+    const M3 nti = m3_transpose(m3_inv(N));
+    const V3 ng_l = normalize(m3_mul_vec(nti, ng));
+    const V3 xi_l = xf_apply(T.inv, xi, 1.0);
+    const V3 xo_l = xf_apply(T.inv, ri.o, 1.0);
+    const V3 wi_l = normalize(xf_apply(T.inv, ri.d, 0.0));
+    const double pdf_l = shape_pdf(L, xo_l, wi_l, xi_l, ng_l);
+    const double height = fabs(dot(ng, xf_apply(T.m, ng_l, 0.0)));
+    const M3 m3{V3{T.m[0], T.m[1], T.m[2]}, V3{T.m[4], T.m[5], T.m[6]}, V3{T.m[8], T.m[9], T.m[10]}};
+    const double jacobian = fabs(m3_det(m3)) / height;
+    const double sa_conv = distance_squared(ri.o, xi) * fabs(dot(wi_l, ng_l)) /
+                           (distance_squared(xo_l, xi_l) * fabs(dot(ri.d, ng)));
+    return pdf_l * sa_conv / jacobian;
 }
 
 }  // namespace dev

@@ -313,13 +313,14 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
             const double rand_u = xs_float(rng);
             const V2 sq = xs_vec2(rng);
             V3 wi;
-            if (!bsdf_sample(sc, m, ho, wo, L, rand_u, sq, wi)) {
+            const bool sampled = bsdf_sample(sc, m, ho, wo, L, rand_u, sq, wi);
+            if (m.kind == LUMO_MAT_MF_DIELECTRIC && !(m.flags & LUMO_MATF_CONSTANT_ETA)) {
+                for (int i = 1; i < NS; ++i) S.lam[4 * s + i] = 0.0;  // lambda terminated (even if None)
+            }
+            if (!sampled) {
                 if (S.flags[s] & 1u) radiance = radiance + gathered * emit(sc, m, L, ho.backface);
                 stc(S.rad, s, radiance);
             } else {
-                if (m.kind == LUMO_MAT_MF_DIELECTRIC && !(m.flags & LUMO_MATF_CONSTANT_ETA)) {
-                    for (int i = 1; i < NS; ++i) S.lam[4 * s + i] = 0.0;  // lambda terminated
-                }
                 // NEE: n_shadow x [light pick, light direction, BSDF sample] (integrator.rs:87-137)
                 if (!mat_is_delta(sc, m, L)) {
                     const int base = s * 2 * ns;
@@ -419,7 +420,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0,
         DColor out = cfill(0.0);
         if (scene_hit_light<STK>(sc, ri, li, hi, C)) {
             const lumo_object& Lo = sc.lights[li];
-            const double p_lig = light_pdf(Lo, ri, hi.p, hi.ng);
+            const double p_lig = light_pdf(sc, Lo, ri, hi.p, hi.ng);
             const double p_sct = S.sh_psct[rec];
             if (!(p_lig == 0.0 || p_sct == 0.0)) {  // mis_sample (integrator.rs:139-184)
                 double L[NS];
@@ -1082,11 +1083,21 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     if (!c || !d) return LUMO_ERR_INVALID;
     if (d->num_lights <= 0 || d->num_light_nodes <= 0 || d->num_dense_spectra < 3 || !d->materials) return LUMO_ERR_INVALID;
     for (int i = 0; i < d->num_materials; ++i) {
-        const int k = d->materials[i].kind;
-        if (k != LUMO_MAT_LAMBERTIAN && k != LUMO_MAT_LIGHT && k != LUMO_MAT_BLANK) return LUMO_ERR_UNSUPPORTED;
+        const lumo_material& m = d->materials[i];
+        if (m.kind < LUMO_MAT_BLANK || m.kind > LUMO_MAT_MF_DIELECTRIC) return LUMO_ERR_UNSUPPORTED;
+        if (m.kind >= LUMO_MAT_MF_DIFFUSE &&
+            (m.eta_idx < 0 || m.eta_idx >= d->num_dense_spectra || m.k_idx < 0 || m.k_idx >= d->num_dense_spectra ||
+             !(m.roughness > 0.0 && m.roughness <= 1.0)))
+            return LUMO_ERR_INVALID;
+        if (m.kind == LUMO_MAT_LIGHT && (m.illuminant < 0 || m.illuminant >= d->num_dense_spectra))
+            return LUMO_ERR_INVALID;
     }
-    for (int i = 0; i < d->num_lights; ++i)
-        if (d->lights[i].type != LUMO_OBJ_RECTANGLE) return LUMO_ERR_UNSUPPORTED;
+    for (int i = 0; i < d->num_lights + d->num_objects; ++i) {
+        const lumo_object& o = i < d->num_lights ? d->lights[i] : d->objects[i - d->num_lights];
+        if (o.type < LUMO_OBJ_KDMESH || o.type > LUMO_OBJ_TRIANGLE) return LUMO_ERR_UNSUPPORTED;
+        if (o.xform >= d->num_transforms || (o.xform >= 0 && !d->transforms)) return LUMO_ERR_INVALID;
+        if (o.type == LUMO_OBJ_TRIANGLE && (o.tri_base < 0 || o.tri_base >= d->num_triangles)) return LUMO_ERR_INVALID;
+    }
     HIPCHK(hipSetDevice(c->device));
     free_scene(*c);
     DScene& s = c->sc;
@@ -1111,6 +1122,7 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     chk(upload(*c, d->alias_pdf, (size_t)d->num_lights, &s.alias_pdf));
     chk(upload(*c, d->materials, (size_t)d->num_materials, &s.mats));
     chk(upload(*c, d->dense_spectra, (size_t)95 * d->num_dense_spectra, &s.dense));
+    chk(upload(*c, d->transforms, (size_t)d->num_transforms, &s.xforms));
     if (st) {
         free_scene(*c);
         return st;
@@ -1136,6 +1148,7 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         s.off_kd_items = put(d->kd_items, sizeof(int32_t) * d->num_kd_items);
         s.off_tris = put(d->triangles, sizeof(lumo_triangle) * d->num_triangles);
         s.off_vertices = put(d->vertices, sizeof(double) * 3 * d->num_vertices);
+        s.off_xforms = put(d->transforms, sizeof(lumo_transform) * d->num_transforms);
         s.hot_bytes = 0;
         if (hot.size() <= 48 * 1024) {
             const char* dp = nullptr;

@@ -93,6 +93,18 @@ int lumo_builder_add_rectangle(void* b, const double* a, const double* bb, const
     sb->add_rectangle(v3p(a), v3p(bb), v3p(c), material, as_light != 0);
     return LUMO_OK;
 }
+int lumo_builder_instance_op(void* b, int is_light, int64_t index, int op, double x, double y, double z) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb) return LUMO_ERR_INVALID;
+    std::vector<HostObject>& v = is_light ? sb->lights : sb->objects;
+    if (index < 0 || index >= (int64_t)v.size()) return LUMO_ERR_INVALID;
+    return instance_op(v[index], op, x, y, z) ? LUMO_OK : LUMO_ERR_INVALID;
+}
+int64_t lumo_builder_count(void* b, int is_light) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb) return -1;
+    return (int64_t)(is_light ? sb->lights.size() : sb->objects.size());
+}
 void* lumo_builder_cornell_box(void) { return new SceneBuilder(SceneBuilder::cornell_box()); }
 int lumo_builder_empty_box(void* b, lumo_spectrum def_color, int mat_left, int mat_right) {
     SceneBuilder* sb = static_cast<SceneBuilder*>(b);

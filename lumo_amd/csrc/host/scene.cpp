@@ -585,7 +585,30 @@ void SceneBuilder::add_mesh(const std::vector<V3>& vertices, const std::vector<F
             o.tris.push_back(t);
         }
     }
-    (as_light ? lights : objects).push_back(std::move(o));
+    if (!as_light) {
+        objects.push_back(std::move(o));
+        return;
+    }
+    for (const HostObject::Tri& t : o.tris) {
+        HostObject l;
+        l.type = LUMO_OBJ_TRIANGLE;
+        l.material = material;
+        HostObject::Tri lt = t;
+        for (int k = 0; k < 3; ++k) {
+            l.vertices.push_back(vertices[t.v[k]]);
+            lt.v[k] = k;
+            if (t.n[k] >= 0) {
+                l.normals.push_back(normals[t.n[k]]);
+                lt.n[k] = (int64_t)l.normals.size() - 1;
+            }
+            if (t.t[k] >= 0) {
+                l.uvs.push_back(uvs[t.t[k]]);
+                lt.t[k] = (int64_t)l.uvs.size() - 1;
+            }
+        }
+        l.tris.push_back(lt);
+        lights.push_back(std::move(l));
+    }
 }
 
 void SceneBuilder::add_rectangle(V3 a, V3 b, V3 c, int material, bool as_light) {
@@ -596,7 +619,11 @@ void SceneBuilder::add_rectangle(V3 a, V3 b, V3 c, int material, bool as_light) 
     const V3 d = origin + b0 + b1;
     Face f;
     f.vidx = {0, 1, 2, 3};
-    add_mesh({a, b, c, d}, {f}, {}, {}, material, as_light);
+    add_mesh({a, b, c, d}, {f}, {}, {}, material, false);
+    if (as_light) {
+        lights.push_back(std::move(objects.back()));
+        objects.pop_back();
+    }
     HostObject& o = as_light ? lights.back() : objects.back();
     o.type = LUMO_OBJ_RECTANGLE;
     o.origin = origin;
@@ -742,6 +769,8 @@ lumo_scene_desc FlatScene::desc() const {
     d.num_dense_spectra = (int32_t)(dense.size() / DENSE);
     d.materials = materials.data();
     d.dense_spectra = dense.data();
+    d.num_transforms = (int32_t)transforms.size();
+    d.transforms = transforms.data();
     return d;
 }
 
@@ -775,10 +804,6 @@ double dense_sample_one(const Dense& d, double lambda) {
     const double x1 = (lambda - l0) / STEP;
     const double x0 = 1.0 - x1;
     return d.v[b0] * x0 + d.v[b1] * x1;
-}
-double object_area(const HostObject& o) {
-    if (o.type == LUMO_OBJ_RECTANGLE) return std::fabs(length(cross(o.b0, o.b1)));
-    throw std::runtime_error("light type without area");
 }
 }  // namespace
 
@@ -845,27 +870,61 @@ std::unique_ptr<FlatScene> build_scene(const SceneBuilder& sb) {
                 lt.material = o.material;
                 fs->triangles.push_back(lt);
             }
-            const KdBuilt kd = build_kdtree(o);
-            lo.kd_root = (int32_t)fs->kd_nodes.size();
-            lo.item_base = (int32_t)fs->kd_items.size();
-            for (lumo_kd_node n : kd.nodes) {
-                if (n.right >= 0) n.right += lo.kd_root;
-                fs->kd_nodes.push_back(n);
+            lo.xform = -1;
+            lo.material_override = -1;
+            if (o.type == LUMO_OBJ_TRIANGLE) {
+                lo.kd_root = -1;
+                lo.item_base = -1;
+                V3 mn, mx;
+                shape_bounds(o, mn, mx);
+                lo.bmin[0] = mn.x; lo.bmin[1] = mn.y; lo.bmin[2] = mn.z;
+                lo.bmax[0] = mx.x; lo.bmax[1] = mx.y; lo.bmax[2] = mx.z;
+                const V3 A = o.vertices[o.tris[0].v[0]], B = o.vertices[o.tris[0].v[1]], Cv = o.vertices[o.tris[0].v[2]];
+                lo.area = length(cross(B - A, Cv - A)) / 2.0;  // triangle.rs:208-210
+            } else {
+                const KdBuilt kd = build_kdtree(o);
+                lo.kd_root = (int32_t)fs->kd_nodes.size();
+                lo.item_base = (int32_t)fs->kd_items.size();
+                for (lumo_kd_node n : kd.nodes) {
+                    if (n.right >= 0) n.right += lo.kd_root;
+                    fs->kd_nodes.push_back(n);
+                }
+                for (int32_t it : kd.items) fs->kd_items.push_back(it);
+                lo.bmin[0] = kd.bmin.x; lo.bmin[1] = kd.bmin.y; lo.bmin[2] = kd.bmin.z;
+                lo.bmax[0] = kd.bmax.x; lo.bmax[1] = kd.bmax.y; lo.bmax[2] = kd.bmax.z;
             }
-            for (int32_t it : kd.items) fs->kd_items.push_back(it);
-            lo.bmin[0] = kd.bmin.x; lo.bmin[1] = kd.bmin.y; lo.bmin[2] = kd.bmin.z;
-            lo.bmax[0] = kd.bmax.x; lo.bmax[1] = kd.bmax.y; lo.bmax[2] = kd.bmax.z;
-            V3 bmn = kd.bmin, bmx = kd.bmax;
             if (o.type == LUMO_OBJ_RECTANGLE) {
                 lo.origin[0] = o.origin.x; lo.origin[1] = o.origin.y; lo.origin[2] = o.origin.z;
                 lo.b0[0] = o.b0.x; lo.b0[1] = o.b0.y; lo.b0[2] = o.b0.z;
                 lo.b1[0] = o.b1.x; lo.b1[1] = o.b1.y; lo.b1[2] = o.b1.z;
                 lo.area = std::fabs(length(cross(o.b0, o.b1)));
-                // Rectangle::bounding_box (rectangle.rs:91-102)
-                const V3 a = o.b1 + o.origin, b = o.origin, c = o.b0 + o.origin, d = o.origin + o.b0 + o.b1;
-                bmn = vmin(vmin(vmin(a, b), c), d);
-                bmx = vmax(vmax(vmax(a, b), c), d);
             }
+            if (o.instanced) {
+                lumo_transform t{};
+                const M4* ms[2] = {&o.xf.m, &o.xf.inv};
+                double* outs[2] = {t.m, t.inv};
+                for (int q = 0; q < 2; ++q) {
+                    const V4 rows[4] = {ms[q]->y0, ms[q]->y1, ms[q]->y2, ms[q]->y3};
+                    for (int r = 0; r < 4; ++r) {
+                        outs[q][4 * r] = rows[r].x;
+                        outs[q][4 * r + 1] = rows[r].y;
+                        outs[q][4 * r + 2] = rows[r].z;
+                        outs[q][4 * r + 3] = rows[r].w;
+                    }
+                }
+                const M3 nrm = xf_normal(o.xf);
+                const V3 nr[3] = {nrm.y0, nrm.y1, nrm.y2};
+                for (int r = 0; r < 3; ++r) {
+                    t.nrm[3 * r] = nr[r].x;
+                    t.nrm[3 * r + 1] = nr[r].y;
+                    t.nrm[3 * r + 2] = nr[r].z;
+                }
+                lo.xform = (int32_t)fs->transforms.size();
+                lo.material_override = o.material_override;
+                fs->transforms.push_back(t);
+            }
+            V3 bmn, bmx;
+            world_bounds(o, bmn, bmx);
             bmins.push_back(bmn);
             bmaxs.push_back(bmx);
             dst.push_back(lo);
@@ -898,7 +957,7 @@ std::unique_ptr<FlatScene> build_scene(const SceneBuilder& sb) {
     for (size_t i = 0; i < n; ++i) {
         const HostObject& o = sb.lights[i];
         const HostMaterial& hm = sb.materials[o.material];
-        const double ar = object_area(o);
+        const double ar = world_area(o);
         double p[4];
         for (int k = 0; k < 4; ++k) {
             // Material::power: s * t.power(lambda) * e.sample(lambda), x2 if two-sided
@@ -1066,6 +1125,119 @@ lumo_camera_desc build_camera(const CameraParams& p) {
     d.filter_radius = p.filter_radius;
     d.filter_sigma = p.filter_sigma;
     return d;
+}
+
+// ---------------------------------------------------------------------------------
+// Instances (object/instance.rs, math/transform.rs)
+namespace {
+Xform xf_rotate(int axis, double theta) {  // transform.rs:158-190
+    const double c = lm_cos(theta), sn = lm_sin(theta);
+    if (axis == 0) return xf_mat3(M3{V3{1.0, 0.0, 0.0}, V3{0.0, c, -sn}, V3{0.0, sn, c}});
+    if (axis == 1) return xf_mat3(M3{V3{c, 0.0, sn}, V3{0.0, 1.0, 0.0}, V3{-sn, 0.0, c}});
+    return xf_mat3(M3{V3{c, -sn, 0.0}, V3{sn, c, 0.0}, V3{0.0, 0.0, 1.0}});
+}
+double comp(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+}  // namespace
+
+void shape_bounds(const HostObject& o, V3& mn, V3& mx) {
+    if (o.type == LUMO_OBJ_RECTANGLE) {  // Rectangle::bounding_box (rectangle.rs:91-102)
+        const V3 a = o.b1 + o.origin, b = o.origin, c = o.b0 + o.origin, d = o.origin + o.b0 + o.b1;
+        mn = vmin(vmin(vmin(a, b), c), d);
+        mx = vmax(vmax(vmax(a, b), c), d);
+        return;
+    }
+    // KdTree boundary: merge of the triangle boxes (kdtree.rs:43-89); Triangle::bounding_box
+    bool first = true;
+    for (const HostObject::Tri& t : o.tris) {
+        const V3 a = o.vertices[t.v[0]], b = o.vertices[t.v[1]], c = o.vertices[t.v[2]];
+        const V3 tmn = vmin(a, vmin(b, c)), tmx = vmax(a, vmax(b, c));
+        mn = first ? tmn : vmin(mn, tmn);
+        mx = first ? tmx : vmax(mx, tmx);
+        first = false;
+    }
+}
+
+void world_bounds(const HostObject& o, V3& mn, V3& mx) {
+    shape_bounds(o, mn, mx);
+    if (!o.instanced) return;
+    // Graphics Gems I, transforming axis-aligned bounding boxes (instance.rs:107-127)
+    const M4& m = o.xf.m;
+    V3 lo{m.y0.w, m.y1.w, m.y2.w}, hi = lo;
+    const V4 rows[3] = {m.y0, m.y1, m.y2};
+    for (int a = 0; a < 3; ++a) {
+        const V3 ri = truncate(rows[a]);
+        const V3 a0 = ri * mn, a1 = ri * mx;
+        const double mi = dot(vmin(a0, a1), V3{1.0, 1.0, 1.0});
+        const double ma = dot(vmax(a0, a1), V3{1.0, 1.0, 1.0});
+        if (a == 0) { lo.x += mi; hi.x += ma; }
+        if (a == 1) { lo.y += mi; hi.y += ma; }
+        if (a == 2) { lo.z += mi; hi.z += ma; }
+    }
+    mn = lo;
+    mx = hi;
+}
+
+bool instance_op(HostObject& o, int op, double x, double y, double z) {
+    Xform t;
+    if (op == INST_TO_UNIT_SIZE) {  // kdtree.rs:93-99 (defined on the kd-tree itself)
+        if (o.instanced) return false;
+        V3 mn, mx;
+        shape_bounds(o, mn, mx);
+        const V3 dim = mx - mn;
+        const double s = 1.0 / rmax(dim.x, rmax(dim.y, dim.z));
+        return instance_op(o, INST_SCALE, s, s, s);
+    }
+    if (!o.instanced) {  // Instance::new: identity
+        o.instanced = true;
+        o.xf = Xform{m4_id(), m4_id()};
+    }
+    V3 mn, mx;
+    switch (op) {
+        case INST_TRANSLATE: t = xf_translation(x, y, z); break;
+        case INST_SCALE:
+            if (x * y * z == 0.0) return false;  // instance.rs:267 assert
+            t = xf_scale(x, y, z);
+            break;
+        case INST_ROTATE_X: t = xf_rotate(0, x); break;
+        case INST_ROTATE_Y: t = xf_rotate(1, x); break;
+        case INST_ROTATE_Z: t = xf_rotate(2, x); break;
+        case INST_TO_ORIGIN: {  // instance.rs:54-59
+            world_bounds(o, mn, mx);
+            const V3 mid = -(mn + mx) / 2.0;
+            t = xf_translation(mid.x, mid.y, mid.z);
+            break;
+        }
+        case INST_SET_X:
+        case INST_SET_Y:
+        case INST_SET_Z: {  // instance.rs:61-80
+            world_bounds(o, mn, mx);
+            const int a = op - INST_SET_X;
+            const double d = x - comp(mn, a);
+            t = xf_translation(a == 0 ? d : 0.0, a == 1 ? d : 0.0, a == 2 ? d : 0.0);
+            break;
+        }
+        default: return false;
+    }
+    o.xf = xf_mul(t, o.xf);  // "apply AFTER current transformations"
+    return true;
+}
+
+double world_area(const HostObject& o) {
+    double a;
+    if (o.type == LUMO_OBJ_RECTANGLE) {
+        a = std::fabs(length(cross(o.b0, o.b1)));
+    } else if (o.type == LUMO_OBJ_TRIANGLE) {
+        const V3 A = o.vertices[o.tris[0].v[0]], B = o.vertices[o.tris[0].v[1]], Cv = o.vertices[o.tris[0].v[2]];
+        a = length(cross(B - A, Cv - A)) / 2.0;
+    } else {
+        throw std::runtime_error("light shape without area (meshes become per-triangle lights)");
+    }
+    if (!o.instanced) return a;
+    const M3 mt = m3_transpose(m4_to_m3(o.xf.m));  // Transform::to_scale
+    const V3 sc{length(mt.y0), length(mt.y1), length(mt.y2)};
+    if (std::fabs(sc.x - sc.y) + std::fabs(sc.y - sc.z) > EPSILON)
+        throw std::runtime_error("light instance with non-uniform scale (instance.rs:137-140)");
+    return sc.x * sc.y * a;
 }
 
 }  // namespace lumo

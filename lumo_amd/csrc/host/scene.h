@@ -54,7 +54,25 @@ struct HostObject {
     };
     std::vector<Tri> tris;
     V3 origin{}, b0{}, b1{};        // Rectangle
+    // Instance (object/instance.rs): local->world transform applied to the shape
+    bool instanced = false;
+    Xform xf{};
+    int material_override = -1;
 };
+
+// Instanceable / Instance transformations (instance.rs:203-299, kdtree.rs:93-99)
+enum {
+    INST_TRANSLATE = 0, INST_SCALE, INST_ROTATE_X, INST_ROTATE_Y, INST_ROTATE_Z, INST_TO_UNIT_SIZE, INST_TO_ORIGIN,
+    INST_SET_X, INST_SET_Y, INST_SET_Z
+};
+// Object::bounding_box of the shape itself (kd boundary, Rectangle / Triangle formulas)
+void shape_bounds(const HostObject& o, V3& mn, V3& mx);
+// bounding box in world space (Instance::bounding_box, instance.rs:107-127, if instanced)
+void world_bounds(const HostObject& o, V3& mn, V3& mx);
+// Apply one Instanceable op; false if invalid (zero scale, to_unit_size of an instance).
+bool instance_op(HostObject& o, int op, double x, double y, double z);
+// Sampleable::area in world space (instance.rs:133-143: uniform scale only)
+double world_area(const HostObject& o);
 
 struct KdBuilt {
     std::vector<lumo_kd_node> nodes;
@@ -79,6 +97,7 @@ class SceneBuilder {
 
     int add_material(const HostMaterial& m);
     // TriangleMesh::new (triangle_mesh.rs:46-60): fan-triangulated faces, degenerate dropped.
+    // As a light, every triangle becomes its own Triangle light (parser/obj.rs:93-103).
     void add_mesh(const std::vector<V3>& vertices, const std::vector<Face>& faces,
                   const std::vector<V3>& normals, const std::vector<V2>& uvs, int material, bool as_light = false);
     // Rectangle::new(Mat3(a, b, c), material) (rectangle.rs:23-45)
@@ -104,6 +123,7 @@ struct FlatScene {
     std::vector<int32_t> alias_idx;
     std::vector<lumo_material> materials;
     std::vector<double> dense;
+    std::vector<lumo_transform> transforms;
     lumo_scene_desc desc() const;
 };
 

@@ -73,6 +73,15 @@ int oracle_bsdf_eval(const lumo_scene_desc* scene, int material, const double* w
 int oracle_furnace(const lumo_scene_desc* scene, int material, const double* wo, size_t n, uint64_t seed,
                    double* out4);
 
+/* Light sampling probes (object.rs:138-156, instance.rs:162-199): for light `light` seen from
+ * point xo, oracle_light_sample draws n directions with sample_towards (rng Xorshift::new(seed));
+ * oracle_light_pdf returns sample_towards_pdf for each direction whose ray hits the light
+ * (Object::hit from xo), else 0. */
+int oracle_light_sample(const lumo_scene_desc* scene, int light, const double* xo, size_t n, uint64_t seed,
+                        double* wi3);
+int oracle_light_pdf(const lumo_scene_desc* scene, int light, const double* xo, const double* wi3, size_t n,
+                     double* pdf);
+
 #ifdef __cplusplus
 }
 #endif

@@ -365,9 +365,37 @@ bool kdtree_hit(const Scene& sc, const lumo_object& ob, const Ray& r, double t_m
     return true;
 }
 
-// Object::hit / hit_t for the flattened object kinds
-bool object_hit(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, Hit* out,
-                Counters& C) {
+// ---- Instance (object/instance.rs:81-105), transforms (math/transform.rs)
+Xform xform_of(const lumo_transform& t) {
+    auto row = [](const double* m, int r) { return V4{m[4 * r], m[4 * r + 1], m[4 * r + 2], m[4 * r + 3]}; };
+    return Xform{M4{row(t.m, 0), row(t.m, 1), row(t.m, 2), row(t.m, 3)},
+                 M4{row(t.inv, 0), row(t.inv, 1), row(t.inv, 2), row(t.inv, 3)}};
+}
+M3 nrm_of(const lumo_transform& t) {
+    return M3{V3{t.nrm[0], t.nrm[1], t.nrm[2]}, V3{t.nrm[3], t.nrm[4], t.nrm[5]}, V3{t.nrm[6], t.nrm[7], t.nrm[8]}};
+}
+M4 m4_abs(const M4& m) {
+    auto a = [](V4 v) { return V4{fabs(v.x), fabs(v.y), fabs(v.z), fabs(v.w)}; };
+    return M4{a(m.y0), a(m.y1), a(m.y2), a(m.y3)};
+}
+// Ray::transform::<NORMALIZE> (ray.rs:24-31)
+Ray ray_to_local(const Xform& X, const Ray& r, bool normalize_dir) {
+    const V3 d = xf_dir_inv(X, r.dir);
+    return Ray{xf_pt_inv(X, r.origin), normalize_dir ? normalize(d) : d};
+}
+// Instance::propagate_fp_err (instance.rs:40-51)
+V3 propagate_fp_err(const Xform& X, V3 xo, V3 fp_error) {
+    const M4 a = m4_abs(X.m);
+    const V3 e3 = vabs(fp_error), p3 = vabs(xo);
+    const V3 base = gamma_n(3) * project(m4_mul_vec(a, extend(p3, 1.0)));
+    if (e3.x == 0.0 && e3.y == 0.0 && e3.z == 0.0) return base;
+    return base + (gamma_n(3) + 1.0) * project(m4_mul_vec(a, extend(e3, 0.0)));
+}
+
+// Object::hit / hit_t of the shape in its own space
+bool shape_hit(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, Hit* out,
+               Counters& C) {
+    if (ob.type == LUMO_OBJ_TRIANGLE) return triangle_hit(sc, ob.tri_base, r, t_min, t_max, true, out, C) != INF;
     if (!kdtree_hit(sc, ob, r, t_min, t_max, true, out, nullptr, C)) return false;
     if (ob.type == LUMO_OBJ_RECTANGLE) {  // rectangle.rs:74-85
         const V3 b0{ob.b0[0], ob.b0[1], ob.b0[2]}, b1{ob.b1[0], ob.b1[1], ob.b1[2]};
@@ -375,10 +403,32 @@ bool object_hit(const Scene& sc, const lumo_object& ob, const Ray& r, double t_m
     }
     return true;
 }
-double object_hit_t(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, Counters& C) {
+double shape_hit_t(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, Counters& C) {
+    if (ob.type == LUMO_OBJ_TRIANGLE) {  // triangle.rs:195-197
+        Hit dummy;
+        return triangle_hit(sc, ob.tri_base, r, t_min, t_max, false, &dummy, C);
+    }
     double t = INF;
     if (!kdtree_hit(sc, ob, r, t_min, t_max, false, nullptr, &t, C)) return INF;
     return t;
+}
+bool object_hit(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, Hit* out,
+                Counters& C) {
+    if (ob.xform < 0) return shape_hit(sc, ob, r, t_min, t_max, out, C);
+    const lumo_transform& T = sc.d->transforms[ob.xform];
+    const Xform X = xform_of(T);
+    if (!shape_hit(sc, ob, ray_to_local(X, r, false), t_min, t_max, out, C)) return false;
+    const M3 N = nrm_of(T);
+    out->ns = normalize(m3_mul_vec(N, out->ns));
+    out->ng = normalize(m3_mul_vec(N, out->ng));
+    out->fp_error = propagate_fp_err(X, out->p, out->fp_error);
+    if (ob.material_override >= 0) out->material = ob.material_override;
+    out->p = xf_pt(X, out->p);
+    return true;
+}
+double object_hit_t(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, Counters& C) {
+    if (ob.xform < 0) return shape_hit_t(sc, ob, r, t_min, t_max, C);
+    return shape_hit_t(sc, ob, ray_to_local(xform_of(sc.d->transforms[ob.xform]), r, false), t_min, t_max, C);
 }
 
 // bvh.rs:315-362. Returns index or -1.
@@ -913,14 +963,51 @@ int sample_light(const Scene& sc, double rand_u) {
     const double fr = rfract(u);
     return fr < sc.d->alias_prob[idx] ? (int)idx : sc.d->alias_idx[idx];
 }
-V3 light_sample_on(const lumo_object& L, V2 rs) {  // Rectangle::sample_on -> point only
+// Sampleable::sample_on -> point (rectangle.rs:113-125, triangle.rs:214-240)
+V3 shape_sample_on(const Scene& sc, const lumo_object& L, V2 rs) {
+    if (L.type == LUMO_OBJ_TRIANGLE) {
+        const lumo_triangle& T = sc.d->triangles[L.tri_base];
+        const V3 A = sc.vert(T.v[0]), B = sc.vert(T.v[1]), Cv = sc.vert(T.v[2]);
+        const double gam = 1.0 - std::sqrt(1.0 - rs.x);
+        const double beta = rs.y * (1.0 - gam);
+        return A + beta * (B - A) + gam * (Cv - A);
+    }
     const V3 o{L.origin[0], L.origin[1], L.origin[2]}, b0{L.b0[0], L.b0[1], L.b0[2]}, b1{L.b1[0], L.b1[1], L.b1[2]};
     return o + rs.x * b0 + rs.y * b1;
 }
-V3 light_sample_towards(const lumo_object& L, V3 xo, V2 rs) { return normalize(light_sample_on(L, rs) - xo); }
-double light_sample_towards_pdf(const lumo_object& L, const Ray& ri, V3 xi, V3 ng) {
+// Sampleable::sample_towards / sample_towards_pdf (object.rs:138-156)
+V3 shape_sample_towards(const Scene& sc, const lumo_object& L, V3 xo, V2 rs) {
+    return normalize(shape_sample_on(sc, L, rs) - xo);
+}
+double shape_sample_towards_pdf(const lumo_object& L, const Ray& ri, V3 xi, V3 ng) {
     const double p_area = 1.0 / L.area;
     return p_area * distance_squared(ri.origin, xi) / fabs(dot(ng, ri.dir));
+}
+// Instance<T: Sampleable> (instance.rs:162-199)
+V3 light_sample_towards(const Scene& sc, const lumo_object& L, V3 xo, V2 rs) {
+    if (L.xform < 0) return shape_sample_towards(sc, L, xo, rs);
+    const Xform X = xform_of(sc.d->transforms[L.xform]);
+    const V3 xo_local = xf_pt_inv(X, xo);
+    const V3 dir_local = shape_sample_towards(sc, L, xo_local, rs);
+    return normalize(xf_dir(X, dir_local));
+}
+double light_sample_towards_pdf(const Scene& sc, const lumo_object& L, const Ray& ri, V3 xi, V3 ng) {
+    if (L.xform < 0) return shape_sample_towards_pdf(L, ri, xi, ng);
+    const lumo_transform& T = sc.d->transforms[L.xform];
+    const Xform X = xform_of(T);
+    const M3 nti = m3_transpose(m3_inv(nrm_of(T)));
+    const V3 ng_local = normalize(m3_mul_vec(nti, ng));
+    const V3 xi_local = xf_pt_inv(X, xi);
+    const Ray ri_local = ray_to_local(X, ri, true);
+    const V3 wi = ri.dir, wi_local = ri_local.dir;
+    const V3 xo = ri.origin, xo_local = ri_local.origin;
+    const double pdf_local = shape_sample_towards_pdf(L, ri_local, xi_local, ng_local);
+    const double height = fabs(dot(ng, xf_dir(X, ng_local)));
+    const double volume = fabs(m3_det(m4_to_m3(X.m)));
+    const double jacobian = volume / height;
+    const double sa_conv = distance_squared(xo, xi) * fabs(dot(wi_local, ng_local)) /
+                           (distance_squared(xo_local, xi_local) * fabs(dot(wi, ng)));
+    return pdf_local * sa_conv / jacobian;
 }
 
 // ------------------------------------------------------------------ integrator
@@ -945,12 +1032,12 @@ Color single_shadow_ray(const Scene& sc, V3 wo, Lambda& L, const Hit& ho, Xorshi
     Color radiance = cconst(0.0);
     {
         const V2 rs = xs_vec2(rng);
-        const V3 wi = light_sample_towards(light, xo, rs);
+        const V3 wi = light_sample_towards(sc, light, xo, rs);
         const Ray ri = generate_ray(ho, wi);
         Hit hi;
         Color add = cconst(0.0);
         if (scene_hit_light(sc, ri, li, &hi, C)) {
-            const double p_lig = light_sample_towards_pdf(light, ri, hi.p, hi.ng);
+            const double p_lig = light_sample_towards_pdf(sc, light, ri, hi.p, hi.ng);
             const double p_sct = bsdf_pdf(sc, ho, wo, wi, L);
             add = mis_sample(sc, wo, wi, ho, hi, L, true, p_lig, p_sct);
         }
@@ -965,7 +1052,7 @@ Color single_shadow_ray(const Scene& sc, V3 wo, Lambda& L, const Hit& ho, Xorshi
             const Ray ri = generate_ray(ho, wi);
             Hit hi;
             if (scene_hit_light(sc, ri, li, &hi, C)) {
-                const double p_lig = light_sample_towards_pdf(light, ri, hi.p, hi.ng);
+                const double p_lig = light_sample_towards_pdf(sc, light, ri, hi.p, hi.ng);
                 const double p_sct = bsdf_pdf(sc, ho, wo, wi, L);
                 add = mis_sample(sc, wo, wi, ho, hi, L, false, p_lig, p_sct);
             }
@@ -1476,5 +1563,34 @@ extern "C" int oracle_furnace(const lumo_scene_desc* scene, int material, const 
     const Color pdf = wl_pdf(L);
     const Color r = radiance * pdf / (pdf * (double)(n - misses));
     for (int k = 0; k < NS; ++k) out4[k] = r.s[k];
+    return LUMO_OK;
+}
+
+extern "C" int oracle_light_sample(const lumo_scene_desc* scene, int light, const double* xo, size_t n, uint64_t seed,
+                                   double* wi3) {
+    if (!scene || !xo || !wi3 || light < 0 || light >= scene->num_lights) return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    Xorshift rng = xs_new(seed);
+    const V3 o{xo[0], xo[1], xo[2]};
+    for (size_t i = 0; i < n; ++i) {
+        const V3 w = light_sample_towards(sc, scene->lights[light], o, xs_vec2(rng));
+        wi3[3 * i] = w.x;
+        wi3[3 * i + 1] = w.y;
+        wi3[3 * i + 2] = w.z;
+    }
+    return LUMO_OK;
+}
+
+extern "C" int oracle_light_pdf(const lumo_scene_desc* scene, int light, const double* xo, const double* wi3, size_t n,
+                                double* pdf) {
+    if (!scene || !xo || !wi3 || !pdf || light < 0 || light >= scene->num_lights) return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    Counters C;
+    const lumo_object& L = scene->lights[light];
+    for (size_t i = 0; i < n; ++i) {
+        const Ray r = ray_new(V3{xo[0], xo[1], xo[2]}, V3{wi3[3 * i], wi3[3 * i + 1], wi3[3 * i + 2]});
+        Hit h;
+        pdf[i] = object_hit(sc, L, r, 0.0, INF, &h, C) ? light_sample_towards_pdf(sc, L, r, h.p, h.ng) : 0.0;
+    }
     return LUMO_OK;
 }

@@ -45,6 +45,10 @@ def load(path=None):
         lib.oracle_bsdf_eval.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, dp, dp, C.c_size_t, dp, dp]
         lib.oracle_furnace.restype = C.c_int
         lib.oracle_furnace.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, C.c_size_t, C.c_uint64, dp]
+        lib.oracle_light_sample.restype = C.c_int
+        lib.oracle_light_sample.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, C.c_size_t, C.c_uint64, dp]
+        lib.oracle_light_pdf.restype = C.c_int
+        lib.oracle_light_pdf.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, dp, C.c_size_t, dp]
         _libs[path] = lib
     return _libs[path]
 
@@ -133,3 +137,18 @@ def furnace(scene_desc, material, wo, n, seed):
     out = np.zeros(4)
     assert load().oracle_furnace(C.byref(scene_desc), material, _dp(wo), n, seed, _dp(out)) == 0
     return out
+
+
+def light_sample(scene_desc, light, xo, n, seed):
+    xo = np.ascontiguousarray(xo, dtype=np.float64)
+    wi = np.zeros((n, 3))
+    assert load().oracle_light_sample(C.byref(scene_desc), light, _dp(xo), n, seed, _dp(wi)) == 0
+    return wi
+
+
+def light_pdf(scene_desc, light, xo, wi):
+    xo = np.ascontiguousarray(xo, dtype=np.float64)
+    wi = np.ascontiguousarray(wi, dtype=np.float64).reshape(-1, 3)
+    pdf = np.zeros(len(wi))
+    assert load().oracle_light_pdf(C.byref(scene_desc), light, _dp(xo), _dp(wi), len(wi), _dp(pdf)) == 0
+    return pdf
