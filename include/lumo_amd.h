@@ -94,8 +94,10 @@ typedef struct {
 enum {
     LUMO_OBJ_KDMESH = 0,    /* KdTree<Triangle> (TriangleMesh::new, triangle_mesh.rs:46-60) */
     LUMO_OBJ_RECTANGLE = 1, /* Rectangle (object/rectangle.rs): 2-triangle kd mesh + uv/sampling */
-    LUMO_OBJ_TRIANGLE = 2   /* a single Triangle (object/triangle.rs), e.g. an emissive OBJ face
+    LUMO_OBJ_TRIANGLE = 2,  /* a single Triangle (object/triangle.rs), e.g. an emissive OBJ face
                                added as a light (parser/obj.rs:93-103)                       */
+    LUMO_OBJ_SPHERE = 3     /* Sphere at the local origin (object/sphere.rs), e.g. the
+                               environment light of Scene::build (scene.rs:33-52)            */
 };
 
 /* Instance transform (object/instance.rs, math/transform.rs): row-major 4x4 local->world `m`,
@@ -119,6 +121,7 @@ typedef struct {
     double bmin[3], bmax[3]; /* kd boundary in the shape's own space (KdTree::boundary) */
     double origin[3], b0[3], b1[3]; /* Rectangle parameters (rectangle.rs:6-13) */
     double area;       /* Sampleable::area of the shape (own space)      */
+    double radius;     /* Sphere radius                                  */
 } lumo_object;
 
 typedef struct {

@@ -40,6 +40,11 @@ int lumo_builder_add_mesh(void* b, const double* vertices, int64_t nv, const int
 /* Rectangle::new(Mat3(a, b, c), material) */
 int lumo_builder_add_rectangle(void* b, const double* a, const double* bb, const double* c, int material,
                                int as_light);
+/* Sphere::new(radius, material) centred at the origin (object/sphere.rs); position it with
+ * lumo_builder_instance_op.  Returns LUMO_OK or LUMO_ERR_INVALID (radius 0 / bad material). */
+int lumo_builder_add_sphere(void* b, double radius, int material, int as_light);
+/* Scene::set_environment_map(Texture::from(tex), scale) (scene.rs:73-78). */
+int lumo_builder_set_environment_map(void* b, lumo_spectrum tex, double scale);
 /* Instanceable / Instance transformations (object/instance.rs:203-299, kdtree.rs:93-99) applied to
  * object `index` of builder b (lights if is_light).  Each op composes AFTER the current transform;
  * rotations take the angle in x (radians).  Returns LUMO_OK or LUMO_ERR_INVALID. */
@@ -87,7 +92,7 @@ int64_t lumo_make_tasks(int64_t width, int64_t height, uint64_t samples, uint64_
                         int64_t cap);
 
 /* Test hook: evaluate the render path's deterministic transcendentals (lmath.h) on the host.
- * which: 0 exp, 1 log1p, 2 cosh, 3 sin, 4 cos, 5 atan. */
+ * which: 0 exp, 1 log1p, 2 cosh, 3 sin, 4 cos, 5 atan, 6 acos. */
 void lumo_lmath(int which, const double* x, double* y, int64_t n);
 
 #ifdef __cplusplus

@@ -250,6 +250,19 @@ class Scene:
         self._flat = None
         return ObjectRef(self, lib().lumo_builder_count(self._b, int(light)) - 1, light)
 
+    def add_sphere(self, radius, material, light=False):
+        """Sphere::new(radius, material) at the origin (object/sphere.rs); returns an ObjectRef
+        for translate / scale (Instanceable)."""
+        m = self._mat(material)
+        check(lib().lumo_builder_add_sphere(self._b, float(radius), m, int(light)), "add_sphere")
+        self._flat = None
+        return ObjectRef(self, lib().lumo_builder_count(self._b, int(light)) - 1, light)
+
+    def set_environment_map(self, tex, scale):
+        """Scene::set_environment_map (scene.rs:73-78): constant-texture environment light."""
+        check(lib().lumo_builder_set_environment_map(self._b, tex._s, float(scale)), "environment map")
+        self._flat = None
+
     def build(self):
         if self._flat is None:
             p = lib().lumo_builder_build(self._b)

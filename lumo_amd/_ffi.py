@@ -50,7 +50,7 @@ class Object(C.Structure):
                 ("item_base", C.c_int32), ("num_tris", C.c_int32), ("xform", C.c_int32),
                 ("material_override", C.c_int32), ("bmin", C.c_double * 3),
                 ("bmax", C.c_double * 3), ("origin", C.c_double * 3), ("b0", C.c_double * 3),
-                ("b1", C.c_double * 3), ("area", C.c_double)]
+                ("b1", C.c_double * 3), ("area", C.c_double), ("radius", C.c_double)]
 
 
 class Triangle(C.Structure):
@@ -170,6 +170,8 @@ HOST_API = [
     ("lumo_builder_instance_op", C.c_int, [C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_double, C.c_double,
                                            C.c_double]),
     ("lumo_builder_count", C.c_int64, [C.c_void_p, C.c_int]),
+    ("lumo_builder_add_sphere", C.c_int, [C.c_void_p, C.c_double, C.c_int, C.c_int]),
+    ("lumo_builder_set_environment_map", C.c_int, [C.c_void_p, Spectrum, C.c_double]),
     ("lumo_builder_add_mesh", C.c_int, [C.c_void_p, c_double_p, C.c_int64, c_int64_p, c_int64_p, C.c_int64,
                                         C.c_int, C.c_int]),
     ("lumo_builder_add_rectangle", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p, C.c_int, C.c_int]),

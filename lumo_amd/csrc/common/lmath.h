@@ -1,4 +1,4 @@
-// Deterministic f64 transcendentals for the render path (exp, log1p, cosh, sin, cos, atan2).
+// Deterministic f64 transcendentals for the render path (exp, log1p, cosh, sin, cos, atan2, acos).
 //
 // lumo calls Rust std (`f64::exp/cos/sin/cosh`, `atanh` = 0.5*ln_1p(..)), i.e. the platform
 // libm.  Device libm (ROCm ocml) and glibc differ by an ulp on some inputs, and in the Cornell
@@ -306,6 +306,44 @@ LUMO_HD double lm_atan2(double y, double x) {
         case 2: return pi - (z - pi_lo);
         default: return (z - pi_lo) - pi;
     }
+}
+
+// musl / fdlibm e_acos.c
+LUMO_HD double lm_acos_R(double z) {
+    const double pS0 = 1.66666666666666657415e-01, pS1 = -3.25565818622400915405e-01,
+                 pS2 = 2.01212532134862925881e-01, pS3 = -4.00555345006794114027e-02,
+                 pS4 = 7.91534994289814532176e-04, pS5 = 3.47933107596021167570e-05,
+                 qS1 = -2.40339491173441421878e+00, qS2 = 2.02094576023350569471e+00,
+                 qS3 = -6.88283971605453293030e-01, qS4 = 7.70381505559019352791e-02;
+    const double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    return p / q;
+}
+LUMO_HD double lm_acos(double x) {
+    const double pio2_hi = 1.57079632679489655800e+00, pio2_lo = 6.12323399573676603587e-17;
+    const uint64_t bits = f64_bits(x);
+    const uint32_t hx = (uint32_t)(bits >> 32), lx = (uint32_t)bits;
+    const uint32_t ix = hx & 0x7fffffffu;
+    if (ix >= 0x3ff00000u) {  // |x| >= 1 or nan
+        if (((ix - 0x3ff00000u) | lx) == 0) return (hx >> 31) ? 2.0 * pio2_hi : 0.0;
+        return (x - x) / (x - x);
+    }
+    if (ix < 0x3fe00000u) {  // |x| < 0.5
+        if (ix <= 0x3c600000u) return pio2_hi;
+        return pio2_hi - (x - (pio2_lo - x * lm_acos_R(x * x)));
+    }
+    if (hx >> 31) {  // x < -0.5
+        const double z = (1.0 + x) * 0.5;
+        const double s = sqrt(z);
+        const double w = lm_acos_R(z) * s - pio2_lo;
+        return 2.0 * (pio2_hi - (s + w));
+    }
+    const double z = (1.0 - x) * 0.5;  // x > 0.5
+    const double s = sqrt(z);
+    const double df = f64_from_bits(f64_bits(s) & 0xffffffff00000000ull);
+    const double c = (z - df * df) / (s + df);
+    const double w = lm_acos_R(z) * s + c;
+    return 2.0 * (df + w);
 }
 
 }  // namespace lumo

@@ -444,11 +444,89 @@ __device__ void instance_fix_hit(const lumo_transform& T, int material_override,
     h.p = xf_apply(T.m, h.p, 1.0);
 }
 
+// ---- Sphere (object/sphere.rs) with EFloat error intervals (efloat.rs)
+struct EF {
+    double v, lo, hi;
+};
+__device__ __forceinline__ EF ef(double x) { return EF{x, x, x}; }
+__device__ __forceinline__ EF ef_add(EF a, EF b) { return EF{a.v + b.v, previous_float(a.lo + b.lo), next_float(a.hi + b.hi)}; }
+__device__ __forceinline__ EF ef_sub(EF a, EF b) { return EF{a.v - b.v, previous_float(a.lo - b.hi), next_float(a.hi - b.lo)}; }
+__device__ __forceinline__ EF ef_mul(EF a, EF b) {
+    const double p0 = a.lo * b.lo, p1 = a.lo * b.hi, p2 = a.hi * b.lo, p3 = a.hi * b.hi;
+    return EF{a.v * b.v, previous_float(rmin(rmin(rmin(p0, p1), p2), p3)), next_float(rmax(rmax(rmax(p0, p1), p2), p3))};
+}
+__device__ __forceinline__ EF ef_div(EF a, EF b) {
+    if (b.lo < 0.0 && b.hi > 0.0) return EF{a.v / b.v, -DINF, DINF};
+    const double d0 = a.lo / b.lo, d1 = a.lo / b.hi, d2 = a.hi / b.lo, d3 = a.hi / b.hi;
+    return EF{a.v / b.v, previous_float(rmin(rmin(rmin(d0, d1), d2), d3)), next_float(rmax(rmax(rmax(d0, d1), d2), d3))};
+}
+// Sphere::hit (sphere.rs:27-78); FULL also builds the record
+template <bool FULL>
+__device__ bool sphere_hit(const lumo_object& ob, const RayX& r, double t_min, double t_max, DHit& out) {
+    const EF dx = ef(r.d.x), dy = ef(r.d.y), dz = ef(r.d.z), ox = ef(r.o.x), oy = ef(r.o.y), oz = ef(r.o.z);
+    const EF radius2 = ef_mul(ef(ob.radius), ef(ob.radius));
+    const EF a = ef_add(ef_add(ef_mul(dx, dx), ef_mul(dy, dy)), ef_mul(dz, dz));
+    const EF b = ef_mul(ef(2.0), ef_add(ef_add(ef_mul(dx, ox), ef_mul(dy, oy)), ef_mul(dz, oz)));
+    const EF c = ef_sub(ef_add(ef_add(ef_mul(ox, ox), ef_mul(oy, oy)), ef_mul(oz, oz)), radius2);
+    const double disc = b.v * b.v - 4.0 * a.v * c.v;
+    if (disc < 0.0) return false;
+    const double sd = sqrt(disc);
+    const EF root{sd, previous_float(sqrt(disc)), next_float(sqrt(disc))};
+    const EF nb{-b.v, -b.lo, -b.hi};
+    const EF a2 = ef_mul(ef(2.0), a);
+    EF t0 = ef_div(ef_sub(nb, root), a2), t1 = ef_div(ef_add(nb, root), a2);
+    if (t0.v > t1.v) {
+        const EF tmp = t0;
+        t0 = t1;
+        t1 = tmp;
+    }
+    if (t0.hi >= t_max || t1.lo <= t_min) return false;
+    EF t = t0;
+    if (!(t0.lo > t_min)) {
+        if (t1.hi >= t_max) return false;
+        t = t1;
+    }
+    out.t = t.v;
+    if (!FULL) return true;
+    V3 xi = r.o + t.v * r.d;
+    xi = xi * ob.radius / length(xi);
+    const V3 ni = xi / ob.radius;
+    out.err = gamma_n(5) * vabs(xi);
+    out.material = ob.material;
+    out.backface = dot(r.d, ni) > 0.0;
+    out.p = xi;
+    out.ns = ni;
+    out.ng = ni;
+    out.uv = wrap_uv(V2{(lm_atan2(-ni.z, ni.x) + PI) / (2.0 * PI), lm_acos(-ni.y) / PI});
+    return true;
+}
+// Sphere::hit_t (sphere.rs:80-97) with util::quadratic (object.rs:60-74)
+__device__ double sphere_hit_t(const lumo_object& ob, const RayX& r, double t_min, double t_max) {
+    const double a = dot(r.d, r.d);
+    const double b = 2.0 * dot(r.d, r.o);
+    const double c = dot(r.o, r.o) - ob.radius * ob.radius;
+    const double disc = b * b - 4.0 * a * c;
+    if (disc < 0.0) return DINF;
+    const double root = sqrt(disc);
+    double t0 = (-b - root) / (2.0 * a), t1 = (-b + root) / (2.0 * a);
+    if (t0 > t1) {
+        const double tmp = t0;
+        t0 = t1;
+        t1 = tmp;
+    }
+    if (t0 >= t_max || t1 <= t_min) return DINF;
+    if (t0 > t_min) return t0;
+    if (t1 >= t_max) return DINF;
+    return t1;
+}
+constexpr int PRIM_SPHERE = -2;
+
 // Object::hit_t of the shape (kdtree.rs:178-180, rectangle.rs:87-89, triangle.rs:195-197)
 template <int STK>
 __device__ __forceinline__ double shape_hit_t(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                               double t_max, Counters& C) {
     if (ob.type == LUMO_OBJ_TRIANGLE) return tri_hit_t(sc, ob.tri_base, r, t_min, t_max, C);
+    if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit_t(ob, r, t_min, t_max);
     return kd_traverse<false, STK>(sc, ob, r, t_min, t_max, nullptr, C);
 }
 template <int STK>
@@ -459,11 +537,12 @@ __device__ __forceinline__ double object_hit_t(const DScene& sc, const lumo_obje
 }
 
 // Object::hit: kd GEO traversal, then the winner's GEO test (acceptance + t only; the record is
-// rebuilt by object_record).  Returns the global triangle index or -1.
+// rebuilt by object_record).  Returns the global triangle index, PRIM_SPHERE, or -1 (miss).
 template <int STK>
 __device__ __forceinline__ int shape_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                              double t_max, Counters& C, DHit& out) {
     if (ob.type == LUMO_OBJ_TRIANGLE) return tri_hit_geo<false>(sc, ob.tri_base, r, t_min, t_max, out) ? ob.tri_base : -1;
+    if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit<false>(ob, r, t_min, t_max, out) ? PRIM_SPHERE : -1;
     int idx = -1;
     kd_traverse<true, STK>(sc, ob, r, t_min, t_max, &idx, C);
     if (idx < 0) return -1;
@@ -481,11 +560,11 @@ __device__ __forceinline__ int object_hit_tri(const DScene& sc, const lumo_objec
 // deterministic, so re-running it reproduces the accepted hit), incl. Rectangle uv
 // (rectangle.rs:74-85) and the instance transform.
 __device__ void object_record(const DScene& sc, const lumo_object& ob, int tri, const RayX& r, DHit& h) {
-    if (ob.xform < 0) {
-        tri_hit_geo<true>(sc, tri, r, 0.0, DINF, h);
-    } else {
-        tri_hit_geo<true>(sc, tri, ray_local(sc.xforms[ob.xform], r), 0.0, DINF, h);
-    }
+    const RayX rl = ob.xform < 0 ? r : ray_local(sc.xforms[ob.xform], r);
+    if (ob.type == LUMO_OBJ_SPHERE)
+        sphere_hit<true>(ob, rl, 0.0, DINF, h);
+    else
+        tri_hit_geo<true>(sc, tri, rl, 0.0, DINF, h);
     if (ob.type == LUMO_OBJ_RECTANGLE) h.uv = wrap_uv(V2{dot(ld3(ob.b0), h.p), dot(ld3(ob.b1), h.p)});
     if (ob.xform >= 0) instance_fix_hit(sc.xforms[ob.xform], ob.material_override, h);
 }
@@ -560,7 +639,7 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     int oi = bvh_traverse<true, STK>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C);
     if (oi >= 0) {
         const int tri = object_hit_tri<STK>(sc, sc.objs[oi], r, 0.0, t_max, C, g);
-        if (tri >= 0) {
+        if (tri != -1) {
             h = HitRef{g.t, 1, oi, tri};
             t_max = g.t;
         }
@@ -568,7 +647,7 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     const int li = bvh_traverse<true, STK>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C);
     if (li >= 0) {
         const int tri = object_hit_tri<STK>(sc, sc.lights[li], r, 0.0, t_max, C, g);
-        if (tri >= 0) h = HitRef{g.t, 2, li, tri};
+        if (tri != -1) h = HitRef{g.t, 2, li, tri};
     }
     return h;
 }
@@ -584,7 +663,7 @@ template <int STK>
 __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit& lh, Counters& C) {
     const lumo_object& L = sc.lights[light];
     const int tri = object_hit_tri<STK>(sc, L, r, 0.0, DINF, C, lh);
-    if (tri < 0) return false;
+    if (tri == -1) return false;
     const double t_max = lh.t - EPSILON;
     if (bvh_hit_t<STK>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C) < t_max) return false;
     if (bvh_hit_t<STK>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C) < t_max) return false;
@@ -931,15 +1010,47 @@ __device__ __forceinline__ V3 shape_sample_on(const DScene& sc, const lumo_objec
     return ld3(L.origin) + rs.x * ld3(L.b0) + rs.y * ld3(L.b1);
 }
 __device__ __forceinline__ double shape_pdf(const lumo_object& L, V3 xo, V3 wi, V3 xi, V3 ng) {
+    if (L.type == LUMO_OBJ_SPHERE) {  // solid angle of the visible cap (sphere.rs:190-206)
+        const double radius2 = L.radius * L.radius;
+        const double d2 = length_squared(xo);
+        if (!(d2 < radius2)) {
+            const double cos_theta_max = sqrt(rmax(1.0 - radius2 / d2, 0.0));
+            return 1.0 / (2.0 * PI * (1.0 - cos_theta_max));
+        }
+    }
     const double p_area = 1.0 / L.area;
     return p_area * distance_squared(xo, xi) / fabs(dot(ng, wi));
 }
-// Sampleable::sample_towards (object.rs:138-141; Instance: instance.rs:162-167)
+// Sampleable::sample_towards in the shape's own space (object.rs:138-141, sphere.rs:131-187)
+__device__ V3 shape_sample_towards(const DScene& sc, const lumo_object& L, V3 xo, V2 rs) {
+    if (L.type != LUMO_OBJ_SPHERE) return normalize(shape_sample_on(sc, L, rs) - xo);
+    const double d2 = length_squared(xo);
+    const double radius2 = L.radius * L.radius;
+    V3 xi;
+    if (d2 < radius2) {
+        const V3 p = L.radius * square_to_sphere(rs);
+        xi = p * L.radius / length(p);
+    } else {
+        const Onb uvw = onb_new(-normalize(xo));
+        const double d = sqrt(d2);
+        const double cos_theta_max = sqrt(rmax(1.0 - radius2 / d2, 0.0));
+        const double cos_theta = (1.0 - rs.x) + rs.x * cos_theta_max;
+        const double sin_theta = sqrt(rmax(1.0 - cos_theta * cos_theta, 0.0));
+        const double phi = 2.0 * PI * rs.y;
+        const double ds = d * cos_theta - sqrt(rmax(radius2 - d2 * sin_theta * sin_theta, 0.0));
+        const double cos_alpha = (d2 + radius2 - ds * ds) / (2.0 * d * L.radius);
+        const double sin_alpha = sqrt(rmax(1.0 - cos_alpha * cos_alpha, 0.0));
+        const V3 ngl{lm_cos(phi) * sin_alpha, lm_sin(phi) * sin_alpha, cos_alpha};
+        xi = normalize(onb_world(uvw, -ngl)) * L.radius;
+    }
+    return normalize(xi - xo);
+}
+// Sampleable::sample_towards (Instance: instance.rs:162-167)
 __device__ V3 light_sample_towards(const DScene& sc, const lumo_object& L, V3 xo, V2 rs) {
-    if (L.xform < 0) return normalize(shape_sample_on(sc, L, rs) - xo);
+    if (L.xform < 0) return shape_sample_towards(sc, L, xo, rs);
     const lumo_transform& T = sc.xforms[L.xform];
     const V3 xl = xf_apply(T.inv, xo, 1.0);
-    const V3 dl = normalize(shape_sample_on(sc, L, rs) - xl);
+    const V3 dl = shape_sample_towards(sc, L, xl, rs);
     return normalize(xf_apply(T.m, dl, 0.0));
 }
 // Sampleable::sample_towards_pdf (object.rs:149-156; Instance: instance.rs:169-199)

@@ -1094,7 +1094,8 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     }
     for (int i = 0; i < d->num_lights + d->num_objects; ++i) {
         const lumo_object& o = i < d->num_lights ? d->lights[i] : d->objects[i - d->num_lights];
-        if (o.type < LUMO_OBJ_KDMESH || o.type > LUMO_OBJ_TRIANGLE) return LUMO_ERR_UNSUPPORTED;
+        if (o.type < LUMO_OBJ_KDMESH || o.type > LUMO_OBJ_SPHERE) return LUMO_ERR_UNSUPPORTED;
+        if (o.type == LUMO_OBJ_SPHERE && !(o.radius != 0.0 && o.area > 0.0)) return LUMO_ERR_INVALID;
         if (o.xform >= d->num_transforms || (o.xform >= 0 && !d->transforms)) return LUMO_ERR_INVALID;
         if (o.type == LUMO_OBJ_TRIANGLE && (o.tri_base < 0 || o.tri_base >= d->num_triangles)) return LUMO_ERR_INVALID;
     }

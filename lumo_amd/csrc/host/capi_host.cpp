@@ -93,6 +93,19 @@ int lumo_builder_add_rectangle(void* b, const double* a, const double* bb, const
     sb->add_rectangle(v3p(a), v3p(bb), v3p(c), material, as_light != 0);
     return LUMO_OK;
 }
+int lumo_builder_add_sphere(void* b, double radius, int material, int as_light) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || material < 0 || material >= (int)sb->materials.size()) return LUMO_ERR_INVALID;
+    return sb->add_sphere(radius, material, as_light != 0) ? LUMO_OK : LUMO_ERR_INVALID;
+}
+int lumo_builder_set_environment_map(void* b, lumo_spectrum tex, double scale) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb) return LUMO_ERR_INVALID;
+    sb->has_env = true;
+    sb->env_tex = tex;
+    sb->env_scale = scale;
+    return LUMO_OK;
+}
 int lumo_builder_instance_op(void* b, int is_light, int64_t index, int op, double x, double y, double z) {
     SceneBuilder* sb = static_cast<SceneBuilder*>(b);
     if (!sb) return LUMO_ERR_INVALID;
@@ -214,6 +227,7 @@ void lumo_lmath(int which, const double* x, double* y, int64_t n) {
             case 2: y[i] = lm_cosh(x[i]); break;
             case 3: y[i] = lm_sin(x[i]); break;
             case 5: y[i] = lm_atan(x[i]); break;
+            case 6: y[i] = lm_acos(x[i]); break;
             default: y[i] = lm_cos(x[i]); break;
         }
     }

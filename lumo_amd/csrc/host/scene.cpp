@@ -631,6 +631,16 @@ void SceneBuilder::add_rectangle(V3 a, V3 b, V3 c, int material, bool as_light) 
     o.b1 = b1;
 }
 
+bool SceneBuilder::add_sphere(double radius, int material, bool as_light) {
+    if (radius == 0.0 || radius != radius) return false;  // sphere.rs:15 assert
+    HostObject o;
+    o.type = LUMO_OBJ_SPHERE;
+    o.material = material;
+    o.radius = radius;
+    (as_light ? lights : objects).push_back(std::move(o));
+    return true;
+}
+
 SceneBuilder SceneBuilder::cornell_box() {
     SceneBuilder s;
     const lumo_spectrum box_spec = spectrum_from_pts(
@@ -872,7 +882,18 @@ std::unique_ptr<FlatScene> build_scene(const SceneBuilder& sb) {
             }
             lo.xform = -1;
             lo.material_override = -1;
-            if (o.type == LUMO_OBJ_TRIANGLE) {
+            if (o.type == LUMO_OBJ_SPHERE) {
+                lo.kd_root = -1;
+                lo.item_base = -1;
+                lo.tri_base = -1;
+                lo.num_tris = 0;
+                lo.radius = o.radius;
+                lo.area = 4.0 * PI * o.radius * o.radius;  // sphere.rs:104-106
+                V3 mn, mx;
+                shape_bounds(o, mn, mx);
+                lo.bmin[0] = mn.x; lo.bmin[1] = mn.y; lo.bmin[2] = mn.z;
+                lo.bmax[0] = mx.x; lo.bmax[1] = mx.y; lo.bmax[2] = mx.z;
+            } else if (o.type == LUMO_OBJ_TRIANGLE) {
                 lo.kd_root = -1;
                 lo.item_base = -1;
                 V3 mn, mx;
@@ -930,9 +951,39 @@ std::unique_ptr<FlatScene> build_scene(const SceneBuilder& sb) {
             dst.push_back(lo);
         }
     };
+    // Scene::build (scene.rs:33-52): environment map -> enclosing two-sided Light sphere
+    std::vector<HostObject> env_lights;
+    const std::vector<HostObject>* light_src = &sb.lights;
+    std::vector<HostMaterial> extra_mats;
+    if (sb.has_env) {
+        bool any = false;
+        V3 bmn{0, 0, 0}, bmx{0, 0, 0};
+        for (const std::vector<HostObject>* v : {&sb.objects, &sb.lights})
+            for (const HostObject& o : *v) {
+                V3 mn, mx;
+                world_bounds(o, mn, mx);
+                bmn = any ? vmin(bmn, mn) : mn;
+                bmx = any ? vmax(bmx, mx) : mx;
+                any = true;
+            }
+        if (!any) throw std::runtime_error("environment map on an empty scene");
+        const V3 center = bmn + (bmx - bmn) / 2.0;  // aabb.rs:46-48
+        const double radius = length(center - bmn);  // Vec3::distance
+        env_lights = sb.lights;
+        HostObject env;
+        env.type = LUMO_OBJ_SPHERE;
+        env.radius = radius;
+        env.material = (int)(sb.materials.size());  // appended below
+        instance_op(env, INST_TRANSLATE, center.x, center.y, center.z);
+        env_lights.push_back(env);
+        light_src = &env_lights;
+        HostMaterial em = material_light(sb.env_tex, DENSE_D65, sb.env_scale, true);
+        fs->materials.push_back(em.m);
+        extra_mats.push_back(em);
+    }
     std::vector<V3> omn, omx, lmn, lmx;
     flatten_objects(sb.objects, fs->objects, omn, omx);
-    flatten_objects(sb.lights, fs->lights, lmn, lmx);
+    flatten_objects(*light_src, fs->lights, lmn, lmx);
     if (!sb.objects.empty()) {
         BvhBuilt ob = build_bvh(omn, omx);
         fs->object_nodes = ob.nodes;
@@ -950,13 +1001,14 @@ std::unique_ptr<FlatScene> build_scene(const SceneBuilder& sb) {
         lambda[i] = wl_sample_one(v);
         pdf[i] = wl_pdf_one(lambda[i]);
     }
-    const size_t n = sb.lights.size();
+    const size_t n = light_src->size();
     double sum = 0.0;
     std::vector<double> apdf;
     std::vector<std::pair<double, int64_t>> table;
     for (size_t i = 0; i < n; ++i) {
-        const HostObject& o = sb.lights[i];
-        const HostMaterial& hm = sb.materials[o.material];
+        const HostObject& o = (*light_src)[i];
+        const HostMaterial& hm =
+            o.material < (int)sb.materials.size() ? sb.materials[o.material] : extra_mats[o.material - sb.materials.size()];
         const double ar = world_area(o);
         double p[4];
         for (int k = 0; k < 4; ++k) {
@@ -1140,6 +1192,11 @@ double comp(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
 }  // namespace
 
 void shape_bounds(const HostObject& o, V3& mn, V3& mx) {
+    if (o.type == LUMO_OBJ_SPHERE) {  // sphere.rs:99-102
+        mx = V3{o.radius, o.radius, o.radius};
+        mn = -mx;
+        return;
+    }
     if (o.type == LUMO_OBJ_RECTANGLE) {  // Rectangle::bounding_box (rectangle.rs:91-102)
         const V3 a = o.b1 + o.origin, b = o.origin, c = o.b0 + o.origin, d = o.origin + o.b0 + o.b1;
         mn = vmin(vmin(vmin(a, b), c), d);
@@ -1180,7 +1237,7 @@ void world_bounds(const HostObject& o, V3& mn, V3& mx) {
 bool instance_op(HostObject& o, int op, double x, double y, double z) {
     Xform t;
     if (op == INST_TO_UNIT_SIZE) {  // kdtree.rs:93-99 (defined on the kd-tree itself)
-        if (o.instanced) return false;
+        if (o.instanced || o.type != LUMO_OBJ_KDMESH) return false;
         V3 mn, mx;
         shape_bounds(o, mn, mx);
         const V3 dim = mx - mn;
@@ -1229,6 +1286,8 @@ double world_area(const HostObject& o) {
     } else if (o.type == LUMO_OBJ_TRIANGLE) {
         const V3 A = o.vertices[o.tris[0].v[0]], B = o.vertices[o.tris[0].v[1]], Cv = o.vertices[o.tris[0].v[2]];
         a = length(cross(B - A, Cv - A)) / 2.0;
+    } else if (o.type == LUMO_OBJ_SPHERE) {
+        a = 4.0 * PI * o.radius * o.radius;
     } else {
         throw std::runtime_error("light shape without area (meshes become per-triangle lights)");
     }

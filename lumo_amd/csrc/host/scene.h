@@ -54,6 +54,7 @@ struct HostObject {
     };
     std::vector<Tri> tris;
     V3 origin{}, b0{}, b1{};        // Rectangle
+    double radius = 0.0;            // Sphere
     // Instance (object/instance.rs): local->world transform applied to the shape
     bool instanced = false;
     Xform xf{};
@@ -102,6 +103,13 @@ class SceneBuilder {
                   const std::vector<V3>& normals, const std::vector<V2>& uvs, int material, bool as_light = false);
     // Rectangle::new(Mat3(a, b, c), material) (rectangle.rs:23-45)
     void add_rectangle(V3 a, V3 b, V3 c, int material, bool as_light);
+    // Sphere::new(radius, material) at the origin (sphere.rs:10-21); place it with instance ops
+    bool add_sphere(double radius, int material, bool as_light);
+    // Scene::set_environment_map(texture, scale) (scene.rs:73-78): at build time a two-sided D65
+    // Light sphere enclosing the scene bounds is added as the last light (scene.rs:33-52).
+    bool has_env = false;
+    lumo_spectrum env_tex{};
+    double env_scale = 0.0;
 
     // Scene::cornell_box (scene/cornell_box.rs:8-193)
     static SceneBuilder cornell_box();

@@ -14,6 +14,7 @@
 #define O_ATAN2 std::atan2
 #define O_COS std::cos
 #define O_SIN std::sin
+#define O_ACOS std::acos
 #else
 #define O_LOG1P lumo::lm_log1p
 #define O_COSH lumo::lm_cosh
@@ -21,6 +22,7 @@
 #define O_ATAN2 lumo::lm_atan2
 #define O_COS lumo::lm_cos
 #define O_SIN lumo::lm_sin
+#define O_ACOS lumo::lm_acos
 #endif
 
 #include <algorithm>
@@ -392,9 +394,79 @@ V3 propagate_fp_err(const Xform& X, V3 xo, V3 fp_error) {
     return base + (gamma_n(3) + 1.0) * project(m4_mul_vec(a, extend(e3, 0.0)));
 }
 
+// ---- EFloat (efloat.rs) and Sphere (object/sphere.rs)
+struct EF {
+    double v, lo, hi;
+};
+EF ef(double x) { return EF{x, x, x}; }
+EF ef_add(EF a, EF b) { return EF{a.v + b.v, previous_float(a.lo + b.lo), next_float(a.hi + b.hi)}; }
+EF ef_sub(EF a, EF b) { return EF{a.v - b.v, previous_float(a.lo - b.hi), next_float(a.hi - b.lo)}; }
+EF ef_neg(EF a) { return EF{-a.v, -a.lo, -a.hi}; }
+EF ef_mul(EF a, EF b) {
+    const double p0 = a.lo * b.lo, p1 = a.lo * b.hi, p2 = a.hi * b.lo, p3 = a.hi * b.hi;
+    return EF{a.v * b.v, previous_float(rmin(rmin(rmin(p0, p1), p2), p3)), next_float(rmax(rmax(rmax(p0, p1), p2), p3))};
+}
+EF ef_div(EF a, EF b) {
+    if (b.lo < 0.0 && b.hi > 0.0) return EF{a.v / b.v, -INF, INF};
+    const double d0 = a.lo / b.lo, d1 = a.lo / b.hi, d2 = a.hi / b.lo, d3 = a.hi / b.hi;
+    return EF{a.v / b.v, previous_float(rmin(rmin(rmin(d0, d1), d2), d3)), next_float(rmax(rmax(rmax(d0, d1), d2), d3))};
+}
+EF ef_sqrt(EF a) { return EF{std::sqrt(a.v), previous_float(std::sqrt(a.lo)), next_float(std::sqrt(a.hi))}; }
+bool ef_quadratic(EF a, EF b, EF c, EF* t0, EF* t1) {  // efloat.rs EFloat::quadratic
+    const double disc = b.v * b.v - 4.0 * a.v * c.v;
+    if (disc < 0.0) return false;
+    const EF root = ef_sqrt(ef(disc));
+    EF x0 = ef_div(ef_sub(ef_neg(b), root), ef_mul(ef(2.0), a));
+    EF x1 = ef_div(ef_add(ef_neg(b), root), ef_mul(ef(2.0), a));
+    if (x0.v > x1.v) std::swap(x0, x1);
+    *t0 = x0;
+    *t1 = x1;
+    return true;
+}
+bool sphere_hit(const lumo_object& ob, const Ray& r, double t_min, double t_max, Hit* out) {  // sphere.rs:27-78
+    const EF dx = ef(r.dir.x), dy = ef(r.dir.y), dz = ef(r.dir.z);
+    const EF ox = ef(r.origin.x), oy = ef(r.origin.y), oz = ef(r.origin.z);
+    const EF radius2 = ef_mul(ef(ob.radius), ef(ob.radius));
+    const EF a = ef_add(ef_add(ef_mul(dx, dx), ef_mul(dy, dy)), ef_mul(dz, dz));
+    const EF b = ef_mul(ef(2.0), ef_add(ef_add(ef_mul(dx, ox), ef_mul(dy, oy)), ef_mul(dz, oz)));
+    const EF c = ef_sub(ef_add(ef_add(ef_mul(ox, ox), ef_mul(oy, oy)), ef_mul(oz, oz)), radius2);
+    EF t0, t1;
+    if (!ef_quadratic(a, b, c, &t0, &t1)) return false;
+    if (t0.hi >= t_max || t1.lo <= t_min) return false;
+    EF t = t0;
+    if (!(t0.lo > t_min)) {
+        if (t1.hi >= t_max) return false;
+        t = t1;
+    }
+    V3 xi = r.origin + t.v * r.dir;
+    xi = xi * ob.radius / length(xi);
+    const V3 err = gamma_n(5) * vabs(xi);
+    const V3 ni = xi / ob.radius;
+    const double u = (O_ATAN2(-ni.z, ni.x) + PI) / (2.0 * PI);
+    const double v = O_ACOS(-ni.y) / PI;
+    *out = hit_new(t.v, ob.material, r.dir, xi, err, ni, ni, V2{u, v});
+    return true;
+}
+double sphere_hit_t(const lumo_object& ob, const Ray& r, double t_min, double t_max) {  // sphere.rs:80-97
+    const V3 xo = r.origin, wi = r.dir;
+    const double a = dot(wi, wi);
+    const double b = 2.0 * dot(wi, xo);
+    const double c = dot(xo, xo) - ob.radius * ob.radius;
+    const double disc = b * b - 4.0 * a * c;  // object.rs:60-74 util::quadratic
+    if (disc < 0.0) return INF;
+    const double root = std::sqrt(disc);
+    double t0 = (-b - root) / (2.0 * a), t1 = (-b + root) / (2.0 * a);
+    if (t0 > t1) std::swap(t0, t1);
+    if (t0 >= t_max || t1 <= t_min) return INF;
+    if (t0 > t_min) return t0;
+    if (t1 >= t_max) return INF;
+    return t1;
+}
+
 // Object::hit / hit_t of the shape in its own space
 bool shape_hit(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, Hit* out,
                Counters& C) {
+    if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit(ob, r, t_min, t_max, out);
     if (ob.type == LUMO_OBJ_TRIANGLE) return triangle_hit(sc, ob.tri_base, r, t_min, t_max, true, out, C) != INF;
     if (!kdtree_hit(sc, ob, r, t_min, t_max, true, out, nullptr, C)) return false;
     if (ob.type == LUMO_OBJ_RECTANGLE) {  // rectangle.rs:74-85
@@ -404,6 +476,7 @@ bool shape_hit(const Scene& sc, const lumo_object& ob, const Ray& r, double t_mi
     return true;
 }
 double shape_hit_t(const Scene& sc, const lumo_object& ob, const Ray& r, double t_min, double t_max, Counters& C) {
+    if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit_t(ob, r, t_min, t_max);
     if (ob.type == LUMO_OBJ_TRIANGLE) {  // triangle.rs:195-197
         Hit dummy;
         return triangle_hit(sc, ob.tri_base, r, t_min, t_max, false, &dummy, C);
@@ -975,11 +1048,48 @@ V3 shape_sample_on(const Scene& sc, const lumo_object& L, V2 rs) {
     const V3 o{L.origin[0], L.origin[1], L.origin[2]}, b0{L.b0[0], L.b0[1], L.b0[2]}, b1{L.b1[0], L.b1[1], L.b1[2]};
     return o + rs.x * b0 + rs.y * b1;
 }
-// Sampleable::sample_towards / sample_towards_pdf (object.rs:138-156)
+// Sphere::sample_on (sphere.rs:108-129) -> point
+V3 sphere_sample_on(const lumo_object& L, V2 rs) {
+    const V3 xo = L.radius * square_to_sphere(rs);
+    return xo * L.radius / length(xo);
+}
+// Sampleable::sample_towards / sample_towards_pdf (object.rs:138-156, sphere.rs:131-206)
 V3 shape_sample_towards(const Scene& sc, const lumo_object& L, V3 xo, V2 rs) {
-    return normalize(shape_sample_on(sc, L, rs) - xo);
+    if (L.type != LUMO_OBJ_SPHERE) return normalize(shape_sample_on(sc, L, rs) - xo);
+    const double dist_origin2 = length_squared(xo);
+    const double radius2 = L.radius * L.radius;
+    V3 xi;
+    if (dist_origin2 < radius2) {
+        xi = sphere_sample_on(L, rs);
+    } else {
+        const Onb uvw = onb_new(-normalize(xo));
+        const double dist_origin = std::sqrt(dist_origin2);
+        const double sin2_theta_max = radius2 / dist_origin2;
+        const double cos_theta_max = std::sqrt(rmax(1.0 - sin2_theta_max, 0.0));
+        const double cos_theta = (1.0 - rs.x) + rs.x * cos_theta_max;
+        const double sin_theta = std::sqrt(rmax(1.0 - cos_theta * cos_theta, 0.0));
+        const double phi = 2.0 * PI * rs.y;
+        const double dist_sampled =
+            dist_origin * cos_theta - std::sqrt(rmax(radius2 - dist_origin2 * sin_theta * sin_theta, 0.0));
+        const double cos_alpha = (dist_origin2 + radius2 - dist_sampled * dist_sampled) / (2.0 * dist_origin * L.radius);
+        const double sin_alpha = std::sqrt(rmax(1.0 - cos_alpha * cos_alpha, 0.0));
+        const V3 ng_local{O_COS(phi) * sin_alpha, O_SIN(phi) * sin_alpha, cos_alpha};
+        const V3 ng = normalize(onb_to_world(uvw, -ng_local));
+        xi = ng * L.radius;
+    }
+    return normalize(xi - xo);
 }
 double shape_sample_towards_pdf(const lumo_object& L, const Ray& ri, V3 xi, V3 ng) {
+    if (L.type == LUMO_OBJ_SPHERE) {
+        const V3 xo = ri.origin;
+        const double radius2 = L.radius * L.radius;
+        const double dist_origin2 = length_squared(xo);
+        if (!(dist_origin2 < radius2)) {
+            const double sin2_theta_max = radius2 / dist_origin2;
+            const double cos_theta_max = std::sqrt(rmax(1.0 - sin2_theta_max, 0.0));
+            return 1.0 / (2.0 * PI * (1.0 - cos_theta_max));
+        }
+    }
     const double p_area = 1.0 / L.area;
     return p_area * distance_squared(ri.origin, xi) / fabs(dot(ng, ri.dir));
 }

@@ -19,7 +19,7 @@ def dev():
     d.close()
 
 
-@pytest.mark.parametrize("tile", [0, 7, 13])
+@pytest.mark.parametrize("tile", [0, 7, 11])
 def test_material_zoo_paths(dev, tile):
     sc = material_zoo()
     cam = default_camera((64, 48))

@@ -69,3 +69,10 @@ def test_trace_instanced(dev):
     r = O.trace(sc.desc(), o, d)
     for a, b in zip(g[:3], r[:3]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("env", [False, True])
+def test_sphere_scene_paths(dev, env):
+    from test_instances_lights import sphere_scene
+    cam = L.Camera.builder().origin(0.0, 0.3, 4.0).towards(0.0, 0.0, 0.0).resolution((32, 32)).build()
+    _paths(dev, sphere_scene(env=env), cam, L.make_tasks(32, 32, 16, SEED)[1])

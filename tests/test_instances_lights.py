@@ -171,3 +171,69 @@ def test_tilted_instance_light_pdf_quirk():
     w[:, 1] = np.abs(w[:, 1])
     est = 2 * np.pi * O.light_pdf(d, 0, xo, w).mean()
     assert abs(est - 1.0) > 0.05
+
+
+def sphere_scene(env=False, light_sphere=True):
+    s = L.Scene()
+    if light_sphere:
+        s.add_sphere(0.3, L.Material.light(NS("WHITE")), light=True).translate(0.0, 1.5, 0.0)
+    s.add_sphere(0.5, L.Material.diffuse(L.Spectrum.from_rgb(0.7, 0.6, 0.5)))
+    s.add_rectangle((-3, -1, -3), (3, -1, -3), (3, -1, 3), grey())
+    if env:
+        s.set_environment_map(L.Spectrum.from_rgb(0.4, 0.5, 0.9), 0.5)
+    return s
+
+
+def test_sphere_intersections():
+    """test_util.rs object tests on Sphere::new(1.0): no self-intersection from the surface,
+    nothing behind, hits towards the centre; hit_t agrees with hit (shadow_hit_accurate)."""
+    s = L.Scene()
+    s.add_sphere(1.0, grey())
+    tiny_light(s)
+    d = s.desc()
+    t, k, _, _ = O.trace(d, np.array([(1.0 + 1e-10, 0, 0), (2.0, 0, 0)]), np.array([(0, 0, 1.0), (1.0, 0, 0)]))
+    assert np.all(k == 0)
+    p = np.array([1.23, 4.56, 7.89])
+    t, k, _, _ = O.trace(d, p[None], -p[None] / np.linalg.norm(p))
+    assert k[0] == 1 and t[0] == pytest.approx(np.linalg.norm(p) - 1.0)
+    xo = sphere_points(5000, 9, 5.0)
+    t, k, _, _ = O.trace(d, xo, -xo / 5.0)
+    assert np.all(k == 1) and np.allclose(t, 4.0)
+
+
+@pytest.mark.parametrize("where", [(0.2, -0.5, 0.1), (0.0, 1.55, 0.05)])
+def test_sphere_light_sampling(where):
+    """sampled_rays_hit + pdf normalisation for a sphere light seen from outside (cone sampling)
+    and from inside (area sampling)."""
+    s = sphere_scene()
+    d = s.desc()
+    xo = np.array(where)
+    wi = O.light_sample(d, 0, xo, 4000, 3)
+    assert np.all(O.light_pdf(d, 0, xo, wi) > 0)
+    rng = np.random.default_rng(4)
+    w = rng.normal(size=(2000000, 3))  # the outside case subtends ~0.6% of the sphere of directions
+    w /= np.linalg.norm(w, axis=1, keepdims=True)
+    est = 4 * np.pi * O.light_pdf(d, 0, xo, w).mean()
+    assert est == pytest.approx(1.0, abs=0.04)
+
+
+def test_environment_map_sphere():
+    """Scene::build adds a two-sided D65 Light sphere enclosing the scene bounds."""
+    s = sphere_scene(env=True)
+    d = s.desc()
+    assert d.num_lights == 2
+    env = d.lights[1]
+    assert env.type == 3 and env.xform >= 0
+    m = d.materials[env.material]
+    assert m.kind == 2 and m.two_sided == 1 and m.scale == 0.5
+    # a ray escaping the scene hits the environment from inside
+    t, k, o, _ = O.trace(d, np.array([(0.0, 0.0, 2.0)]), np.array([(0.0, 0.0, 1.0)]))
+    assert k[0] == 2 and o[0] == 1
+    cam = L.Camera.builder().origin(0.0, 0.3, 4.0).towards(0.0, 0.0, 0.0).resolution((16, 16)).build()
+    tasks = L.make_tasks(16, 16, 8, 5)
+    bufs, _, _ = O.render_tasks(d, cam.desc, tasks, O.WAVEFRONT, 4)
+    f = L.Film(16, 16)
+    for tk, b in zip(tasks, bufs):
+        f.add_tile(tk, b)
+    img = f.rgb()
+    assert np.all(np.isfinite(img)) and img[..., 2].mean() > img[..., 0].mean()  # bluish sky
