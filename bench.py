@@ -43,8 +43,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--res", type=int, default=1024)
-    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3"],
+                    help="c1 Cornell 1024^2@1024 (BASELINE configs[1]); c2 dragon.rs 1920x1080@256 with the "
+                         "871k-triangle stand-in (configs[2]); c3 Bistro stand-in 1920x1080@256 (configs[3])")
+    ap.add_argument("--res", type=int, default=None, help="square resolution override")
+    ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--max-paths", type=int, default=1 << 23, help="paths in flight per wavefront")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-tile-stride", type=int, default=32, help="CPU sample: every k-th tile of each batch")
@@ -64,12 +67,11 @@ def main():
         dist.init_process_group(backend=backend)
         pg = dist
 
-    scene = L.Scene.cornell_box()
-    cam = L.Camera.cornell_box((args.res, args.res))
-    tasks = L.make_tasks(args.res, args.res, args.spp, SEED)
+    scene, cam, (W, H), spp, wl = build_config(args)
+    tasks = L.make_tasks(W, H, spp, SEED)
     from lumo_amd.dist import shard_tasks, tiles_per_batch
-    tiles = tiles_per_batch(args.res, args.res)
-    mine = shard_tasks(tasks, args.res, args.res, rank, ws)
+    tiles = tiles_per_batch(W, H)
+    mine = shard_tasks(tasks, W, H, rank, ws)
     mine_arr = (_ffi.TileTask * len(mine))(*mine)
 
     dev = L.Device(local)
@@ -114,7 +116,7 @@ def main():
 
     if rank == 0:
         roof = roofline(st)
-        cpu = cpu_baseline(scene, cam, tasks, tiles, args) if (args.cpu_baseline and ws == 1) else None
+        cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp) if (args.cpu_baseline and ws == 1) else None
         value = q / elapsed / 1e6
         out = {
             "metric": "Mrays/s",
@@ -128,13 +130,13 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (Scene::cornell_box defined in code; no assets needed)",
+            "data": wl["data"],
             "config": {
-                "workload": f"cornell_{args.res}x{args.res}_{args.spp}spp_pathtrace",
-                "scene": "Scene::cornell_box (32 triangles, 1 rectangle light)",
-                "camera": "Camera::cornell_box",
-                "resolution": [args.res, args.res],
-                "spp": args.spp,
+                "workload": f"{wl['name']}_{W}x{H}_{spp}spp_pathtrace",
+                "scene": wl["scene"],
+                "camera": wl["camera"],
+                "resolution": [W, H],
+                "spp": spp,
                 "integrator": "PathTrace (NEE + MIS + RR)",
                 "seed": SEED,
                 "rng_mode": "wavefront (per-path Xorshiftr128+ streams; DESIGN.md §RNG)",
@@ -143,6 +145,7 @@ def main():
             "msamples_per_s": round(cams / elapsed / 1e6, 3),
             "lumo_total_rays_per_s_M": round(rays / elapsed / 1e6, 3),
             "queries_per_step": q / args.steps,
+            "scene_build_s": wl["scene_build_s"],
             "roofline": roof,
             "cpu_baseline": cpu,
         }
@@ -150,6 +153,37 @@ def main():
     dev.close()
     if pg is not None:
         pg.destroy_process_group()
+
+
+def build_config(args):
+    """(scene, camera, (W, H), spp, labels) of BASELINE.json's configs, built with lumo's API."""
+    import lumo_amd as L
+    from lumo_amd import scenes
+    t0 = time.perf_counter()
+    if args.config == "c1":
+        W = H = args.res or 1024
+        spp = args.spp or 1024
+        scene, cam = scenes.cornell(), L.Camera.cornell_box((W, H))
+        wl = {"name": "cornell", "scene": "Scene::cornell_box (32 triangles, 1 rectangle light)",
+              "camera": "Camera::cornell_box", "data": "synthetic (Scene::cornell_box defined in code; no assets)"}
+    elif args.config == "c2":
+        W, H = (args.res, args.res) if args.res else (1920, 1080)
+        spp = args.spp or 256
+        scene, cam = scenes.dragon(), scenes.default_camera((W, H))
+        wl = {"name": "dragon", "scene": "examples/dragon.rs: empty_box + 871414-triangle procedural stand-in "
+                                         "(transparent MfDielectric 0.03, eta 1.5 glass curve) as an Instance",
+              "camera": "Camera::builder() default", "data": "synthetic (procedural stand-in for dragon.obj)"}
+    else:
+        W, H = (args.res, args.res) if args.res else (1920, 1080)
+        spp = args.spp or 256
+        scene, cam = scenes.bistro(), scenes.bistro_camera((W, H))
+        wl = {"name": "bistro", "scene": "procedural Bistro stand-in: ~2.8M triangles in 400 material groups, "
+                                         "2048 emissive triangles, environment light",
+              "camera": "origin (-16,5,-1) towards (0,0,0) (bistro.rs:15-18)",
+              "data": "synthetic (procedural stand-in for Bistro exterior)"}
+    scene.build()
+    wl["scene_build_s"] = round(time.perf_counter() - t0, 2)
+    return scene, cam, (W, H), spp, wl
 
 
 def roofline(st):
@@ -199,7 +233,7 @@ def pmc_traffic(kernel):
         return {}
 
 
-def cpu_baseline(scene, cam, tasks, tiles, args):
+def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp):
     """The oracle (f64 restatement of lumo's CPU path, lumo's own tile-serial RNG order) on this
     host: every k-th tile of every batch of the same frame, all spp; Mrays/s of that sample."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -218,7 +252,7 @@ def cpu_baseline(scene, cam, tasks, tiles, args):
     return {"value": round(q / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "msamples_per_s": round(paths / dt / 1e6, 4), "seconds": round(dt, 2),
             "sample": f"{len(sample)} tasks = every {args.cpu_tile_stride}th 16x16 tile of each 256-spp batch of "
-                      f"the {args.res}^2 @ {args.spp} spp frame ({paths} paths), lumo tile-serial RNG order"}
+                      f"the {W}x{H} @ {spp} spp frame ({paths} paths), lumo tile-serial RNG order"}
 
 
 if __name__ == "__main__":

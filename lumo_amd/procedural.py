@@ -48,3 +48,96 @@ def torus_knot_tube(n_along, n_around, p=3, q=7, R=1.0, r_knot=0.42, r_tube=0.13
 def dragon_standin(seed=1):
     """871 414-triangle closed mesh: (3, 7) torus-knot tube with 10 627 x 41 quads."""
     return torus_knot_tube(10627, 41, seed=seed)
+
+
+BISTRO_GROUPS = 400        # ~ number of usemtl groups (one kd-tree each, parser/obj.rs:85-108)
+BISTRO_LAMPS = 1024        # emissive quads -> 2048 Triangle lights (num_shadow_rays = 11)
+
+
+def _box_grid(center, size, n, rng, jitter=0.0):
+    """Axis-aligned box with each face split into n x n quads (outward winding)."""
+    cx, cy, cz = center
+    sx, sy, sz = size
+    g = np.linspace(0.0, 1.0, n + 1)
+    U, V = np.meshgrid(g, g, indexing="ij")
+    faces_v, faces_f, base = [], [], 0
+    # (origin, edge u, edge v) per face, u x v pointing outwards
+    lo = np.array([cx - sx / 2, cy, cz - sz / 2])
+    E = [np.array([sx, 0, 0]), np.array([0, sy, 0]), np.array([0, 0, sz])]
+    specs = [(lo, E[2], E[1]), (lo + E[0], E[1], E[2]),  # -x, +x
+             (lo, E[0], E[2]), (lo + E[1], E[2], E[0]),  # -y, +y
+             (lo, E[1], E[0]), (lo + E[2], E[0], E[1])]  # -z, +z
+    for o, eu, ev in specs:
+        P = o + U[..., None] * eu + V[..., None] * ev
+        if jitter:
+            nrm = np.cross(eu, ev)
+            nrm = nrm / np.linalg.norm(nrm)
+            inner = np.zeros_like(U, dtype=bool)
+            inner[1:-1, 1:-1] = True
+            P = P + (jitter * rng.standard_normal(U.shape) * inner)[..., None] * nrm
+        faces_v.append(P.reshape(-1, 3))
+        i = np.arange(n)[:, None] * (n + 1) + np.arange(n)[None, :]
+        q = np.stack([i, i + n + 1, i + n + 2, i + 1], -1).reshape(-1, 4) + base
+        faces_f.append(q)
+        base += (n + 1) * (n + 1)
+    return np.concatenate(faces_v), np.concatenate(faces_f)
+
+
+def bistro_standin(seed=7, groups=BISTRO_GROUPS, lamps=BISTRO_LAMPS, n=24):
+    """Procedural stand-in for the Bistro exterior: a ground plane and (groups - 1) buildings,
+    each its own mesh (material group), ~6 900 triangles per group (~2.8 M total), plus `lamps`
+    small emissive quads on the facades.  Returns (groups: [(v, f, kind, rgb)], lamps: [(v, f)])."""
+    rng = np.random.default_rng(seed)
+    cam = np.array([-16.0, 5.0, -1.0])
+    # candidate building sites on a street grid, keeping the camera's line of sight to the origin open
+    xs = np.arange(-30.0, 30.1, 2.4)
+    cand = []
+    for x in xs:
+        for z in xs:
+            p = np.array([x, 0.0, z])
+            d = p[[0, 2]]
+            seg = cam[[0, 2]]
+            t = np.clip(np.dot(d, seg) / np.dot(seg, seg), 0.0, 1.0)
+            if np.linalg.norm(d - t * seg) < 2.6 or np.linalg.norm(d) < 3.0:
+                continue
+            cand.append(p)
+    cand.sort(key=lambda p: np.linalg.norm(p))
+    sites = cand[:groups - 1]
+    out = []
+    ground_n = int(round(np.sqrt(6912 / 2)))
+    gv, gf = _box_grid((0.0, -0.05, 0.0), (64.0, 0.05, 64.0), 1, rng)  # thin slab under the streets
+    # replace the slab top with a finely split ground plane
+    g = np.linspace(-32.0, 32.0, ground_n + 1)
+    X, Z = np.meshgrid(g, g, indexing="ij")
+    gv = np.stack([X, np.zeros_like(X), Z], -1).reshape(-1, 3)
+    i = np.arange(ground_n)[:, None] * (ground_n + 1) + np.arange(ground_n)[None, :]
+    gf = np.stack([i, i + 1, i + ground_n + 2, i + ground_n + 1], -1).reshape(-1, 4)
+    out.append((gv, gf, "diffuse", (0.35, 0.33, 0.3)))
+    facade = []
+    for k, p in enumerate(sites):
+        h = rng.uniform(1.5, 7.0)
+        w = rng.uniform(1.2, 1.9)
+        d = rng.uniform(1.2, 1.9)
+        v, f = _box_grid((p[0], 0.0, p[2]), (w, h, d), n, rng, jitter=0.004)
+        kind = "metal" if rng.uniform() < 0.1 else "diffuse"
+        out.append((v, f, kind, tuple(rng.uniform(0.2, 0.9, 3))))
+        facade.append((p, w, h, d))
+    lamps_out = []
+    for k in range(lamps):
+        p, w, h, d = facade[k % len(facade)]
+        side = rng.integers(4)
+        y = rng.uniform(0.8, min(h - 0.3, 3.0))
+        s = 0.08
+        off = 0.02
+        if side == 0:
+            c, eu, ev = np.array([p[0] - w / 2 - off, y, p[2] + rng.uniform(-d, d) * 0.4]), [0, 0, s], [0, s, 0]
+        elif side == 1:
+            c, eu, ev = np.array([p[0] + w / 2 + off, y, p[2] + rng.uniform(-d, d) * 0.4]), [0, s, 0], [0, 0, s]
+        elif side == 2:
+            c, eu, ev = np.array([p[0] + rng.uniform(-w, w) * 0.4, y, p[2] - d / 2 - off]), [s, 0, 0], [0, s, 0]
+        else:
+            c, eu, ev = np.array([p[0] + rng.uniform(-w, w) * 0.4, y, p[2] + d / 2 + off]), [0, s, 0], [s, 0, 0]
+        eu, ev = np.array(eu, dtype=float), np.array(ev, dtype=float)
+        v = np.array([c - eu - ev, c + eu - ev, c + eu + ev, c - eu + ev])
+        lamps_out.append((v, np.array([[0, 1, 2, 3]])))
+    return out, lamps_out

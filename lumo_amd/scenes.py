@@ -27,3 +27,28 @@ def dragon(mesh=None):
 def default_camera(resolution):
     """Camera::builder().build() with the resolution overridden."""
     return Camera.builder().resolution(resolution).build()
+
+
+def bistro(standin=None):
+    """Bistro exterior (examples/bistro.rs, night variant) as a procedural stand-in: every
+    material group is its own mesh, emissive faces are Triangle lights, plus a constant
+    environment light (the HDR map is not available)."""
+    from . import Material, Spectrum
+    from .procedural import bistro_standin
+    groups, lamps = standin if standin is not None else bistro_standin()
+    scene = Scene()
+    for v, f, kind, rgb in groups:
+        spec = Spectrum.from_rgb(*rgb)
+        mat = Material.metal(spec, 0.25, 1.5, 3.0) if kind == "metal" else Material.diffuse(spec)
+        scene.add_mesh(v, f, mat)
+    # D65 / Light emission is ~100 x the texture (dense illuminant scale), like bistro.rs's 0.001 HDR scale
+    lamp_mat = Material.light(Spectrum.from_srgb(255, 197, 143), scale=0.5)
+    for v, f in lamps:
+        scene.add_mesh(v, f, lamp_mat, light=True)
+    scene.set_environment_map(Spectrum.from_rgb(0.3, 0.4, 0.8), 0.002)
+    return scene
+
+
+def bistro_camera(resolution):
+    """bistro.rs:15-18 exterior camera."""
+    return Camera.builder().origin(-16.0, 5.0, -1.0).towards(0.0, 0.0, 0.0).resolution(resolution).build()

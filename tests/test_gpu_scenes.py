@@ -76,3 +76,12 @@ def test_sphere_scene_paths(dev, env):
     from test_instances_lights import sphere_scene
     cam = L.Camera.builder().origin(0.0, 0.3, 4.0).towards(0.0, 0.0, 0.0).resolution((32, 32)).build()
     _paths(dev, sphere_scene(env=env), cam, L.make_tasks(32, 32, 16, SEED)[1])
+
+
+def test_bistro_standin_paths(dev):
+    """Many Triangle lights (n_shadow = ilog2(#lights)), per-group meshes, metal + diffuse
+    materials and the environment sphere."""
+    from lumo_amd.procedural import bistro_standin
+    sc = scenes.bistro(bistro_standin(groups=40, lamps=64, n=4))
+    cam = scenes.bistro_camera((48, 32))
+    _paths(dev, sc, cam, L.make_tasks(48, 32, 8, SEED)[4])
