@@ -24,8 +24,24 @@ constexpr double SVI = 253.819;  // SAMPLE_VISIBLE_INTEGRAL
 // and the host picks the smallest class >= the deepest kd / BVH path (lumo itself uses 64,
 // kdtree.rs:110, bvh.rs:324; a scene needing more than 64 would panic there too).
 
+// kd node packed to 16 B for the device (lumo_kd_node is 32 B): interior nodes hold the split
+// point, leaves {first, count}; meta = right << 2 | axis, axis == 3 marks a leaf.
+struct alignas(16) DKd {
+    union {
+        double point;
+        struct {
+            int32_t first, count;
+        } leaf;
+    } u;
+    int32_t meta;
+    int32_t pad;
+};
+constexpr int TV_STRIDE = 10;  // doubles per triangle in the vertex soup (A, B, C, pad) -> 80 B
+
 struct DScene {
     const double* vertices;
+    const double* tv;  // per-triangle vertex soup: A.xyz B.xyz C.xyz (removes the index indirection)
+    const DKd* kdp;    // packed kd nodes
     const double* normals;
     const double* uvs;
     const lumo_triangle* tris;
@@ -48,8 +64,8 @@ struct DScene {
     // can be staged into LDS once per workgroup; hot_bytes == 0 disables staging.
     const char* hot;
     uint32_t hot_bytes;
-    uint32_t off_onodes, off_oitems, off_lnodes, off_litems, off_objs, off_lights, off_kd, off_kd_items, off_tris,
-        off_vertices, off_xforms;
+    uint32_t off_onodes, off_oitems, off_lnodes, off_litems, off_objs, off_lights, off_kd_items, off_tris, off_xforms,
+        off_tv, off_kdp;
 };
 
 // Copy the packed traversal set into LDS and point a scene view at it.
@@ -65,11 +81,11 @@ __device__ __forceinline__ DScene stage_scene_lds(const DScene& sc, char* lds) {
     v.litems = reinterpret_cast<const int32_t*>(lds + sc.off_litems);
     v.objs = reinterpret_cast<const lumo_object*>(lds + sc.off_objs);
     v.lights = reinterpret_cast<const lumo_object*>(lds + sc.off_lights);
-    v.kd = reinterpret_cast<const lumo_kd_node*>(lds + sc.off_kd);
     v.kd_items = reinterpret_cast<const int32_t*>(lds + sc.off_kd_items);
     v.tris = reinterpret_cast<const lumo_triangle*>(lds + sc.off_tris);
-    v.vertices = reinterpret_cast<const double*>(lds + sc.off_vertices);
     v.xforms = reinterpret_cast<const lumo_transform*>(lds + sc.off_xforms);
+    v.tv = reinterpret_cast<const double*>(lds + sc.off_tv);
+    v.kdp = reinterpret_cast<const DKd*>(lds + sc.off_kdp);
     return v;
 }
 
@@ -256,8 +272,8 @@ __device__ __forceinline__ void slab(const double* bmin, const double* bmax, V3 
 __device__ __forceinline__ double tri_hit_t(const DScene& sc, int ti, const RayX& r, double t_min, double t_max,
                                             Counters& C) {
     C.tri++;
-    const lumo_triangle T = sc.tris[ti];
-    const V3 A = ld3(sc.vertices + 3 * T.v[0]), B = ld3(sc.vertices + 3 * T.v[1]), Cv = ld3(sc.vertices + 3 * T.v[2]);
+    const double* tv = sc.tv + TV_STRIDE * ti;
+    const V3 A = ld3(tv), B = ld3(tv + 3), Cv = ld3(tv + 6);
     const int kz = r.kz;
     const V3 wi = r.wi;
     V3 at = perm_kz(kz, A - r.o), bt = perm_kz(kz, B - r.o), ct = perm_kz(kz, Cv - r.o);
@@ -281,8 +297,8 @@ __device__ __forceinline__ double tri_hit_t(const DScene& sc, int ti, const RayX
 // check (callers that only need acceptance and t; the record is rebuilt identically later).
 template <bool FULL>
 __device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_min, double t_max, DHit& out) {
-    const lumo_triangle T = sc.tris[ti];
-    const V3 A = ld3(sc.vertices + 3 * T.v[0]), B = ld3(sc.vertices + 3 * T.v[1]), Cv = ld3(sc.vertices + 3 * T.v[2]);
+    const double* tv = sc.tv + TV_STRIDE * ti;
+    const V3 A = ld3(tv), B = ld3(tv + 3), Cv = ld3(tv + 6);
     const int kz = r.kz;
     const V3 wi = r.wi;
     V3 at = perm_kz(kz, A - r.o), bt = perm_kz(kz, B - r.o), ct = perm_kz(kz, Cv - r.o);
@@ -312,6 +328,7 @@ __device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_mi
     out.t = t;
     if (!FULL) return true;
     const V3 bary = e / det;
+    const lumo_triangle T = sc.tris[ti];
     const V3 ng = normalize(cross(B - A, Cv - A));
     V3 ns = ng;
     if (T.n[0] >= 0)
@@ -362,10 +379,12 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
     double t_start = rmax(ts, t_min), t_end = rmin(te, t_max);
     for (;;) {
         if (t_hit < t_start) break;
-        const lumo_kd_node node = sc.kd[curr];
-        if (node.leaf) {
-            for (int k = 0; k < node.count; ++k) {
-                const int i = sc.kd_items[ob.item_base + node.first + k];
+        const DKd node = sc.kdp[curr];
+        const int axis = node.meta & 3;
+        if (axis == 3) {
+            const int first = node.u.leaf.first, count = node.u.leaf.count;
+            for (int k = 0; k < count; ++k) {
+                const int i = sc.kd_items[ob.item_base + first + k];
                 const double t = tri_hit_t(sc, ob.tri_base + i, r, t_min, t_end, C);
                 if (GEO) {
                     if (t < t_end) {
@@ -384,11 +403,13 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
             t_end = st_te[sp];
         } else {
             C.kd++;
-            const int ax = node.axis;
-            const double t_split = (node.point - origin[ax]) * inv_dir[ax];
-            const bool left_first = origin[ax] < node.point || (origin[ax] == node.point && inv_dir[ax] <= 0.0);
-            const int first = left_first ? curr + 1 : node.right;
-            const int second = left_first ? node.right : curr + 1;
+            const int ax = axis;
+            const double point = node.u.point;
+            const int right = node.meta >> 2;
+            const double t_split = (point - origin[ax]) * inv_dir[ax];
+            const bool left_first = origin[ax] < point || (origin[ax] == point && inv_dir[ax] <= 0.0);
+            const int first = left_first ? curr + 1 : right;
+            const int second = left_first ? right : curr + 1;
             if (t_split > t_end || t_split <= 0.0) {
                 curr = first;
             } else if (t_split < t_start) {
@@ -1000,9 +1021,8 @@ __device__ __forceinline__ int sample_light(const DScene& sc, double u) {
 // Sampleable::sample_on -> point (rectangle.rs:113-125, triangle.rs:214-240)
 __device__ __forceinline__ V3 shape_sample_on(const DScene& sc, const lumo_object& L, V2 rs) {
     if (L.type == LUMO_OBJ_TRIANGLE) {
-        const lumo_triangle T = sc.tris[L.tri_base];
-        const V3 A = ld3(sc.vertices + 3 * T.v[0]), B = ld3(sc.vertices + 3 * T.v[1]),
-                 Cv = ld3(sc.vertices + 3 * T.v[2]);
+        const double* tv = sc.tv + TV_STRIDE * L.tri_base;
+        const V3 A = ld3(tv), B = ld3(tv + 3), Cv = ld3(tv + 6);
         const double gam = 1.0 - sqrt(1.0 - rs.x);
         const double beta = rs.y * (1.0 - gam);
         return A + beta * (B - A) + gam * (Cv - A);

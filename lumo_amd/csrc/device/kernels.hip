@@ -761,6 +761,7 @@ void by_stack_class(int cls, F&& f) {
         case 8: f(std::integral_constant<int, 8>{}); break;
         case 16: f(std::integral_constant<int, 16>{}); break;
         case 32: f(std::integral_constant<int, 32>{}); break;
+        case 48: f(std::integral_constant<int, 48>{}); break;
         default: f(std::integral_constant<int, 64>{}); break;
     }
 }
@@ -1124,6 +1125,28 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     chk(upload(*c, d->materials, (size_t)d->num_materials, &s.mats));
     chk(upload(*c, d->dense_spectra, (size_t)95 * d->num_dense_spectra, &s.dense));
     chk(upload(*c, d->transforms, (size_t)d->num_transforms, &s.xforms));
+    // device-only layouts: triangle vertex soup and 16-B kd nodes
+    std::vector<double> tv((size_t)TV_STRIDE * d->num_triangles, 0.0);
+    for (int i = 0; i < d->num_triangles; ++i)
+        for (int k = 0; k < 3; ++k)
+            for (int a = 0; a < 3; ++a) tv[(size_t)TV_STRIDE * i + 3 * k + a] = d->vertices[3 * d->triangles[i].v[k] + a];
+    std::vector<DKd> kdp(d->num_kd_nodes);
+    for (int i = 0; i < d->num_kd_nodes; ++i) {
+        const lumo_kd_node& n = d->kd_nodes[i];
+        DKd k{};
+        if (n.leaf) {
+            k.u.leaf.first = n.first;
+            k.u.leaf.count = n.count;
+            k.meta = 3;
+        } else {
+            if (n.right < 0 || n.right >= (1 << 29) || n.axis < 0 || n.axis > 2) chk(LUMO_ERR_INVALID);
+            k.u.point = n.point;
+            k.meta = (n.right << 2) | n.axis;
+        }
+        kdp[i] = k;
+    }
+    chk(upload(*c, tv.data(), tv.size(), &s.tv));
+    chk(upload(*c, kdp.data(), kdp.size(), &s.kdp));
     if (st) {
         free_scene(*c);
         return st;
@@ -1145,10 +1168,10 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         s.off_litems = put(d->light_items, sizeof(int32_t) * d->num_light_items);
         s.off_objs = put(d->objects, sizeof(lumo_object) * d->num_objects);
         s.off_lights = put(d->lights, sizeof(lumo_object) * d->num_lights);
-        s.off_kd = put(d->kd_nodes, sizeof(lumo_kd_node) * d->num_kd_nodes);
+        s.off_kdp = put(kdp.data(), sizeof(DKd) * kdp.size());
         s.off_kd_items = put(d->kd_items, sizeof(int32_t) * d->num_kd_items);
         s.off_tris = put(d->triangles, sizeof(lumo_triangle) * d->num_triangles);
-        s.off_vertices = put(d->vertices, sizeof(double) * 3 * d->num_vertices);
+        s.off_tv = put(tv.data(), sizeof(double) * tv.size());
         s.off_xforms = put(d->transforms, sizeof(lumo_transform) * d->num_transforms);
         s.hot_bytes = 0;
         if (hot.size() <= 48 * 1024) {
@@ -1200,10 +1223,10 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         free_scene(*c);
         return LUMO_ERR_UNSUPPORTED;  // lumo's fixed [_; 64] stacks would overflow too
     }
-    s.stack_class = need <= 8 ? 8 : need <= 16 ? 16 : need <= 32 ? 32 : 64;
+    s.stack_class = need <= 8 ? 8 : need <= 16 ? 16 : need <= 32 ? 32 : need <= 48 ? 48 : 64;
     if (const char* e = std::getenv("LUMO_STACK_CLASS")) {  // A/B override (never below `need`)
         const int f = std::atoi(e);
-        if (f >= need && (f == 8 || f == 16 || f == 32 || f == 64)) s.stack_class = f;
+        if (f >= need && (f == 8 || f == 16 || f == 32 || f == 48 || f == 64)) s.stack_class = f;
     }
     c->has_scene = true;
     return LUMO_OK;
