@@ -59,7 +59,7 @@ struct DScene {
     const lumo_material* mats;
     const double* dense;
     const lumo_transform* xforms;
-    int32_t n_onodes, n_lnodes, n_lights, n_shadow, stack_class;
+    int32_t n_onodes, n_lnodes, n_lights, n_shadow, stack_class, full;
     // Traversal working set packed contiguously (16-B aligned sub-arrays) so that a small scene
     // can be staged into LDS once per workgroup; hot_bytes == 0 disables staging.
     const char* hot;
@@ -543,55 +543,72 @@ __device__ double sphere_hit_t(const lumo_object& ob, const RayX& r, double t_mi
 constexpr int PRIM_SPHERE = -2;
 
 // Object::hit_t of the shape (kdtree.rs:178-180, rectangle.rs:87-89, triangle.rs:195-197)
-template <int STK>
+// FX: full feature set (instances, spheres, triangle objects, microfacet materials); scenes made
+// only of kd meshes / rectangles with Lambertian + Light materials run the FX = false kernels.
+template <int STK, bool FX>
 __device__ __forceinline__ double shape_hit_t(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                               double t_max, Counters& C) {
-    if (ob.type == LUMO_OBJ_TRIANGLE) return tri_hit_t(sc, ob.tri_base, r, t_min, t_max, C);
-    if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit_t(ob, r, t_min, t_max);
+    if constexpr (FX) {
+        if (ob.type == LUMO_OBJ_TRIANGLE) return tri_hit_t(sc, ob.tri_base, r, t_min, t_max, C);
+        if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit_t(ob, r, t_min, t_max);
+    }
     return kd_traverse<false, STK>(sc, ob, r, t_min, t_max, nullptr, C);
 }
-template <int STK>
+template <int STK, bool FX>
 __device__ __forceinline__ double object_hit_t(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                                double t_max, Counters& C) {
-    if (ob.xform < 0) return shape_hit_t<STK>(sc, ob, r, t_min, t_max, C);
-    return shape_hit_t<STK>(sc, ob, ray_local(sc.xforms[ob.xform], r), t_min, t_max, C);
+    if constexpr (FX) {
+        if (ob.xform >= 0) return shape_hit_t<STK, FX>(sc, ob, ray_local(sc.xforms[ob.xform], r), t_min, t_max, C);
+    }
+    return shape_hit_t<STK, FX>(sc, ob, r, t_min, t_max, C);
 }
 
 // Object::hit: kd GEO traversal, then the winner's GEO test (acceptance + t only; the record is
 // rebuilt by object_record).  Returns the global triangle index, PRIM_SPHERE, or -1 (miss).
-template <int STK>
+template <int STK, bool FX>
 __device__ __forceinline__ int shape_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                              double t_max, Counters& C, DHit& out) {
-    if (ob.type == LUMO_OBJ_TRIANGLE) return tri_hit_geo<false>(sc, ob.tri_base, r, t_min, t_max, out) ? ob.tri_base : -1;
-    if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit<false>(ob, r, t_min, t_max, out) ? PRIM_SPHERE : -1;
+    if constexpr (FX) {
+        if (ob.type == LUMO_OBJ_TRIANGLE)
+            return tri_hit_geo<false>(sc, ob.tri_base, r, t_min, t_max, out) ? ob.tri_base : -1;
+        if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit<false>(ob, r, t_min, t_max, out) ? PRIM_SPHERE : -1;
+    }
     int idx = -1;
     kd_traverse<true, STK>(sc, ob, r, t_min, t_max, &idx, C);
     if (idx < 0) return -1;
     if (!tri_hit_geo<false>(sc, ob.tri_base + idx, r, t_min, t_max, out)) return -1;
     return ob.tri_base + idx;
 }
-template <int STK>
+template <int STK, bool FX>
 __device__ __forceinline__ int object_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                               double t_max, Counters& C, DHit& out) {
-    if (ob.xform < 0) return shape_hit_tri<STK>(sc, ob, r, t_min, t_max, C, out);
-    return shape_hit_tri<STK>(sc, ob, ray_local(sc.xforms[ob.xform], r), t_min, t_max, C, out);
+    if constexpr (FX) {
+        if (ob.xform >= 0) return shape_hit_tri<STK, FX>(sc, ob, ray_local(sc.xforms[ob.xform], r), t_min, t_max, C, out);
+    }
+    return shape_hit_tri<STK, FX>(sc, ob, r, t_min, t_max, C, out);
 }
 
 // Full hit record of triangle `tri` of object `ob` for world ray r (the GEO test is
 // deterministic, so re-running it reproduces the accepted hit), incl. Rectangle uv
 // (rectangle.rs:74-85) and the instance transform.
+template <bool FX>
 __device__ void object_record(const DScene& sc, const lumo_object& ob, int tri, const RayX& r, DHit& h) {
-    const RayX rl = ob.xform < 0 ? r : ray_local(sc.xforms[ob.xform], r);
-    if (ob.type == LUMO_OBJ_SPHERE)
-        sphere_hit<true>(ob, rl, 0.0, DINF, h);
-    else
-        tri_hit_geo<true>(sc, tri, rl, 0.0, DINF, h);
-    if (ob.type == LUMO_OBJ_RECTANGLE) h.uv = wrap_uv(V2{dot(ld3(ob.b0), h.p), dot(ld3(ob.b1), h.p)});
-    if (ob.xform >= 0) instance_fix_hit(sc.xforms[ob.xform], ob.material_override, h);
+    if constexpr (!FX) {
+        tri_hit_geo<true>(sc, tri, r, 0.0, DINF, h);
+        if (ob.type == LUMO_OBJ_RECTANGLE) h.uv = wrap_uv(V2{dot(ld3(ob.b0), h.p), dot(ld3(ob.b1), h.p)});
+    } else {
+        const RayX rl = ob.xform < 0 ? r : ray_local(sc.xforms[ob.xform], r);
+        if (ob.type == LUMO_OBJ_SPHERE)
+            sphere_hit<true>(ob, rl, 0.0, DINF, h);
+        else
+            tri_hit_geo<true>(sc, tri, rl, 0.0, DINF, h);
+        if (ob.type == LUMO_OBJ_RECTANGLE) h.uv = wrap_uv(V2{dot(ld3(ob.b0), h.p), dot(ld3(ob.b1), h.p)});
+        if (ob.xform >= 0) instance_fix_hit(sc.xforms[ob.xform], ob.material_override, h);
+    }
 }
 
 // bvh.rs:315-362: returns object index or -1
-template <bool GEO, int STK>
+template <bool GEO, int STK, bool FX>
 __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_nodes, const int32_t* items,
                             const lumo_object* objs, const RayX& r, double t_min, double t_max, Counters& C,
                             double* t_found = nullptr) {
@@ -616,7 +633,7 @@ __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_
             }
             for (int k = 0; k < count; ++k) {
                 const int i = items[node.first + k];
-                const double t = object_hit_t<STK>(sc, objs[i], r, t_min, tt, C);
+                const double t = object_hit_t<STK, FX>(sc, objs[i], r, t_min, tt, C);
                 if (GEO) {
                     if (t < tt) {
                         tt = t;
@@ -635,14 +652,14 @@ __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_
 }
 
 // BVH::hit_t (bvh.rs:371-374)
-template <int STK>
+template <int STK, bool FX>
 __device__ __forceinline__ double bvh_hit_t(const DScene& sc, const lumo_bvh_node* nodes, int n, const int32_t* items,
                                             const lumo_object* objs, const RayX& r, double t_min, double t_max,
                                             Counters& C) {
     // bvh.rs:371-374 re-runs objects[idx].hit_t(r, t_min, t_max); in any-hit mode the traversal
     // called exactly that (tt == t_max), so its value is reused.
     double t = DINF;
-    const int idx = bvh_traverse<false, STK>(sc, nodes, n, items, objs, r, t_min, t_max, C, &t);
+    const int idx = bvh_traverse<false, STK, FX>(sc, nodes, n, items, objs, r, t_min, t_max, C, &t);
     if (idx < 0) return DINF;
     return t;
 }
@@ -652,44 +669,45 @@ struct HitRef {
     double t;
     int kind, obj, tri;
 };
-template <int STK>
+template <int STK, bool FX>
 __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     HitRef h{DINF, 0, -1, -1};
     double t_max = DINF;
     DHit g;
-    int oi = bvh_traverse<true, STK>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C);
+    int oi = bvh_traverse<true, STK, FX>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C);
     if (oi >= 0) {
-        const int tri = object_hit_tri<STK>(sc, sc.objs[oi], r, 0.0, t_max, C, g);
+        const int tri = object_hit_tri<STK, FX>(sc, sc.objs[oi], r, 0.0, t_max, C, g);
         if (tri != -1) {
             h = HitRef{g.t, 1, oi, tri};
             t_max = g.t;
         }
     }
-    const int li = bvh_traverse<true, STK>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C);
+    const int li = bvh_traverse<true, STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C);
     if (li >= 0) {
-        const int tri = object_hit_tri<STK>(sc, sc.lights[li], r, 0.0, t_max, C, g);
+        const int tri = object_hit_tri<STK, FX>(sc, sc.lights[li], r, 0.0, t_max, C, g);
         if (tri != -1) h = HitRef{g.t, 2, li, tri};
     }
     return h;
 }
 
 // Rebuild the full hit record of a closest hit (the GEO test is deterministic).
+template <bool FX>
 __device__ __forceinline__ void hit_record(const DScene& sc, const HitRef& hr, const RayX& r, DHit& h) {
     const lumo_object& ob = hr.kind == 1 ? sc.objs[hr.obj] : sc.lights[hr.obj];
-    object_record(sc, ob, hr.tri, r, h);
+    object_record<FX>(sc, ob, hr.tri, r, h);
 }
 
 // Scene::hit_light (scene.rs:165-189): returns true and the light hit if visible.
-template <int STK>
+template <int STK, bool FX>
 __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit& lh, Counters& C) {
     const lumo_object& L = sc.lights[light];
-    const int tri = object_hit_tri<STK>(sc, L, r, 0.0, DINF, C, lh);
+    const int tri = object_hit_tri<STK, FX>(sc, L, r, 0.0, DINF, C, lh);
     if (tri == -1) return false;
     const double t_max = lh.t - EPSILON;
-    if (bvh_hit_t<STK>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C) < t_max) return false;
-    if (bvh_hit_t<STK>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C) < t_max) return false;
+    if (bvh_hit_t<STK, FX>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C) < t_max) return false;
+    if (bvh_hit_t<STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C) < t_max) return false;
     // visible: build the light hit record (same GEO test, now in full)
-    object_record(sc, L, tri, r, lh);
+    object_record<FX>(sc, L, tri, r, lh);
     return true;
 }
 
@@ -864,8 +882,14 @@ __device__ __forceinline__ bool standard_kind(int k) {
 }
 
 // Material::bsdf_sample (material.rs:273-289 -> bsdf.rs -> bxdf.rs:104-124); may terminate L
+template <bool FX>
 __device__ bool bsdf_sample(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, double* L,
                             double rand_u, V2 rs, V3& wi) {
+    if constexpr (!FX) {  // Lambertian / Light only
+        if (m.kind != LUMO_MAT_LAMBERTIAN || h.backface) return false;
+        wi = onb_world(onb_new(h.ns), square_to_cos_hemisphere(rs));
+        return true;
+    }
     if (!standard_kind(m.kind)) return false;
     const Onb uvw = onb_new(h.ns);
     const V3 o = onb_local(uvw, wo);
@@ -908,7 +932,14 @@ __device__ bool bsdf_sample(const DScene& sc, const lumo_material& m, const DHit
     return true;
 }
 // Material::bsdf_pdf (material.rs:292-306 -> bsdf.rs:70-84 -> bxdf.rs:127-150)
+template <bool FX>
 __device__ double bsdf_pdf(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, V3 wi, const double* L) {
+    if constexpr (!FX) {
+        if (m.kind != LUMO_MAT_LAMBERTIAN) return 0.0;
+        if (!(dot(h.ng, wi) * dot(h.ng, wo) >= 0.0)) return 0.0;
+        const Onb uvw = onb_new(h.ns);
+        return cos_hemisphere_pdf(onb_local(uvw, wo), onb_local(uvw, wi));
+    }
     if (!standard_kind(m.kind)) return 0.0;
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
     const Onb uvw = onb_new(h.ns);
@@ -949,7 +980,13 @@ __device__ double bsdf_pdf(const DScene& sc, const lumo_material& m, const DHit&
     return mf_normal_pdf(d, wh, o) * fabs(hwi) / sq(hwi + hwo / er) * pt / (pr + pt);
 }
 // Material::bsdf_f, Transport::Radiance (material.rs:254-270 -> bsdf.rs:28-48 -> bxdf.rs:71-100)
+template <bool FX>
 __device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, V3 wi, const double* L) {
+    if constexpr (!FX) {
+        if (m.kind != LUMO_MAT_LAMBERTIAN) return cfill(0.0);
+        if (!(dot(h.ng, wi) * dot(h.ng, wo) >= 0.0) || h.backface) return cfill(0.0);
+        return spec_sample(m.albedo, L) / PI;
+    }
     if (!standard_kind(m.kind)) return cfill(0.0);
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
     const Onb uvw = onb_new(h.ns);
@@ -993,12 +1030,16 @@ __device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h
 __device__ __forceinline__ double shading_cosine(const lumo_material& m, V3 wi, V3 ns) {
     return standard_kind(m.kind) ? fabs(dot(ns, wi)) : 1.0;
 }
+template <bool FX>
 __device__ __forceinline__ bool mat_is_specular(const lumo_material& m) {  // bxdf.rs:33-40
+    if constexpr (!FX) return false;
     if (m.kind == LUMO_MAT_MF_DIELECTRIC) return true;
     if (m.kind == LUMO_MAT_MF_CONDUCTOR) return (m.roughness + m.roughness) / 2.0 < 0.01;
     return false;
 }
+template <bool FX>
 __device__ __forceinline__ bool mat_is_delta(const DScene& sc, const lumo_material& m, const double* L) {
+    if constexpr (!FX) return false;
     if (m.kind == LUMO_MAT_MF_CONDUCTOR) return (m.roughness + m.roughness) / 2.0 < 1e-3;
     if (m.kind == LUMO_MAT_MF_DIELECTRIC)
         return (m.roughness + m.roughness) / 2.0 < 1e-3 || dense_one(sc.dense + 95 * m.eta_idx, L[0]) == 1.0;
@@ -1066,7 +1107,9 @@ __device__ V3 shape_sample_towards(const DScene& sc, const lumo_object& L, V3 xo
     return normalize(xi - xo);
 }
 // Sampleable::sample_towards (Instance: instance.rs:162-167)
+template <bool FX>
 __device__ V3 light_sample_towards(const DScene& sc, const lumo_object& L, V3 xo, V2 rs) {
+    if constexpr (!FX) return normalize(ld3(L.origin) + rs.x * ld3(L.b0) + rs.y * ld3(L.b1) - xo);  // Rectangle
     if (L.xform < 0) return shape_sample_towards(sc, L, xo, rs);
     const lumo_transform& T = sc.xforms[L.xform];
     const V3 xl = xf_apply(T.inv, xo, 1.0);
@@ -1074,7 +1117,12 @@ __device__ V3 light_sample_towards(const DScene& sc, const lumo_object& L, V3 xo
     return normalize(xf_apply(T.m, dl, 0.0));
 }
 // Sampleable::sample_towards_pdf (object.rs:149-156; Instance: instance.rs:169-199)
+template <bool FX>
 __device__ double light_pdf(const DScene& sc, const lumo_object& L, const RayX& ri, V3 xi, V3 ng) {
+    if constexpr (!FX) {
+        const double p_area = 1.0 / L.area;
+        return p_area * distance_squared(ri.o, xi) / fabs(dot(ng, ri.d));
+    }
     if (L.xform < 0) return shape_pdf(L, ri.o, ri.d, xi, ng);
     const lumo_transform& T = sc.xforms[L.xform];
     const M3 N{V3{T.nrm[0], T.nrm[1], T.nrm[2]}, V3{T.nrm[3], T.nrm[4], T.nrm[5]}, V3{T.nrm[6], T.nrm[7], T.nrm[8]}};

@@ -262,7 +262,7 @@ __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, in
 }
 
 // ------------------------------------------------------------------ closest hit
-template <int STK, bool LDS>
+template <int STK, bool LDS, bool FX>
 __global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc0, Paths S, const int32_t* queue, uint32_t count) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
         const int s = queue[q];
         const RayX r = rayx(Ray{ldv3(S.ro, s), ldv3(S.rd, s)});
-        const HitRef h = scene_hit<STK>(sc, r, C);
+        const HitRef h = scene_hit<STK, FX>(sc, r, C);
         S.hit_t[s] = h.t;
         S.hit_kind[s] = h.kind;
         S.hit_obj[s] = h.obj;
@@ -281,6 +281,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc
 }
 
 // ------------------------------------------------------------------ shade
+template <bool FX>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue, uint32_t count,
                                                   int32_t* next_queue) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -295,7 +296,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
             const Ray ro{ldv3(S.ro, s), ldv3(S.rd, s)};
             const HitRef hr{S.hit_t[s], kind, S.hit_obj[s], S.hit_tri[s]};
             DHit ho;
-            hit_record(sc, hr, rayx(ro), ho);
+            hit_record<FX>(sc, hr, rayx(ro), ho);
             const lumo_material m = sc.mats[ho.material];
             Xorshift rng{S.rng[2 * s], S.rng[2 * s + 1]};
             if (s == g_dbg.slot && g_dbg.pass == g_dbg.cur_pass && g_dbg.n < 64) {
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
             const double rand_u = xs_float(rng);
             const V2 sq = xs_vec2(rng);
             V3 wi;
-            const bool sampled = bsdf_sample(sc, m, ho, wo, L, rand_u, sq, wi);
+            const bool sampled = bsdf_sample<FX>(sc, m, ho, wo, L, rand_u, sq, wi);
             if (m.kind == LUMO_MAT_MF_DIELECTRIC && !(m.flags & LUMO_MATF_CONSTANT_ETA)) {
                 for (int i = 1; i < NS; ++i) S.lam[4 * s + i] = 0.0;  // lambda terminated (even if None)
             }
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
                 stc(S.rad, s, radiance);
             } else {
                 // NEE: n_shadow x [light pick, light direction, BSDF sample] (integrator.rs:87-137)
-                if (!mat_is_delta(sc, m, L)) {
+                if (!mat_is_delta<FX>(sc, m, L)) {
                     const int base = s * 2 * ns;
                     for (int i = 0; i < ns; ++i) {
                         const int li = sample_light(sc, xs_float(rng));
@@ -330,13 +331,13 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
                         S.pdf_l[s * ns + i] = sc.alias_pdf[li];
                         {
                             const V2 rs = xs_vec2(rng);
-                            const V3 w = light_sample_towards(sc, Lo, ho.p, rs);
+                            const V3 w = light_sample_towards<FX>(sc, Lo, ho.p, rs);
                             const Ray ri = spawn(ho, w);
                             const int rec = base + 2 * i;
                             stv3(S.sh_o, rec, ri.o);
                             stv3(S.sh_d, rec, ri.d);
-                            stc(S.sh_f, rec, bsdf_f(sc, m, ho, wo, w, L));
-                            S.sh_psct[rec] = bsdf_pdf(sc, m, ho, wo, w, L);
+                            stc(S.sh_f, rec, bsdf_f<FX>(sc, m, ho, wo, w, L));
+                            S.sh_psct[rec] = bsdf_pdf<FX>(sc, m, ho, wo, w, L);
                             S.sh_cos[rec] = shading_cosine(m, w, ho.ns);
                             S.sh_light[rec] = li;
                             S.sh_flags[rec] = 1 | 2;  // valid | light-sampled
@@ -347,12 +348,12 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
                             const V2 rsq = xs_vec2(rng);
                             V3 w;
                             const int rec = base + 2 * i + 1;
-                            if (bsdf_sample(sc, m, ho, wo, L, ru, rsq, w)) {
+                            if (bsdf_sample<FX>(sc, m, ho, wo, L, ru, rsq, w)) {
                                 const Ray ri = spawn(ho, w);
                                 stv3(S.sh_o, rec, ri.o);
                                 stv3(S.sh_d, rec, ri.d);
-                                stc(S.sh_f, rec, bsdf_f(sc, m, ho, wo, w, L));
-                                S.sh_psct[rec] = bsdf_pdf(sc, m, ho, wo, w, L);
+                                stc(S.sh_f, rec, bsdf_f<FX>(sc, m, ho, wo, w, L));
+                                S.sh_psct[rec] = bsdf_pdf<FX>(sc, m, ho, wo, w, L);
                                 S.sh_cos[rec] = shading_cosine(m, w, ho.ns);
                                 S.sh_light[rec] = li;
                                 S.sh_flags[rec] = 1;
@@ -368,9 +369,9 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
                 // spawn the continuation (path_trace.rs:42-77)
                 const Ray ri = spawn(ho, wi);
                 const V3 wi2 = ri.d;
-                const double p_scatter = bsdf_pdf(sc, m, ho, wo, wi2, L);
+                const double p_scatter = bsdf_pdf<FX>(sc, m, ho, wo, wi2, L);
                 if (p_scatter > 0.0) {
-                    const DColor bsdf = bsdf_f(sc, m, ho, wo, wi2, L);
+                    const DColor bsdf = bsdf_f<FX>(sc, m, ho, wo, wi2, L);
                     gathered = gathered * (bsdf * shading_cosine(m, wi2, ho.ns) / p_scatter);
                     bool cont = true;
                     const uint32_t depth = S.depth[s];
@@ -383,7 +384,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
                             gathered = gathered / rr_prob;
                     }
                     if (cont) {
-                        S.flags[s] = mat_is_specular(m) ? 1u : 0u;  // last_specular
+                        S.flags[s] = mat_is_specular<FX>(m) ? 1u : 0u;  // last_specular
                         S.depth[s] = depth + 1;
                         stv3(S.ro, s, ri.o);
                         stv3(S.rd, s, ri.d);
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
 // ------------------------------------------------------------------ shadow (hit_light + MIS)
 // One thread per (resolve-queue slot, shadow record); `count` = resolve count x 2 n_shadow.
 // Records whose BSDF sample failed are skipped (k_resolve reads them as black).
-template <int STK, bool LDS>
+template <int STK, bool LDS, bool FX>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0, Paths S, uint32_t count) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
@@ -418,9 +419,9 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0,
         const int li = S.sh_light[rec];
         DHit hi;
         DColor out = cfill(0.0);
-        if (scene_hit_light<STK>(sc, ri, li, hi, C)) {
+        if (scene_hit_light<STK, FX>(sc, ri, li, hi, C)) {
             const lumo_object& Lo = sc.lights[li];
-            const double p_lig = light_pdf(sc, Lo, ri, hi.p, hi.ng);
+            const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
             const double p_sct = S.sh_psct[rec];
             if (!(p_lig == 0.0 || p_sct == 0.0)) {  // mis_sample (integrator.rs:139-184)
                 double L[NS];
@@ -600,7 +601,7 @@ __global__ void k_trace(DScene sc, const double* o, const double* d, const int32
     if (i < n) {
         const RayX r = rayx(Ray{ldv3(o, i), ldv3(d, i)});
         if (!any_hit) {
-            const HitRef h = scene_hit<STK>(sc, r, C);
+            const HitRef h = scene_hit<STK, true>(sc, r, C);
             t_out[i] = h.t;
             kind_out[i] = h.kind;
             obj_out[i] = h.obj;
@@ -608,7 +609,7 @@ __global__ void k_trace(DScene sc, const double* o, const double* d, const int32
         } else {
             DHit lh;
             const int li = light[i];
-            const bool vis = scene_hit_light<STK>(sc, r, li, lh, C);
+            const bool vis = scene_hit_light<STK, true>(sc, r, li, lh, C);
             t_out[i] = vis ? lh.t : DINF;
             kind_out[i] = vis ? 2 : 0;
             obj_out[i] = vis ? li : -1;
@@ -774,10 +775,16 @@ void launch_trav(Ctx& c, uint32_t count, F&& f) {
     const bool lds = g_lds && c.sc.hot_bytes > 0;
     const int grid_full = ceil_div(count, BLOCK);
     by_stack_class(c.sc.stack_class, [&](auto K) {
-        if (lds)
-            f(K, std::true_type{}, std::min(grid_full, c.lds_grid_cap), (size_t)c.sc.hot_bytes);
+        auto go = [&](auto Fx) {
+            if (lds)
+                f(K, std::true_type{}, Fx, std::min(grid_full, c.lds_grid_cap), (size_t)c.sc.hot_bytes);
+            else
+                f(K, std::false_type{}, Fx, grid_full, (size_t)0);
+        };
+        if (c.sc.full)
+            go(std::true_type{});
         else
-            f(K, std::false_type{}, grid_full, (size_t)0);
+            go(std::false_type{});
     });
 }
 
@@ -923,13 +930,17 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * 4, sm));
             {
                 StageTimer tm(c, g_timing, ST_CLOSEST);
-                launch_trav(c, qn, [&](auto K, auto Lds, int grid, size_t shm) {
-                    k_closest<decltype(K)::value, decltype(Lds)::value><<<grid, BLOCK, shm, sm>>>(c.sc, S, qa, qn);
+                launch_trav(c, qn, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                    k_closest<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
+                        <<<grid, BLOCK, shm, sm>>>(c.sc, S, qa, qn);
                 });
             }
             {
                 StageTimer tm(c, g_timing, ST_SHADE);
-                k_shade<<<ceil_div(qn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qn, qb);
+                if (c.sc.full)
+                    k_shade<true><<<ceil_div(qn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qn, qb);
+                else
+                    k_shade<false><<<ceil_div(qn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qn, qb);
             }
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(counts, S.counts, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, sm));
@@ -939,8 +950,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             const uint32_t sn = rn * 2u * (uint32_t)ns;
             if (sn > 0) {
                 StageTimer tm(c, g_timing, ST_SHADOW);
-                launch_trav(c, sn, [&](auto K, auto Lds, int grid, size_t shm) {
-                    k_shadow<decltype(K)::value, decltype(Lds)::value><<<grid, BLOCK, shm, sm>>>(c.sc, S, sn);
+                launch_trav(c, sn, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                    k_shadow<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
+                        <<<grid, BLOCK, shm, sm>>>(c.sc, S, sn);
                 });
             }
             if (rn > 0) {
@@ -1228,6 +1240,16 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         const int f = std::atoi(e);
         if (f >= need && (f == 8 || f == 16 || f == 32 || f == 48 || f == 64)) s.stack_class = f;
     }
+    // feature class: the lean kernels cover kd meshes / rectangles with Lambertian + Light only
+    bool full = d->num_transforms > 0;
+    for (int i = 0; i < d->num_materials; ++i)
+        full = full || (d->materials[i].kind != LUMO_MAT_LAMBERTIAN && d->materials[i].kind != LUMO_MAT_LIGHT &&
+                        d->materials[i].kind != LUMO_MAT_BLANK);
+    for (int i = 0; i < d->num_objects; ++i)
+        full = full || (d->objects[i].type != LUMO_OBJ_KDMESH && d->objects[i].type != LUMO_OBJ_RECTANGLE);
+    for (int i = 0; i < d->num_lights; ++i) full = full || d->lights[i].type != LUMO_OBJ_RECTANGLE;
+    if (const char* e = std::getenv("LUMO_FULL_KERNELS")) full = full || std::atoi(e) != 0;  // A/B switch
+    s.full = full ? 1 : 0;
     c->has_scene = true;
     return LUMO_OK;
 }
