@@ -55,6 +55,15 @@ enum {
 int lumo_builder_instance_op(void* b, int is_light, int64_t index, int op, double x, double y, double z);
 /* Number of objects (is_light = 0) or lights (is_light != 0) added so far. */
 int64_t lumo_builder_count(void* b, int is_light);
+/* .obj ingest (parser.rs, parser/obj.rs, parser/mtl.rs) from in-memory file contents.
+ * lumo_builder_add_obj_mesh: parser::mesh_from_path - the whole file as one TriangleMesh with
+ *   `material`; returns the new object's index (for instance ops) or -1.
+ * lumo_builder_load_obj_scene: parser::scene_from_file - materials from the .mtl (mtl may be NULL),
+ *   one mesh per usemtl group, emissive (Ke) groups added as Triangle lights.  Returns LUMO_OK or
+ *   LUMO_ERR_INVALID; lumo_builder_error() then describes the problem. */
+int64_t lumo_builder_add_obj_mesh(void* b, const char* obj, size_t n, int material);
+int lumo_builder_load_obj_scene(void* b, const char* obj, size_t n_obj, const char* mtl, size_t n_mtl);
+const char* lumo_builder_error(void* b);
 /* Scene::cornell_box() */
 void* lumo_builder_cornell_box(void);
 /* Scene::empty_box(def_color, mat_left, mat_right) (scene/empty_box.rs:16-97) added to builder b;

@@ -145,6 +145,23 @@ class Material:
                                              int(bool(self.kw["two_sided"])))
 
 
+def _read_source(source, suffix):
+    """bytes of a file: raw bytes, a path, or (zip path, member name) -- the member is matched
+    case-insensitively by suffix like parser.rs::_extract_zip."""
+    if isinstance(source, (bytes, bytearray)):
+        return bytes(source)
+    if isinstance(source, tuple):
+        import zipfile
+        zpath, member = source
+        with zipfile.ZipFile(zpath) as z:
+            hits = [n for n in z.namelist() if n.lower().endswith((member or suffix).lower())]
+            if len(hits) != 1:
+                raise ValueError(f"{len(hits)} files matching {member or suffix} in {zpath}")
+            return z.read(hits[0])
+    with open(source, "rb") as f:
+        return f.read()
+
+
 class ObjectRef:
     """Handle to an object added to a Scene; Instanceable transformations compose in call order
     (object/instance.rs:203-299): mesh.to_unit_size().to_origin().rotate_y(a).translate(x, y, z)."""
@@ -249,6 +266,34 @@ class Scene:
         check(st, "add_rectangle")
         self._flat = None
         return ObjectRef(self, lib().lumo_builder_count(self._b, int(light)) - 1, light)
+
+    def add_obj(self, source, material):
+        """parser::mesh_from_path / mesh_from_url (parser.rs): the .obj (path, bytes, or
+        (zip path, member suffix)) as one TriangleMesh with `material`; returns an ObjectRef."""
+        data = _read_source(source, ".obj")
+        m = self._mat(material)
+        idx = lib().lumo_builder_add_obj_mesh(self._b, data, len(data), m)
+        if idx < 0:
+            raise ValueError("obj: " + lib().lumo_builder_error(self._b).decode())
+        self._flat = None
+        return ObjectRef(self, idx)
+
+    @staticmethod
+    def from_file(path, obj_name=None, mtllib=None):
+        """parser::scene_from_file (parser.rs): `path` a .zip holding `obj_name` (and `mtllib`),
+        or a plain .obj path with an optional .mtl path.  One mesh per usemtl group; emissive
+        groups become Triangle lights.  Image texture maps are not supported."""
+        if str(path).lower().endswith(".zip"):
+            obj = _read_source((path, obj_name), ".obj")
+            mtl = _read_source((path, mtllib), ".mtl") if mtllib else None
+        else:
+            obj = _read_source(path, ".obj")
+            mtl = _read_source(mtllib, ".mtl") if mtllib else None
+        s = Scene()
+        st = lib().lumo_builder_load_obj_scene(s._b, obj, len(obj), mtl, len(mtl) if mtl else 0)
+        if st != _ffi.LUMO_OK:
+            raise ValueError("obj scene: " + lib().lumo_builder_error(s._b).decode())
+        return s
 
     def add_sphere(self, radius, material, light=False):
         """Sphere::new(radius, material) at the origin (object/sphere.rs); returns an ObjectRef

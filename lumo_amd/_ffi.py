@@ -172,6 +172,9 @@ HOST_API = [
     ("lumo_builder_count", C.c_int64, [C.c_void_p, C.c_int]),
     ("lumo_builder_add_sphere", C.c_int, [C.c_void_p, C.c_double, C.c_int, C.c_int]),
     ("lumo_builder_set_environment_map", C.c_int, [C.c_void_p, Spectrum, C.c_double]),
+    ("lumo_builder_add_obj_mesh", C.c_int64, [C.c_void_p, C.c_char_p, C.c_size_t, C.c_int]),
+    ("lumo_builder_load_obj_scene", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]),
+    ("lumo_builder_error", C.c_char_p, [C.c_void_p]),
     ("lumo_builder_add_mesh", C.c_int, [C.c_void_p, c_double_p, C.c_int64, c_int64_p, c_int64_p, C.c_int64,
                                         C.c_int, C.c_int]),
     ("lumo_builder_add_rectangle", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p, C.c_int, C.c_int]),

@@ -6,6 +6,7 @@
 #include "../common/lmath.h"
 #include "../common/rng.h"
 #include "rgb2spec.h"
+#include "obj.h"
 #include "scene.h"
 
 using namespace lumo;
@@ -105,6 +106,31 @@ int lumo_builder_set_environment_map(void* b, lumo_spectrum tex, double scale) {
     sb->env_tex = tex;
     sb->env_scale = scale;
     return LUMO_OK;
+}
+int64_t lumo_builder_add_obj_mesh(void* b, const char* obj, size_t n, int material) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || !obj || material < 0 || material >= (int)sb->materials.size()) return -1;
+    try {
+        if (!load_obj_mesh(*sb, obj, n, material, sb->error)) return -1;
+    } catch (const std::exception& e) {
+        sb->error = e.what();
+        return -1;
+    }
+    return (int64_t)sb->objects.size() - 1;
+}
+int lumo_builder_load_obj_scene(void* b, const char* obj, size_t n_obj, const char* mtl, size_t n_mtl) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || !obj) return LUMO_ERR_INVALID;
+    try {
+        return load_obj_scene(*sb, obj, n_obj, mtl, n_mtl, sb->error) ? LUMO_OK : LUMO_ERR_INVALID;
+    } catch (const std::exception& e) {
+        sb->error = e.what();
+        return LUMO_ERR_INVALID;
+    }
+}
+const char* lumo_builder_error(void* b) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    return sb ? sb->error.c_str() : "null builder";
 }
 int lumo_builder_instance_op(void* b, int is_light, int64_t index, int op, double x, double y, double z) {
     SceneBuilder* sb = static_cast<SceneBuilder*>(b);

@@ -95,6 +95,7 @@ class SceneBuilder {
     std::vector<HostMaterial> materials;
     std::vector<HostObject> objects;
     std::vector<HostObject> lights;
+    std::string error;  // last builder error message (C ABI: lumo_builder_error)
 
     int add_material(const HostMaterial& m);
     // TriangleMesh::new (triangle_mesh.rs:46-60): fan-triangulated faces, degenerate dropped.

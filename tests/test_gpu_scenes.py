@@ -85,3 +85,12 @@ def test_bistro_standin_paths(dev):
     sc = scenes.bistro(bistro_standin(groups=40, lamps=64, n=4))
     cam = scenes.bistro_camera((48, 32))
     _paths(dev, sc, cam, L.make_tasks(48, 32, 8, SEED)[4])
+
+
+def test_obj_scene_paths(dev, tmp_path):
+    from test_obj import MTL, OBJ
+    (tmp_path / "s.obj").write_bytes(OBJ)
+    (tmp_path / "s.mtl").write_bytes(MTL)
+    sc = L.Scene.from_file(str(tmp_path / "s.obj"), mtllib=str(tmp_path / "s.mtl"))
+    cam = L.Camera.builder().origin(0.0, 1.2, 4.0).towards(0.0, 0.5, 0.0).resolution((32, 32)).build()
+    _paths(dev, sc, cam, L.make_tasks(32, 32, 16, SEED)[3])
