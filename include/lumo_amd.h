@@ -205,8 +205,10 @@ typedef struct {
     int32_t integrator; /* LUMO_INTEGRATOR_*                              */
     int32_t rng_mode;   /* LUMO_RNG_WAVEFRONT (GPU); lumo-order: oracle only */
     int32_t max_paths;  /* cap on paths in flight (0 = all pixels of the call) */
-    int32_t pad0;
+    int32_t tone_map;   /* LUMO_TONEMAP_* applied per sample before the film (task.rs:73-76)  */
+    double tone_arg;    /* ToneMap::Clamp upper bound                                          */
 } lumo_render_cfg;
+enum { LUMO_TONEMAP_NONE = 0, LUMO_TONEMAP_CLAMP = 1, LUMO_TONEMAP_REINHARD = 2 }; /* tone_mapping.rs */
 
 /* Ray batch for traversal-only queries (parity + micro-benchmarks). */
 typedef struct {

@@ -18,7 +18,7 @@ import numpy as np
 from . import _ffi
 from ._ffi import check
 
-__all__ = ["Spectrum", "Material", "Scene", "Camera", "Renderer", "Integrator", "Film", "Device",
+__all__ = ["Spectrum", "Material", "Scene", "Camera", "Renderer", "Integrator", "ToneMap", "Film", "Device",
            "DENSE", "TILE_SIZE", "SAMPLES_INCREMENT", "make_tasks"]
 
 TILE_SIZE = 16          # renderer.rs:15
@@ -375,14 +375,22 @@ class Camera:
             self.p.illuminant = DENSE[name] if isinstance(name, str) else int(name)
             return self
 
+        def color_space(self, cs):
+            """0 sRGB, 1 DCI-P3 (default), 2 Rec. 2020 (color/space.rs)."""
+            self.p.color_space = int(cs)
+            return self
+
         def build(self):
             d = _ffi.CameraDesc()
             check(lib().lumo_camera_build(C.byref(self.p), C.byref(d)), "camera build")
-            return Camera(d, (self.p.width, self.p.height))
+            cam = Camera(d, (self.p.width, self.p.height))
+            cam.color_space = self.p.color_space
+            return cam
 
-    def __init__(self, desc, resolution):
+    def __init__(self, desc, resolution, color_space=1):
         self.desc = desc
         self.resolution = resolution
+        self.color_space = color_space
 
     @staticmethod
     def builder():
@@ -405,6 +413,16 @@ class Integrator:
     PathTrace = 0
 
 
+class ToneMap:
+    """tone_mapping.rs: (kind, arg) pairs applied per sample before the film."""
+    NO_MAP = (0, 0.0)
+    REINHARD = (2, 0.0)
+
+    @staticmethod
+    def clamp(mx):
+        return (1, float(mx))
+
+
 def make_tasks(width, height, samples, seed):
     """renderer.rs:179-204: (batch, tile) tasks in publish order with their stream seeds."""
     L = lib()
@@ -417,8 +435,9 @@ def make_tasks(width, height, samples, seed):
 class Film:
     """Film pixels (film.rs:57-92): per pixel sum of w*rgb and sum of w (PIXEL_BUFFERS = 1)."""
 
-    def __init__(self, width, height):
+    def __init__(self, width, height, color_space=1):
         self.width, self.height = width, height
+        self.color_space = color_space  # the camera's ColorSpace (default DCI-P3)
         self.pixels = np.zeros((height, width, 4), dtype=np.float64)
 
     def add_tile(self, task, rgb_w):
@@ -431,6 +450,16 @@ class Film:
         """Pixel::value (film.rs:82-91): sum(w*rgb) / sum(w), linear colour-space RGB."""
         with np.errstate(invalid="ignore", divide="ignore"):
             return self.pixels[..., :3] / self.pixels[..., 3:4]
+
+    def rgb_image(self):
+        """Film::rgb_image (film.rs:173-192): encoded 8-bit RGB, rows top to bottom."""
+        from .image import encode
+        return encode(self.rgb(), self.color_space)
+
+    def save(self, path):
+        """Film::save (film.rs:195-210): 8-bit RGB PNG."""
+        from .image import write_png
+        write_png(path, self.rgb_image())
 
 
 class Device:
@@ -453,8 +482,9 @@ class Device:
             check(L.lumo_camera_set(self.ctx, C.byref(camera.desc)), "camera set")
         self.scene = scene
 
-    def render_tasks(self, tasks, max_paths=0):
-        """lumo_render_tiles over `tasks`; returns per-task (rgb_w array, result)."""
+    def render_tasks(self, tasks, max_paths=0, tone_map=None):
+        """lumo_render_tiles over `tasks`; returns per-task (rgb_w array, result).
+        tone_map: None, ToneMap.clamp(x) or ToneMap.REINHARD (tone_mapping.rs)."""
         L = lib()
         n = len(tasks)
         bufs, res = [], (_ffi.TileResult * n)()
@@ -464,7 +494,8 @@ class Device:
             bufs.append(b)
             res[i].rgb_w = b.ctypes.data_as(_ffi.c_double_p)
         arr = tasks if isinstance(tasks, C.Array) else (_ffi.TileTask * n)(*tasks)
-        cfg = _ffi.RenderCfg(0, 0, max_paths, 0)
+        tm = tone_map or ToneMap.NO_MAP
+        cfg = _ffi.RenderCfg(0, 0, max_paths, tm[0], tm[1])
         check(L.lumo_render_tiles(self.ctx, arr, n, C.byref(cfg), res), "render_tiles")
         return bufs, res
 
@@ -512,6 +543,7 @@ class Renderer:
         self._seed = None
         self._integrator = Integrator.PathTrace
         self._device = 0
+        self._tone_map = ToneMap.NO_MAP
 
     def samples(self, n):
         self._samples = int(n)
@@ -525,6 +557,11 @@ class Renderer:
         if i != Integrator.PathTrace:
             raise NotImplementedError("only Integrator.PathTrace is on the GPU path")
         self._integrator = i
+        return self
+
+    def tone_map(self, tm):
+        """Renderer::tone_map (renderer.rs:66-69)."""
+        self._tone_map = tm
         return self
 
     def device(self, d):
@@ -543,8 +580,8 @@ class Renderer:
         mine = shard_tasks(tasks, w, h, rank, world_size)
         dev = Device(self._device)
         dev.upload(self.scene, self.camera)
-        film = Film(w, h)
-        bufs, res = dev.render_tasks(mine)
+        film = Film(w, h, getattr(self.camera, "color_space", 1))
+        bufs, res = dev.render_tasks(mine, tone_map=self._tone_map)
         for t, b in zip(mine, bufs):
             film.add_tile(t, b)
         self.num_rays = sum(r.num_rays for r in res)

@@ -100,7 +100,7 @@ class TileResult(C.Structure):
 
 class RenderCfg(C.Structure):
     _fields_ = [("integrator", C.c_int32), ("rng_mode", C.c_int32), ("max_paths", C.c_int32),
-                ("pad0", C.c_int32)]
+                ("tone_map", C.c_int32), ("tone_arg", C.c_double)]
 
 
 class RaySoA(C.Structure):

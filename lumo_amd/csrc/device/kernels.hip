@@ -459,15 +459,27 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(DScene sc, Paths S, uint32_t 
 
 // ------------------------------------------------------------------ finish + film + ring
 __global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, int n, uint32_t pass, Dump dump,
-                                                   int dump_p) {
+                                                   int dump_p, int tone_map, double tone_arg) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n || !S.p_valid[s]) return;
     double L[NS];
     for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
     const DColor c = ldc(S.rad, s);
-    const V3 rgb = m3_mul_vec(cam.x2r, m3_mul_vec(cam.wb, color_xyz(sc, c, L)));
+    const double lum = luminance(sc, c, L);
+    DColor tc = c;  // ToneMap::map (tone_mapping.rs:38-63)
+    if (tone_map == LUMO_TONEMAP_CLAMP) {
+        for (int i = 0; i < NS; ++i) {
+            double v = tc.s[i];
+            if (v < 0.0) v = 0.0;
+            if (v > tone_arg) v = tone_arg;
+            tc.s[i] = v;
+        }
+    } else if (tone_map == LUMO_TONEMAP_REINHARD) {
+        tc = c / (1.0 + lum);
+    }
+    const V3 rgb = m3_mul_vec(cam.x2r, m3_mul_vec(cam.wb, color_xyz(sc, tc, L)));
     stv3(S.p_rgb, s, rgb);
-    S.p_lum[s] = luminance(sc, c, L);
+    S.p_lum[s] = lum;
     S.p_cost[s] = S.depth[s];
     if (dump.rad) {
         const size_t o = (size_t)pass * dump_p + S.pix[s];
@@ -650,6 +662,8 @@ struct Ctx {
     lumo_stats stats{};
     hipEvent_t ev[2 * ST_COUNT];
     int lds_grid_cap = 2048;
+    int tone_map = LUMO_TONEMAP_NONE;  // of the lumo_render_tiles call in progress
+    double tone_arg = 0.0;
 };
 
 lumo_status dev_alloc(DevBuf& b, size_t bytes) {
@@ -965,7 +979,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         }
         {
             StageTimer tm(c, g_timing, ST_FINISH);
-            k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, S, c.cam, N, (uint32_t)pass, D, dump_p);
+            k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, S, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg);
         }
         {
             StageTimer tm(c, g_timing, ST_FILM);
@@ -1289,7 +1303,14 @@ lumo_status lumo_render_tiles(void* ctx, const lumo_tile_task* tasks, size_t n, 
     if (!c || (!tasks && n) || (!out && n)) return LUMO_ERR_INVALID;
     if (cfg && cfg->rng_mode != LUMO_RNG_WAVEFRONT) return LUMO_ERR_UNSUPPORTED;
     if (cfg && cfg->integrator != LUMO_INTEGRATOR_PATH_TRACE) return LUMO_ERR_UNSUPPORTED;
+    if (cfg && (cfg->tone_map < LUMO_TONEMAP_NONE || cfg->tone_map > LUMO_TONEMAP_REINHARD)) return LUMO_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
+    struct ToneScope {  // the tone map applies to this call only
+        Ctx* c;
+        ~ToneScope() { c->tone_map = LUMO_TONEMAP_NONE; }
+    } scope{c};
+    c->tone_map = cfg ? cfg->tone_map : LUMO_TONEMAP_NONE;
+    c->tone_arg = cfg ? cfg->tone_arg : 0.0;
     const size_t max_paths = (cfg && cfg->max_paths > 0) ? (size_t)cfg->max_paths : (size_t)1 << 30;
     size_t i = 0;
     while (i < n) {  // chunk the task list so that at most max_paths slots are in flight

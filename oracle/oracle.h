@@ -47,6 +47,10 @@ int oracle_render_tiles(const lumo_scene_desc* scene, const lumo_camera_desc* ca
                         const lumo_tile_task* tasks, size_t n, int mode, int threads,
                         lumo_tile_result* out, oracle_counters* counters);
 
+/* Renderer::tone_map (tone_mapping.rs) for subsequent oracle_render_tiles calls:
+ * kind LUMO_TONEMAP_NONE / CLAMP (arg = upper bound) / REINHARD. */
+void oracle_set_tone_map(int kind, double arg);
+
 /* Per-path record of the wavefront order for one task (for per-path parity tests):
  * out arrays sized (pixels * samples), pixel-major within each pass (pass s, pixel j). */
 int oracle_trace_paths(const lumo_scene_desc* scene, const lumo_camera_desc* camera,

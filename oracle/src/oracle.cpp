@@ -1342,8 +1342,22 @@ struct Tile {
     uint64_t x0, y0, x1, y1;
     std::vector<double> px;  // 4 per pixel: w*r, w*g, w*b, w
 };
+struct ToneMap {  // tone_mapping.rs:38-63
+    int kind;
+    double arg;
+};
+Color tone_map_apply(const Scene& sc, const ToneMap& tm, const Color& c, const Lambda& L) {
+    if (tm.kind == LUMO_TONEMAP_CLAMP) {
+        Color o = c;
+        for (int i = 0; i < NS; ++i) o.s[i] = rclamp(o.s[i], 0.0, tm.arg);
+        return o;
+    }
+    if (tm.kind == LUMO_TONEMAP_REINHARD) return c / (1.0 + luminance(sc, c, L));
+    return c;
+}
+ToneMap g_tone{LUMO_TONEMAP_NONE, 0.0};  // set by oracle_set_tone_map before a render
 void tile_add_sample(const Scene& sc, const Cam& k, Tile& T, const Sample& s) {
-    const V3 xyz = color_xyz(sc, s.color, s.lambda);
+    const V3 xyz = color_xyz(sc, tone_map_apply(sc, g_tone, s.color, s.lambda), s.lambda);
     const V3 rgb = m3_mul_vec(k.x2r, m3_mul_vec(k.wb, xyz));
     auto to_u64 = [](double v) -> uint64_t { return v > 0.0 ? (uint64_t)v : 0; };
     const uint64_t pxx = to_u64(std::floor(s.raster.x)), pxy = to_u64(std::floor(s.raster.y));
@@ -1400,7 +1414,7 @@ void exec_lumo_order(const Scene& sc, const Cam& k, const lumo_tile_task& t, lum
                 ns[ptr] = s.cost;
                 fs[ptr] = luminance(sc, s.color, s.lambda);
                 ptr = (ptr + 1) % t.samples;
-                tile_add_sample(sc, k, T, s);  // ToneMap::NoMap
+                tile_add_sample(sc, k, T, s);
             }
         }
     }
@@ -1704,3 +1718,5 @@ extern "C" int oracle_light_pdf(const lumo_scene_desc* scene, int light, const d
     }
     return LUMO_OK;
 }
+
+extern "C" void oracle_set_tone_map(int kind, double arg) { g_tone = ToneMap{kind, arg}; }

@@ -37,6 +37,8 @@ def load(path=None):
         lib.oracle_trace.restype = C.c_int
         lib.oracle_trace.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(_ffi.RaySoA), C.c_size_t,
                                      C.POINTER(_ffi.HitSoA), C.c_int, C.POINTER(Counters)]
+        lib.oracle_set_tone_map.restype = None
+        lib.oracle_set_tone_map.argtypes = [C.c_int, C.c_double]
         dp = _ffi.c_double_p
         lib.oracle_bsdf_sample.restype = C.c_int
         lib.oracle_bsdf_sample.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, dp, C.c_size_t, C.c_uint64, dp,
@@ -53,9 +55,10 @@ def load(path=None):
     return _libs[path]
 
 
-def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path=None):
+def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path=None, tone_map=(0, 0.0)):
     """Returns (list of rgb_w arrays, results array, counters)."""
     lib = load(path)
+    lib.oracle_set_tone_map(*tone_map)
     n = len(tasks)
     arr = tasks if isinstance(tasks, C.Array) else (_ffi.TileTask * n)(*tasks)
     res = (_ffi.TileResult * n)()

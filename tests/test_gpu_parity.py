@@ -100,3 +100,16 @@ def test_renderer_api_matches_oracle(cornell):
 def test_errors_are_loud(dev):
     with pytest.raises(Exception):
         L.Device(1 << 20)
+
+
+@pytest.mark.parametrize("tm", [L.ToneMap.REINHARD, L.ToneMap.clamp(0.2)])
+def test_tone_mapped_tiles_match_oracle(dev, cornell, tm):
+    cam = L.Camera.cornell_box((32, 32))
+    dev.upload(cornell, cam)
+    tasks = L.make_tasks(32, 32, 8, SEED)
+    bufs, _ = dev.render_tasks(tasks, tone_map=tm)
+    obufs, _, _ = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, 8, tone_map=tm)
+    for b, ob in zip(bufs, obufs):
+        np.testing.assert_array_equal(b, ob)
+    plain, _ = dev.render_tasks(tasks)
+    assert not np.array_equal(np.concatenate(plain), np.concatenate(bufs))
