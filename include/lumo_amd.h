@@ -191,15 +191,28 @@ typedef struct {
 /* RenderTaskResult (renderer/task.rs:106-116) + its FilmTile pixels (film/tile.rs).
  * `rgb_w` is caller-allocated: 4 doubles (sum w*r, w*g, w*b, sum w) per pixel of the
  * tile, row-major over [px_min, px_max). */
+/* A light-tracing splat of BDPT (FilmSample with splat = true): filtered RGB added to the
+ * full-frame splat buffer at pixel (x, y) (film/tile.rs:96-101, film.rs:167-170). */
+typedef struct {
+    uint32_t x, y;
+    double rgb[3];
+} lumo_splat;
+
 typedef struct {
     double* rgb_w;
     uint64_t num_camera_rays;
     uint64_t num_rays;       /* sum of FilmSample.cost (path depth), task.rs:65 */
     uint64_t num_queries;    /* closest-hit + shadow visibility queries issued  */
+    /* BDPT splats of this task in lumo's order; caller-allocated `splat_cap` entries.  On
+     * return num_splats is the count produced; a count above splat_cap fails the call with
+     * LUMO_ERR_OOM (retry with a larger buffer). */
+    lumo_splat* splats;
+    uint64_t splat_cap;
+    uint64_t num_splats;
 } lumo_tile_result;
 
 enum { LUMO_RNG_WAVEFRONT = 0, LUMO_RNG_LUMO_ORDER = 1 };
-enum { LUMO_INTEGRATOR_PATH_TRACE = 0 };
+enum { LUMO_INTEGRATOR_PATH_TRACE = 0, LUMO_INTEGRATOR_BDPT = 1 };
 
 typedef struct {
     int32_t integrator; /* LUMO_INTEGRATOR_*                              */

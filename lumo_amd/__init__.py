@@ -435,21 +435,39 @@ def make_tasks(width, height, samples, seed):
 class Film:
     """Film pixels (film.rs:57-92): per pixel sum of w*rgb and sum of w (PIXEL_BUFFERS = 1)."""
 
-    def __init__(self, width, height, color_space=1):
+    def __init__(self, width, height, color_space=1, samples=1, filter_radius=1.5, filter_sigma=0.375):
         self.width, self.height = width, height
         self.color_space = color_space  # the camera's ColorSpace (default DCI-P3)
         self.pixels = np.zeros((height, width, 4), dtype=np.float64)
+        self.splats = np.zeros((height, width, 3), dtype=np.float64)  # BDPT light tracing (film.rs:136)
+        self.splat_scale = 1.0 / samples  # film.rs:137
+        self.filter_radius, self.filter_sigma = filter_radius, filter_sigma
 
-    def add_tile(self, task, rgb_w):
-        """Film::add_tile (film.rs:155-171)."""
+    def add_tile(self, task, rgb_w, splats=None):
+        """Film::add_tile (film.rs:155-171): tile pixels, then the tile's splats in order."""
         x0, y0 = task.px_min[0], task.px_min[1]
         x1, y1 = task.px_max[0], task.px_max[1]
         self.pixels[y0:y1, x0:x1, :] += rgb_w.reshape(y1 - y0, x1 - x0, 4)
+        if splats is not None:
+            for sp in splats:  # sequential, in lumo's order
+                self.splats[sp["y"], sp["x"]] += sp["rgb"]
+
+    def filter_integral(self):
+        """PixelFilter::integral for the Gaussian (filter.rs:103-114)."""
+        import math
+        r, s = self.filter_radius, self.filter_sigma
+        denom = s * math.sqrt(2.0)
+        ig = 0.5 * (math.erf(r / denom) - math.erf(-r / denom))
+        gr = math.exp(-(r * r) / (2.0 * s * s)) / math.sqrt(max(2.0 * math.pi * s * s, 0.0))
+        return (ig - 2.0 * r * gr) ** 2
 
     def rgb(self):
-        """Pixel::value (film.rs:82-91): sum(w*rgb) / sum(w), linear colour-space RGB."""
+        """Pixel::value (film.rs:82-91) + splat_scale * splat / filter integral (film.rs:173-182)."""
         with np.errstate(invalid="ignore", divide="ignore"):
-            return self.pixels[..., :3] / self.pixels[..., 3:4]
+            direct = self.pixels[..., :3] / self.pixels[..., 3:4]
+        if not self.splats.any():
+            return direct
+        return direct + self.splat_scale * self.splats / self.filter_integral()
 
     def rgb_image(self):
         """Film::rgb_image (film.rs:173-192): encoded 8-bit RGB, rows top to bottom."""

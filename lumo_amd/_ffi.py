@@ -93,9 +93,14 @@ class TileTask(C.Structure):
                 ("samples", C.c_uint64), ("total_samples", C.c_uint64), ("seed", C.c_uint64)]
 
 
+class Splat(C.Structure):
+    _fields_ = [("x", C.c_uint32), ("y", C.c_uint32), ("rgb", C.c_double * 3)]
+
+
 class TileResult(C.Structure):
     _fields_ = [("rgb_w", c_double_p), ("num_camera_rays", C.c_uint64), ("num_rays", C.c_uint64),
-                ("num_queries", C.c_uint64)]
+                ("num_queries", C.c_uint64), ("splats", C.POINTER(Splat)), ("splat_cap", C.c_uint64),
+                ("num_splats", C.c_uint64)]
 
 
 class RenderCfg(C.Structure):

@@ -50,6 +50,8 @@ int oracle_render_tiles(const lumo_scene_desc* scene, const lumo_camera_desc* ca
 /* Renderer::tone_map (tone_mapping.rs) for subsequent oracle_render_tiles calls:
  * kind LUMO_TONEMAP_NONE / CLAMP (arg = upper bound) / REINHARD. */
 void oracle_set_tone_map(int kind, double arg);
+/* Integrator for subsequent renders: LUMO_INTEGRATOR_PATH_TRACE or LUMO_INTEGRATOR_BDPT. */
+void oracle_set_integrator(int integrator);
 
 /* Per-path record of the wavefront order for one task (for per-path parity tests):
  * out arrays sized (pixels * samples), pixel-major within each pass (pass s, pixel j). */

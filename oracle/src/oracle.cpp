@@ -886,7 +886,7 @@ double diffuse_pdf(const Mfd& d, V3 wo, V3 wi) {
     return pr * p_ref + ps * p_sct;
 }
 // dielectric (:201-374)
-Color dielectric_f(const Mfd& d, V3 wo, V3 wi, const Lambda& L, bool reflection) {
+Color dielectric_f(const Mfd& d, V3 wo, V3 wi, const Lambda& L, bool reflection, bool importance) {
     const double cwo = wo.z, cwi = wi.z;
     const bool wo_inside = cwo < 0.0;
     const double eta = eta_at(d, L.l[0]);
@@ -900,7 +900,7 @@ Color dielectric_f(const Mfd& d, V3 wo, V3 wi, const Lambda& L, bool reflection)
     }
     const Color F = f_fresnel(d, wo, wh, L);
     if (wh.z < 0.0) wh = -wh;
-    const double scale = eta_ratio * eta_ratio;  // Transport::Radiance
+    const double scale = importance ? 1.0 : eta_ratio * eta_ratio;  // Transport::Importance / Radiance
     const Color tf = spec_c(d.tf, L);
     if (flat) return tf * (WHITE_C - F) / (scale * fabs(cwi));
     const double D = mf_d(d, wh);
@@ -988,7 +988,7 @@ double bsdf_pdf(const Scene& sc, const Hit& h, V3 wo, V3 wi, const Lambda& L) {
     }
 }
 // material.rs:254-270 -> bsdf.rs:28-48 -> bxdf.rs:71-100
-Color bsdf_f(const Scene& sc, const Hit& h, V3 wo, V3 wi, const Lambda& L) {
+Color bsdf_f(const Scene& sc, const Hit& h, V3 wo, V3 wi, const Lambda& L, bool importance = false) {
     const lumo_material& m = mat(sc, h.material);
     if (!is_standard(m.kind)) return cconst(0.0);
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
@@ -999,7 +999,7 @@ Color bsdf_f(const Scene& sc, const Hit& h, V3 wo, V3 wi, const Lambda& L) {
         case LUMO_MAT_LAMBERTIAN: return spec_sample(m.albedo, L) / PI;
         case LUMO_MAT_MF_DIFFUSE: return diffuse_f(mfd_of(sc, m), wol, wil, L);
         case LUMO_MAT_MF_CONDUCTOR: return conductor_f(mfd_of(sc, m), wol, wil, L);
-        default: return dielectric_f(mfd_of(sc, m), wol, wil, L, reflection);
+        default: return dielectric_f(mfd_of(sc, m), wol, wil, L, reflection, importance);
     }
 }
 double shading_cosine(const Scene& sc, int material, V3 wi, V3 ns) {  // material.rs:315-320
@@ -1242,6 +1242,7 @@ struct Cam {
     double lens_radius, focal_length;
     M3 wb, x2r;
     double fr, fsig;
+    double width, height, image_plane_area;
 };
 Cam cam_of(const lumo_camera_desc* c) {
     Cam k;
@@ -1264,6 +1265,17 @@ Cam cam_of(const lumo_camera_desc* c) {
     k.x2r = m3(c->xyz_to_rgb);
     k.fr = c->filter_radius;
     k.fsig = c->filter_sigma;
+    k.width = (double)c->width;
+    k.height = (double)c->height;
+    // CameraConfig::new (camera.rs:47-76): image plane area at z = 1
+    V3 p_min3 = xf_pt_inv(k.sctr, V3{0.0, 0.0, 0.0});
+    V3 p_max3 = xf_pt_inv(k.sctr, V3{k.width, k.height, 0.0});
+    p_min3 = xf_pt_inv(k.cts, p_min3);
+    p_max3 = xf_pt_inv(k.cts, p_max3);
+    const V2 p_min = V2{p_min3.x, p_min3.y} / (p_min3.z == 0.0 ? 1.0 : p_min3.z);
+    const V2 p_max = V2{p_max3.x, p_max3.y} / (p_max3.z == 0.0 ? 1.0 : p_max3.z);
+    const V2 pd = p_max - p_min;
+    k.image_plane_area = fabs(pd.x * pd.y);
     return k;
 }
 // camera.rs:257-268 (Perspective) + add_dof :221-243
@@ -1282,12 +1294,500 @@ Ray camera_ray(const Cam& k, V2 raster_xy, V2 rand_sq) {
     return ray_new(xf_pt_inv(k.wtc, xo_local), xf_dir_inv(k.wtc, wi_local));
 }
 
-// integrator.rs:45-70 (PathTrace)
-Sample integrate(const Scene& sc, const Cam& k, Xorshift& rng, double delta, V2 raster, Counters& C) {
+struct Splat;
+int g_integrator = LUMO_INTEGRATOR_PATH_TRACE;  // set by oracle_set_integrator before a render
+Sample bdpt_integrate(const Scene& sc, const Cam& cam, Ray r, Xorshift& rng, Lambda L, double delta, V2 raster,
+                      std::vector<Splat>& splats, Counters& C);
+// integrator.rs:45-70: lens, wavelengths, then the integrator; BDPT light-tracing splats are
+// appended to `splats` (they precede the main sample in lumo's Vec<FilmSample>)
+Sample integrate(const Scene& sc, const Cam& k, Xorshift& rng, double delta, V2 raster, Counters& C,
+                 std::vector<Splat>* splats) {
     const V2 lens = xs_vec2(rng);
     const Ray r = camera_ray(k, raster, lens);
     const Lambda L = wl_sample(xs_float(rng));
+    if (g_integrator == LUMO_INTEGRATOR_BDPT) return bdpt_integrate(sc, k, r, rng, L, delta, raster, *splats, C);
     return path_trace(sc, r, rng, L, delta, raster, C);
+}
+
+// ------------------------------------------------------------------ BDPT (integrator/bd_path_trace*.rs)
+// Camera importance functions (camera.rs:47-115, 157-388), Perspective only.
+double powi3(double x) { return x * (x * x); }
+double powi4(double x) {
+    const double x2 = x * x;
+    return x2 * x2;
+}
+double lens_area(const Cam& c) {  // camera.rs:233-240
+    return c.lens_radius == 0.0 ? 1.0 : PI * (c.lens_radius * c.lens_radius);
+}
+bool raster_xy(const Cam& c, const Ray& ri, V2* out) {  // camera.rs:170-214 (Perspective)
+    const V3 wl = xf_dir(c.wtc, ri.dir);
+    const double cos_theta = wl.z;
+    if (cos_theta <= 0.0) return false;
+    const double fl = c.lens_radius == 0.0 ? 1.0 / cos_theta : c.focal_length / cos_theta;
+    const V3 xo_local = xf_pt(c.wtc, ri.origin);
+    const V3 focus = xo_local + wl * fl;
+    const V3 rast = xf_pt(c.sctr, xf_pt(c.cts, focus));
+    const V2 r{rast.x, rast.y};
+    if (!(r.x >= 0.0 && r.x < c.width && r.y >= 0.0 && r.y < c.height)) return false;
+    *out = r;
+    return true;
+}
+double cam_pdf_wi(const Cam& c, const Ray& ri) {  // camera.rs:323-345
+    V2 r;
+    if (!raster_xy(c, ri, &r)) return 0.0;
+    const double cos_theta = xf_dir(c.wtc, ri.dir).z;
+    return 1.0 / (c.image_plane_area * powi3(cos_theta));
+}
+double cam_pdf_xo(const Cam& c, const Ray& ri) {  // camera.rs:297-320
+    const V3 xl = xf_pt(c.wtc, ri.origin);
+    const double r = c.lens_radius + EPSILON;
+    return length_squared(xl - V3{0.0, 0.0, 0.0}) < r * r ? 1.0 / lens_area(c) : 0.0;
+}
+bool cam_sample_towards(const Cam& c, V3 xi, V2 rs, Ray* out) {  // camera.rs:271-294
+    const V2 lens = c.lens_radius * square_to_disk(rs);
+    const V3 xo_local{lens.x, lens.y, 0.0};
+    const V3 xi_local = xf_pt(c.wtc, xi);
+    const V3 wi_local = normalize(xi_local - xo_local);
+    const Ray ri = ray_new(xf_pt_inv(c.wtc, xo_local), xf_dir_inv(c.wtc, wi_local));
+    V2 r;
+    if (!raster_xy(c, ri, &r)) return false;
+    *out = ri;
+    return true;
+}
+double cam_pdf_importance(const Cam& c, const Ray& ri, V3 xi) {  // camera.rs:348-365
+    V2 r;
+    if (!raster_xy(c, ri, &r)) return 0.0;
+    const V3 ng = m3_mul_vec(xf_normal_inv(c.wtc), V3{0.0, 0.0, 1.0});
+    const double pdf = distance_squared(xi, ri.origin) / (fabs(dot(ng, ri.dir)) * lens_area(c));
+    return rmax(pdf, 0.0);
+}
+bool cam_sample_importance(const Cam& c, const Ray& ri, Color* imp, V2* raster) {  // camera.rs:368-387
+    if (!raster_xy(c, ri, raster)) return false;
+    const double cos_theta = xf_dir(c.wtc, ri.dir).z;
+    const double denom = c.image_plane_area * powi4(cos_theta) * lens_area(c);
+    *imp = (1.0 / denom) * cconst(1.0);
+    return true;
+}
+
+// Sampleable::sample_on with the full hit (rectangle.rs:113-130, triangle.rs:214-240,
+// sphere.rs:108-129, instance.rs:146-159) and sample_leaving(_pdf) (object.rs:99-126)
+double light_area(const Scene& sc, const lumo_object& L) {  // Sampleable::area (instance: uniform scale)
+    if (L.xform < 0) return L.area;
+    const M3 mt = m3_transpose(m4_to_m3(xform_of(sc.d->transforms[L.xform]).m));
+    return length(mt.y0) * length(mt.y1) * L.area;
+}
+Hit light_sample_on_hit(const Scene& sc, const lumo_object& L, V2 rs) {
+    Hit h;
+    if (L.type == LUMO_OBJ_RECTANGLE) {
+        const V3 o{L.origin[0], L.origin[1], L.origin[2]}, b0{L.b0[0], L.b0[1], L.b0[2]}, b1{L.b1[0], L.b1[1], L.b1[2]};
+        const V3 xo = o + rs.x * b0 + rs.y * b1;
+        const V3 ng = normalize(cross(b0, b1));
+        const V3 err = gamma_n(4) * (vabs(o) + vabs(rs.x * b0) + vabs(rs.y * b1));
+        h = hit_new(0.0, L.material, -ng, xo, err, ng, ng, V2{0.0, 0.0});
+    } else if (L.type == LUMO_OBJ_TRIANGLE) {
+        const lumo_triangle& T = sc.d->triangles[L.tri_base];
+        const V3 A = sc.vert(T.v[0]), B = sc.vert(T.v[1]), Cv = sc.vert(T.v[2]);
+        const double gam = 1.0 - std::sqrt(1.0 - rs.x);
+        const double beta = rs.y * (1.0 - gam);
+        const double alpha = 1.0 - gam - beta;
+        const V3 bma = B - A, cma = Cv - A;
+        const V3 ng = normalize(cross(bma, cma));
+        V3 ns = ng;
+        if (T.n[0] >= 0) {
+            auto nv = [&](int i) { return V3{sc.d->normals[3 * i], sc.d->normals[3 * i + 1], sc.d->normals[3 * i + 2]}; };
+            ns = normalize(alpha * nv(T.n[0]) + beta * nv(T.n[1]) + gam * nv(T.n[2]));
+        }
+        const V3 xo = A + beta * bma + gam * cma;
+        const V3 err = gamma_n(6) * (vabs(A) + vabs(beta * bma) + vabs(gam * cma));
+        h = hit_new(0.0, T.material, -ng, xo, err, ns, ng, V2{0.0, 0.0});
+    } else {  // Sphere
+        V3 xo = L.radius * square_to_sphere(rs);
+        xo = xo * L.radius / length(xo);
+        const V3 err = vabs(xo) * gamma_n(5);
+        const V3 ng = xo / L.radius;
+        h = hit_new(0.0, L.material, -ng, xo, err, ng, ng, V2{0.0, 0.0});
+    }
+    if (L.xform >= 0) {
+        const lumo_transform& T = sc.d->transforms[L.xform];
+        const Xform X = xform_of(T);
+        const M3 N = nrm_of(T);
+        h.ng = normalize(m3_mul_vec(N, h.ng));
+        h.ns = normalize(m3_mul_vec(N, h.ns));
+        h.p = xf_pt(X, h.p);
+        h.fp_error = propagate_fp_err(X, h.p, h.fp_error);  // after moving p (instance.rs:151-152)
+        if (L.material_override >= 0) h.material = L.material_override;
+    }
+    return h;
+}
+
+enum { TR_RADIANCE = 0, TR_IMPORTANCE = 1 };
+// BVH::get_light_at (bvh.rs:97-102): the closest light (by hit_t) along -ng from just outside h
+int get_light_at(const Scene& sc, const Hit& h, Counters& C) {
+    const Ray ri = ray_new(ray_origin(h, true), -h.ng);
+    const BvhView b = lights_of(sc);
+    return bvh_hit_idx(sc, b.nodes, b.n, b.items, b.objs, ri, 0.0, INF, true, C);
+}
+struct Vtx {  // bd_path_trace/vertex.rs
+    Hit h;
+    bool blank;  // camera vertex: Material::Blank
+    Color gathered;
+    double pdf_fwd, pdf_bck;
+    V3 wo;
+    int light;
+};
+double sa_to_area(double pdf, V3 xo, V3 xi, V3 wi, V3 ngi) {  // measure.rs
+    return pdf * fabs(dot(wi, ngi)) / distance_squared(xo, xi);
+}
+bool v_is_delta(const Scene& sc, const Vtx& v, const Lambda& L) { return !v.blank && is_delta(sc, v.h.material, L); }
+bool v_is_surface(const Vtx& v) { return !v.blank; }
+double v_shading_cosine(const Scene& sc, const Vtx& v, V3 wi, V3 n) {
+    return v.blank ? 1.0 : shading_cosine(sc, v.h.material, wi, n);
+}
+double v_shading_correction(const Scene& sc, const Vtx& v, V3 wi) {  // vertex.rs:92-100
+    const V3 ng = v.h.ng, ns = v.h.ns;
+    return v_shading_cosine(sc, v, wi, ng) * v_shading_cosine(sc, v, v.wo, ns) /
+           (v_shading_cosine(sc, v, v.wo, ng) * v_shading_cosine(sc, v, wi, ns));
+}
+Color v_f(const Scene& sc, const Vtx& v, const Vtx& next, const Lambda& L, int mode) {
+    if (v.blank) return cconst(0.0);
+    const V3 wi = normalize(next.h.p - v.h.p);
+    return bsdf_f(sc, v.h, v.wo, wi, L, mode == TR_IMPORTANCE);
+}
+double v_bsdf_pdf(const Scene& sc, const Vtx& v, V3 wi, const Lambda& L, bool swap) {
+    if (v.blank) return 0.0;
+    return swap ? bsdf_pdf(sc, v.h, wi, v.wo, L) : bsdf_pdf(sc, v.h, v.wo, wi, L);
+}
+double v_pdf_prev(const Scene& sc, const Vtx& v, const Vtx& prev, V3 wi, const Lambda& L) {  // vertex.rs:119-134
+    if (v_is_delta(sc, v, L) || v_is_delta(sc, prev, L)) return 0.0;
+    const double pdf_sa = v_bsdf_pdf(sc, v, wi, L, true);
+    const V3 ngp = !v_is_surface(prev) ? -v.wo : prev.h.ng;
+    return sa_to_area(pdf_sa, v.h.p, prev.h.p, -v.wo, ngp);
+}
+Vtx vtx_camera(V3 xo, double pdf_fwd, Color gathered) {
+    Vtx v;
+    v.h = hit_new(0.0, -1, V3{-1.0, 0.0, 0.0}, xo, V3{0.0, 0.0, 0.0}, V3{1.0, 0.0, 0.0}, V3{1.0, 0.0, 0.0}, V2{1.0, 0.0});
+    v.blank = true;
+    v.gathered = gathered;
+    v.pdf_fwd = pdf_fwd;
+    v.pdf_bck = 0.0;
+    v.wo = V3{0.0, 0.0, 0.0};
+    v.light = -1;
+    return v;
+}
+Vtx vtx_light(const Hit& h, int light, Color gathered, double pdf_fwd) {
+    Vtx v;
+    v.h = h;
+    v.blank = false;
+    v.gathered = gathered;
+    v.light = light;
+    v.pdf_bck = 0.0;
+    v.pdf_fwd = pdf_fwd;
+    v.wo = V3{0.0, 0.0, 0.0};
+    return v;
+}
+Vtx vtx_surface(const Scene& sc, V3 wo, const Hit& h, Color gathered, double pdf_sa, const Lambda& L,
+                const Vtx& prev) {  // vertex.rs:50-76
+    Vtx v;
+    v.h = h;
+    v.blank = false;
+    v.gathered = gathered;
+    v.pdf_fwd = is_delta(sc, h.material, L) ? 0.0 : sa_to_area(pdf_sa, prev.h.p, h.p, -wo, h.ng);
+    v.light = -1;
+    v.pdf_bck = 0.0;
+    v.wo = wo;
+    return v;
+}
+
+const int BDPT_RR_DEPTH = 5, BDPT_MAX_DEPTH = 1024;
+// path_gen.rs:52-157
+void bdpt_walk(const Scene& sc, Ray ro, Xorshift& rng, Lambda& L, double delta, Vtx root, Color gathered,
+               double pdf_dir, int mode, std::vector<Vtx>& verts, Counters& C) {
+    int depth = 0;
+    verts.clear();
+    verts.push_back(root);
+    double pdf_fwd = pdf_dir;
+    for (;;) {
+        Hit ho;
+        int kind = 0, which = -1;
+        if (!scene_hit(sc, ro, &ho, &kind, &which, C)) break;
+        const int prev = depth;
+        const V3 wo = -ro.dir;
+        verts.push_back(vtx_surface(sc, wo, ho, gathered, pdf_fwd, L, verts[prev]));
+        depth += 1;
+        const int curr = depth;
+        const double u = xs_float(rng);
+        const V2 sq = xs_vec2(rng);
+        V3 wi;
+        if (!bsdf_sample(sc, verts[curr].h, wo, L, u, sq, &wi)) {
+            if (mode == TR_IMPORTANCE)
+                verts.pop_back();
+            else
+                verts[curr].light = get_light_at(sc, verts[curr].h, C);
+            break;
+        }
+        const Ray ri = generate_ray(verts[curr].h, wi);
+        const V3 wi2 = ri.dir;
+        pdf_fwd = bsdf_pdf(sc, verts[curr].h, wo, wi2, L);
+        if (pdf_fwd == 0.0) break;
+        const double corr = mode == TR_RADIANCE ? 1.0 : v_shading_correction(sc, verts[curr], wi2);
+        const Color bsdf = bsdf_f(sc, verts[curr].h, wo, wi2, L, mode == TR_IMPORTANCE);
+        gathered = gathered * (bsdf * v_shading_cosine(sc, verts[curr], wi2, verts[curr].h.ns) * corr / pdf_fwd);
+        verts[prev].pdf_bck = v_pdf_prev(sc, verts[curr], verts[prev], wi2, L);
+        if (depth >= BDPT_RR_DEPTH) {
+            const double lum = luminance(sc, gathered, L);
+            const double rr_prob = rmin(lum / delta, 1.0);
+            if (xs_float(rng) > rr_prob) break;
+            if (depth >= BDPT_MAX_DEPTH) break;
+            gathered = gathered / rr_prob;
+        }
+        if (is_delta(sc, verts[curr].h.material, L)) pdf_fwd = 0.0;
+        ro = ri;
+    }
+}
+void bdpt_camera_path(const Scene& sc, const Cam& cam, const Ray& r, Xorshift& rng, double delta, Lambda& L,
+                      std::vector<Vtx>& out, Counters& C) {
+    const double pdf_wi = cam_pdf_wi(cam, r);
+    const double pdf_xo = cam_pdf_xo(cam, r);
+    bdpt_walk(sc, r, rng, L, delta, vtx_camera(r.origin, pdf_xo, cconst(1.0)), cconst(1.0), pdf_wi, TR_RADIANCE, out,
+              C);
+}
+void bdpt_light_path(const Scene& sc, Xorshift& rng, double delta, Lambda& L, std::vector<Vtx>& out, Counters& C) {
+    const int li = sample_light(sc, xs_float(rng));
+    const lumo_object& light = sc.d->lights[li];
+    const double pdf_light = sc.d->alias_pdf[li];
+    const V2 rs0 = xs_vec2(rng);
+    const V2 rs1 = xs_vec2(rng);
+    const Hit ho = light_sample_on_hit(sc, light, rs0);  // Sampleable::sample_leaving
+    const V3 wi_l = square_to_cos_hemisphere(rs1);
+    const Ray ri = generate_ray(ho, onb_to_world(onb_new(ho.ns), wi_l));
+    const double pdf_origin = 1.0 / light_area(sc, light);
+    const double pdf_dir = dot(ho.ng, ri.dir) / PI;
+    const Color em = emit(sc, ho.material, L, ho);
+    const Vtx root = vtx_light(ho, li, em, pdf_origin * pdf_light);
+    const Color gathered = em * fabs(dot(ri.dir, ho.ns)) / (pdf_light * pdf_origin * pdf_dir);
+    bdpt_walk(sc, ri, rng, L, delta, root, gathered, pdf_dir, TR_IMPORTANCE, out, C);
+}
+
+// mis.rs
+double pdf_light_leaving(const Scene& sc, const Vtx& curr, const Vtx& next, const Lambda& L) {
+    if (v_is_delta(sc, next, L)) return 0.0;
+    if (curr.light < 0) return 0.0;
+    const V3 xo = curr.h.p, xi = next.h.p;
+    const Ray ri = ray_new(xo, xi - xo);
+    const V3 wi = ri.dir;
+    const double pdf_dir = dot(curr.h.ng, ri.dir) / PI;  // sample_leaving_pdf
+    const V3 ngi = !v_is_surface(next) ? wi : next.h.ng;
+    return sa_to_area(pdf_dir, xo, xi, wi, ngi);
+}
+double pdf_camera_leaving(const Cam& cam, const Scene& sc, const Vtx& curr, const Vtx& next, const Lambda& L) {
+    if (v_is_delta(sc, next, L)) return 0.0;
+    const V3 xo = curr.h.p, xi = next.h.p;
+    const V3 wi = normalize(xi - xo);
+    const double pdf_wi = cam_pdf_wi(cam, ray_new(xo, wi));
+    const V3 ngi = !v_is_surface(next) ? wi : next.h.ng;
+    return sa_to_area(pdf_wi, xo, xi, wi, ngi);
+}
+double pdf_light_origin(const Scene& sc, const Vtx& v) {
+    if (v.light < 0) return 0.0;
+    return sc.d->alias_pdf[v.light] / light_area(sc, sc.d->lights[v.light]);
+}
+double pdf_connection(const Scene& sc, const Vtx& curr, const Vtx& next, const Lambda& L, const Vtx* prev) {
+    if (v_is_delta(sc, next, L)) return 0.0;
+    const V3 xo = curr.h.p, xi = next.h.p;
+    double pdf_sa;
+    V3 wi;
+    if (prev) {
+        const V3 wo = normalize(prev->h.p - xo);
+        pdf_sa = v_bsdf_pdf(sc, curr, wo, L, true);
+        wi = curr.wo;
+    } else {
+        wi = normalize(xi - xo);
+        pdf_sa = v_bsdf_pdf(sc, curr, wi, L, false);
+    }
+    const V3 ngi = !v_is_surface(next) ? wi : next.h.ng;
+    return sa_to_area(pdf_sa, xo, xi, wi, ngi);
+}
+double mis_weight(const Scene& sc, const Cam& cam, const Lambda& L, const Vtx* lp, int s, const Vtx* cp, int t) {
+    if (s + t == 2) return 1.0;
+    auto map0 = [](double p) { return p == 0.0 ? 1.0 : p; };
+    const Vtx& ct1 = cp[t - 1];
+    const Vtx& ls1 = s == 0 ? cp[0] : lp[s - 1];
+    std::vector<double> rad, imp;
+    std::vector<char> del;
+    for (int i = 0; i < std::max(s, 2) - 2; ++i) {
+        rad.push_back(lp[i].pdf_bck);
+        imp.push_back(lp[i].pdf_fwd);
+        del.push_back(v_is_delta(sc, lp[i], L));
+    }
+    if (s > 1) {
+        const Vtx& ls2 = lp[s - 2];
+        rad.push_back(pdf_connection(sc, ls1, ls2, L, &ct1));
+        imp.push_back(ls2.pdf_fwd);
+        del.push_back(v_is_delta(sc, ls2, L));
+    }
+    if (s > 0) {
+        rad.push_back(t == 1 ? pdf_camera_leaving(cam, sc, ct1, ls1, L) : pdf_connection(sc, ct1, ls1, L, nullptr));
+        imp.push_back(ls1.pdf_fwd);
+        del.push_back(false);
+    }
+    if (t > 0) {
+        const double bck = s == 0 ? pdf_light_origin(sc, ct1)
+                                  : (s == 1 ? pdf_light_leaving(sc, ls1, ct1, L) : pdf_connection(sc, ls1, ct1, L, nullptr));
+        rad.push_back(ct1.pdf_fwd);
+        imp.push_back(bck);
+        del.push_back(false);
+    }
+    if (t > 1) {
+        const Vtx& ct2 = cp[t - 2];
+        const double bck = s == 0 ? pdf_light_leaving(sc, ct1, ct2, L) : pdf_connection(sc, ct1, ct2, L, &ls1);
+        rad.push_back(ct2.pdf_fwd);
+        imp.push_back(bck);
+        del.push_back(v_is_delta(sc, ct2, L));
+    }
+    for (int i = std::max(t, 2) - 2 - 1; i >= 0; --i) {
+        rad.push_back(cp[i].pdf_fwd);
+        imp.push_back(cp[i].pdf_bck);
+        del.push_back(v_is_delta(sc, cp[i], L));
+    }
+    double sum_ri = 0.0, ri = 1.0;
+    for (int i = s - 1; i >= 0; --i) {
+        ri *= map0(rad[i]) / map0(imp[i]);
+        if (!del[i] && !(i > 0 && del[i - 1])) sum_ri += ri * ri;
+    }
+    ri = 1.0;
+    sum_ri += ri;
+    for (int i = s; i < s + t - 1; ++i) {
+        ri *= map0(imp[i]) / map0(rad[i]);
+        if (!del[i] && !del[i + 1]) sum_ri += ri * ri;
+    }
+    return 1.0 / sum_ri;
+}
+
+struct Splat {
+    V2 raster;
+    Color color;
+    Lambda lambda;
+};
+// bd_path_trace.rs:77-145
+bool connect_light_path(const Scene& sc, const Cam& cam, Xorshift& rng, const Lambda& L, const Vtx* lp, int s,
+                        Splat* out, Counters& C) {
+    const Vtx& ll = lp[s - 1];
+    if (v_is_delta(sc, ll, L)) return false;
+    const V3 xi = ll.h.p;
+    Ray ri;
+    if (!cam_sample_towards(cam, xi, xs_vec2(rng), &ri)) return false;
+    const V3 xo = ri.origin, wi = ri.dir;
+    const double p_sct = v_bsdf_pdf(sc, ll, -wi, L, false);
+    const double p_imp = cam_pdf_importance(cam, ri, xi);
+    if (p_sct == 0.0 || p_imp == 0.0) return false;
+    Hit hc;
+    int kind = 0, which = -1;
+    // Option::is_none_or(test): no hit, or a hit farther than sqrt(EPSILON) from xi, fails
+    if (!scene_hit(sc, ri, &hc, &kind, &which, C)) return false;
+    const V3 dd = vabs(hc.p - xi);
+    if (rmax(rmax(dd.x, dd.y), dd.z) > std::sqrt(EPSILON)) return false;
+    Color color;
+    V2 raster;
+    if (!cam_sample_importance(cam, ri, &color, &raster)) return false;
+    if (color.s[0] == 0.0 && color.s[1] == 0.0 && color.s[2] == 0.0 && color.s[3] == 0.0) return false;
+    color = color / p_imp;
+    const double p_xo = cam_pdf_xo(cam, ri);
+    const Vtx cl = vtx_camera(xo, p_xo, color / p_imp);
+    const double t2 = distance_squared(xo, xi);
+    (void)t2;
+    color = color * (ll.gathered * cconst(1.0) * v_shading_cosine(sc, ll, -wi, ll.h.ns) *
+                     v_shading_correction(sc, ll, -wi) * v_f(sc, ll, cl, L, TR_IMPORTANCE) *
+                     mis_weight(sc, cam, L, lp, s, &cl, 1));
+    *out = Splat{raster, color, L};
+    return true;
+}
+Color add_camera_path(const Scene& sc, const Cam& cam, const Lambda& L, const Vtx* cp, int t) {
+    if (cp[t - 1].light < 0) return cconst(0.0);
+    const Vtx& ct = cp[t - 1];
+    const Color rad = ct.gathered * emit(sc, ct.h.material, L, ct.h);
+    if (rad.s[0] == 0.0 && rad.s[1] == 0.0 && rad.s[2] == 0.0 && rad.s[3] == 0.0) return cconst(0.0);
+    return rad * mis_weight(sc, cam, L, nullptr, 0, cp, t);
+}
+Color connect_camera_path(const Scene& sc, const Cam& cam, Xorshift& rng, const Lambda& L, const Vtx* cp, int t,
+                          Counters& C) {
+    const Vtx& cl = cp[t - 1];
+    if (v_is_delta(sc, cl, L) || cl.light >= 0) return cconst(0.0);
+    const int li = sample_light(sc, xs_float(rng));
+    const lumo_object& light = sc.d->lights[li];
+    const double pdf_light = sc.d->alias_pdf[li];
+    const V3 xo = cl.h.p;
+    V3 wi = light_sample_towards(sc, light, xo, xs_vec2(rng));
+    const double p_sct = v_bsdf_pdf(sc, cl, wi, L, false);
+    if (p_sct == 0.0) return cconst(0.0);
+    const Ray ri = generate_ray(cl.h, wi);
+    Hit hi;
+    if (!scene_hit_light(sc, ri, li, &hi, C)) return cconst(0.0);
+    const V3 xi = hi.p;
+    const V3 ngi = !v_is_surface(cl) ? wi : hi.ng;
+    const double p_lig = light_sample_towards_pdf(sc, light, ri, xi, ngi) * pdf_light;
+    if (p_lig == 0.0) return cconst(0.0);
+    wi = ri.dir;
+    const double pdf_origin = sa_to_area(p_lig, xo, xi, wi, ngi);
+    const Color em = emit(sc, hi.material, L, hi);
+    const Vtx ll = vtx_light(hi, li, em, pdf_origin);
+    const Color bsdf = v_f(sc, cl, ll, L, TR_RADIANCE);
+    const double cos_wi = v_shading_cosine(sc, cl, wi, cl.h.ns);
+    const Color radiance = cl.gathered * bsdf * em * cconst(1.0) * cos_wi / p_lig;
+    return radiance * mis_weight(sc, cam, L, &ll, 1, cp, t);
+}
+bool bdpt_visible(const Scene& sc, const Hit& h1, const Hit& h2, Counters& C) {  // bd_path_trace.rs:279-290
+    const V3 xo = h1.p, xi = h2.p;
+    const Ray ri = generate_ray(h1, xi - xo);
+    if (dot(ri.dir, h1.ng) < EPSILON) return false;
+    // Scene::hit_t (scene.rs:150-162): any-hit-first over objects, then lights
+    double t = INF;
+    t = rmin(t, bvh_hit_t(sc, objects_of(sc), ri, 0.0, t, C));
+    t = rmin(t, bvh_hit_t(sc, lights_of(sc), ri, 0.0, t, C));
+    return fabs(std::sqrt(rmax(distance_squared(xo, xi), 0.0)) - t) < EPSILON;
+}
+Color connect_paths(const Scene& sc, const Cam& cam, const Lambda& L, const Vtx* lp, int s, const Vtx* cp, int t,
+                    Counters& C) {
+    const Vtx& ll = lp[s - 1];
+    const Vtx& cl = cp[t - 1];
+    if (v_is_delta(sc, cl, L) || cl.light >= 0 || v_is_delta(sc, ll, L) || !bdpt_visible(sc, ll.h, cl.h, C))
+        return cconst(0.0);
+    const V3 xc = cl.h.p, xl = ll.h.p;
+    const V3 wi = normalize(xl - xc);
+    const double p_sct = v_bsdf_pdf(sc, cl, wi, L, false) * v_bsdf_pdf(sc, ll, -wi, L, false);
+    if (p_sct == 0.0) return cconst(0.0);
+    const Color lb = v_f(sc, ll, cl, L, TR_IMPORTANCE);
+    const Color cb = v_f(sc, cl, ll, L, TR_RADIANCE);
+    const Color radiance = ll.gathered * lb * v_shading_cosine(sc, ll, -wi, ll.h.ns) * cl.gathered * cb *
+                           v_shading_cosine(sc, cl, wi, cl.h.ns) * cconst(1.0) / distance_squared(xc, xl);
+    if (radiance.s[0] == 0.0 && radiance.s[1] == 0.0 && radiance.s[2] == 0.0 && radiance.s[3] == 0.0)
+        return cconst(0.0);
+    return radiance * mis_weight(sc, cam, L, lp, s, cp, t);
+}
+// bd_path_trace.rs:23-74
+Sample bdpt_integrate(const Scene& sc, const Cam& cam, Ray r, Xorshift& rng, Lambda L, double delta, V2 raster,
+                      std::vector<Splat>& splats, Counters& C) {
+    std::vector<Vtx> lp, cp;
+    bdpt_light_path(sc, rng, delta, L, lp, C);
+    bdpt_camera_path(sc, cam, r, rng, delta, L, cp, C);
+    Color radiance = cconst(0.0);
+    uint64_t cost = lp.size() + cp.size();
+    const int S = (int)lp.size(), T = (int)cp.size();
+    for (int s = 2; s <= S; ++s) {
+        if (!v_is_delta(sc, lp[s - 1], L)) cost += 1;
+        Splat sp;
+        if (connect_light_path(sc, cam, rng, L, lp.data(), s, &sp, C)) splats.push_back(sp);
+    }
+    radiance = radiance + add_camera_path(sc, cam, L, cp.data(), T);
+    for (int t = 2; t <= T; ++t) {
+        if (!v_is_delta(sc, cp[t - 1], L) && cp[t - 1].light >= 0) cost += 1;
+        radiance = radiance + connect_camera_path(sc, cam, rng, L, cp.data(), t, C);
+    }
+    for (int t = 2; t <= T; ++t)
+        for (int s = 2; s <= S; ++s) {
+            cost += 1;
+            radiance = radiance + connect_paths(sc, cam, L, lp.data(), s, cp.data(), t, C);
+        }
+    return Sample{radiance, L, raster, cost};
 }
 
 // ------------------------------------------------------------------ sampler (samplers.rs:136-193)
@@ -1341,6 +1841,7 @@ double gauss(double x, double sigma) {
 struct Tile {
     uint64_t x0, y0, x1, y1;
     std::vector<double> px;  // 4 per pixel: w*r, w*g, w*b, w
+    std::vector<lumo_splat> splats;
 };
 struct ToneMap {  // tone_mapping.rs:38-63
     int kind;
@@ -1382,6 +1883,40 @@ void tile_add_sample(const Scene& sc, const Cam& k, Tile& T, const Sample& s) {
     }
 }
 
+// FilmTile::add_sample with sample.splat = true (film/tile.rs:65-111): the footprint is clipped
+// to the image, not the tile, and each weighted tap is recorded as a TileSplat.
+void tile_add_splat(const Scene& sc, const Cam& k, Tile& T, const Splat& s) {
+    const V3 xyz = color_xyz(sc, tone_map_apply(sc, g_tone, s.color, s.lambda), s.lambda);
+    const V3 rgb = m3_mul_vec(k.x2r, m3_mul_vec(k.wb, xyz));
+    auto to_u64 = [](double v) -> uint64_t { return v > 0.0 ? (uint64_t)v : 0; };
+    const uint64_t pxx = to_u64(std::floor(s.raster.x)), pxy = to_u64(std::floor(s.raster.y));
+    const uint64_t r = (uint64_t)std::ceil(k.fr - 0.5);
+    const uint64_t rx = (uint64_t)k.width, ry = (uint64_t)k.height;
+    const uint64_t mix = pxx >= r ? pxx - r : 0, miy = pxy >= r ? pxy - r : 0;  // saturating_sub
+    const uint64_t mxx = std::min(pxx + r, rx - 1), mxy = std::min(pxy + r, ry - 1);
+    for (uint64_t fy = miy; fy <= mxy; ++fy) {
+        for (uint64_t fx = mix; fx <= mxx; ++fx) {
+            const V2 v = V2{s.raster.x - (0.5 + (double)fx), s.raster.y - (0.5 + (double)fy)};
+            const double gx = gauss(v.x, k.fsig), gy = gauss(v.y, k.fsig), gr = gauss(k.fr, k.fsig);
+            const double wt = rmax(gx - gr, 0.0) * rmax(gy - gr, 0.0);
+            if (wt != 0.0) {
+                const V3 c = rgb * wt;
+                T.splats.push_back(lumo_splat{(uint32_t)fx, (uint32_t)fy, {c.x, c.y, c.z}});
+            }
+        }
+    }
+}
+std::atomic<bool> g_splat_overflow{false};
+void copy_splats(const Tile& T, lumo_tile_result& res) {
+    res.num_splats = T.splats.size();
+    if (T.splats.empty()) return;
+    if (!res.splats || res.splat_cap < T.splats.size()) {
+        g_splat_overflow = true;
+        return;
+    }
+    std::memcpy(res.splats, T.splats.data(), T.splats.size() * sizeof(lumo_splat));
+}
+
 double ring_delta(const uint64_t* ns, const double* fs, uint64_t n) {  // task.rs:42-53
     double f = 0.0, f2 = 0.0;
     for (uint64_t i = 0; i < n; ++i) f = f + fs[i];
@@ -1409,7 +1944,9 @@ void exec_lumo_order(const Scene& sc, const Cam& k, const lumo_tile_task& t, lum
             while (mj_next(m, &rs)) {
                 const V2 raster = xy + rs;
                 const double delta = ring_delta(ns, fs, t.samples);
-                Sample s = integrate(sc, k, rng, delta, raster, C);
+                std::vector<Splat> sp;
+                Sample s = integrate(sc, k, rng, delta, raster, C, &sp);
+                for (const Splat& x : sp) tile_add_splat(sc, k, T, x);
                 num_rays += s.cost;
                 ns[ptr] = s.cost;
                 fs[ptr] = luminance(sc, s.color, s.lambda);
@@ -1421,6 +1958,7 @@ void exec_lumo_order(const Scene& sc, const Cam& k, const lumo_tile_task& t, lum
     std::memcpy(res.rgb_w, T.px.data(), T.px.size() * sizeof(double));
     res.num_camera_rays = (T.x1 - T.x0) * (T.y1 - T.y0) * t.samples;
     res.num_rays = num_rays;
+    copy_splats(T, res);
 }
 
 }  // namespace
@@ -1465,7 +2003,9 @@ void exec_wavefront(const Scene& sc, const Cam& k, const lumo_tile_task& t, lumo
             const V2 raster = V2{(double)(T.x0 + j % W), (double)(T.y0 + j / W)} + rs;
             Xorshift prng = xs_new(lumo_oracle_wavefront::path_seed(pseed[j], s));
             if (dbg && dbg->log && (int)s == dbg->dbg_pass && (int)j == dbg->dbg_pixel) g_dbg = dbg->log;
-            pass[j] = integrate(sc, k, prng, delta, raster, C);
+            std::vector<Splat> sp;
+            pass[j] = integrate(sc, k, prng, delta, raster, C, &sp);
+            for (const Splat& x : sp) tile_add_splat(sc, k, T, x);
             g_dbg = nullptr;
             tile_add_sample(sc, k, T, pass[j]);
             if (dbg) dbg->paths->push_back(pass[j]);
@@ -1481,6 +2021,7 @@ void exec_wavefront(const Scene& sc, const Cam& k, const lumo_tile_task& t, lumo
         std::memcpy(res->rgb_w, T.px.data(), T.px.size() * sizeof(double));
         res->num_camera_rays = P * t.samples;
         res->num_rays = num_rays;
+        copy_splats(T, *res);
     }
 }
 
@@ -1499,6 +2040,7 @@ extern "C" int oracle_render_tiles(const lumo_scene_desc* scene, const lumo_came
     const Scene sc{scene};
     const Cam k = cam_of(camera);
     if (threads < 1) threads = 1;
+    g_splat_overflow = false;
     std::atomic<size_t> next{0};
     std::vector<Counters> cs(threads);
     std::vector<std::thread> pool;
@@ -1528,7 +2070,7 @@ extern "C" int oracle_render_tiles(const lumo_scene_desc* scene, const lumo_came
             counters->shadow_queries += c.shadow;
         }
     }
-    return LUMO_OK;
+    return g_splat_overflow ? LUMO_ERR_OOM : LUMO_OK;
 }
 
 extern "C" int oracle_trace_paths(const lumo_scene_desc* scene, const lumo_camera_desc* camera,
@@ -1720,3 +2262,5 @@ extern "C" int oracle_light_pdf(const lumo_scene_desc* scene, int light, const d
 }
 
 extern "C" void oracle_set_tone_map(int kind, double arg) { g_tone = ToneMap{kind, arg}; }
+
+extern "C" void oracle_set_integrator(int integrator) { g_integrator = integrator; }

@@ -37,6 +37,8 @@ def load(path=None):
         lib.oracle_trace.restype = C.c_int
         lib.oracle_trace.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(_ffi.RaySoA), C.c_size_t,
                                      C.POINTER(_ffi.HitSoA), C.c_int, C.POINTER(Counters)]
+        lib.oracle_set_integrator.restype = None
+        lib.oracle_set_integrator.argtypes = [C.c_int]
         lib.oracle_set_tone_map.restype = None
         lib.oracle_set_tone_map.argtypes = [C.c_int, C.c_double]
         dp = _ffi.c_double_p
@@ -55,23 +57,44 @@ def load(path=None):
     return _libs[path]
 
 
-def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path=None, tone_map=(0, 0.0)):
-    """Returns (list of rgb_w arrays, results array, counters)."""
+def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path=None, tone_map=(0, 0.0),
+                 integrator=0, splats_out=None):
+    """Returns (list of rgb_w arrays, results array, counters).  With integrator = 1 (BDPT) the
+    per-task light-tracing splats are appended to `splats_out` (a list) as (x, y, rgb) arrays."""
     lib = load(path)
     lib.oracle_set_tone_map(*tone_map)
+    lib.oracle_set_integrator(integrator)
     n = len(tasks)
     arr = tasks if isinstance(tasks, C.Array) else (_ffi.TileTask * n)(*tasks)
-    res = (_ffi.TileResult * n)()
-    bufs = []
-    for i, t in enumerate(arr):
-        P = (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1])
-        b = np.zeros(4 * P)
-        bufs.append(b)
-        res[i].rgb_w = b.ctypes.data_as(_ffi.c_double_p)
-    cnt = Counters()
-    st = lib.oracle_render_tiles(C.byref(scene_desc), C.byref(camera_desc), arr, n, mode, threads, res,
-                                 C.byref(cnt))
-    assert st == 0, st
+    caps = [16 * (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1]) * t.samples if integrator else 0
+            for t in arr]
+    while True:
+        res = (_ffi.TileResult * n)()
+        bufs, sbufs = [], []
+        for i, t in enumerate(arr):
+            P = (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1])
+            b = np.zeros(4 * P)
+            bufs.append(b)
+            res[i].rgb_w = b.ctypes.data_as(_ffi.c_double_p)
+            sb = (_ffi.Splat * max(caps[i], 1))()
+            sbufs.append(sb)
+            res[i].splats = sb
+            res[i].splat_cap = caps[i]
+        cnt = Counters()
+        st = lib.oracle_render_tiles(C.byref(scene_desc), C.byref(camera_desc), arr, n, mode, threads, res,
+                                     C.byref(cnt))
+        if st == 7:  # LUMO_ERR_OOM: splat buffers too small, retry with the reported counts
+            caps = [max(c, r.num_splats) for c, r in zip(caps, res)]
+            continue
+        assert st == 0, st
+        break
+    lib.oracle_set_integrator(0)
+    if splats_out is not None:
+        for i in range(n):
+            m = res[i].num_splats
+            a = np.ctypeslib.as_array(sbufs[i])[:m] if m else np.zeros(0, dtype=[("x", "<u4"), ("y", "<u4"),
+                                                                               ("rgb", "<f8", (3,))])
+            splats_out.append(a.copy())
     return bufs, res, cnt
 
 
