@@ -27,7 +27,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 SEED = 0x5EED_1234
 # Algorithmic bytes per unit: f64 data touched by the algorithm.
 B_AABB, B_KD, B_TRI = 48, 16, 84           # slab test bounds; kd split node; 3 vertices + indices
-B_CLOSEST_IO, B_SHADOW_IO = 48 + 20, 104 + 32  # ray in + hit out; shadow record in + contribution out
+B_CLOSEST_IO = 48 + 20  # ray in + hit out
+B_RECORD, B_FOLD = 104, 104  # shadow record in; per path: gathered + pdf_light + radiance read/write
 STAGES = ["camera", "closest", "shade", "shadow", "resolve", "finish", "film", "ring"]
 
 
@@ -115,7 +116,7 @@ def main():
         q, cams, rays = (float(x) for x in s.tolist())
 
     if rank == 0:
-        roof = roofline(st)
+        roof = roofline(st, n_shadow_rays(scene))
         cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp) if (args.cpu_baseline and ws == 1) else None
         value = q / elapsed / 1e6
         out = {
@@ -186,7 +187,7 @@ def build_config(args):
     return scene, cam, (W, H), spp, wl
 
 
-def roofline(st):
+def roofline(st, n_shadow):
     """Dominant-kernel roofline from live per-launch HIP-event times and traversal counters."""
     ms = list(st.kernel_ms)
     launches = list(st.launches)
@@ -197,7 +198,9 @@ def roofline(st):
         nbytes = (st.closest_queries * B_CLOSEST_IO + st.aabb_tests[0] * B_AABB + st.kd_nodes[0] * B_KD +
                   st.tri_tests[0] * B_TRI)
     elif name == "shadow":
-        nbytes = (st.shadow_queries * B_SHADOW_IO + st.aabb_tests[1] * B_AABB + st.kd_nodes[1] * B_KD +
+        # k_shadow folds a path's 2 n_shadow records into its radiance: B_FOLD is amortised per query
+        b_io = B_RECORD + B_FOLD / (2 * n_shadow)
+        nbytes = (st.shadow_queries * b_io + st.aabb_tests[1] * B_AABB + st.kd_nodes[1] * B_KD +
                   st.tri_tests[1] * B_TRI)
     else:
         nbytes = None
@@ -220,6 +223,12 @@ def roofline(st):
     else:
         out.update({"achieved": None, "frac": None})
     return out
+
+
+def n_shadow_rays(scene):
+    """Scene::num_shadow_rays (scene.rs:90-92): max(ilog2(#lights), 1)."""
+    n = scene.desc().num_lights
+    return max(n.bit_length() - 1, 1)
 
 
 def pmc_traffic(kernel):

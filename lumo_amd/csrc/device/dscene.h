@@ -20,9 +20,13 @@ constexpr double DINF = __builtin_huge_val();
 constexpr int NS = 4;
 constexpr double Y_INTEGRAL = 106.856895;
 constexpr double SVI = 253.819;  // SAMPLE_VISIBLE_INTEGRAL
-// Traversal stacks are sized per scene: the kernels are instantiated for STK in {8,16,32,64}
-// and the host picks the smallest class >= the deepest kd / BVH path (lumo itself uses 64,
-// kdtree.rs:110, bvh.rs:324; a scene needing more than 64 would panic there too).
+// Traversal stacks are sized per scene.  A stack class STK encodes two capacities,
+// STK = 100 * (BVH stack) + (kd stack); the kernels are instantiated for a few classes and the
+// host picks the smallest one covering the deepest BVH and kd paths of the uploaded scene (lumo
+// itself uses 64 for both, kdtree.rs:110, bvh.rs:324; a scene needing more would panic there
+// too).  Small stacks stay in VGPRs; every spare slot costs registers in each nested traversal.
+constexpr int stk_bvh(int stk) { return stk / 100; }
+constexpr int stk_kd(int stk) { return stk % 100; }
 
 // kd node packed to 16 B for the device (lumo_kd_node is 32 B): interior nodes hold the split
 // point, leaves {first, count}; meta = right << 2 | axis, axis == 3 marks a leaf.
@@ -367,8 +371,8 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
                               int* idx_out, Counters& C) {
     const double origin[3] = {r.o.x, r.o.y, r.o.z};
     const double inv_dir[3] = {r.inv.x, r.inv.y, r.inv.z};
-    int st_node[STK];
-    double st_ts[STK], st_te[STK];
+    int st_node[stk_kd(STK)];
+    double st_ts[stk_kd(STK)], st_te[stk_kd(STK)];
     int sp = 0;
     double t_hit = DINF;
     int curr = ob.kd_root;
@@ -614,7 +618,7 @@ __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_
                             double* t_found = nullptr) {
     if (n_nodes == 0) return -1;
     const V3 inv_dir = r.inv;
-    int stack[STK];
+    int stack[stk_bvh(STK)];
     int sp = 0, curr = 0, idx = -1;
     double tt = t_max;
     for (;;) {

@@ -6,8 +6,8 @@
 //     k_closest  Scene::hit for the active queue                     (scene.rs:119-147)
 //     k_shade    BSDF sample, NEE shadow-ray records, spawn, RR       (path_trace.rs:18-77,
 //                                                                      integrator.rs:87-137)
-//     k_shadow   Scene::hit_light + MIS for every shadow record        (integrator.rs:139-184)
-//     k_resolve  radiance += sum(gathered * single) / n_shadow         (integrator.rs:74-85)
+//     k_shadow   Scene::hit_light + MIS for the shadow records of each  (integrator.rs:74-184)
+//                path, folded into its radiance in lumo's order
 //   k_finish   per-sample XYZ -> white balance -> RGB, luminance, cost (film/tile.rs:65-66, task.rs:64-69)
 //   k_film     tile-clipped Gaussian splat as a deterministic gather   (film/tile.rs:65-111)
 //   k_ring     adaptive-RR ring buffer + delta of the next pass        (task.rs:28-69)
@@ -46,8 +46,11 @@ constexpr int BLOCK = 256;
 constexpr uint64_t SAMPLES_INCREMENT = 256;
 constexpr int RR_DEPTH = 5;
 
+// ST_RESOLVE is kept for the stats layout; the fold now runs inside k_shadow.
 enum Stage { ST_CAMERA = 0, ST_CLOSEST, ST_SHADE, ST_SHADOW, ST_RESOLVE, ST_FINISH, ST_FILM, ST_RING, ST_COUNT };
-enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_N };
+// Device-side queue counters: the bounce kernels read their counts from here, so the host never
+// waits for a count before launching the next stage.
+enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_N };
 enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
 
 struct DCam {
@@ -68,14 +71,14 @@ struct Paths {
     double* hit_t;
     int32_t *hit_kind, *hit_obj, *hit_tri;
     // shadow records, R = N * 2 * n_shadow (fixed slot-major layout)
-    double *sh_o, *sh_d, *sh_f, *sh_psct, *sh_cos, *sh_out;
+    double *sh_o, *sh_d, *sh_f, *sh_psct, *sh_cos;
     int32_t *sh_light, *sh_flags;
     double *g_sh, *pdf_l;
     // per-pass outputs
     double *p_rgb, *p_lum;
     uint32_t *p_cost, *p_valid;
     double* film;
-    int32_t *q0, *q1, *sq, *rq;
+    int32_t *q0, *q1, *rq;
     uint32_t* counts;
     unsigned long long* tcount;  // [2][TC_N]
 };
@@ -263,8 +266,10 @@ __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, in
 
 // ------------------------------------------------------------------ closest hit
 template <int STK, bool LDS, bool FX>
-__global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc0, Paths S, const int32_t* queue, uint32_t count) {
+__global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc0, Paths S, const int32_t* queue) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+    const uint32_t count = S.counts[CNT_CUR];
+    if (count <= blockIdx.x * blockDim.x) return;  // before staging: whole block idle
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     Counters C{0, 0, 0};
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
@@ -281,16 +286,13 @@ __global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc
 }
 
 // ------------------------------------------------------------------ shade
+// One path's bounce: hit record, emission, BSDF sample, NEE records, RR, spawn.
 template <bool FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue, uint32_t count,
-                                                  int32_t* next_queue) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    bool alive = false, resolve = false;
-    int s = -1;
+__device__ __forceinline__ void shade_one(const DScene& sc, const Paths& S, const Tasks& T, int s, bool& alive,
+                                          bool& resolve) {
     const int ns = sc.n_shadow;
     int n_sh = 0;
-    if (q < count) {
-        s = queue[q];
+    {
         const int kind = S.hit_kind[s];
         if (kind != 0) {
             const Ray ro{ldv3(S.ro, s), ldv3(S.rd, s)};
@@ -398,63 +400,88 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
             S.queries[s] += (uint32_t)n_sh;
         }
     }
-    block_append(alive, s, next_queue, S.counts + CNT_NEXT);
-    block_append(resolve, s, S.rq, S.counts + CNT_RESOLVE);
 }
 
-// ------------------------------------------------------------------ shadow (hit_light + MIS)
-// One thread per (resolve-queue slot, shadow record); `count` = resolve count x 2 n_shadow.
-// Records whose BSDF sample failed are skipped (k_resolve reads them as black).
+template <bool FX>
+__global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue,
+                                                                    int32_t* next_queue) {
+    const uint32_t count = S.counts[CNT_CUR];
+    // grid-stride over whole blocks: block_append needs every thread of the block each round
+    for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
+        const uint32_t q = base + threadIdx.x;
+        bool alive = false, resolve = false;
+        int s = -1;
+        if (q < count) {
+            s = queue[q];
+            shade_one<FX>(sc, S, T, s, alive, resolve);
+        }
+        block_append(alive, s, next_queue, S.counts + CNT_NEXT);
+        block_append(resolve, s, S.rq, S.counts + CNT_RESOLVE);
+    }
+}
+
+// ------------------------------------------------------------------ shadow rays (hit_light + MIS + fold)
+// One thread per path of the resolve queue: its 2 n_shadow records in lumo's order
+// (integrator.rs:74-184): per light sample i, single = (light-sampled + BSDF-sampled MIS
+// contributions) / pdf_light, radiance += gathered * sum(single) / n_shadow.  Records whose
+// BSDF sample failed contribute black without a query.
 template <int STK, bool LDS, bool FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0, Paths S, uint32_t count) {
+__device__ __forceinline__ DColor shadow_record(const DScene& sc, const Paths& S, int s, int rec, Counters& C) {
+    const RayX ri = rayx(Ray{ldv3(S.sh_o, rec), ldv3(S.sh_d, rec)});
+    const int li = S.sh_light[rec];
+    DHit hi;
+    DColor out = cfill(0.0);
+    if (scene_hit_light<STK, FX>(sc, ri, li, hi, C)) {
+        const lumo_object& Lo = sc.lights[li];
+        const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
+        const double p_sct = S.sh_psct[rec];
+        if (!(p_lig == 0.0 || p_sct == 0.0)) {  // mis_sample (integrator.rs:139-184)
+            double L[NS];
+            for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
+            const bool li_mode = (S.sh_flags[rec] & 2) != 0;
+            const double denom = p_lig * p_lig + p_sct * p_sct;
+            const double weight = li_mode ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
+            const double p_denom = li_mode ? p_lig : p_sct;
+            const lumo_material hm = sc.mats[hi.material];
+            out = ldc(S.sh_f, rec) * cfill(1.0) * emit(sc, hm, L, hi.backface) * S.sh_cos[rec] * weight / p_denom;
+        }
+    }
+    return out;
+}
+template <int STK, bool LDS, bool FX>
+__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0, Paths S) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+    const uint32_t count = S.counts[CNT_RESOLVE];
+    if (count <= blockIdx.x * blockDim.x) return;
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     Counters C{0, 0, 0};
-    const uint32_t per = 2u * (uint32_t)sc.n_shadow;
+    const int ns = sc.n_shadow;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
-        const int s = S.rq[q / per];
-        const int rec = s * (int)per + (int)(q % per);
-        if ((S.sh_flags[rec] & 1) == 0) continue;
-        const RayX ri = rayx(Ray{ldv3(S.sh_o, rec), ldv3(S.sh_d, rec)});
-        const int li = S.sh_light[rec];
-        DHit hi;
-        DColor out = cfill(0.0);
-        if (scene_hit_light<STK, FX>(sc, ri, li, hi, C)) {
-            const lumo_object& Lo = sc.lights[li];
-            const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
-            const double p_sct = S.sh_psct[rec];
-            if (!(p_lig == 0.0 || p_sct == 0.0)) {  // mis_sample (integrator.rs:139-184)
-                double L[NS];
-                for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
-                const bool li_mode = (S.sh_flags[rec] & 2) != 0;
-                const double denom = p_lig * p_lig + p_sct * p_sct;
-                const double weight = li_mode ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
-                const double p_denom = li_mode ? p_lig : p_sct;
-                const lumo_material hm = sc.mats[hi.material];
-                out = ldc(S.sh_f, rec) * cfill(1.0) * emit(sc, hm, L, hi.backface) * S.sh_cos[rec] * weight / p_denom;
+        const int s = S.rq[q];
+        DColor acc = cfill(0.0), a = cfill(0.0);
+        for (int r = 0; r < 2 * ns; ++r) {  // one call site keeps the traversal inlined once
+            const int rec = s * 2 * ns + r;
+            DColor o = cfill(0.0);
+            if ((r & 1) == 0 || (S.sh_flags[rec] & 1)) o = shadow_record<STK, LDS, FX>(sc, S, s, rec, C);
+            if ((r & 1) == 0) {
+                a = o;
+            } else {
+                const DColor single = (cfill(0.0) + a + o) / S.pdf_l[s * ns + (r >> 1)];
+                acc = acc + ldc(S.g_sh, s) * single;
             }
         }
-        stc(S.sh_out, rec, out);
+        stc(S.rad, s, ldc(S.rad, s) + acc / (double)ns);
     }
     flush_counters(C, S.tcount + TC_N);
 }
 
-// ------------------------------------------------------------------ resolve (shadow_rays fold)
-__global__ __launch_bounds__(BLOCK) void k_resolve(DScene sc, Paths S, uint32_t count) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= count) return;
-    const int s = S.rq[q];
-    const int ns = sc.n_shadow;
-    const DColor g = ldc(S.g_sh, s);
-    DColor acc = cfill(0.0);
-    for (int i = 0; i < ns; ++i) {
-        const int rec = s * 2 * ns + 2 * i;
-        const DColor a = ldc(S.sh_out, rec);
-        const DColor b = (S.sh_flags[rec + 1] & 1) ? ldc(S.sh_out, rec + 1) : cfill(0.0);
-        const DColor single = (cfill(0.0) + a + b) / S.pdf_l[s * ns + i];
-        acc = acc + g * single;
+// Start of a bounce: the alive queue just built becomes the current one.
+__global__ void k_bounce_begin(uint32_t* counts) {
+    if (threadIdx.x == 0) {
+        counts[CNT_CUR] = counts[CNT_NEXT];
+        counts[CNT_NEXT] = 0;
+        counts[CNT_RESOLVE] = 0;
     }
-    stc(S.rad, s, ldc(S.rad, s) + acc / (double)ns);
 }
 
 // ------------------------------------------------------------------ finish + film + ring
@@ -664,6 +691,11 @@ struct Ctx {
     int lds_grid_cap = 2048;
     int tone_map = LUMO_TONEMAP_NONE;  // of the lumo_render_tiles call in progress
     double tone_arg = 0.0;
+    // per-bounce queue-count snapshots (pinned) and their completion events
+    static constexpr int SNAP_RING = 64;
+    uint32_t* snap = nullptr;
+    hipEvent_t snap_ev[SNAP_RING];
+    int bounce_ahead = 3;
 };
 
 lumo_status dev_alloc(DevBuf& b, size_t bytes) {
@@ -770,14 +802,17 @@ void resolve_timers(Ctx& c) {
 
 bool g_timing = false;
 
+// Stack classes STK = 100 * bvh + kd (dscene.h); the list the kernels are instantiated for.
+constexpr int STACK_CLASSES[] = {404, 408, 1616, 1632, 1648, 6464};
 template <typename F>
 void by_stack_class(int cls, F&& f) {
     switch (cls) {
-        case 8: f(std::integral_constant<int, 8>{}); break;
-        case 16: f(std::integral_constant<int, 16>{}); break;
-        case 32: f(std::integral_constant<int, 32>{}); break;
-        case 48: f(std::integral_constant<int, 48>{}); break;
-        default: f(std::integral_constant<int, 64>{}); break;
+        case 404: f(std::integral_constant<int, 404>{}); break;
+        case 408: f(std::integral_constant<int, 408>{}); break;
+        case 1616: f(std::integral_constant<int, 1616>{}); break;
+        case 1632: f(std::integral_constant<int, 1632>{}); break;
+        case 1648: f(std::integral_constant<int, 1648>{}); break;
+        default: f(std::integral_constant<int, 6464>{}); break;
     }
 }
 
@@ -785,7 +820,7 @@ void by_stack_class(int cls, F&& f) {
 // grid-stride loop) so each workgroup copies the packed scene once per launch.
 bool g_lds = true;
 template <typename F>
-void launch_trav(Ctx& c, uint32_t count, F&& f) {
+void launch_trav(Ctx& c, uint64_t count, F&& f) {
     const bool lds = g_lds && c.sc.hot_bytes > 0;
     const int grid_full = ceil_div(count, BLOCK);
     by_stack_class(c.sc.stack_class, [&](auto K) {
@@ -860,7 +895,6 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     S.sh_f = wbuf<double>(c, W_SH_F, 4 * R, st);
     S.sh_psct = wbuf<double>(c, W_SH_PSCT, R, st);
     S.sh_cos = wbuf<double>(c, W_SH_COS, R, st);
-    S.sh_out = wbuf<double>(c, W_SH_OUT, 4 * R, st);
     S.sh_light = wbuf<int32_t>(c, W_SH_LIGHT, R, st);
     S.sh_flags = wbuf<int32_t>(c, W_SH_FLAGS, R, st);
     S.g_sh = wbuf<double>(c, W_G_SH, 4 * (size_t)N, st);
@@ -872,9 +906,8 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     S.film = wbuf<double>(c, W_FILM, 4 * (size_t)N, st);
     S.q0 = wbuf<int32_t>(c, W_Q0, N, st);
     S.q1 = wbuf<int32_t>(c, W_Q1, N, st);
-    S.sq = wbuf<int32_t>(c, W_SQ, R, st);
     S.rq = wbuf<int32_t>(c, W_RQ, N, st);
-    S.counts = wbuf<uint32_t>(c, W_COUNTS, 4, st);
+    S.counts = wbuf<uint32_t>(c, W_COUNTS, CNT_N, st);
     S.tcount = wbuf<unsigned long long>(c, W_TCOUNT, 2 * TC_N, st);
     Tasks T{};
     T.t = wbuf<lumo_tile_task>(c, W_TASKS, n_tasks, st);
@@ -918,7 +951,13 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     HIPCHK(hipGetLastError());
 
     uint64_t bounces = 0, closest_q = 0, shadow_q = 0;
-    uint32_t counts[4];
+    // Bounces are enqueued ahead of the host's knowledge of the queue counts: each bounce ends
+    // with an async copy of its counters into a pinned ring, and the host only blocks on the
+    // snapshot of the bounce `ahead` launches back.  Launch grids use the last known alive count
+    // as an upper bound (counts never grow within a pass); the kernels read the exact counts from
+    // device memory.  A pass ends once a snapshot shows no path alive; the bounces enqueued past
+    // that point see empty queues and exit at once.
+    const int ahead = c.bounce_ahead;
     for (uint64_t pass = 0; pass < max_samples; ++pass) {
         {
             const int cp = (int)pass;
@@ -926,57 +965,67 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                                           hipMemcpyHostToDevice, sm));
         }
         if (dump_host) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, sm));
-        HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * 4, sm));
+        HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));
         {
             StageTimer tm(c, g_timing, ST_CAMERA);
             k_camera<<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass);
         }
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(counts, S.counts, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, sm));
-        HIPCHK(hipStreamSynchronize(sm));
-        if (g_timing) resolve_timers(c);
-        uint32_t qn = counts[CNT_NEXT];
         int32_t* qa = S.q0;
         int32_t* qb = S.q1;
-        while (qn > 0) {
-            bounces++;
-            closest_q += qn;
-            HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * 4, sm));
+        uint32_t ub = (uint32_t)N;  // upper bound on the alive count of the next bounce
+        int issued = 0, consumed = 0;
+        bool done = false;
+        for (;;) {
+            while (consumed < issued) {
+                hipEvent_t e = c.snap_ev[consumed % Ctx::SNAP_RING];
+                if (issued - consumed >= ahead) {
+                    HIPCHK(hipEventSynchronize(e));
+                } else if (hipEventQuery(e) != hipSuccess) {
+                    break;
+                }
+                const uint32_t* k = c.snap + CNT_N * (consumed % Ctx::SNAP_RING);
+                closest_q += k[CNT_CUR];
+                bounces += k[CNT_CUR] > 0 ? 1 : 0;
+                ub = k[CNT_NEXT];
+                done = done || ub == 0;
+                consumed++;
+            }
+            if (done) break;
+            k_bounce_begin<<<1, 64, 0, sm>>>(S.counts);
             {
                 StageTimer tm(c, g_timing, ST_CLOSEST);
-                launch_trav(c, qn, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                launch_trav(c, ub, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
                     k_closest<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                        <<<grid, BLOCK, shm, sm>>>(c.sc, S, qa, qn);
+                        <<<grid, BLOCK, shm, sm>>>(c.sc, S, qa);
                 });
             }
             {
                 StageTimer tm(c, g_timing, ST_SHADE);
                 if (c.sc.full)
-                    k_shade<true><<<ceil_div(qn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qn, qb);
+                    k_shade<true><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb);
                 else
-                    k_shade<false><<<ceil_div(qn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qn, qb);
+                    k_shade<false><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb);
             }
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(counts, S.counts, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, sm));
-            HIPCHK(hipStreamSynchronize(sm));
-            if (g_timing) resolve_timers(c);
-            const uint32_t rn = counts[CNT_RESOLVE];
-            const uint32_t sn = rn * 2u * (uint32_t)ns;
-            if (sn > 0) {
+            {
                 StageTimer tm(c, g_timing, ST_SHADOW);
-                launch_trav(c, sn, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                launch_trav(c, ub, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
                     k_shadow<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                        <<<grid, BLOCK, shm, sm>>>(c.sc, S, sn);
+                        <<<grid, BLOCK, shm, sm>>>(c.sc, S);
                 });
             }
-            if (rn > 0) {
-                StageTimer tm(c, g_timing, ST_RESOLVE);
-                k_resolve<<<ceil_div(rn, BLOCK), BLOCK, 0, sm>>>(c.sc, S, rn);
-            }
             HIPCHK(hipGetLastError());
-            qn = counts[CNT_NEXT];
+            HIPCHK(hipMemcpyAsync(c.snap + CNT_N * (issued % Ctx::SNAP_RING), S.counts, sizeof(uint32_t) * CNT_N,
+                                  hipMemcpyDeviceToHost, sm));
+            HIPCHK(hipEventRecord(c.snap_ev[issued % Ctx::SNAP_RING], sm));
+            issued++;
             std::swap(qa, qb);
         }
+        while (consumed < issued) {  // trailing empty bounces
+            HIPCHK(hipEventSynchronize(c.snap_ev[consumed % Ctx::SNAP_RING]));
+            consumed++;
+        }
+        if (g_timing) resolve_timers(c);
         {
             StageTimer tm(c, g_timing, ST_FINISH);
             k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, S, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg);
@@ -1079,6 +1128,14 @@ lumo_status lumo_create(int device, void** ctx_out) {
         return LUMO_ERR_HIP;
     }
     for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventCreate(&c->ev[i]);
+    for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventCreateWithFlags(&c->snap_ev[i], hipEventDisableTiming);
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->snap), sizeof(uint32_t) * CNT_N * Ctx::SNAP_RING) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return LUMO_ERR_OOM;
+    }
+    if (const char* e = std::getenv("LUMO_BOUNCE_AHEAD"))
+        c->bounce_ahead = std::min(Ctx::SNAP_RING - 1, std::max(1, std::atoi(e)));
     {
         DebugLog h{};
         h.slot = -1;
@@ -1101,6 +1158,8 @@ void lumo_destroy(void* ctx) {
     for (DevBuf& b : c->work)
         if (b.p) (void)hipFree(b.p);
     for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventDestroy(c->ev[i]);
+    for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventDestroy(c->snap_ev[i]);
+    if (c->snap) (void)hipHostFree(c->snap);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1218,7 +1277,6 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     }
     s.n_shadow = lg > 1 ? lg : 1;  // scene.rs:90-92
     // deepest pending-stack use: BVH (right children pending on a root-leaf path) and kd trees
-    int need = 1;
     auto bvh_need = [&](const lumo_bvh_node* nodes, int n) {
         std::vector<int> pend(n > 0 ? n : 1, 0);
         int mx = 0;
@@ -1232,8 +1290,9 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         }
         return mx;
     };
-    need = std::max(need, bvh_need(d->object_nodes, d->num_object_nodes));
-    need = std::max(need, bvh_need(d->light_nodes, d->num_light_nodes));
+    const int need_b = std::max({1, bvh_need(d->object_nodes, d->num_object_nodes),
+                                 bvh_need(d->light_nodes, d->num_light_nodes)});
+    int need_k = 1;
     {
         std::vector<int> depth(d->num_kd_nodes > 0 ? d->num_kd_nodes : 1, 0);
         for (int i = 0; i < d->num_kd_nodes; ++i) {
@@ -1241,18 +1300,25 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
                 if (i + 1 < d->num_kd_nodes) depth[i + 1] = std::max(depth[i + 1], depth[i] + 1);
                 const int r = d->kd_nodes[i].right;
                 if (r >= 0 && r < d->num_kd_nodes) depth[r] = std::max(depth[r], depth[i] + 1);
-                need = std::max(need, depth[i] + 1);
+                need_k = std::max(need_k, depth[i] + 1);
             }
         }
     }
-    if (need > 64) {
+    if (need_b > 64 || need_k > 64) {
         free_scene(*c);
         return LUMO_ERR_UNSUPPORTED;  // lumo's fixed [_; 64] stacks would overflow too
     }
-    s.stack_class = need <= 8 ? 8 : need <= 16 ? 16 : need <= 32 ? 32 : need <= 48 ? 48 : 64;
-    if (const char* e = std::getenv("LUMO_STACK_CLASS")) {  // A/B override (never below `need`)
+    auto fits = [&](int cls) { return stk_bvh(cls) >= need_b && stk_kd(cls) >= need_k; };
+    s.stack_class = 6464;
+    for (int cls : STACK_CLASSES)
+        if (fits(cls)) {
+            s.stack_class = cls;
+            break;
+        }
+    if (const char* e = std::getenv("LUMO_STACK_CLASS")) {  // A/B override (never below the needs)
         const int f = std::atoi(e);
-        if (f >= need && (f == 8 || f == 16 || f == 32 || f == 48 || f == 64)) s.stack_class = f;
+        for (int cls : STACK_CLASSES)
+            if (cls == f && fits(cls)) s.stack_class = f;
     }
     // feature class: the lean kernels cover kd meshes / rectangles with Lambertian + Light only
     bool full = d->num_transforms > 0;

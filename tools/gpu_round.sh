@@ -5,7 +5,7 @@
 set -eo pipefail
 TAG=${1:-r01}
 mkdir -p gpurun_out
-timeout -k 10 900 python3 -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1
 timeout -k 10 600 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 if [ "${PROFILE:-1}" = "1" ]; then
