@@ -448,29 +448,46 @@ __device__ __forceinline__ DColor shadow_record(const DScene& sc, const Paths& S
     }
     return out;
 }
+// Thread (path, light sample i): single_i = (light-sampled + BSDF-sampled) / pdf_light, staged
+// in LDS; the path's i == 0 thread then folds acc += gathered * single_i in i order and adds
+// acc / n_shadow to the radiance.  A block round covers BLOCK / n_shadow whole paths.
 template <int STK, bool LDS, bool FX>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0, Paths S) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+    __shared__ DColor singles[BLOCK];
     const uint32_t count = S.counts[CNT_RESOLVE];
-    if (count <= blockIdx.x * blockDim.x) return;
+    const int ns = sc0.n_shadow;
+    const uint32_t per_block = (uint32_t)(BLOCK / ns);  // paths per block round
+    if (count <= blockIdx.x * per_block) return;
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     Counters C{0, 0, 0};
-    const int ns = sc.n_shadow;
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
-        const int s = S.rq[q];
-        DColor acc = cfill(0.0), a = cfill(0.0);
-        for (int r = 0; r < 2 * ns; ++r) {  // one call site keeps the traversal inlined once
-            const int rec = s * 2 * ns + r;
-            DColor o = cfill(0.0);
-            if ((r & 1) == 0 || (S.sh_flags[rec] & 1)) o = shadow_record<STK, LDS, FX>(sc, S, s, rec, C);
-            if ((r & 1) == 0) {
-                a = o;
+    const int i = (int)threadIdx.x % ns;
+    for (uint32_t base = blockIdx.x * per_block; base < count; base += gridDim.x * per_block) {
+        const uint32_t q = base + threadIdx.x / ns;
+        const bool mine = threadIdx.x < per_block * ns && q < count;
+        int s = -1;
+        if (mine) {
+            s = S.rq[q];
+            const int rec = s * 2 * ns + 2 * i;
+            const DColor a = shadow_record<STK, LDS, FX>(sc, S, s, rec, C);
+            const DColor b = (S.sh_flags[rec + 1] & 1) ? shadow_record<STK, LDS, FX>(sc, S, s, rec + 1, C) : cfill(0.0);
+            const DColor single = (cfill(0.0) + a + b) / S.pdf_l[s * ns + i];
+            if (ns == 1) {
+                stc(S.rad, s, ldc(S.rad, s) + (cfill(0.0) + ldc(S.g_sh, s) * single) / 1.0);
             } else {
-                const DColor single = (cfill(0.0) + a + o) / S.pdf_l[s * ns + (r >> 1)];
-                acc = acc + ldc(S.g_sh, s) * single;
+                singles[threadIdx.x] = single;
             }
         }
-        stc(S.rad, s, ldc(S.rad, s) + acc / (double)ns);
+        if (ns > 1) {  // uniform over the block
+            __syncthreads();
+            if (mine && i == 0) {
+                const DColor g = ldc(S.g_sh, s);
+                DColor acc = cfill(0.0);
+                for (int k = 0; k < ns; ++k) acc = acc + g * singles[threadIdx.x + k];
+                stc(S.rad, s, ldc(S.rad, s) + acc / (double)ns);
+            }
+            __syncthreads();
+        }
     }
     flush_counters(C, S.tcount + TC_N);
 }
@@ -803,13 +820,15 @@ void resolve_timers(Ctx& c) {
 bool g_timing = false;
 
 // Stack classes STK = 100 * bvh + kd (dscene.h); the list the kernels are instantiated for.
-constexpr int STACK_CLASSES[] = {404, 408, 1616, 1632, 1648, 6464};
+constexpr int STACK_CLASSES[] = {404, 408, 448, 1616, 1624, 1632, 1648, 6464};
 template <typename F>
 void by_stack_class(int cls, F&& f) {
     switch (cls) {
         case 404: f(std::integral_constant<int, 404>{}); break;
         case 408: f(std::integral_constant<int, 408>{}); break;
+        case 448: f(std::integral_constant<int, 448>{}); break;
         case 1616: f(std::integral_constant<int, 1616>{}); break;
+        case 1624: f(std::integral_constant<int, 1624>{}); break;
         case 1632: f(std::integral_constant<int, 1632>{}); break;
         case 1648: f(std::integral_constant<int, 1648>{}); break;
         default: f(std::integral_constant<int, 6464>{}); break;
@@ -1009,7 +1028,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             }
             {
                 StageTimer tm(c, g_timing, ST_SHADOW);
-                launch_trav(c, ub, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                launch_trav(c, (uint64_t)ub * (uint32_t)ns, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
                     k_shadow<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
                         <<<grid, BLOCK, shm, sm>>>(c.sc, S);
                 });
