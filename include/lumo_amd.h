@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define LUMO_ABI_VERSION 1
+#define LUMO_ABI_VERSION 2
 
 typedef int32_t lumo_status;
 enum {
@@ -220,6 +220,13 @@ typedef struct {
     int32_t max_paths;  /* cap on paths in flight (0 = all pixels of the call) */
     int32_t tone_map;   /* LUMO_TONEMAP_* applied per sample before the film (task.rs:73-76)  */
     double tone_arg;    /* ToneMap::Clamp upper bound                                          */
+    /* BDPT only.  max_vertices: storage per subpath (0 = 64); a longer subpath fails the call
+     * with LUMO_ERR_UNSUPPORTED instead of truncating it.  splat_film: optional row-major
+     * width x height x 3 array; when a task's result has no `splats` list, its light-tracing
+     * taps are summed into it (film.rs:167-170; summation order unspecified, as lumo's tile
+     * completion order). */
+    int32_t max_vertices, pad0;
+    double* splat_film;
 } lumo_render_cfg;
 enum { LUMO_TONEMAP_NONE = 0, LUMO_TONEMAP_CLAMP = 1, LUMO_TONEMAP_REINHARD = 2 }; /* tone_mapping.rs */
 
@@ -291,6 +298,8 @@ void lumo_set_timing(int on);
 
 /* Test hook: render one task in the wavefront order and dump every path. */
 lumo_status lumo_debug_paths(void* ctx, const lumo_tile_task* task, lumo_path_dump* dump);
+/* Integrator of lumo_debug_paths (LUMO_INTEGRATOR_*; BDPT splats are not collected there). */
+lumo_status lumo_debug_set_integrator(void* ctx, int integrator);
 /* Diagnostics: per-bounce record (20 doubles per bounce, at most 64 bounces) of the path of
  * `pixel` in sample pass `pass` of `task`; *n_out = number of bounces recorded. */
 lumo_status lumo_debug_trace(void* ctx, const lumo_tile_task* task, int pass, int pixel, double* out,

@@ -410,7 +410,9 @@ class Camera:
 
 
 class Integrator:
+    """integrator.rs:14-28: PathTrace (NEE + MIS) or BDPathTrace (bidirectional, MIS)."""
     PathTrace = 0
+    BDPathTrace = 1
 
 
 class ToneMap:
@@ -500,21 +502,50 @@ class Device:
             check(L.lumo_camera_set(self.ctx, C.byref(camera.desc)), "camera set")
         self.scene = scene
 
-    def render_tasks(self, tasks, max_paths=0, tone_map=None):
+    def render_tasks(self, tasks, max_paths=0, tone_map=None, integrator=0, splats_out=None, splat_film=None,
+                     max_vertices=0):
         """lumo_render_tiles over `tasks`; returns per-task (rgb_w array, result).
-        tone_map: None, ToneMap.clamp(x) or ToneMap.REINHARD (tone_mapping.rs)."""
+        tone_map: None, ToneMap.clamp(x) or ToneMap.REINHARD (tone_mapping.rs).
+        integrator = Integrator.BDPathTrace: the light-tracing splats of each task are appended
+        to `splats_out` (a list of (x, y, rgb) record arrays, lumo's order), or, when
+        `splats_out` is None, summed into `splat_film` (an H x W x 3 float64 array)."""
         L = lib()
         n = len(tasks)
-        bufs, res = [], (_ffi.TileResult * n)()
-        for i, t in enumerate(tasks):
-            P = (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1])
-            b = np.zeros(4 * P, dtype=np.float64)
-            bufs.append(b)
-            res[i].rgb_w = b.ctypes.data_as(_ffi.c_double_p)
         arr = tasks if isinstance(tasks, C.Array) else (_ffi.TileTask * n)(*tasks)
         tm = tone_map or ToneMap.NO_MAP
-        cfg = _ffi.RenderCfg(0, 0, max_paths, tm[0], tm[1])
-        check(L.lumo_render_tiles(self.ctx, arr, n, C.byref(cfg), res), "render_tiles")
+        lists = integrator == Integrator.BDPathTrace and splats_out is not None
+        if integrator == Integrator.BDPathTrace and not lists:
+            if splat_film is None or splat_film.dtype != np.float64 or not splat_film.flags.c_contiguous:
+                raise ValueError("BDPT needs splats_out or a C-contiguous float64 splat_film")
+        caps = [16 * (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1]) * t.samples if lists else 0
+                for t in arr]
+        while True:
+            bufs, sbufs, res = [], [], (_ffi.TileResult * n)()
+            for i, t in enumerate(arr):
+                P = (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1])
+                b = np.zeros(4 * P, dtype=np.float64)
+                bufs.append(b)
+                res[i].rgb_w = b.ctypes.data_as(_ffi.c_double_p)
+                if lists:
+                    sb = (_ffi.Splat * max(caps[i], 1))()
+                    sbufs.append(sb)
+                    res[i].splats = sb
+                    res[i].splat_cap = caps[i]
+            cfg = _ffi.RenderCfg(integrator, 0, max_paths, tm[0], tm[1], max_vertices, 0,
+                                 splat_film.ctypes.data_as(_ffi.c_double_p) if (splat_film is not None and not lists)
+                                 else None)
+            st = L.lumo_render_tiles(self.ctx, arr, n, C.byref(cfg), res)
+            if st == _ffi.LUMO_ERR_OOM and lists and any(r.num_splats > c for r, c in zip(res, caps)):
+                caps = [max(c, r.num_splats) for c, r in zip(caps, res)]  # splat lists too small: retry
+                continue
+            check(st, "render_tiles")
+            break
+        if lists:
+            for i in range(n):
+                m = res[i].num_splats
+                a = (np.ctypeslib.as_array(sbufs[i])[:m] if m else
+                     np.zeros(0, dtype=[("x", "<u4"), ("y", "<u4"), ("rgb", "<f8", (3,))]))
+                splats_out.append(a.copy())
         return bufs, res
 
     def trace(self, origins, dirs, lights=None):
@@ -572,8 +603,9 @@ class Renderer:
         return self
 
     def integrator(self, i):
-        if i != Integrator.PathTrace:
-            raise NotImplementedError("only Integrator.PathTrace is on the GPU path")
+        """Renderer::integrator (renderer.rs:72-75): PathTrace or BDPathTrace."""
+        if i not in (Integrator.PathTrace, Integrator.BDPathTrace):
+            raise ValueError(f"unknown integrator {i}")
         self._integrator = i
         return self
 
@@ -598,8 +630,13 @@ class Renderer:
         mine = shard_tasks(tasks, w, h, rank, world_size)
         dev = Device(self._device)
         dev.upload(self.scene, self.camera)
-        film = Film(w, h, getattr(self.camera, "color_space", 1))
-        bufs, res = dev.render_tasks(mine, tone_map=self._tone_map)
+        film = Film(w, h, getattr(self.camera, "color_space", 1), samples=self._samples)
+        if self._integrator == Integrator.BDPathTrace:
+            # light-tracing splats are summed on the device straight into the film's splat buffer
+            bufs, res = dev.render_tasks(mine, tone_map=self._tone_map, integrator=self._integrator,
+                                         splat_film=film.splats)
+        else:
+            bufs, res = dev.render_tasks(mine, tone_map=self._tone_map)
         for t, b in zip(mine, bufs):
             film.add_tile(t, b)
         self.num_rays = sum(r.num_rays for r in res)

@@ -16,6 +16,7 @@ c_int64_p = C.POINTER(C.c_int64)
 c_uint64_p = C.POINTER(C.c_uint64)
 
 LUMO_OK = 0
+LUMO_ERR_OOM = 7
 STATUS = {0: "OK", 1: "INVALID", 2: "NO_DEVICE", 3: "HIP", 4: "NO_SCENE", 5: "NO_CAMERA",
           6: "UNSUPPORTED", 7: "OOM"}
 
@@ -105,7 +106,8 @@ class TileResult(C.Structure):
 
 class RenderCfg(C.Structure):
     _fields_ = [("integrator", C.c_int32), ("rng_mode", C.c_int32), ("max_paths", C.c_int32),
-                ("tone_map", C.c_int32), ("tone_arg", C.c_double)]
+                ("tone_map", C.c_int32), ("tone_arg", C.c_double), ("max_vertices", C.c_int32),
+                ("pad0", C.c_int32), ("splat_film", c_double_p)]
 
 
 class RaySoA(C.Structure):
@@ -151,6 +153,7 @@ DEVICE_API = [
     ("lumo_stats_reset", C.c_int32, [C.c_void_p]),
     ("lumo_set_timing", None, [C.c_int]),
     ("lumo_set_lds_staging", None, [C.c_int]),
+    ("lumo_debug_set_integrator", C.c_int32, [C.c_void_p, C.c_int]),
     ("lumo_debug_trace", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.c_int, C.c_int, c_double_p, C.POINTER(C.c_int)]),
     ("lumo_debug_paths", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.POINTER(PathDump)]),
 ]

@@ -983,9 +983,11 @@ __device__ double bsdf_pdf(const DScene& sc, const lumo_material& m, const DHit&
     if (flat) return 1.0 - wh.z < EPSILON ? pt / (pr + pt) : 0.0;
     return mf_normal_pdf(d, wh, o) * fabs(hwi) / sq(hwi + hwo / er) * pt / (pr + pt);
 }
-// Material::bsdf_f, Transport::Radiance (material.rs:254-270 -> bsdf.rs:28-48 -> bxdf.rs:71-100)
+// Material::bsdf_f (material.rs:254-270 -> bsdf.rs:28-48 -> bxdf.rs:71-100); `importance` selects
+// Transport::Importance (BDPT light subpaths), which only changes dielectric transmission.
 template <bool FX>
-__device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, V3 wi, const double* L) {
+__device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, V3 wi, const double* L,
+                         bool importance = false) {
     if constexpr (!FX) {
         if (m.kind != LUMO_MAT_LAMBERTIAN) return cfill(0.0);
         if (!(dot(h.ng, wi) * dot(h.ng, wo) >= 0.0) || h.backface) return cfill(0.0);
@@ -1024,7 +1026,7 @@ __device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h
     }
     const DColor F = fresnel(d, o, wh, L);
     if (wh.z < 0.0) wh = -wh;
-    const double scale = er * er;
+    const double scale = importance ? 1.0 : er * er;
     const DColor tf = spec_sample(m.tf, L);
     if (flat) return tf * (cfill(1.0) - F) / (scale * fabs(i.z));
     const double hwo = dot(wh, o), hwi = dot(wh, i);

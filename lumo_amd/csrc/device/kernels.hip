@@ -25,6 +25,8 @@
 #include <vector>
 
 #include "../../../include/lumo_amd.h"
+#include <hipcub/hipcub.hpp>
+
 #include "dscene.h"
 
 using namespace lumo;
@@ -58,6 +60,7 @@ struct DCam {
     double lens_radius, focal_length;
     M3 wb, x2r;
     double fr, fsig;
+    double width, height, image_plane_area;  // CameraConfig (camera.rs:47-76), for BDPT importance
 };
 
 // Path state (SoA)
@@ -502,15 +505,11 @@ __global__ void k_bounce_begin(uint32_t* counts) {
 }
 
 // ------------------------------------------------------------------ finish + film + ring
-__global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, int n, uint32_t pass, Dump dump,
-                                                   int dump_p, int tone_map, double tone_arg) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n || !S.p_valid[s]) return;
-    double L[NS];
-    for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
-    const DColor c = ldc(S.rad, s);
-    const double lum = luminance(sc, c, L);
-    DColor tc = c;  // ToneMap::map (tone_mapping.rs:38-63)
+// ToneMap::map (tone_mapping.rs:38-63), then XYZ -> white balance -> colour space
+// (film/tile.rs:65-66, space.rs:125-151)
+__device__ __forceinline__ V3 sample_rgb(const DScene& sc, const DCam& cam, const DColor& c, const double* L,
+                                         int tone_map, double tone_arg) {
+    DColor tc = c;
     if (tone_map == LUMO_TONEMAP_CLAMP) {
         for (int i = 0; i < NS; ++i) {
             double v = tc.s[i];
@@ -519,9 +518,20 @@ __global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, 
             tc.s[i] = v;
         }
     } else if (tone_map == LUMO_TONEMAP_REINHARD) {
-        tc = c / (1.0 + lum);
+        tc = c / (1.0 + luminance(sc, c, L));
     }
-    const V3 rgb = m3_mul_vec(cam.x2r, m3_mul_vec(cam.wb, color_xyz(sc, tc, L)));
+    return m3_mul_vec(cam.x2r, m3_mul_vec(cam.wb, color_xyz(sc, tc, L)));
+}
+
+__global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, int n, uint32_t pass, Dump dump,
+                                                   int dump_p, int tone_map, double tone_arg) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n || !S.p_valid[s]) return;
+    double L[NS];
+    for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
+    const DColor c = ldc(S.rad, s);
+    const double lum = luminance(sc, c, L);
+    const V3 rgb = sample_rgb(sc, cam, c, L, tone_map, tone_arg);
     stv3(S.p_rgb, s, rgb);
     S.p_lum[s] = lum;
     S.p_cost[s] = S.depth[s];
@@ -647,6 +657,82 @@ __global__ __launch_bounds__(64) void k_ring(Paths S, Tasks T, int n_tasks, int 
     }
 }
 
+#include "bdpt.h"
+
+// ------------------------------------------------------------------ BDPT splats -> film taps
+// FilmTile::add_sample with splat = true (film/tile.rs:65-111): tone map, XYZ, white balance,
+// RGB, then the Gaussian taps over the whole image (not the tile).  MODE 0 counts the taps of
+// each slot, 1 writes them from the slot's offset (lumo's order: slot = pixel order within the
+// task, tasks in order), 2 adds them into a full-frame film.
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void k_bdpt_taps(DScene sc, Paths S, Bdpt B, Bdpt R, DCam cam, int n, int tone_map,
+                                                      double tone_arg, uint32_t* cnt, const uint32_t* off,
+                                                      lumo_splat* out, double* film) {
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= n) return;
+    if (!S.p_valid[slot]) {
+        if (MODE == 0) cnt[slot] = 0;
+        return;
+    }
+    const int ri = B.redo_index[slot];  // re-run samples keep their splats in the redo store
+    const SplatStore& sp = ri >= 0 ? R.sp : B.sp;
+    const int si = ri >= 0 ? ri : slot;
+    const int nsp = sp.n[si];
+    const uint64_t r = (uint64_t)ceil(cam.fr - 0.5);
+    const uint64_t rx = (uint64_t)cam.width, ry = (uint64_t)cam.height;
+    const double gr = gauss(cam.fr, cam.fsig);
+    uint32_t k = MODE == 1 ? off[slot] : 0u;
+    for (int j = 0; j < nsp; ++j) {
+        const V2 raster{sp.D(0, j, si), sp.D(1, j, si)};
+        V3 rgb{0.0, 0.0, 0.0};
+        if (MODE != 0) {
+            DColor c;
+            double L[NS];
+            for (int i = 0; i < NS; ++i) {
+                c.s[i] = sp.D(2 + i, j, si);
+                L[i] = sp.D(6 + i, j, si);
+            }
+            rgb = sample_rgb(sc, cam, c, L, tone_map, tone_arg);
+        }
+        const uint64_t pxx = raster.x > 0.0 ? (uint64_t)floor(raster.x) : 0, pxy = raster.y > 0.0 ? (uint64_t)floor(raster.y) : 0;
+        const uint64_t mix = pxx >= r ? pxx - r : 0, miy = pxy >= r ? pxy - r : 0;
+        const uint64_t mxx = std::min(pxx + r, rx - 1), mxy = std::min(pxy + r, ry - 1);
+        for (uint64_t fy = miy; fy <= mxy; ++fy) {
+            for (uint64_t fx = mix; fx <= mxx; ++fx) {
+                const double vx = raster.x - (0.5 + (double)fx), vy = raster.y - (0.5 + (double)fy);
+                const double wt = rmax(gauss(vx, cam.fsig) - gr, 0.0) * rmax(gauss(vy, cam.fsig) - gr, 0.0);
+                if (wt == 0.0) continue;
+                if (MODE == 0) {
+                    k++;
+                } else {
+                    const V3 c = rgb * wt;
+                    if (MODE == 1) {
+                        lumo_splat& o = out[k++];
+                        o.x = (uint32_t)fx;
+                        o.y = (uint32_t)fy;
+                        o.rgb[0] = c.x;
+                        o.rgb[1] = c.y;
+                        o.rgb[2] = c.z;
+                    } else {
+                        double* f = film + 3 * (fy * rx + fx);
+                        atomicAdd(f, c.x);
+                        atomicAdd(f + 1, c.y);
+                        atomicAdd(f + 2, c.z);
+                    }
+                }
+            }
+        }
+    }
+    if (MODE == 0) cnt[slot] = k;
+}
+// first tap of each task in this pass (exclusive scan gathered at the tasks' first slots)
+__global__ void k_task_tap_ranges(Tasks T, const uint32_t* cnt, const uint32_t* off, int n_tasks, int n,
+                                  uint64_t* ranges) {
+    const int ti = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ti > n_tasks) return;
+    ranges[ti] = ti < n_tasks ? (uint64_t)off[T.first[ti]] : (uint64_t)off[n - 1] + cnt[n - 1];
+}
+
 // ------------------------------------------------------------------ traversal-only entry (lumo_trace)
 template <int STK>
 __global__ void k_trace(DScene sc, const double* o, const double* d, const int32_t* light, int n, int any_hit,
@@ -713,6 +799,11 @@ struct Ctx {
     uint32_t* snap = nullptr;
     hipEvent_t snap_ev[SNAP_RING];
     int bounce_ahead = 3;
+    // integrator of the call in progress (BDPT: vertex storage per subpath, optional splat film)
+    int integrator = LUMO_INTEGRATOR_PATH_TRACE;
+    int max_vertices = 64;
+    double* splat_film = nullptr;
+    int debug_integrator = LUMO_INTEGRATOR_PATH_TRACE;  // lumo_debug_paths
 };
 
 lumo_status dev_alloc(DevBuf& b, size_t bytes) {
@@ -752,7 +843,10 @@ enum WorkId {
     W_MJSTATE, W_PERM, W_HIT_T, W_HIT_KIND, W_HIT_OBJ, W_HIT_TRI, W_SH_O, W_SH_D, W_SH_F, W_SH_PSCT, W_SH_COS,
     W_SH_OUT, W_SH_LIGHT, W_SH_FLAGS, W_G_SH, W_PDF_L, W_P_RGB, W_P_LUM, W_P_COST, W_P_VALID, W_FILM, W_Q0, W_Q1,
     W_SQ, W_RQ, W_COUNTS, W_TCOUNT, W_TASKS, W_FIRST, W_RING_COST, W_RING_LUM, W_RING_PTR, W_DELTA, W_NUM_RAYS,
-    W_TQUERIES, W_DUMP_RAD, W_DUMP_LAM, W_DUMP_RASTER, W_DUMP_DEPTH, W_DUMP_DELTA, W_COUNT
+    W_TQUERIES, W_DUMP_RAD, W_DUMP_LAM, W_DUMP_RASTER, W_DUMP_DEPTH, W_DUMP_DELTA,
+    W_BD_LD, W_BD_LI, W_BD_CD, W_BD_CI, W_BD_SP, W_BD_SPN, W_BD_OVF, W_BD_CNT, W_BD_OFF, W_BD_RANGES, W_BD_TAPS,
+    W_BD_FILM, W_BD_SCAN, W_BD_REDO_LIST, W_BD_REDO_INDEX, W_BDR_LD, W_BDR_LI, W_BDR_CD, W_BDR_CI, W_BDR_SP,
+    W_BDR_SPN, W_COUNT
 };
 
 template <typename T>
@@ -948,9 +1042,52 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         D.depth = wbuf<unsigned long long>(c, W_DUMP_DEPTH, m, st);
         D.delta = wbuf<double>(c, W_DUMP_DELTA, dump_samples, st);
     }
+    const bool bdpt = c.integrator == LUMO_INTEGRATOR_BDPT;
+    Bdpt B{}, BR{};  // BR: redo storage for subpaths longer than B holds
+    bool splat_lists = true;
+    uint32_t* tap_cnt = nullptr;
+    uint32_t* tap_off = nullptr;
+    uint64_t* tap_ranges = nullptr;
+    double* dfilm = nullptr;
+    size_t film_n = 0;
+    if (bdpt) {
+        const int V = c.max_vertices;
+        B.lp = VStore{wbuf<double>(c, W_BD_LD, (size_t)VD_N * V * N, st), wbuf<int32_t>(c, W_BD_LI, (size_t)VI_N * V * N, st), V, N};
+        B.cp = VStore{wbuf<double>(c, W_BD_CD, (size_t)VD_N * V * N, st), wbuf<int32_t>(c, W_BD_CI, (size_t)VI_N * V * N, st), V, N};
+        B.sp = SplatStore{wbuf<double>(c, W_BD_SP, (size_t)10 * V * N, st), wbuf<int32_t>(c, W_BD_SPN, N, st), V, N};
+        B.overflow = wbuf<uint32_t>(c, W_BD_OVF, 2, st);
+        B.redo_count = B.overflow + 1;
+        B.redo_cap = (uint32_t)std::min(N, 4096);
+        B.redo_list = wbuf<int32_t>(c, W_BD_REDO_LIST, B.redo_cap, st);
+        B.redo_index = wbuf<int32_t>(c, W_BD_REDO_INDEX, N, st);
+        const int VR = BDPT_MAX_DEPTH + 1, NR = (int)B.redo_cap;  // storage for lumo's deepest subpath
+        BR = B;
+        BR.lp = VStore{wbuf<double>(c, W_BDR_LD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_LI, (size_t)VI_N * VR * NR, st), VR, NR};
+        BR.cp = VStore{wbuf<double>(c, W_BDR_CD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_CI, (size_t)VI_N * VR * NR, st), VR, NR};
+        BR.sp = SplatStore{wbuf<double>(c, W_BDR_SP, (size_t)10 * VR * NR, st), wbuf<int32_t>(c, W_BDR_SPN, NR, st), VR, NR};
+        for (size_t i = 0; i < n_tasks && out; ++i) splat_lists = splat_lists && out[i].splats != nullptr;
+        if (!out) splat_lists = false;
+        if (splat_lists) {
+            tap_cnt = wbuf<uint32_t>(c, W_BD_CNT, N, st);
+            tap_off = wbuf<uint32_t>(c, W_BD_OFF, N, st);
+            tap_ranges = wbuf<uint64_t>(c, W_BD_RANGES, n_tasks + 1, st);
+        } else if (c.splat_film) {
+            film_n = (size_t)3 * (size_t)c.cam.width * (size_t)c.cam.height;
+            dfilm = wbuf<double>(c, W_BD_FILM, film_n, st);
+        } else if (out) {
+            return LUMO_ERR_INVALID;  // BDPT splats need per-task lists or a splat film
+        }
+    }
     if (st) return st;
 
     hipStream_t sm = c.stream;
+    if (bdpt) {
+        HIPCHK(hipMemsetAsync(B.overflow, 0, sizeof(uint32_t), sm));
+        if (dfilm) HIPCHK(hipMemsetAsync(dfilm, 0, sizeof(double) * film_n, sm));
+    }
+    std::vector<uint64_t> n_splats(n_tasks, 0);
+    std::vector<lumo_splat> taps_h;
+    std::vector<uint64_t> ranges_h(n_tasks + 1);
     HIPCHK(hipMemcpyAsync(T.t, tasks, sizeof(lumo_tile_task) * n_tasks, hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemcpyAsync(T.first, first.data(), sizeof(int32_t) * (n_tasks + 1), hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemcpyAsync(S.task, task_of.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, sm));
@@ -994,8 +1131,22 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         int32_t* qb = S.q1;
         uint32_t ub = (uint32_t)N;  // upper bound on the alive count of the next bounce
         int issued = 0, consumed = 0;
-        bool done = false;
+        bool done = bdpt;
+        if (bdpt) {
+            StageTimer tm(c, g_timing, ST_SHADE);
+            HIPCHK(hipMemsetAsync(B.redo_count, 0, sizeof(uint32_t), sm));
+            launch_trav(c, (uint64_t)N, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                k_bdpt<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
+                    <<<grid, BLOCK, shm, sm>>>(c.sc, S, T, c.cam, B, N);
+            });
+            launch_trav(c, (uint64_t)B.redo_cap, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                k_bdpt_redo<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
+                    <<<grid, BLOCK, shm, sm>>>(c.sc, S, T, c.cam, B, BR);
+            });
+            HIPCHK(hipGetLastError());
+        }
         for (;;) {
+            if (done) break;
             while (consumed < issued) {
                 hipEvent_t e = c.snap_ev[consumed % Ctx::SNAP_RING];
                 if (issued - consumed >= ahead) {
@@ -1058,6 +1209,43 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 1);
         }
         HIPCHK(hipGetLastError());
+        if (bdpt && dfilm) {
+            k_bdpt_taps<2><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BR, c.cam, N, c.tone_map, c.tone_arg, nullptr, nullptr, nullptr,
+                                                 dfilm);
+            HIPCHK(hipGetLastError());
+        } else if (bdpt && splat_lists) {
+            // this pass's taps in lumo's order: count per slot, exclusive scan (slots are tasks in
+            // order, pixels in order within a task), write, then append per task on the host
+            k_bdpt_taps<0><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BR, c.cam, N, c.tone_map, c.tone_arg, tap_cnt, nullptr, nullptr,
+                                                 nullptr);
+            size_t tmp_bytes = 0;
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, tap_cnt, tap_off, N, sm));
+            void* tmp = wbuf<char>(c, W_BD_SCAN, tmp_bytes, st);
+            if (st) return st;
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, tap_cnt, tap_off, N, sm));
+            k_task_tap_ranges<<<ceil_div(n_tasks + 1, BLOCK), BLOCK, 0, sm>>>(T, tap_cnt, tap_off, (int)n_tasks, N,
+                                                                              tap_ranges);
+            HIPCHK(hipMemcpyAsync(ranges_h.data(), tap_ranges, sizeof(uint64_t) * (n_tasks + 1), hipMemcpyDeviceToHost, sm));
+            HIPCHK(hipStreamSynchronize(sm));
+            const uint64_t total = ranges_h[n_tasks];
+            if (total > 0) {
+                lumo_splat* dtaps = wbuf<lumo_splat>(c, W_BD_TAPS, total, st);
+                if (st) return st;
+                k_bdpt_taps<1><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BR, c.cam, N, c.tone_map, c.tone_arg, nullptr, tap_off,
+                                                     dtaps, nullptr);
+                HIPCHK(hipGetLastError());
+                taps_h.resize(total);
+                HIPCHK(hipMemcpyAsync(taps_h.data(), dtaps, sizeof(lumo_splat) * total, hipMemcpyDeviceToHost, sm));
+                HIPCHK(hipStreamSynchronize(sm));
+                for (size_t i = 0; i < n_tasks; ++i) {
+                    const uint64_t a = ranges_h[i], b = ranges_h[i + 1];
+                    for (uint64_t k = a; k < b; ++k) {
+                        if (n_splats[i] < out[i].splat_cap) out[i].splats[n_splats[i]] = taps_h[k];
+                        n_splats[i]++;
+                    }
+                }
+            }
+        }
     }
     // results
     std::vector<double> film((size_t)4 * N);
@@ -1078,6 +1266,21 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     }
     HIPCHK(hipStreamSynchronize(sm));
     if (g_timing) resolve_timers(c);
+    bool splat_oom = false;
+    if (bdpt) {
+        uint32_t ovf = 0;
+        HIPCHK(hipMemcpy(&ovf, B.overflow, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (ovf) return LUMO_ERR_UNSUPPORTED;  // more long subpaths in one pass than the redo list holds
+        if (dfilm) {
+            std::vector<double> f(film_n);
+            HIPCHK(hipMemcpy(f.data(), dfilm, sizeof(double) * film_n, hipMemcpyDeviceToHost));
+            for (size_t k = 0; k < film_n; ++k) c.splat_film[k] += f[k];
+        }
+        for (size_t i = 0; i < n_tasks && out; ++i) {
+            out[i].num_splats = n_splats[i];
+            splat_oom = splat_oom || (splat_lists && n_splats[i] > out[i].splat_cap);
+        }
+    }
     for (size_t i = 0; i < n_tasks; ++i) {
         if (!out) break;
         const lumo_tile_task& t = tasks[i];
@@ -1087,12 +1290,13 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         out[i].num_rays = rays[i];
         out[i].num_queries = queries[i];
     }
-    c.stats.closest_queries += closest_q;
     {
         unsigned long long total_q = 0;
         for (size_t i = 0; i < n_tasks; ++i) total_q += queries[i];
+        if (bdpt) closest_q = total_q;  // BDPT: all scene queries of the samples
         shadow_q = total_q - closest_q;  // per-slot query counters: 1 per closest + 1 per valid record
     }
+    c.stats.closest_queries += closest_q;
     c.stats.shadow_queries += shadow_q;
     c.stats.bounces += bounces;
     for (int k = 0; k < 2; ++k) {
@@ -1100,7 +1304,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         c.stats.kd_nodes[k] += tc[k * TC_N + TC_KD];
         c.stats.tri_tests[k] += tc[k * TC_N + TC_TRI];
     }
-    return LUMO_OK;
+    return splat_oom ? LUMO_ERR_OOM : LUMO_OK;
 }
 
 }  // namespace
@@ -1377,6 +1581,19 @@ lumo_status lumo_camera_set(void* ctx, const lumo_camera_desc* d) {
     c->cam.x2r = m3(d->xyz_to_rgb);
     c->cam.fr = d->filter_radius;
     c->cam.fsig = d->filter_sigma;
+    c->cam.width = (double)d->width;
+    c->cam.height = (double)d->height;
+    {   // CameraConfig::new (camera.rs:47-76): image plane area at z = 1
+        const DCam& k = c->cam;
+        V3 p_min3 = xf_pt_inv(k.sctr, V3{0.0, 0.0, 0.0});
+        V3 p_max3 = xf_pt_inv(k.sctr, V3{k.width, k.height, 0.0});
+        p_min3 = xf_pt_inv(k.cts, p_min3);
+        p_max3 = xf_pt_inv(k.cts, p_max3);
+        const V2 p_min = V2{p_min3.x, p_min3.y} / (p_min3.z == 0.0 ? 1.0 : p_min3.z);
+        const V2 p_max = V2{p_max3.x, p_max3.y} / (p_max3.z == 0.0 ? 1.0 : p_max3.z);
+        const V2 pd = p_max - p_min;
+        c->cam.image_plane_area = fabs(pd.x * pd.y);
+    }
     if ((uint64_t)std::ceil(d->filter_radius - 0.5) != 1) return LUMO_ERR_UNSUPPORTED;  // 3x3 gather footprint
     c->has_camera = true;
     return LUMO_OK;
@@ -1387,16 +1604,27 @@ lumo_status lumo_render_tiles(void* ctx, const lumo_tile_task* tasks, size_t n, 
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c || (!tasks && n) || (!out && n)) return LUMO_ERR_INVALID;
     if (cfg && cfg->rng_mode != LUMO_RNG_WAVEFRONT) return LUMO_ERR_UNSUPPORTED;
-    if (cfg && cfg->integrator != LUMO_INTEGRATOR_PATH_TRACE) return LUMO_ERR_UNSUPPORTED;
+    if (cfg && cfg->integrator != LUMO_INTEGRATOR_PATH_TRACE && cfg->integrator != LUMO_INTEGRATOR_BDPT)
+        return LUMO_ERR_UNSUPPORTED;
+    if (cfg && (cfg->max_vertices < 0 || cfg->max_vertices > BDPT_MAX_DEPTH + 1)) return LUMO_ERR_INVALID;
     if (cfg && (cfg->tone_map < LUMO_TONEMAP_NONE || cfg->tone_map > LUMO_TONEMAP_REINHARD)) return LUMO_ERR_INVALID;
     HIPCHK(hipSetDevice(c->device));
-    struct ToneScope {  // the tone map applies to this call only
+    struct CallScope {  // tone map and integrator settings apply to this call only
         Ctx* c;
-        ~ToneScope() { c->tone_map = LUMO_TONEMAP_NONE; }
+        ~CallScope() {
+            c->tone_map = LUMO_TONEMAP_NONE;
+            c->integrator = LUMO_INTEGRATOR_PATH_TRACE;
+            c->splat_film = nullptr;
+        }
     } scope{c};
     c->tone_map = cfg ? cfg->tone_map : LUMO_TONEMAP_NONE;
     c->tone_arg = cfg ? cfg->tone_arg : 0.0;
-    const size_t max_paths = (cfg && cfg->max_paths > 0) ? (size_t)cfg->max_paths : (size_t)1 << 30;
+    c->integrator = cfg ? cfg->integrator : LUMO_INTEGRATOR_PATH_TRACE;
+    c->max_vertices = (cfg && cfg->max_vertices > 0) ? cfg->max_vertices : 64;
+    c->splat_film = cfg ? cfg->splat_film : nullptr;
+    size_t max_paths = (cfg && cfg->max_paths > 0) ? (size_t)cfg->max_paths : (size_t)1 << 30;
+    if (c->integrator == LUMO_INTEGRATOR_BDPT)  // vertex storage: ~30 KB per slot at 64 vertices
+        max_paths = std::min(max_paths, (size_t)(((size_t)1 << 20) * 64 / (size_t)c->max_vertices));
     size_t i = 0;
     while (i < n) {  // chunk the task list so that at most max_paths slots are in flight
         size_t j = i, paths = 0;
@@ -1494,7 +1722,18 @@ lumo_status lumo_debug_paths(void* ctx, const lumo_tile_task* task, lumo_path_du
     HIPCHK(hipSetDevice(c->device));
     Dump D{dump->radiance, dump->lambda_, dump->raster, dump->delta,
            reinterpret_cast<unsigned long long*>(dump->depth)};
-    return render_impl(*c, task, 1, nullptr, &D, task->samples);
+    c->integrator = c->debug_integrator;
+    const lumo_status st = render_impl(*c, task, 1, nullptr, &D, task->samples);
+    c->integrator = LUMO_INTEGRATOR_PATH_TRACE;
+    return st;
+}
+
+// Integrator used by lumo_debug_paths (test hook; BDPT splats are not collected there).
+lumo_status lumo_debug_set_integrator(void* ctx, int integrator) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || (integrator != LUMO_INTEGRATOR_PATH_TRACE && integrator != LUMO_INTEGRATOR_BDPT)) return LUMO_ERR_INVALID;
+    c->debug_integrator = integrator;
+    return LUMO_OK;
 }
 
 }  // extern "C"

@@ -141,3 +141,38 @@ def bistro_standin(seed=7, groups=BISTRO_GROUPS, lamps=BISTRO_LAMPS, n=24):
         v = np.array([c - eu - ev, c + eu - ev, c + eu + ev, c - eu + ev])
         lamps_out.append((v, np.array([[0, 1, 2, 3]])))
     return out, lamps_out
+
+
+SUZANNE_TRIANGLES = 968  # suzanne.obj (examples/caustics.rs) triangulated
+
+
+def suzanne_standin(seed=3):
+    """Closed ~1k-triangle head-like blob in place of suzanne.obj: a UV sphere (22 x 22 quads,
+    fan-capped poles -> 968 triangles) squashed and given two seeded 'ear' bulges and low-frequency
+    bumps, so that mirror / glass caustics come from a curved, non-convex-looking surface."""
+    rng = np.random.default_rng(seed)
+    n_lat, n_lon = 23, 22
+    th = np.arange(1, n_lat) * (np.pi / n_lat)      # interior latitude rings
+    ph = np.arange(n_lon) * (2 * np.pi / n_lon)
+    T, P = np.meshgrid(th, ph, indexing="ij")
+    d = np.stack([np.sin(T) * np.cos(P), np.cos(T), np.sin(T) * np.sin(P)], -1)
+    k = rng.integers(1, 5, size=(4, 2))
+    phase = rng.uniform(0, 2 * np.pi, size=4)
+    bump = sum(np.sin(kk[0] * T + kk[1] * P + f) for kk, f in zip(k, phase)) * 0.04
+    ears = 0.35 * (np.exp(-((d[..., 0] - 0.8) ** 2 + (d[..., 1] - 0.4) ** 2) * 12.0) +
+                   np.exp(-((d[..., 0] + 0.8) ** 2 + (d[..., 1] - 0.4) ** 2) * 12.0))
+    r = (1.0 + bump + ears)[..., None]
+    v = (d * r * np.array([1.0, 0.85, 0.9])).reshape(-1, 3)
+    top, bot = len(v), len(v) + 1
+    v = np.vstack([v, [[0.0, 0.85, 0.0], [0.0, -0.85, 0.0]]])
+    faces = []
+    for i in range(n_lat - 2):
+        for j in range(n_lon):
+            a, b = i * n_lon + j, i * n_lon + (j + 1) % n_lon
+            c, e = (i + 1) * n_lon + (j + 1) % n_lon, (i + 1) * n_lon + j
+            faces += [(a, b, c), (a, c, e)]
+    last = (n_lat - 2) * n_lon
+    for j in range(n_lon):
+        faces.append((top, (j + 1) % n_lon, j))
+        faces.append((bot, last + j, last + (j + 1) % n_lon))
+    return v, np.asarray(faces, dtype=np.int64)

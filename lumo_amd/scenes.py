@@ -4,7 +4,7 @@ procedural stand-ins of lumo_amd.procedural."""
 import math
 
 from . import Camera, Material, Scene, Spectrum, named_spectrum
-from .procedural import dragon_standin
+from .procedural import dragon_standin, suzanne_standin
 
 
 def cornell():
@@ -52,3 +52,23 @@ def bistro(standin=None):
 def bistro_camera(resolution):
     """bistro.rs:15-18 exterior camera."""
     return Camera.builder().origin(-16.0, 5.0, -1.0).towards(0.0, 0.0, 0.0).resolution(resolution).build()
+
+
+def caustics(mesh=None):
+    """examples/caustics.rs:7-37: empty box with MAGENTA / CYAN walls, a mirror and a glass copy
+    of suzanne (`mesh` = (vertices, faces); default: the 968-triangle procedural stand-in),
+    each to_unit_size -> to_origin -> rotations -> translate."""
+    v, f = mesh if mesh is not None else suzanne_standin()
+    scene = Scene.empty_box(Spectrum.from_srgb(242, 242, 242), Material.diffuse(named_spectrum("MAGENTA")),
+                            Material.diffuse(named_spectrum("CYAN")))
+    pi = math.pi
+    scene.add_mesh(v, f, Material.mirror()).to_unit_size().to_origin() \
+        .rotate_y(-pi / 8.0).rotate_z(pi / 8.0).rotate_x(-pi / 8.0).translate(0.5, -0.3, -1.0)
+    scene.add_mesh(v, f, Material.glass()).to_unit_size().to_origin() \
+        .rotate_y(pi / 8.0).rotate_z(-pi / 8.0).rotate_x(pi / 16.0).translate(-0.35, 0.25, -1.25)
+    return scene
+
+
+def caustics_camera(resolution):
+    """caustics.rs:7-10: origin (0, 0, 2), zoom 3."""
+    return Camera.builder().origin(0.0, 0.0, 2.0).zoom(3.0).resolution(resolution).build()

@@ -98,8 +98,9 @@ def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path
     return bufs, res, cnt
 
 
-def trace_paths(scene_desc, camera_desc, task, path=None):
+def trace_paths(scene_desc, camera_desc, task, path=None, integrator=0):
     lib = load(path)
+    lib.oracle_set_integrator(integrator)
     P = (task.px_max[0] - task.px_min[0]) * (task.px_max[1] - task.px_min[1])
     m = P * task.samples
     rad, lam, ras = np.zeros(4 * m), np.zeros(4 * m), np.zeros(2 * m)
@@ -108,6 +109,7 @@ def trace_paths(scene_desc, camera_desc, task, path=None):
                                 rad.ctypes.data_as(_ffi.c_double_p), lam.ctypes.data_as(_ffi.c_double_p),
                                 ras.ctypes.data_as(_ffi.c_double_p), depth.ctypes.data_as(_ffi.c_uint64_p),
                                 delta.ctypes.data_as(_ffi.c_double_p))
+    lib.oracle_set_integrator(0)
     assert st == 0, st
     return dict(radiance=rad.reshape(-1, 4), lam=lam.reshape(-1, 4), raster=ras.reshape(-1, 2), depth=depth,
                 delta=delta)
