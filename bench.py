@@ -20,6 +20,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -44,9 +46,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3"],
+    ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3", "c4"],
                     help="c1 Cornell 1024^2@1024 (BASELINE configs[1]); c2 dragon.rs 1920x1080@256 with the "
-                         "871k-triangle stand-in (configs[2]); c3 Bistro stand-in 1920x1080@256 (configs[3])")
+                         "871k-triangle stand-in (configs[2]); c3 Bistro stand-in 1920x1080@256 (configs[3]); "
+                         "c4 caustics.rs BDPT 1024^2@4096 (configs[4])")
     ap.add_argument("--res", type=int, default=None, help="square resolution override")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--max-paths", type=int, default=1 << 23, help="paths in flight per wavefront")
@@ -75,12 +78,18 @@ def main():
     mine = shard_tasks(tasks, W, H, rank, ws)
     mine_arr = (_ffi.TileTask * len(mine))(*mine)
 
+    splat_film = np.zeros((H, W, 3)) if wl.get("integrator") == L.Integrator.BDPathTrace else None
     dev = L.Device(local)
     dev.upload(scene, cam)
     lib = _ffi.load()
 
     def step():
-        bufs, res = dev.render_tasks(mine_arr, max_paths=args.max_paths)
+        if wl.get("integrator") == L.Integrator.BDPathTrace:
+            splat_film[:] = 0.0
+            bufs, res = dev.render_tasks(mine_arr, max_paths=args.max_paths, integrator=L.Integrator.BDPathTrace,
+                                         splat_film=splat_film)
+        else:
+            bufs, res = dev.render_tasks(mine_arr, max_paths=args.max_paths)
         return sum(r.num_queries for r in res), sum(r.num_camera_rays for r in res), sum(r.num_rays for r in res)
 
     def barrier():
@@ -116,8 +125,8 @@ def main():
         q, cams, rays = (float(x) for x in s.tolist())
 
     if rank == 0:
-        roof = roofline(st, n_shadow_rays(scene))
-        cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp) if (args.cpu_baseline and ws == 1) else None
+        roof = roofline(st, n_shadow_rays(scene), bdpt=wl.get("integrator") == L.Integrator.BDPathTrace)
+        cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl) if (args.cpu_baseline and ws == 1) else None
         value = q / elapsed / 1e6
         out = {
             "metric": "Mrays/s",
@@ -133,12 +142,12 @@ def main():
             "dtype": "f64",
             "data": wl["data"],
             "config": {
-                "workload": f"{wl['name']}_{W}x{H}_{spp}spp_pathtrace",
+                "workload": f"{wl['name']}_{W}x{H}_{spp}spp_{wl.get('tag', 'pathtrace')}",
                 "scene": wl["scene"],
                 "camera": wl["camera"],
                 "resolution": [W, H],
                 "spp": spp,
-                "integrator": "PathTrace (NEE + MIS + RR)",
+                "integrator": wl.get("integrator_name", "PathTrace (NEE + MIS + RR)"),
                 "seed": SEED,
                 "rng_mode": "wavefront (per-path Xorshiftr128+ streams; DESIGN.md §RNG)",
                 "parallelism": f"tiles sharded tile%{ws}",
@@ -174,6 +183,16 @@ def build_config(args):
         wl = {"name": "dragon", "scene": "examples/dragon.rs: empty_box + 871414-triangle procedural stand-in "
                                          "(transparent MfDielectric 0.03, eta 1.5 glass curve) as an Instance",
               "camera": "Camera::builder() default", "data": "synthetic (procedural stand-in for dragon.obj)"}
+    elif args.config == "c4":
+        W = H = args.res or 1024
+        spp = args.spp or 4096
+        scene, cam = scenes.caustics(), scenes.caustics_camera((W, H))
+        wl = {"name": "caustics", "scene": "examples/caustics.rs: empty_box MAGENTA/CYAN + mirror and glass "
+                                           "instances of a 968-triangle suzanne stand-in",
+              "camera": "origin (0,0,2), zoom 3 (caustics.rs:7-10)",
+              "data": "synthetic (procedural stand-in for suzanne.obj)", "integrator": L.Integrator.BDPathTrace,
+              "integrator_name": "BDPathTrace (all (s,t) strategies, MIS, light-tracing splats)", "tag": "bdpt",
+              "cpu_tile_stride": 512, "cpu_batches": 1}
     else:
         W, H = (args.res, args.res) if args.res else (1920, 1080)
         spp = args.spp or 256
@@ -187,7 +206,7 @@ def build_config(args):
     return scene, cam, (W, H), spp, wl
 
 
-def roofline(st, n_shadow):
+def roofline(st, n_shadow, bdpt=False):
     """Dominant-kernel roofline from live per-launch HIP-event times and traversal counters."""
     ms = list(st.kernel_ms)
     launches = list(st.launches)
@@ -204,8 +223,9 @@ def roofline(st, n_shadow):
                   st.tri_tests[1] * B_TRI)
     else:
         nbytes = None
-    pmc = pmc_traffic(name)
-    out = {"bound": "hbm", "kernel": f"k_{name}", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    kname = "k_bdpt" if (bdpt and name == "shade") else f"k_{name}"  # BDPT times its kernel as the shade stage
+    pmc = pmc_traffic(kname[2:])
+    out = {"bound": "hbm", "kernel": kname, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "traffic": pmc.get("hbm_bytes_per_launch"), "traffic_raw": pmc.get("hbm_bytes_per_launch_raw"),
            "traffic_source": "profiles/pmc_traffic.json" if pmc else None, "stages": per_stage}
     cq, sq = max(st.closest_queries, 1), max(st.shadow_queries, 1)
@@ -242,7 +262,7 @@ def pmc_traffic(kernel):
         return {}
 
 
-def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp):
+def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl):
     """The oracle (f64 restatement of lumo's CPU path, lumo's own tile-serial RNG order) on this
     host: every k-th tile of every batch of the same frame, all spp; Mrays/s of that sample."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -251,16 +271,21 @@ def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp):
         O.load()
     except OSError:
         return None
-    sample = [t for i, t in enumerate(tasks) if (i % tiles) % args.cpu_tile_stride == 0]
+    integrator = wl.get("integrator", 0)
+    stride = wl.get("cpu_tile_stride", args.cpu_tile_stride)
+    batches = wl.get("cpu_batches", None)  # BDPT: the first batch only (CPU BDPT is ~100x slower)
+    sample = [t for i, t in enumerate(tasks) if (i % tiles) % stride == 0 and (batches is None or i // tiles < batches)]
     threads = min(16, os.cpu_count() or 1)
     t0 = time.perf_counter()
-    bufs, res, cnt = O.render_tasks(scene.desc(), cam.desc, sample, O.LUMO_ORDER, threads)
+    bufs, res, cnt = O.render_tasks(scene.desc(), cam.desc, sample, O.LUMO_ORDER, threads, integrator=integrator,
+                                    splats_out=[] if integrator else None)
     dt = time.perf_counter() - t0
     q = sum(r.num_queries for r in res)
     paths = sum(r.num_camera_rays for r in res)
     return {"value": round(q / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "msamples_per_s": round(paths / dt / 1e6, 4), "seconds": round(dt, 2),
-            "sample": f"{len(sample)} tasks = every {args.cpu_tile_stride}th 16x16 tile of each 256-spp batch of "
+            "sample": f"{len(sample)} tasks = every {stride}th 16x16 tile of "
+                      f"{'each' if batches is None else f'the first {batches}'} 256-spp batch(es) of "
                       f"the {W}x{H} @ {spp} spp frame ({paths} paths), lumo tile-serial RNG order"}
 
 

@@ -1195,6 +1195,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             HIPCHK(hipEventSynchronize(c.snap_ev[consumed % Ctx::SNAP_RING]));
             consumed++;
         }
+        if (g_timing && bdpt) HIPCHK(hipStreamSynchronize(sm));  // BDPT passes have no bounce snapshots
         if (g_timing) resolve_timers(c);
         {
             StageTimer tm(c, g_timing, ST_FINISH);

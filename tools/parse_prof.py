@@ -16,7 +16,8 @@ def rows(pattern):
 
 def short(name):
     for k in ("k_camera", "k_closest", "k_shade", "k_shadow_queue", "k_shadow", "k_resolve", "k_finish", "k_film",
-              "k_ring", "k_init_mj", "k_init_seeds", "k_trace"):
+              "k_ring", "k_init_mj", "k_init_seeds", "k_trace", "k_bdpt_redo", "k_bdpt_taps", "k_bdpt",
+              "k_bounce_begin", "k_task_tap_ranges"):
         if k in name:
             return k
     return name[:60]
