@@ -20,13 +20,10 @@ constexpr double DINF = __builtin_huge_val();
 constexpr int NS = 4;
 constexpr double Y_INTEGRAL = 106.856895;
 constexpr double SVI = 253.819;  // SAMPLE_VISIBLE_INTEGRAL
-// Traversal stacks are sized per scene.  A stack class STK encodes two capacities,
-// STK = 100 * (BVH stack) + (kd stack); the kernels are instantiated for a few classes and the
-// host picks the smallest one covering the deepest BVH and kd paths of the uploaded scene (lumo
-// itself uses 64 for both, kdtree.rs:110, bvh.rs:324; a scene needing more would panic there
-// too).  Small stacks stay in VGPRs; every spare slot costs registers in each nested traversal.
-constexpr int stk_bvh(int stk) { return stk / 100; }
-constexpr int stk_kd(int stk) { return stk % 100; }
+// The kd-tree traversal stack is sized per scene: the kernels are instantiated for a few stack
+// classes STK and the host picks the smallest one covering the deepest kd path of the uploaded
+// scene (lumo uses 64, kdtree.rs:110; a scene needing more would panic there too).  Small stacks
+// stay in VGPRs.  The BVH walk needs no stack (DBvh escape indices).
 
 // kd node packed to 16 B for the device (lumo_kd_node is 32 B): interior nodes hold the split
 // point, leaves {first, count}; meta = right << 2 | axis, axis == 3 marks a leaf.
@@ -42,6 +39,16 @@ struct alignas(16) DKd {
 };
 constexpr int TV_STRIDE = 10;  // doubles per triangle in the vertex soup (A, B, C, pad) -> 80 B
 
+// BVH node as the device walks it: lumo's preorder layout (left child = i + 1) with the right
+// child replaced by the escape index, the next node in preorder after this node's subtree
+// (-1 past the end).  lumo's DFS (bvh.rs:315-362) pushes the right child and descends left; the
+// node it pops after a miss or a leaf is exactly the escape index, so the stackless walk visits
+// the same nodes in the same order with the same t_max at every test.
+struct DBvh {
+    double bmin[3], bmax[3];
+    int32_t escape, first, count, pad0;
+};
+
 struct DScene {
     const double* vertices;
     const double* tv;  // per-triangle vertex soup: A.xyz B.xyz C.xyz (removes the index indirection)
@@ -52,10 +59,10 @@ struct DScene {
     const lumo_kd_node* kd;
     const int32_t* kd_items;
     const lumo_object* objs;
-    const lumo_bvh_node* onodes;
+    const DBvh* onodes;
     const int32_t* oitems;
     const lumo_object* lights;
-    const lumo_bvh_node* lnodes;
+    const DBvh* lnodes;
     const int32_t* litems;
     const double* alias_prob;
     const int32_t* alias_idx;
@@ -79,9 +86,9 @@ __device__ __forceinline__ DScene stage_scene_lds(const DScene& sc, char* lds) {
     for (uint32_t i = threadIdx.x; i < sc.hot_bytes / 16; i += blockDim.x) dst[i] = src[i];
     __syncthreads();
     DScene v = sc;
-    v.onodes = reinterpret_cast<const lumo_bvh_node*>(lds + sc.off_onodes);
+    v.onodes = reinterpret_cast<const DBvh*>(lds + sc.off_onodes);
     v.oitems = reinterpret_cast<const int32_t*>(lds + sc.off_oitems);
-    v.lnodes = reinterpret_cast<const lumo_bvh_node*>(lds + sc.off_lnodes);
+    v.lnodes = reinterpret_cast<const DBvh*>(lds + sc.off_lnodes);
     v.litems = reinterpret_cast<const int32_t*>(lds + sc.off_litems);
     v.objs = reinterpret_cast<const lumo_object*>(lds + sc.off_objs);
     v.lights = reinterpret_cast<const lumo_object*>(lds + sc.off_lights);
@@ -371,8 +378,8 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
                               int* idx_out, Counters& C) {
     const double origin[3] = {r.o.x, r.o.y, r.o.z};
     const double inv_dir[3] = {r.inv.x, r.inv.y, r.inv.z};
-    int st_node[stk_kd(STK)];
-    double st_ts[stk_kd(STK)], st_te[stk_kd(STK)];
+    int st_node[STK];
+    double st_ts[STK], st_te[STK];
     int sp = 0;
     double t_hit = DINF;
     int curr = ob.kd_root;
@@ -611,18 +618,17 @@ __device__ void object_record(const DScene& sc, const lumo_object& ob, int tri, 
     }
 }
 
-// bvh.rs:315-362: returns object index or -1
+// bvh.rs:315-362 (stackless, see DBvh): returns object index or -1
 template <bool GEO, int STK, bool FX>
-__device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_nodes, const int32_t* items,
+__device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, const int32_t* items,
                             const lumo_object* objs, const RayX& r, double t_min, double t_max, Counters& C,
                             double* t_found = nullptr) {
     if (n_nodes == 0) return -1;
     const V3 inv_dir = r.inv;
-    int stack[stk_bvh(STK)];
-    int sp = 0, curr = 0, idx = -1;
+    int curr = 0, idx = -1;
     double tt = t_max;
-    for (;;) {
-        const lumo_bvh_node& node = nodes[curr];
+    while (curr >= 0) {
+        const DBvh& node = nodes[curr];
         double ts, te;
         C.aabb++;
         slab(node.bmin, node.bmax, r.o, inv_dir, ts, te);
@@ -632,7 +638,6 @@ __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_
             const int count = node.count;
             if (count == 0) {
                 curr += 1;
-                if (node.right >= 0) stack[sp++] = node.right;
                 continue;
             }
             for (int k = 0; k < count; ++k) {
@@ -649,15 +654,14 @@ __device__ int bvh_traverse(const DScene& sc, const lumo_bvh_node* nodes, int n_
                 }
             }
         }
-        if (sp == 0) break;
-        curr = stack[--sp];
+        curr = node.escape;
     }
     return idx;
 }
 
 // BVH::hit_t (bvh.rs:371-374)
 template <int STK, bool FX>
-__device__ __forceinline__ double bvh_hit_t(const DScene& sc, const lumo_bvh_node* nodes, int n, const int32_t* items,
+__device__ __forceinline__ double bvh_hit_t(const DScene& sc, const DBvh* nodes, int n, const int32_t* items,
                                             const lumo_object* objs, const RayX& r, double t_min, double t_max,
                                             Counters& C) {
     // bvh.rs:371-374 re-runs objects[idx].hit_t(r, t_min, t_max); in any-hit mode the traversal

@@ -913,19 +913,18 @@ void resolve_timers(Ctx& c) {
 
 bool g_timing = false;
 
-// Stack classes STK = 100 * bvh + kd (dscene.h); the list the kernels are instantiated for.
-constexpr int STACK_CLASSES[] = {404, 408, 448, 1616, 1624, 1632, 1648, 6464};
+// kd stack classes (dscene.h); the list the kernels are instantiated for.
+constexpr int STACK_CLASSES[] = {4, 8, 16, 24, 32, 48, 64};
 template <typename F>
 void by_stack_class(int cls, F&& f) {
     switch (cls) {
-        case 404: f(std::integral_constant<int, 404>{}); break;
-        case 408: f(std::integral_constant<int, 408>{}); break;
-        case 448: f(std::integral_constant<int, 448>{}); break;
-        case 1616: f(std::integral_constant<int, 1616>{}); break;
-        case 1624: f(std::integral_constant<int, 1624>{}); break;
-        case 1632: f(std::integral_constant<int, 1632>{}); break;
-        case 1648: f(std::integral_constant<int, 1648>{}); break;
-        default: f(std::integral_constant<int, 6464>{}); break;
+        case 4: f(std::integral_constant<int, 4>{}); break;
+        case 8: f(std::integral_constant<int, 8>{}); break;
+        case 16: f(std::integral_constant<int, 16>{}); break;
+        case 24: f(std::integral_constant<int, 24>{}); break;
+        case 32: f(std::integral_constant<int, 32>{}); break;
+        case 48: f(std::integral_constant<int, 48>{}); break;
+        default: f(std::integral_constant<int, 64>{}); break;
     }
 }
 
@@ -1423,10 +1422,35 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     chk(upload(*c, d->kd_nodes, (size_t)d->num_kd_nodes, &s.kd));
     chk(upload(*c, d->kd_items, (size_t)d->num_kd_items, &s.kd_items));
     chk(upload(*c, d->objects, (size_t)d->num_objects, &s.objs));
-    chk(upload(*c, d->object_nodes, (size_t)d->num_object_nodes, &s.onodes));
+    // device BVHs: right child -> escape index (DBvh, dscene.h)
+    auto escapes = [&](const lumo_bvh_node* nodes, int n, std::vector<DBvh>& out) {
+        out.assign(n > 0 ? n : 0, DBvh{});
+        std::vector<int32_t> esc(n > 0 ? n : 1, -1);
+        for (int i = 0; i < n; ++i) {  // parents precede children (preorder)
+            const lumo_bvh_node& b = nodes[i];
+            if (b.count == 0) {
+                if (i + 1 < n) esc[i + 1] = b.right >= 0 ? b.right : esc[i];
+                if (b.right >= 0 && b.right < n) esc[b.right] = esc[i];
+            }
+        }
+        for (int i = 0; i < n; ++i) {
+            DBvh& o = out[i];
+            for (int a = 0; a < 3; ++a) {
+                o.bmin[a] = nodes[i].bmin[a];
+                o.bmax[a] = nodes[i].bmax[a];
+            }
+            o.escape = esc[i];
+            o.first = nodes[i].first;
+            o.count = nodes[i].count;
+        }
+    };
+    std::vector<DBvh> obvh, lbvh;
+    escapes(d->object_nodes, d->num_object_nodes, obvh);
+    escapes(d->light_nodes, d->num_light_nodes, lbvh);
+    chk(upload(*c, obvh.data(), obvh.size(), &s.onodes));
     chk(upload(*c, d->object_items, (size_t)d->num_object_items, &s.oitems));
     chk(upload(*c, d->lights, (size_t)d->num_lights, &s.lights));
-    chk(upload(*c, d->light_nodes, (size_t)d->num_light_nodes, &s.lnodes));
+    chk(upload(*c, lbvh.data(), lbvh.size(), &s.lnodes));
     chk(upload(*c, d->light_items, (size_t)d->num_light_items, &s.litems));
     chk(upload(*c, d->alias_prob, (size_t)d->num_lights, &s.alias_prob));
     chk(upload(*c, d->alias_idx, (size_t)d->num_lights, &s.alias_idx));
@@ -1471,9 +1495,9 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
             if (bytes) std::memcpy(hot.data() + off, p, bytes);
             return (uint32_t)off;
         };
-        s.off_onodes = put(d->object_nodes, sizeof(lumo_bvh_node) * d->num_object_nodes);
+        s.off_onodes = put(obvh.data(), sizeof(DBvh) * obvh.size());
         s.off_oitems = put(d->object_items, sizeof(int32_t) * d->num_object_items);
-        s.off_lnodes = put(d->light_nodes, sizeof(lumo_bvh_node) * d->num_light_nodes);
+        s.off_lnodes = put(lbvh.data(), sizeof(DBvh) * lbvh.size());
         s.off_litems = put(d->light_items, sizeof(int32_t) * d->num_light_items);
         s.off_objs = put(d->objects, sizeof(lumo_object) * d->num_objects);
         s.off_lights = put(d->lights, sizeof(lumo_object) * d->num_lights);
@@ -1532,8 +1556,8 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         free_scene(*c);
         return LUMO_ERR_UNSUPPORTED;  // lumo's fixed [_; 64] stacks would overflow too
     }
-    auto fits = [&](int cls) { return stk_bvh(cls) >= need_b && stk_kd(cls) >= need_k; };
-    s.stack_class = 6464;
+    auto fits = [&](int cls) { return cls >= need_k; };
+    s.stack_class = 64;
     for (int cls : STACK_CLASSES)
         if (fits(cls)) {
             s.stack_class = cls;
