@@ -213,7 +213,9 @@ def roofline(st, n_shadow, bdpt=False):
     per_stage = {STAGES[i]: {"ms": round(ms[i], 3), "launches": int(launches[i])} for i in range(8)}
     dom = max(range(8), key=lambda i: ms[i])
     name = STAGES[dom]
-    if name == "closest":
+    if bdpt:
+        nbytes = None  # BDPT: no algorithmic byte model yet
+    elif name == "closest":
         nbytes = (st.closest_queries * B_CLOSEST_IO + st.aabb_tests[0] * B_AABB + st.kd_nodes[0] * B_KD +
                   st.tri_tests[0] * B_TRI)
     elif name == "shadow":
@@ -223,7 +225,14 @@ def roofline(st, n_shadow, bdpt=False):
                   st.tri_tests[1] * B_TRI)
     else:
         nbytes = None
-    kname = "k_bdpt" if (bdpt and name == "shade") else f"k_{name}"  # BDPT times its kernel as the shade stage
+    # BDPT stage slots: walk traces = closest (k_closest), walk steps = shade (k_bdpt_step),
+    # connections = shadow (k_bdpt_conn_a + k_bdpt_vis + k_bdpt_paths), re-runs + fold = resolve
+    bd_names = {"closest": "bdpt_walk_trace", "shade": "bdpt_walk_step", "shadow": "bdpt_connections",
+                "resolve": "bdpt_redo_fold"}
+    if bdpt:
+        per_stage = {bd_names.get(k, k): v for k, v in per_stage.items()}
+    kname = {"closest": "k_closest", "shade": "k_bdpt_step", "shadow": "k_bdpt_vis",
+             "resolve": "k_bdpt_redo"}.get(name, f"k_{name}") if bdpt else f"k_{name}"
     pmc = pmc_traffic(kname[2:])
     out = {"bound": "hbm", "kernel": kname, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "traffic": pmc.get("hbm_bytes_per_launch"), "traffic_raw": pmc.get("hbm_bytes_per_launch_raw"),

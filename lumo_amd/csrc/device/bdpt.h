@@ -1,8 +1,10 @@
 // Bidirectional path tracing on the device (integrator/bd_path_trace*.rs), included by
 // kernels.hip inside its anonymous namespace after DCam / Paths.
 //
-// One thread per path slot runs one BDPT sample (bd_path_trace.rs:23-74): the light subpath,
-// the camera subpath, then every (s, t) strategy with MIS.  Subpath vertices live in HBM,
+// A BDPT sample (bd_path_trace.rs:23-74) runs as a wavefront: the light subpaths of all slots
+// bounce through k_closest + k_bdpt_step, then the camera subpaths; k_bdpt_conn then evaluates
+// every (s, t) strategy of every sample as its own work item (visibility, MIS weight,
+// contribution) and k_bdpt_fold adds the contributions in lumo's order.  Subpath vertices live in HBM,
 // structure-of-arrays by vertex index (lanes of a wave walk the same depth together, so vertex
 // reads and writes coalesce).  Light-tracing connections (t = 1) produce splats, kept per slot in
 // generation order and turned into film taps by k_bdpt_taps.  Everything follows the oracle's
@@ -14,7 +16,7 @@
 
 constexpr int BDPT_RR_DEPTH = 5, BDPT_MAX_DEPTH = 1024;  // path_gen.rs
 enum { TR_RADIANCE = 0, TR_IMPORTANCE = 1 };
-enum { VF_BLANK = 1, VF_BACKFACE = 2 };
+enum { VF_BLANK = 1, VF_BACKFACE = 2, VF_DELTA = 4 };  // VF_DELTA: Material::is_delta at L[0] (never changes)
 constexpr int VD_N = 22, VI_N = 3;  // doubles / ints per stored vertex
 
 // A subpath vertex (vertex.rs).  `blank` marks the camera vertex (Material::Blank).
@@ -24,6 +26,7 @@ struct BVtx {
     double pdf_fwd, pdf_bck;
     int mat, light;
     bool blank, backface;
+    bool del = false;  // stored flag only (walk vertices); v_is_delta recomputes it
 };
 
 // Vertex storage of one subpath kind: field f of vertex v of slot s at ((f * V + v) * N + s).
@@ -45,7 +48,7 @@ struct VStore {
         D(20, v, s) = x.pdf_bck;
         I(0, v, s) = x.mat;
         I(1, v, s) = x.light;
-        I(2, v, s) = (x.blank ? VF_BLANK : 0) | (x.backface ? VF_BACKFACE : 0);
+        I(2, v, s) = (x.blank ? VF_BLANK : 0) | (x.backface ? VF_BACKFACE : 0) | (x.del ? VF_DELTA : 0);
     }
     __device__ BVtx load(int v, int s) const {
         BVtx x;
@@ -59,6 +62,7 @@ struct VStore {
         const int f = I(2, v, s);
         x.blank = (f & VF_BLANK) != 0;
         x.backface = (f & VF_BACKFACE) != 0;
+        x.del = (f & VF_DELTA) != 0;
         return x;
     }
 };
@@ -71,17 +75,24 @@ struct SplatStore {
     __device__ __forceinline__ double& D(int f, int k, int s) const { return d[((size_t)f * V + k) * N + s]; }
 };
 
-// Subpaths longer than the per-slot storage are not truncated: the sample is abandoned and
-// re-run from the same slot state (camera ray, wavelengths, RNG, delta are untouched until a
-// sample completes) by k_bdpt_redo with storage for lumo's maximum depth.
+// A store: subpath vertices, splats and the connections' random numbers, indexed by `si`.  The
+// main store holds `max_vertices` per subpath for every slot; subpaths longer than that are not
+// truncated: the sample is abandoned in the wavefront walk and re-run from its saved start state
+// by k_bdpt_redo into a second store with room for lumo's maximum depth (1025 vertices).
 struct Bdpt {
     VStore lp, cp;
-    SplatStore sp;           // indexed like the vertex stores
+    SplatStore sp;
+    double* draws;           // 2 per light vertex (k = s-2), then 3 per camera vertex (k = t-2)
+    int32_t* ok;             // (k = s-2, si): the t = 1 connection produced a splat
     uint32_t* overflow;      // set when the redo list itself overflows
     uint32_t* redo_count;
     int32_t* redo_list;      // slots to re-run
     int32_t* redo_index;     // per slot: position in the redo list, or -1
     uint32_t redo_cap;
+    __device__ __forceinline__ double& Dr(int f, int k, int si) const {
+        return draws[((size_t)f * lp.V + k) * lp.N + si];
+    }
+    __device__ __forceinline__ int32_t& Ok(int k, int si) const { return ok[(size_t)k * lp.N + si]; }
 };
 
 __device__ __forceinline__ DHit vtx_hit(const BVtx& v) {
@@ -310,7 +321,8 @@ __device__ int bdpt_walk(const DScene& sc, const VStore& st, int slot, Ray ro, X
         const lumo_material m = sc.mats[ho.material];
         // vertex.rs:50-76 (pdf_fwd of the new vertex from the previous one)
         BVtx curr = vtx_of_hit(ho, gathered, 0.0, wo, -1);
-        curr.pdf_fwd = mat_is_delta<FX>(sc, m, L) ? 0.0 : sa_to_area(pdf_fwd, prev.p, ho.p, -wo, ho.ng);
+        curr.del = mat_is_delta<FX>(sc, m, L);
+        curr.pdf_fwd = curr.del ? 0.0 : sa_to_area(pdf_fwd, prev.p, ho.p, -wo, ho.ng);
         if (depth + 1 >= st.V) return -1;  // storage exhausted: the caller re-runs the sample
         depth += 1;
         st.store(depth, slot, curr);
@@ -371,8 +383,7 @@ __device__ MisE mis_plain(const DScene& sc, const PView& pv, int i, const double
     }
     const VStore& st = *pv.st;
     const double fwd = st.D(19, i, pv.slot), bck = st.D(20, i, pv.slot);
-    const bool blank = (st.I(2, i, pv.slot) & VF_BLANK) != 0;
-    const bool del = !blank && mat_is_delta<FX>(sc, sc.mats[st.I(0, i, pv.slot)], L);
+    const bool del = (st.I(2, i, pv.slot) & VF_DELTA) != 0;  // == v_is_delta (blank vertices never set it)
     return light_side ? MisE{bck, fwd, del} : MisE{fwd, bck, del};
 }
 
@@ -494,13 +505,14 @@ __device__ bool bdpt_visible(const DScene& sc, const BVtx& a, const BVtx& b, Cou
 
 // bd_path_trace.rs:77-145 (t = 1): returns true with the splat
 template <int STK, bool FX>
-__device__ bool connect_light_path(const DScene& sc, const DCam& cam, Xorshift& rng, const double* L, const PView& lp,
+// `rs` is the lens sample the reference draws here (only for a non-delta ll; the caller draws it).
+__device__ bool connect_light_path(const DScene& sc, const DCam& cam, V2 rs, const double* L, const PView& lp,
                                    int s, const BVtx& ll, V2* raster_out, DColor* color_out, Counters& C,
                                    uint32_t& queries) {
     if (v_is_delta<FX>(sc, ll, L)) return false;
     const V3 xi = ll.p;
     Ray ri;
-    if (!cam_sample_towards(cam, xi, xs_vec2(rng), &ri)) return false;
+    if (!cam_sample_towards(cam, xi, rs, &ri)) return false;
     const V3 xo = ri.o, wi = ri.d;
     const double p_sct = v_bsdf_pdf<FX>(sc, ll, -wi, L, false);
     const double p_imp = cam_pdf_importance(cam, ri, xi);
@@ -537,14 +549,16 @@ __device__ DColor add_camera_path(const DScene& sc, const DCam& cam, const doubl
     return rad * mis_weight<FX>(sc, cam, L, none, 0, cp, t);
 }
 template <int STK, bool FX>
-__device__ DColor connect_camera_path(const DScene& sc, const DCam& cam, Xorshift& rng, const double* L, const PView& cp,
-                                      int t, const BVtx& cl, Counters& C, uint32_t& queries) {
+// `u`, `rs`: the light pick and light sample the reference draws here (only when cl is neither
+// delta nor on a light; the caller draws them).
+__device__ DColor connect_camera_path(const DScene& sc, const DCam& cam, double u, V2 rs, const double* L,
+                                      const PView& cp, int t, const BVtx& cl, Counters& C, uint32_t& queries) {
     if (v_is_delta<FX>(sc, cl, L) || cl.light >= 0) return cfill(0.0);
-    const int li = sample_light(sc, xs_float(rng));
+    const int li = sample_light(sc, u);
     const lumo_object& light = sc.lights[li];
     const double pdf_light = sc.alias_pdf[li];
     const V3 xo = cl.p;
-    V3 wi = light_sample_towards<FX>(sc, light, xo, xs_vec2(rng));
+    V3 wi = light_sample_towards<FX>(sc, light, xo, rs);
     const double p_sct = v_bsdf_pdf<FX>(sc, cl, wi, L, false);
     if (p_sct == 0.0) return cfill(0.0);
     const Ray ri = spawn(vtx_hit(cl), wi);
@@ -566,11 +580,14 @@ __device__ DColor connect_camera_path(const DScene& sc, const DCam& cam, Xorshif
     const PView lv{nullptr, 0, &ll};
     return radiance * mis_weight<FX>(sc, cam, L, lv, 1, cp, t);
 }
-template <int STK, bool FX>
+
+// connect_paths with the visibility test (bdpt_visible, the last condition of lumo's guard) done
+// beforehand by k_bdpt_vis: `visible` is its result, evaluated only when the other conditions
+// pass, exactly as the short-circuit guard does.
+template <bool FX>
 __device__ DColor connect_paths(const DScene& sc, const DCam& cam, const double* L, const PView& lp, int s,
-                                const PView& cp, int t, const BVtx& ll, const BVtx& cl, Counters& C) {
-    if (v_is_delta<FX>(sc, cl, L) || cl.light >= 0 || v_is_delta<FX>(sc, ll, L) || !bdpt_visible<STK, FX>(sc, ll, cl, C))
-        return cfill(0.0);
+                                const PView& cp, int t, const BVtx& ll, const BVtx& cl, bool visible) {
+    if (v_is_delta<FX>(sc, cl, L) || cl.light >= 0 || v_is_delta<FX>(sc, ll, L) || !visible) return cfill(0.0);
     const V3 xc = cl.p, xl = ll.p;
     const V3 wi = normalize(xl - xc);
     const double p_sct = v_bsdf_pdf<FX>(sc, cl, wi, L, false) * v_bsdf_pdf<FX>(sc, ll, -wi, L, false);
@@ -583,22 +600,254 @@ __device__ DColor connect_paths(const DScene& sc, const DCam& cam, const double*
     return radiance * mis_weight<FX>(sc, cam, L, lp, s, cp, t);
 }
 
-// One BDPT sample (bd_path_trace.rs:23-74) of path slot `slot`, subpaths and splats kept at
-// index `si` of the stores B.  k_camera has drawn the lens and wavelength samples and left the
-// camera ray and the path RNG in the slot.  Returns false, leaving the slot untouched, when a
-// subpath does not fit.
+// ---- per-slot state of the wavefront walks and the connection items
+struct BItems {
+    int32_t *nl, *nc;     // subpath lengths per slot
+    uint32_t *n_a, *n_b;  // items per slot: (a) t = 1, s = 0, s = 1 strategies; (b) s, t >= 2
+    uint32_t *off_a, *off_b;  // exclusive scans
+    double *term_a, *term_b;  // 4 per item
+    uint8_t* vis;         // per (b) item: bdpt_visible
+    double* pdf;          // running pdf_fwd of the walk
+    int32_t* wdepth;      // index of the walk's last stored vertex
+    double *cam_o, *cam_d;  // the camera ray, kept while the light subpath walks
+    uint64_t* rng0;       // the slot's RNG at the start of the sample (2 per slot), for re-runs
+    double* lam0;         // its wavelengths at the start of the sample (4 per slot)
+};
+__device__ __forceinline__ uint32_t bdpt_n_a(int S, int T) { return (uint32_t)(S + T - 1); }
+__device__ __forceinline__ uint32_t bdpt_n_b(int S, int T) { return (uint32_t)(S - 1) * (uint32_t)(T - 1); }
+// last slot with off[slot] <= q (slots without items share offsets)
+__device__ __forceinline__ int item_slot(const uint32_t* off, int n, uint32_t q) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= q) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// After both walks (lumo's order): the random numbers drawn inside the connections (a lens
+// sample per non-delta light vertex s >= 2; a light pick + light sample per camera vertex t >= 2
+// that is neither delta nor on a light), the sample's cost (task.rs:65) and its item count.
+__device__ void bdpt_post_walks(const Bdpt& X, int si, const Paths& S, const BItems& I, int slot, Xorshift& rng,
+                                int n_l, int n_c) {
+    uint64_t cost = (uint64_t)n_l + (uint64_t)n_c;
+    for (int s = 2; s <= n_l; ++s) {
+        if (X.lp.I(2, s - 1, si) & VF_DELTA) continue;
+        cost += 1;
+        const V2 rs = xs_vec2(rng);
+        X.Dr(0, s - 2, si) = rs.x;
+        X.Dr(1, s - 2, si) = rs.y;
+    }
+    for (int t = 2; t <= n_c; ++t) {
+        const bool del = (X.cp.I(2, t - 1, si) & VF_DELTA) != 0;
+        const bool on_light = X.cp.I(1, t - 1, si) >= 0;
+        if (!del && on_light) cost += 1;
+        if (del || on_light) continue;
+        const double u = xs_float(rng);
+        const V2 rs = xs_vec2(rng);
+        X.Dr(2, t - 2, si) = u;
+        X.Dr(3, t - 2, si) = rs.x;
+        X.Dr(4, t - 2, si) = rs.y;
+    }
+    cost += (uint64_t)(n_l - 1) * (uint64_t)(n_c - 1);
+    I.nl[slot] = n_l;
+    I.nc[slot] = n_c;
+    I.n_a[slot] = bdpt_n_a(n_l, n_c);
+    I.n_b[slot] = bdpt_n_b(n_l, n_c);
+    S.depth[slot] = (uint32_t)cost;
+}
+
+// ---- wavefront subpath walks (path_gen.rs:4-157): the light subpaths of all slots bounce by
+// bounce through k_closest + k_bdpt_step, then the camera subpaths.  The RNG stream of a slot is
+// consumed in lumo's order (light pick, light samples, light-walk draws, camera-walk draws).
+
+// Sample start: saves the re-run state, draws the light vertex (path_gen.rs:4-50) and queues the
+// light subpath.
+template <bool FX>
+__global__ __launch_bounds__(BLOCK) void k_bdpt_light_init(DScene sc, Paths S, Bdpt B, BItems I, int n) {
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    bool go = false;
+    if (slot < n && S.p_valid[slot]) {
+        go = true;
+        B.redo_index[slot] = -1;
+        I.n_a[slot] = 0;
+        I.n_b[slot] = 0;
+        for (int k = 0; k < 3; ++k) {
+            I.cam_o[3 * slot + k] = S.ro[3 * slot + k];
+            I.cam_d[3 * slot + k] = S.rd[3 * slot + k];
+        }
+        I.rng0[2 * slot] = S.rng[2 * slot];
+        I.rng0[2 * slot + 1] = S.rng[2 * slot + 1];
+        double L[NS];
+        for (int i = 0; i < NS; ++i) L[i] = I.lam0[4 * slot + i] = S.lam[4 * slot + i];
+        Xorshift rng{S.rng[2 * slot], S.rng[2 * slot + 1]};
+        const int li = sample_light(sc, xs_float(rng));
+        const lumo_object& light = sc.lights[li];
+        const double pdf_light = sc.alias_pdf[li];
+        const V2 rs0 = xs_vec2(rng);
+        const V2 rs1 = xs_vec2(rng);
+        const DHit ho = light_sample_on_hit(sc, light, rs0);
+        const V3 wi_l = square_to_cos_hemisphere(rs1);
+        const Ray ri = spawn(ho, onb_world(onb_new(ho.ns), wi_l));
+        const double pdf_origin = 1.0 / light_area(sc, light);
+        const double pdf_dir = dot(ho.ng, ri.d) / PI;
+        const DColor em = emit(sc, sc.mats[ho.material], L, ho.backface);
+        B.lp.store(0, slot, vtx_of_hit(ho, em, pdf_origin * pdf_light, V3{0.0, 0.0, 0.0}, li));
+        stc(S.gath, slot, em * fabs(dot(ri.d, ho.ns)) / (pdf_light * pdf_origin * pdf_dir));
+        stv3(S.ro, slot, ri.o);
+        stv3(S.rd, slot, ri.d);
+        I.pdf[slot] = pdf_dir;
+        I.wdepth[slot] = 0;
+        S.rng[2 * slot] = rng.hi;
+        S.rng[2 * slot + 1] = rng.lo;
+    }
+    block_append(go, slot, S.q0, S.counts + CNT_NEXT);
+}
+
+// Camera subpath start (bd_path_trace.rs:27): the camera vertex and ray of the slot.
+__global__ __launch_bounds__(BLOCK) void k_bdpt_cam_init(Paths S, Bdpt B, BItems I, DCam cam, int n) {
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    bool go = false;
+    if (slot < n && S.p_valid[slot] && B.redo_index[slot] < 0) {
+        go = true;
+        const Ray r{ldv3(I.cam_o, slot), ldv3(I.cam_d, slot)};
+        const double pdf_wi = cam_pdf_wi(cam, r);
+        const double pdf_xo = cam_pdf_xo(cam, r);
+        B.cp.store(0, slot, vtx_camera(r.o, pdf_xo, cfill(1.0)));
+        stc(S.gath, slot, cfill(1.0));
+        stv3(S.ro, slot, r.o);
+        stv3(S.rd, slot, r.d);
+        I.pdf[slot] = pdf_wi;
+        I.wdepth[slot] = 0;
+    }
+    block_append(go, slot, S.q0, S.counts + CNT_NEXT);
+}
+
+// One walk step (the loop body of path_gen.rs:52-157) after k_closest found the hit.
 template <int STK, bool FX>
-__device__ bool bdpt_sample(const DScene& sc, const Paths& S, const Tasks& T, const DCam& cam, const Bdpt& B, int slot,
-                            int si, Counters& C) {
-    Xorshift rng{S.rng[2 * slot], S.rng[2 * slot + 1]};
-    double L[NS];
-    for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * slot + i];
+__device__ void bdpt_step_one(const DScene& sc, const Paths& S, const Tasks& T, const Bdpt& B, const BItems& I,
+                              int mode, int slot, bool& alive, Counters& C) {
+    const VStore& st = mode == TR_IMPORTANCE ? B.lp : B.cp;
+    int depth = I.wdepth[slot];
+    int n_end = -1;  // subpath length when the walk ends here
+    if (S.hit_kind[slot] == 0) {
+        n_end = depth + 1;
+    } else {
+        const Ray ro{ldv3(S.ro, slot), ldv3(S.rd, slot)};
+        const RayX rx = rayx(ro);
+        const HitRef hr{S.hit_t[slot], S.hit_kind[slot], S.hit_obj[slot], S.hit_tri[slot]};
+        DHit ho;
+        hit_record<FX>(sc, hr, rx, ho);
+        const V3 wo = -ro.d;
+        const lumo_material m = sc.mats[ho.material];
+        double L[NS];
+        for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * slot + i];
+        DColor gathered = ldc(S.gath, slot);
+        double pdf_fwd = I.pdf[slot];
+        const BVtx prev = st.load(depth, slot);
+        BVtx curr = vtx_of_hit(ho, gathered, 0.0, wo, -1);
+        curr.del = mat_is_delta<FX>(sc, m, L);
+        curr.pdf_fwd = curr.del ? 0.0 : sa_to_area(pdf_fwd, prev.p, ho.p, -wo, ho.ng);
+        if (depth + 1 >= st.V) {  // does not fit: re-run the whole sample with full-depth storage
+            const uint32_t pos = atomicAdd(B.redo_count, 1u);
+            if (pos < B.redo_cap) {
+                B.redo_list[pos] = slot;
+                B.redo_index[slot] = (int32_t)pos;
+            } else {
+                atomicOr(B.overflow, 1u);
+            }
+            return;
+        }
+        depth += 1;
+        st.store(depth, slot, curr);
+        Xorshift rng{S.rng[2 * slot], S.rng[2 * slot + 1]};
+        const double delta = T.delta[S.task[slot]];
+        const double u = xs_float(rng);
+        const V2 sq = xs_vec2(rng);
+        V3 wi;
+        if (!bsdf_sample<FX>(sc, m, ho, wo, L, u, sq, wi)) {
+            if (mode == TR_IMPORTANCE)
+                depth -= 1;  // verts.pop()
+            else
+                st.I(1, depth, slot) = get_light_at<STK, FX>(sc, curr, C);
+            n_end = depth + 1;
+        } else {
+            const Ray ri = spawn(ho, wi);
+            const V3 wi2 = ri.d;
+            pdf_fwd = bsdf_pdf<FX>(sc, m, ho, wo, wi2, L);
+            if (pdf_fwd == 0.0) {
+                n_end = depth + 1;
+            } else {
+                const double corr = mode == TR_RADIANCE ? 1.0 : v_shading_correction(sc, curr, wi2);
+                const DColor bsdf = bsdf_f<FX>(sc, m, ho, wo, wi2, L, mode == TR_IMPORTANCE);
+                gathered = gathered * (bsdf * v_shading_cosine(sc, curr, wi2, curr.ns) * corr / pdf_fwd);
+                st.D(20, depth - 1, slot) = v_pdf_prev<FX>(sc, curr, prev, wi2, L);  // verts[prev].pdf_bck
+                bool cont = true;
+                if (depth >= BDPT_RR_DEPTH) {
+                    const double lum = luminance(sc, gathered, L);
+                    const double rr_prob = rmin(lum / delta, 1.0);
+                    if (xs_float(rng) > rr_prob || depth >= BDPT_MAX_DEPTH)
+                        cont = false;
+                    else
+                        gathered = gathered / rr_prob;
+                }
+                if (cont) {
+                    if (curr.del) pdf_fwd = 0.0;
+                    stv3(S.ro, slot, ri.o);
+                    stv3(S.rd, slot, ri.d);
+                    stc(S.gath, slot, gathered);
+                    I.pdf[slot] = pdf_fwd;
+                    I.wdepth[slot] = depth;
+                    alive = true;
+                } else {
+                    n_end = depth + 1;
+                }
+            }
+        }
+        for (int i = 0; i < NS; ++i) S.lam[4 * slot + i] = L[i];  // possibly terminated
+        S.rng[2 * slot] = rng.hi;
+        S.rng[2 * slot + 1] = rng.lo;
+    }
+    if (n_end >= 0) {
+        if (mode == TR_IMPORTANCE) {
+            I.nl[slot] = n_end;
+        } else {  // both subpaths done: the connections' draws, cost, items
+            Xorshift rng{S.rng[2 * slot], S.rng[2 * slot + 1]};
+            bdpt_post_walks(B, slot, S, I, slot, rng, I.nl[slot], n_end);
+            S.rng[2 * slot] = rng.hi;
+            S.rng[2 * slot + 1] = rng.lo;
+        }
+    }
+}
+template <int STK, bool FX>
+__global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_bdpt_step(DScene sc, Paths S, Tasks T, Bdpt B, BItems I,
+                                                                       int mode, const int32_t* queue, int32_t* next_queue) {
+    const uint32_t count = S.counts[CNT_CUR];
+    Counters C{0, 0, 0};
+    for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
+        const uint32_t q = base + threadIdx.x;
+        bool alive = false;
+        int slot = -1;
+        if (q < count) {
+            slot = queue[q];
+            bdpt_step_one<STK, FX>(sc, S, T, B, I, mode, slot, alive, C);
+        }
+        block_append(alive, slot, next_queue, S.counts + CNT_NEXT);
+    }
+    flush_counters(C, S.tcount);
+}
+
+// The same two walks in one thread (path_gen.rs as written), from the slot's saved start state
+// into store X at `si`: used to re-run the samples whose subpaths did not fit the main store.
+template <int STK, bool FX>
+__device__ bool bdpt_walks(const DScene& sc, const Paths& S, const Tasks& T, const DCam& cam, const BItems& I,
+                           const Bdpt& X, int slot, int si, Xorshift& rng, double* L, Counters& C, uint32_t& queries,
+                           int& n_l, int& n_c) {
+    rng = Xorshift{I.rng0[2 * slot], I.rng0[2 * slot + 1]};
+    for (int i = 0; i < NS; ++i) L[i] = I.lam0[4 * slot + i];
     const double delta = T.delta[S.task[slot]];
-    const Ray r{ldv3(S.ro, slot), ldv3(S.rd, slot)};
-    uint32_t queries = 0;
-    // light subpath (path_gen.rs:4-50)
-    int n_l;
-    {
+    const Ray r{ldv3(I.cam_o, slot), ldv3(I.cam_d, slot)};
+    {   // light subpath (path_gen.rs:4-50)
         const int li = sample_light(sc, xs_float(rng));
         const lumo_object& light = sc.lights[li];
         const double pdf_light = sc.alias_pdf[li];
@@ -612,89 +861,207 @@ __device__ bool bdpt_sample(const DScene& sc, const Paths& S, const Tasks& T, co
         const DColor em = emit(sc, sc.mats[ho.material], L, ho.backface);
         const BVtx root = vtx_of_hit(ho, em, pdf_origin * pdf_light, V3{0.0, 0.0, 0.0}, li);
         const DColor gathered = em * fabs(dot(ri.d, ho.ns)) / (pdf_light * pdf_origin * pdf_dir);
-        n_l = bdpt_walk<STK, FX>(sc, B.lp, si, ri, rng, L, delta, root, gathered, pdf_dir, TR_IMPORTANCE, C, queries);
+        n_l = bdpt_walk<STK, FX>(sc, X.lp, si, ri, rng, L, delta, root, gathered, pdf_dir, TR_IMPORTANCE, C, queries);
         if (n_l < 0) return false;
     }
-    // camera subpath
-    int n_c;
-    {
+    {   // camera subpath
         const double pdf_wi = cam_pdf_wi(cam, r);
         const double pdf_xo = cam_pdf_xo(cam, r);
-        n_c = bdpt_walk<STK, FX>(sc, B.cp, si, r, rng, L, delta, vtx_camera(r.o, pdf_xo, cfill(1.0)), cfill(1.0), pdf_wi,
+        n_c = bdpt_walk<STK, FX>(sc, X.cp, si, r, rng, L, delta, vtx_camera(r.o, pdf_xo, cfill(1.0)), cfill(1.0), pdf_wi,
                                   TR_RADIANCE, C, queries);
         if (n_c < 0) return false;
     }
-    const PView lp{&B.lp, si, nullptr}, cp{&B.cp, si, nullptr};
-    DColor radiance = cfill(0.0);
-    uint64_t cost = (uint64_t)n_l + (uint64_t)n_c;
-    int n_sp = 0;  // at most n_l - 1 < V splats
-    for (int s = 2; s <= n_l; ++s) {
-        const BVtx ll = B.lp.load(s - 1, si);
-        if (!v_is_delta<FX>(sc, ll, L)) cost += 1;
-        V2 raster;
-        DColor color;
-        if (connect_light_path<STK, FX>(sc, cam, rng, L, lp, s, ll, &raster, &color, C, queries)) {
-            B.sp.D(0, n_sp, si) = raster.x;
-            B.sp.D(1, n_sp, si) = raster.y;
-            for (int k = 0; k < NS; ++k) B.sp.D(2 + k, n_sp, si) = color.s[k];
-            n_sp++;
-        }
-    }
-    radiance = radiance + add_camera_path<FX>(sc, cam, L, cp, n_c);
-    for (int t = 2; t <= n_c; ++t) {
-        const BVtx cl = B.cp.load(t - 1, si);
-        if (!v_is_delta<FX>(sc, cl, L) && cl.light >= 0) cost += 1;
-        radiance = radiance + connect_camera_path<STK, FX>(sc, cam, rng, L, cp, t, cl, C, queries);
-    }
-    for (int t = 2; t <= n_c; ++t) {
-        const BVtx cl = B.cp.load(t - 1, si);
-        for (int s = 2; s <= n_l; ++s) {
-            cost += 1;
-            radiance = radiance + connect_paths<STK, FX>(sc, cam, L, lp, s, cp, t, B.lp.load(s - 1, si), cl, C);
-        }
-    }
-    // splats carry the wavelengths at the end of the sample (they are read after both walks)
-    for (int k = 0; k < n_sp; ++k)
-        for (int i = 0; i < NS; ++i) B.sp.D(6 + i, k, si) = L[i];
-    B.sp.n[si] = n_sp;
-    stc(S.rad, slot, radiance);
-    for (int i = 0; i < NS; ++i) S.lam[4 * slot + i] = L[i];
-    S.depth[slot] = (uint32_t)cost;
-    S.queries[slot] = queries;
     return true;
 }
 
+// Re-run of the samples whose subpaths did not fit: the walks into R, then the same post-walk
+// bookkeeping; their connections go through the item kernels like every other sample.
 template <int STK, bool LDS, bool FX>
-__global__ __launch_bounds__(BLOCK) void k_bdpt(DScene sc0, Paths S, Tasks T, DCam cam, Bdpt B, int n) {
-    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
-    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
-    Counters C{0, 0, 0};
-    for (int slot = blockIdx.x * blockDim.x + threadIdx.x; slot < n; slot += gridDim.x * blockDim.x) {
-        if (!S.p_valid[slot]) continue;
-        if (bdpt_sample<STK, FX>(sc, S, T, cam, B, slot, slot, C)) {
-            B.redo_index[slot] = -1;
-        } else {
-            const uint32_t pos = atomicAdd(B.redo_count, 1u);
-            if (pos < B.redo_cap) {
-                B.redo_list[pos] = slot;
-                B.redo_index[slot] = (int32_t)pos;
-            } else {
-                atomicOr(B.overflow, 1u);
-            }
-        }
-    }
-    flush_counters(C, S.tcount);
-}
-
-// Re-run of the samples whose subpaths did not fit, with storage R for lumo's maximum depth.
-template <int STK, bool LDS, bool FX>
-__global__ __launch_bounds__(BLOCK) void k_bdpt_redo(DScene sc0, Paths S, Tasks T, DCam cam, Bdpt B, Bdpt R) {
+__global__ __launch_bounds__(BLOCK) void k_bdpt_redo(DScene sc0, Paths S, Tasks T, DCam cam, Bdpt B, Bdpt R, BItems I) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = min(*B.redo_count, B.redo_cap);
     if (count <= blockIdx.x * blockDim.x) return;
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     Counters C{0, 0, 0};
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x)
-        if (!bdpt_sample<STK, FX>(sc, S, T, cam, R, B.redo_list[q], (int)q, C)) atomicOr(B.overflow, 1u);
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
+        const int slot = B.redo_list[q];
+        Xorshift rng;
+        double L[NS];
+        uint32_t queries = 0;
+        int n_l, n_c;
+        if (!bdpt_walks<STK, FX>(sc, S, T, cam, I, R, slot, (int)q, rng, L, C, queries, n_l, n_c)) {
+            atomicOr(B.overflow, 1u);
+            continue;
+        }
+        for (int i = 0; i < NS; ++i) S.lam[4 * slot + i] = L[i];
+        S.queries[slot] = queries;  // replaces the abandoned wavefront walk's count
+        bdpt_post_walks(R, (int)q, S, I, slot, rng, n_l, n_c);
+    }
     flush_counters(C, S.tcount);
+}
+
+// ---- connections as flat lists of work items (one thread each), in lumo's evaluation order.
+// Per slot with subpaths of S light and T camera vertices:
+//   (a) j = 0 .. S+T-2:  [0, S-1) t = 1 light-tracing connection s = j + 2 (splat);
+//                        S-1 the camera subpath's own emission (s = 0, t = T);
+//                        [S, S+T-1) light sampling s = 1, t = j - S + 2
+//   (b) k = 0 .. (S-1)(T-1)-1:  s, t >= 2, t major: t = 2 + k / (S-1), s = 2 + k % (S-1)
+// The connections' random numbers were drawn after the walks (bdpt_post_walks), so every item is
+// independent.  The (b) items, the bulk, are split into k_bdpt_vis (the visibility ray only:
+// lean, high occupancy) and k_bdpt_paths (MIS + contribution, no traversal).  k_bdpt_fold adds
+// the terms per slot in lumo's order and compacts the splats.
+struct ItemSel {
+    int slot, si;
+    const Bdpt* X;
+};
+__device__ __forceinline__ ItemSel item_store(const Bdpt& B, const Bdpt& R, int slot) {
+    const int ri = B.redo_index[slot];
+    return ri >= 0 ? ItemSel{slot, ri, &R} : ItemSel{slot, slot, &B};
+}
+
+template <int STK, bool LDS, bool FX>
+__global__ __launch_bounds__(BLOCK) void k_bdpt_conn_a(DScene sc0, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n,
+                                                        const uint32_t* totals) {
+    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+    const uint32_t total = totals[0];
+    if (total <= blockIdx.x * blockDim.x) return;
+    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    Counters C{0, 0, 0};
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+        const int slot = item_slot(I.off_a, n, q);
+        const ItemSel e = item_store(B, R, slot);
+        const Bdpt& X = *e.X;
+        const int si = e.si;
+        const uint32_t j = q - I.off_a[slot];
+        const int Sl = I.nl[slot], Tc = I.nc[slot];
+        double L[NS];
+        for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * slot + i];
+        const PView lp{&X.lp, si, nullptr}, cp{&X.cp, si, nullptr};
+        uint32_t queries = 0;
+        DColor term = cfill(0.0);
+        if (j < (uint32_t)(Sl - 1)) {
+            const int s = (int)j + 2;
+            const BVtx ll = X.lp.load(s - 1, si);
+            const V2 rs = ll.del ? V2{0.0, 0.0} : V2{X.Dr(0, s - 2, si), X.Dr(1, s - 2, si)};
+            V2 raster;
+            DColor color;
+            const bool ok = connect_light_path<STK, FX>(sc, cam, rs, L, lp, s, ll, &raster, &color, C, queries);
+            X.Ok(s - 2, si) = ok ? 1 : 0;
+            if (ok) {
+                X.sp.D(0, s - 2, si) = raster.x;
+                X.sp.D(1, s - 2, si) = raster.y;
+                for (int k = 0; k < NS; ++k) X.sp.D(2 + k, s - 2, si) = color.s[k];
+            }
+        } else if (j == (uint32_t)(Sl - 1)) {
+            term = add_camera_path<FX>(sc, cam, L, cp, Tc);
+        } else {
+            const int t = (int)j - Sl + 2;
+            const BVtx cl = X.cp.load(t - 1, si);
+            const bool draws = !(cl.del || cl.light >= 0);
+            const double u = draws ? X.Dr(2, t - 2, si) : 0.0;
+            const V2 rs = draws ? V2{X.Dr(3, t - 2, si), X.Dr(4, t - 2, si)} : V2{0.0, 0.0};
+            term = connect_camera_path<STK, FX>(sc, cam, u, rs, L, cp, t, cl, C, queries);
+        }
+        for (int i = 0; i < NS; ++i) I.term_a[4 * (size_t)q + i] = term.s[i];
+        if (queries) atomicAdd(&S.queries[slot], queries);
+    }
+    flush_counters(C, S.tcount);
+}
+
+__device__ __forceinline__ void item_b_st(const BItems& I, int slot, uint32_t q, int& s, int& t) {
+    const uint32_t k = q - I.off_b[slot];
+    const uint32_t sm1 = (uint32_t)(I.nl[slot] - 1);
+    t = 2 + (int)(k / sm1);
+    s = 2 + (int)(k % sm1);
+}
+
+// bdpt_visible of every (b) item whose guard reaches it (bd_path_trace.rs:279-290)
+template <int STK, bool LDS, bool FX>
+__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_vis(DScene sc0, Paths S, Bdpt B, Bdpt R, BItems I,
+                                                                       int n, const uint32_t* totals) {
+    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+    const uint32_t total = totals[1];
+    if (total <= blockIdx.x * blockDim.x) return;
+    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    Counters C{0, 0, 0};
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+        const int slot = item_slot(I.off_b, n, q);
+        const ItemSel e = item_store(B, R, slot);
+        int s, t;
+        item_b_st(I, slot, q, s, t);
+        const VStore& lv = e.X->lp;
+        const VStore& cv = e.X->cp;
+        const int fl = lv.I(2, s - 1, e.si), fc = cv.I(2, t - 1, e.si);
+        bool vis = false;
+        if (!((fc & VF_DELTA) || cv.I(1, t - 1, e.si) >= 0 || (fl & VF_DELTA))) {
+            BVtx a, b;  // only p, ng, err are read by bdpt_visible (spawn from a)
+            a.p = V3{lv.D(0, s - 1, e.si), lv.D(1, s - 1, e.si), lv.D(2, s - 1, e.si)};
+            a.err = V3{lv.D(3, s - 1, e.si), lv.D(4, s - 1, e.si), lv.D(5, s - 1, e.si)};
+            a.ng = V3{lv.D(9, s - 1, e.si), lv.D(10, s - 1, e.si), lv.D(11, s - 1, e.si)};
+            a.ns = a.ng;
+            a.mat = 0;
+            a.backface = false;
+            b.p = V3{cv.D(0, t - 1, e.si), cv.D(1, t - 1, e.si), cv.D(2, t - 1, e.si)};
+            vis = bdpt_visible<STK, FX>(sc, a, b, C);
+        }
+        I.vis[q] = vis ? 1 : 0;
+    }
+    flush_counters(C, S.tcount + TC_N);  // counted with the visibility (shadow) class
+}
+
+// MIS weight and contribution of every (b) item (bd_path_trace.rs:148-277), visibility from k_bdpt_vis
+template <bool FX>
+__global__ __launch_bounds__(BLOCK) void k_bdpt_paths(DScene sc, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n,
+                                                       const uint32_t* totals) {
+    const uint32_t total = totals[1];
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+        const int slot = item_slot(I.off_b, n, q);
+        const ItemSel e = item_store(B, R, slot);
+        int s, t;
+        item_b_st(I, slot, q, s, t);
+        double L[NS];
+        for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * slot + i];
+        const PView lp{&e.X->lp, e.si, nullptr}, cp{&e.X->cp, e.si, nullptr};
+        const DColor term = connect_paths<FX>(sc, cam, L, lp, s, cp, t, e.X->lp.load(s - 1, e.si),
+                                              e.X->cp.load(t - 1, e.si), I.vis[q] != 0);
+        for (int i = 0; i < NS; ++i) I.term_b[4 * (size_t)q + i] = term.s[i];
+    }
+}
+
+// radiance = 0 + emission term + sum_t light-sampling terms + sum_t sum_s connection terms, in
+// lumo's order (bd_path_trace.rs:40-73); the splats are compacted in s order and given the
+// sample's wavelengths.
+__global__ __launch_bounds__(BLOCK) void k_bdpt_fold(Paths S, Bdpt B, Bdpt R, BItems I, int n) {
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= n || !S.p_valid[slot]) return;
+    const ItemSel e = item_store(B, R, slot);
+    const Bdpt& X = *e.X;
+    const int si = e.si;
+    const int Sl = I.nl[slot], Tc = I.nc[slot];
+    auto term = [](const double* p) { return DColor{{p[0], p[1], p[2], p[3]}}; };
+    const double* ta = I.term_a + 4 * (size_t)I.off_a[slot];
+    const double* tb = I.term_b + 4 * (size_t)I.off_b[slot];
+    DColor radiance = cfill(0.0);
+    radiance = radiance + term(ta + 4 * (Sl - 1));
+    for (int t = 2; t <= Tc; ++t) radiance = radiance + term(ta + 4 * (Sl + t - 2));
+    const uint32_t nb = bdpt_n_b(Sl, Tc);
+    for (uint32_t k = 0; k < nb; ++k) radiance = radiance + term(tb + 4 * (size_t)k);
+    stc(S.rad, slot, radiance);
+    int n_sp = 0;
+    for (int s = 2; s <= Sl; ++s) {
+        if (!X.Ok(s - 2, si)) continue;
+        if (n_sp != s - 2)
+            for (int f = 0; f < 6; ++f) X.sp.D(f, n_sp, si) = X.sp.D(f, s - 2, si);
+        for (int i = 0; i < NS; ++i) X.sp.D(6 + i, n_sp, si) = S.lam[4 * slot + i];
+        n_sp++;
+    }
+    X.sp.n[si] = n_sp;
+}
+
+// item totals of the pass: (a), (b)
+__global__ void k_bdpt_total(BItems I, int n, uint32_t* totals) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        totals[0] = I.off_a[n - 1] + I.n_a[n - 1];
+        totals[1] = I.off_b[n - 1] + I.n_b[n - 1];
+    }
 }

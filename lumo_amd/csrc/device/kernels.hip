@@ -846,7 +846,8 @@ enum WorkId {
     W_TQUERIES, W_DUMP_RAD, W_DUMP_LAM, W_DUMP_RASTER, W_DUMP_DEPTH, W_DUMP_DELTA,
     W_BD_LD, W_BD_LI, W_BD_CD, W_BD_CI, W_BD_SP, W_BD_SPN, W_BD_OVF, W_BD_CNT, W_BD_OFF, W_BD_RANGES, W_BD_TAPS,
     W_BD_FILM, W_BD_SCAN, W_BD_REDO_LIST, W_BD_REDO_INDEX, W_BDR_LD, W_BDR_LI, W_BDR_CD, W_BDR_CI, W_BDR_SP,
-    W_BDR_SPN, W_COUNT
+    W_BDR_SPN, W_BD_NL, W_BD_NC, W_BD_NITEMS, W_BD_IOFF, W_BD_DRAWS, W_BD_OK, W_BD_ITOTAL, W_BD_TERM, W_BD_PDF, W_BD_WDEPTH,
+    W_BD_CAMO, W_BD_CAMD, W_BD_RNG0, W_BD_LAM0, W_BDR_DRAWS, W_BDR_OK, W_BD_NB, W_BD_OFFB, W_BD_TERMB, W_BD_VIS, W_COUNT
 };
 
 template <typename T>
@@ -1043,6 +1044,8 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     }
     const bool bdpt = c.integrator == LUMO_INTEGRATOR_BDPT;
     Bdpt B{}, BR{};  // BR: redo storage for subpaths longer than B holds
+    BItems BI{};     // connection work items
+    uint32_t* items_total = nullptr;
     bool splat_lists = true;
     uint32_t* tap_cnt = nullptr;
     uint32_t* tap_off = nullptr;
@@ -1060,10 +1063,27 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         B.redo_list = wbuf<int32_t>(c, W_BD_REDO_LIST, B.redo_cap, st);
         B.redo_index = wbuf<int32_t>(c, W_BD_REDO_INDEX, N, st);
         const int VR = BDPT_MAX_DEPTH + 1, NR = (int)B.redo_cap;  // storage for lumo's deepest subpath
+        B.draws = wbuf<double>(c, W_BD_DRAWS, (size_t)5 * V * N, st);
+        B.ok = wbuf<int32_t>(c, W_BD_OK, (size_t)V * N, st);
+        BI.nl = wbuf<int32_t>(c, W_BD_NL, N, st);
+        BI.nc = wbuf<int32_t>(c, W_BD_NC, N, st);
+        BI.n_a = wbuf<uint32_t>(c, W_BD_NITEMS, N, st);
+        BI.off_a = wbuf<uint32_t>(c, W_BD_IOFF, N, st);
+        BI.n_b = wbuf<uint32_t>(c, W_BD_NB, N, st);
+        BI.off_b = wbuf<uint32_t>(c, W_BD_OFFB, N, st);
+        BI.pdf = wbuf<double>(c, W_BD_PDF, N, st);
+        BI.wdepth = wbuf<int32_t>(c, W_BD_WDEPTH, N, st);
+        BI.cam_o = wbuf<double>(c, W_BD_CAMO, 3 * (size_t)N, st);
+        BI.cam_d = wbuf<double>(c, W_BD_CAMD, 3 * (size_t)N, st);
+        BI.rng0 = wbuf<uint64_t>(c, W_BD_RNG0, 2 * (size_t)N, st);
+        BI.lam0 = wbuf<double>(c, W_BD_LAM0, 4 * (size_t)N, st);
+        items_total = wbuf<uint32_t>(c, W_BD_ITOTAL, 2, st);
         BR = B;
         BR.lp = VStore{wbuf<double>(c, W_BDR_LD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_LI, (size_t)VI_N * VR * NR, st), VR, NR};
         BR.cp = VStore{wbuf<double>(c, W_BDR_CD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_CI, (size_t)VI_N * VR * NR, st), VR, NR};
         BR.sp = SplatStore{wbuf<double>(c, W_BDR_SP, (size_t)10 * VR * NR, st), wbuf<int32_t>(c, W_BDR_SPN, NR, st), VR, NR};
+        BR.draws = wbuf<double>(c, W_BDR_DRAWS, (size_t)5 * VR * NR, st);
+        BR.ok = wbuf<int32_t>(c, W_BDR_OK, (size_t)VR * NR, st);
         for (size_t i = 0; i < n_tasks && out; ++i) splat_lists = splat_lists && out[i].splats != nullptr;
         if (!out) splat_lists = false;
         if (splat_lists) {
@@ -1126,73 +1146,149 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             k_camera<<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass);
         }
         HIPCHK(hipGetLastError());
-        int32_t* qa = S.q0;
-        int32_t* qb = S.q1;
-        uint32_t ub = (uint32_t)N;  // upper bound on the alive count of the next bounce
-        int issued = 0, consumed = 0;
-        bool done = bdpt;
-        if (bdpt) {
-            StageTimer tm(c, g_timing, ST_SHADE);
-            HIPCHK(hipMemsetAsync(B.redo_count, 0, sizeof(uint32_t), sm));
-            launch_trav(c, (uint64_t)N, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
-                k_bdpt<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                    <<<grid, BLOCK, shm, sm>>>(c.sc, S, T, c.cam, B, N);
-            });
-            launch_trav(c, (uint64_t)B.redo_cap, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
-                k_bdpt_redo<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                    <<<grid, BLOCK, shm, sm>>>(c.sc, S, T, c.cam, B, BR);
-            });
-            HIPCHK(hipGetLastError());
-        }
-        for (;;) {
-            if (done) break;
-            while (consumed < issued) {
-                hipEvent_t e = c.snap_ev[consumed % Ctx::SNAP_RING];
-                if (issued - consumed >= ahead) {
-                    HIPCHK(hipEventSynchronize(e));
-                } else if (hipEventQuery(e) != hipSuccess) {
-                    break;
+        // Bounce loop over the alive queue (q0 filled by the producer just launched): k_closest, then
+        // `step` (the integrator's per-hit kernels).  Bounces are enqueued ahead of the host's
+        // knowledge of the counts; see above.
+        auto bounce_loop = [&](auto&& step) -> lumo_status {
+            int32_t* qa = S.q0;
+            int32_t* qb = S.q1;
+            uint32_t ub = (uint32_t)N;  // upper bound on the alive count of the next bounce
+            int issued = 0, consumed = 0;
+            bool done = false;
+            for (;;) {
+                while (consumed < issued) {
+                    hipEvent_t e = c.snap_ev[consumed % Ctx::SNAP_RING];
+                    if (issued - consumed >= ahead) {
+                        HIPCHK(hipEventSynchronize(e));
+                    } else if (hipEventQuery(e) != hipSuccess) {
+                        break;
+                    }
+                    const uint32_t* k = c.snap + CNT_N * (consumed % Ctx::SNAP_RING);
+                    closest_q += k[CNT_CUR];
+                    bounces += k[CNT_CUR] > 0 ? 1 : 0;
+                    ub = k[CNT_NEXT];
+                    done = done || ub == 0;
+                    consumed++;
                 }
-                const uint32_t* k = c.snap + CNT_N * (consumed % Ctx::SNAP_RING);
-                closest_q += k[CNT_CUR];
-                bounces += k[CNT_CUR] > 0 ? 1 : 0;
-                ub = k[CNT_NEXT];
-                done = done || ub == 0;
+                if (done) break;
+                k_bounce_begin<<<1, 64, 0, sm>>>(S.counts);
+                {
+                    StageTimer tm(c, g_timing, ST_CLOSEST);
+                    launch_trav(c, ub, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                        k_closest<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
+                            <<<grid, BLOCK, shm, sm>>>(c.sc, S, qa);
+                    });
+                }
+                step(ub, qa, qb);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipMemcpyAsync(c.snap + CNT_N * (issued % Ctx::SNAP_RING), S.counts, sizeof(uint32_t) * CNT_N,
+                                      hipMemcpyDeviceToHost, sm));
+                HIPCHK(hipEventRecord(c.snap_ev[issued % Ctx::SNAP_RING], sm));
+                issued++;
+                std::swap(qa, qb);
+            }
+            while (consumed < issued) {  // trailing empty bounces
+                HIPCHK(hipEventSynchronize(c.snap_ev[consumed % Ctx::SNAP_RING]));
                 consumed++;
             }
-            if (done) break;
-            k_bounce_begin<<<1, 64, 0, sm>>>(S.counts);
+            return LUMO_OK;
+        };
+        lumo_status bst = LUMO_OK;
+        if (!bdpt) {
+            bst = bounce_loop([&](uint32_t ub, int32_t* qa, int32_t* qb) {
+                {
+                    StageTimer tm(c, g_timing, ST_SHADE);
+                    if (c.sc.full)
+                        k_shade<true><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb);
+                    else
+                        k_shade<false><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb);
+                }
+                {
+                    StageTimer tm(c, g_timing, ST_SHADOW);
+                    launch_trav(c, (uint64_t)ub * (uint32_t)ns, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                        k_shadow<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
+                            <<<grid, BLOCK, shm, sm>>>(c.sc, S);
+                    });
+                }
+            });
+            if (bst) return bst;
+        } else {
+            // BDPT (bdpt.h): light subpaths, then camera subpaths, bounce by bounce through k_closest
+            // + k_bdpt_step; re-runs of samples that did not fit; connection items; fold.  Stage
+            // slots: walks = CLOSEST + SHADE, items = SHADOW, re-runs + fold = RESOLVE.
+            auto walk_step = [&](int mode) {
+                return [&, mode](uint32_t ub, int32_t* qa, int32_t* qb) {
+                    StageTimer tm(c, g_timing, ST_SHADE);
+                    by_stack_class(c.sc.stack_class, [&](auto K) {
+                        if (c.sc.full)
+                            k_bdpt_step<decltype(K)::value, true><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, B, BI, mode, qa, qb);
+                        else
+                            k_bdpt_step<decltype(K)::value, false><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, B, BI, mode, qa, qb);
+                    });
+                };
+            };
+            HIPCHK(hipMemsetAsync(B.redo_count, 0, sizeof(uint32_t), sm));
+            HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));  // drop k_camera's queue
+            if (c.sc.full)
+                k_bdpt_light_init<true><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BI, N);
+            else
+                k_bdpt_light_init<false><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BI, N);
+            bst = bounce_loop(walk_step(TR_IMPORTANCE));
+            if (bst) return bst;
+            HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));
+            k_bdpt_cam_init<<<gN, BLOCK, 0, sm>>>(S, B, BI, c.cam, N);
+            bst = bounce_loop(walk_step(TR_RADIANCE));
+            if (bst) return bst;
             {
-                StageTimer tm(c, g_timing, ST_CLOSEST);
-                launch_trav(c, ub, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
-                    k_closest<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                        <<<grid, BLOCK, shm, sm>>>(c.sc, S, qa);
+                StageTimer tm(c, g_timing, ST_RESOLVE);
+                launch_trav(c, (uint64_t)B.redo_cap, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                    k_bdpt_redo<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
+                        <<<grid, BLOCK, shm, sm>>>(c.sc, S, T, c.cam, B, BR, BI);
                 });
             }
-            {
-                StageTimer tm(c, g_timing, ST_SHADE);
-                if (c.sc.full)
-                    k_shade<true><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb);
-                else
-                    k_shade<false><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb);
+            // connection items: scan the per-slot counts, size the term buffers, one thread per item
+            for (int k = 0; k < 2; ++k) {
+                uint32_t* cnt = k == 0 ? BI.n_a : BI.n_b;
+                uint32_t* off = k == 0 ? BI.off_a : BI.off_b;
+                size_t tmp_bytes = 0;
+                HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, N, sm));
+                void* tmp = wbuf<char>(c, W_BD_SCAN, tmp_bytes, st);
+                if (st) return st;
+                HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, N, sm));
             }
+            k_bdpt_total<<<1, 64, 0, sm>>>(BI, N, items_total);
+            uint32_t totals[2] = {0, 0};
+            HIPCHK(hipMemcpyAsync(totals, items_total, sizeof(totals), hipMemcpyDeviceToHost, sm));
+            HIPCHK(hipStreamSynchronize(sm));
+            BI.term_a = wbuf<double>(c, W_BD_TERM, 4 * (size_t)std::max(totals[0], 1u), st);
+            BI.term_b = wbuf<double>(c, W_BD_TERMB, 4 * (size_t)std::max(totals[1], 1u), st);
+            BI.vis = wbuf<uint8_t>(c, W_BD_VIS, std::max(totals[1], 1u), st);
+            if (st) return st;
             {
                 StageTimer tm(c, g_timing, ST_SHADOW);
-                launch_trav(c, (uint64_t)ub * (uint32_t)ns, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
-                    k_shadow<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                        <<<grid, BLOCK, shm, sm>>>(c.sc, S);
-                });
+                if (totals[0] > 0)
+                    launch_trav(c, (uint64_t)totals[0], [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                        k_bdpt_conn_a<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
+                            <<<grid, BLOCK, shm, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                    });
+                if (totals[1] > 0)
+                    launch_trav(c, (uint64_t)totals[1], [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
+                        k_bdpt_vis<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
+                            <<<grid, BLOCK, shm, sm>>>(c.sc, S, B, BR, BI, N, items_total);
+                    });
+                if (totals[1] > 0) {
+                    const int grid = std::min(ceil_div(totals[1], BLOCK), 1 << 16);
+                    if (c.sc.full)
+                        k_bdpt_paths<true><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                    else
+                        k_bdpt_paths<false><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                }
+            }
+            {
+                StageTimer tm(c, g_timing, ST_RESOLVE);
+                k_bdpt_fold<<<gN, BLOCK, 0, sm>>>(S, B, BR, BI, N);
             }
             HIPCHK(hipGetLastError());
-            HIPCHK(hipMemcpyAsync(c.snap + CNT_N * (issued % Ctx::SNAP_RING), S.counts, sizeof(uint32_t) * CNT_N,
-                                  hipMemcpyDeviceToHost, sm));
-            HIPCHK(hipEventRecord(c.snap_ev[issued % Ctx::SNAP_RING], sm));
-            issued++;
-            std::swap(qa, qb);
-        }
-        while (consumed < issued) {  // trailing empty bounces
-            HIPCHK(hipEventSynchronize(c.snap_ev[consumed % Ctx::SNAP_RING]));
-            consumed++;
         }
         if (g_timing && bdpt) HIPCHK(hipStreamSynchronize(sm));  // BDPT passes have no bounce snapshots
         if (g_timing) resolve_timers(c);
