@@ -503,12 +503,13 @@ __device__ bool bdpt_visible(const DScene& sc, const BVtx& a, const BVtx& b, Cou
     return fabs(sqrt(rmax(distance_squared(xo, xi), 0.0)) - t) < EPSILON;
 }
 
-// bd_path_trace.rs:77-145 (t = 1): returns true with the splat
-template <int STK, bool FX>
-// `rs` is the lens sample the reference draws here (only for a non-delta ll; the caller draws it).
+// bd_path_trace.rs:77-145 (t = 1): returns true with the splat.  `rs` is the lens sample the
+// reference draws here (only for a non-delta ll; the caller draws it).  `trace(rx)` is
+// Scene::hit of the camera ray: done inline, or looked up from k_bdpt_trace_a.
+template <bool FX, typename Trace>
 __device__ bool connect_light_path(const DScene& sc, const DCam& cam, V2 rs, const double* L, const PView& lp,
-                                   int s, const BVtx& ll, V2* raster_out, DColor* color_out, Counters& C,
-                                   uint32_t& queries) {
+                                   int s, const BVtx& ll, V2* raster_out, DColor* color_out, uint32_t& queries,
+                                   Trace&& trace) {
     if (v_is_delta<FX>(sc, ll, L)) return false;
     const V3 xi = ll.p;
     Ray ri;
@@ -518,7 +519,7 @@ __device__ bool connect_light_path(const DScene& sc, const DCam& cam, V2 rs, con
     const double p_imp = cam_pdf_importance(cam, ri, xi);
     if (p_sct == 0.0 || p_imp == 0.0) return false;
     const RayX rx = rayx(ri);
-    const HitRef hr = scene_hit<STK, FX>(sc, rx, C);
+    const HitRef hr = trace(rx);
     queries += 1;
     if (hr.kind == 0) return false;
     DHit hc;
@@ -548,11 +549,12 @@ __device__ DColor add_camera_path(const DScene& sc, const DCam& cam, const doubl
     const PView none{nullptr, 0, nullptr};
     return rad * mis_weight<FX>(sc, cam, L, none, 0, cp, t);
 }
-template <int STK, bool FX>
-// `u`, `rs`: the light pick and light sample the reference draws here (only when cl is neither
-// delta nor on a light; the caller draws them).
+// bd_path_trace.rs:147-210 (s = 1).  `u`, `rs`: the light pick and light sample the reference
+// draws here (only when cl is neither delta nor on a light; the caller draws them).
+// `vis(rx, li)` is Scene::hit_light: the light triangle hit, or -1 when occluded / missed.
+template <bool FX, typename Vis>
 __device__ DColor connect_camera_path(const DScene& sc, const DCam& cam, double u, V2 rs, const double* L,
-                                      const PView& cp, int t, const BVtx& cl, Counters& C, uint32_t& queries) {
+                                      const PView& cp, int t, const BVtx& cl, uint32_t& queries, Vis&& vis) {
     if (v_is_delta<FX>(sc, cl, L) || cl.light >= 0) return cfill(0.0);
     const int li = sample_light(sc, u);
     const lumo_object& light = sc.lights[li];
@@ -563,9 +565,11 @@ __device__ DColor connect_camera_path(const DScene& sc, const DCam& cam, double 
     if (p_sct == 0.0) return cfill(0.0);
     const Ray ri = spawn(vtx_hit(cl), wi);
     const RayX rx = rayx(ri);
-    DHit hi;
     queries += 1;
-    if (!scene_hit_light<STK, FX>(sc, rx, li, hi, C)) return cfill(0.0);
+    const int tri = vis(rx, li);
+    if (tri == -1) return cfill(0.0);
+    DHit hi;
+    object_record<FX>(sc, light, tri, rx, hi);  // scene_hit_light's record of the visible light
     const V3 xi = hi.p;
     const V3 ngi = cl.blank ? wi : hi.ng;
     const double p_lig = light_pdf<FX>(sc, light, rx, xi, ngi) * pdf_light;
@@ -607,6 +611,8 @@ struct BItems {
     uint32_t *off_a, *off_b;  // exclusive scans
     double *term_a, *term_b;  // 4 per item
     uint8_t* vis;         // per (b) item: bdpt_visible
+    double* a_t;          // per (a) item: the traced hit (t = 1: Scene::hit; s = 1: a_tri = light triangle or -1)
+    int32_t *a_kind, *a_obj, *a_tri;
     double* pdf;          // running pdf_fwd of the walk
     int32_t* wdepth;      // index of the walk's last stored vertex
     double *cam_o, *cam_d;  // the camera ray, kept while the light subpath walks
@@ -919,14 +925,55 @@ __device__ __forceinline__ ItemSel item_store(const Bdpt& B, const Bdpt& R, int 
     return ri >= 0 ? ItemSel{slot, ri, &R} : ItemSel{slot, slot, &B};
 }
 
+// (a) items, traversal part: the camera ray of each t = 1 connection and the light ray of each
+// s = 1 connection, traced whenever the ray exists (before lumo's BSDF-pdf guards, which
+// k_bdpt_eval_a evaluates; a ray the guards reject is never read and not counted as a query).
 template <int STK, bool LDS, bool FX>
-__global__ __launch_bounds__(BLOCK) void k_bdpt_conn_a(DScene sc0, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n,
-                                                        const uint32_t* totals) {
+__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_trace_a(DScene sc0, Paths S, DCam cam, Bdpt B, Bdpt R,
+                                                                           BItems I, int n, const uint32_t* totals) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t total = totals[0];
     if (total <= blockIdx.x * blockDim.x) return;
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     Counters C{0, 0, 0};
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+        const int slot = item_slot(I.off_a, n, q);
+        const ItemSel e = item_store(B, R, slot);
+        const Bdpt& X = *e.X;
+        const int si = e.si;
+        const uint32_t j = q - I.off_a[slot];
+        const int Sl = I.nl[slot];
+        HitRef hr{DINF, 0, -1, -1};
+        if (j < (uint32_t)(Sl - 1)) {
+            const int s = (int)j + 2;
+            if (!(X.lp.I(2, s - 1, si) & VF_DELTA)) {
+                const V3 xi{X.lp.D(0, s - 1, si), X.lp.D(1, s - 1, si), X.lp.D(2, s - 1, si)};
+                Ray ri;
+                if (cam_sample_towards(cam, xi, V2{X.Dr(0, s - 2, si), X.Dr(1, s - 2, si)}, &ri))
+                    hr = scene_hit<STK, FX>(sc, rayx(ri), C);
+            }
+        } else if (j > (uint32_t)(Sl - 1)) {
+            const int t = (int)j - Sl + 2;
+            const BVtx cl = X.cp.load(t - 1, si);
+            if (!(cl.del || cl.light >= 0)) {
+                const int li = sample_light(sc, X.Dr(2, t - 2, si));
+                const V3 wi = light_sample_towards<FX>(sc, sc.lights[li], cl.p, V2{X.Dr(3, t - 2, si), X.Dr(4, t - 2, si)});
+                hr.tri = scene_hit_light_tri<STK, FX>(sc, rayx(spawn(vtx_hit(cl), wi)), li, C);
+            }
+        }
+        I.a_t[q] = hr.t;
+        I.a_kind[q] = hr.kind;
+        I.a_obj[q] = hr.obj;
+        I.a_tri[q] = hr.tri;
+    }
+    flush_counters(C, S.tcount + TC_N);
+}
+
+// (a) items, evaluation: lumo's connection code with the traces looked up
+template <bool FX>
+__global__ __launch_bounds__(BLOCK) void k_bdpt_eval_a(DScene sc, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n,
+                                                        const uint32_t* totals) {
+    const uint32_t total = totals[0];
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
         const int slot = item_slot(I.off_a, n, q);
         const ItemSel e = item_store(B, R, slot);
@@ -945,7 +992,9 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_conn_a(DScene sc0, Paths S, DCam
             const V2 rs = ll.del ? V2{0.0, 0.0} : V2{X.Dr(0, s - 2, si), X.Dr(1, s - 2, si)};
             V2 raster;
             DColor color;
-            const bool ok = connect_light_path<STK, FX>(sc, cam, rs, L, lp, s, ll, &raster, &color, C, queries);
+            const bool ok = connect_light_path<FX>(sc, cam, rs, L, lp, s, ll, &raster, &color, queries, [&](const RayX&) {
+                return HitRef{I.a_t[q], I.a_kind[q], I.a_obj[q], I.a_tri[q]};
+            });
             X.Ok(s - 2, si) = ok ? 1 : 0;
             if (ok) {
                 X.sp.D(0, s - 2, si) = raster.x;
@@ -960,12 +1009,12 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_conn_a(DScene sc0, Paths S, DCam
             const bool draws = !(cl.del || cl.light >= 0);
             const double u = draws ? X.Dr(2, t - 2, si) : 0.0;
             const V2 rs = draws ? V2{X.Dr(3, t - 2, si), X.Dr(4, t - 2, si)} : V2{0.0, 0.0};
-            term = connect_camera_path<STK, FX>(sc, cam, u, rs, L, cp, t, cl, C, queries);
+            term = connect_camera_path<FX>(sc, cam, u, rs, L, cp, t, cl, queries,
+                                           [&](const RayX&, int) { return I.a_tri[q]; });
         }
         for (int i = 0; i < NS; ++i) I.term_a[4 * (size_t)q + i] = term.s[i];
         if (queries) atomicAdd(&S.queries[slot], queries);
     }
-    flush_counters(C, S.tcount);
 }
 
 __device__ __forceinline__ void item_b_st(const BItems& I, int slot, uint32_t q, int& s, int& t) {

@@ -719,6 +719,20 @@ __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit
     return true;
 }
 
+// Scene::hit_light without the record: the light triangle (or PRIM_SPHERE) when visible, else -1;
+// object_record rebuilds the record (the same GEO test).
+template <int STK, bool FX>
+__device__ int scene_hit_light_tri(const DScene& sc, const RayX& r, int light, Counters& C) {
+    const lumo_object& L = sc.lights[light];
+    DHit lh;
+    const int tri = object_hit_tri<STK, FX>(sc, L, r, 0.0, DINF, C, lh);
+    if (tri == -1) return -1;
+    const double t_max = lh.t - EPSILON;
+    if (bvh_hit_t<STK, FX>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C) < t_max) return -1;
+    if (bvh_hit_t<STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C) < t_max) return -1;
+    return tri;
+}
+
 // ---------------------------------------------------------------- materials
 struct Onb {
     V3 u, v, w;

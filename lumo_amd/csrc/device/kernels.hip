@@ -847,7 +847,8 @@ enum WorkId {
     W_BD_LD, W_BD_LI, W_BD_CD, W_BD_CI, W_BD_SP, W_BD_SPN, W_BD_OVF, W_BD_CNT, W_BD_OFF, W_BD_RANGES, W_BD_TAPS,
     W_BD_FILM, W_BD_SCAN, W_BD_REDO_LIST, W_BD_REDO_INDEX, W_BDR_LD, W_BDR_LI, W_BDR_CD, W_BDR_CI, W_BDR_SP,
     W_BDR_SPN, W_BD_NL, W_BD_NC, W_BD_NITEMS, W_BD_IOFF, W_BD_DRAWS, W_BD_OK, W_BD_ITOTAL, W_BD_TERM, W_BD_PDF, W_BD_WDEPTH,
-    W_BD_CAMO, W_BD_CAMD, W_BD_RNG0, W_BD_LAM0, W_BDR_DRAWS, W_BDR_OK, W_BD_NB, W_BD_OFFB, W_BD_TERMB, W_BD_VIS, W_COUNT
+    W_BD_CAMO, W_BD_CAMD, W_BD_RNG0, W_BD_LAM0, W_BDR_DRAWS, W_BDR_OK, W_BD_NB, W_BD_OFFB, W_BD_TERMB, W_BD_VIS, W_BD_AT, W_BD_AKIND, W_BD_AOBJ,
+    W_BD_ATRI, W_COUNT
 };
 
 template <typename T>
@@ -1263,14 +1264,24 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             BI.term_a = wbuf<double>(c, W_BD_TERM, 4 * (size_t)std::max(totals[0], 1u), st);
             BI.term_b = wbuf<double>(c, W_BD_TERMB, 4 * (size_t)std::max(totals[1], 1u), st);
             BI.vis = wbuf<uint8_t>(c, W_BD_VIS, std::max(totals[1], 1u), st);
+            BI.a_t = wbuf<double>(c, W_BD_AT, std::max(totals[0], 1u), st);
+            BI.a_kind = wbuf<int32_t>(c, W_BD_AKIND, std::max(totals[0], 1u), st);
+            BI.a_obj = wbuf<int32_t>(c, W_BD_AOBJ, std::max(totals[0], 1u), st);
+            BI.a_tri = wbuf<int32_t>(c, W_BD_ATRI, std::max(totals[0], 1u), st);
             if (st) return st;
             {
                 StageTimer tm(c, g_timing, ST_SHADOW);
-                if (totals[0] > 0)
+                if (totals[0] > 0) {
                     launch_trav(c, (uint64_t)totals[0], [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
-                        k_bdpt_conn_a<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
+                        k_bdpt_trace_a<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
                             <<<grid, BLOCK, shm, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
                     });
+                    const int grid = std::min(ceil_div(totals[0], BLOCK), 1 << 16);
+                    if (c.sc.full)
+                        k_bdpt_eval_a<true><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                    else
+                        k_bdpt_eval_a<false><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                }
                 if (totals[1] > 0)
                     launch_trav(c, (uint64_t)totals[1], [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
                         k_bdpt_vis<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
