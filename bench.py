@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--res", type=int, default=None, help="square resolution override")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--max-paths", type=int, default=1 << 23, help="paths in flight per wavefront")
+    ap.add_argument("--max-vertices", type=int, default=0, help="BDPT vertex storage per subpath (0 = 64)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-tile-stride", type=int, default=32, help="CPU sample: every k-th tile of each batch")
     args = ap.parse_args()
@@ -87,7 +88,7 @@ def main():
         if wl.get("integrator") == L.Integrator.BDPathTrace:
             splat_film[:] = 0.0
             bufs, res = dev.render_tasks(mine_arr, max_paths=args.max_paths, integrator=L.Integrator.BDPathTrace,
-                                         splat_film=splat_film)
+                                         splat_film=splat_film, max_vertices=args.max_vertices)
         else:
             bufs, res = dev.render_tasks(mine_arr, max_paths=args.max_paths)
         return sum(r.num_queries for r in res), sum(r.num_camera_rays for r in res), sum(r.num_rays for r in res)

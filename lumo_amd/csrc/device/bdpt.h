@@ -16,7 +16,8 @@
 
 constexpr int BDPT_RR_DEPTH = 5, BDPT_MAX_DEPTH = 1024;  // path_gen.rs
 enum { TR_RADIANCE = 0, TR_IMPORTANCE = 1 };
-enum { VF_BLANK = 1, VF_BACKFACE = 2, VF_DELTA = 4 };  // VF_DELTA: Material::is_delta at L[0] (never changes)
+enum { VF_BLANK = 1, VF_BACKFACE = 2, VF_DELTA = 4 };
+constexpr int32_t REDO_DROPPED = -2;  // redo_index of a sample that overflowed a full redo list  // VF_DELTA: Material::is_delta at L[0] (never changes)
 constexpr int VD_N = 22, VI_N = 3;  // doubles / ints per stored vertex
 
 // A subpath vertex (vertex.rs).  `blank` marks the camera vertex (Material::Blank).
@@ -714,7 +715,7 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_light_init(DScene sc, Paths S, B
 __global__ __launch_bounds__(BLOCK) void k_bdpt_cam_init(Paths S, Bdpt B, BItems I, DCam cam, int n) {
     const int slot = blockIdx.x * blockDim.x + threadIdx.x;
     bool go = false;
-    if (slot < n && S.p_valid[slot] && B.redo_index[slot] < 0) {
+    if (slot < n && S.p_valid[slot] && B.redo_index[slot] == -1) {  // not re-run, not dropped
         go = true;
         const Ray r{ldv3(I.cam_o, slot), ldv3(I.cam_d, slot)};
         const double pdf_wi = cam_pdf_wi(cam, r);
@@ -759,7 +760,8 @@ __device__ void bdpt_step_one(const DScene& sc, const Paths& S, const Tasks& T, 
             if (pos < B.redo_cap) {
                 B.redo_list[pos] = slot;
                 B.redo_index[slot] = (int32_t)pos;
-            } else {
+            } else {  // the redo list is full: the sample is dropped and the render fails loudly
+                B.redo_index[slot] = REDO_DROPPED;
                 atomicOr(B.overflow, 1u);
             }
             return;
@@ -1083,6 +1085,11 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_paths(DScene sc, Paths S, DCam c
 __global__ __launch_bounds__(BLOCK) void k_bdpt_fold(Paths S, Bdpt B, Bdpt R, BItems I, int n) {
     const int slot = blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= n || !S.p_valid[slot]) return;
+    if (B.redo_index[slot] == REDO_DROPPED) {  // the render fails (overflow flag); keep the slot inert
+        stc(S.rad, slot, cfill(0.0));
+        B.sp.n[slot] = 0;
+        return;
+    }
     const ItemSel e = item_store(B, R, slot);
     const Bdpt& X = *e.X;
     const int si = e.si;

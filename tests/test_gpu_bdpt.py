@@ -113,3 +113,16 @@ def test_renderer_bdpt_image(dev):
     assert np.isfinite(img_b).all()
     mb, mp = img_b.mean(axis=(0, 1)), img_p.mean(axis=(0, 1))
     np.testing.assert_allclose(mb, mp, rtol=0.08)
+
+
+def test_bdpt_redo_list_overflow_fails_loudly(dev):
+    """More long samples in one pass than the redo list holds (4096): the call fails with
+    LUMO_ERR_UNSUPPORTED instead of truncating subpaths, and the context stays usable."""
+    sc, cam = _scene("cornell", (128, 64))
+    dev.upload(sc, cam)
+    tasks = L.make_tasks(128, 64, 1, 5)
+    film = np.zeros((64, 128, 3))
+    with pytest.raises(RuntimeError, match="UNSUPPORTED"):
+        dev.render_tasks(tasks, integrator=BDPT, splat_film=film, max_vertices=2)
+    bufs, _ = dev.render_tasks(tasks, integrator=BDPT, splat_film=film)
+    assert all(np.isfinite(b).all() for b in bufs)
