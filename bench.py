@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--res", type=int, default=None, help="square resolution override")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--max-paths", type=int, default=1 << 23, help="paths in flight per wavefront")
-    ap.add_argument("--max-vertices", type=int, default=0, help="BDPT vertex storage per subpath (0 = 64)")
+    ap.add_argument("--max-vertices", type=int, default=0, help="BDPT vertex storage per subpath (0 = 128)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-tile-stride", type=int, default=32, help="CPU sample: every k-th tile of each batch")
     args = ap.parse_args()

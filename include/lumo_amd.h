@@ -220,11 +220,12 @@ typedef struct {
     int32_t max_paths;  /* cap on paths in flight (0 = all pixels of the call) */
     int32_t tone_map;   /* LUMO_TONEMAP_* applied per sample before the film (task.rs:73-76)  */
     double tone_arg;    /* ToneMap::Clamp upper bound                                          */
-    /* BDPT only.  max_vertices: storage per subpath (0 = 64); a longer subpath fails the call
-     * with LUMO_ERR_UNSUPPORTED instead of truncating it.  splat_film: optional row-major
-     * width x height x 3 array; when a task's result has no `splats` list, its light-tracing
-     * taps are summed into it (film.rs:167-170; summation order unspecified, as lumo's tile
-     * completion order). */
+    /* BDPT only.  max_vertices: storage per subpath (0 = 128).  A sample whose subpath is longer
+     * is re-run with storage for lumo's maximum depth (1025); more than 4096 such samples in one
+     * pass fail the call with LUMO_ERR_UNSUPPORTED (never truncated).  splat_film: optional
+     * row-major width x height x 3 array; when a task's result has no `splats` list, its
+     * light-tracing taps are summed into it (film.rs:167-170; summation order unspecified, as
+     * lumo's tile completion order). */
     int32_t max_vertices, pad0;
     double* splat_film;
 } lumo_render_cfg;

@@ -1752,11 +1752,11 @@ lumo_status lumo_render_tiles(void* ctx, const lumo_tile_task* tasks, size_t n, 
     c->tone_map = cfg ? cfg->tone_map : LUMO_TONEMAP_NONE;
     c->tone_arg = cfg ? cfg->tone_arg : 0.0;
     c->integrator = cfg ? cfg->integrator : LUMO_INTEGRATOR_PATH_TRACE;
-    c->max_vertices = (cfg && cfg->max_vertices > 0) ? cfg->max_vertices : 64;
+    c->max_vertices = (cfg && cfg->max_vertices > 0) ? cfg->max_vertices : 128;
     c->splat_film = cfg ? cfg->splat_film : nullptr;
     size_t max_paths = (cfg && cfg->max_paths > 0) ? (size_t)cfg->max_paths : (size_t)1 << 30;
-    if (c->integrator == LUMO_INTEGRATOR_BDPT)  // vertex storage: ~30 KB per slot at 64 vertices
-        max_paths = std::min(max_paths, (size_t)(((size_t)1 << 20) * 64 / (size_t)c->max_vertices));
+    if (c->integrator == LUMO_INTEGRATOR_BDPT)  // BDPT storage: ~64 KB per slot at 128 vertices -> 64 GB
+        max_paths = std::min(max_paths, (size_t)(((size_t)1 << 27) / (size_t)c->max_vertices));
     size_t i = 0;
     while (i < n) {  // chunk the task list so that at most max_paths slots are in flight
         size_t j = i, paths = 0;
