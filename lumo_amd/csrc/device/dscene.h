@@ -70,7 +70,7 @@ struct DScene {
     const lumo_material* mats;
     const double* dense;
     const lumo_transform* xforms;
-    int32_t n_onodes, n_lnodes, n_lights, n_shadow, stack_class, full;
+    int32_t n_onodes, n_lnodes, n_lights, n_shadow, stack_class, full, n_objs, pad_n;
     // Traversal working set packed contiguously (16-B aligned sub-arrays) so that a small scene
     // can be staged into LDS once per workgroup; hot_bytes == 0 disables staging.
     const char* hot;

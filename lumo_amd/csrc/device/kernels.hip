@@ -52,7 +52,11 @@ constexpr int RR_DEPTH = 5;
 enum Stage { ST_CAMERA = 0, ST_CLOSEST, ST_SHADE, ST_SHADOW, ST_RESOLVE, ST_FINISH, ST_FILM, ST_RING, ST_COUNT };
 // Device-side queue counters: the bounce kernels read their counts from here, so the host never
 // waits for a count before launching the next stage.
-enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_N };
+enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_BUCKET0, CNT_N = CNT_BUCKET0 + 8 };
+// The resolve queue is split into NB buckets by the shadow rays' origin object so that a wave's
+// visibility queries start on the same surface and walk similar BVH / kd paths (LUMO_BUCKETS=0:
+// one bucket).  Bucket b holds its entries at rq[b * N ...]; k_shadow walks the buckets in order.
+constexpr int NB = 8;
 enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
 
 struct DCam {
@@ -134,6 +138,22 @@ __device__ __forceinline__ void block_append(bool pred, int32_t value, int32_t* 
     }
     __syncthreads();
     if (pred) queue[base_s + wtot[w] + prefix] = value;
+    __syncthreads();
+}
+
+// block_append into NB bucket segments of `queue` (stride `seg`): per-block LDS counters, one
+// global atomic per non-empty bucket per block.  Every thread of the block must call it.
+__device__ __forceinline__ void block_append_bucket(bool pred, int bucket, int32_t value, int32_t* queue, uint32_t seg,
+                                                    uint32_t* counters) {
+    __shared__ uint32_t cnt[NB], base_s[NB];
+    if (threadIdx.x < NB) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t local = 0;
+    if (pred) local = atomicAdd(&cnt[bucket], 1u);
+    __syncthreads();
+    if (threadIdx.x < NB) base_s[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(counters + threadIdx.x, cnt[threadIdx.x]) : 0u;
+    __syncthreads();
+    if (pred) queue[(size_t)bucket * seg + base_s[bucket] + local] = value;
     __syncthreads();
 }
 
@@ -407,7 +427,7 @@ __device__ __forceinline__ void shade_one(const DScene& sc, const Paths& S, cons
 
 template <bool FX>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue,
-                                                                    int32_t* next_queue) {
+                                                                    int32_t* next_queue, uint32_t seg, int buckets) {
     const uint32_t count = S.counts[CNT_CUR];
     // grid-stride over whole blocks: block_append needs every thread of the block each round
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
@@ -419,7 +439,12 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Pa
             shade_one<FX>(sc, S, T, s, alive, resolve);
         }
         block_append(alive, s, next_queue, S.counts + CNT_NEXT);
-        block_append(resolve, s, S.rq, S.counts + CNT_RESOLVE);
+        int b = 0;
+        if (resolve && buckets > 1) {  // origin object of the shadow rays (objects, then lights)
+            const int key = S.hit_kind[s] == 2 ? sc.n_objs + S.hit_obj[s] : S.hit_obj[s];
+            b = key < NB ? key : key % NB;
+        }
+        block_append_bucket(resolve, b, s, S.rq, seg, S.counts + CNT_BUCKET0);
     }
 }
 
@@ -455,10 +480,14 @@ __device__ __forceinline__ DColor shadow_record(const DScene& sc, const Paths& S
 // in LDS; the path's i == 0 thread then folds acc += gathered * single_i in i order and adds
 // acc / n_shadow to the radiance.  A block round covers BLOCK / n_shadow whole paths.
 template <int STK, bool LDS, bool FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0, Paths S) {
+__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0, Paths S, uint32_t seg) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     __shared__ DColor singles[BLOCK];
-    const uint32_t count = S.counts[CNT_RESOLVE];
+    uint32_t bc[NB], count = 0;
+    for (int b = 0; b < NB; ++b) {
+        bc[b] = S.counts[CNT_BUCKET0 + b];
+        count += bc[b];
+    }
     const int ns = sc0.n_shadow;
     const uint32_t per_block = (uint32_t)(BLOCK / ns);  // paths per block round
     if (count <= blockIdx.x * per_block) return;
@@ -470,7 +499,10 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0,
         const bool mine = threadIdx.x < per_block * ns && q < count;
         int s = -1;
         if (mine) {
-            s = S.rq[q];
+            uint32_t r = q;
+            int bk = 0;
+            while (r >= bc[bk]) r -= bc[bk++];  // q < count, so bk < NB
+            s = S.rq[(size_t)bk * seg + r];
             const int rec = s * 2 * ns + 2 * i;
             const DColor a = shadow_record<STK, LDS, FX>(sc, S, s, rec, C);
             const DColor b = (S.sh_flags[rec + 1] & 1) ? shadow_record<STK, LDS, FX>(sc, S, s, rec + 1, C) : cfill(0.0);
@@ -501,6 +533,7 @@ __global__ void k_bounce_begin(uint32_t* counts) {
         counts[CNT_CUR] = counts[CNT_NEXT];
         counts[CNT_NEXT] = 0;
         counts[CNT_RESOLVE] = 0;
+        for (int b = 0; b < NB; ++b) counts[CNT_BUCKET0 + b] = 0;
     }
 }
 
@@ -933,6 +966,7 @@ void by_stack_class(int cls, F&& f) {
 // Traversal launch: stack class x LDS staging.  With LDS staging the grid is capped (persistent
 // grid-stride loop) so each workgroup copies the packed scene once per launch.
 bool g_lds = true;
+int g_buckets = NB;  // LUMO_BUCKETS=0: a single resolve bucket
 template <typename F>
 void launch_trav(Ctx& c, uint64_t count, F&& f) {
     const bool lds = g_lds && c.sc.hot_bytes > 0;
@@ -1020,7 +1054,8 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     S.film = wbuf<double>(c, W_FILM, 4 * (size_t)N, st);
     S.q0 = wbuf<int32_t>(c, W_Q0, N, st);
     S.q1 = wbuf<int32_t>(c, W_Q1, N, st);
-    S.rq = wbuf<int32_t>(c, W_RQ, N, st);
+    const uint32_t rq_seg = (uint32_t)N;
+    S.rq = wbuf<int32_t>(c, W_RQ, (size_t)(g_buckets > 1 ? NB : 1) * N, st);
     S.counts = wbuf<uint32_t>(c, W_COUNTS, CNT_N, st);
     S.tcount = wbuf<unsigned long long>(c, W_TCOUNT, 2 * TC_N, st);
     Tasks T{};
@@ -1200,15 +1235,15 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 {
                     StageTimer tm(c, g_timing, ST_SHADE);
                     if (c.sc.full)
-                        k_shade<true><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb);
+                        k_shade<true><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb, rq_seg, g_buckets);
                     else
-                        k_shade<false><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb);
+                        k_shade<false><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb, rq_seg, g_buckets);
                 }
                 {
                     StageTimer tm(c, g_timing, ST_SHADOW);
                     launch_trav(c, (uint64_t)ub * (uint32_t)ns, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
                         k_shadow<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                            <<<grid, BLOCK, shm, sm>>>(c.sc, S);
+                            <<<grid, BLOCK, shm, sm>>>(c.sc, S, rq_seg);
                     });
                 }
             });
@@ -1472,6 +1507,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &h, sizeof(h));
     }
     if (const char* e = std::getenv("LUMO_LDS")) g_lds = e[0] != '0';
+    if (const char* e = std::getenv("LUMO_BUCKETS")) g_buckets = e[0] == '0' ? 1 : NB;
     if (const char* e = std::getenv("LUMO_LDS_GRID")) c->lds_grid_cap = std::max(1, std::atoi(e));
     const char* tm = std::getenv("LUMO_TIMING");
     g_timing = tm && tm[0] == '1';
@@ -1594,6 +1630,7 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     s.n_onodes = d->num_object_nodes;
     s.n_lnodes = d->num_light_nodes;
     s.n_lights = d->num_lights;
+    s.n_objs = d->num_objects;
     {   // packed traversal set for LDS staging (scenes up to 48 KiB)
         std::vector<char> hot;
         auto put = [&](const void* p, size_t bytes) -> uint32_t {
