@@ -126,7 +126,8 @@ def main():
         q, cams, rays = (float(x) for x in s.tolist())
 
     if rank == 0:
-        roof = roofline(st, n_shadow_rays(scene), bdpt=wl.get("integrator") == L.Integrator.BDPathTrace)
+        roof = roofline(st, n_shadow_rays(scene), bdpt=wl.get("integrator") == L.Integrator.BDPathTrace,
+                        workload=args.config)
         cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl) if (args.cpu_baseline and ws == 1) else None
         value = q / elapsed / 1e6
         out = {
@@ -207,7 +208,7 @@ def build_config(args):
     return scene, cam, (W, H), spp, wl
 
 
-def roofline(st, n_shadow, bdpt=False):
+def roofline(st, n_shadow, bdpt=False, workload="c1"):
     """Dominant-kernel roofline from live per-launch HIP-event times and traversal counters."""
     ms = list(st.kernel_ms)
     launches = list(st.launches)
@@ -234,7 +235,7 @@ def roofline(st, n_shadow, bdpt=False):
         per_stage = {bd_names.get(k, k): v for k, v in per_stage.items()}
     kname = {"closest": "k_closest", "shade": "k_bdpt_step", "shadow": "k_bdpt_vis",
              "resolve": "k_bdpt_redo"}.get(name, f"k_{name}") if bdpt else f"k_{name}"
-    pmc = pmc_traffic(kname[2:])
+    pmc = pmc_traffic(kname[2:]) if workload == "c1" else {}  # the committed PMC table profiles C1
     out = {"bound": "hbm", "kernel": kname, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "traffic": pmc.get("hbm_bytes_per_launch"), "traffic_raw": pmc.get("hbm_bytes_per_launch_raw"),
            "traffic_source": "profiles/pmc_traffic.json" if pmc else None, "stages": per_stage}
