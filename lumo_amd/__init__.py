@@ -502,6 +502,25 @@ class Device:
             check(L.lumo_camera_set(self.ctx, C.byref(camera.desc)), "camera set")
         self.scene = scene
 
+    @staticmethod
+    def _result_buffers(arr, n):
+        """Per-task {Σw·rgb, Σw} buffers (4 f64 per tile pixel) as views of one allocation, with
+        the lumo_tile_result array pointing at them.  Vectorised over the task array's fields
+        (all u64): a per-task Python loop cost ~0.2 s per 16k-task frame, inside the timed step."""
+        res = (_ffi.TileResult * n)()
+        if n == 0:
+            return [], [], res
+        tv = np.frombuffer(arr, dtype=np.uint64).reshape(n, C.sizeof(_ffi.TileTask) // 8)
+        if (tv[:, 2] < tv[:, 0]).any() or (tv[:, 3] < tv[:, 1]).any():
+            raise ValueError("tile task with px_max < px_min")
+        P = ((tv[:, 2] - tv[:, 0]) * (tv[:, 3] - tv[:, 1])).astype(np.int64)
+        off = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(4 * P, out=off[1:])
+        big = np.zeros(int(off[-1]), dtype=np.float64)
+        rv = np.frombuffer(res, dtype=np.uint64).reshape(n, C.sizeof(_ffi.TileResult) // 8)
+        rv[:, 0] = np.uint64(big.ctypes.data) + 8 * off[:-1].astype(np.uint64)
+        return np.split(big, off[1:-1]), [], res
+
     def render_tasks(self, tasks, max_paths=0, tone_map=None, integrator=0, splats_out=None, splat_film=None,
                      max_vertices=0):
         """lumo_render_tiles over `tasks`; returns per-task (rgb_w array, result).
@@ -520,13 +539,9 @@ class Device:
         caps = [16 * (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1]) * t.samples if lists else 0
                 for t in arr]
         while True:
-            bufs, sbufs, res = [], [], (_ffi.TileResult * n)()
-            for i, t in enumerate(arr):
-                P = (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1])
-                b = np.zeros(4 * P, dtype=np.float64)
-                bufs.append(b)
-                res[i].rgb_w = b.ctypes.data_as(_ffi.c_double_p)
-                if lists:
+            bufs, sbufs, res = self._result_buffers(arr, n)
+            if lists:
+                for i in range(n):
                     sb = (_ffi.Splat * max(caps[i], 1))()
                     sbufs.append(sb)
                     res[i].splats = sb

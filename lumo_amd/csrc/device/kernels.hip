@@ -1390,9 +1390,15 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         }
     }
     // results
-    std::vector<double> film((size_t)4 * N);
+    // Per-task {sum w*rgb, sum w} tiles: straight into the caller's buffers when they are laid out
+    // back to back in slot order (the Python wrapper allocates them so), else via a host copy.
+    bool direct = out != nullptr && n_tasks > 0 && out[0].rgb_w != nullptr;
+    for (size_t i = 1; i < n_tasks && direct; ++i)
+        direct = out[i].rgb_w == out[0].rgb_w + 4 * (size_t)first[i];
+    std::vector<double> film(direct ? 0 : (size_t)4 * N);
     std::vector<unsigned long long> rays(n_tasks), queries(n_tasks);
-    HIPCHK(hipMemcpyAsync(film.data(), S.film, sizeof(double) * 4 * N, hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipMemcpyAsync(direct ? out[0].rgb_w : film.data(), S.film, sizeof(double) * 4 * N, hipMemcpyDeviceToHost,
+                          sm));
     HIPCHK(hipMemcpyAsync(rays.data(), T.num_rays, sizeof(unsigned long long) * n_tasks, hipMemcpyDeviceToHost, sm));
     HIPCHK(hipMemcpyAsync(queries.data(), T.queries, sizeof(unsigned long long) * n_tasks, hipMemcpyDeviceToHost,
                           sm));
@@ -1427,7 +1433,8 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         if (!out) break;
         const lumo_tile_task& t = tasks[i];
         const size_t P = (size_t)(first[i + 1] - first[i]);
-        if (out[i].rgb_w) std::memcpy(out[i].rgb_w, film.data() + 4 * (size_t)first[i], sizeof(double) * 4 * P);
+        if (out[i].rgb_w && !direct)
+            std::memcpy(out[i].rgb_w, film.data() + 4 * (size_t)first[i], sizeof(double) * 4 * P);
         out[i].num_camera_rays = P * t.samples;
         out[i].num_rays = rays[i];
         out[i].num_queries = queries[i];
