@@ -556,16 +556,14 @@ __device__ __forceinline__ V3 sample_rgb(const DScene& sc, const DCam& cam, cons
     return m3_mul_vec(cam.x2r, m3_mul_vec(cam.wb, color_xyz(sc, tc, L)));
 }
 
-__global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, int n, uint32_t pass, Dump dump,
-                                                   int dump_p, int tone_map, double tone_arg) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n || !S.p_valid[s]) return;
+// Per sample: luminance and cost for the ring, tone map -> XYZ -> WB -> RGB for the film.
+__device__ __forceinline__ V3 finish_one(const DScene& sc, const Paths& S, const DCam& cam, int s, uint32_t pass,
+                                         const Dump& dump, int dump_p, int tone_map, double tone_arg) {
     double L[NS];
     for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
     const DColor c = ldc(S.rad, s);
     const double lum = luminance(sc, c, L);
     const V3 rgb = sample_rgb(sc, cam, c, L, tone_map, tone_arg);
-    stv3(S.p_rgb, s, rgb);
     S.p_lum[s] = lum;
     S.p_cost[s] = S.depth[s];
     if (dump.rad) {
@@ -578,24 +576,29 @@ __global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, 
         dump.raster[2 * o + 1] = S.raster[2 * s + 1];
         dump.depth[o] = S.depth[s];
     }
+    return rgb;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, int n, uint32_t pass, Dump dump,
+                                                   int dump_p, int tone_map, double tone_arg) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n || !S.p_valid[s]) return;
+    stv3(S.p_rgb, s, finish_one(sc, S, cam, s, pass, dump, dump_p, tone_map, tone_arg));
 }
 
 __device__ __forceinline__ double gauss(double x, double sigma) {
     return lm_exp(-(x * x) / (2.0 * sigma * sigma)) / sqrt(rmax(2.0 * PI * sigma * sigma, 0.0));
 }
 
-// FilmTile::add_sample as a gather: destination pixel d receives, in source raster order, the
-// samples whose (tile-clipped) 3x3 footprint contains d.  Sources farther than 2 px cannot.
-__global__ __launch_bounds__(BLOCK) void k_film(Paths S, Tasks T, DCam cam, int n) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
-    const int ti = S.task[s];
-    const lumo_tile_task& t = T.t[ti];
+// FilmTile::add_sample as a gather: destination pixel j of task t (slot s) receives, in source
+// raster order, the samples whose (tile-clipped) 3x3 footprint contains it.  Sources farther
+// than 2 px cannot.  `src` reads a source sample by its pixel index within the tile.
+template <class Src>
+__device__ __forceinline__ void film_gather(const Paths& S, const lumo_tile_task& t, const DCam& cam, int s, int j,
+                                            const Src& src) {
     const int W = (int)(t.px_max[0] - t.px_min[0]), H = (int)(t.px_max[1] - t.px_min[1]);
-    const int j = S.pix[s];
     const int dx = j % W, dy = j / W;
     const uint64_t gx = t.px_min[0] + dx, gy = t.px_min[1] + dy;
-    const int first = T.first[ti];
     const uint64_t r = (uint64_t)ceil(cam.fr - 0.5);
     double acc[4] = {S.film[4 * s], S.film[4 * s + 1], S.film[4 * s + 2], S.film[4 * s + 3]};
     const double gr = gauss(cam.fr, cam.fsig);
@@ -603,9 +606,9 @@ __global__ __launch_bounds__(BLOCK) void k_film(Paths S, Tasks T, DCam cam, int 
         if (sy < 0 || sy >= H) continue;
         for (int sx = dx - 2; sx <= dx + 1; ++sx) {
             if (sx < 0 || sx >= W) continue;
-            const int src = first + sy * W + sx;
-            if (!S.p_valid[src]) continue;
-            const double rx = S.raster[2 * src], ry = S.raster[2 * src + 1];
+            const int k = sy * W + sx;
+            if (!src.valid(k)) continue;
+            const double rx = src.rx(k), ry = src.ry(k);
             const uint64_t px = rx > 0.0 ? (uint64_t)floor(rx) : 0, py = ry > 0.0 ? (uint64_t)floor(ry) : 0;
             const uint64_t mix = std::max(px >= r ? px - r : 0, t.px_min[0]);
             const uint64_t miy = std::max(py >= r ? py - r : 0, t.px_min[1]);
@@ -614,7 +617,7 @@ __global__ __launch_bounds__(BLOCK) void k_film(Paths S, Tasks T, DCam cam, int 
             const double vx = rx - (0.5 + (double)gx), vy = ry - (0.5 + (double)gy);
             const double w = rmax(gauss(vx, cam.fsig) - gr, 0.0) * rmax(gauss(vy, cam.fsig) - gr, 0.0);
             if (w != 0.0) {
-                const V3 c = ldv3(S.p_rgb, src) * w;
+                const V3 c = src.rgb(k) * w;
                 acc[0] += c.x;
                 acc[1] += c.y;
                 acc[2] += c.z;
@@ -623,6 +626,61 @@ __global__ __launch_bounds__(BLOCK) void k_film(Paths S, Tasks T, DCam cam, int 
         }
     }
     for (int i = 0; i < 4; ++i) S.film[4 * s + i] = acc[i];
+}
+
+struct HbmSrc {  // sources read from the per-slot buffers k_finish wrote
+    const Paths& S;
+    int first;
+    __device__ bool valid(int k) const { return S.p_valid[first + k] != 0; }
+    __device__ double rx(int k) const { return S.raster[2 * (first + k)]; }
+    __device__ double ry(int k) const { return S.raster[2 * (first + k) + 1]; }
+    __device__ V3 rgb(int k) const { return ldv3(S.p_rgb, first + k); }
+};
+
+__global__ __launch_bounds__(BLOCK) void k_film(Paths S, Tasks T, DCam cam, int n) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const int ti = S.task[s];
+    film_gather(S, T.t[ti], cam, s, S.pix[s], HbmSrc{S, T.first[ti]});
+}
+
+struct LdsSrc {  // sources staged in LDS by k_finish_film
+    const double* rgb_;
+    const double* ras;
+    const uint32_t* ok;
+    __device__ bool valid(int k) const { return ok[k] != 0; }
+    __device__ double rx(int k) const { return ras[2 * k]; }
+    __device__ double ry(int k) const { return ras[2 * k + 1]; }
+    __device__ V3 rgb(int k) const { return V3{rgb_[3 * k], rgb_[3 * k + 1], rgb_[3 * k + 2]}; }
+};
+
+// k_finish + k_film for tasks of at most BLOCK pixels (lumo's 16x16 tiles): one block per task,
+// the tile's sample RGB and raster positions staged in LDS instead of a round trip through HBM.
+// Same arithmetic as the two kernels, so the film is bit-identical.
+__global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S, Tasks T, DCam cam, uint32_t pass, Dump dump,
+                                                        int dump_p, int tone_map, double tone_arg) {
+    __shared__ double l_rgb[3 * BLOCK];
+    __shared__ double l_ras[2 * BLOCK];
+    __shared__ uint32_t l_ok[BLOCK];
+    const int ti = blockIdx.x;
+    const int first = T.first[ti];
+    const int P = T.first[ti + 1] - first;
+    const int j = threadIdx.x;
+    const int s = first + j;
+    if (j < P) {
+        const bool ok = S.p_valid[s] != 0;
+        l_ok[j] = ok ? 1u : 0u;
+        if (ok) {
+            const V3 rgb = finish_one(sc, S, cam, s, pass, dump, dump_p, tone_map, tone_arg);
+            l_rgb[3 * j] = rgb.x;
+            l_rgb[3 * j + 1] = rgb.y;
+            l_rgb[3 * j + 2] = rgb.z;
+            l_ras[2 * j] = S.raster[2 * s];
+            l_ras[2 * j + 1] = S.raster[2 * s + 1];
+        }
+    }
+    __syncthreads();
+    if (j < P) film_gather(S, T.t[ti], cam, s, j, LdsSrc{l_rgb, l_ras, l_ok});
 }
 
 // task.rs:42-53 + 64-69: ring update in pixel order, then delta for the next pass.
@@ -992,7 +1050,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     if (n_tasks == 0) return LUMO_OK;
     // slots
     std::vector<int32_t> first(n_tasks + 1), task_of, pix_of;
-    uint64_t max_total = 1, max_samples = 0;
+    uint64_t max_total = 1, max_samples = 0, max_P = 0;
     for (size_t i = 0; i < n_tasks; ++i) {
         const lumo_tile_task& t = tasks[i];
         if (!(t.px_max[0] > t.px_min[0] && t.px_max[1] > t.px_min[1]) || t.samples == 0 ||
@@ -1000,6 +1058,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             t.px_max[0] > (uint64_t)1 << 31 || t.px_max[1] > (uint64_t)1 << 31)
             return LUMO_ERR_INVALID;
         const uint64_t P = (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1]);
+        max_P = std::max(max_P, P);
         first[i] = (int32_t)task_of.size();
         for (uint64_t j = 0; j < P; ++j) {
             task_of.push_back((int32_t)i);
@@ -1338,13 +1397,19 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         }
         if (g_timing && bdpt) HIPCHK(hipStreamSynchronize(sm));  // BDPT passes have no bounce snapshots
         if (g_timing) resolve_timers(c);
-        {
-            StageTimer tm(c, g_timing, ST_FINISH);
-            k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, S, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg);
-        }
-        {
+        if (max_P <= BLOCK) {  // one block per tile (lumo's 16x16 tiles)
             StageTimer tm(c, g_timing, ST_FILM);
-            k_film<<<gN, BLOCK, 0, sm>>>(S, T, c.cam, N);
+            k_finish_film<<<(int)n_tasks, BLOCK, 0, sm>>>(c.sc, S, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
+                                                          c.tone_arg);
+        } else {
+            {
+                StageTimer tm(c, g_timing, ST_FINISH);
+                k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, S, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg);
+            }
+            {
+                StageTimer tm(c, g_timing, ST_FILM);
+                k_film<<<gN, BLOCK, 0, sm>>>(S, T, c.cam, N);
+            }
         }
         {
             StageTimer tm(c, g_timing, ST_RING);

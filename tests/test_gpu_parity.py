@@ -55,6 +55,22 @@ def test_tiles_match_oracle(dev, cornell):
         assert r.num_queries == orr.num_queries
 
 
+def test_large_tiles_match_oracle(dev, cornell):
+    """Tasks of more than 256 pixels (32x48 tiles) take the unfused finish + film kernels; lumo's
+    16x16 tiles take the fused per-tile kernel.  Both are held to the oracle bit for bit."""
+    from lumo_amd import _ffi
+    cam = L.Camera.cornell_box((64, 48))
+    dev.upload(cornell, cam)
+    seeds = [t.seed for t in L.make_tasks(64, 48, 4, SEED)]
+    tasks = (_ffi.TileTask * 2)(*[_ffi.TileTask((32 * i, 0), (32 * i + 32, 48), 0, 4, 4, seeds[i]) for i in range(2)])
+    bufs, res = dev.render_tasks(tasks)
+    obufs, ores, _ = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, 2)
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        assert b.shape == (4 * 32 * 48,)
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+
+
 def test_multi_batch_tiles_match_oracle(dev, cornell):
     """Two 256-spp batches + a ragged 44-spp batch (ring buffer wrap, RR delta in use) on a
     ragged frame (tiles clipped at the right/bottom edge)."""
