@@ -14,8 +14,12 @@ HIPFLAGS := -O3 -std=c++17 -fPIC $(FPFLAGS) --offload-arch=$(ARCH) -Wall -Wno-un
 
 HOST_SRC := $(wildcard lumo_amd/csrc/host/*.cpp)
 HOST_OBJ := $(patsubst lumo_amd/csrc/host/%.cpp,build/host/%.o,$(HOST_SRC))
-DEV_SRC  := $(wildcard lumo_amd/csrc/device/*.hip)
-DEV_OBJ  := $(patsubst lumo_amd/csrc/device/%.hip,build/device/%.o,$(DEV_SRC))
+# kernels.hip: host orchestration, C ABI and the non-traversal kernels.  The traversal kernels
+# are instantiated once per kd stack class (launch.h STACK_CLASSES) in their own translation
+# units, so they compile in parallel: inst_pt.hip / inst_bd.hip built with -DLUMO_STK=<class>.
+STK_CLASSES := 4 8 16 24 32 48 64
+DEV_OBJ  := build/device/kernels.o $(foreach k,$(STK_CLASSES),build/device/inst_pt_$(k).o build/device/inst_bd_$(k).o)
+DEV_H    := $(wildcard lumo_amd/csrc/device/*.h)
 COMMON_H := $(wildcard lumo_amd/csrc/common/*.h) include/lumo_amd.h include/lumo_host.h
 
 LIB      := lumo_amd/liblumo_amd.so
@@ -28,9 +32,17 @@ build/host/%.o: lumo_amd/csrc/host/%.cpp $(COMMON_H) $(wildcard lumo_amd/csrc/ho
 	@mkdir -p build/host
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-build/device/%.o: lumo_amd/csrc/device/%.hip $(COMMON_H) $(wildcard lumo_amd/csrc/device/*.h)
+build/device/kernels.o: lumo_amd/csrc/device/kernels.hip $(COMMON_H) $(DEV_H)
 	@mkdir -p build/device
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -c $< -o $@
+
+build/device/inst_pt_%.o: lumo_amd/csrc/device/inst_pt.hip $(COMMON_H) $(DEV_H)
+	@mkdir -p build/device
+	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -DLUMO_STK=$* -c $< -o $@
+
+build/device/inst_bd_%.o: lumo_amd/csrc/device/inst_bd.hip $(COMMON_H) $(DEV_H)
+	@mkdir -p build/device
+	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -DLUMO_STK=$* -c $< -o $@
 
 $(LIB): $(HOST_OBJ) $(DEV_OBJ)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -lpthread
@@ -43,15 +55,9 @@ $(ORACLE_G): oracle/src/oracle.cpp oracle/oracle.h $(COMMON_H)
 	@mkdir -p oracle/_build
 	$(CXX) $(CXXFLAGS) -O2 -DLUMO_ORACLE_GLIBC -shared -o $@ oracle/src/oracle.cpp -lpthread
 
-# A/B variants of the device code (perf experiments): lumo_amd/liblumo_amd_<name>.so
-VARIANTS ?= lb4:-DLUMO_TRAVERSAL_WAVES=4 noinl:-DLUMO_NOINLINE_KD
-variants: $(HOST_OBJ)
-	@for v in $(VARIANTS); do n=$${v%%:*}; f=$${v#*:}; f=$$(echo $$f | tr ',' ' '); \
-	  echo "variant $$n: $$f"; \
-	  $(HIPCC) $(HIPFLAGS) $$f -c lumo_amd/csrc/device/kernels.hip -o build/device/kernels_$$n.o && \
-	  $(HIPCC) -shared --offload-arch=$(ARCH) -o lumo_amd/liblumo_amd_$$n.so $(HOST_OBJ) build/device/kernels_$$n.o -lpthread; done
+# DEVFLAGS: extra device defines for A/B builds, e.g. make DEVFLAGS=-DLUMO_TRAVERSAL_WAVES=4
 
 clean:
 	rm -rf build $(LIB) oracle/_build
 
-.PHONY: all clean variants
+.PHONY: all clean

@@ -1,21 +1,28 @@
 #!/usr/bin/env python3
-"""Benchmark: lumo's Cornell box, PathTrace, 1024x1024 @ 1024 spp (BASELINE.json configs[1]).
+"""Benchmark: BASELINE.json's metric, "Mrays/sec + Msamples/sec ... Cornell 1024spp and Bistro 256spp".
 
-One "step" = the full C1 render: every (256-spp batch, 16x16 tile) RenderTask of the frame
-(renderer.rs:179-204), 4 batches x 4096 tiles = 1.07e9 camera paths.  With N ranks (one per GPU,
-launched by torch.distributed.run) the tasks are sharded by tile index (tile % N == rank), the
-scene is replicated, and no collective touches the data path; only the timing barrier and the
-final max/sum reductions use the process group.
+Default run (the driver's `python bench.py --gpus N --steps K --warmup W`):
+  * C1 = BASELINE configs[1]: lumo's Cornell box, PathTrace, 1024x1024 @ 1024 spp.  One "step" is
+    the whole frame: every (256-spp batch, 16x16 tile) RenderTask (renderer.rs:179-204),
+    4 batches x 4096 tiles = 1.07e9 camera paths.  W warmup frames, then K timed frames.  These
+    are the top-level fields of the JSON line.
+  * C3 = BASELINE configs[3]: the Bistro stand-in, PathTrace, 1920x1080 @ 256 spp, one timed
+    frame after a 1-spp warmup frame (`--bistro-frames`, 0 disables).  Reported under "c3" with
+    its own ms_per_step, roofline and CPU baseline.
+With N ranks (one per GPU, launched by torch.distributed.run) the tasks are sharded by tile index
+(tile % N == rank, all batches of a tile on one rank), the scene is replicated, and no collective
+touches the data path; only the timing barriers and the final max/sum of scalars use the group.
 
-Prints ONE JSON line (rank 0).  `value` is whole-job Mrays/s = (closest-hit + shadow-visibility
-queries of all ranks) / max-over-ranks wall time of the K timed steps.  Also reported:
-Msamples/s (camera paths), lumo's own "total rays" rate (sum of path depths, task.rs:65), the
-roofline of the dominant kernel (algorithmic bytes from the kernels' own traversal counters over
-live HIP-event kernel time), and the CPU baseline (the f64 oracle in lumo's tile-serial order on
-this host's cores, on a bounded sample of the same frame).
+`value` is whole-job Mrays/s = (closest-hit + shadow-visibility queries of all ranks) / max-over-
+ranks wall time of the timed frames.  Also reported: Msamples/s (camera paths), lumo's own "total
+rays" rate (sum of path depths, task.rs:65), the roofline of the dominant kernel (algorithmic
+bytes from the kernels' own traversal counters over live HIP-event kernel time, DESIGN.md
+§Roofline), and the CPU baseline (the f64 oracle in lumo's tile-serial order on this host's
+cores, on a bounded sample of the same frame, at all usable cores and at lumo's default 4).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -31,7 +38,8 @@ SEED = 0x5EED_1234
 B_AABB, B_KD, B_TRI = 48, 16, 84           # slab test bounds; kd split node; 3 vertices + indices
 B_CLOSEST_IO = 48 + 20  # ray in + hit out
 B_RECORD, B_FOLD = 104, 104  # shadow record in; per path: gathered + pdf_light + radiance read/write
-STAGES = ["camera", "closest", "shade", "shadow", "resolve", "finish", "film", "ring"]
+B_CONN_IO = 104  # BDPT connection query: the two vertices' position / error / normal in, result out
+LUMO_DEFAULT_THREADS = 4  # renderer.rs:21
 
 
 def dist_env():
@@ -52,16 +60,16 @@ def main():
                          "c4 caustics.rs BDPT 1024^2@4096 (configs[4])")
     ap.add_argument("--res", type=int, default=None, help="square resolution override")
     ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--bistro-frames", type=int, default=1,
+                    help="with --config c1: also time this many C3 Bistro frames at 1920x1080@256 (0: skip)")
+    ap.add_argument("--bistro-spp", type=int, default=256)
     ap.add_argument("--max-paths", type=int, default=1 << 23, help="paths in flight per wavefront")
     ap.add_argument("--max-vertices", type=int, default=0, help="BDPT vertex storage per subpath (0 = 128)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
-    ap.add_argument("--cpu-tile-stride", type=int, default=32, help="CPU sample: every k-th tile of each batch")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU work per baseline run")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
-    import lumo_amd as L
-    from lumo_amd import _ffi
-
     pg = None
     if ws > 1:
         import torch
@@ -72,26 +80,55 @@ def main():
         dist.init_process_group(backend=backend)
         pg = dist
 
-    scene, cam, (W, H), spp, wl = build_config(args)
-    tasks = L.make_tasks(W, H, spp, SEED)
+    main_res = run(args.config, args, ws, rank, local, pg, steps=args.steps, warmup=args.warmup,
+                   res=args.res, spp=args.spp)
+    c3 = None
+    if args.config == "c1" and args.bistro_frames > 0:
+        c3 = run("c3", args, ws, rank, local, pg, steps=args.bistro_frames, warmup=1, spp=args.bistro_spp,
+                 warm_spp=1)
+    if rank == 0:
+        out = main_res
+        if c3 is not None:
+            out["c3"] = {k: c3[k] for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype",
+                                            "data", "config", "msamples_per_s", "lumo_total_rays_per_s_M",
+                                            "queries_per_step", "scene_build_s", "sample_checks", "roofline",
+                                            "cpu_baseline")}
+        print(json.dumps(out))
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, warm_spp=None):
+    """Render `steps` timed frames of `config` (after `warmup` frames, at `warm_spp` if given) and
+    return the JSON record (rank 0 fields complete)."""
+    import lumo_amd as L
+    from lumo_amd import _ffi
     from lumo_amd.dist import shard_tasks, tiles_per_batch
+
+    scene, cam, (W, H), spp, wl = build_config(config, res, spp)
+    bdpt = wl.get("integrator") == L.Integrator.BDPathTrace
+    tasks = L.make_tasks(W, H, spp, SEED)
     tiles = tiles_per_batch(W, H)
     mine = shard_tasks(tasks, W, H, rank, ws)
     mine_arr = (_ffi.TileTask * len(mine))(*mine)
+    warm_arr = mine_arr
+    if warm_spp is not None:
+        wt = shard_tasks(L.make_tasks(W, H, warm_spp, SEED), W, H, rank, ws)
+        warm_arr = (_ffi.TileTask * len(wt))(*wt)
 
-    splat_film = np.zeros((H, W, 3)) if wl.get("integrator") == L.Integrator.BDPathTrace else None
+    splat_film = np.zeros((H, W, 3)) if bdpt else None
     dev = L.Device(local)
     dev.upload(scene, cam)
     lib = _ffi.load()
 
-    def step():
-        if wl.get("integrator") == L.Integrator.BDPathTrace:
+    def step(arr):
+        if bdpt:
             splat_film[:] = 0.0
-            bufs, res = dev.render_tasks(mine_arr, max_paths=args.max_paths, integrator=L.Integrator.BDPathTrace,
-                                         splat_film=splat_film, max_vertices=args.max_vertices)
+            bufs, res_ = dev.render_tasks(arr, max_paths=args.max_paths, integrator=L.Integrator.BDPathTrace,
+                                          splat_film=splat_film, max_vertices=args.max_vertices)
         else:
-            bufs, res = dev.render_tasks(mine_arr, max_paths=args.max_paths)
-        return sum(r.num_queries for r in res), sum(r.num_camera_rays for r in res), sum(r.num_rays for r in res)
+            bufs, res_ = dev.render_tasks(arr, max_paths=args.max_paths)
+        return sum(r.num_queries for r in res_), sum(r.num_camera_rays for r in res_), sum(r.num_rays for r in res_)
 
     def barrier():
         if pg is not None:
@@ -100,20 +137,21 @@ def main():
                 torch.cuda.synchronize()
             pg.barrier()
 
-    for _ in range(args.warmup):
-        step()
+    for _ in range(warmup):
+        step(warm_arr)
     lib.lumo_set_timing(1)
     lib.lumo_stats_reset(dev.ctx)
     barrier()
     t0 = time.perf_counter()
     q = cams = rays = 0
-    for _ in range(args.steps):
-        a, b, c = step()
+    for _ in range(steps):
+        a, b, c = step(mine_arr)
         q, cams, rays = q + a, cams + b, rays + c
     barrier()  # lumo_render_tiles returns only after its stream has drained
     elapsed = time.perf_counter() - t0
     lib.lumo_set_timing(0)
     st = dev.stats()
+    checks = [st.samples_nan, st.samples_neg, st.samples_large]
 
     if pg is not None:
         import torch
@@ -121,23 +159,24 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
         elapsed = float(t.item())
-        s = torch.tensor([q, cams, rays], dtype=torch.float64, device=dev_t)
+        s = torch.tensor([q, cams, rays] + checks, dtype=torch.float64, device=dev_t)
         pg.all_reduce(s, op=pg.ReduceOp.SUM)
-        q, cams, rays = (float(x) for x in s.tolist())
+        q, cams, rays = (float(x) for x in s.tolist()[:3])
+        checks = [int(x) for x in s.tolist()[3:]]
+    dev.close()
 
+    out = None
     if rank == 0:
-        roof = roofline(st, n_shadow_rays(scene), bdpt=wl.get("integrator") == L.Integrator.BDPathTrace,
-                        workload=args.config)
+        roof = roofline(st, n_shadow_rays(scene), bdpt=bdpt, workload=config)
         cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl) if (args.cpu_baseline and ws == 1) else None
-        value = q / elapsed / 1e6
         out = {
             "metric": "Mrays/s",
-            "value": round(value, 3),
+            "value": round(q / elapsed / 1e6, 3),
             "unit": "Mrays/s",
             "n_gpus": ws,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "steps": steps,
+            "warmup": warmup,
+            "ms_per_step": round(elapsed / steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -156,38 +195,42 @@ def main():
             },
             "msamples_per_s": round(cams / elapsed / 1e6, 3),
             "lumo_total_rays_per_s_M": round(rays / elapsed / 1e6, 3),
-            "queries_per_step": q / args.steps,
+            "queries_per_step": q / steps,
             "scene_build_s": wl["scene_build_s"],
+            # tone_mapping.rs:42-56 debug checks over the timed camera samples: NaN, negative, > 1000
+            "sample_checks": {"nan": checks[0], "negative": checks[1], "large": checks[2]},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out))
-    dev.close()
-    if pg is not None:
-        pg.destroy_process_group()
+        if warm_spp is not None:
+            out["warmup_spp"] = warm_spp
+    del scene
+    return out
 
 
-def build_config(args):
+def build_config(name, res=None, spp_override=None):
     """(scene, camera, (W, H), spp, labels) of BASELINE.json's configs, built with lumo's API."""
     import lumo_amd as L
     from lumo_amd import scenes
     t0 = time.perf_counter()
-    if args.config == "c1":
-        W = H = args.res or 1024
-        spp = args.spp or 1024
+    if name == "c1":
+        W = H = res or 1024
+        spp = spp_override or 1024
         scene, cam = scenes.cornell(), L.Camera.cornell_box((W, H))
         wl = {"name": "cornell", "scene": "Scene::cornell_box (32 triangles, 1 rectangle light)",
-              "camera": "Camera::cornell_box", "data": "synthetic (Scene::cornell_box defined in code; no assets)"}
-    elif args.config == "c2":
-        W, H = (args.res, args.res) if args.res else (1920, 1080)
-        spp = args.spp or 256
+              "camera": "Camera::cornell_box", "data": "synthetic (Scene::cornell_box defined in code; no assets)",
+              "cpu_tile_stride": 32}
+    elif name == "c2":
+        W, H = (res, res) if res else (1920, 1080)
+        spp = spp_override or 256
         scene, cam = scenes.dragon(), scenes.default_camera((W, H))
         wl = {"name": "dragon", "scene": "examples/dragon.rs: empty_box + 871414-triangle procedural stand-in "
                                          "(transparent MfDielectric 0.03, eta 1.5 glass curve) as an Instance",
-              "camera": "Camera::builder() default", "data": "synthetic (procedural stand-in for dragon.obj)"}
-    elif args.config == "c4":
-        W = H = args.res or 1024
-        spp = args.spp or 4096
+              "camera": "Camera::builder() default", "data": "synthetic (procedural stand-in for dragon.obj)",
+              "cpu_tile_stride": 256}
+    elif name == "c4":
+        W = H = res or 1024
+        spp = spp_override or 4096
         scene, cam = scenes.caustics(), scenes.caustics_camera((W, H))
         wl = {"name": "caustics", "scene": "examples/caustics.rs: empty_box MAGENTA/CYAN + mirror and glass "
                                            "instances of a 968-triangle suzanne stand-in",
@@ -196,61 +239,66 @@ def build_config(args):
               "integrator_name": "BDPathTrace (all (s,t) strategies, MIS, light-tracing splats)", "tag": "bdpt",
               "cpu_tile_stride": 512, "cpu_batches": 1}
     else:
-        W, H = (args.res, args.res) if args.res else (1920, 1080)
-        spp = args.spp or 256
+        W, H = (res, res) if res else (1920, 1080)
+        spp = spp_override or 256
         scene, cam = scenes.bistro(), scenes.bistro_camera((W, H))
         wl = {"name": "bistro", "scene": "procedural Bistro stand-in: ~2.8M triangles in 400 material groups, "
                                          "2048 emissive triangles, environment light",
               "camera": "origin (-16,5,-1) towards (0,0,0) (bistro.rs:15-18)",
-              "data": "synthetic (procedural stand-in for Bistro exterior)"}
+              "data": "synthetic (procedural stand-in for Bistro exterior)", "cpu_tile_stride": 512}
     scene.build()
     wl["scene_build_s"] = round(time.perf_counter() - t0, 2)
     return scene, cam, (W, H), spp, wl
 
 
 def roofline(st, n_shadow, bdpt=False, workload="c1"):
-    """Dominant-kernel roofline from live per-launch HIP-event times and traversal counters."""
+    """Dominant-kernel roofline from live per-launch HIP-event times and traversal counters.
+
+    Unit = one ray query; bytes = IO + 48 per AABB test + 16 per kd split visit + 84 per triangle
+    test (f64), the counters being the kernels' own (identical to the oracle's on the same rays).
+    PathTrace: k_closest (closest IO) or k_shadow (shadow record + the per-path fold amortised
+    over its 2 n_shadow queries).  BDPT: the walk traces (k_closest) or the connection
+    traversals (k_bdpt_trace_a + k_bdpt_vis, one query each)."""
+    from lumo_amd._ffi import STAGES
     ms = list(st.kernel_ms)
     launches = list(st.launches)
-    per_stage = {STAGES[i]: {"ms": round(ms[i], 3), "launches": int(launches[i])} for i in range(8)}
-    dom = max(range(8), key=lambda i: ms[i])
-    name = STAGES[dom]
-    if bdpt:
-        nbytes = None  # BDPT: no algorithmic byte model yet (DESIGN.md §7)
-    elif name == "closest":
-        nbytes = (st.closest_queries * B_CLOSEST_IO + st.aabb_tests[0] * B_AABB + st.kd_nodes[0] * B_KD +
-                  st.tri_tests[0] * B_TRI)
-    elif name == "shadow":
-        # k_shadow folds a path's 2 n_shadow records into its radiance: B_FOLD is amortised per query
-        b_io = B_RECORD + B_FOLD / (2 * n_shadow)
-        nbytes = (st.shadow_queries * b_io + st.aabb_tests[1] * B_AABB + st.kd_nodes[1] * B_KD +
-                  st.tri_tests[1] * B_TRI)
-    else:
-        nbytes = None
-    # BDPT stage slots: walk traces = closest (k_closest), walk steps = shade (k_bdpt_step),
-    # connections = shadow (k_bdpt_conn_a + k_bdpt_vis + k_bdpt_paths), re-runs + fold = resolve
-    bd_names = {"closest": "bdpt_walk_trace", "shade": "bdpt_walk_step", "shadow": "bdpt_connections",
-                "resolve": "bdpt_redo_fold"}
-    if bdpt:
-        per_stage = {bd_names.get(k, k): v for k, v in per_stage.items()}
-    kname = {"closest": "k_closest", "shade": "k_bdpt_step", "shadow": "k_bdpt_vis",
-             "resolve": "k_bdpt_redo"}.get(name, f"k_{name}") if bdpt else f"k_{name}"
-    pmc = pmc_traffic(kname[2:]) if workload == "c1" else {}  # the committed PMC table profiles C1
-    out = {"bound": "hbm", "kernel": kname, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "traffic": pmc.get("hbm_bytes_per_launch"), "traffic_raw": pmc.get("hbm_bytes_per_launch_raw"),
-           "traffic_source": "profiles/pmc_traffic.json" if pmc else None, "stages": per_stage}
+    per_stage = {STAGES[i]: {"ms": round(ms[i], 3), "launches": int(launches[i])} for i in range(len(STAGES))}
     cq, sq = max(st.closest_queries, 1), max(st.shadow_queries, 1)
+    closest_bytes = (st.closest_queries * B_CLOSEST_IO + st.aabb_tests[0] * B_AABB + st.kd_nodes[0] * B_KD +
+                     st.tri_tests[0] * B_TRI)
+    trav1 = st.aabb_tests[1] * B_AABB + st.kd_nodes[1] * B_KD + st.tri_tests[1] * B_TRI
+    if bdpt:
+        # candidates: walk traces; connection traversals (both item kernels as one unit)
+        conn_ms = ms[8] + ms[10]
+        conn_launches = launches[8] + launches[10]
+        cands = {"k_closest": (ms[1], launches[1], closest_bytes),
+                 "k_bdpt_trace_a+k_bdpt_vis": (conn_ms, conn_launches, st.shadow_queries * B_CONN_IO + trav1)}
+    else:
+        b_io = B_RECORD + B_FOLD / (2 * n_shadow)
+        cands = {"k_closest": (ms[1], launches[1], closest_bytes),
+                 "k_shadow": (ms[3], launches[3], st.shadow_queries * b_io + trav1)}
+    # the dominant kernel of the step: the longest of all timed stages; if that is not a
+    # traversal kernel, the roofline is still reported for the longest traversal kernel
+    dom_stage = STAGES[max(range(len(STAGES)), key=lambda i: ms[i])]
+    kname = max(cands, key=lambda k: cands[k][0])
+    kms, kl, nbytes = cands[kname]
+    pmc = pmc_traffic(workload, kname)
+    out = {"bound": "hbm", "kernel": kname, "longest_stage": dom_stage, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "traffic": pmc.get("hbm_bytes_per_launch"), "traffic_raw": pmc.get("hbm_bytes_per_launch_raw"),
+           "traffic_source": f"profiles/pmc_traffic.json[{workload}]" if pmc else None, "stages": per_stage}
     out["per_query"] = {
         "closest": {"aabb": st.aabb_tests[0] / cq, "kd": st.kd_nodes[0] / cq, "tri": st.tri_tests[0] / cq},
-        "shadow": {"aabb": st.aabb_tests[1] / sq, "kd": st.kd_nodes[1] / sq, "tri": st.tri_tests[1] / sq}}
-    if nbytes is not None and ms[dom] > 0 and launches[dom] > 0:
-        achieved = nbytes / (ms[dom] * 1e-3) / 1e9
-        avg_s = ms[dom] * 1e-3 / launches[dom]
+        ("connection" if bdpt else "shadow"): {"aabb": st.aabb_tests[1] / sq, "kd": st.kd_nodes[1] / sq,
+                                               "tri": st.tri_tests[1] / sq}}
+    if kms > 0 and kl > 0:
+        achieved = nbytes / (kms * 1e-3) / 1e9
+        avg_s = kms * 1e-3 / kl
         out.update({"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 5),
-                    "bytes_per_launch": nbytes / launches[dom], "avg_launch_us": avg_s * 1e6})
+                    "bytes_per_launch": nbytes / kl, "avg_launch_us": avg_s * 1e6})
         if out["traffic"]:
             # measured DRAM-side rate of the same kernel: PMC bytes per launch over live launch time
             out["hbm_gbs_measured"] = round(out["traffic"] / avg_s / 1e9, 2)
+            out["traffic_over_algorithmic"] = round(out["traffic"] / (nbytes / kl), 3)
     else:
         out.update({"achieved": None, "frac": None})
     return out
@@ -262,20 +310,47 @@ def n_shadow_rays(scene):
     return max(n.bit_length() - 1, 1)
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if present."""
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` for `workload` from the committed rocprofv3 PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get(f"k_{kernel}", {})
+        return d.get(workload, {}).get(kernel, {})
     except (OSError, ValueError):
         return {}
 
 
+def host_cpus():
+    """Cores this process may use: the affinity mask, capped by a cgroup v2 CPU quota if one is
+    set (on the GPU box os.cpu_count() reports the whole machine), and the CPU model."""
+    n_aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    usable = min(n_aff, max(1, math.floor(quota))) if quota else n_aff
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"usable": usable, "os_cpu_count": os.cpu_count(), "affinity": n_aff,
+            "cgroup_quota_cpus": quota, "model": model}
+
+
 def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl):
     """The oracle (f64 restatement of lumo's CPU path, lumo's own tile-serial RNG order) on this
-    host: every k-th tile of every batch of the same frame, all spp; Mrays/s of that sample."""
+    host, BASELINE.md §5: once with every usable core and once with lumo's default 4 threads
+    (renderer.rs:21).  Each run renders every k-th tile of the frame's batches at the frame's spp,
+    with k scaled to the thread count so each run is ~--cpu-seconds of work; the rate is per query
+    (and per camera sample) of that sample."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     try:
         import oracle_ffi as O
@@ -283,21 +358,30 @@ def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl):
     except OSError:
         return None
     integrator = wl.get("integrator", 0)
-    stride = wl.get("cpu_tile_stride", args.cpu_tile_stride)
     batches = wl.get("cpu_batches", None)  # BDPT: the first batch only (CPU BDPT is ~100x slower)
-    sample = [t for i, t in enumerate(tasks) if (i % tiles) % stride == 0 and (batches is None or i // tiles < batches)]
-    threads = min(16, os.cpu_count() or 1)
-    t0 = time.perf_counter()
-    bufs, res, cnt = O.render_tasks(scene.desc(), cam.desc, sample, O.LUMO_ORDER, threads, integrator=integrator,
-                                    splats_out=[] if integrator else None)
-    dt = time.perf_counter() - t0
-    q = sum(r.num_queries for r in res)
-    paths = sum(r.num_camera_rays for r in res)
-    return {"value": round(q / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "msamples_per_s": round(paths / dt / 1e6, 4), "seconds": round(dt, 2),
-            "sample": f"{len(sample)} tasks = every {stride}th 16x16 tile of "
-                      f"{'each' if batches is None else f'the first {batches}'} 256-spp batch(es) of "
-                      f"the {W}x{H} @ {spp} spp frame ({paths} paths), lumo tile-serial RNG order"}
+    info = host_cpus()
+    runs = []
+    # stride for 16 threads at ~8 s (measured per config), scaled to the thread count
+    base_stride = wl.get("cpu_tile_stride", 32)
+    for threads in sorted({info["usable"], LUMO_DEFAULT_THREADS}, reverse=True):
+        stride = max(1, int(round(base_stride * 16 / threads * 8.0 / args.cpu_seconds))) | 1  # odd: all columns
+        sample = [t for i, t in enumerate(tasks)
+                  if (i % tiles) % stride == 0 and (batches is None or i // tiles < batches)]
+        t0 = time.perf_counter()
+        bufs, res, cnt = O.render_tasks(scene.desc(), cam.desc, sample, O.LUMO_ORDER, threads,
+                                        integrator=integrator, splats_out=[] if integrator else None)
+        dt = time.perf_counter() - t0
+        q = sum(r.num_queries for r in res)
+        paths = sum(r.num_camera_rays for r in res)
+        runs.append({"threads": threads, "value": round(q / dt / 1e6, 4), "msamples_per_s": round(paths / dt / 1e6, 4),
+                     "seconds": round(dt, 2),
+                     "sample": f"{len(sample)} tasks = every {stride}th 16x16 tile of "
+                               f"{'each' if batches is None else f'the first {batches}'} 256-spp batch(es) of "
+                               f"the {W}x{H} @ {spp} spp frame ({paths} paths), lumo tile-serial RNG order"})
+    best = runs[0]
+    return {"value": best["value"], "unit": "Mrays/s", "cores": best["threads"], "kind": "port",
+            "msamples_per_s": best["msamples_per_s"], "seconds": best["seconds"], "sample": best["sample"],
+            "cpu_model": info["model"], "host": info, "runs": runs}
 
 
 if __name__ == "__main__":

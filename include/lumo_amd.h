@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define LUMO_ABI_VERSION 2
+#define LUMO_ABI_VERSION 3
 
 typedef int32_t lumo_status;
 enum {
@@ -248,14 +248,20 @@ typedef struct {
 
 /* Per-stage device time (HIP events; only with LUMO_TIMING=1 in the environment), launch
  * counts, query counts and traversal counters (AABB slab tests, kd split-node visits,
- * triangle tests) of the closest-hit [0] and shadow [1] kernels, summed over renders. */
+ * triangle tests) of the closest-hit [0] and shadow / connection [1] kernels, summed over
+ * renders.  BDPT: CLOSEST + SHADE are the subpath walks, RESOLVE the re-runs + fold, BD_* the
+ * connection items.  samples_{nan,neg,large} count the camera samples whose radiance has a NaN,
+ * a negative or a > 1000 component (the debug_assertions checks of tone_mapping.rs:42-56,
+ * counted instead of recoloured; the image is unchanged). */
 enum { LUMO_STAGE_CAMERA = 0, LUMO_STAGE_CLOSEST, LUMO_STAGE_SHADE, LUMO_STAGE_SHADOW, LUMO_STAGE_RESOLVE,
-       LUMO_STAGE_FINISH, LUMO_STAGE_FILM, LUMO_STAGE_RING };
+       LUMO_STAGE_FINISH, LUMO_STAGE_FILM, LUMO_STAGE_RING, LUMO_STAGE_BD_TRACE_A, LUMO_STAGE_BD_EVAL_A,
+       LUMO_STAGE_BD_VIS, LUMO_STAGE_BD_PATHS, LUMO_STAGE_COUNT };
 typedef struct {
-    double kernel_ms[8];
-    uint64_t launches[8];
+    double kernel_ms[LUMO_STAGE_COUNT];
+    uint64_t launches[LUMO_STAGE_COUNT];
     uint64_t closest_queries, shadow_queries, bounces;
     uint64_t aabb_tests[2], kd_nodes[2], tri_tests[2];
+    uint64_t samples_nan, samples_neg, samples_large;
 } lumo_stats;
 
 /* Per-path dump of one task (test hook for per-path parity): arrays sized samples x pixels
@@ -305,6 +311,17 @@ lumo_status lumo_debug_set_integrator(void* ctx, int integrator);
  * `pixel` in sample pass `pass` of `task`; *n_out = number of bounces recorded. */
 lumo_status lumo_debug_trace(void* ctx, const lumo_tile_task* task, int pass, int pixel, double* out,
                              int* n_out);
+/* Kernel variant selected for the uploaded scene: kd stack class, bytes of scene staged in LDS
+ * (0: no staging), feature class (1: instances / spheres / triangle lights / microfacet
+ * materials), shadow rays per bounce (scene.rs:90-92). */
+typedef struct {
+    int32_t stack_class, lds_bytes, full_kernels, n_shadow;
+} lumo_scene_info_t;
+lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info);
+/* Diagnostics: one coalesced 8-B-per-lane read stream and one write stream over n doubles
+ * (kernels k_calib_read8 / k_calib_write8), to calibrate rocprofv3 FETCH_SIZE / WRITE_SIZE for
+ * the access width of the path kernels. */
+lumo_status lumo_debug_stream(void* ctx, size_t n);
 /* Perf switch: stage the packed scene in LDS inside the traversal kernels (default on; also
  * LUMO_LDS=0 in the environment). */
 void lumo_set_lds_staging(int on);

@@ -536,8 +536,10 @@ class Device:
         if integrator == Integrator.BDPathTrace and not lists:
             if splat_film is None or splat_film.dtype != np.float64 or not splat_film.flags.c_contiguous:
                 raise ValueError("BDPT needs splats_out or a C-contiguous float64 splat_film")
-        caps = [16 * (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1]) * t.samples if lists else 0
-                for t in arr]
+        caps = None
+        if lists:  # splat-list capacity per task: 16 taps per camera sample to start with
+            tv = np.frombuffer(arr, dtype=np.uint64).reshape(n, C.sizeof(_ffi.TileTask) // 8)
+            caps = (16 * (tv[:, 2] - tv[:, 0]) * (tv[:, 3] - tv[:, 1]) * tv[:, 5]).astype(np.int64).tolist()
         while True:
             bufs, sbufs, res = self._result_buffers(arr, n)
             if lists:
@@ -579,6 +581,12 @@ class Device:
                            obj.ctypes.data_as(_ffi.c_int32_p), prim.ctypes.data_as(_ffi.c_int32_p))
         check(lib().lumo_trace(self.ctx, C.byref(rays), n, C.byref(hits), int(li is not None)), "trace")
         return t, kind, obj, prim
+
+    def scene_info(self):
+        """Kernel variant chosen for the uploaded scene (stack class, LDS bytes, feature class)."""
+        s = _ffi.SceneInfo()
+        check(lib().lumo_scene_info(self.ctx, C.byref(s)), "scene_info")
+        return s
 
     def stats(self):
         s = _ffi.Stats()

@@ -118,10 +118,21 @@ class HitSoA(C.Structure):
     _fields_ = [("t", c_double_p), ("kind", c_int32_p), ("object", c_int32_p), ("prim", c_int32_p)]
 
 
+class SceneInfo(C.Structure):
+    _fields_ = [("stack_class", C.c_int32), ("lds_bytes", C.c_int32), ("full_kernels", C.c_int32),
+                ("n_shadow", C.c_int32)]
+
+
+STAGE_COUNT = 12  # LUMO_STAGE_COUNT
+STAGES = ["camera", "closest", "shade", "shadow", "resolve", "finish", "film", "ring",
+          "bd_trace_a", "bd_eval_a", "bd_vis", "bd_paths"]
+
+
 class Stats(C.Structure):
-    _fields_ = [("kernel_ms", C.c_double * 8), ("launches", C.c_uint64 * 8), ("closest_queries", C.c_uint64),
-                ("shadow_queries", C.c_uint64), ("bounces", C.c_uint64), ("aabb_tests", C.c_uint64 * 2),
-                ("kd_nodes", C.c_uint64 * 2), ("tri_tests", C.c_uint64 * 2)]
+    _fields_ = [("kernel_ms", C.c_double * STAGE_COUNT), ("launches", C.c_uint64 * STAGE_COUNT),
+                ("closest_queries", C.c_uint64), ("shadow_queries", C.c_uint64), ("bounces", C.c_uint64),
+                ("aabb_tests", C.c_uint64 * 2), ("kd_nodes", C.c_uint64 * 2), ("tri_tests", C.c_uint64 * 2),
+                ("samples_nan", C.c_uint64), ("samples_neg", C.c_uint64), ("samples_large", C.c_uint64)]
 
 
 class CameraParams(C.Structure):
@@ -153,6 +164,8 @@ DEVICE_API = [
     ("lumo_stats_reset", C.c_int32, [C.c_void_p]),
     ("lumo_set_timing", None, [C.c_int]),
     ("lumo_set_lds_staging", None, [C.c_int]),
+    ("lumo_debug_stream", C.c_int32, [C.c_void_p, C.c_size_t]),
+    ("lumo_scene_info", C.c_int32, [C.c_void_p, C.POINTER(SceneInfo)]),
     ("lumo_debug_set_integrator", C.c_int32, [C.c_void_p, C.c_int]),
     ("lumo_debug_trace", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.c_int, C.c_int, c_double_p, C.POINTER(C.c_int)]),
     ("lumo_debug_paths", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.POINTER(PathDump)]),

@@ -1,5 +1,5 @@
-// Bidirectional path tracing on the device (integrator/bd_path_trace*.rs), included by
-// kernels.hip inside its anonymous namespace after DCam / Paths.
+// Bidirectional path tracing on the device (integrator/bd_path_trace*.rs).  The kernels templated
+// on the stack class are instantiated in inst_bd.hip; the others (LUMO_MAIN_TU) in kernels.hip.
 //
 // A BDPT sample (bd_path_trace.rs:23-74) runs as a wavefront: the light subpaths of all slots
 // bounce through k_closest + k_bdpt_step, then the camera subpaths; k_bdpt_conn then evaluates
@@ -13,6 +13,12 @@
 //
 // Reference: bd_path_trace.rs:23-290, bd_path_trace/{path_gen.rs:4-157, mis.rs:4-239,
 // vertex.rs:1-162, measure.rs}, camera.rs:170-388, object.rs:99-126.
+
+#pragma once
+#include "state.h"
+
+namespace lumo {
+namespace dev {
 
 constexpr int BDPT_RR_DEPTH = 5, BDPT_MAX_DEPTH = 1024;  // path_gen.rs
 enum { TR_RADIANCE = 0, TR_IMPORTANCE = 1 };
@@ -711,6 +717,7 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_light_init(DScene sc, Paths S, B
     block_append(go, slot, S.q0, S.counts + CNT_NEXT);
 }
 
+#ifdef LUMO_MAIN_TU
 // Camera subpath start (bd_path_trace.rs:27): the camera vertex and ray of the slot.
 __global__ __launch_bounds__(BLOCK) void k_bdpt_cam_init(Paths S, Bdpt B, BItems I, DCam cam, int n) {
     const int slot = blockIdx.x * blockDim.x + threadIdx.x;
@@ -729,6 +736,8 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_cam_init(Paths S, Bdpt B, BItems
     }
     block_append(go, slot, S.q0, S.counts + CNT_NEXT);
 }
+
+#endif  // LUMO_MAIN_TU
 
 // One walk step (the loop body of path_gen.rs:52-157) after k_closest found the hit.
 template <int STK, bool FX>
@@ -1079,6 +1088,7 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_paths(DScene sc, Paths S, DCam c
     }
 }
 
+#ifdef LUMO_MAIN_TU
 // radiance = 0 + emission term + sum_t light-sampling terms + sum_t sum_s connection terms, in
 // lumo's order (bd_path_trace.rs:40-73); the splats are compacted in s order and given the
 // sample's wavelengths.
@@ -1114,6 +1124,9 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_fold(Paths S, Bdpt B, Bdpt R, BI
     X.sp.n[si] = n_sp;
 }
 
+#endif  // LUMO_MAIN_TU
+
+#ifdef LUMO_MAIN_TU
 // item totals of the pass: (a), (b)
 __global__ void k_bdpt_total(BItems I, int n, uint32_t* totals) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
@@ -1121,3 +1134,7 @@ __global__ void k_bdpt_total(BItems I, int n, uint32_t* totals) {
         totals[1] = I.off_b[n - 1] + I.n_b[n - 1];
     }
 }
+#endif  // LUMO_MAIN_TU
+
+}  // namespace dev
+}  // namespace lumo

@@ -1,0 +1,58 @@
+// BDPT traversal kernels of one kd stack class (compiled once per class with -DLUMO_STK=<class>,
+// see Makefile STK_CLASSES): walk steps, re-runs, (a)-item traces, (b)-item visibility.
+#include "launch.h"
+
+#ifndef LUMO_STK
+#error "inst_bd.hip is compiled with -DLUMO_STK=<stack class>"
+#endif
+
+namespace lumo {
+namespace dev {
+
+template <int STK>
+void launch_bdpt_step(int grid, hipStream_t sm, bool fx, const DScene& sc, const Paths& S, const Tasks& T,
+                      const Bdpt& B, const BItems& I, int mode, const int32_t* queue, int32_t* next_queue) {
+    if (fx) k_bdpt_step<STK, true><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue);
+    else k_bdpt_step<STK, false><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue);
+}
+
+#define LUMO_TRAV_LAUNCH(KERNEL, ...)                                                        \
+    do {                                                                                     \
+        if (l.lds) {                                                                         \
+            if (l.fx) KERNEL<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(__VA_ARGS__);  \
+            else KERNEL<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(__VA_ARGS__);     \
+        } else {                                                                             \
+            if (l.fx) KERNEL<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(__VA_ARGS__);     \
+            else KERNEL<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(__VA_ARGS__);        \
+        }                                                                                    \
+    } while (0)
+
+template <int STK>
+void launch_bdpt_redo(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const DCam& cam,
+                      const Bdpt& B, const Bdpt& R, const BItems& I) {
+    LUMO_TRAV_LAUNCH(k_bdpt_redo, sc, S, T, cam, B, R, I);
+}
+
+template <int STK>
+void launch_bdpt_trace_a(const TravLaunch& l, const DScene& sc, const Paths& S, const DCam& cam, const Bdpt& B,
+                         const Bdpt& R, const BItems& I, int n, const uint32_t* totals) {
+    LUMO_TRAV_LAUNCH(k_bdpt_trace_a, sc, S, cam, B, R, I, n, totals);
+}
+
+template <int STK>
+void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, const Bdpt& B, const Bdpt& R,
+                     const BItems& I, int n, const uint32_t* totals) {
+    LUMO_TRAV_LAUNCH(k_bdpt_vis, sc, S, B, R, I, n, totals);
+}
+
+template void launch_bdpt_step<LUMO_STK>(int, hipStream_t, bool, const DScene&, const Paths&, const Tasks&,
+                                         const Bdpt&, const BItems&, int, const int32_t*, int32_t*);
+template void launch_bdpt_redo<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Tasks&, const DCam&,
+                                         const Bdpt&, const Bdpt&, const BItems&);
+template void launch_bdpt_trace_a<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const DCam&, const Bdpt&,
+                                            const Bdpt&, const BItems&, int, const uint32_t*);
+template void launch_bdpt_vis<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Bdpt&, const Bdpt&,
+                                        const BItems&, int, const uint32_t*);
+
+}  // namespace dev
+}  // namespace lumo

@@ -1,0 +1,48 @@
+// Path-tracing traversal kernels of one kd stack class (compiled once per class with
+// -DLUMO_STK=<class>, see Makefile STK_CLASSES): k_closest, k_shadow, k_trace and their launchers.
+#include "launch.h"
+#include "pt.h"
+
+#ifndef LUMO_STK
+#error "inst_pt.hip is compiled with -DLUMO_STK=<stack class>"
+#endif
+
+namespace lumo {
+namespace dev {
+
+template <int STK>
+void launch_closest(const TravLaunch& l, const DScene& sc, const Paths& S, const int32_t* queue) {
+    if (l.lds) {
+        if (l.fx) k_closest<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, queue);
+        else k_closest<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, queue);
+    } else {
+        if (l.fx) k_closest<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, queue);
+        else k_closest<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, queue);
+    }
+}
+
+template <int STK>
+void launch_shadow(const TravLaunch& l, const DScene& sc, const Paths& S, uint32_t seg) {
+    if (l.lds) {
+        if (l.fx) k_shadow<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, seg);
+        else k_shadow<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, seg);
+    } else {
+        if (l.fx) k_shadow<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, seg);
+        else k_shadow<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, seg);
+    }
+}
+
+template <int STK>
+void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, const double* d, const int32_t* light,
+                  int n, int any_hit, double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
+                  unsigned long long* tcount) {
+    k_trace<STK><<<grid, BLOCK, 0, sm>>>(sc, o, d, light, n, any_hit, t_out, kind_out, obj_out, prim_out, tcount);
+}
+
+template void launch_closest<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const int32_t*);
+template void launch_shadow<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, uint32_t);
+template void launch_trace<LUMO_STK>(int, hipStream_t, const DScene&, const double*, const double*, const int32_t*,
+                                     int, int, double*, int32_t*, int32_t*, int32_t*, unsigned long long*);
+
+}  // namespace dev
+}  // namespace lumo

@@ -27,166 +27,14 @@
 #include "../../../include/lumo_amd.h"
 #include <hipcub/hipcub.hpp>
 
-#include "dscene.h"
+#define LUMO_MAIN_TU
+#include "launch.h"
+#include "pt.h"
 
 using namespace lumo;
 using namespace lumo::dev;
 
 namespace {
-
-constexpr int BLOCK = 256;
-// Minimum waves per SIMD (register budget) per kernel, tuned by A/B on MI355X.
-#ifndef LUMO_CLOSEST_WAVES
-#define LUMO_CLOSEST_WAVES 4
-#endif
-#ifndef LUMO_SHADOW_WAVES
-#define LUMO_SHADOW_WAVES 4
-#endif
-#ifndef LUMO_SHADE_WAVES
-#define LUMO_SHADE_WAVES 1
-#endif
-constexpr uint64_t SAMPLES_INCREMENT = 256;
-constexpr int RR_DEPTH = 5;
-
-// ST_RESOLVE is kept for the stats layout; the fold now runs inside k_shadow.
-enum Stage { ST_CAMERA = 0, ST_CLOSEST, ST_SHADE, ST_SHADOW, ST_RESOLVE, ST_FINISH, ST_FILM, ST_RING, ST_COUNT };
-// Device-side queue counters: the bounce kernels read their counts from here, so the host never
-// waits for a count before launching the next stage.
-enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_BUCKET0, CNT_N = CNT_BUCKET0 + 8 };
-// The resolve queue is split into NB buckets by the shadow rays' origin object so that a wave's
-// visibility queries start on the same surface and walk similar BVH / kd paths (LUMO_BUCKETS=0:
-// one bucket).  Bucket b holds its entries at rq[b * N ...]; k_shadow walks the buckets in order.
-constexpr int NB = 8;
-enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
-
-struct DCam {
-    Xform wtc, sctr, cts;
-    double lens_radius, focal_length;
-    M3 wb, x2r;
-    double fr, fsig;
-    double width, height, image_plane_area;  // CameraConfig (camera.rs:47-76), for BDPT importance
-};
-
-// Path state (SoA)
-struct Paths {
-    double *ro, *rd, *gath, *rad, *lam, *raster;
-    uint64_t *rng;  // 2 per slot: hi, lo
-    uint32_t *depth, *flags, *queries;
-    int32_t *task, *pix;
-    uint64_t *pseed, *mj_rng, *mj_state;
-    uint16_t* perm;  // 2 * dim per slot
-    double* hit_t;
-    int32_t *hit_kind, *hit_obj, *hit_tri;
-    // shadow records, R = N * 2 * n_shadow (fixed slot-major layout)
-    double *sh_o, *sh_d, *sh_f, *sh_psct, *sh_cos;
-    int32_t *sh_light, *sh_flags;
-    double *g_sh, *pdf_l;
-    // per-pass outputs
-    double *p_rgb, *p_lum;
-    uint32_t *p_cost, *p_valid;
-    double* film;
-    int32_t *q0, *q1, *rq;
-    uint32_t* counts;
-    unsigned long long* tcount;  // [2][TC_N]
-};
-
-struct Tasks {
-    lumo_tile_task* t;
-    int32_t* first;  // first slot of each task (n_tasks + 1)
-    uint64_t* ring_cost;
-    double* ring_lum;
-    uint32_t* ring_ptr;
-    double* delta;
-    unsigned long long *num_rays, *queries;
-};
-
-// Per-bounce trace of one path (diagnostics; lumo_debug_trace).
-struct DebugLog {
-    int slot, pass, cur_pass, n;
-    double rec[64][20];
-};
-__device__ DebugLog g_dbg;
-
-struct Dump {
-    double *rad, *lam, *raster, *delta;
-    unsigned long long* depth;
-};
-
-__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)); }
-
-// Workgroup-aggregated stream compaction: ballot + mbcnt inside each wave, wave totals scanned
-// in LDS, ONE atomicAdd per workgroup on the queue counter (a single hot counter word
-// saturates near 88 M atomics/s on MI355X, MI355X_MICROARCH.md "dequeue").  Every thread of
-// the block must call it (it synchronises the block).
-__device__ __forceinline__ void block_append(bool pred, int32_t value, int32_t* queue, uint32_t* counter) {
-    __shared__ uint32_t wtot[BLOCK / 64];
-    __shared__ uint32_t base_s;
-    const uint64_t mask = __ballot(pred);
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-    const uint32_t prefix =
-        __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-    if (lane == 0) wtot[w] = (uint32_t)__popcll(mask);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
-            const uint32_t cnt = wtot[i];
-            wtot[i] = t;
-            t += cnt;
-        }
-        base_s = t ? atomicAdd(counter, t) : 0u;
-    }
-    __syncthreads();
-    if (pred) queue[base_s + wtot[w] + prefix] = value;
-    __syncthreads();
-}
-
-// block_append into NB bucket segments of `queue` (stride `seg`): per-block LDS counters, one
-// global atomic per non-empty bucket per block.  Every thread of the block must call it.
-__device__ __forceinline__ void block_append_bucket(bool pred, int bucket, int32_t value, int32_t* queue, uint32_t seg,
-                                                    uint32_t* counters) {
-    __shared__ uint32_t cnt[NB], base_s[NB];
-    if (threadIdx.x < NB) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    uint32_t local = 0;
-    if (pred) local = atomicAdd(&cnt[bucket], 1u);
-    __syncthreads();
-    if (threadIdx.x < NB) base_s[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(counters + threadIdx.x, cnt[threadIdx.x]) : 0u;
-    __syncthreads();
-    if (pred) queue[(size_t)bucket * seg + base_s[bucket] + local] = value;
-    __syncthreads();
-}
-
-// Wave-reduced traversal counters (one atomic per wavefront).
-__device__ __forceinline__ void flush_counters(const Counters& C, unsigned long long* dst) {
-    unsigned long long a = C.aabb, k = C.kd, t = C.tri;
-    for (int off = 32; off > 0; off >>= 1) {
-        a += __shfl_down(a, off);
-        k += __shfl_down(k, off);
-        t += __shfl_down(t, off);
-    }
-    if (lane_id() == 0) {
-        if (a) atomicAdd(dst + TC_AABB, a);
-        if (k) atomicAdd(dst + TC_KD, k);
-        if (t) atomicAdd(dst + TC_TRI, t);
-    }
-}
-
-__device__ __forceinline__ V3 ldv3(const double* p, int i) { return V3{p[3 * i], p[3 * i + 1], p[3 * i + 2]}; }
-__device__ __forceinline__ void stv3(double* p, int i, V3 v) {
-    p[3 * i] = v.x;
-    p[3 * i + 1] = v.y;
-    p[3 * i + 2] = v.z;
-}
-__device__ __forceinline__ DColor ldc(const double* p, int i) {
-    return DColor{{p[4 * i], p[4 * i + 1], p[4 * i + 2], p[4 * i + 3]}};
-}
-__device__ __forceinline__ void stc(double* p, int i, const DColor& c) {
-    p[4 * i] = c.s[0];
-    p[4 * i + 1] = c.s[1];
-    p[4 * i + 2] = c.s[2];
-    p[4 * i + 3] = c.s[3];
-}
 
 // ------------------------------------------------------------------ init
 // Pixel sampler seeds: the tile stream's first P outputs.
@@ -287,246 +135,6 @@ __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, in
     block_append(active, s, S.q0, S.counts + CNT_NEXT);
 }
 
-// ------------------------------------------------------------------ closest hit
-template <int STK, bool LDS, bool FX>
-__global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc0, Paths S, const int32_t* queue) {
-    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
-    const uint32_t count = S.counts[CNT_CUR];
-    if (count <= blockIdx.x * blockDim.x) return;  // before staging: whole block idle
-    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
-    Counters C{0, 0, 0};
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
-        const int s = queue[q];
-        const RayX r = rayx(Ray{ldv3(S.ro, s), ldv3(S.rd, s)});
-        const HitRef h = scene_hit<STK, FX>(sc, r, C);
-        S.hit_t[s] = h.t;
-        S.hit_kind[s] = h.kind;
-        S.hit_obj[s] = h.obj;
-        S.hit_tri[s] = h.tri;
-        S.queries[s] += 1;
-    }
-    flush_counters(C, S.tcount);
-}
-
-// ------------------------------------------------------------------ shade
-// One path's bounce: hit record, emission, BSDF sample, NEE records, RR, spawn.
-template <bool FX>
-__device__ __forceinline__ void shade_one(const DScene& sc, const Paths& S, const Tasks& T, int s, bool& alive,
-                                          bool& resolve) {
-    const int ns = sc.n_shadow;
-    int n_sh = 0;
-    {
-        const int kind = S.hit_kind[s];
-        if (kind != 0) {
-            const Ray ro{ldv3(S.ro, s), ldv3(S.rd, s)};
-            const HitRef hr{S.hit_t[s], kind, S.hit_obj[s], S.hit_tri[s]};
-            DHit ho;
-            hit_record<FX>(sc, hr, rayx(ro), ho);
-            const lumo_material m = sc.mats[ho.material];
-            Xorshift rng{S.rng[2 * s], S.rng[2 * s + 1]};
-            if (s == g_dbg.slot && g_dbg.pass == g_dbg.cur_pass && g_dbg.n < 64) {
-                double* d = g_dbg.rec[g_dbg.n++];
-                d[0] = S.depth[s]; d[1] = hr.kind; d[2] = hr.obj; d[3] = hr.tri; d[4] = hr.t;
-                d[5] = ro.o.x; d[6] = ro.o.y; d[7] = ro.o.z; d[8] = ro.d.x; d[9] = ro.d.y; d[10] = ro.d.z;
-                d[11] = ho.p.x; d[12] = ho.p.y; d[13] = ho.p.z; d[14] = ho.ng.x; d[15] = ho.ng.y; d[16] = ho.ng.z;
-                d[17] = (double)(rng.hi >> 11); d[18] = ho.backface; d[19] = S.gath[4 * s];
-            }
-            double L[NS];
-            for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
-            DColor gathered = ldc(S.gath, s);
-            DColor radiance = ldc(S.rad, s);
-            const V3 wo = -ro.d;
-            const double rand_u = xs_float(rng);
-            const V2 sq = xs_vec2(rng);
-            V3 wi;
-            const bool sampled = bsdf_sample<FX>(sc, m, ho, wo, L, rand_u, sq, wi);
-            if (m.kind == LUMO_MAT_MF_DIELECTRIC && !(m.flags & LUMO_MATF_CONSTANT_ETA)) {
-                for (int i = 1; i < NS; ++i) S.lam[4 * s + i] = 0.0;  // lambda terminated (even if None)
-            }
-            if (!sampled) {
-                if (S.flags[s] & 1u) radiance = radiance + gathered * emit(sc, m, L, ho.backface);
-                stc(S.rad, s, radiance);
-            } else {
-                // NEE: n_shadow x [light pick, light direction, BSDF sample] (integrator.rs:87-137)
-                if (!mat_is_delta<FX>(sc, m, L)) {
-                    const int base = s * 2 * ns;
-                    for (int i = 0; i < ns; ++i) {
-                        const int li = sample_light(sc, xs_float(rng));
-                        const lumo_object& Lo = sc.lights[li];
-                        S.pdf_l[s * ns + i] = sc.alias_pdf[li];
-                        {
-                            const V2 rs = xs_vec2(rng);
-                            const V3 w = light_sample_towards<FX>(sc, Lo, ho.p, rs);
-                            const Ray ri = spawn(ho, w);
-                            const int rec = base + 2 * i;
-                            stv3(S.sh_o, rec, ri.o);
-                            stv3(S.sh_d, rec, ri.d);
-                            stc(S.sh_f, rec, bsdf_f<FX>(sc, m, ho, wo, w, L));
-                            S.sh_psct[rec] = bsdf_pdf<FX>(sc, m, ho, wo, w, L);
-                            S.sh_cos[rec] = shading_cosine(m, w, ho.ns);
-                            S.sh_light[rec] = li;
-                            S.sh_flags[rec] = 1 | 2;  // valid | light-sampled
-                            n_sh++;
-                        }
-                        {
-                            const double ru = xs_float(rng);
-                            const V2 rsq = xs_vec2(rng);
-                            V3 w;
-                            const int rec = base + 2 * i + 1;
-                            if (bsdf_sample<FX>(sc, m, ho, wo, L, ru, rsq, w)) {
-                                const Ray ri = spawn(ho, w);
-                                stv3(S.sh_o, rec, ri.o);
-                                stv3(S.sh_d, rec, ri.d);
-                                stc(S.sh_f, rec, bsdf_f<FX>(sc, m, ho, wo, w, L));
-                                S.sh_psct[rec] = bsdf_pdf<FX>(sc, m, ho, wo, w, L);
-                                S.sh_cos[rec] = shading_cosine(m, w, ho.ns);
-                                S.sh_light[rec] = li;
-                                S.sh_flags[rec] = 1;
-                                n_sh++;
-                            } else {
-                                S.sh_flags[rec] = 0;
-                            }
-                        }
-                    }
-                    stc(S.g_sh, s, gathered);
-                    resolve = true;
-                }
-                // spawn the continuation (path_trace.rs:42-77)
-                const Ray ri = spawn(ho, wi);
-                const V3 wi2 = ri.d;
-                const double p_scatter = bsdf_pdf<FX>(sc, m, ho, wo, wi2, L);
-                if (p_scatter > 0.0) {
-                    const DColor bsdf = bsdf_f<FX>(sc, m, ho, wo, wi2, L);
-                    gathered = gathered * (bsdf * shading_cosine(m, wi2, ho.ns) / p_scatter);
-                    bool cont = true;
-                    const uint32_t depth = S.depth[s];
-                    if ((int)depth >= RR_DEPTH) {
-                        const double lum = luminance(sc, gathered, L);
-                        const double rr_prob = rmin(lum / T.delta[S.task[s]], 1.0);
-                        if (xs_float(rng) > rr_prob)
-                            cont = false;
-                        else
-                            gathered = gathered / rr_prob;
-                    }
-                    if (cont) {
-                        S.flags[s] = mat_is_specular<FX>(m) ? 1u : 0u;  // last_specular
-                        S.depth[s] = depth + 1;
-                        stv3(S.ro, s, ri.o);
-                        stv3(S.rd, s, ri.d);
-                        stc(S.gath, s, gathered);
-                        alive = true;
-                    }
-                }
-            }
-            S.rng[2 * s] = rng.hi;
-            S.rng[2 * s + 1] = rng.lo;
-            S.queries[s] += (uint32_t)n_sh;
-        }
-    }
-}
-
-template <bool FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue,
-                                                                    int32_t* next_queue, uint32_t seg, int buckets) {
-    const uint32_t count = S.counts[CNT_CUR];
-    // grid-stride over whole blocks: block_append needs every thread of the block each round
-    for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
-        const uint32_t q = base + threadIdx.x;
-        bool alive = false, resolve = false;
-        int s = -1;
-        if (q < count) {
-            s = queue[q];
-            shade_one<FX>(sc, S, T, s, alive, resolve);
-        }
-        block_append(alive, s, next_queue, S.counts + CNT_NEXT);
-        int b = 0;
-        if (resolve && buckets > 1) {  // origin object of the shadow rays (objects, then lights)
-            const int key = S.hit_kind[s] == 2 ? sc.n_objs + S.hit_obj[s] : S.hit_obj[s];
-            b = key < NB ? key : key % NB;
-        }
-        block_append_bucket(resolve, b, s, S.rq, seg, S.counts + CNT_BUCKET0);
-    }
-}
-
-// ------------------------------------------------------------------ shadow rays (hit_light + MIS + fold)
-// One thread per path of the resolve queue: its 2 n_shadow records in lumo's order
-// (integrator.rs:74-184): per light sample i, single = (light-sampled + BSDF-sampled MIS
-// contributions) / pdf_light, radiance += gathered * sum(single) / n_shadow.  Records whose
-// BSDF sample failed contribute black without a query.
-template <int STK, bool LDS, bool FX>
-__device__ __forceinline__ DColor shadow_record(const DScene& sc, const Paths& S, int s, int rec, Counters& C) {
-    const RayX ri = rayx(Ray{ldv3(S.sh_o, rec), ldv3(S.sh_d, rec)});
-    const int li = S.sh_light[rec];
-    DHit hi;
-    DColor out = cfill(0.0);
-    if (scene_hit_light<STK, FX>(sc, ri, li, hi, C)) {
-        const lumo_object& Lo = sc.lights[li];
-        const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
-        const double p_sct = S.sh_psct[rec];
-        if (!(p_lig == 0.0 || p_sct == 0.0)) {  // mis_sample (integrator.rs:139-184)
-            double L[NS];
-            for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
-            const bool li_mode = (S.sh_flags[rec] & 2) != 0;
-            const double denom = p_lig * p_lig + p_sct * p_sct;
-            const double weight = li_mode ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
-            const double p_denom = li_mode ? p_lig : p_sct;
-            const lumo_material hm = sc.mats[hi.material];
-            out = ldc(S.sh_f, rec) * cfill(1.0) * emit(sc, hm, L, hi.backface) * S.sh_cos[rec] * weight / p_denom;
-        }
-    }
-    return out;
-}
-// Thread (path, light sample i): single_i = (light-sampled + BSDF-sampled) / pdf_light, staged
-// in LDS; the path's i == 0 thread then folds acc += gathered * single_i in i order and adds
-// acc / n_shadow to the radiance.  A block round covers BLOCK / n_shadow whole paths.
-template <int STK, bool LDS, bool FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0, Paths S, uint32_t seg) {
-    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
-    __shared__ DColor singles[BLOCK];
-    uint32_t bc[NB], count = 0;
-    for (int b = 0; b < NB; ++b) {
-        bc[b] = S.counts[CNT_BUCKET0 + b];
-        count += bc[b];
-    }
-    const int ns = sc0.n_shadow;
-    const uint32_t per_block = (uint32_t)(BLOCK / ns);  // paths per block round
-    if (count <= blockIdx.x * per_block) return;
-    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
-    Counters C{0, 0, 0};
-    const int i = (int)threadIdx.x % ns;
-    for (uint32_t base = blockIdx.x * per_block; base < count; base += gridDim.x * per_block) {
-        const uint32_t q = base + threadIdx.x / ns;
-        const bool mine = threadIdx.x < per_block * ns && q < count;
-        int s = -1;
-        if (mine) {
-            uint32_t r = q;
-            int bk = 0;
-            while (r >= bc[bk]) r -= bc[bk++];  // q < count, so bk < NB
-            s = S.rq[(size_t)bk * seg + r];
-            const int rec = s * 2 * ns + 2 * i;
-            const DColor a = shadow_record<STK, LDS, FX>(sc, S, s, rec, C);
-            const DColor b = (S.sh_flags[rec + 1] & 1) ? shadow_record<STK, LDS, FX>(sc, S, s, rec + 1, C) : cfill(0.0);
-            const DColor single = (cfill(0.0) + a + b) / S.pdf_l[s * ns + i];
-            if (ns == 1) {
-                stc(S.rad, s, ldc(S.rad, s) + (cfill(0.0) + ldc(S.g_sh, s) * single) / 1.0);
-            } else {
-                singles[threadIdx.x] = single;
-            }
-        }
-        if (ns > 1) {  // uniform over the block
-            __syncthreads();
-            if (mine && i == 0) {
-                const DColor g = ldc(S.g_sh, s);
-                DColor acc = cfill(0.0);
-                for (int k = 0; k < ns; ++k) acc = acc + g * singles[threadIdx.x + k];
-                stc(S.rad, s, ldc(S.rad, s) + acc / (double)ns);
-            }
-            __syncthreads();
-        }
-    }
-    flush_counters(C, S.tcount + TC_N);
-}
-
 // Start of a bounce: the alive queue just built becomes the current one.
 __global__ void k_bounce_begin(uint32_t* counts) {
     if (threadIdx.x == 0) {
@@ -557,6 +165,28 @@ __device__ __forceinline__ V3 sample_rgb(const DScene& sc, const DCam& cam, cons
 }
 
 // Per sample: luminance and cost for the ring, tone map -> XYZ -> WB -> RGB for the film.
+// debug_assertions sample checks of ToneMap::map (tone_mapping.rs:42-56), counted: 1 NaN, 2 negative,
+// 3 suspiciously large (max > 1000), in lumo's precedence; 0 otherwise.
+__device__ __forceinline__ int sample_check(const DColor& c) {
+    bool nan = false, neg = false;
+    double mx = -DINF;
+    for (int i = 0; i < NS; ++i) {
+        nan = nan || c.s[i] != c.s[i];
+        neg = neg || c.s[i] < 0.0;
+        mx = rmax(mx, c.s[i]);
+    }
+    return nan ? 1 : (neg ? 2 : (mx > 1000.0 ? 3 : 0));
+}
+// Wave-aggregated check counters; every lane of the wave must call it.
+__device__ __forceinline__ void count_checks(int cat, unsigned long long* dst) {
+    const uint64_t m1 = __ballot(cat == 1), m2 = __ballot(cat == 2), m3 = __ballot(cat == 3);
+    if (lane_id() == 0) {
+        if (m1) atomicAdd(dst, (unsigned long long)__popcll(m1));
+        if (m2) atomicAdd(dst + 1, (unsigned long long)__popcll(m2));
+        if (m3) atomicAdd(dst + 2, (unsigned long long)__popcll(m3));
+    }
+}
+
 __device__ __forceinline__ V3 finish_one(const DScene& sc, const Paths& S, const DCam& cam, int s, uint32_t pass,
                                          const Dump& dump, int dump_p, int tone_map, double tone_arg) {
     double L[NS];
@@ -582,8 +212,12 @@ __device__ __forceinline__ V3 finish_one(const DScene& sc, const Paths& S, const
 __global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, int n, uint32_t pass, Dump dump,
                                                    int dump_p, int tone_map, double tone_arg) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n || !S.p_valid[s]) return;
-    stv3(S.p_rgb, s, finish_one(sc, S, cam, s, pass, dump, dump_p, tone_map, tone_arg));
+    int cat = 0;
+    if (s < n && S.p_valid[s]) {
+        cat = sample_check(ldc(S.rad, s));
+        stv3(S.p_rgb, s, finish_one(sc, S, cam, s, pass, dump, dump_p, tone_map, tone_arg));
+    }
+    count_checks(cat, S.checks);
 }
 
 __device__ __forceinline__ double gauss(double x, double sigma) {
@@ -680,6 +314,7 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S, Tasks
         }
     }
     __syncthreads();
+    count_checks(j < P && l_ok[j] ? sample_check(ldc(S.rad, s)) : 0, S.checks);
     if (j < P) film_gather(S, T.t[ti], cam, s, j, LdsSrc{l_rgb, l_ras, l_ok});
 }
 
@@ -748,7 +383,6 @@ __global__ __launch_bounds__(64) void k_ring(Paths S, Tasks T, int n_tasks, int 
     }
 }
 
-#include "bdpt.h"
 
 // ------------------------------------------------------------------ BDPT splats -> film taps
 // FilmTile::add_sample with splat = true (film/tile.rs:65-111): tone map, XYZ, white balance,
@@ -824,32 +458,17 @@ __global__ void k_task_tap_ranges(Tasks T, const uint32_t* cnt, const uint32_t* 
     ranges[ti] = ti < n_tasks ? (uint64_t)off[T.first[ti]] : (uint64_t)off[n - 1] + cnt[n - 1];
 }
 
-// ------------------------------------------------------------------ traversal-only entry (lumo_trace)
-template <int STK>
-__global__ void k_trace(DScene sc, const double* o, const double* d, const int32_t* light, int n, int any_hit,
-                        double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
-                        unsigned long long* tcount) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    Counters C{0, 0, 0};
-    if (i < n) {
-        const RayX r = rayx(Ray{ldv3(o, i), ldv3(d, i)});
-        if (!any_hit) {
-            const HitRef h = scene_hit<STK, true>(sc, r, C);
-            t_out[i] = h.t;
-            kind_out[i] = h.kind;
-            obj_out[i] = h.obj;
-            prim_out[i] = h.tri;
-        } else {
-            DHit lh;
-            const int li = light[i];
-            const bool vis = scene_hit_light<STK, true>(sc, r, li, lh, C);
-            t_out[i] = vis ? lh.t : DINF;
-            kind_out[i] = vis ? 2 : 0;
-            obj_out[i] = vis ? li : -1;
-            prim_out[i] = -1;
-        }
-    }
-    flush_counters(C, tcount);
+// ------------------------------------------------------------------ PMC calibration (lumo_debug_stream)
+// Streams of known byte counts with the access width the path kernels use (8-B f64 per lane,
+// coalesced): the rocprofv3 FETCH_SIZE / WRITE_SIZE of these kernels calibrate the counters for
+// that width (MI355X_MICROARCH.md: only 16-B/lane streams are calibrated there).
+__global__ __launch_bounds__(BLOCK) void k_calib_read8(const double* __restrict__ in, size_t n, double* out) {
+    double acc = 0.0;
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (size_t)gridDim.x * BLOCK) acc += in[i];
+    if (acc == 12345.678) out[blockIdx.x] = acc;  // keeps the loads; never true for the zeroed input
+}
+__global__ __launch_bounds__(BLOCK) void k_calib_write8(double* __restrict__ out, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (size_t)gridDim.x * BLOCK) out[i] = (double)i;
 }
 
 // ================================================================== host side
@@ -939,7 +558,7 @@ enum WorkId {
     W_BD_FILM, W_BD_SCAN, W_BD_REDO_LIST, W_BD_REDO_INDEX, W_BDR_LD, W_BDR_LI, W_BDR_CD, W_BDR_CI, W_BDR_SP,
     W_BDR_SPN, W_BD_NL, W_BD_NC, W_BD_NITEMS, W_BD_IOFF, W_BD_DRAWS, W_BD_OK, W_BD_ITOTAL, W_BD_TERM, W_BD_PDF, W_BD_WDEPTH,
     W_BD_CAMO, W_BD_CAMD, W_BD_RNG0, W_BD_LAM0, W_BDR_DRAWS, W_BDR_OK, W_BD_NB, W_BD_OFFB, W_BD_TERMB, W_BD_VIS, W_BD_AT, W_BD_AKIND, W_BD_AOBJ,
-    W_BD_ATRI, W_COUNT
+    W_BD_ATRI, W_CHECKS, W_COUNT
 };
 
 template <typename T>
@@ -1006,8 +625,7 @@ void resolve_timers(Ctx& c) {
 
 bool g_timing = false;
 
-// kd stack classes (dscene.h); the list the kernels are instantiated for.
-constexpr int STACK_CLASSES[] = {4, 8, 16, 24, 32, 48, 64};
+// Stack-class dispatch (launch.h STACK_CLASSES).
 template <typename F>
 void by_stack_class(int cls, F&& f) {
     switch (cls) {
@@ -1029,18 +647,9 @@ template <typename F>
 void launch_trav(Ctx& c, uint64_t count, F&& f) {
     const bool lds = g_lds && c.sc.hot_bytes > 0;
     const int grid_full = ceil_div(count, BLOCK);
-    by_stack_class(c.sc.stack_class, [&](auto K) {
-        auto go = [&](auto Fx) {
-            if (lds)
-                f(K, std::true_type{}, Fx, std::min(grid_full, c.lds_grid_cap), (size_t)c.sc.hot_bytes);
-            else
-                f(K, std::false_type{}, Fx, grid_full, (size_t)0);
-        };
-        if (c.sc.full)
-            go(std::true_type{});
-        else
-            go(std::false_type{});
-    });
+    const TravLaunch l{lds ? std::min(grid_full, c.lds_grid_cap) : grid_full, lds ? (size_t)c.sc.hot_bytes : 0, lds,
+                       c.sc.full != 0, c.stream};
+    by_stack_class(c.sc.stack_class, [&](auto K) { f(K, l); });
 }
 
 lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lumo_tile_result* out, Dump* dump_host,
@@ -1117,6 +726,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     S.rq = wbuf<int32_t>(c, W_RQ, (size_t)(g_buckets > 1 ? NB : 1) * N, st);
     S.counts = wbuf<uint32_t>(c, W_COUNTS, CNT_N, st);
     S.tcount = wbuf<unsigned long long>(c, W_TCOUNT, 2 * TC_N, st);
+    S.checks = wbuf<unsigned long long>(c, W_CHECKS, 3, st);
     Tasks T{};
     T.t = wbuf<lumo_tile_task>(c, W_TASKS, n_tasks, st);
     T.first = wbuf<int32_t>(c, W_FIRST, n_tasks + 1, st);
@@ -1213,6 +823,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     HIPCHK(hipMemsetAsync(T.queries, 0, sizeof(unsigned long long) * n_tasks, sm));
     HIPCHK(hipMemsetAsync(S.film, 0, sizeof(double) * 4 * N, sm));
     HIPCHK(hipMemsetAsync(S.tcount, 0, sizeof(unsigned long long) * 2 * TC_N, sm));
+    HIPCHK(hipMemsetAsync(S.checks, 0, sizeof(unsigned long long) * 3, sm));
 
     const int gT = ceil_div(n_tasks, BLOCK), gN = ceil_div(N, BLOCK);
     k_init_seeds<<<gT, BLOCK, 0, sm>>>(T, S, (int)n_tasks);
@@ -1229,11 +840,6 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     // that point see empty queues and exit at once.
     const int ahead = c.bounce_ahead;
     for (uint64_t pass = 0; pass < max_samples; ++pass) {
-        {
-            const int cp = (int)pass;
-            HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dbg), &cp, sizeof(int), offsetof(DebugLog, cur_pass),
-                                          hipMemcpyHostToDevice, sm));
-        }
         if (dump_host) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, sm));
         HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));
         {
@@ -1269,10 +875,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 k_bounce_begin<<<1, 64, 0, sm>>>(S.counts);
                 {
                     StageTimer tm(c, g_timing, ST_CLOSEST);
-                    launch_trav(c, ub, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
-                        k_closest<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                            <<<grid, BLOCK, shm, sm>>>(c.sc, S, qa);
-                    });
+                    launch_trav(c, ub, [&](auto K, const TravLaunch& l) { launch_closest<decltype(K)::value>(l, c.sc, S, qa); });
                 }
                 step(ub, qa, qb);
                 HIPCHK(hipGetLastError());
@@ -1300,10 +903,8 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 }
                 {
                     StageTimer tm(c, g_timing, ST_SHADOW);
-                    launch_trav(c, (uint64_t)ub * (uint32_t)ns, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
-                        k_shadow<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                            <<<grid, BLOCK, shm, sm>>>(c.sc, S, rq_seg);
-                    });
+                    launch_trav(c, (uint64_t)ub * (uint32_t)ns,
+                                [&](auto K, const TravLaunch& l) { launch_shadow<decltype(K)::value>(l, c.sc, S, rq_seg); });
                 }
             });
             if (bst) return bst;
@@ -1315,10 +916,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 return [&, mode](uint32_t ub, int32_t* qa, int32_t* qb) {
                     StageTimer tm(c, g_timing, ST_SHADE);
                     by_stack_class(c.sc.stack_class, [&](auto K) {
-                        if (c.sc.full)
-                            k_bdpt_step<decltype(K)::value, true><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, B, BI, mode, qa, qb);
-                        else
-                            k_bdpt_step<decltype(K)::value, false><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, B, BI, mode, qa, qb);
+                        launch_bdpt_step<decltype(K)::value>(ceil_div(ub, BLOCK), sm, c.sc.full != 0, c.sc, S, T, B, BI, mode, qa, qb);
                     });
                 };
             };
@@ -1336,9 +934,8 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             if (bst) return bst;
             {
                 StageTimer tm(c, g_timing, ST_RESOLVE);
-                launch_trav(c, (uint64_t)B.redo_cap, [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
-                    k_bdpt_redo<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                        <<<grid, BLOCK, shm, sm>>>(c.sc, S, T, c.cam, B, BR, BI);
+                launch_trav(c, (uint64_t)B.redo_cap, [&](auto K, const TravLaunch& l) {
+                    launch_bdpt_redo<decltype(K)::value>(l, c.sc, S, T, c.cam, B, BR, BI);
                 });
             }
             // connection items: scan the per-slot counts, size the term buffers, one thread per item
@@ -1363,31 +960,33 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             BI.a_obj = wbuf<int32_t>(c, W_BD_AOBJ, std::max(totals[0], 1u), st);
             BI.a_tri = wbuf<int32_t>(c, W_BD_ATRI, std::max(totals[0], 1u), st);
             if (st) return st;
-            {
-                StageTimer tm(c, g_timing, ST_SHADOW);
-                if (totals[0] > 0) {
-                    launch_trav(c, (uint64_t)totals[0], [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
-                        k_bdpt_trace_a<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                            <<<grid, BLOCK, shm, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+            if (totals[0] > 0) {
+                {
+                    StageTimer tm(c, g_timing, ST_BD_TRACE_A);
+                    launch_trav(c, (uint64_t)totals[0], [&](auto K, const TravLaunch& l) {
+                        launch_bdpt_trace_a<decltype(K)::value>(l, c.sc, S, c.cam, B, BR, BI, N, items_total);
                     });
-                    const int grid = std::min(ceil_div(totals[0], BLOCK), 1 << 16);
-                    if (c.sc.full)
-                        k_bdpt_eval_a<true><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
-                    else
-                        k_bdpt_eval_a<false><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
                 }
-                if (totals[1] > 0)
-                    launch_trav(c, (uint64_t)totals[1], [&](auto K, auto Lds, auto Fx, int grid, size_t shm) {
-                        k_bdpt_vis<decltype(K)::value, decltype(Lds)::value, decltype(Fx)::value>
-                            <<<grid, BLOCK, shm, sm>>>(c.sc, S, B, BR, BI, N, items_total);
+                StageTimer tm(c, g_timing, ST_BD_EVAL_A);
+                const int grid = std::min(ceil_div(totals[0], BLOCK), 1 << 16);
+                if (c.sc.full)
+                    k_bdpt_eval_a<true><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                else
+                    k_bdpt_eval_a<false><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+            }
+            if (totals[1] > 0) {
+                {
+                    StageTimer tm(c, g_timing, ST_BD_VIS);
+                    launch_trav(c, (uint64_t)totals[1], [&](auto K, const TravLaunch& l) {
+                        launch_bdpt_vis<decltype(K)::value>(l, c.sc, S, B, BR, BI, N, items_total);
                     });
-                if (totals[1] > 0) {
-                    const int grid = std::min(ceil_div(totals[1], BLOCK), 1 << 16);
-                    if (c.sc.full)
-                        k_bdpt_paths<true><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
-                    else
-                        k_bdpt_paths<false><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
                 }
+                StageTimer tm(c, g_timing, ST_BD_PATHS);
+                const int grid = std::min(ceil_div(totals[1], BLOCK), 1 << 16);
+                if (c.sc.full)
+                    k_bdpt_paths<true><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                else
+                    k_bdpt_paths<false><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
             }
             {
                 StageTimer tm(c, g_timing, ST_RESOLVE);
@@ -1467,8 +1066,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     HIPCHK(hipMemcpyAsync(rays.data(), T.num_rays, sizeof(unsigned long long) * n_tasks, hipMemcpyDeviceToHost, sm));
     HIPCHK(hipMemcpyAsync(queries.data(), T.queries, sizeof(unsigned long long) * n_tasks, hipMemcpyDeviceToHost,
                           sm));
-    unsigned long long tc[2 * TC_N];
+    unsigned long long tc[2 * TC_N], checks[3];
     HIPCHK(hipMemcpyAsync(tc, S.tcount, sizeof(tc), hipMemcpyDeviceToHost, sm));
+    HIPCHK(hipMemcpyAsync(checks, S.checks, sizeof(checks), hipMemcpyDeviceToHost, sm));
     if (dump_host) {
         const size_t m = (size_t)dump_samples * N;
         HIPCHK(hipMemcpyAsync(dump_host->rad, D.rad, sizeof(double) * 4 * m, hipMemcpyDeviceToHost, sm));
@@ -1507,12 +1107,16 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     {
         unsigned long long total_q = 0;
         for (size_t i = 0; i < n_tasks; ++i) total_q += queries[i];
-        if (bdpt) closest_q = total_q;  // BDPT: all scene queries of the samples
-        shadow_q = total_q - closest_q;  // per-slot query counters: 1 per closest + 1 per valid record
+        // per-slot query counters: PT 1 per closest + 1 per valid record; BDPT walk traces (the
+        // bounce snapshots) + connection / re-run queries
+        shadow_q = total_q >= closest_q ? total_q - closest_q : 0;
     }
     c.stats.closest_queries += closest_q;
     c.stats.shadow_queries += shadow_q;
     c.stats.bounces += bounces;
+    c.stats.samples_nan += checks[0];
+    c.stats.samples_neg += checks[1];
+    c.stats.samples_large += checks[2];
     for (int k = 0; k < 2; ++k) {
         c.stats.aabb_tests[k] += tc[k * TC_N + TC_AABB];
         c.stats.kd_nodes[k] += tc[k * TC_N + TC_KD];
@@ -1573,11 +1177,6 @@ lumo_status lumo_create(int device, void** ctx_out) {
     }
     if (const char* e = std::getenv("LUMO_BOUNCE_AHEAD"))
         c->bounce_ahead = std::min(Ctx::SNAP_RING - 1, std::max(1, std::atoi(e)));
-    {
-        DebugLog h{};
-        h.slot = -1;
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &h, sizeof(h));
-    }
     if (const char* e = std::getenv("LUMO_LDS")) g_lds = e[0] != '0';
     if (const char* e = std::getenv("LUMO_BUCKETS")) g_buckets = e[0] == '0' ? 1 : NB;
     if (const char* e = std::getenv("LUMO_LDS_GRID")) c->lds_grid_cap = std::max(1, std::atoi(e));
@@ -1907,15 +1506,32 @@ lumo_status lumo_trace(void* ctx, const lumo_ray_soa* rays, size_t n, lumo_hit_s
     if (any_hit) HIPCHK(hipMemcpyAsync(light, rays->light, sizeof(int32_t) * n, hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemsetAsync(tc, 0, sizeof(unsigned long long) * 2 * TC_N, sm));
     by_stack_class(c->sc.stack_class, [&](auto K) {
-        k_trace<decltype(K)::value>
-            <<<ceil_div(n, BLOCK), BLOCK, 0, sm>>>(c->sc, o, d, light, (int)n, any_hit, t, kind, obj, prim, tc);
+        launch_trace<decltype(K)::value>(ceil_div(n, BLOCK), sm, c->sc, o, d, light, (int)n, any_hit, t, kind, obj, prim, tc);
     });
     HIPCHK(hipGetLastError());
     if (hits->t) HIPCHK(hipMemcpyAsync(hits->t, t, sizeof(double) * n, hipMemcpyDeviceToHost, sm));
     if (hits->kind) HIPCHK(hipMemcpyAsync(hits->kind, kind, sizeof(int32_t) * n, hipMemcpyDeviceToHost, sm));
     if (hits->object) HIPCHK(hipMemcpyAsync(hits->object, obj, sizeof(int32_t) * n, hipMemcpyDeviceToHost, sm));
     if (hits->prim) HIPCHK(hipMemcpyAsync(hits->prim, prim, sizeof(int32_t) * n, hipMemcpyDeviceToHost, sm));
+    unsigned long long tch[2 * TC_N];
+    HIPCHK(hipMemcpyAsync(tch, tc, sizeof(unsigned long long) * TC_N, hipMemcpyDeviceToHost, sm));
     HIPCHK(hipStreamSynchronize(sm));
+    const int k = any_hit ? 1 : 0;  // traversal counters of the batch: class 0 closest, 1 visibility
+    c->stats.aabb_tests[k] += tch[TC_AABB];
+    c->stats.kd_nodes[k] += tch[TC_KD];
+    c->stats.tri_tests[k] += tch[TC_TRI];
+    (any_hit ? c->stats.shadow_queries : c->stats.closest_queries) += n;
+    return LUMO_OK;
+}
+
+lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !info) return LUMO_ERR_INVALID;
+    if (!c->has_scene) return LUMO_ERR_NO_SCENE;
+    info->stack_class = c->sc.stack_class;
+    info->lds_bytes = g_lds ? (int32_t)c->sc.hot_bytes : 0;
+    info->full_kernels = c->sc.full;
+    info->n_shadow = c->sc.n_shadow;
     return LUMO_OK;
 }
 
@@ -1923,6 +1539,22 @@ lumo_status lumo_stats_get(void* ctx, lumo_stats* stats) {
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c || !stats) return LUMO_ERR_INVALID;
     *stats = c->stats;
+    return LUMO_OK;
+}
+
+// Diagnostics: one k_calib_read8 and one k_calib_write8 launch over n doubles (PMC calibration).
+lumo_status lumo_debug_stream(void* ctx, size_t n) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || n == 0) return LUMO_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    double* buf = nullptr;
+    HIPCHK(hipMalloc(&buf, sizeof(double) * n + sizeof(double) * 4096));
+    HIPCHK(hipMemsetAsync(buf, 0, sizeof(double) * n, c->stream));
+    k_calib_read8<<<2048, BLOCK, 0, c->stream>>>(buf, n, buf + n);
+    k_calib_write8<<<2048, BLOCK, 0, c->stream>>>(buf, n);
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    (void)hipFree(buf);
+    HIPCHK(e);
     return LUMO_OK;
 }
 
@@ -1936,24 +1568,12 @@ lumo_status lumo_stats_reset(void* ctx) {
     return LUMO_OK;
 }
 
-// Diagnostics: trace one slot (pass, pixel of a single-task render) bounce by bounce.
+// Diagnostics: per-bounce trace of one slot.  The device-side trace log was removed from the
+// hot shade kernel (a global compare per path per bounce); per-path dumps (lumo_debug_paths)
+// remain the parity instrument.
 lumo_status lumo_debug_trace(void* ctx, const lumo_tile_task* task, int pass, int pixel, double* out, int* n_out) {
-    Ctx* c = static_cast<Ctx*>(ctx);
-    if (!c || !task || !out || !n_out) return LUMO_ERR_INVALID;
-    HIPCHK(hipSetDevice(c->device));
-    DebugLog h{};
-    h.slot = pixel;
-    h.pass = pass;
-    h.cur_pass = -1;
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &h, sizeof(h)));
-    const lumo_status st = render_impl(*c, task, 1, nullptr, nullptr, 0);
-    if (st) return st;
-    HIPCHK(hipMemcpyFromSymbol(&h, HIP_SYMBOL(g_dbg), sizeof(h)));
-    *n_out = h.n;
-    std::memcpy(out, h.rec, sizeof(double) * 20 * h.n);
-    h.slot = -1;
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &h, sizeof(h)));
-    return LUMO_OK;
+    (void)ctx; (void)task; (void)pass; (void)pixel; (void)out; (void)n_out;
+    return LUMO_ERR_UNSUPPORTED;
 }
 
 lumo_status lumo_debug_paths(void* ctx, const lumo_tile_task* task, lumo_path_dump* dump) {

@@ -1,0 +1,71 @@
+// Launchers of the traversal kernels, one explicit instantiation per kd stack class STK.  Each
+// class is compiled in its own translation units (inst_pt.hip / inst_bd.hip built with
+// -DLUMO_STK=<class>), so the kernel instantiations build in parallel; kernels.hip only calls
+// these functions.
+#pragma once
+#include "bdpt.h"
+
+namespace lumo {
+namespace dev {
+
+// kd stack classes the kernels are instantiated for (Makefile STK_CLASSES must match).
+constexpr int STACK_CLASSES[] = {4, 8, 16, 24, 32, 48, 64};
+
+// Launch geometry of a traversal kernel: grid, dynamic LDS (staged scene), LDS staging on/off,
+// feature class (FX), stream.
+struct TravLaunch {
+    int grid;
+    size_t shm;
+    bool lds;
+    bool fx;
+    hipStream_t sm;
+};
+
+template <int STK>
+void launch_closest(const TravLaunch& l, const DScene& sc, const Paths& S, const int32_t* queue);
+template <int STK>
+void launch_shadow(const TravLaunch& l, const DScene& sc, const Paths& S, uint32_t seg);
+template <int STK>
+void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, const double* d, const int32_t* light,
+                  int n, int any_hit, double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
+                  unsigned long long* tcount);
+
+template <int STK>
+void launch_bdpt_step(int grid, hipStream_t sm, bool fx, const DScene& sc, const Paths& S, const Tasks& T,
+                      const Bdpt& B, const BItems& I, int mode, const int32_t* queue, int32_t* next_queue);
+template <int STK>
+void launch_bdpt_redo(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const DCam& cam,
+                      const Bdpt& B, const Bdpt& R, const BItems& I);
+template <int STK>
+void launch_bdpt_trace_a(const TravLaunch& l, const DScene& sc, const Paths& S, const DCam& cam, const Bdpt& B,
+                         const Bdpt& R, const BItems& I, int n, const uint32_t* totals);
+template <int STK>
+void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, const Bdpt& B, const Bdpt& R,
+                     const BItems& I, int n, const uint32_t* totals);
+
+#define LUMO_EXTERN_STK(K)                                                                                        \
+    extern template void launch_closest<K>(const TravLaunch&, const DScene&, const Paths&, const int32_t*);        \
+    extern template void launch_shadow<K>(const TravLaunch&, const DScene&, const Paths&, uint32_t);               \
+    extern template void launch_trace<K>(int, hipStream_t, const DScene&, const double*, const double*,          \
+                                         const int32_t*, int, int, double*, int32_t*, int32_t*, int32_t*,         \
+                                         unsigned long long*);                                                    \
+    extern template void launch_bdpt_step<K>(int, hipStream_t, bool, const DScene&, const Paths&, const Tasks&,   \
+                                             const Bdpt&, const BItems&, int, const int32_t*, int32_t*);          \
+    extern template void launch_bdpt_redo<K>(const TravLaunch&, const DScene&, const Paths&, const Tasks&,        \
+                                             const DCam&, const Bdpt&, const Bdpt&, const BItems&);               \
+    extern template void launch_bdpt_trace_a<K>(const TravLaunch&, const DScene&, const Paths&, const DCam&,      \
+                                                const Bdpt&, const Bdpt&, const BItems&, int, const uint32_t*);   \
+    extern template void launch_bdpt_vis<K>(const TravLaunch&, const DScene&, const Paths&, const Bdpt&,          \
+                                            const Bdpt&, const BItems&, int, const uint32_t*);
+#ifndef LUMO_STK
+LUMO_EXTERN_STK(4)
+LUMO_EXTERN_STK(8)
+LUMO_EXTERN_STK(16)
+LUMO_EXTERN_STK(24)
+LUMO_EXTERN_STK(32)
+LUMO_EXTERN_STK(48)
+LUMO_EXTERN_STK(64)
+#endif
+
+}  // namespace dev
+}  // namespace lumo

@@ -24,16 +24,27 @@ def shard_tasks(tasks, width, height, rank, world_size):
 
 
 def reduce_film(film, group=None, dst=None):
-    """Sum partial films over the process group (all ranks, or only `dst` when given)."""
+    """Sum partial films over the process group (all ranks, or only `dst` when given).
+
+    Film::add_tile (film.rs:155-171) adds a tile's pixels and then its splats; across ranks the
+    tiles are disjoint, so the pixel sum is exact, and the BDPT light-tracing splats
+    (tile.rs:96-101, full-frame) are summed in one collective with them.  The film's colour
+    space, splat scale (1 / samples, film.rs:137) and filter carry over."""
     import torch
     import torch.distributed as dist
     backend = dist.get_backend(group)
     dev = "cuda" if backend == "nccl" else "cpu"
-    t = torch.from_numpy(np.ascontiguousarray(film.pixels)).to(dev)
+    n_pix = film.pixels.size
+    flat = np.concatenate([np.ascontiguousarray(film.pixels).ravel(), np.ascontiguousarray(film.splats).ravel()])
+    t = torch.from_numpy(flat).to(dev)
     if dst is None:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     else:
         dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM, group=group)
-    out = Film(film.width, film.height)
-    out.pixels[...] = t.cpu().numpy()
+    out = Film(film.width, film.height, film.color_space, filter_radius=film.filter_radius,
+               filter_sigma=film.filter_sigma)
+    out.splat_scale = film.splat_scale
+    v = t.cpu().numpy()
+    out.pixels[...] = v[:n_pix].reshape(out.pixels.shape)
+    out.splats[...] = v[n_pix:].reshape(out.splats.shape)
     return out

@@ -1,7 +1,8 @@
-"""Multi-rank tile sharding over torch.distributed (gloo, world_size 2, CPU): the sharded
-renders summed with lumo_amd.dist.reduce_film equal the single-process render exactly.  The
-per-rank renderer here is the oracle (no GPU in this container); the GPU path uses the same
-shard_tasks / reduce_film code (bench.py, Renderer.render)."""
+"""Multi-rank tile sharding over torch.distributed (gloo, world_size 2): the sharded renders
+summed with lumo_amd.dist.reduce_film equal the single-process render.  PathTrace and BDPT
+(whose light-tracing splats are full-frame, tile.rs:96-101, and are summed across ranks) run
+through the oracle on the CPU; the GPU test drives Renderer.render(rank, world_size) on cuda:0
+from both ranks (the one-GPU box) and compares with the single-process render."""
 import os
 import socket
 import sys
@@ -23,19 +24,28 @@ def _free_port():
     return p
 
 
-def _render(tasks):
+def _scene(integrator):
+    import lumo_amd as L
+    from lumo_amd import scenes
+    if integrator == 0:
+        return L.Scene.cornell_box(), L.Camera.cornell_box((W, H))
+    return scenes.caustics(), scenes.caustics_camera((W, H))
+
+
+def _render(tasks, integrator=0):
     import lumo_amd as L
     import oracle_ffi as O
-    sc = L.Scene.cornell_box()
-    cam = L.Camera.cornell_box((W, H))
-    bufs, res, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 2)
-    film = L.Film(W, H)
-    for t, b in zip(tasks, bufs):
-        film.add_tile(t, b)
+    sc, cam = _scene(integrator)
+    splats = [] if integrator else None
+    bufs, res, _ = O.render_tasks(sc.build().desc(), cam.desc, tasks, O.WAVEFRONT, 2, integrator=integrator,
+                                  splats_out=splats)
+    film = L.Film(W, H, samples=SPP)
+    for i, (t, b) in enumerate(zip(tasks, bufs)):
+        film.add_tile(t, b, splats[i] if splats is not None else None)
     return film, sum(r.num_rays for r in res)
 
 
-def _worker(rank, ws, port, out_dir):
+def _worker(rank, ws, port, out_dir, integrator):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
     import torch.distributed as dist
     import lumo_amd as L
@@ -43,27 +53,71 @@ def _worker(rank, ws, port, out_dir):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
     tasks = L.make_tasks(W, H, SPP, SEED)
     mine = shard_tasks(tasks, W, H, rank, ws)
-    film, rays = _render(mine)
+    film, rays = _render(mine, integrator)
     total = reduce_film(film)
     np.save(os.path.join(out_dir, f"film{rank}.npy"), total.pixels)
+    np.save(os.path.join(out_dir, f"splats{rank}.npy"), total.splats)
+    np.save(os.path.join(out_dir, f"meta{rank}.npy"), np.array([total.splat_scale, total.color_space,
+                                                                   total.filter_radius, total.filter_sigma]))
     np.save(os.path.join(out_dir, f"rays{rank}.npy"), np.array([rays, len(mine)]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws", [2])
-def test_sharded_render_equals_single(ws, tmp_path):
+def _spawn(fn, ws, *args):
     import torch.multiprocessing as mp
+    mp.start_processes(fn, args=(ws, _free_port()) + args, nprocs=ws, join=True, start_method="spawn")
+
+
+@pytest.mark.parametrize("integrator", [0, 1], ids=["pathtrace", "bdpt"])
+def test_sharded_render_equals_single(integrator, tmp_path):
     import lumo_amd as L
-    port = _free_port()
-    mp.start_processes(_worker, args=(ws, port, str(tmp_path)), nprocs=ws, join=True, start_method="spawn")
+    ws = 2
+    _spawn(_worker, ws, str(tmp_path), integrator)
     tasks = L.make_tasks(W, H, SPP, SEED)
-    film, rays = _render(list(tasks))
+    film, rays = _render(list(tasks), integrator)
     parts = [np.load(tmp_path / f"rays{r}.npy") for r in range(ws)]
     assert sum(int(p[1]) for p in parts) == len(tasks)
     assert sum(int(p[0]) for p in parts) == rays
+    if integrator:
+        assert film.splats.any()  # the caustics scene has light-tracing splats
     for r in range(ws):
         got = np.load(tmp_path / f"film{r}.npy")
-        # tiles are disjoint per rank and a pixel's splats only come from its own tile, so the
-        # sum is exact
+        # tiles are disjoint per rank and a pixel's non-splat samples only come from its own
+        # tile, so the pixel sum is exact
         np.testing.assert_array_equal(got, film.pixels)
+        # splats are full-frame: summed per rank, then across ranks (a different float order)
+        np.testing.assert_allclose(np.load(tmp_path / f"splats{r}.npy"), film.splats, rtol=0, atol=1e-12)
+        meta = np.load(tmp_path / f"meta{r}.npy")
+        np.testing.assert_array_equal(meta, [film.splat_scale, film.color_space, film.filter_radius,
+                                             film.filter_sigma])
+
+
+def _gpu_worker(rank, ws, port, out_dir, integrator):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    import lumo_amd as L
+    from lumo_amd.dist import reduce_film
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+    sc, cam = _scene(integrator)
+    r = L.Renderer(sc, cam).samples(SPP).seed(SEED).integrator(
+        L.Integrator.BDPathTrace if integrator else L.Integrator.PathTrace)
+    total = reduce_film(r.render(rank, ws))
+    np.save(os.path.join(out_dir, f"film{rank}.npy"), total.pixels)
+    np.save(os.path.join(out_dir, f"splats{rank}.npy"), total.splats)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("integrator", [0, 1], ids=["pathtrace", "bdpt"])
+def test_gpu_renderer_sharded_equals_single(integrator, tmp_path):
+    """Renderer.render(rank, 2) on both ranks + reduce_film == Renderer.render() in one process."""
+    import lumo_amd as L
+    _spawn(_gpu_worker, 2, str(tmp_path), integrator)
+    sc, cam = _scene(integrator)
+    single = L.Renderer(sc, cam).samples(SPP).seed(SEED).integrator(
+        L.Integrator.BDPathTrace if integrator else L.Integrator.PathTrace).render()
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"film{r}.npy"), single.pixels)
+        np.testing.assert_allclose(np.load(tmp_path / f"splats{r}.npy"), single.splats, rtol=0, atol=1e-12)

@@ -129,3 +129,32 @@ def test_tone_mapped_tiles_match_oracle(dev, cornell, tm):
         np.testing.assert_array_equal(b, ob)
     plain, _ = dev.render_tasks(tasks)
     assert not np.array_equal(np.concatenate(plain), np.concatenate(bufs))
+
+
+def nan_normal_scene():
+    """Cornell box + a glass (MfDielectric 0.03) quad whose shading normals are NaN: the BSDF pdf
+    of a bounce off it is NaN.  path_trace.rs:47 breaks only on `p_scatter <= 0.0`, so a NaN pdf
+    continues the path (one more bounce, a NaN throughput) in lumo and in the oracle."""
+    sc = L.Scene.cornell_box()
+    obj = (b"v 150 100 300\nv 400 100 300\nv 400 400 300\nv 150 400 300\n"
+           b"vn 0 0 1\nvn 0 0 1\nvn 0 0 1\nvn 0 0 1\nf 1//1 2//2 3//3\nf 1//1 3//3 4//4\n")
+    sc.add_obj(obj, L.Material.transparent(L.named_spectrum("MAGENTA"), 0.03, 1.5))
+    sc.build()
+    d = sc.desc()
+    nrm = np.ctypeslib.as_array(d.normals, shape=(d.num_normals * 3,))
+    nrm[:] = np.nan
+    return sc
+
+
+def test_nan_pdf_continues_path(dev):
+    sc = nan_normal_scene()
+    cam = L.Camera.cornell_box((32, 32))
+    dev.upload(sc, cam)
+    task = L.make_tasks(32, 32, 16, SEED)[1]
+    g = gpu_paths(dev, task)
+    o = O.trace_paths(sc.desc(), cam.desc, task)
+    for k in ("depth", "raster", "lam", "radiance", "delta"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+    assert np.isnan(g["radiance"]).any()  # the NaN pdf was reached (and counted, below)
+    st = dev.stats()
+    assert st.samples_nan > 0

@@ -1,0 +1,193 @@
+"""GPU parity at the benchmarked scale and over every kernel variant the bench can select.
+
+* The full-size C2 (dragon.rs + the 871 414-triangle stand-in, kd stack class 48) and C3 (Bistro
+  stand-in, ~2.8 M triangles in 400 groups, 2 048 triangle lights, class 24) scenes exactly as
+  bench.py builds them: lumo_trace on >= 1 M rays, closest hit (Scene::hit, scene.rs:119-147)
+  and light visibility (Scene::hit_light, scene.rs:165-189), against the oracle, bit-exact in
+  t / kind / object and in the traversal counters (AABB / kd / triangle tests, the roofline's
+  inputs); per-path parity of two 16x16 tiles at each bench camera (k_closest / k_shade /
+  k_shadow of that stack class, kdtree.rs:101-169 + bvh.rs:315-362 semantics).
+* Cornell and the small dragon over every stack class >= the scene's need x LDS staging on/off
+  x lean/full feature kernels (LUMO_STACK_CLASS, lumo_set_lds_staging, LUMO_FULL_KERNELS):
+  per-path parity and tile parity for each instantiation, with lumo_scene_info confirming the
+  variant that ran.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import lumo_amd as L
+import oracle_ffi as O
+from lumo_amd import _ffi, scenes
+from lumo_amd.procedural import torus_knot_tube
+from parity import gpu_paths
+
+pytestmark = pytest.mark.gpu
+SEED = 0x5EED1234
+CLASSES = [4, 8, 16, 24, 32, 48, 64]  # launch.h STACK_CLASSES
+
+
+@pytest.fixture(scope="module")
+def dev():
+    d = L.Device(0)
+    yield d
+    d.close()
+
+
+@pytest.fixture(scope="module")
+def c2():
+    return scenes.dragon().build()
+
+
+@pytest.fixture(scope="module")
+def c3():
+    return scenes.bistro().build()
+
+
+def _arrays(desc):
+    v = np.ctypeslib.as_array(desc.vertices, shape=(desc.num_vertices, 3))
+    tris = np.ctypeslib.as_array(desc.triangles, shape=(desc.num_triangles,))
+    return v, tris
+
+
+def _closest_rays(desc, eye, n, seed):
+    """Half camera-like rays from the bench eye, half rays from random points of the scene's
+    bounds in random directions (the secondary-ray mix)."""
+    rng = np.random.default_rng(seed)
+    v, _ = _arrays(desc)
+    lo, hi = v.min(0), v.max(0)
+    m = n // 2
+    o1 = np.repeat(np.asarray(eye, dtype=np.float64)[None], m, 0)
+    d1 = (rng.uniform(lo, hi, size=(m, 3)) - o1)
+    o2 = rng.uniform(lo, hi, size=(n - m, 3))
+    d2 = rng.normal(size=(n - m, 3))
+    o, d = np.concatenate([o1, o2]), np.concatenate([d1, d2])
+    return o, d / np.linalg.norm(d, axis=1, keepdims=True)
+
+
+def _visibility_rays(desc, n, seed):
+    """Rays from random points of the bounds towards a random point of a random light
+    (triangle lights: a uniform barycentric point; the environment sphere: a random direction)."""
+    rng = np.random.default_rng(seed)
+    v, tris = _arrays(desc)
+    lights = np.ctypeslib.as_array(desc.lights, shape=(desc.num_lights,))
+    lo, hi = v.min(0), v.max(0)
+    o = rng.uniform(lo, hi, size=(n, 3))
+    li = rng.integers(0, desc.num_lights, size=n).astype(np.int32)
+    d = rng.normal(size=(n, 3))
+    is_tri = lights["type"][li] == 2  # LUMO_OBJ_TRIANGLE
+    tb = lights["tri_base"][li[is_tri]]
+    vi = np.stack([tris["v"][tb][:, k] for k in range(3)], 1)
+    a, b, c = v[vi[:, 0]], v[vi[:, 1]], v[vi[:, 2]]
+    u = rng.uniform(size=(len(tb), 2))
+    s = np.sqrt(u[:, :1])
+    p = (1 - s) * a + s * (1 - u[:, 1:]) * b + s * u[:, 1:] * c
+    d[is_tri] = p - o[is_tri]
+    return o, d / np.linalg.norm(d, axis=1, keepdims=True), li
+
+
+def _trace_cmp(dev, sc, o, d, lights=None):
+    dev.upload(sc)
+    before = dev.stats()
+    g = dev.trace(o, d, lights)
+    after = dev.stats()
+    t, kind, obj, cnt = O.trace(sc.desc(), o, d, lights)
+    np.testing.assert_array_equal(g[0], t)
+    np.testing.assert_array_equal(g[1], kind)
+    np.testing.assert_array_equal(g[2], obj)
+    k = 0 if lights is None else 1
+    got = [after.aabb_tests[k] - before.aabb_tests[k], after.kd_nodes[k] - before.kd_nodes[k],
+           after.tri_tests[k] - before.tri_tests[k]]
+    assert got == [cnt.aabb_tests, cnt.kd_nodes, cnt.tri_tests]
+    return g
+
+
+@pytest.mark.parametrize("which", ["c2", "c3"])
+def test_trace_closest_full_scale(dev, which, request):
+    sc = request.getfixturevalue(which)
+    eye = (0.0, 0.0, 0.0) if which == "c2" else (-16.0, 5.0, -1.0)
+    o, d = _closest_rays(sc.desc(), eye, 1 << 20, 11)
+    g = _trace_cmp(dev, sc, o, d)
+    info = dev.scene_info()
+    assert info.stack_class == (48 if which == "c2" else 24)
+    assert np.mean(g[1] > 0) > 0.3
+
+
+@pytest.mark.parametrize("which", ["c2", "c3"])
+def test_trace_visibility_full_scale(dev, which, request):
+    sc = request.getfixturevalue(which)
+    o, d, li = _visibility_rays(sc.desc(), 1 << 20, 12)
+    g = _trace_cmp(dev, sc, o, d, lights=li)
+    assert 0.001 < np.mean(g[1] == 2) < 0.999
+
+
+def _paths(dev, sc, cam, task):
+    dev.upload(sc, cam)
+    g = gpu_paths(dev, task)
+    o = O.trace_paths(sc.desc(), cam.desc, task)
+    for k in ("depth", "raster", "lam", "radiance", "delta"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+    return g
+
+
+@pytest.mark.parametrize("which", ["c2", "c3"])
+def test_paths_full_scale_bench_camera(dev, which, request):
+    """Two tiles of the bench frame (1920x1080, the bench camera): one central, one off-centre."""
+    sc = request.getfixturevalue(which)
+    cam = scenes.default_camera((1920, 1080)) if which == "c2" else scenes.bistro_camera((1920, 1080))
+    tasks = L.make_tasks(1920, 1080, 4, SEED)
+    tiles_x = 1920 // 16
+    for ty, tx in ((34, 60), (20, 35)):
+        g = _paths(dev, sc, cam, tasks[ty * tiles_x + tx])
+        assert (g["depth"] > 1).any()
+
+
+# ---------------------------------------------------------------------------- kernel variants
+@pytest.fixture
+def variant_env():
+    saved = {k: os.environ.get(k) for k in ("LUMO_STACK_CLASS", "LUMO_FULL_KERNELS")}
+    yield
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    _ffi.load().lumo_set_lds_staging(1)
+
+
+def _variant_scene(name):
+    if name == "cornell":
+        return L.Scene.cornell_box(), L.Camera.cornell_box((48, 48)), L.make_tasks(48, 48, 8, SEED)
+    sc = scenes.dragon(torus_knot_tube(300, 12))
+    return sc, scenes.default_camera((48, 32)), L.make_tasks(48, 32, 8, SEED)
+
+
+@pytest.mark.parametrize("full", [0, 1])
+@pytest.mark.parametrize("lds", [1, 0])
+@pytest.mark.parametrize("cls", CLASSES)
+@pytest.mark.parametrize("name", ["cornell", "small_dragon"])
+def test_kernel_variants(dev, variant_env, name, cls, lds, full):
+    sc, cam, tasks = _variant_scene(name)
+    sc.build()
+    os.environ["LUMO_STACK_CLASS"] = str(cls)
+    os.environ["LUMO_FULL_KERNELS"] = str(full)
+    _ffi.load().lumo_set_lds_staging(lds)
+    dev.upload(sc, cam)
+    info = dev.scene_info()
+    if info.stack_class != cls:
+        # the override never goes below the scene's need (kdtree.rs:110 stack bound)
+        assert info.stack_class > cls
+        pytest.skip(f"stack class {cls} below the scene's need ({info.stack_class})")
+    assert (info.lds_bytes > 0) == (lds == 1 and name == "cornell")  # the dragon mesh exceeds 48 KiB
+    assert info.full_kernels == (1 if (full or name == "small_dragon") else 0)
+    g = gpu_paths(dev, tasks[1])
+    o = O.trace_paths(sc.desc(), cam.desc, tasks[1])
+    for k in ("depth", "raster", "lam", "radiance", "delta"):
+        np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+    sub = list(tasks)[:6]
+    bufs, res = dev.render_tasks(sub)
+    obufs, ores, _ = O.render_tasks(sc.desc(), cam.desc, sub, O.WAVEFRONT, 8)
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)

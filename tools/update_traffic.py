@@ -1,14 +1,15 @@
 """Copy a tools/profile.sh run into profiles/<round>/ and refresh profiles/pmc_traffic.json
 (HBM bytes per launch per kernel, read by bench.py's roofline).
-Usage: python tools/update_traffic.py gpurun_out/prof/<tag> <round>"""
+Usage: python tools/update_traffic.py gpurun_out/prof/<tag> <round> [workload=c1]"""
 import json
 import os
 import shutil
 import sys
 
 src, rnd = sys.argv[1], sys.argv[2]
+workload = sys.argv[3] if len(sys.argv) > 3 else "c1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-dst = os.path.join(ROOT, "profiles", rnd)
+dst = os.path.join(ROOT, "profiles", rnd, workload)
 os.makedirs(dst, exist_ok=True)
 summary = json.load(open(os.path.join(src, "summary.json")))
 shutil.copy(os.path.join(src, "summary.json"), os.path.join(dst, "rocprof_summary.json"))
@@ -17,12 +18,25 @@ for name in ("bench_trace.json", "bench_fetch.json", "bench_write.json"):
     p = os.path.join(src, name)
     if os.path.exists(p):
         shutil.copy(p, os.path.join(dst, name.replace("bench_", "bench_under_rocprof_")))
-out = {"source": f"profiles/{rnd}/rocprof_summary.json (tools/profile.sh: separate FETCH_SIZE and WRITE_SIZE "
-                  "passes, no traces)",
-       "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE counts half of wide coalesced reads, "
-                     "MI355X_MICROARCH.md HBM section); raw = FETCH_SIZE + WRITE_SIZE. Bytes per launch."}
+path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+try:
+    table = json.load(open(path))
+except (OSError, ValueError):
+    table = {}
+table["correction"] = ("hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE counts half of wide coalesced reads, "
+                       "MI355X_MICROARCH.md HBM section); raw = FETCH_SIZE + WRITE_SIZE. Bytes per launch.")
+out = {"source": f"profiles/{rnd}/{workload}/rocprof_summary.json (tools/profile.sh: separate FETCH_SIZE and "
+                 "WRITE_SIZE passes, no traces)"}
 for k, v in summary.items():
     if k.startswith("k_") and "hbm_bytes_per_launch" in v:
         out[k] = {kk: v[kk] for kk in ("hbm_bytes_per_launch", "hbm_bytes_per_launch_raw", "avg_us", "launches")}
-json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1, sort_keys=True)
+if "k_bdpt_trace_a" in out and "k_bdpt_vis" in out:  # bench.py's BDPT connection unit: both kernels
+    a, b = out["k_bdpt_trace_a"], out["k_bdpt_vis"]
+    n = a["launches"] + b["launches"]
+    out["k_bdpt_trace_a+k_bdpt_vis"] = {
+        kk: (a[kk] * a["launches"] + b[kk] * b["launches"]) / n
+        for kk in ("hbm_bytes_per_launch", "hbm_bytes_per_launch_raw", "avg_us")}
+    out["k_bdpt_trace_a+k_bdpt_vis"]["launches"] = n
+table[workload] = out
+json.dump(table, open(path, "w"), indent=1, sort_keys=True)
 print("updated", dst)
