@@ -580,13 +580,16 @@ template <int STK, bool FX>
 __device__ __forceinline__ int shape_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                              double t_max, Counters& C, DHit& out) {
     if constexpr (FX) {
-        if (ob.type == LUMO_OBJ_TRIANGLE)
+        if (ob.type == LUMO_OBJ_TRIANGLE) {
+            C.tri++;  // the GEO test counts as a triangle test (triangle.rs:63, as the oracle counts it)
             return tri_hit_geo<false>(sc, ob.tri_base, r, t_min, t_max, out) ? ob.tri_base : -1;
+        }
         if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit<false>(ob, r, t_min, t_max, out) ? PRIM_SPHERE : -1;
     }
     int idx = -1;
     kd_traverse<true, STK>(sc, ob, r, t_min, t_max, &idx, C);
     if (idx < 0) return -1;
+    C.tri++;
     if (!tri_hit_geo<false>(sc, ob.tri_base + idx, r, t_min, t_max, out)) return -1;
     return ob.tri_base + idx;
 }
