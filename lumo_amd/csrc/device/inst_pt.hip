@@ -22,13 +22,24 @@ void launch_closest(const TravLaunch& l, const DScene& sc, const Paths& S, const
 }
 
 template <int STK>
-void launch_shadow(const TravLaunch& l, const DScene& sc, const Paths& S, uint32_t seg) {
+void launch_closest_q(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& cur) {
     if (l.lds) {
-        if (l.fx) k_shadow<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, seg);
-        else k_shadow<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, seg);
+        if (l.fx) k_closest_q<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, cur);
+        else k_closest_q<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, cur);
     } else {
-        if (l.fx) k_shadow<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, seg);
-        else k_shadow<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, seg);
+        if (l.fx) k_closest_q<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, cur);
+        else k_closest_q<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, cur);
+    }
+}
+
+template <int STK>
+void launch_shadow_q(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& nxt) {
+    if (l.lds) {
+        if (l.fx) k_shadow_q<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, nxt);
+        else k_shadow_q<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, nxt);
+    } else {
+        if (l.fx) k_shadow_q<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, nxt);
+        else k_shadow_q<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, nxt);
     }
 }
 
@@ -40,7 +51,8 @@ void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, c
 }
 
 template void launch_closest<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const int32_t*);
-template void launch_shadow<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, uint32_t);
+template void launch_closest_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const QState&);
+template void launch_shadow_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const QState&);
 template void launch_trace<LUMO_STK>(int, hipStream_t, const DScene&, const double*, const double*, const int32_t*,
                                      int, int, double*, int32_t*, int32_t*, int32_t*, unsigned long long*);
 

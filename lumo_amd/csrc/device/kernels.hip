@@ -75,11 +75,19 @@ __device__ __forceinline__ uint64_t wf_path_seed(uint64_t pixel_seed, uint64_t k
 }
 
 // ------------------------------------------------------------------ camera (pass `pass`)
+// QUEUE (path tracer): the camera paths enter the queue-order state qs[0]; otherwise (BDPT) the
+// ray, throughput, wavelengths and RNG stay per slot and the slot ids are queued in q0.
+template <bool QUEUE>
 __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, int n, int dim_stride, uint32_t pass) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     bool active = false;
+    Ray ray{V3{0, 0, 0}, V3{0, 0, 0}};
+    double L[NS] = {0.0, 0.0, 0.0, 0.0};
+    Xorshift r{0, 0};
+    int task = 0;
     if (s < n) {
-        const lumo_tile_task& t = T.t[S.task[s]];
+        task = S.task[s];
+        const lumo_tile_task& t = T.t[task];
         active = pass < t.samples;
         S.p_valid[s] = active ? 1u : 0u;
         if (active) {
@@ -103,7 +111,7 @@ __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, in
             const V2 xy = V2{(double)(t.px_min[0] + (uint64_t)j % W), (double)(t.px_min[1] + (uint64_t)j / W)};
             const V2 raster = xy + (offset0 + offset1 + rsq);
             // Integrator::integrate: lens sample (2 draws), then wavelengths (1 draw)
-            Xorshift r = xs_new(wf_path_seed(S.pseed[s], pass));
+            r = xs_new(wf_path_seed(S.pseed[s], pass));
             const V2 lens = xs_vec2(r);
             const V3 screen = xf_pt_inv(cam.sctr, V3{raster.x, raster.y, 0.0});
             const V3 wl0 = normalize(xf_pt_inv(cam.cts, screen));
@@ -115,24 +123,44 @@ __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, in
                 xo_local = xo_local + lz;
                 wi_local = focus - lz;
             }
-            const Ray ray = ray_new(xf_pt_inv(cam.wtc, xo_local), xf_dir_inv(cam.wtc, wi_local));
-            double L[NS];
+            ray = ray_new(xf_pt_inv(cam.wtc, xo_local), xf_dir_inv(cam.wtc, wi_local));
             wl_sample(xs_float(r), L);
-            stv3(S.ro, s, ray.o);
-            stv3(S.rd, s, ray.d);
-            stc(S.gath, s, cfill(1.0));
-            stc(S.rad, s, cfill(0.0));
-            for (int i = 0; i < NS; ++i) S.lam[4 * s + i] = L[i];
             S.raster[2 * s] = raster.x;
             S.raster[2 * s + 1] = raster.y;
-            S.rng[2 * s] = r.hi;
-            S.rng[2 * s + 1] = r.lo;
-            S.depth[s] = 0;
-            S.flags[s] = 1u;  // last_specular
-            S.queries[s] = 0;
+            if (!QUEUE) {
+                stv3(S.ro, s, ray.o);
+                stv3(S.rd, s, ray.d);
+                stc(S.gath, s, cfill(1.0));
+                stc(S.rad, s, cfill(0.0));
+                for (int i = 0; i < NS; ++i) S.lam[4 * s + i] = L[i];
+                S.rng[2 * s] = r.hi;
+                S.rng[2 * s + 1] = r.lo;
+                S.depth[s] = 0;
+                S.flags[s] = 1u;  // last_specular
+                S.queries[s] = 0;
+            }
         }
     }
-    block_append(active, s, S.q0, S.counts + CNT_NEXT);
+    if (QUEUE) {
+        const uint32_t q = block_slot(active, S.counts + CNT_NEXT);
+        if (active) {
+            const QState& Q = S.qs[0];
+            qv3(Q, QD_O, q, ray.o);
+            qv3(Q, QD_D, q, ray.d);
+            qc(Q, QD_G, q, cfill(1.0));
+            qc(Q, QD_R, q, cfill(0.0));
+            for (int i = 0; i < NS; ++i) Q.D(QD_L + i, q) = L[i];
+            Q.R(0, q) = r.hi;
+            Q.R(1, q) = r.lo;
+            Q.I(QI_SLOT, q) = s;
+            Q.I(QI_TASK, q) = task;
+            Q.I(QI_DEPTH, q) = 0;
+            Q.I(QI_FLAGS, q) = QF_SPECULAR;  // last_specular starts true (path_trace.rs:14)
+            Q.I(QI_QUERIES, q) = 0;
+        }
+    } else {
+        block_append(active, s, S.q0, S.counts + CNT_NEXT);
+    }
 }
 
 // Start of a bounce: the alive queue just built becomes the current one.
@@ -140,8 +168,8 @@ __global__ void k_bounce_begin(uint32_t* counts) {
     if (threadIdx.x == 0) {
         counts[CNT_CUR] = counts[CNT_NEXT];
         counts[CNT_NEXT] = 0;
+        counts[CNT_SHADOW] = 0;
         counts[CNT_RESOLVE] = 0;
-        for (int b = 0; b < NB; ++b) counts[CNT_BUCKET0 + b] = 0;
     }
 }
 
@@ -558,7 +586,8 @@ enum WorkId {
     W_BD_FILM, W_BD_SCAN, W_BD_REDO_LIST, W_BD_REDO_INDEX, W_BDR_LD, W_BDR_LI, W_BDR_CD, W_BDR_CI, W_BDR_SP,
     W_BDR_SPN, W_BD_NL, W_BD_NC, W_BD_NITEMS, W_BD_IOFF, W_BD_DRAWS, W_BD_OK, W_BD_ITOTAL, W_BD_TERM, W_BD_PDF, W_BD_WDEPTH,
     W_BD_CAMO, W_BD_CAMD, W_BD_RNG0, W_BD_LAM0, W_BDR_DRAWS, W_BDR_OK, W_BD_NB, W_BD_OFFB, W_BD_TERMB, W_BD_VIS, W_BD_AT, W_BD_AKIND, W_BD_AOBJ,
-    W_BD_ATRI, W_CHECKS, W_COUNT
+    W_BD_ATRI, W_CHECKS, W_QS0_D, W_QS0_R, W_QS0_I, W_QS1_D, W_QS1_R, W_QS1_I, W_HQ_T, W_HQ_I, W_SQ_D, W_SQ_I,
+    W_SQ_HD, W_SQ_HI, W_COUNT
 };
 
 template <typename T>
@@ -642,7 +671,7 @@ void by_stack_class(int cls, F&& f) {
 // Traversal launch: stack class x LDS staging.  With LDS staging the grid is capped (persistent
 // grid-stride loop) so each workgroup copies the packed scene once per launch.
 bool g_lds = true;
-int g_buckets = NB;  // LUMO_BUCKETS=0: a single resolve bucket
+int g_buckets = NB;  // LUMO_BUCKETS=0: NEE records not grouped by origin object
 template <typename F>
 void launch_trav(Ctx& c, uint64_t count, F&& f) {
     const bool lds = g_lds && c.sc.hot_bytes > 0;
@@ -680,21 +709,17 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     first[n_tasks] = (int32_t)task_of.size();
     const int N = (int)task_of.size();
     const int ns = c.sc.n_shadow;
-    const size_t R = (size_t)N * 2 * ns;
     const int dim_stride = (int)std::ceil(std::sqrt((double)max_total));
     if (dim_stride > 65535) return LUMO_ERR_INVALID;
 
     lumo_status st = LUMO_OK;
+    const bool bdpt = c.integrator == LUMO_INTEGRATOR_BDPT;
     Paths S{};
-    S.ro = wbuf<double>(c, W_RO, 3 * (size_t)N, st);
-    S.rd = wbuf<double>(c, W_RD, 3 * (size_t)N, st);
-    S.gath = wbuf<double>(c, W_GATH, 4 * (size_t)N, st);
+    // per slot: camera sampler, raster, final values; BDPT also its walk state
     S.rad = wbuf<double>(c, W_RAD, 4 * (size_t)N, st);
     S.lam = wbuf<double>(c, W_LAM, 4 * (size_t)N, st);
     S.raster = wbuf<double>(c, W_RASTER, 2 * (size_t)N, st);
-    S.rng = wbuf<uint64_t>(c, W_RNG, 2 * (size_t)N, st);
     S.depth = wbuf<uint32_t>(c, W_DEPTH, N, st);
-    S.flags = wbuf<uint32_t>(c, W_FLAGS, N, st);
     S.queries = wbuf<uint32_t>(c, W_QUERIES, N, st);
     S.task = wbuf<int32_t>(c, W_TASK, N, st);
     S.pix = wbuf<int32_t>(c, W_PIX, N, st);
@@ -702,28 +727,42 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     S.mj_rng = wbuf<uint64_t>(c, W_MJRNG, 2 * (size_t)N, st);
     S.mj_state = wbuf<uint64_t>(c, W_MJSTATE, N, st);
     S.perm = wbuf<uint16_t>(c, W_PERM, 2 * (size_t)dim_stride * N, st);
-    S.hit_t = wbuf<double>(c, W_HIT_T, N, st);
-    S.hit_kind = wbuf<int32_t>(c, W_HIT_KIND, N, st);
-    S.hit_obj = wbuf<int32_t>(c, W_HIT_OBJ, N, st);
-    S.hit_tri = wbuf<int32_t>(c, W_HIT_TRI, N, st);
-    S.sh_o = wbuf<double>(c, W_SH_O, 3 * R, st);
-    S.sh_d = wbuf<double>(c, W_SH_D, 3 * R, st);
-    S.sh_f = wbuf<double>(c, W_SH_F, 4 * R, st);
-    S.sh_psct = wbuf<double>(c, W_SH_PSCT, R, st);
-    S.sh_cos = wbuf<double>(c, W_SH_COS, R, st);
-    S.sh_light = wbuf<int32_t>(c, W_SH_LIGHT, R, st);
-    S.sh_flags = wbuf<int32_t>(c, W_SH_FLAGS, R, st);
-    S.g_sh = wbuf<double>(c, W_G_SH, 4 * (size_t)N, st);
-    S.pdf_l = wbuf<double>(c, W_PDF_L, (size_t)ns * N, st);
+    if (bdpt) {
+        S.ro = wbuf<double>(c, W_RO, 3 * (size_t)N, st);
+        S.rd = wbuf<double>(c, W_RD, 3 * (size_t)N, st);
+        S.gath = wbuf<double>(c, W_GATH, 4 * (size_t)N, st);
+        S.rng = wbuf<uint64_t>(c, W_RNG, 2 * (size_t)N, st);
+        S.flags = wbuf<uint32_t>(c, W_FLAGS, N, st);
+        S.hit_t = wbuf<double>(c, W_HIT_T, N, st);
+        S.hit_kind = wbuf<int32_t>(c, W_HIT_KIND, N, st);
+        S.hit_obj = wbuf<int32_t>(c, W_HIT_OBJ, N, st);
+        S.hit_tri = wbuf<int32_t>(c, W_HIT_TRI, N, st);
+        S.q0 = wbuf<int32_t>(c, W_Q0, N, st);
+        S.q1 = wbuf<int32_t>(c, W_Q1, N, st);
+    } else {
+        // path tracer: queue-order state (ping-pong), hits, NEE records (state.h)
+        const size_t cap = (size_t)N;
+        for (int k = 0; k < 2; ++k) {
+            S.qs[k].cap = cap;
+            S.qs[k].d = wbuf<double>(c, k ? W_QS1_D : W_QS0_D, QD_N * cap, st);
+            S.qs[k].r = wbuf<uint64_t>(c, k ? W_QS1_R : W_QS0_R, 2 * cap, st);
+            S.qs[k].i = wbuf<int32_t>(c, k ? W_QS1_I : W_QS0_I, QI_N * cap, st);
+        }
+        S.hq.cap = cap;
+        S.hq.t = wbuf<double>(c, W_HQ_T, cap, st);
+        S.hq.i = wbuf<int32_t>(c, W_HQ_I, 3 * cap, st);
+        S.sq.cap = cap * (size_t)ns;
+        S.sq.hcap = cap;
+        S.sq.d = wbuf<double>(c, W_SQ_D, SD_N * S.sq.cap, st);
+        S.sq.i = wbuf<int32_t>(c, W_SQ_I, SI_N * S.sq.cap, st);
+        S.sq.hd = wbuf<double>(c, W_SQ_HD, SH_N * cap, st);
+        S.sq.hi = wbuf<int32_t>(c, W_SQ_HI, SHI_N * cap, st);
+    }
     S.p_rgb = wbuf<double>(c, W_P_RGB, 3 * (size_t)N, st);
     S.p_lum = wbuf<double>(c, W_P_LUM, N, st);
     S.p_cost = wbuf<uint32_t>(c, W_P_COST, N, st);
     S.p_valid = wbuf<uint32_t>(c, W_P_VALID, N, st);
     S.film = wbuf<double>(c, W_FILM, 4 * (size_t)N, st);
-    S.q0 = wbuf<int32_t>(c, W_Q0, N, st);
-    S.q1 = wbuf<int32_t>(c, W_Q1, N, st);
-    const uint32_t rq_seg = (uint32_t)N;
-    S.rq = wbuf<int32_t>(c, W_RQ, (size_t)(g_buckets > 1 ? NB : 1) * N, st);
     S.counts = wbuf<uint32_t>(c, W_COUNTS, CNT_N, st);
     S.tcount = wbuf<unsigned long long>(c, W_TCOUNT, 2 * TC_N, st);
     S.checks = wbuf<unsigned long long>(c, W_CHECKS, 3, st);
@@ -747,7 +786,6 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         D.depth = wbuf<unsigned long long>(c, W_DUMP_DEPTH, m, st);
         D.delta = wbuf<double>(c, W_DUMP_DELTA, dump_samples, st);
     }
-    const bool bdpt = c.integrator == LUMO_INTEGRATOR_BDPT;
     Bdpt B{}, BR{};  // BR: redo storage for subpaths longer than B holds
     BItems BI{};     // connection work items
     uint32_t* items_total = nullptr;
@@ -844,11 +882,15 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));
         {
             StageTimer tm(c, g_timing, ST_CAMERA);
-            k_camera<<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass);
+            if (bdpt)
+                k_camera<false><<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass);
+            else
+                k_camera<true><<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass);
         }
         HIPCHK(hipGetLastError());
-        // Bounce loop over the alive queue (q0 filled by the producer just launched): k_closest, then
-        // `step` (the integrator's per-hit kernels).  Bounces are enqueued ahead of the host's
+        // Bounce loop over the alive queue (filled by the producer just launched): `step` launches
+        // the bounce's kernels (closest hit, then the integrator's per-hit kernels) for bounce
+        // `b` (its parity selects the ping-pong buffers).  Bounces are enqueued ahead of the host's
         // knowledge of the counts; see above.
         auto bounce_loop = [&](auto&& step) -> lumo_status {
             int32_t* qa = S.q0;
@@ -873,11 +915,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 }
                 if (done) break;
                 k_bounce_begin<<<1, 64, 0, sm>>>(S.counts);
-                {
-                    StageTimer tm(c, g_timing, ST_CLOSEST);
-                    launch_trav(c, ub, [&](auto K, const TravLaunch& l) { launch_closest<decltype(K)::value>(l, c.sc, S, qa); });
-                }
-                step(ub, qa, qb);
+                step(ub, issued, qa, qb);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipMemcpyAsync(c.snap + CNT_N * (issued % Ctx::SNAP_RING), S.counts, sizeof(uint32_t) * CNT_N,
                                       hipMemcpyDeviceToHost, sm));
@@ -893,18 +931,24 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         };
         lumo_status bst = LUMO_OK;
         if (!bdpt) {
-            bst = bounce_loop([&](uint32_t ub, int32_t* qa, int32_t* qb) {
+            bst = bounce_loop([&](uint32_t ub, int b, int32_t*, int32_t*) {
+                const QState& cur = S.qs[b & 1];
+                const QState& nxt = S.qs[(b + 1) & 1];
+                {
+                    StageTimer tm(c, g_timing, ST_CLOSEST);
+                    launch_trav(c, ub, [&](auto K, const TravLaunch& l) { launch_closest_q<decltype(K)::value>(l, c.sc, S, cur); });
+                }
                 {
                     StageTimer tm(c, g_timing, ST_SHADE);
                     if (c.sc.full)
-                        k_shade<true><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb, rq_seg, g_buckets);
+                        k_shade_q<true><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
                     else
-                        k_shade<false><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, qa, qb, rq_seg, g_buckets);
+                        k_shade_q<false><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
                 }
                 {
                     StageTimer tm(c, g_timing, ST_SHADOW);
                     launch_trav(c, (uint64_t)ub * (uint32_t)ns,
-                                [&](auto K, const TravLaunch& l) { launch_shadow<decltype(K)::value>(l, c.sc, S, rq_seg); });
+                                [&](auto K, const TravLaunch& l) { launch_shadow_q<decltype(K)::value>(l, c.sc, S, nxt); });
                 }
             });
             if (bst) return bst;
@@ -913,7 +957,11 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             // + k_bdpt_step; re-runs of samples that did not fit; connection items; fold.  Stage
             // slots: walks = CLOSEST + SHADE, items = SHADOW, re-runs + fold = RESOLVE.
             auto walk_step = [&](int mode) {
-                return [&, mode](uint32_t ub, int32_t* qa, int32_t* qb) {
+                return [&, mode](uint32_t ub, int, int32_t* qa, int32_t* qb) {
+                    {
+                        StageTimer tm(c, g_timing, ST_CLOSEST);
+                        launch_trav(c, ub, [&](auto K, const TravLaunch& l) { launch_closest<decltype(K)::value>(l, c.sc, S, qa); });
+                    }
                     StageTimer tm(c, g_timing, ST_SHADE);
                     by_stack_class(c.sc.stack_class, [&](auto K) {
                         launch_bdpt_step<decltype(K)::value>(ceil_div(ub, BLOCK), sm, c.sc.full != 0, c.sc, S, T, B, BI, mode, qa, qb);

@@ -24,7 +24,9 @@ struct TravLaunch {
 template <int STK>
 void launch_closest(const TravLaunch& l, const DScene& sc, const Paths& S, const int32_t* queue);
 template <int STK>
-void launch_shadow(const TravLaunch& l, const DScene& sc, const Paths& S, uint32_t seg);
+void launch_closest_q(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& cur);
+template <int STK>
+void launch_shadow_q(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& nxt);
 template <int STK>
 void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, const double* d, const int32_t* light,
                   int n, int any_hit, double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
@@ -45,7 +47,8 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
 
 #define LUMO_EXTERN_STK(K)                                                                                        \
     extern template void launch_closest<K>(const TravLaunch&, const DScene&, const Paths&, const int32_t*);        \
-    extern template void launch_shadow<K>(const TravLaunch&, const DScene&, const Paths&, uint32_t);               \
+    extern template void launch_closest_q<K>(const TravLaunch&, const DScene&, const Paths&, const QState&);       \
+    extern template void launch_shadow_q<K>(const TravLaunch&, const DScene&, const Paths&, const QState&);        \
     extern template void launch_trace<K>(int, hipStream_t, const DScene&, const double*, const double*,          \
                                          const int32_t*, int, int, double*, int32_t*, int32_t*, int32_t*,         \
                                          unsigned long long*);                                                    \

@@ -1,6 +1,7 @@
 // Path-tracing wavefront kernels (integrator.rs:45-184, path_trace.rs:5-82, scene.rs:119-189)
 // as templates over the kd stack class STK, LDS staging and the feature class FX.  The
-// traversal kernels are instantiated per stack class in inst_pt.hip; k_shade in kernels.hip.
+// traversal kernels are instantiated per stack class in inst_pt.hip; k_shade_q in kernels.hip.
+// k_closest (slot-indexed queue of slot ids) serves the BDPT subpath walks.
 #pragma once
 #include "state.h"
 
@@ -28,200 +29,274 @@ __global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc
     flush_counters(C, S.tcount);
 }
 
-// ------------------------------------------------------------------ shade
-// One path's bounce: hit record, emission, BSDF sample, NEE records, RR, spawn.
-template <bool FX>
-__device__ __forceinline__ void shade_one(const DScene& sc, const Paths& S, const Tasks& T, int s, bool& alive,
-                                          bool& resolve) {
-    const int ns = sc.n_shadow;
-    int n_sh = 0;
-    {
-        const int kind = S.hit_kind[s];
-        if (kind != 0) {
-            const Ray ro{ldv3(S.ro, s), ldv3(S.rd, s)};
-            const HitRef hr{S.hit_t[s], kind, S.hit_obj[s], S.hit_tri[s]};
-            DHit ho;
-            hit_record<FX>(sc, hr, rayx(ro), ho);
-            const lumo_material m = sc.mats[ho.material];
-            Xorshift rng{S.rng[2 * s], S.rng[2 * s + 1]};
-            double L[NS];
-            for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
-            DColor gathered = ldc(S.gath, s);
-            DColor radiance = ldc(S.rad, s);
-            const V3 wo = -ro.d;
-            const double rand_u = xs_float(rng);
-            const V2 sq = xs_vec2(rng);
-            V3 wi;
-            const bool sampled = bsdf_sample<FX>(sc, m, ho, wo, L, rand_u, sq, wi);
-            if (m.kind == LUMO_MAT_MF_DIELECTRIC && !(m.flags & LUMO_MATF_CONSTANT_ETA)) {
-                for (int i = 1; i < NS; ++i) S.lam[4 * s + i] = 0.0;  // lambda terminated (even if None)
-            }
-            if (!sampled) {
-                if (S.flags[s] & 1u) radiance = radiance + gathered * emit(sc, m, L, ho.backface);
-                stc(S.rad, s, radiance);
-            } else {
-                // NEE: n_shadow x [light pick, light direction, BSDF sample] (integrator.rs:87-137)
-                if (!mat_is_delta<FX>(sc, m, L)) {
-                    const int base = s * 2 * ns;
-                    for (int i = 0; i < ns; ++i) {
-                        const int li = sample_light(sc, xs_float(rng));
-                        const lumo_object& Lo = sc.lights[li];
-                        S.pdf_l[s * ns + i] = sc.alias_pdf[li];
-                        {
-                            const V2 rs = xs_vec2(rng);
-                            const V3 w = light_sample_towards<FX>(sc, Lo, ho.p, rs);
-                            const Ray ri = spawn(ho, w);
-                            const int rec = base + 2 * i;
-                            stv3(S.sh_o, rec, ri.o);
-                            stv3(S.sh_d, rec, ri.d);
-                            stc(S.sh_f, rec, bsdf_f<FX>(sc, m, ho, wo, w, L));
-                            S.sh_psct[rec] = bsdf_pdf<FX>(sc, m, ho, wo, w, L);
-                            S.sh_cos[rec] = shading_cosine(m, w, ho.ns);
-                            S.sh_light[rec] = li;
-                            S.sh_flags[rec] = 1 | 2;  // valid | light-sampled
-                            n_sh++;
-                        }
-                        {
-                            const double ru = xs_float(rng);
-                            const V2 rsq = xs_vec2(rng);
-                            V3 w;
-                            const int rec = base + 2 * i + 1;
-                            if (bsdf_sample<FX>(sc, m, ho, wo, L, ru, rsq, w)) {
-                                const Ray ri = spawn(ho, w);
-                                stv3(S.sh_o, rec, ri.o);
-                                stv3(S.sh_d, rec, ri.d);
-                                stc(S.sh_f, rec, bsdf_f<FX>(sc, m, ho, wo, w, L));
-                                S.sh_psct[rec] = bsdf_pdf<FX>(sc, m, ho, wo, w, L);
-                                S.sh_cos[rec] = shading_cosine(m, w, ho.ns);
-                                S.sh_light[rec] = li;
-                                S.sh_flags[rec] = 1;
-                                n_sh++;
-                            } else {
-                                S.sh_flags[rec] = 0;
-                            }
-                        }
-                    }
-                    stc(S.g_sh, s, gathered);
-                    resolve = true;
-                }
-                // spawn the continuation (path_trace.rs:42-77)
-                const Ray ri = spawn(ho, wi);
-                const V3 wi2 = ri.d;
-                const double p_scatter = bsdf_pdf<FX>(sc, m, ho, wo, wi2, L);
-                if (!(p_scatter <= 0.0)) {  // path_trace.rs:47: a NaN pdf continues the path
-                    const DColor bsdf = bsdf_f<FX>(sc, m, ho, wo, wi2, L);
-                    gathered = gathered * (bsdf * shading_cosine(m, wi2, ho.ns) / p_scatter);
-                    bool cont = true;
-                    const uint32_t depth = S.depth[s];
-                    if ((int)depth >= RR_DEPTH) {
-                        const double lum = luminance(sc, gathered, L);
-                        const double rr_prob = rmin(lum / T.delta[S.task[s]], 1.0);
-                        if (xs_float(rng) > rr_prob)
-                            cont = false;
-                        else
-                            gathered = gathered / rr_prob;
-                    }
-                    if (cont) {
-                        S.flags[s] = mat_is_specular<FX>(m) ? 1u : 0u;  // last_specular
-                        S.depth[s] = depth + 1;
-                        stv3(S.ro, s, ri.o);
-                        stv3(S.rd, s, ri.d);
-                        stc(S.gath, s, gathered);
-                        alive = true;
-                    }
-                }
-            }
-            S.rng[2 * s] = rng.hi;
-            S.rng[2 * s + 1] = rng.lo;
-            S.queries[s] += (uint32_t)n_sh;
-        }
-    }
+// ------------------------------------------------------------------ path tracer, queue order
+// One bounce = k_closest_q -> k_shade_q -> k_shadow_q over the compacted queue of live paths.
+// Every kernel reads and writes its per-path data as structure-of-arrays planes in queue order
+// (lane i touches element q + i): the ray queue and path state (QState, ping-pong by bounce), the
+// closest hits (HitQ) and the NEE records (ShadowQ).  Only the camera sampler state and each
+// path's final values (radiance, wavelengths, depth, queries; written when the path ends) are
+// per slot.
+
+__device__ __forceinline__ V3 qv3(const QState& Q, int k, size_t q) { return V3{Q.D(k, q), Q.D(k + 1, q), Q.D(k + 2, q)}; }
+__device__ __forceinline__ void qv3(const QState& Q, int k, size_t q, V3 v) {
+    Q.D(k, q) = v.x;
+    Q.D(k + 1, q) = v.y;
+    Q.D(k + 2, q) = v.z;
+}
+__device__ __forceinline__ DColor qc(const QState& Q, int k, size_t q) {
+    return DColor{{Q.D(k, q), Q.D(k + 1, q), Q.D(k + 2, q), Q.D(k + 3, q)}};
+}
+__device__ __forceinline__ void qc(const QState& Q, int k, size_t q, const DColor& c) {
+    for (int i = 0; i < NS; ++i) Q.D(k + i, q) = c.s[i];
 }
 
-template <bool FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade(DScene sc, Paths S, Tasks T, const int32_t* queue,
-                                                                    int32_t* next_queue, uint32_t seg, int buckets) {
+// Scene::hit (scene.rs:119-147) of every queued ray.
+template <int STK, bool LDS, bool FX>
+__global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest_q(DScene sc0, Paths S, QState cur) {
+    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
-    // grid-stride over whole blocks: block_append needs every thread of the block each round
+    if (count <= blockIdx.x * blockDim.x) return;  // before staging: whole block idle
+    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    const HitQ hq = S.hq;
+    Counters C{0, 0, 0};
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
+        const RayX r = rayx(Ray{qv3(cur, QD_O, q), qv3(cur, QD_D, q)});
+        const HitRef h = scene_hit<STK, FX>(sc, r, C);
+        hq.t[q] = h.t;
+        hq.i[q] = h.kind;
+        hq.i[hq.cap + q] = h.obj;
+        hq.i[2 * hq.cap + q] = h.tri;
+    }
+    flush_counters(C, S.tcount);
+}
+
+// One record of a NEE pair at plane base b (L: SD_LO, B: SD_BO): origin, direction, bsdf_f,
+// bsdf_pdf, shading cosine.
+__device__ __forceinline__ void put_record(const ShadowQ& Q, int b, size_t r, const Ray& ri, const DColor& f, double pdf,
+                                           double cosv) {
+    Q.D(b + 0, r) = ri.o.x;
+    Q.D(b + 1, r) = ri.o.y;
+    Q.D(b + 2, r) = ri.o.z;
+    Q.D(b + 3, r) = ri.d.x;
+    Q.D(b + 4, r) = ri.d.y;
+    Q.D(b + 5, r) = ri.d.z;
+    for (int k = 0; k < NS; ++k) Q.D(b + 6 + k, r) = f.s[k];
+    Q.D(b + 10, r) = pdf;
+    Q.D(b + 11, r) = cosv;
+}
+
+// The bounce of every queued path (path_trace.rs:18-77): the pending NEE term of the previous
+// bounce, the hit record, emission, BSDF sample, the NEE records of integrator.rs:87-137
+// (n_shadow x [light pick, light direction, BSDF sample]), the continuation and Russian
+// roulette.  Continuing paths are compacted into `nxt`; ending ones write their final values
+// per slot (the radiance after k_shadow_q when the path still has shadow rays pending).
+template <bool FX>
+__global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade_q(DScene sc, Paths S, Tasks T, QState cur, QState nxt,
+                                                                      int buckets) {
+    const uint32_t count = S.counts[CNT_CUR];
+    const int ns = sc.n_shadow;
+    const HitQ hq = S.hq;
+    const ShadowQ sq = S.sq;
+    // grid-stride over whole blocks: the block collectives need every thread of the block each round
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
         const uint32_t q = base + threadIdx.x;
-        bool alive = false, resolve = false;
-        int s = -1;
-        if (q < count) {
-            s = queue[q];
-            shade_one<FX>(sc, S, T, s, alive, resolve);
+        const bool live = q < count;
+        int slot = 0, task = 0, key = 0;
+        uint32_t depth = 0, flags = 0, queries = 0;
+        double L[NS] = {0.0, 0.0, 0.0, 0.0};
+        DColor gathered = cfill(0.0), radiance = cfill(0.0);
+        Xorshift rng{0, 0};
+        Ray ro{V3{0, 0, 0}, V3{0, 0, 0}};
+        DHit ho;
+        lumo_material m{};
+        V3 wo{0, 0, 0}, wi{0, 0, 0};
+        bool sampled = false, resolve = false, alive = false;
+        if (live) {
+            slot = cur.I(QI_SLOT, q);
+            task = cur.I(QI_TASK, q);
+            depth = (uint32_t)cur.I(QI_DEPTH, q);
+            flags = (uint32_t)cur.I(QI_FLAGS, q);
+            queries = (uint32_t)cur.I(QI_QUERIES, q) + 1u;  // this bounce's closest query
+            ro = Ray{qv3(cur, QD_O, q), qv3(cur, QD_D, q)};
+            gathered = qc(cur, QD_G, q);
+            radiance = qc(cur, QD_R, q);
+            if (flags & QF_PENDING) radiance = radiance + qc(cur, QD_P, q);  // previous bounce's NEE
+            for (int i = 0; i < NS; ++i) L[i] = cur.D(QD_L + i, q);
+            rng = Xorshift{cur.R(0, q), cur.R(1, q)};
+            const int kind = hq.i[q];
+            if (kind != 0) {
+                const HitRef hr{hq.t[q], kind, hq.i[hq.cap + q], hq.i[2 * hq.cap + q]};
+                hit_record<FX>(sc, hr, rayx(ro), ho);
+                m = sc.mats[ho.material];
+                wo = -ro.d;
+                const double rand_u = xs_float(rng);
+                const V2 rsq = xs_vec2(rng);
+                sampled = bsdf_sample<FX>(sc, m, ho, wo, L, rand_u, rsq, wi);  // may terminate L
+                if (!sampled) {
+                    if (flags & QF_SPECULAR) radiance = radiance + gathered * emit(sc, m, L, ho.backface);
+                } else {
+                    resolve = !mat_is_delta<FX>(sc, m, L);
+                    if (resolve && buckets > 1) {  // origin object of the shadow rays (objects, then lights)
+                        const int k = kind == 2 ? sc.n_objs + hr.obj : hr.obj;
+                        key = k % NB;
+                    }
+                }
+            }
         }
-        block_append(alive, s, next_queue, S.counts + CNT_NEXT);
-        int b = 0;
-        if (resolve && buckets > 1) {  // origin object of the shadow rays (objects, then lights)
-            const int key = S.hit_kind[s] == 2 ? sc.n_objs + S.hit_obj[s] : S.hit_obj[s];
-            b = key < NB ? key : key % NB;
+        // NEE records (integrator.rs:87-137), grouped by origin object within the block
+        const uint32_t sp = block_slot_sorted(resolve, key, S.counts + CNT_SHADOW);
+        if (resolve) {
+            uint32_t n_sh = 0;
+            for (int i = 0; i < ns; ++i) {
+                const size_t r = (size_t)sp * ns + i;
+                const int li = sample_light(sc, xs_float(rng));
+                const lumo_object& Lo = sc.lights[li];
+                sq.D(SD_PDFL, r) = sc.alias_pdf[li];
+                sq.I(SI_LIGHT, r) = li;
+                {
+                    const V2 rs = xs_vec2(rng);
+                    const V3 w = light_sample_towards<FX>(sc, Lo, ho.p, rs);
+                    put_record(sq, SD_LO, r, spawn(ho, w), bsdf_f<FX>(sc, m, ho, wo, w, L),
+                               bsdf_pdf<FX>(sc, m, ho, wo, w, L), shading_cosine(m, w, ho.ns));
+                    n_sh++;
+                }
+                {
+                    const double ru = xs_float(rng);
+                    const V2 rsq = xs_vec2(rng);
+                    V3 w;
+                    const bool ok = bsdf_sample<FX>(sc, m, ho, wo, L, ru, rsq, w);
+                    sq.I(SI_BVALID, r) = ok ? 1 : 0;
+                    if (ok) {
+                        put_record(sq, SD_BO, r, spawn(ho, w), bsdf_f<FX>(sc, m, ho, wo, w, L),
+                                   bsdf_pdf<FX>(sc, m, ho, wo, w, L), shading_cosine(m, w, ho.ns));
+                        n_sh++;
+                    }
+                }
+            }
+            for (int k = 0; k < NS; ++k) {
+                sq.HD(SH_G + k, sp) = gathered.s[k];
+                sq.HD(SH_L + k, sp) = L[k];
+            }
+            sq.HI(SHI_SLOT, sp) = slot;
+            queries += n_sh;
         }
-        block_append_bucket(resolve, b, s, S.rq, seg, S.counts + CNT_BUCKET0);
+        // continuation (path_trace.rs:42-77)
+        Ray rn = ro;
+        if (sampled) {
+            rn = spawn(ho, wi);
+            const V3 wi2 = rn.d;
+            const double p_scatter = bsdf_pdf<FX>(sc, m, ho, wo, wi2, L);
+            if (!(p_scatter <= 0.0)) {  // path_trace.rs:47: a NaN pdf continues the path
+                const DColor bsdf = bsdf_f<FX>(sc, m, ho, wo, wi2, L);
+                gathered = gathered * (bsdf * shading_cosine(m, wi2, ho.ns) / p_scatter);
+                bool cont = true;
+                if ((int)depth >= RR_DEPTH) {
+                    const double lum = luminance(sc, gathered, L);
+                    const double rr_prob = rmin(lum / T.delta[task], 1.0);
+                    if (xs_float(rng) > rr_prob)
+                        cont = false;
+                    else
+                        gathered = gathered / rr_prob;
+                }
+                alive = cont;
+            }
+        }
+        const uint32_t np = block_slot(alive, S.counts + CNT_NEXT);
+        if (alive) {
+            qv3(nxt, QD_O, np, rn.o);
+            qv3(nxt, QD_D, np, rn.d);
+            qc(nxt, QD_G, np, gathered);
+            qc(nxt, QD_R, np, radiance);
+            for (int i = 0; i < NS; ++i) nxt.D(QD_L + i, np) = L[i];
+            nxt.R(0, np) = rng.hi;
+            nxt.R(1, np) = rng.lo;
+            nxt.I(QI_SLOT, np) = slot;
+            nxt.I(QI_TASK, np) = task;
+            nxt.I(QI_DEPTH, np) = (int32_t)(depth + 1);
+            nxt.I(QI_FLAGS, np) = (mat_is_specular<FX>(m) ? QF_SPECULAR : 0) | (resolve ? QF_PENDING : 0);
+            nxt.I(QI_QUERIES, np) = (int32_t)queries;
+        }
+        if (resolve) {
+            sq.HI(SHI_NEXT, sp) = alive ? (int32_t)np : -1;
+            if (!alive)
+                for (int k = 0; k < NS; ++k) sq.HD(SH_R + k, sp) = radiance.s[k];
+        }
+        if (live && !alive) {  // the path ends here: its final values (FilmSample, path_trace.rs:79-81)
+            for (int i = 0; i < NS; ++i) S.lam[4 * slot + i] = L[i];
+            S.depth[slot] = depth;
+            S.queries[slot] = queries;
+            if (!resolve) stc(S.rad, slot, radiance);  // else k_shadow_q adds the NEE term first
+        }
     }
 }
 
-// ------------------------------------------------------------------ shadow rays (hit_light + MIS + fold)
-// One thread per path of the resolve queue: its 2 n_shadow records in lumo's order
-// (integrator.rs:74-184): per light sample i, single = (light-sampled + BSDF-sampled MIS
-// contributions) / pdf_light, radiance += gathered * sum(single) / n_shadow.  Records whose
-// BSDF sample failed contribute black without a query.
-template <int STK, bool LDS, bool FX>
-__device__ __forceinline__ DColor shadow_record(const DScene& sc, const Paths& S, int s, int rec, Counters& C) {
-    const RayX ri = rayx(Ray{ldv3(S.sh_o, rec), ldv3(S.sh_d, rec)});
-    const int li = S.sh_light[rec];
+// Scene::hit_light + mis_sample of one NEE record (integrator.rs:100-184); plane base b.
+template <int STK, bool FX>
+__device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const ShadowQ& Q, int b, size_t r, bool li_mode,
+                                                  const double* L, Counters& C) {
+    const RayX ri = rayx(Ray{V3{Q.D(b, r), Q.D(b + 1, r), Q.D(b + 2, r)}, V3{Q.D(b + 3, r), Q.D(b + 4, r), Q.D(b + 5, r)}});
+    const int li = Q.I(SI_LIGHT, r);
     DHit hi;
     DColor out = cfill(0.0);
     if (scene_hit_light<STK, FX>(sc, ri, li, hi, C)) {
         const lumo_object& Lo = sc.lights[li];
         const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
-        const double p_sct = S.sh_psct[rec];
+        const double p_sct = Q.D(b + 10, r);
         if (!(p_lig == 0.0 || p_sct == 0.0)) {  // mis_sample (integrator.rs:139-184)
-            double L[NS];
-            for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
-            const bool li_mode = (S.sh_flags[rec] & 2) != 0;
             const double denom = p_lig * p_lig + p_sct * p_sct;
             const double weight = li_mode ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
             const double p_denom = li_mode ? p_lig : p_sct;
             const lumo_material hm = sc.mats[hi.material];
-            out = ldc(S.sh_f, rec) * cfill(1.0) * emit(sc, hm, L, hi.backface) * S.sh_cos[rec] * weight / p_denom;
+            const DColor f{{Q.D(b + 6, r), Q.D(b + 7, r), Q.D(b + 8, r), Q.D(b + 9, r)}};
+            out = f * cfill(1.0) * emit(sc, hm, L, hi.backface) * Q.D(b + 11, r) * weight / p_denom;
         }
     }
     return out;
 }
-// Thread (path, light sample i): single_i = (light-sampled + BSDF-sampled) / pdf_light, staged
-// in LDS; the path's i == 0 thread then folds acc += gathered * single_i in i order and adds
-// acc / n_shadow to the radiance.  A block round covers BLOCK / n_shadow whole paths.
+
+// The path's NEE term radiance += (0 + gathered * single_i ...) / n_shadow (integrator.rs:74-85):
+// into the next bounce's state (folded by its k_shade_q), or straight into the final radiance
+// of a path that ended this bounce.
+__device__ __forceinline__ void deliver_nee(const Paths& S, const ShadowQ& Q, const QState& nxt, uint32_t p,
+                                            const DColor& X) {
+    const int next = Q.HI(SHI_NEXT, p);
+    if (next >= 0) {
+        qc(nxt, QD_P, (size_t)next, X);
+    } else {
+        const DColor R{{Q.HD(SH_R, p), Q.HD(SH_R + 1, p), Q.HD(SH_R + 2, p), Q.HD(SH_R + 3, p)}};
+        stc(S.rad, Q.HI(SHI_SLOT, p), R + X);
+    }
+}
+
+// Thread (path p, light sample i): single_i = (light-sampled + BSDF-sampled) / pdf_light
+// (integrator.rs:87-137); with n_shadow > 1 staged in LDS and folded by the path's i == 0 thread
+// in i order.  A block round covers BLOCK / n_shadow whole paths; the pair records of a round
+// are contiguous.
 template <int STK, bool LDS, bool FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0, Paths S, uint32_t seg) {
+__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc0, Paths S, QState nxt) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     __shared__ DColor singles[BLOCK];
-    uint32_t bc[NB], count = 0;
-    for (int b = 0; b < NB; ++b) {
-        bc[b] = S.counts[CNT_BUCKET0 + b];
-        count += bc[b];
-    }
+    const uint32_t count = S.counts[CNT_SHADOW];
     const int ns = sc0.n_shadow;
     const uint32_t per_block = (uint32_t)(BLOCK / ns);  // paths per block round
     if (count <= blockIdx.x * per_block) return;
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    const ShadowQ Q = S.sq;
     Counters C{0, 0, 0};
     const int i = (int)threadIdx.x % ns;
     for (uint32_t base = blockIdx.x * per_block; base < count; base += gridDim.x * per_block) {
-        const uint32_t q = base + threadIdx.x / ns;
-        const bool mine = threadIdx.x < per_block * ns && q < count;
-        int s = -1;
+        const uint32_t p = base + threadIdx.x / ns;
+        const bool mine = threadIdx.x < per_block * ns && p < count;
         if (mine) {
-            uint32_t r = q;
-            int bk = 0;
-            while (r >= bc[bk]) r -= bc[bk++];  // q < count, so bk < NB
-            s = S.rq[(size_t)bk * seg + r];
-            const int rec = s * 2 * ns + 2 * i;
-            const DColor a = shadow_record<STK, LDS, FX>(sc, S, s, rec, C);
-            const DColor b = (S.sh_flags[rec + 1] & 1) ? shadow_record<STK, LDS, FX>(sc, S, s, rec + 1, C) : cfill(0.0);
-            const DColor single = (cfill(0.0) + a + b) / S.pdf_l[s * ns + i];
+            double L[NS];
+            for (int k = 0; k < NS; ++k) L[k] = Q.HD(SH_L + k, p);
+            const size_t r = (size_t)p * ns + i;
+            const DColor a = shadow_record_q<STK, FX>(sc, Q, SD_LO, r, true, L, C);
+            const DColor b = Q.I(SI_BVALID, r) ? shadow_record_q<STK, FX>(sc, Q, SD_BO, r, false, L, C) : cfill(0.0);
+            const DColor single = (cfill(0.0) + a + b) / Q.D(SD_PDFL, r);
             if (ns == 1) {
-                stc(S.rad, s, ldc(S.rad, s) + (cfill(0.0) + ldc(S.g_sh, s) * single) / 1.0);
+                const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};
+                deliver_nee(S, Q, nxt, p, (cfill(0.0) + g * single) / 1.0);
             } else {
                 singles[threadIdx.x] = single;
             }
@@ -229,10 +304,10 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow(DScene sc0,
         if (ns > 1) {  // uniform over the block
             __syncthreads();
             if (mine && i == 0) {
-                const DColor g = ldc(S.g_sh, s);
+                const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};
                 DColor acc = cfill(0.0);
                 for (int k = 0; k < ns; ++k) acc = acc + g * singles[threadIdx.x + k];
-                stc(S.rad, s, ldc(S.rad, s) + acc / (double)ns);
+                deliver_nee(S, Q, nxt, p, acc / (double)ns);
             }
             __syncthreads();
         }

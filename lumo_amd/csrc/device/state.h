@@ -35,10 +35,10 @@ enum Stage {
 static_assert(ST_COUNT == LUMO_STAGE_COUNT, "stage slots match lumo_stats");
 // Device-side queue counters: the bounce kernels read their counts from here, so the host never
 // waits for a count before launching the next stage.
-enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_BUCKET0, CNT_N = CNT_BUCKET0 + 8 };
-// The resolve queue is split into NB buckets by the shadow rays' origin object so that a wave's
-// visibility queries start on the same surface and walk similar BVH / kd paths (LUMO_BUCKETS=0:
-// one bucket).  Bucket b holds its entries at rq[b * N ...]; k_shadow walks the buckets in order.
+enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_N = 8 };
+// k_shade_q groups a block's NEE records by the shadow rays' origin object (NB keys) so that a
+// wave's visibility queries start on the same surface and walk similar BVH / kd paths
+// (LUMO_BUCKETS=0: one key).
 constexpr int NB = 8;
 enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
 
@@ -51,6 +51,50 @@ struct DCam {
 };
 
 // Path state (SoA)
+// Path-tracer state in queue order (one bounce's live paths, compacted), structure of arrays:
+// plane k of entry q at k * cap + q, so lane i of a wave reads element q + i of every plane.
+enum { QD_O = 0, QD_D = 3, QD_G = 6, QD_R = 10, QD_L = 14, QD_P = 18, QD_N = 22 };  // f64 planes
+enum { QI_SLOT = 0, QI_TASK, QI_DEPTH, QI_FLAGS, QI_QUERIES, QI_N };                   // i32 planes
+enum { QF_SPECULAR = 1, QF_PENDING = 2 };  // last_specular; QD_P holds the previous bounce's NEE term
+struct QState {
+    double* d;    // ray o, d; gathered; radiance; wavelengths; pending NEE term
+    uint64_t* r;  // RNG hi, lo
+    int32_t* i;
+    size_t cap;
+    __device__ __forceinline__ double& D(int k, size_t q) const { return d[(size_t)k * cap + q]; }
+    __device__ __forceinline__ uint64_t& R(int k, size_t q) const { return r[(size_t)k * cap + q]; }
+    __device__ __forceinline__ int32_t& I(int k, size_t q) const { return i[(size_t)k * cap + q]; }
+};
+// Closest hits of the current ray queue, same order.
+struct HitQ {
+    double* t;
+    int32_t* i;  // kind, object, triangle planes
+    size_t cap;
+};
+// NEE records in queue order: per path with shadow rays a header (gathered, wavelengths, radiance
+// of a path that ends this bounce, slot, next-queue position or -1), and per light sample i the
+// pair of records (light-sampled L, BSDF-sampled B) at pair index p * n_shadow + i.
+enum { SD_LO = 0, SD_LD = 3, SD_LF = 6, SD_LPS = 10, SD_LCOS = 11, SD_BO = 12, SD_BD = 15, SD_BF = 18,
+       SD_BPS = 22, SD_BCOS = 23, SD_PDFL = 24, SD_N = 25 };
+enum { SI_LIGHT = 0, SI_BVALID, SI_N };
+enum { SH_G = 0, SH_L = 4, SH_R = 8, SH_N = 12 };
+enum { SHI_SLOT = 0, SHI_NEXT, SHI_N };
+struct ShadowQ {
+    double* d;   // SD_* planes, cap pairs
+    int32_t* i;  // SI_* planes
+    size_t cap;
+    double* hd;   // SH_* planes, hcap paths
+    int32_t* hi;  // SHI_* planes
+    size_t hcap;
+    __device__ __forceinline__ double& D(int k, size_t r) const { return d[(size_t)k * cap + r]; }
+    __device__ __forceinline__ int32_t& I(int k, size_t r) const { return i[(size_t)k * cap + r]; }
+    __device__ __forceinline__ double& HD(int k, size_t p) const { return hd[(size_t)k * hcap + p]; }
+    __device__ __forceinline__ int32_t& HI(int k, size_t p) const { return hi[(size_t)k * hcap + p]; }
+};
+
+// Per-slot state.  The path tracer keeps only the camera sampler state, the raster position and
+// the path's final values here (radiance, wavelengths, depth, queries, written when it ends);
+// BDPT keeps its whole walk state per slot (bdpt.h).
 struct Paths {
     double *ro, *rd, *gath, *rad, *lam, *raster;
     uint64_t *rng;  // 2 per slot: hi, lo
@@ -60,18 +104,18 @@ struct Paths {
     uint16_t* perm;  // 2 * dim per slot
     double* hit_t;
     int32_t *hit_kind, *hit_obj, *hit_tri;
-    // shadow records, R = N * 2 * n_shadow (fixed slot-major layout)
-    double *sh_o, *sh_d, *sh_f, *sh_psct, *sh_cos;
-    int32_t *sh_light, *sh_flags;
-    double *g_sh, *pdf_l;
     // per-pass outputs
     double *p_rgb, *p_lum;
     uint32_t *p_cost, *p_valid;
     double* film;
-    int32_t *q0, *q1, *rq;
+    int32_t *q0, *q1;  // BDPT walk queues (slot ids)
     uint32_t* counts;
     unsigned long long* tcount;  // [2][TC_N]
     unsigned long long* checks;  // sample checks: NaN, negative, large (tone_mapping.rs:42-56)
+    // path tracer: queue-order state (ping-pong by bounce parity), hits, NEE records
+    QState qs[2];
+    HitQ hq;
+    ShadowQ sq;
 };
 
 struct Tasks {
@@ -91,17 +135,21 @@ struct Dump {
 
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)); }
 
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
 // Workgroup-aggregated stream compaction: ballot + mbcnt inside each wave, wave totals scanned
 // in LDS, ONE atomicAdd per workgroup on the queue counter (a single hot counter word
-// saturates near 88 M atomics/s on MI355X, MI355X_MICROARCH.md "dequeue").  Every thread of
-// the block must call it (it synchronises the block).
-__device__ __forceinline__ void block_append(bool pred, int32_t value, int32_t* queue, uint32_t* counter) {
+// saturates near 88 M atomics/s on MI355X, MI355X_MICROARCH.md "dequeue").  Returns this
+// thread's queue position (meaningful when pred), in lane order within the block.  Every
+// thread of the block must call it (it synchronises the block).
+__device__ __forceinline__ uint32_t block_slot(bool pred, uint32_t* counter) {
     __shared__ uint32_t wtot[BLOCK / 64];
     __shared__ uint32_t base_s;
     const uint64_t mask = __ballot(pred);
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    const uint32_t prefix =
-        __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+    const uint32_t prefix = mbcnt64(mask);
     if (lane == 0) wtot[w] = (uint32_t)__popcll(mask);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -114,24 +162,45 @@ __device__ __forceinline__ void block_append(bool pred, int32_t value, int32_t* 
         base_s = t ? atomicAdd(counter, t) : 0u;
     }
     __syncthreads();
-    if (pred) queue[base_s + wtot[w] + prefix] = value;
+    const uint32_t pos = base_s + wtot[w] + prefix;
     __syncthreads();
+    return pos;
+}
+__device__ __forceinline__ void block_append(bool pred, int32_t value, int32_t* queue, uint32_t* counter) {
+    const uint32_t pos = block_slot(pred, counter);
+    if (pred) queue[pos] = value;
 }
 
-// block_append into NB bucket segments of `queue` (stride `seg`): per-block LDS counters, one
-// global atomic per non-empty bucket per block.  Every thread of the block must call it.
-__device__ __forceinline__ void block_append_bucket(bool pred, int bucket, int32_t value, int32_t* queue, uint32_t seg,
-                                                    uint32_t* counters) {
-    __shared__ uint32_t cnt[NB], base_s[NB];
-    if (threadIdx.x < NB) cnt[threadIdx.x] = 0;
+// block_slot with the block's entries grouped by `key` in [0, NB) (a block-local counting sort:
+// one ballot per key per wave), so that consecutive queue entries share the key.  One atomic
+// per block.  Every thread of the block must call it.
+__device__ __forceinline__ uint32_t block_slot_sorted(bool pred, int key, uint32_t* counter) {
+    constexpr int NW = BLOCK / 64;
+    __shared__ uint32_t cnt[NB][NW];
+    __shared__ uint32_t base_s;
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t rank = 0;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const uint64_t m = __ballot(pred && key == b);
+        if (pred && key == b) rank = mbcnt64(m);
+        if (lane == 0) cnt[b][w] = (uint32_t)__popcll(m);
+    }
     __syncthreads();
-    uint32_t local = 0;
-    if (pred) local = atomicAdd(&cnt[bucket], 1u);
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int b = 0; b < NB; ++b)
+            for (int i = 0; i < NW; ++i) {
+                const uint32_t c = cnt[b][i];
+                cnt[b][i] = t;
+                t += c;
+            }
+        base_s = t ? atomicAdd(counter, t) : 0u;
+    }
     __syncthreads();
-    if (threadIdx.x < NB) base_s[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(counters + threadIdx.x, cnt[threadIdx.x]) : 0u;
+    const uint32_t pos = base_s + (pred ? cnt[key][w] : 0u) + rank;
     __syncthreads();
-    if (pred) queue[(size_t)bucket * seg + base_s[bucket] + local] = value;
-    __syncthreads();
+    return pos;
 }
 
 // Wave-reduced traversal counters (one atomic per wavefront).
