@@ -568,7 +568,11 @@ bool bvh_hit(const Scene& sc, const BvhView& b, const Ray& r, double t_min, doub
 double bvh_hit_t(const Scene& sc, const BvhView& b, const Ray& r, double t_min, double t_max, Counters& C) {
     const int idx = bvh_hit_idx(sc, b.nodes, b.n, b.items, b.objs, r, t_min, t_max, false, C);
     if (idx < 0) return INF;
-    return object_hit_t(sc, b.objs[idx], r, t_min, t_max, C);
+    // bvh.rs:371-374 re-runs objects[idx].hit_t with the same arguments the traversal's last
+    // object test had (any-hit: tt == t_max), so it repeats that test exactly; the repeat is not
+    // counted (the device reuses the value), keeping the counters comparable with the kernels'.
+    Counters rerun;
+    return object_hit_t(sc, b.objs[idx], r, t_min, t_max, rerun);
 }
 
 // scene.rs:119-147. kind: 0 miss, 1 object, 2 light.
