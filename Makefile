@@ -13,16 +13,17 @@ HIPFLAGS := -O3 -std=c++17 -fPIC $(FPFLAGS) --offload-arch=$(ARCH) -Wall -Wno-un
             -munsafe-fp-atomics
 
 HOST_SRC := $(wildcard lumo_amd/csrc/host/*.cpp)
+BUILD    ?= build
 HOST_OBJ := $(patsubst lumo_amd/csrc/host/%.cpp,build/host/%.o,$(HOST_SRC))
 # kernels.hip: host orchestration, C ABI and the non-traversal kernels.  The traversal kernels
 # are instantiated once per kd stack class (launch.h STACK_CLASSES) in their own translation
 # units, so they compile in parallel: inst_pt.hip / inst_bd.hip built with -DLUMO_STK=<class>.
 STK_CLASSES := 4 8 16 24 32 48 64
-DEV_OBJ  := build/device/kernels.o $(foreach k,$(STK_CLASSES),build/device/inst_pt_$(k).o build/device/inst_bd_$(k).o)
+DEV_OBJ  := $(BUILD)/device/kernels.o $(foreach k,$(STK_CLASSES),$(BUILD)/device/inst_pt_$(k).o $(BUILD)/device/inst_bd_$(k).o)
 DEV_H    := $(wildcard lumo_amd/csrc/device/*.h)
 COMMON_H := $(wildcard lumo_amd/csrc/common/*.h) include/lumo_amd.h include/lumo_host.h
 
-LIB      := lumo_amd/liblumo_amd.so
+LIB      ?= lumo_amd/liblumo_amd.so
 ORACLE   := oracle/_build/liblumo_oracle.so
 ORACLE_G := oracle/_build/liblumo_oracle_glibc.so
 
@@ -32,16 +33,16 @@ build/host/%.o: lumo_amd/csrc/host/%.cpp $(COMMON_H) $(wildcard lumo_amd/csrc/ho
 	@mkdir -p build/host
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-build/device/kernels.o: lumo_amd/csrc/device/kernels.hip $(COMMON_H) $(DEV_H)
-	@mkdir -p build/device
+$(BUILD)/device/kernels.o: lumo_amd/csrc/device/kernels.hip $(COMMON_H) $(DEV_H)
+	@mkdir -p $(BUILD)/device
 	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -c $< -o $@
 
-build/device/inst_pt_%.o: lumo_amd/csrc/device/inst_pt.hip $(COMMON_H) $(DEV_H)
-	@mkdir -p build/device
+$(BUILD)/device/inst_pt_%.o: lumo_amd/csrc/device/inst_pt.hip $(COMMON_H) $(DEV_H)
+	@mkdir -p $(BUILD)/device
 	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -DLUMO_STK=$* -c $< -o $@
 
-build/device/inst_bd_%.o: lumo_amd/csrc/device/inst_bd.hip $(COMMON_H) $(DEV_H)
-	@mkdir -p build/device
+$(BUILD)/device/inst_bd_%.o: lumo_amd/csrc/device/inst_bd.hip $(COMMON_H) $(DEV_H)
+	@mkdir -p $(BUILD)/device
 	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -DLUMO_STK=$* -c $< -o $@
 
 $(LIB): $(HOST_OBJ) $(DEV_OBJ)
@@ -55,9 +56,14 @@ $(ORACLE_G): oracle/src/oracle.cpp oracle/oracle.h $(COMMON_H)
 	@mkdir -p oracle/_build
 	$(CXX) $(CXXFLAGS) -O2 -DLUMO_ORACLE_GLIBC -shared -o $@ oracle/src/oracle.cpp -lpthread
 
-# DEVFLAGS: extra device defines for A/B builds, e.g. make DEVFLAGS=-DLUMO_TRAVERSAL_WAVES=4
+# A/B builds of the device code (perf experiments, loaded with LUMO_AMD_LIB=<path>):
+#   make variant NAME=rs0 DEVFLAGS=-DLUMO_KD_REG=0   ->  lumo_amd/var/liblumo_amd_rs0.so
+variant:
+	@mkdir -p lumo_amd/var
+	$(MAKE) BUILD=build/var_$(NAME) LIB=lumo_amd/var/liblumo_amd_$(NAME).so DEVFLAGS="$(DEVFLAGS)" lumo_amd/var/liblumo_amd_$(NAME).so
+
 
 clean:
-	rm -rf build $(LIB) oracle/_build
+	rm -rf build $(LIB) oracle/_build lumo_amd/var
 
-.PHONY: all clean
+.PHONY: all clean variant

@@ -2268,3 +2268,147 @@ extern "C" int oracle_light_pdf(const lumo_scene_desc* scene, int light, const d
 extern "C" void oracle_set_tone_map(int kind, double arg) { g_tone = ToneMap{kind, arg}; }
 
 extern "C" void oracle_set_integrator(int integrator) { g_integrator = integrator; }
+
+// ------------------------------------------------------------------ MIS weights sum to one
+// bd_path_trace/mis_tests.rs:96-352 (test_scene, _from_light, _from_camera, _reverse): build a full
+// path from the light (connected to the camera) or from the camera (connected to a light), reverse
+// it, and sum mis::weight over every strategy (s, t) the integrator uses.  sums[i] = that sum for
+// path i (lumo asserts |1 - sum| < 0.01).  Followed as written, including _from_camera's use of
+// the sampled direction as a point ((sample_towards(xo) - xo).normalize()), which only changes
+// which paths are drawn.
+namespace {
+std::vector<Vtx> mis_reverse(std::vector<Vtx> p) {  // mis_tests.rs:321-352
+    std::reverse(p.begin(), p.end());
+    for (size_t i = p.size() - 1; i >= 1; --i) p[i].wo = -p[i - 1].wo;
+    p[0].wo = V3{0.0, 0.0, 0.0};
+    for (Vtx& v : p) std::swap(v.pdf_fwd, v.pdf_bck);
+    return p;
+}
+
+void mis_from_light(const Scene& sc, const Cam& cam, Xorshift& rng, Lambda& L, std::vector<Vtx>& cp,
+                    std::vector<Vtx>& lp, Counters& C) {  // mis_tests.rs:266-319
+    std::vector<Vtx> pth;
+    const Ray r = camera_ray(cam, V2{0.0, 0.0}, xs_vec2(rng));
+    const V3 xc = r.origin;
+    for (;;) {
+        bdpt_light_path(sc, rng, 0.0, L, pth, C);
+        if (pth.size() <= 2) continue;
+        const Vtx& ls = pth.back();
+        if (v_is_delta(sc, ls, L)) continue;
+        const Vtx& ls_m = pth[pth.size() - 2];
+        const V3 xo = ls_m.h.p, wo = ls.wo, ngo = ls_m.h.ng, ngi = ls.h.ng, xi = ls.h.p;
+        const double t2 = distance_squared(xi, xc);
+        const V3 wi = normalize(xi - xc);
+        const Ray ri = ray_new(xc, wi);
+        Hit h;
+        int kind = 0, which = -1;
+        if (scene_hit(sc, ri, &h, &kind, &which, C) && h.t * h.t < t2 - EPSILON * EPSILON) continue;
+        pth.push_back(vtx_camera(xc, 0.0, cconst(1.0)));
+        const size_t len = pth.size();
+        pth[len - 1].wo = wi;
+        const double pdf_sa = cam_pdf_wi(cam, ri);
+        const V3 ngi2 = !v_is_surface(pth[len - 2]) ? wi : ngi;
+        pth[len - 2].pdf_bck = sa_to_area(pdf_sa, xc, xi, wi, ngi2);
+        if (!v_is_delta(sc, pth[len - 3], L)) {
+            const double p2 = v_bsdf_pdf(sc, pth[len - 2], -wi, L, true);
+            const V3 ngo2 = !v_is_surface(pth[len - 3]) ? wo : ngo;
+            pth[len - 3].pdf_bck = sa_to_area(p2, xo, xi, wo, ngo2);
+        }
+        break;
+    }
+    lp = pth;
+    cp = mis_reverse(lp);
+}
+
+bool mis_from_camera(const Scene& sc, const Cam& cam, Xorshift& rng, Lambda& L, std::vector<Vtx>& cp,
+                     std::vector<Vtx>& lp, Counters& C) {  // mis_tests.rs:161-264
+    std::vector<Vtx> pth;
+    const V2 res{(double)cam.width, (double)cam.height};
+    const size_t min_len = 3;
+    for (int attempt = 0; attempt < 1000000; ++attempt) {
+        const V2 u = xs_vec2(rng);
+        const Ray ro = camera_ray(cam, V2{res.x * u.x, res.y * u.y}, xs_vec2(rng));
+        bdpt_camera_path(sc, cam, ro, rng, 0.0, L, pth, C);
+        if (pth.size() < min_len) continue;
+        if (pth.back().light >= 0) goto done;
+        pth.push_back(vtx_camera(V3{0.0, 0.0, 0.0}, 0.0, cconst(0.0)));
+        while (pth.size() > min_len - 1) {
+            pth.pop_back();
+            const Vtx& ct = pth.back();
+            if (v_is_delta(sc, ct, L)) continue;
+            const V3 xo = ct.h.p;
+            const int li = sample_light(sc, xs_float(rng));
+            const V3 xi = light_sample_towards(sc, sc.d->lights[li], xo, xs_vec2(rng));
+            const V3 wi = normalize(xi - xo);
+            const Ray rr = generate_ray(ct.h, wi);
+            Hit hi;
+            if (!scene_hit_light(sc, rr, li, &hi, C)) continue;
+            const double pdf_sa = v_bsdf_pdf(sc, ct, wi, L, false);
+            if (pdf_sa == 0.0) continue;
+            Vtx v = vtx_surface(sc, -wi, hi, cconst(1.0), pdf_sa, L, ct);
+            v.light = li;
+            pth.push_back(v);
+            goto done;
+        }
+    }
+    return false;
+done:
+    {
+        const size_t len = pth.size();
+        const Vtx& ct = pth[len - 1];
+        const Vtx& ct_m = pth[len - 2];
+        const Vtx& ct_mm = pth[len - 3];
+        const lumo_object& light = sc.d->lights[ct.light];
+        const double light_pdf = sc.d->alias_pdf[ct.light];
+        const V3 xo = ct_m.h.p, xi = ct.h.p, xp = ct_mm.h.p;
+        const V3 wi = normalize(xi - xo);
+        const V3 ngi = ct.h.ng, ngo = ct_m.h.ng, ngp = ct_mm.h.ng;
+        const Ray rl = ray_new(xi, -wi);
+        const double pdf_origin = 1.0 / light_area(sc, light);  // Sampleable::sample_leaving_pdf
+        const double pdf_dir = dot(ngi, rl.dir) / PI;
+        pth[len - 1].pdf_bck = light_pdf * pdf_origin;
+        if (!v_is_delta(sc, pth[len - 2], L)) {
+            const V3 n = !v_is_surface(pth[len - 2]) ? -wi : ngo;
+            pth[len - 2].pdf_bck = sa_to_area(pdf_dir, xi, xo, -wi, n);
+        }
+        if (!v_is_delta(sc, pth[len - 3], L)) {
+            const double p2 = v_bsdf_pdf(sc, pth[len - 2], wi, L, true);
+            const V3 wo = pth[len - 2].wo;
+            const V3 n = !v_is_surface(pth[len - 3]) ? wo : ngp;
+            pth[len - 3].pdf_bck = sa_to_area(p2, xo, xp, wo, n);
+        }
+    }
+    cp = pth;
+    lp = mis_reverse(cp);
+    return true;
+}
+}  // namespace
+
+extern "C" int oracle_mis_sums(const lumo_scene_desc* scene, const lumo_camera_desc* camera, size_t n, uint64_t seed,
+                               double* sums, int32_t* lengths) {
+    if (!scene || !camera || !sums) return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    const Cam cam = cam_of(camera);
+    Counters C;
+    Xorshift rng = xs_new(seed);
+    for (size_t i = 0; i < n; ++i) {  // mis_tests.rs:103-158
+        Lambda lambda = wl_sample(xs_float(rng));
+        const Lambda l = lambda;
+        std::vector<Vtx> cp, lp;
+        if (i % 2 == 0)
+            mis_from_light(sc, cam, rng, lambda, cp, lp, C);
+        else if (!mis_from_camera(sc, cam, rng, lambda, cp, lp, C))
+            return LUMO_ERR_UNSUPPORTED;
+        double sumw = 0.0;
+        const int len = (int)lp.size();
+        for (int s = 0; s < len; ++s) {
+            const int t = len - s;
+            if (t == 1 && s < 2) continue;
+            if (v_is_delta(sc, lp[s], l) || (s > 0 && v_is_delta(sc, lp[s - 1], l))) continue;
+            sumw += mis_weight(sc, cam, l, lp.data(), s, cp.data(), t);
+        }
+        sums[i] = sumw;
+        if (lengths) lengths[i] = len;
+    }
+    return LUMO_OK;
+}

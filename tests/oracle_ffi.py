@@ -53,6 +53,9 @@ def load(path=None):
         lib.oracle_light_sample.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, C.c_size_t, C.c_uint64, dp]
         lib.oracle_light_pdf.restype = C.c_int
         lib.oracle_light_pdf.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, dp, C.c_size_t, dp]
+        lib.oracle_mis_sums.restype = C.c_int
+        lib.oracle_mis_sums.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(_ffi.CameraDesc), C.c_size_t, C.c_uint64,
+                                        dp, _ffi.c_int32_p]
         _libs[path] = lib
     return _libs[path]
 
@@ -180,3 +183,14 @@ def light_pdf(scene_desc, light, xo, wi):
     pdf = np.zeros(len(wi))
     assert load().oracle_light_pdf(C.byref(scene_desc), light, _dp(xo), _dp(wi), len(wi), _dp(pdf)) == 0
     return pdf
+
+
+def mis_sums(scene_desc, camera_desc, n, seed):
+    """Per path: the sum of mis::weight over its strategies (mis_tests.rs test_scene) and its length."""
+    lib = load()
+    sums = np.zeros(n)
+    lens = np.zeros(n, dtype=np.int32)
+    st = lib.oracle_mis_sums(C.byref(scene_desc), C.byref(camera_desc), n, seed, _dp(sums),
+                             lens.ctypes.data_as(_ffi.c_int32_p))
+    assert st == 0, st
+    return sums, lens

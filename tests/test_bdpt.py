@@ -59,3 +59,33 @@ def test_bdpt_splats_and_counters():
         np.testing.assert_array_equal(x, y)
     for x, y in zip(sp, sp2):
         np.testing.assert_array_equal(x, y)
+
+
+def _mis_scene(kind):
+    """The scenes of bd_path_trace/mis_tests.rs:9-94 (the orthographic camera and the medium
+    variants are out of scope here)."""
+    if kind == "big_scale":
+        cam = L.Camera.builder().origin(278.0, 273.0, -800.0).towards(278.0, 273.0, 0.0).zoom(2.8) \
+            .focal_length(0.035).resolution((512, 512)).build()
+        return L.Scene.cornell_box(), cam
+    sc = L.Scene.empty_box(L.named_spectrum("WHITE"), L.Material.diffuse(L.named_spectrum("RED")),
+                           L.Material.lambertian(L.named_spectrum("GREEN")))
+    white = L.named_spectrum("WHITE")
+    if kind == "specular_delta":
+        sc.add_sphere(0.25, L.Material.mirror()).translate(-0.45, -0.5, -1.5)
+        sc.add_sphere(0.25, L.Material.glass()).translate(0.45, -0.5, -1.3)
+    elif kind == "specular_rough":
+        sc.add_sphere(0.25, L.Material.metal(white, 0.5, 1.5, 1.5)).translate(-0.45, -0.5, -1.5)
+        sc.add_sphere(0.25, L.Material.transparent(white, 0.5, 1.5)).translate(0.45, -0.5, -1.3)
+    return sc, L.Camera.builder().build()
+
+
+@pytest.mark.parametrize("kind", ["diffuse", "specular_delta", "specular_rough", "big_scale"])
+def test_mis_weights_sum_to_one(kind):
+    """mis_tests.rs all_sum_to_one_*: for full paths built from the light and from the camera,
+    the MIS weights of every strategy the integrator evaluates sum to 1 (|1 - sum| < 0.01, lumo's
+    bound), here for 10 000 paths per scene on the oracle's restated mis::weight."""
+    sc, cam = _mis_scene(kind)
+    sums, lens = O.mis_sums(sc.build().desc(), cam.desc, 10_000, 0x5EED + len(kind))
+    assert np.all(np.abs(1.0 - sums) < 0.01), (kind, sums[np.abs(1.0 - sums) >= 0.01][:5])
+    assert lens.min() >= 3 and lens.max() > 4  # paths of several lengths were exercised
