@@ -366,73 +366,11 @@ __device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_mi
     return true;
 }
 
-// The kd traversal stack (kdtree.rs:110, [_; 64] of (node, t0, t1)): the top RS entries live in
-// registers as a shift register (constant indices only, so they stay in VGPRs); deeper entries
-// spill to a per-lane array (scratch).  Most pushes and pops never reach the spill array, which
-// is what a traversal stack in scratch costs on every push.  LUMO_KD_REG=0 keeps the whole stack
-// in the array.
-#ifndef LUMO_KD_REG
-#define LUMO_KD_REG 4
-#endif
-template <int STK>
-struct KdStack {
-    static constexpr int RS = LUMO_KD_REG < STK ? LUMO_KD_REG : STK;
-    static constexpr int SP = STK - RS > 0 ? STK - RS : 1;
-    int rn[RS > 0 ? RS : 1];
-    double rts[RS > 0 ? RS : 1], rte[RS > 0 ? RS : 1];
-    int sn[SP];
-    double sts[SP], ste[SP];
-    int sp = 0;
-    __device__ __forceinline__ void push(int node, double ts, double te) {
-        if constexpr (RS == 0) {
-            sn[sp] = node;
-            sts[sp] = ts;
-            ste[sp] = te;
-        } else {
-            if (sp >= RS) {
-                sn[sp - RS] = rn[RS - 1];
-                sts[sp - RS] = rts[RS - 1];
-                ste[sp - RS] = rte[RS - 1];
-            }
-#pragma unroll
-            for (int k = RS - 1; k > 0; --k) {
-                rn[k] = rn[k - 1];
-                rts[k] = rts[k - 1];
-                rte[k] = rte[k - 1];
-            }
-            rn[0] = node;
-            rts[0] = ts;
-            rte[0] = te;
-        }
-        sp++;
-    }
-    __device__ __forceinline__ void pop(int& node, double& ts, double& te) {
-        sp--;
-        if constexpr (RS == 0) {
-            node = sn[sp];
-            ts = sts[sp];
-            te = ste[sp];
-        } else {
-            node = rn[0];
-            ts = rts[0];
-            te = rte[0];
-#pragma unroll
-            for (int k = 0; k < RS - 1; ++k) {
-                rn[k] = rn[k + 1];
-                rts[k] = rts[k + 1];
-                rte[k] = rte[k + 1];
-            }
-            if (sp >= RS) {
-                rn[RS - 1] = sn[sp - RS];
-                rts[RS - 1] = sts[sp - RS];
-                rte[RS - 1] = ste[sp - RS];
-            }
-        }
-    }
-};
-
 // kdtree.rs:101-169.  GEO: returns the winning local triangle index (or -1);
-// !GEO: returns t of the first hit found (or INF).
+// !GEO: returns t of the first hit found (or INF).  The (node, t0, t1) stack is sized by the
+// stack class STK (lumo: 64); it lives in scratch for the classes above ~8.  Keeping its top 2 /
+// 4 / 8 entries in registers as a shift register measured 6 / 27 / 92 % slower on C3 (the extra
+// VGPRs push more of the traversal state into scratch at 4 waves/SIMD).
 #ifdef LUMO_NOINLINE_KD
 #define KD_INLINE __noinline__
 #else
@@ -443,7 +381,9 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
                               int* idx_out, Counters& C) {
     const double origin[3] = {r.o.x, r.o.y, r.o.z};
     const double inv_dir[3] = {r.inv.x, r.inv.y, r.inv.z};
-    KdStack<STK> st;
+    int st_node[STK];
+    double st_ts[STK], st_te[STK];
+    int sp = 0;
     double t_hit = DINF;
     int curr = ob.kd_root;
     int idx = -1;
@@ -470,8 +410,11 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
                     return t;
                 }
             }
-            if (st.sp == 0) break;
-            st.pop(curr, t_start, t_end);
+            if (sp == 0) break;
+            sp--;
+            curr = st_node[sp];
+            t_start = st_ts[sp];
+            t_end = st_te[sp];
         } else {
             C.kd++;
             const int ax = axis;
@@ -487,8 +430,11 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
                 curr = second;
             } else {
                 curr = first;
-                st.push(second, t_split, t_end);
+                st_node[sp] = second;
+                st_ts[sp] = t_split;
+                st_te[sp] = t_end;
                 t_end = t_split;
+                sp++;
             }
         }
     }

@@ -170,6 +170,7 @@ __global__ void k_bounce_begin(uint32_t* counts) {
         counts[CNT_NEXT] = 0;
         counts[CNT_SHADOW] = 0;
         counts[CNT_RESOLVE] = 0;
+        for (int b = 0; b < NB; ++b) counts[CNT_BUCKET0 + b] = 0;
     }
 }
 
@@ -751,12 +752,15 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         S.hq.cap = cap;
         S.hq.t = wbuf<double>(c, W_HQ_T, cap, st);
         S.hq.i = wbuf<int32_t>(c, W_HQ_I, 3 * cap, st);
-        S.sq.cap = cap * (size_t)ns;
-        S.sq.hcap = cap;
+        // bucket segments of `cap` paths each (MI355X has the HBM for the worst case)
+        const int nb = g_buckets > 1 ? NB : 1;
+        S.sq.seg = (uint32_t)cap;
+        S.sq.hcap = cap * nb;
+        S.sq.cap = S.sq.hcap * (size_t)ns;
         S.sq.d = wbuf<double>(c, W_SQ_D, SD_N * S.sq.cap, st);
         S.sq.i = wbuf<int32_t>(c, W_SQ_I, SI_N * S.sq.cap, st);
-        S.sq.hd = wbuf<double>(c, W_SQ_HD, SH_N * cap, st);
-        S.sq.hi = wbuf<int32_t>(c, W_SQ_HI, SHI_N * cap, st);
+        S.sq.hd = wbuf<double>(c, W_SQ_HD, SH_N * S.sq.hcap, st);
+        S.sq.hi = wbuf<int32_t>(c, W_SQ_HI, SHI_N * S.sq.hcap, st);
     }
     S.p_rgb = wbuf<double>(c, W_P_RGB, 3 * (size_t)N, st);
     S.p_lum = wbuf<double>(c, W_P_LUM, N, st);
@@ -949,6 +953,10 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                     StageTimer tm(c, g_timing, ST_SHADOW);
                     launch_trav(c, (uint64_t)ub * (uint32_t)ns,
                                 [&](auto K, const TravLaunch& l) { launch_shadow_q<decltype(K)::value>(l, c.sc, S, nxt); });
+                }
+                if (ns > 1) {
+                    StageTimer tm(c, g_timing, ST_RESOLVE);
+                    k_nee_fold<<<std::min(ceil_div(ub, BLOCK), 1 << 14), BLOCK, 0, sm>>>(S, nxt, ns);
                 }
             });
             if (bst) return bst;

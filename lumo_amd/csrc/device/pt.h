@@ -143,8 +143,8 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade_q(DScene sc, 
                 }
             }
         }
-        // NEE records (integrator.rs:87-137), grouped by origin object within the block
-        const uint32_t sp = block_slot_sorted(resolve, key, S.counts + CNT_SHADOW);
+        // NEE records (integrator.rs:87-137), filed into the bucket of the origin object
+        const uint32_t sp = key * sq.seg + block_slot_bucket(resolve, key, S.counts + CNT_BUCKET0);
         if (resolve) {
             uint32_t n_sh = 0;
             for (int i = 0; i < ns; ++i) {
@@ -268,52 +268,71 @@ __device__ __forceinline__ void deliver_nee(const Paths& S, const ShadowQ& Q, co
     }
 }
 
-// Thread (path p, light sample i): single_i = (light-sampled + BSDF-sampled) / pdf_light
-// (integrator.rs:87-137); with n_shadow > 1 staged in LDS and folded by the path's i == 0 thread
-// in i order.  A block round covers BLOCK / n_shadow whole paths; the pair records of a round
-// are contiguous.
+// Thread per pair r = p * n_shadow + i (path p, light sample i): single_i = (light-sampled +
+// BSDF-sampled) / pdf_light (integrator.rs:87-137).  With n_shadow = 1 the thread also folds the
+// path's NEE term; otherwise it stores single_i over the pair's (consumed) L-record bsdf_f planes
+// and k_nee_fold adds the path's singles in i order.  No block barrier: a wave that finishes its
+// traversals early moves on to its next pairs.
 template <int STK, bool LDS, bool FX>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc0, Paths S, QState nxt) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
-    __shared__ DColor singles[BLOCK];
-    const uint32_t count = S.counts[CNT_SHADOW];
     const int ns = sc0.n_shadow;
-    const uint32_t per_block = (uint32_t)(BLOCK / ns);  // paths per block round
-    if (count <= blockIdx.x * per_block) return;
+    uint32_t bc[NB], count = 0;  // pairs per bucket
+    for (int b = 0; b < NB; ++b) {
+        bc[b] = S.counts[CNT_BUCKET0 + b] * (uint32_t)ns;
+        count += bc[b];
+    }
+    if (count <= blockIdx.x * blockDim.x) return;
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     const ShadowQ Q = S.sq;
     Counters C{0, 0, 0};
-    const int i = (int)threadIdx.x % ns;
-    for (uint32_t base = blockIdx.x * per_block; base < count; base += gridDim.x * per_block) {
-        const uint32_t p = base + threadIdx.x / ns;
-        const bool mine = threadIdx.x < per_block * ns && p < count;
-        if (mine) {
-            double L[NS];
-            for (int k = 0; k < NS; ++k) L[k] = Q.HD(SH_L + k, p);
-            const size_t r = (size_t)p * ns + i;
-            const DColor a = shadow_record_q<STK, FX>(sc, Q, SD_LO, r, true, L, C);
-            const DColor b = Q.I(SI_BVALID, r) ? shadow_record_q<STK, FX>(sc, Q, SD_BO, r, false, L, C) : cfill(0.0);
-            const DColor single = (cfill(0.0) + a + b) / Q.D(SD_PDFL, r);
-            if (ns == 1) {
-                const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};
-                deliver_nee(S, Q, nxt, p, (cfill(0.0) + g * single) / 1.0);
-            } else {
-                singles[threadIdx.x] = single;
-            }
-        }
-        if (ns > 1) {  // uniform over the block
-            __syncthreads();
-            if (mine && i == 0) {
-                const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};
-                DColor acc = cfill(0.0);
-                for (int k = 0; k < ns; ++k) acc = acc + g * singles[threadIdx.x + k];
-                deliver_nee(S, Q, nxt, p, acc / (double)ns);
-            }
-            __syncthreads();
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
+        uint32_t lj = j;
+        int bk = 0;
+        while (lj >= bc[bk]) lj -= bc[bk++];  // j < count, so bk < NB
+        const size_t r = (size_t)bk * Q.seg * ns + lj;  // pair index
+        const uint32_t p = (uint32_t)(ns == 1 ? r : r / (size_t)ns);
+        double L[NS];
+        for (int k = 0; k < NS; ++k) L[k] = Q.HD(SH_L + k, p);
+        const DColor a = shadow_record_q<STK, FX>(sc, Q, SD_LO, r, true, L, C);
+        const DColor b = Q.I(SI_BVALID, r) ? shadow_record_q<STK, FX>(sc, Q, SD_BO, r, false, L, C) : cfill(0.0);
+        const DColor single = (cfill(0.0) + a + b) / Q.D(SD_PDFL, r);
+        if (ns == 1) {
+            const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};
+            deliver_nee(S, Q, nxt, p, (cfill(0.0) + g * single) / 1.0);
+        } else {
+            for (int k = 0; k < NS; ++k) Q.D(SD_LF + k, r) = single.s[k];
         }
     }
     flush_counters(C, S.tcount + TC_N);
 }
+
+#ifdef LUMO_MAIN_TU
+// n_shadow > 1: radiance += (0 + gathered * single_0 + ... + gathered * single_{n-1}) / n_shadow
+// per path, in lumo's order (integrator.rs:74-85).
+__global__ __launch_bounds__(BLOCK) void k_nee_fold(Paths S, QState nxt, int ns) {
+    uint32_t bc[NB], count = 0;  // paths per bucket
+    for (int b = 0; b < NB; ++b) {
+        bc[b] = S.counts[CNT_BUCKET0 + b];
+        count += bc[b];
+    }
+    const ShadowQ Q = S.sq;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
+        uint32_t lj = j;
+        int bk = 0;
+        while (lj >= bc[bk]) lj -= bc[bk++];
+        const uint32_t p = bk * Q.seg + lj;
+        const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};
+        DColor acc = cfill(0.0);
+        for (int i = 0; i < ns; ++i) {
+            const size_t r = (size_t)p * ns + i;
+            const DColor single{{Q.D(SD_LF, r), Q.D(SD_LF + 1, r), Q.D(SD_LF + 2, r), Q.D(SD_LF + 3, r)}};
+            acc = acc + g * single;
+        }
+        deliver_nee(S, Q, nxt, p, acc / (double)ns);
+    }
+}
+#endif  // LUMO_MAIN_TU
 
 // ------------------------------------------------------------------ traversal-only entry (lumo_trace)
 template <int STK>

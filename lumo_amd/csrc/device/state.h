@@ -27,7 +27,7 @@ constexpr int BLOCK = 256;
 constexpr uint64_t SAMPLES_INCREMENT = 256;
 constexpr int RR_DEPTH = 5;
 
-// ST_RESOLVE is kept for the stats layout; the fold now runs inside k_shadow.
+// ST_RESOLVE: path tracer k_nee_fold (n_shadow > 1); BDPT re-runs + fold.
 enum Stage {
     ST_CAMERA = 0, ST_CLOSEST, ST_SHADE, ST_SHADOW, ST_RESOLVE, ST_FINISH, ST_FILM, ST_RING,
     ST_BD_TRACE_A, ST_BD_EVAL_A, ST_BD_VIS, ST_BD_PATHS, ST_COUNT
@@ -35,10 +35,11 @@ enum Stage {
 static_assert(ST_COUNT == LUMO_STAGE_COUNT, "stage slots match lumo_stats");
 // Device-side queue counters: the bounce kernels read their counts from here, so the host never
 // waits for a count before launching the next stage.
-enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_N = 8 };
-// k_shade_q groups a block's NEE records by the shadow rays' origin object (NB keys) so that a
-// wave's visibility queries start on the same surface and walk similar BVH / kd paths
-// (LUMO_BUCKETS=0: one key).
+enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_BUCKET0, CNT_N = CNT_BUCKET0 + 8 };
+// k_shade_q files each path's NEE records into one of NB buckets by the shadow rays' origin
+// object (objects, then lights, mod NB), each bucket a contiguous segment of the record queue, so
+// that a wave's visibility queries start on the same surface and walk the same BVH / kd nodes
+// (LUMO_BUCKETS=0: one bucket).  k_shadow_q walks the buckets in order.
 constexpr int NB = 8;
 enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
 
@@ -73,7 +74,8 @@ struct HitQ {
 };
 // NEE records in queue order: per path with shadow rays a header (gathered, wavelengths, radiance
 // of a path that ends this bounce, slot, next-queue position or -1), and per light sample i the
-// pair of records (light-sampled L, BSDF-sampled B) at pair index p * n_shadow + i.
+// pair of records (light-sampled L, BSDF-sampled B) at pair index P * n_shadow + i.  Path P of
+// bucket b is at P = b * seg + (its position in the bucket); hcap = NB * seg.
 enum { SD_LO = 0, SD_LD = 3, SD_LF = 6, SD_LPS = 10, SD_LCOS = 11, SD_BO = 12, SD_BD = 15, SD_BF = 18,
        SD_BPS = 22, SD_BCOS = 23, SD_PDFL = 24, SD_N = 25 };
 enum { SI_LIGHT = 0, SI_BVALID, SI_N };
@@ -86,6 +88,7 @@ struct ShadowQ {
     double* hd;   // SH_* planes, hcap paths
     int32_t* hi;  // SHI_* planes
     size_t hcap;
+    uint32_t seg;  // paths per bucket segment
     __device__ __forceinline__ double& D(int k, size_t r) const { return d[(size_t)k * cap + r]; }
     __device__ __forceinline__ int32_t& I(int k, size_t r) const { return i[(size_t)k * cap + r]; }
     __device__ __forceinline__ double& HD(int k, size_t p) const { return hd[(size_t)k * hcap + p]; }
@@ -171,13 +174,13 @@ __device__ __forceinline__ void block_append(bool pred, int32_t value, int32_t* 
     if (pred) queue[pos] = value;
 }
 
-// block_slot with the block's entries grouped by `key` in [0, NB) (a block-local counting sort:
-// one ballot per key per wave), so that consecutive queue entries share the key.  One atomic
-// per block.  Every thread of the block must call it.
-__device__ __forceinline__ uint32_t block_slot_sorted(bool pred, int key, uint32_t* counter) {
+// block_slot into NB queues (one counter each, counters[key]): per-key ballots inside each wave,
+// per-key wave totals scanned in LDS, one atomic per non-empty key per block.  Returns this
+// thread's position within its key's queue.  Every thread of the block must call it.
+__device__ __forceinline__ uint32_t block_slot_bucket(bool pred, int key, uint32_t* counters) {
     constexpr int NW = BLOCK / 64;
     __shared__ uint32_t cnt[NB][NW];
-    __shared__ uint32_t base_s;
+    __shared__ uint32_t base_s[NB];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     uint32_t rank = 0;
 #pragma unroll
@@ -187,18 +190,18 @@ __device__ __forceinline__ uint32_t block_slot_sorted(bool pred, int key, uint32
         if (lane == 0) cnt[b][w] = (uint32_t)__popcll(m);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < NB) {
+        const int b = threadIdx.x;
         uint32_t t = 0;
-        for (int b = 0; b < NB; ++b)
-            for (int i = 0; i < NW; ++i) {
-                const uint32_t c = cnt[b][i];
-                cnt[b][i] = t;
-                t += c;
-            }
-        base_s = t ? atomicAdd(counter, t) : 0u;
+        for (int i = 0; i < NW; ++i) {
+            const uint32_t c = cnt[b][i];
+            cnt[b][i] = t;
+            t += c;
+        }
+        base_s[b] = t ? atomicAdd(counters + b, t) : 0u;
     }
     __syncthreads();
-    const uint32_t pos = base_s + (pred ? cnt[key][w] : 0u) + rank;
+    const uint32_t pos = pred ? base_s[key] + cnt[key][w] + rank : 0u;
     __syncthreads();
     return pos;
 }
