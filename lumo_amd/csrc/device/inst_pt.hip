@@ -32,15 +32,23 @@ void launch_closest_q(const TravLaunch& l, const DScene& sc, const Paths& S, con
     }
 }
 
+template <int STK, bool NS1>
+void launch_shadow_q_ns(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& nxt) {
+    if (l.lds) {
+        if (l.fx) k_shadow_q<STK, true, true, NS1><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, nxt);
+        else k_shadow_q<STK, true, false, NS1><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, nxt);
+    } else {
+        if (l.fx) k_shadow_q<STK, false, true, NS1><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, nxt);
+        else k_shadow_q<STK, false, false, NS1><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, nxt);
+    }
+}
+
 template <int STK>
 void launch_shadow_q(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& nxt) {
-    if (l.lds) {
-        if (l.fx) k_shadow_q<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, nxt);
-        else k_shadow_q<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, nxt);
-    } else {
-        if (l.fx) k_shadow_q<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, nxt);
-        else k_shadow_q<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, nxt);
-    }
+    if (sc.n_shadow == 1)
+        launch_shadow_q_ns<STK, true>(l, sc, S, nxt);
+    else
+        launch_shadow_q_ns<STK, false>(l, sc, S, nxt);
 }
 
 template <int STK>

@@ -230,10 +230,12 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade_q(DScene sc, 
     }
 }
 
-// Scene::hit_light + mis_sample of one NEE record (integrator.rs:100-184); plane base b.
+// Scene::hit_light + mis_sample of one NEE record (integrator.rs:100-184); plane base b.  The
+// path's wavelengths (header p) are read only after a visible hit, so they are not live across
+// the traversal.
 template <int STK, bool FX>
 __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const ShadowQ& Q, int b, size_t r, bool li_mode,
-                                                  const double* L, Counters& C) {
+                                                  uint32_t p, Counters& C) {
     const RayX ri = rayx(Ray{V3{Q.D(b, r), Q.D(b + 1, r), Q.D(b + 2, r)}, V3{Q.D(b + 3, r), Q.D(b + 4, r), Q.D(b + 5, r)}});
     const int li = Q.I(SI_LIGHT, r);
     DHit hi;
@@ -243,6 +245,8 @@ __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const Shadow
         const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
         const double p_sct = Q.D(b + 10, r);
         if (!(p_lig == 0.0 || p_sct == 0.0)) {  // mis_sample (integrator.rs:139-184)
+            double L[NS];
+            for (int k = 0; k < NS; ++k) L[k] = Q.HD(SH_L + k, p);
             const double denom = p_lig * p_lig + p_sct * p_sct;
             const double weight = li_mode ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
             const double p_denom = li_mode ? p_lig : p_sct;
@@ -269,19 +273,17 @@ __device__ __forceinline__ void deliver_nee(const Paths& S, const ShadowQ& Q, co
 }
 
 // Thread per pair r = p * n_shadow + i (path p, light sample i): single_i = (light-sampled +
-// BSDF-sampled) / pdf_light (integrator.rs:87-137).  With n_shadow = 1 the thread also folds the
-// path's NEE term; otherwise it stores single_i over the pair's (consumed) L-record bsdf_f planes
-// and k_nee_fold adds the path's singles in i order.  No block barrier: a wave that finishes its
-// traversals early moves on to its next pairs.
-template <int STK, bool LDS, bool FX>
+// BSDF-sampled) / pdf_light (integrator.rs:87-137).  NS1 (n_shadow = 1): the thread also folds
+// the path's NEE term; otherwise it stores single_i over the pair's (consumed) L-record bsdf_f
+// planes and k_nee_fold adds the path's singles in i order.  No block barrier: a wave that
+// finishes its traversals early moves on to its next pairs.
+template <int STK, bool LDS, bool FX, bool NS1>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc0, Paths S, QState nxt) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
-    const int ns = sc0.n_shadow;
-    uint32_t bc[NB], count = 0;  // pairs per bucket
-    for (int b = 0; b < NB; ++b) {
-        bc[b] = S.counts[CNT_BUCKET0 + b] * (uint32_t)ns;
-        count += bc[b];
-    }
+    const int ns = NS1 ? 1 : sc0.n_shadow;
+    uint32_t count = 0;  // pairs over all buckets
+    for (int b = 0; b < NB; ++b) count += S.counts[CNT_BUCKET0 + b];
+    count *= (uint32_t)ns;
     if (count <= blockIdx.x * blockDim.x) return;
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     const ShadowQ Q = S.sq;
@@ -289,15 +291,18 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
         uint32_t lj = j;
         int bk = 0;
-        while (lj >= bc[bk]) lj -= bc[bk++];  // j < count, so bk < NB
+        for (;;) {  // bucket of pair j (j < count, so bk < NB)
+            const uint32_t c = S.counts[CNT_BUCKET0 + bk] * (uint32_t)ns;
+            if (lj < c) break;
+            lj -= c;
+            bk++;
+        }
         const size_t r = (size_t)bk * Q.seg * ns + lj;  // pair index
-        const uint32_t p = (uint32_t)(ns == 1 ? r : r / (size_t)ns);
-        double L[NS];
-        for (int k = 0; k < NS; ++k) L[k] = Q.HD(SH_L + k, p);
-        const DColor a = shadow_record_q<STK, FX>(sc, Q, SD_LO, r, true, L, C);
-        const DColor b = Q.I(SI_BVALID, r) ? shadow_record_q<STK, FX>(sc, Q, SD_BO, r, false, L, C) : cfill(0.0);
+        const uint32_t p = (uint32_t)(NS1 ? r : r / (size_t)ns);
+        const DColor a = shadow_record_q<STK, FX>(sc, Q, SD_LO, r, true, p, C);
+        const DColor b = Q.I(SI_BVALID, r) ? shadow_record_q<STK, FX>(sc, Q, SD_BO, r, false, p, C) : cfill(0.0);
         const DColor single = (cfill(0.0) + a + b) / Q.D(SD_PDFL, r);
-        if (ns == 1) {
+        if (NS1) {
             const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};
             deliver_nee(S, Q, nxt, p, (cfill(0.0) + g * single) / 1.0);
         } else {
