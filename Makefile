@@ -46,7 +46,7 @@ $(BUILD)/device/inst_bd_%.o: lumo_amd/csrc/device/inst_bd.hip $(COMMON_H) $(DEV_
 	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -DLUMO_STK=$* -c $< -o $@
 
 $(LIB): $(HOST_OBJ) $(DEV_OBJ)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -lpthread
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -lpthread -lz
 
 $(ORACLE): oracle/src/oracle.cpp oracle/oracle.h $(COMMON_H)
 	@mkdir -p oracle/_build

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define LUMO_ABI_VERSION 3
+#define LUMO_ABI_VERSION 4
 
 typedef int32_t lumo_status;
 enum {
@@ -53,6 +53,34 @@ enum {
 };
 enum { LUMO_MATF_CONSTANT_ETA = 1 /* DenseSpectrum::is_constant of eta (no dispersion) */ };
 
+/* Textures (texture.rs:23-92, image.rs).  A material's albedo / ks / tf slot is its solid
+ * spectrum when the slot's texture index is -1, else textures[index] evaluated at the hit's uv. */
+enum {
+    LUMO_TEX_SOLID = 0,        /* Texture::Solid                                        */
+    LUMO_TEX_IMAGE = 1,        /* Texture::Image (image.rs:99-128, 170-184): texels[first..]  */
+    LUMO_TEX_CHECKERBOARD = 2, /* Texture::Checkerboard(first, second, scale)           */
+    LUMO_TEX_MARBLE = 3,       /* Texture::Marble(perlin[first], spec)                  */
+    LUMO_TEX_MANDELBROT = 4    /* Texture::Mandelbrot                                   */
+};
+typedef struct {
+    int32_t kind;          /* LUMO_TEX_*                                                 */
+    int32_t width, height; /* IMAGE                                                      */
+    int32_t first;         /* IMAGE: first texel; CHECKERBOARD: even cells; MARBLE: perlin */
+    int32_t second;        /* CHECKERBOARD: odd cells                                    */
+    int32_t pad0;
+    double scale;          /* CHECKERBOARD                                               */
+    lumo_spectrum spec;    /* SOLID / MARBLE colour; IMAGE: mean (Texture::power)        */
+} lumo_texture;
+/* Image<Normal> bump map (image.rs:131-166): normal_texels[3 * (first + x + y * width)..] */
+typedef struct {
+    int32_t width, height, first, pad0;
+} lumo_normal_map;
+/* Perlin noise lattice (perlin.rs): 256 unit normals and the x / y / z permutations */
+typedef struct {
+    double lattice[256][3];
+    int32_t perm[3][256];
+} lumo_perlin;
+
 typedef struct {
     int32_t kind;       /* LUMO_MAT_*                                           */
     int32_t two_sided;  /* Light: emits from the back face too                   */
@@ -65,6 +93,9 @@ typedef struct {
     lumo_spectrum albedo; /* Lambertian spectrum / Light texture / microfacet kd  */
     lumo_spectrum ks;
     lumo_spectrum tf;
+    /* texture indices of albedo / ks / tf (-1: the solid spectrum above) and the bump map
+     * (-1: none) of Material::Standard (material.rs:323-331) */
+    int32_t albedo_tex, ks_tex, tf_tex, normal_map;
 } lumo_material;
 
 /* lumo BVH node (object/bvh.rs:18-26, bvh/node.rs:8-14), depth-first layout:
@@ -162,6 +193,15 @@ typedef struct {
     /* instance transforms referenced by lumo_object.xform */
     int32_t num_transforms, pad1;
     const lumo_transform* transforms;
+    /* textures (texture.rs), their texels (Spectrum per pixel), bump maps, Perlin lattices */
+    int32_t num_textures, num_texels;
+    const lumo_texture* textures;
+    const lumo_spectrum* texels;
+    int32_t num_normal_maps, num_normal_texels;
+    const lumo_normal_map* normal_maps;
+    const double* normal_texels; /* xyz f64 */
+    int32_t num_perlin, pad2;
+    const lumo_perlin* perlin;
 } lumo_scene_desc;
 
 /* Camera (camera.rs:17-38, CameraConfig): world_to_camera, screen_to_raster and

@@ -45,6 +45,34 @@ int lumo_builder_add_rectangle(void* b, const double* a, const double* bb, const
 int lumo_builder_add_sphere(void* b, double radius, int material, int as_light);
 /* Scene::set_environment_map(Texture::from(tex), scale) (scene.rs:73-78). */
 int lumo_builder_set_environment_map(void* b, lumo_spectrum tex, double scale);
+/* ... with a texture (e.g. an HDR image, Image::from_hdri_bytes): texture index of b. */
+int lumo_builder_set_environment_texture(void* b, int texture, double scale);
+
+/* Textures (texture.rs:23-92).  Each returns the texture index in b, or -1 (lumo_builder_error).
+ * texture_image: a PNG file's bytes (Image::from_file, image.rs:17-75, 254-276: 8-bit grey / grey+
+ * alpha / RGB / RGBA or palette images; texels Spectrum::from_srgb).  texture_hdr: a Radiance
+ * .hdr file's bytes (Image::from_hdri_bytes, image.rs:205-252: flat RGBE).  texture_marble:
+ * Perlin::new(seed) (perlin.rs:31-47). */
+int lumo_builder_texture_solid(void* b, lumo_spectrum spec);
+int lumo_builder_texture_image(void* b, const char* png, size_t n);
+int lumo_builder_texture_hdr(void* b, const char* hdr, size_t n);
+int lumo_builder_texture_checkerboard(void* b, int even, int odd, double scale);
+int lumo_builder_texture_marble(void* b, uint64_t seed, lumo_spectrum spec);
+int lumo_builder_texture_mandelbrot(void* b);
+/* A bump map from a PNG file's bytes (Image::bump_from_file, image.rs:142-166); returns its
+ * index or -1. */
+int lumo_builder_normal_map(void* b, const char* png, size_t n);
+/* Copy of material `base` with textured slots: albedo (microfacet kd / Light texture), ks, tf
+ * (texture indices, -1 keeps the solid spectrum) and a bump map (-1: none).  Returns the new
+ * material index or -1. */
+int lumo_builder_material_textured(void* b, int base, int albedo_tex, int ks_tex, int tf_tex, int normal_map);
+/* Register a named file (texture / bump map) for the MTL map_Kd / map_Ks / map_Ke / map_Bump
+ * statements of lumo_builder_load_obj_scene (parser.rs:_img_from_zip looks names up in the zip:
+ * '\\' becomes '/'). */
+int lumo_builder_add_file(void* b, const char* name, const char* bytes, size_t n);
+/* MtlTaskExecutor map_ks flag (parser/mtl/task.rs:53-69): 0 (default) reads map_Ks as an
+ * occlusion / roughness / metalness image (mean roughness and k, Ks = white); 1 as a texture. */
+int lumo_builder_set_map_ks(void* b, int map_ks);
 /* Instanceable / Instance transformations (object/instance.rs:203-299, kdtree.rs:93-99) applied to
  * object `index` of builder b (lights if is_light).  Each op composes AFTER the current transform;
  * rotations take the angle in x (radians).  Returns LUMO_OK or LUMO_ERR_INVALID. */

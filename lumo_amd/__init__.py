@@ -18,7 +18,7 @@ import numpy as np
 from . import _ffi
 from ._ffi import check
 
-__all__ = ["Spectrum", "Material", "Scene", "Camera", "Renderer", "Integrator", "ToneMap", "Film", "Device",
+__all__ = ["Spectrum", "Texture", "NormalMap", "Material", "Scene", "Camera", "Renderer", "Integrator", "ToneMap", "Film", "Device",
            "DENSE", "TILE_SIZE", "SAMPLES_INCREMENT", "make_tasks"]
 
 TILE_SIZE = 16          # renderer.rs:15
@@ -78,6 +78,94 @@ def named_spectrum(name):
     return Spectrum.from_rgb(*_NAMED[name])
 
 
+class Texture:
+    """lumo's Texture (texture.rs:23-92): Solid / Checkerboard / Marble / Image / Mandelbrot.
+    Registered with a scene's builder when a material (or the environment map) using it is
+    added; anywhere a Texture is accepted a Spectrum means Texture::Solid."""
+
+    def __init__(self, kind, **kw):
+        self.kind, self.kw = kind, kw
+
+    @staticmethod
+    def solid(spec):
+        return Texture("solid", spec=spec)
+
+    @staticmethod
+    def image(source):
+        """Texture::Image(Image::from_path / from_file): a PNG as a path, bytes, or (zip, member)."""
+        return Texture("image", data=_read_source(source, ".png"))
+
+    @staticmethod
+    def hdr(source):
+        """Texture::Image(Image::from_hdri_bytes): a Radiance .hdr (flat RGBE) image."""
+        return Texture("hdr", data=_read_source(source, ".hdr"))
+
+    @staticmethod
+    def checkerboard(even, odd, scale):
+        """Texture::Checkerboard(even, odd, scale): `even` where floor(u s) + floor(v s) is even."""
+        return Texture("checkerboard", even=_as_texture(even), odd=_as_texture(odd), scale=float(scale))
+
+    @staticmethod
+    def marble(seed, spec):
+        """Texture::Marble(Perlin::new(seed), spec)."""
+        return Texture("marble", seed=int(seed), spec=spec)
+
+    @staticmethod
+    def mandelbrot():
+        return Texture("mandelbrot")
+
+    def _solid_spec(self):
+        return self.kw["spec"] if self.kind == "solid" else None
+
+    def _add(self, b, cache):
+        """Index of this texture in builder b; `cache` (owned by the Scene) registers it once."""
+        if id(self) in cache:
+            return cache[id(self)][1]
+        L, k = lib(), self.kw
+        if self.kind == "solid":
+            i = L.lumo_builder_texture_solid(b, k["spec"]._s)
+        elif self.kind == "image":
+            i = L.lumo_builder_texture_image(b, k["data"], len(k["data"]))
+        elif self.kind == "hdr":
+            i = L.lumo_builder_texture_hdr(b, k["data"], len(k["data"]))
+        elif self.kind == "checkerboard":
+            i = L.lumo_builder_texture_checkerboard(b, k["even"]._add(b, cache), k["odd"]._add(b, cache), k["scale"])
+        elif self.kind == "marble":
+            i = L.lumo_builder_texture_marble(b, k["seed"], k["spec"]._s)
+        else:
+            i = L.lumo_builder_texture_mandelbrot(b)
+        if i < 0:
+            raise ValueError(f"texture {self.kind}: " + L.lumo_builder_error(b).decode())
+        cache[id(self)] = (self, i)
+        return i
+
+
+class NormalMap:
+    """A bump map, Image<Normal> (image.rs:142-166): n = normalize(rgb / 128 - 1) of a PNG."""
+
+    def __init__(self, source):
+        self.data = _read_source(source, ".png")
+
+    def _add(self, b, cache):
+        if id(self) not in cache:
+            i = lib().lumo_builder_normal_map(b, self.data, len(self.data))
+            if i < 0:
+                raise ValueError("normal map: " + lib().lumo_builder_error(b).decode())
+            cache[id(self)] = (self, i)
+        return cache[id(self)][1]
+
+
+def _as_texture(t):
+    return t if isinstance(t, Texture) else Texture.solid(t)
+
+
+def _split(t):
+    """(solid spectrum for the material slot, texture or None)"""
+    t = _as_texture(t)
+    spec = t._solid_spec()
+    return (spec, None) if spec is not None else (Spectrum.black(), t)
+
+
 class Material:
     def __init__(self, kind, **kw):
         self.kind = kind
@@ -89,14 +177,16 @@ class Material:
 
     @staticmethod
     def light(tex, illuminant="D65", scale=1.0, two_sided=False):
-        """Material::Light(texture, illuminant, scale, two_sided); Material::light uses D65."""
+        """Material::Light(texture, illuminant, scale, two_sided); Material::light uses D65.
+        `tex` a Spectrum (solid) or an image Texture (power = the image mean, image.rs:187-189)."""
         return Material("light", spec=tex, illuminant=illuminant, scale=scale, two_sided=two_sided)
 
     @staticmethod
-    def microfacet(roughness, eta, k, is_transparent, fresnel_enabled, kd, ks, tf):
-        """Material::microfacet (material.rs:26-68), solid-colour textures."""
+    def microfacet(roughness, eta, k, is_transparent, fresnel_enabled, kd, ks, tf, bump_map=None):
+        """Material::microfacet (material.rs:26-68): kd / ks / tf Textures (or Spectra), an
+        optional NormalMap bump map."""
         return Material("microfacet", roughness=roughness, eta=eta, k=k, is_transparent=is_transparent,
-                        fresnel_enabled=fresnel_enabled, kd=kd, ks=ks, tf=tf)
+                        fresnel_enabled=fresnel_enabled, kd=kd, ks=ks, tf=tf, bump_map=bump_map)
 
     @staticmethod
     def diffuse(kd):
@@ -121,9 +211,28 @@ class Material:
     def glass():
         return Material("glass")
 
-    def _add(self, b):
+    def _add(self, b, cache=None):
+        """Add to builder b: the material with the solid slots, then (when a slot holds a
+        non-solid texture or there is a bump map) its textured copy."""
+        k = dict(self.kw)
+        tex = {}
+        for slot in ("kd", "ks", "tf", "spec"):
+            if slot in k and not (self.kind == "lambertian"):
+                k[slot], t = _split(k[slot])
+                if t is not None:
+                    tex[slot] = t
+        base = self._add_solid(b, k)
+        nm = k.get("bump_map")
+        if base < 0 or (not tex and nm is None):
+            return base
+        cache = {} if cache is None else cache
+        ti = {s: t._add(b, cache) for s, t in tex.items()}
+        albedo = ti.get("kd", ti.get("spec", -1))
+        return lib().lumo_builder_material_textured(b, base, albedo, ti.get("ks", -1), ti.get("tf", -1),
+                                                    nm._add(b, cache) if nm is not None else -1)
+
+    def _add_solid(self, b, k):
         L = lib()
-        k = self.kw
         if self.kind == "lambertian":
             return L.lumo_builder_material_lambertian(b, k["spec"]._s)
         if self.kind == "microfacet":
@@ -139,10 +248,9 @@ class Material:
             return L.lumo_builder_material_mirror(b)
         if self.kind == "glass":
             return L.lumo_builder_material_glass(b)
-        ill = self.kw["illuminant"]
+        ill = k["illuminant"]
         ill = DENSE[ill] if isinstance(ill, str) else int(ill)
-        return L.lumo_builder_material_light(b, self.kw["spec"]._s, ill, float(self.kw["scale"]),
-                                             int(bool(self.kw["two_sided"])))
+        return L.lumo_builder_material_light(b, k["spec"]._s, ill, float(k["scale"]), int(bool(k["two_sided"])))
 
 
 def _read_source(source, suffix):
@@ -218,6 +326,7 @@ class Scene:
         L = lib()
         self._b = _builder if _builder is not None else L.lumo_builder_new()
         self._flat = None
+        self._tex = {}  # id(Texture / NormalMap) -> (object, index in this builder)
 
     @staticmethod
     def cornell_box():
@@ -233,7 +342,7 @@ class Scene:
         return s
 
     def _mat(self, m):
-        idx = m._add(self._b)
+        idx = m._add(self._b, self._tex)
         if idx < 0:
             raise ValueError("invalid material")
         return idx
@@ -279,20 +388,55 @@ class Scene:
         return ObjectRef(self, idx)
 
     @staticmethod
-    def from_file(path, obj_name=None, mtllib=None):
-        """parser::scene_from_file (parser.rs): `path` a .zip holding `obj_name` (and `mtllib`),
-        or a plain .obj path with an optional .mtl path.  One mesh per usemtl group; emissive
-        groups become Triangle lights.  Image texture maps are not supported."""
+    def from_file(path, obj_name=None, mtllib=None, map_ks=False, env_map=None):
+        """parser::scene_from_file (parser.rs:203-265): `path` a .zip holding `obj_name` (and
+        `mtllib`), or a plain .obj path with an optional .mtl path (texture files then resolve
+        relative to the .mtl's directory).  One mesh per usemtl group; emissive groups become
+        Triangle lights; map_Kd / map_Ke / map_Ks / map_Bump read the archive's PNGs (map_ks as in
+        MtlTaskExecutor); env_map = (member name, scale) sets a Radiance .hdr environment."""
+        import os
+        s = Scene()
+        L = lib()
         if str(path).lower().endswith(".zip"):
+            import zipfile
             obj = _read_source((path, obj_name), ".obj")
             mtl = _read_source((path, mtllib), ".mtl") if mtllib else None
+            with zipfile.ZipFile(path) as z:
+                for n in z.namelist():
+                    if not n.endswith("/") and not n.lower().endswith((".obj", ".mtl")):
+                        data = z.read(n)
+                        check(L.lumo_builder_add_file(s._b, n.encode(), data, len(data)), "add_file")
+            env = (_read_source((path, env_map[0]), ".hdr"), env_map[1]) if env_map else None
         else:
             obj = _read_source(path, ".obj")
             mtl = _read_source(mtllib, ".mtl") if mtllib else None
-        s = Scene()
-        st = lib().lumo_builder_load_obj_scene(s._b, obj, len(obj), mtl, len(mtl) if mtl else 0)
+            base = os.path.dirname(os.path.abspath(mtllib if mtllib else path))
+            for root, _, files in os.walk(base):
+                for f in files:
+                    if f.lower().endswith((".png", ".hdr")):
+                        full = os.path.join(root, f)
+                        with open(full, "rb") as fh:
+                            data = fh.read()
+                        rel = os.path.relpath(full, base).replace(os.sep, "/")
+                        check(L.lumo_builder_add_file(s._b, rel.encode(), data, len(data)), "add_file")
+            env = (_read_source(env_map[0], ".hdr"), env_map[1]) if env_map else None
+        # parser.rs:219-249: the explicit mtllib, then every `mtllib` statement of the .obj
+        mtls = [mtl] if mtl else []
+        for line in obj.decode("utf-8", "replace").splitlines():
+            tok = line.split()
+            if len(tok) >= 2 and tok[0] == "mtllib":
+                name = tok[1]
+                if str(path).lower().endswith(".zip"):
+                    mtls.append(_read_source((path, name), ".mtl"))
+                else:
+                    mtls.append(_read_source(os.path.join(os.path.dirname(os.path.abspath(path)), name), ".mtl"))
+        mtl = b"\n".join(mtls) if mtls else None
+        check(L.lumo_builder_set_map_ks(s._b, int(bool(map_ks))), "map_ks")
+        st = L.lumo_builder_load_obj_scene(s._b, obj, len(obj), mtl, len(mtl) if mtl else 0)
         if st != _ffi.LUMO_OK:
-            raise ValueError("obj scene: " + lib().lumo_builder_error(s._b).decode())
+            raise ValueError("obj scene: " + L.lumo_builder_error(s._b).decode())
+        if env is not None:
+            s.set_environment_map(Texture("hdr", data=env[0]), env[1])
         return s
 
     def add_sphere(self, radius, material, light=False):
@@ -304,8 +448,14 @@ class Scene:
         return ObjectRef(self, lib().lumo_builder_count(self._b, int(light)) - 1, light)
 
     def set_environment_map(self, tex, scale):
-        """Scene::set_environment_map (scene.rs:73-78): constant-texture environment light."""
-        check(lib().lumo_builder_set_environment_map(self._b, tex._s, float(scale)), "environment map")
+        """Scene::set_environment_map (scene.rs:73-78): a Spectrum (constant) or an image / HDR
+        Texture on the environment sphere."""
+        spec, t = _split(tex)
+        if t is None:
+            check(lib().lumo_builder_set_environment_map(self._b, spec._s, float(scale)), "environment map")
+        else:
+            check(lib().lumo_builder_set_environment_texture(self._b, t._add(self._b, self._tex), float(scale)),
+                  "environment map")
         self._flat = None
 
     def build(self):

@@ -29,7 +29,25 @@ class Material(C.Structure):
     _fields_ = [("kind", C.c_int32), ("two_sided", C.c_int32), ("illuminant", C.c_int32),
                 ("eta_idx", C.c_int32), ("k_idx", C.c_int32), ("flags", C.c_int32),
                 ("scale", C.c_double), ("roughness", C.c_double),
-                ("albedo", Spectrum), ("ks", Spectrum), ("tf", Spectrum)]
+                ("albedo", Spectrum), ("ks", Spectrum), ("tf", Spectrum),
+                ("albedo_tex", C.c_int32), ("ks_tex", C.c_int32), ("tf_tex", C.c_int32), ("normal_map", C.c_int32)]
+
+
+MAT_BLANK, MAT_LAMBERTIAN, MAT_LIGHT, MAT_MF_DIFFUSE, MAT_MF_CONDUCTOR, MAT_MF_DIELECTRIC = range(6)
+TEX_SOLID, TEX_IMAGE, TEX_CHECKERBOARD, TEX_MARBLE, TEX_MANDELBROT = range(5)
+
+
+class Texture(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("width", C.c_int32), ("height", C.c_int32), ("first", C.c_int32),
+                ("second", C.c_int32), ("pad0", C.c_int32), ("scale", C.c_double), ("spec", Spectrum)]
+
+
+class NormalMap(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("first", C.c_int32), ("pad0", C.c_int32)]
+
+
+class Perlin(C.Structure):
+    _fields_ = [("lattice", (C.c_double * 3) * 256), ("perm", (C.c_int32 * 256) * 3)]
 
 
 class BvhNode(C.Structure):
@@ -74,6 +92,11 @@ class SceneDesc(C.Structure):
         ("num_materials", C.c_int32), ("num_dense_spectra", C.c_int32),
         ("materials", C.POINTER(Material)), ("dense_spectra", c_double_p),
         ("num_transforms", C.c_int32), ("pad1", C.c_int32), ("transforms", C.POINTER(Transform)),
+        ("num_textures", C.c_int32), ("num_texels", C.c_int32),
+        ("textures", C.POINTER(Texture)), ("texels", C.POINTER(Spectrum)),
+        ("num_normal_maps", C.c_int32), ("num_normal_texels", C.c_int32),
+        ("normal_maps", C.POINTER(NormalMap)), ("normal_texels", c_double_p),
+        ("num_perlin", C.c_int32), ("pad2", C.c_int32), ("perlin", C.POINTER(Perlin)),
     ]
 
 
@@ -193,6 +216,17 @@ HOST_API = [
     ("lumo_builder_count", C.c_int64, [C.c_void_p, C.c_int]),
     ("lumo_builder_add_sphere", C.c_int, [C.c_void_p, C.c_double, C.c_int, C.c_int]),
     ("lumo_builder_set_environment_map", C.c_int, [C.c_void_p, Spectrum, C.c_double]),
+    ("lumo_builder_set_environment_texture", C.c_int, [C.c_void_p, C.c_int, C.c_double]),
+    ("lumo_builder_texture_solid", C.c_int, [C.c_void_p, Spectrum]),
+    ("lumo_builder_texture_image", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    ("lumo_builder_texture_hdr", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    ("lumo_builder_texture_checkerboard", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double]),
+    ("lumo_builder_texture_marble", C.c_int, [C.c_void_p, C.c_uint64, Spectrum]),
+    ("lumo_builder_texture_mandelbrot", C.c_int, [C.c_void_p]),
+    ("lumo_builder_normal_map", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    ("lumo_builder_material_textured", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    ("lumo_builder_add_file", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t]),
+    ("lumo_builder_set_map_ks", C.c_int, [C.c_void_p, C.c_int]),
     ("lumo_builder_add_obj_mesh", C.c_int64, [C.c_void_p, C.c_char_p, C.c_size_t, C.c_int]),
     ("lumo_builder_load_obj_scene", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]),
     ("lumo_builder_error", C.c_char_p, [C.c_void_p]),

@@ -24,11 +24,12 @@ constexpr int BDPT_RR_DEPTH = 5, BDPT_MAX_DEPTH = 1024;  // path_gen.rs
 enum { TR_RADIANCE = 0, TR_IMPORTANCE = 1 };
 enum { VF_BLANK = 1, VF_BACKFACE = 2, VF_DELTA = 4 };
 constexpr int32_t REDO_DROPPED = -2;  // redo_index of a sample that overflowed a full redo list  // VF_DELTA: Material::is_delta at L[0] (never changes)
-constexpr int VD_N = 22, VI_N = 3;  // doubles / ints per stored vertex
+constexpr int VD_N = 23, VI_N = 3;  // doubles / ints per stored vertex
 
 // A subpath vertex (vertex.rs).  `blank` marks the camera vertex (Material::Blank).
 struct BVtx {
     V3 p, err, ns, ng, wo;
+    V2 uv;  // the hit's texture coordinates (textures and bump maps of the vertex's material)
     DColor gath;
     double pdf_fwd, pdf_bck;
     int mat, light;
@@ -53,6 +54,8 @@ struct VStore {
         for (int k = 0; k < NS; ++k) D(15 + k, v, s) = x.gath.s[k];
         D(19, v, s) = x.pdf_fwd;
         D(20, v, s) = x.pdf_bck;
+        D(21, v, s) = x.uv.x;
+        D(22, v, s) = x.uv.y;
         I(0, v, s) = x.mat;
         I(1, v, s) = x.light;
         I(2, v, s) = (x.blank ? VF_BLANK : 0) | (x.backface ? VF_BACKFACE : 0) | (x.del ? VF_DELTA : 0);
@@ -64,6 +67,7 @@ struct VStore {
         for (int k = 0; k < NS; ++k) x.gath.s[k] = D(15 + k, v, s);
         x.pdf_fwd = D(19, v, s);
         x.pdf_bck = D(20, v, s);
+        x.uv = V2{D(21, v, s), D(22, v, s)};
         x.mat = I(0, v, s);
         x.light = I(1, v, s);
         const int f = I(2, v, s);
@@ -110,7 +114,7 @@ __device__ __forceinline__ DHit vtx_hit(const BVtx& v) {
     h.err = v.err;
     h.ns = v.ns;
     h.ng = v.ng;
-    h.uv = V2{0.0, 0.0};
+    h.uv = v.uv;
     h.backface = v.backface;
     return h;
 }
@@ -275,6 +279,7 @@ __device__ __forceinline__ BVtx vtx_camera(V3 xo, double pdf_fwd, DColor gathere
     v.ns = V3{1.0, 0.0, 0.0};
     v.ng = V3{1.0, 0.0, 0.0};
     v.wo = V3{0.0, 0.0, 0.0};
+    v.uv = V2{0.0, 0.0};
     v.gath = gathered;
     v.pdf_fwd = pdf_fwd;
     v.pdf_bck = 0.0;
@@ -291,6 +296,7 @@ __device__ __forceinline__ BVtx vtx_of_hit(const DHit& h, DColor gathered, doubl
     v.ns = h.ns;
     v.ng = h.ng;
     v.wo = wo;
+    v.uv = h.uv;
     v.gath = gathered;
     v.pdf_fwd = pdf_fwd;
     v.pdf_bck = 0.0;
@@ -551,7 +557,7 @@ template <bool FX>
 __device__ DColor add_camera_path(const DScene& sc, const DCam& cam, const double* L, const PView& cp, int t) {
     const BVtx ct = cp.get(t - 1);
     if (ct.light < 0) return cfill(0.0);
-    const DColor rad = ct.gath * emit(sc, sc.mats[ct.mat], L, ct.backface);
+    const DColor rad = ct.gath * emit(sc, sc.mats[ct.mat], L, ct.backface, ct.uv);
     if (rad.s[0] == 0.0 && rad.s[1] == 0.0 && rad.s[2] == 0.0 && rad.s[3] == 0.0) return cfill(0.0);
     const PView none{nullptr, 0, nullptr};
     return rad * mis_weight<FX>(sc, cam, L, none, 0, cp, t);
@@ -583,7 +589,7 @@ __device__ DColor connect_camera_path(const DScene& sc, const DCam& cam, double 
     if (p_lig == 0.0) return cfill(0.0);
     wi = ri.d;
     const double pdf_origin = sa_to_area(p_lig, xo, xi, wi, ngi);
-    const DColor em = emit(sc, sc.mats[hi.material], L, hi.backface);
+    const DColor em = emit(sc, sc.mats[hi.material], L, hi.backface, hi.uv);
     const BVtx ll = vtx_of_hit(hi, em, pdf_origin, V3{0.0, 0.0, 0.0}, li);
     const DColor bsdf = v_f<FX>(sc, cl, ll.p, L, TR_RADIANCE);
     const double cos_wi = v_shading_cosine(sc, cl, wi, cl.ns);
@@ -704,7 +710,7 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_light_init(DScene sc, Paths S, B
         const Ray ri = spawn(ho, onb_world(onb_new(ho.ns), wi_l));
         const double pdf_origin = 1.0 / light_area(sc, light);
         const double pdf_dir = dot(ho.ng, ri.d) / PI;
-        const DColor em = emit(sc, sc.mats[ho.material], L, ho.backface);
+        const DColor em = emit(sc, sc.mats[ho.material], L, ho.backface, ho.uv);
         B.lp.store(0, slot, vtx_of_hit(ho, em, pdf_origin * pdf_light, V3{0.0, 0.0, 0.0}, li));
         stc(S.gath, slot, em * fabs(dot(ri.d, ho.ns)) / (pdf_light * pdf_origin * pdf_dir));
         stv3(S.ro, slot, ri.o);
@@ -875,7 +881,7 @@ __device__ bool bdpt_walks(const DScene& sc, const Paths& S, const Tasks& T, con
         const Ray ri = spawn(ho, onb_world(onb_new(ho.ns), wi_l));
         const double pdf_origin = 1.0 / light_area(sc, light);
         const double pdf_dir = dot(ho.ng, ri.d) / PI;
-        const DColor em = emit(sc, sc.mats[ho.material], L, ho.backface);
+        const DColor em = emit(sc, sc.mats[ho.material], L, ho.backface, ho.uv);
         const BVtx root = vtx_of_hit(ho, em, pdf_origin * pdf_light, V3{0.0, 0.0, 0.0}, li);
         const DColor gathered = em * fabs(dot(ri.d, ho.ns)) / (pdf_light * pdf_origin * pdf_dir);
         n_l = bdpt_walk<STK, FX>(sc, X.lp, si, ri, rng, L, delta, root, gathered, pdf_dir, TR_IMPORTANCE, C, queries);

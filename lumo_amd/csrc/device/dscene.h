@@ -70,6 +70,11 @@ struct DScene {
     const lumo_material* mats;
     const double* dense;
     const lumo_transform* xforms;
+    const lumo_texture* textures;
+    const lumo_spectrum* texels;
+    const lumo_normal_map* nmaps;
+    const double* ntexels;
+    const lumo_perlin* perlin;
     int32_t n_onodes, n_lnodes, n_lights, n_shadow, stack_class, full, n_objs, pad_n;
     // Traversal working set packed contiguously (16-B aligned sub-arrays) so that a small scene
     // can be staged into LDS once per workgroup; hot_bytes == 0 disables staging.
@@ -245,6 +250,107 @@ __device__ __forceinline__ V3 color_xyz(const DScene& sc, const DColor& c, const
     return V3{cmean(dense_sample(sc.dense, L) * c / pdf), cmean(dense_sample(sc.dense + 95, L) * c / pdf),
               cmean(dense_sample(sc.dense + 190, L) * c / pdf)} /
            Y_INTEGRAL;
+}
+
+// ---------------------------------------------------------------- textures (texture.rs, image.rs, perlin.rs)
+// Rust `as` casts saturate (NaN and negatives -> 0).
+__device__ __forceinline__ uint32_t sat_u32(double x) { return x != x || x <= 0.0 ? 0u : (x >= 4294967295.0 ? 4294967295u : (uint32_t)x); }
+__device__ __forceinline__ uint64_t sat_u64(double x) {
+    return x != x || x <= 0.0 ? 0ull : (x >= 18446744073709551615.0 ? ~0ull : (uint64_t)x);
+}
+// Image::bilin_interp (image.rs:99-128): texel corners and weights of uv
+struct Bilin {
+    uint32_t i00, i10, i01, i11;
+    double wx, wy;  // x0y0
+};
+__device__ __forceinline__ Bilin bilin(int32_t width, int32_t height, V2 uv) {
+    const double w = (double)width, h = (double)height;
+    const V2 xy{uv.x * w, (1.0 - uv.y) * h};
+    const V2 xoyo{floor(xy.x - 0.5), floor(xy.y - 0.5)};
+    const V2 x1y1{xy.x - xoyo.x - 0.5, xy.y - xoyo.y - 0.5};
+    const uint32_t W = (uint32_t)width, H = (uint32_t)height;
+    const uint32_t xo = sat_u32(xoyo.x + w) % W, yo = sat_u32(xoyo.y + h) % H;
+    const uint32_t xi = (xo + 1) % W, yi = (yo + 1) % H;
+    return Bilin{xo + yo * W, xi + yo * W, xo + yi * W, xi + yi * W, 1.0 - x1y1.x, 1.0 - x1y1.y};
+}
+// Image<Spectrum>::value_at (image.rs:170-184)
+__device__ __forceinline__ DColor image_at(const DScene& sc, const lumo_texture& T, V2 uv, const double* L) {
+    const Bilin b = bilin(T.width, T.height, uv);
+    const lumo_spectrum* tx = sc.texels + T.first;
+    const DColor y0 = spec_sample(tx[b.i00], L) * b.wx + spec_sample(tx[b.i10], L) * (1.0 - b.wx);
+    const DColor y1 = spec_sample(tx[b.i01], L) * b.wx + spec_sample(tx[b.i11], L) * (1.0 - b.wx);
+    return y0 * b.wy + y1 * (1.0 - b.wy);
+}
+// Perlin::noise_at (perlin.rs:50-125)
+__device__ __forceinline__ V3 vfract(V3 v) { return V3{v.x - trunc(v.x), v.y - trunc(v.y), v.z - trunc(v.z)}; }
+__device__ double perlin_noise(const lumo_perlin& P, V3 p) {
+    const V3 w0 = vfract(p);
+    const V3 fl{floor(p.x), floor(p.y), floor(p.z)};
+    auto smoother = [](double x) { return ((6.0 * x - 15.0) * x + 10.0) * x * x * x; };
+    const V3 w{smoother(w0.x), smoother(w0.y), smoother(w0.z)};
+    const uint64_t bx = sat_u64(fl.x), by = sat_u64(fl.y), bz = sat_u64(fl.z);
+    double acc = 0.0;
+    for (int c = 0; c < 8; ++c) {  // cartesian (x, y, z), z fastest
+        const int i = c >> 2, j = (c >> 1) & 1, k = c & 1;
+        const int hsh = P.perm[0][(bx + i) % 256] ^ P.perm[1][(by + j) % 256] ^ P.perm[2][(bz + k) % 256];
+        const V3 nrm{P.lattice[hsh][0], P.lattice[hsh][1], P.lattice[hsh][2]};
+        const V3 idx{(double)i, (double)j, (double)k};
+        const V3 widx{2.0 * w.x * idx.x + 1.0 - w.x - idx.x, 2.0 * w.y * idx.y + 1.0 - w.y - idx.y,
+                      2.0 * w.z * idx.z + 1.0 - w.z - idx.z};
+        acc = acc + widx.x * widx.y * widx.z * dot(nrm, w - idx);
+    }
+    return acc;
+}
+__device__ __forceinline__ double powi6(double x) {  // llvm.powi(x, 6): x^2 * (x^2)^2
+    const double x2 = x * x;
+    return x2 * (x2 * x2);
+}
+// Texture::albedo_at (texture.rs:53-92); tex < 0: the solid spectrum of the material slot
+__device__ DColor tex_at(const DScene& sc, int tex, const lumo_spectrum& solid, V2 uv, const double* L) {
+    if (tex < 0) return spec_sample(solid, L);
+    for (;;) {  // checkerboards descend to a child (children precede parents: terminates)
+        const lumo_texture& T = sc.textures[tex];
+        if (T.kind == LUMO_TEX_SOLID) return spec_sample(T.spec, L);
+        if (T.kind == LUMO_TEX_IMAGE) return image_at(sc, T, uv, L);
+        if (T.kind == LUMO_TEX_CHECKERBOARD) {
+            const V2 uvs{uv.x * T.scale, uv.y * T.scale};
+            tex = sat_u64(floor(uvs.x) + floor(uvs.y)) % 2 == 0 ? T.first : T.second;
+            continue;
+        }
+        if (T.kind == LUMO_TEX_MARBLE) {
+            const lumo_perlin& P = sc.perlin[T.first];
+            V3 p = 4.0 * V3{fabs(uv.x), fabs(uv.y), 0.0};  // MARBLE_SCALE * uvw.abs()
+            double turb = 0.0;
+            double gain = 1.0;
+            for (int d = 0; d < 6; ++d) {  // turbulence: MARBLE_OCTAVES 6, MARBLE_GAIN 0.5
+                turb = turb + gain * fabs(perlin_noise(P, p));
+                p = 2.0 * p;
+                gain = gain * 0.5;
+            }
+            const double scaled = 1.0 - powi6(0.5 + 0.5 * lm_sin(60.0 * uv.x + 20.0 * turb));
+            return spec_sample(T.spec, L) * scaled;
+        }
+        // Mandelbrot: 256 iterations, escape radius 64
+        const double cr = 2.0 * (uv.x - 0.75), ci = 2.0 * (uv.y - 0.5);
+        double zr = 0.0, zi = 0.0;
+        int depth = 0;
+        while (depth < 256 && zr * zr + zi * zi < 4096.0) {
+            const double nr = zr * zr - zi * zi + cr;
+            const double ni = zr * zi + zi * zr + ci;
+            zr = nr;
+            zi = ni;
+            depth++;
+        }
+        return cfill(depth == 256 ? 1.0 : 0.0);
+    }
+}
+// Image<Normal>::value_at (image.rs:131-140) and Material::map_normal (material.rs:323-331)
+__device__ __forceinline__ V3 nmap_at(const DScene& sc, const lumo_normal_map& M, V2 uv) {
+    const Bilin b = bilin(M.width, M.height, uv);
+    const double* t = sc.ntexels + 3 * (size_t)M.first;
+    auto n = [&](uint32_t i) { return V3{t[3 * i], t[3 * i + 1], t[3 * i + 2]}; };
+    auto lerp = [](V3 n0, V3 n1, double v) { return normalize(n0 * v + n1 * (1.0 - v)); };
+    return lerp(lerp(n(b.i00), n(b.i10), b.wx), lerp(n(b.i01), n(b.i11), b.wx), b.wy);
 }
 
 // ---------------------------------------------------------------- hits
@@ -909,6 +1015,25 @@ __device__ __forceinline__ bool standard_kind(int k) {
            k == LUMO_MAT_MF_DIELECTRIC;
 }
 
+// Material::map_normal (material.rs:323-331): the bump-mapped shading normal of Standard materials
+template <bool FX>
+__device__ __forceinline__ V3 mapped_ns(const DScene& sc, const lumo_material& m, const DHit& h) {
+    if constexpr (FX) {
+        if (m.normal_map >= 0) return normalize(onb_world(onb_new(h.ns), nmap_at(sc, sc.nmaps[m.normal_map], h.uv)));
+    }
+    return h.ns;
+}
+// MfDistribution::kd / ks / tf (microfacet.rs:118-134): Texture::albedo_at at the hit's uv
+__device__ __forceinline__ DColor mat_kd(const DScene& sc, const lumo_material& m, V2 uv, const double* L) {
+    return tex_at(sc, m.albedo_tex, m.albedo, uv, L);
+}
+__device__ __forceinline__ DColor mat_ks(const DScene& sc, const lumo_material& m, V2 uv, const double* L) {
+    return tex_at(sc, m.ks_tex, m.ks, uv, L);
+}
+__device__ __forceinline__ DColor mat_tf(const DScene& sc, const lumo_material& m, V2 uv, const double* L) {
+    return tex_at(sc, m.tf_tex, m.tf, uv, L);
+}
+
 // Material::bsdf_sample (material.rs:273-289 -> bsdf.rs -> bxdf.rs:104-124); may terminate L
 template <bool FX>
 __device__ bool bsdf_sample(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, double* L,
@@ -919,7 +1044,7 @@ __device__ bool bsdf_sample(const DScene& sc, const lumo_material& m, const DHit
         return true;
     }
     if (!standard_kind(m.kind)) return false;
-    const Onb uvw = onb_new(h.ns);
+    const Onb uvw = onb_new(mapped_ns<FX>(sc, m, h));
     const V3 o = onb_local(uvw, wo);
     if (h.backface && m.kind != LUMO_MAT_MF_DIELECTRIC) return false;
     V3 w;
@@ -970,7 +1095,7 @@ __device__ double bsdf_pdf(const DScene& sc, const lumo_material& m, const DHit&
     }
     if (!standard_kind(m.kind)) return 0.0;
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
-    const Onb uvw = onb_new(h.ns);
+    const Onb uvw = onb_new(mapped_ns<FX>(sc, m, h));
     const V3 o = onb_local(uvw, wo), i = onb_local(uvw, wi);
     if (!reflection && m.kind != LUMO_MAT_MF_DIELECTRIC) return 0.0;
     if (m.kind == LUMO_MAT_LAMBERTIAN) return cos_hemisphere_pdf(o, i);
@@ -1019,7 +1144,7 @@ __device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h
     }
     if (!standard_kind(m.kind)) return cfill(0.0);
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
-    const Onb uvw = onb_new(h.ns);
+    const Onb uvw = onb_new(mapped_ns<FX>(sc, m, h));
     const V3 o = onb_local(uvw, wo), i = onb_local(uvw, wi);
     if ((!reflection || h.backface) && m.kind != LUMO_MAT_MF_DIELECTRIC) return cfill(0.0);
     if (m.kind == LUMO_MAT_LAMBERTIAN) return spec_sample(m.albedo, L) / PI;
@@ -1032,10 +1157,10 @@ __device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h
         const double r2 = sq(d.a);
         const double fd90 = 0.5 * r2 + 2.0 * sq(wh.z) * r2;
         const double fd = schlick(1.0, fd90, o.z) * schlick(1.0, fd90, i.z) * (1.0 + r2 * (1.0 / 1.51 - 1.0));
-        return fr * spec_sample(m.ks, L) + spec_sample(m.albedo, L) * (cfill(1.0) - F) * fd / PI;
+        return fr * mat_ks(sc, m, h.uv, L) + mat_kd(sc, m, h.uv, L) * (cfill(1.0) - F) * fd / PI;
     }
     if (m.kind == LUMO_MAT_MF_CONDUCTOR) {
-        const DColor ks = spec_sample(m.ks, L);
+        const DColor ks = mat_ks(sc, m, h.uv, L);
         if (mf_delta(d)) return ks * fresnel(d, o, V3{0.0, 0.0, 1.0}, L) / fabs(i.z);
         return ks * reflect_coeff(d, o, i, L);
     }
@@ -1044,14 +1169,14 @@ __device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h
     const bool flat = eta == 1.0 || mf_delta(d);
     V3 wh = flat ? V3{0.0, 0.0, 1.0} : normalize(i * er + o);
     if (reflection) {
-        const DColor ks = spec_sample(m.ks, L);
+        const DColor ks = mat_ks(sc, m, h.uv, L);
         if (flat) return ks * fresnel(d, o, wh, L) / fabs(i.z);
         return ks * reflect_coeff(d, o, i, L);
     }
     const DColor F = fresnel(d, o, wh, L);
     if (wh.z < 0.0) wh = -wh;
     const double scale = importance ? 1.0 : er * er;
-    const DColor tf = spec_sample(m.tf, L);
+    const DColor tf = mat_tf(sc, m, h.uv, L);
     if (flat) return tf * (cfill(1.0) - F) / (scale * fabs(i.z));
     const double hwo = dot(wh, o), hwi = dot(wh, i);
     return tf * mf_D(d, wh) * (cfill(1.0) - F) * mf_G(d, o, i, wh) / scale * fabs(hwi * hwo / (i.z * o.z)) /
@@ -1075,10 +1200,11 @@ __device__ __forceinline__ bool mat_is_delta(const DScene& sc, const lumo_materi
         return (m.roughness + m.roughness) / 2.0 < 1e-3 || dense_one(sc.dense + 95 * m.eta_idx, L[0]) == 1.0;
     return false;
 }
-__device__ __forceinline__ DColor emit(const DScene& sc, const lumo_material& m, const double* L, bool backface) {
+// Material::emit (material.rs:221-234): Texture::albedo_at of the emission texture at the hit's uv
+__device__ __forceinline__ DColor emit(const DScene& sc, const lumo_material& m, const double* L, bool backface, V2 uv) {
     if (m.kind != LUMO_MAT_LIGHT) return cfill(0.0);
     if (!m.two_sided && backface) return cfill(0.0);
-    return m.scale * spec_sample(m.albedo, L) * dense_sample(sc.dense + 95 * m.illuminant, L);
+    return m.scale * tex_at(sc, m.albedo_tex, m.albedo, uv, L) * dense_sample(sc.dense + 95 * m.illuminant, L);
 }
 
 // lights (bvh.rs:51-86; Rectangle sample_on / sample_towards_pdf)

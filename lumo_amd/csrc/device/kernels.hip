@@ -1270,6 +1270,25 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
             return LUMO_ERR_INVALID;
         if (m.kind == LUMO_MAT_LIGHT && (m.illuminant < 0 || m.illuminant >= d->num_dense_spectra))
             return LUMO_ERR_INVALID;
+        for (int t : {m.albedo_tex, m.ks_tex, m.tf_tex})
+            if (t < -1 || t >= d->num_textures) return LUMO_ERR_INVALID;
+        if (m.normal_map < -1 || m.normal_map >= d->num_normal_maps) return LUMO_ERR_INVALID;
+    }
+    // texture tables (texture.rs): checkerboard children precede their parent, so sampling ends
+    for (int i = 0; i < d->num_textures; ++i) {
+        const lumo_texture& t = d->textures[i];
+        const bool ok = t.kind == LUMO_TEX_SOLID || t.kind == LUMO_TEX_MANDELBROT ||
+                        (t.kind == LUMO_TEX_IMAGE && t.width > 0 && t.height > 0 && t.first >= 0 &&
+                         (int64_t)t.first + (int64_t)t.width * t.height <= d->num_texels) ||
+                        (t.kind == LUMO_TEX_CHECKERBOARD && t.first >= 0 && t.first < i && t.second >= 0 && t.second < i) ||
+                        (t.kind == LUMO_TEX_MARBLE && t.first >= 0 && t.first < d->num_perlin);
+        if (!ok) return LUMO_ERR_INVALID;
+    }
+    for (int i = 0; i < d->num_normal_maps; ++i) {
+        const lumo_normal_map& n = d->normal_maps[i];
+        if (!(n.width > 0 && n.height > 0 && n.first >= 0 &&
+              (int64_t)n.first + (int64_t)n.width * n.height <= d->num_normal_texels))
+            return LUMO_ERR_INVALID;
     }
     for (int i = 0; i < d->num_lights + d->num_objects; ++i) {
         const lumo_object& o = i < d->num_lights ? d->lights[i] : d->objects[i - d->num_lights];
@@ -1328,6 +1347,11 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     chk(upload(*c, d->materials, (size_t)d->num_materials, &s.mats));
     chk(upload(*c, d->dense_spectra, (size_t)95 * d->num_dense_spectra, &s.dense));
     chk(upload(*c, d->transforms, (size_t)d->num_transforms, &s.xforms));
+    chk(upload(*c, d->textures, (size_t)d->num_textures, &s.textures));
+    chk(upload(*c, d->texels, (size_t)d->num_texels, &s.texels));
+    chk(upload(*c, d->normal_maps, (size_t)d->num_normal_maps, &s.nmaps));
+    chk(upload(*c, d->normal_texels, (size_t)3 * d->num_normal_texels, &s.ntexels));
+    chk(upload(*c, d->perlin, (size_t)d->num_perlin, &s.perlin));
     // device-only layouts: triangle vertex soup and 16-B kd nodes
     std::vector<double> tv((size_t)TV_STRIDE * d->num_triangles, 0.0);
     for (int i = 0; i < d->num_triangles; ++i)
@@ -1447,6 +1471,10 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     for (int i = 0; i < d->num_objects; ++i)
         full = full || (d->objects[i].type != LUMO_OBJ_KDMESH && d->objects[i].type != LUMO_OBJ_RECTANGLE);
     for (int i = 0; i < d->num_lights; ++i) full = full || d->lights[i].type != LUMO_OBJ_RECTANGLE;
+    for (int i = 0; i < d->num_materials; ++i) {  // textures and bump maps are sampled by the full kernels only
+        const lumo_material& m = d->materials[i];
+        full = full || m.albedo_tex >= 0 || m.ks_tex >= 0 || m.tf_tex >= 0 || m.normal_map >= 0;
+    }
     if (const char* e = std::getenv("LUMO_FULL_KERNELS")) full = full || std::atoi(e) != 0;  // A/B switch
     s.full = full ? 1 : 0;
     c->has_scene = true;

@@ -133,7 +133,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade_q(DScene sc, 
                 const V2 rsq = xs_vec2(rng);
                 sampled = bsdf_sample<FX>(sc, m, ho, wo, L, rand_u, rsq, wi);  // may terminate L
                 if (!sampled) {
-                    if (flags & QF_SPECULAR) radiance = radiance + gathered * emit(sc, m, L, ho.backface);
+                    if (flags & QF_SPECULAR) radiance = radiance + gathered * emit(sc, m, L, ho.backface, ho.uv);
                 } else {
                     resolve = !mat_is_delta<FX>(sc, m, L);
                     if (resolve && buckets > 1) {  // origin object of the shadow rays (objects, then lights)
@@ -252,7 +252,7 @@ __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const Shadow
             const double p_denom = li_mode ? p_lig : p_sct;
             const lumo_material hm = sc.mats[hi.material];
             const DColor f{{Q.D(b + 6, r), Q.D(b + 7, r), Q.D(b + 8, r), Q.D(b + 9, r)}};
-            out = f * cfill(1.0) * emit(sc, hm, L, hi.backface) * Q.D(b + 11, r) * weight / p_denom;
+            out = f * cfill(1.0) * emit(sc, hm, L, hi.backface, hi.uv) * Q.D(b + 11, r) * weight / p_denom;
         }
     }
     return out;

@@ -118,6 +118,111 @@ int64_t lumo_builder_add_obj_mesh(void* b, const char* obj, size_t n, int materi
     }
     return (int64_t)sb->objects.size() - 1;
 }
+int lumo_builder_set_environment_texture(void* b, int texture, double scale) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || texture < 0 || texture >= (int)sb->textures.size()) return LUMO_ERR_INVALID;
+    sb->has_env = true;
+    sb->env_tex = spectrum_black();
+    sb->env_texture = texture;
+    sb->env_scale = scale;
+    return LUMO_OK;
+}
+
+namespace {
+int push_texture(SceneBuilder* sb, const HostTexture& t) {
+    sb->textures.push_back(t);
+    return (int)sb->textures.size() - 1;
+}
+}  // namespace
+
+int lumo_builder_texture_solid(void* b, lumo_spectrum spec) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb) return -1;
+    HostTexture t;
+    t.t.kind = LUMO_TEX_SOLID;
+    t.t.spec = spec;
+    return push_texture(sb, t);
+}
+int lumo_builder_texture_image(void* b, const char* png, size_t n) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || !png) return -1;
+    HostTexture t;
+    if (!texture_from_png(reinterpret_cast<const uint8_t*>(png), n, t, sb->error)) return -1;
+    return push_texture(sb, t);
+}
+int lumo_builder_texture_hdr(void* b, const char* hdr, size_t n) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || !hdr) return -1;
+    HostTexture t;
+    if (!texture_from_hdr(reinterpret_cast<const uint8_t*>(hdr), n, t, sb->error)) return -1;
+    return push_texture(sb, t);
+}
+int lumo_builder_texture_checkerboard(void* b, int even, int odd, double scale) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    // children must already exist: the texture graph stays acyclic (Box<Texture> in texture.rs:30)
+    if (!sb || even < 0 || odd < 0 || even >= (int)sb->textures.size() || odd >= (int)sb->textures.size()) return -1;
+    HostTexture t;
+    t.t.kind = LUMO_TEX_CHECKERBOARD;
+    t.t.first = even;
+    t.t.second = odd;
+    t.t.scale = scale;
+    return push_texture(sb, t);
+}
+int lumo_builder_texture_marble(void* b, uint64_t seed, lumo_spectrum spec) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb) return -1;
+    sb->perlins.push_back(perlin_new(seed));
+    HostTexture t;
+    t.t.kind = LUMO_TEX_MARBLE;
+    t.t.first = (int32_t)sb->perlins.size() - 1;
+    t.t.spec = spec;
+    return push_texture(sb, t);
+}
+int lumo_builder_texture_mandelbrot(void* b) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb) return -1;
+    HostTexture t;
+    t.t.kind = LUMO_TEX_MANDELBROT;
+    return push_texture(sb, t);
+}
+int lumo_builder_normal_map(void* b, const char* png, size_t n) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || !png) return -1;
+    HostNormalMap m;
+    if (!normal_map_from_png(reinterpret_cast<const uint8_t*>(png), n, m, sb->error)) return -1;
+    sb->normal_maps.push_back(std::move(m));
+    return (int)sb->normal_maps.size() - 1;
+}
+int lumo_builder_material_textured(void* b, int base, int albedo_tex, int ks_tex, int tf_tex, int normal_map) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || base < 0 || base >= (int)sb->materials.size()) return -1;
+    const int nt = (int)sb->textures.size();
+    for (int t : {albedo_tex, ks_tex, tf_tex})
+        if (t < -1 || t >= nt) return -1;
+    if (normal_map < -1 || normal_map >= (int)sb->normal_maps.size()) return -1;
+    HostMaterial m = sb->materials[base];
+    m.m.albedo_tex = albedo_tex;
+    m.m.ks_tex = ks_tex;
+    m.m.tf_tex = tf_tex;
+    m.m.normal_map = normal_map;
+    return sb->add_material(m);
+}
+int lumo_builder_add_file(void* b, const char* name, const char* bytes, size_t n) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || !name || (!bytes && n)) return LUMO_ERR_INVALID;
+    std::string nm(name);
+    for (char& ch : nm)
+        if (ch == '\\') ch = '/';
+    sb->files.emplace_back(nm, std::vector<uint8_t>(bytes, bytes + n));
+    return LUMO_OK;
+}
+int lumo_builder_set_map_ks(void* b, int map_ks) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb) return LUMO_ERR_INVALID;
+    sb->map_ks = map_ks != 0;
+    return LUMO_OK;
+}
+
 int lumo_builder_load_obj_scene(void* b, const char* obj, size_t n_obj, const char* mtl, size_t n_mtl) {
     SceneBuilder* sb = static_cast<SceneBuilder*>(b);
     if (!sb || !obj) return LUMO_ERR_INVALID;

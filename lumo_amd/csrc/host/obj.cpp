@@ -1,7 +1,6 @@
 // Wavefront .obj / .mtl ingest (lumo src/parser.rs, parser/obj.rs, parser/mtl.rs,
-// parser/mtl/task.rs).  Texture maps (map_Kd / map_Ks / map_Ke / map_Bump) are not supported:
-// image textures are outside the implemented scope, and such statements are
-// reported as an error rather than silently ignored.
+// parser/mtl/task.rs).  Texture maps (map_Kd / map_Ks / map_Ke / map_Bump) are read from the
+// files registered with the builder (lumo_builder_add_file), as lumo reads them from the zip.
 #include "obj.h"
 
 #include <cmath>
@@ -166,7 +165,8 @@ bool parse_obj(const char* data, size_t n, const std::unordered_map<std::string,
     return true;
 }
 
-bool parse_mtl(const char* data, size_t n, std::vector<std::pair<std::string, HostMaterial>>& out, std::string& err) {
+bool parse_mtl(SceneBuilder& sb, const char* data, size_t n, std::vector<std::pair<std::string, HostMaterial>>& out,
+               std::string& err) {
     Lines lines{data, data + n};
     std::string line;
     std::vector<std::string> tok;
@@ -177,6 +177,23 @@ bool parse_mtl(const char* data, size_t n, std::vector<std::pair<std::string, Ho
         lumo_spectrum kd{}, ks{}, ke{}, tf{};
         double eta = 1.5, k = 0.0, roughness = 1.0;
         bool fresnel = false, transparent = false;
+        int map_kd = -1, map_ks = -1, map_ke = -1, map_bump = -1;  // texture / bump map indices
+        auto file_of = [&](const std::vector<std::string>& t) -> const std::vector<uint8_t>* {
+            std::string nm;  // tokens[1..].join(" ")
+            for (size_t i = 1; i < t.size(); ++i) nm += (i > 1 ? " " : "") + t[i];
+            const std::vector<uint8_t>* f = sb.find_file(nm);
+            if (!f) err = "material " + name + ": no file " + nm + " for " + t[0] + " (lumo_builder_add_file)";
+            return f;
+        };
+        auto image = [&](const std::vector<std::string>& t, int& dst) -> bool {
+            const std::vector<uint8_t>* f = file_of(t);
+            if (!f) return false;
+            HostTexture tex;
+            if (!texture_from_png(f->data(), f->size(), tex, err)) return false;
+            sb.textures.push_back(std::move(tex));
+            dst = (int)sb.textures.size() - 1;
+            return true;
+        };
         double x[3];
         for (const auto& t : block) {
             const std::string& c = t[0];
@@ -200,17 +217,41 @@ bool parse_mtl(const char* data, size_t n, std::vector<std::pair<std::string, Ho
                 if (illum == 5) fresnel = true;
                 if (illum == 6) transparent = true;
                 if (illum == 7) fresnel = transparent = true;
-            } else if (c == "map_Kd" || c == "map_Ke" || c == "map_Ks" || c == "map_Bump") {
-                err = "material " + name + ": image textures (" + c + ") are not supported";
-                return false;
+            } else if (c == "map_Kd") {
+                if (!image(t, map_kd)) return false;
+            } else if (c == "map_Ke") {
+                if (!image(t, map_ke)) return false;
+            } else if (c == "map_Ks") {
+                if (sb.map_ks) {
+                    if (!image(t, map_ks)) return false;
+                } else {  // occlusion / roughness / metalness image: its means (mtl/task.rs:60-68)
+                    const std::vector<uint8_t>* f = file_of(t);
+                    double orm[3];
+                    if (!f || !png_mean_vec3(f->data(), f->size(), orm, err)) return false;
+                    roughness = orm[1];
+                    k = orm[2];
+                    ks = spectrum_from_rgb(1.0, 1.0, 1.0);
+                }
+            } else if (c == "map_Bump") {
+                const std::vector<uint8_t>* f = file_of(t);
+                if (!f) return false;
+                HostNormalMap nm;
+                if (!normal_map_from_png(f->data(), f->size(), nm, err)) return false;
+                sb.normal_maps.push_back(std::move(nm));
+                map_bump = (int)sb.normal_maps.size() - 1;
             }
         }
         HostMaterial m;
-        if (ke.scale != 0.0f) {  // !Ke.is_black(): Material::light(Texture::from(Ke)), D65
+        if (ke.scale != 0.0f || map_ke >= 0) {  // MtlConfig::build_material (mtl.rs:60-90): a light, D65
             m = material_light(ke, DENSE_D65, 1.0, false);
+            m.m.albedo_tex = map_ke;
         } else if (!material_microfacet(roughness, eta, k, transparent, fresnel, kd, ks, tf, m)) {
             err = "material " + name + ": roughness outside [0, 1]";
             return false;
+        } else {
+            m.m.albedo_tex = map_kd;
+            m.m.ks_tex = map_ks;
+            m.m.normal_map = map_bump;
         }
         out.emplace_back(name, m);
         block.clear();
@@ -271,7 +312,7 @@ bool load_obj_mesh(SceneBuilder& sb, const char* data, size_t n, int material, s
 bool load_obj_scene(SceneBuilder& sb, const char* obj, size_t n_obj, const char* mtl, size_t n_mtl,
                     std::string& err) {
     std::vector<std::pair<std::string, HostMaterial>> mats;
-    if (mtl && !parse_mtl(mtl, n_mtl, mats, err)) return false;
+    if (mtl && !parse_mtl(sb, mtl, n_mtl, mats, err)) return false;
     std::unordered_map<std::string, int> index;
     for (auto& m : mats)
         if (!index.count(m.first)) index[m.first] = sb.add_material(m.second);  // first definition wins

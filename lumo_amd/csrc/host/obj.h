@@ -23,7 +23,8 @@ struct ObjData {
 bool parse_obj(const char* data, size_t n, const std::unordered_map<std::string, int>* material_index, ObjData& out,
                std::string& err);
 // parser/mtl.rs + mtl/task.rs: newmtl blocks -> materials (MtlConfig::build_material)
-bool parse_mtl(const char* data, size_t n, std::vector<std::pair<std::string, HostMaterial>>& out, std::string& err);
+bool parse_mtl(SceneBuilder& sb, const char* data, size_t n, std::vector<std::pair<std::string, HostMaterial>>& out,
+               std::string& err);
 // parser.rs mesh_from_path: the whole file as one mesh with `material`
 bool load_obj_mesh(SceneBuilder& sb, const char* data, size_t n, int material, std::string& err);
 // parser.rs scene_from_file: per usemtl group one mesh; emissive groups become Triangle lights

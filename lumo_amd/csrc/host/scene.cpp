@@ -3,6 +3,7 @@
 #include "../common/lmath.h"
 
 #include <algorithm>
+#include <cctype>
 #include <cstring>
 #include <deque>
 #include <limits>
@@ -781,7 +782,37 @@ lumo_scene_desc FlatScene::desc() const {
     d.dense_spectra = dense.data();
     d.num_transforms = (int32_t)transforms.size();
     d.transforms = transforms.data();
+    d.num_textures = (int32_t)textures.size();
+    d.num_texels = (int32_t)texels.size();
+    d.textures = textures.data();
+    d.texels = texels.data();
+    d.num_normal_maps = (int32_t)normal_maps.size();
+    d.num_normal_texels = (int32_t)(normal_texels.size() / 3);
+    d.normal_maps = normal_maps.data();
+    d.normal_texels = normal_texels.data();
+    d.num_perlin = (int32_t)perlin.size();
+    d.perlin = perlin.data();
     return d;
+}
+
+const std::vector<uint8_t>* SceneBuilder::find_file(const std::string& name) const {
+    std::string n = name;
+    for (char& ch : n) {
+        if (ch == '\\') ch = '/';  // parser/mtl/task.rs: .replace('\\', "/")
+        ch = (char)std::tolower((unsigned char)ch);
+    }
+    // parser.rs:88-114 _extract_zip: the one archive member whose lower-cased name ends with the
+    // lower-cased request (none or several: an error)
+    const std::vector<uint8_t>* hit = nullptr;
+    for (const auto& f : files) {
+        std::string m = f.first;
+        for (char& ch : m) ch = (char)std::tolower((unsigned char)ch);
+        if (m.size() >= n.size() && m.compare(m.size() - n.size(), n.size(), n) == 0) {
+            if (hit) return nullptr;
+            hit = &f.second;
+        }
+    }
+    return hit;
 }
 
 namespace {
@@ -844,6 +875,30 @@ std::unique_ptr<FlatScene> build_scene(const SceneBuilder& sb) {
         }
         fs->materials.push_back(m);
     }
+    // textures: image texels appended in texture order; bump maps likewise (texture.rs, image.rs)
+    for (const HostTexture& ht : sb.textures) {
+        lumo_texture t = ht.t;
+        if (t.kind == LUMO_TEX_IMAGE) {
+            t.first = (int32_t)fs->texels.size();
+            fs->texels.insert(fs->texels.end(), ht.texels.begin(), ht.texels.end());
+        }
+        fs->textures.push_back(t);
+    }
+    for (const HostNormalMap& nm : sb.normal_maps) {
+        lumo_normal_map m{};
+        m.width = nm.width;
+        m.height = nm.height;
+        m.first = (int32_t)(fs->normal_texels.size() / 3);
+        fs->normal_texels.insert(fs->normal_texels.end(), nm.n.begin(), nm.n.end());
+        fs->normal_maps.push_back(m);
+    }
+    fs->perlin = sb.perlins;
+    auto tex_ok = [&](int t) { return t >= -1 && t < (int)sb.textures.size(); };
+    for (const lumo_material& m : fs->materials)
+        if (!tex_ok(m.albedo_tex) || !tex_ok(m.ks_tex) || !tex_ok(m.tf_tex) || m.normal_map < -1 ||
+            m.normal_map >= (int)sb.normal_maps.size())
+            throw std::runtime_error("material references a texture that does not exist");
+    if (!tex_ok(sb.env_texture)) throw std::runtime_error("environment texture does not exist");
 
     auto flatten_objects = [&](const std::vector<HostObject>& src, std::vector<lumo_object>& dst,
                                std::vector<V3>& bmins, std::vector<V3>& bmaxs) {
@@ -978,6 +1033,7 @@ std::unique_ptr<FlatScene> build_scene(const SceneBuilder& sb) {
         env_lights.push_back(env);
         light_src = &env_lights;
         HostMaterial em = material_light(sb.env_tex, DENSE_D65, sb.env_scale, true);
+        em.m.albedo_tex = sb.env_texture;
         fs->materials.push_back(em.m);
         extra_mats.push_back(em);
     }
@@ -1015,7 +1071,15 @@ std::unique_ptr<FlatScene> build_scene(const SceneBuilder& sb) {
             // Material::power: s * t.power(lambda) * e.sample(lambda), x2 if two-sided
             double phi = 0.0;
             if (hm.m.kind == LUMO_MAT_LIGHT) {
-                phi = hm.m.scale * spec_sample_one(hm.m.albedo, lambda[k]);
+                // Texture::power (texture.rs:95-101): the solid spectrum or an image's mean
+                lumo_spectrum tp = hm.m.albedo;
+                if (hm.m.albedo_tex >= 0) {
+                    const lumo_texture& t = sb.textures[hm.m.albedo_tex].t;
+                    if (t.kind != LUMO_TEX_SOLID && t.kind != LUMO_TEX_IMAGE)
+                        throw std::runtime_error("light texture without a power (texture.rs:99: unimplemented)");
+                    tp = t.spec;
+                }
+                phi = hm.m.scale * spec_sample_one(tp, lambda[k]);
                 phi = phi * dense_sample_one(builtin_dense(hm.m.illuminant), lambda[k]);
                 if (hm.m.two_sided) phi = 2.0 * phi;
             }

@@ -12,11 +12,13 @@
 
 #include "../../../include/lumo_amd.h"
 #include "color.h"
+#include "texture.h"
 
 namespace lumo {
 
 struct HostMaterial {
     lumo_material m{};
+    HostMaterial() { m.albedo_tex = m.ks_tex = m.tf_tex = m.normal_map = -1; }
     const Dense* illum = nullptr;  // light illuminant (dense)
     Dense illum_owned;
     bool has_owned = false;
@@ -110,7 +112,16 @@ class SceneBuilder {
     // Light sphere enclosing the scene bounds is added as the last light (scene.rs:33-52).
     bool has_env = false;
     lumo_spectrum env_tex{};
+    int env_texture = -1;  // a texture of this builder (e.g. an HDR image), else the solid env_tex
     double env_scale = 0.0;
+    // textures (texture.rs), bump maps (image.rs:131-166), Perlin lattices (perlin.rs)
+    std::vector<HostTexture> textures;
+    std::vector<HostNormalMap> normal_maps;
+    std::vector<lumo_perlin> perlins;
+    // named files for the MTL map_* statements (parser.rs _img_from_zip) and the map_ks flag
+    std::vector<std::pair<std::string, std::vector<uint8_t>>> files;
+    bool map_ks = false;
+    const std::vector<uint8_t>* find_file(const std::string& name) const;
 
     // Scene::cornell_box (scene/cornell_box.rs:8-193)
     static SceneBuilder cornell_box();
@@ -133,6 +144,11 @@ struct FlatScene {
     std::vector<lumo_material> materials;
     std::vector<double> dense;
     std::vector<lumo_transform> transforms;
+    std::vector<lumo_texture> textures;
+    std::vector<lumo_spectrum> texels;
+    std::vector<lumo_normal_map> normal_maps;
+    std::vector<double> normal_texels;
+    std::vector<lumo_perlin> perlin;
     lumo_scene_desc desc() const;
 };
 

@@ -186,6 +186,104 @@ V3 color_xyz(const Scene& sc, const Color& c, const Lambda& L) {  // color.rs:97
            Y_INTEGRAL;
 }
 
+// ------------------------------------------------------------------ textures (texture.rs, image.rs, perlin.rs)
+uint32_t as_u32(double x) {  // Rust `as u32`: saturating, NaN -> 0
+    if (!(x > 0.0)) return 0;
+    return x >= 4294967295.0 ? 4294967295u : (uint32_t)x;
+}
+uint64_t as_u64(double x) {
+    if (!(x > 0.0)) return 0;
+    return x >= 18446744073709551615.0 ? UINT64_MAX : (uint64_t)x;
+}
+// image.rs:99-128 bilin_interp: the four texels around uv and the lerp weights (x0y0)
+struct Corners {
+    size_t xy00, xy10, xy01, xy11;
+    double x0, y0;
+};
+Corners bilin_interp(uint32_t width, uint32_t height, V2 uv) {
+    const double w = width, h = height;
+    const double x = uv.x * w, y = (1.0 - uv.y) * h;
+    const double xo_f = std::floor(x - 0.5), yo_f = std::floor(y - 0.5);
+    const double x1 = x - xo_f - 0.5, y1 = y - yo_f - 0.5;
+    const uint32_t xo = as_u32(xo_f + w) % width;
+    const uint32_t yo = as_u32(yo_f + h) % height;
+    const uint32_t xi = (xo + 1) % width;
+    const uint32_t yi = (yo + 1) % height;
+    return Corners{xo + yo * width, xi + yo * width, xo + yi * width, xi + yi * width, 1.0 - x1, 1.0 - y1};
+}
+// perlin.rs:50-107
+double perlin_noise_at(const lumo_perlin& pn, V3 p) {
+    auto fract = [](double v) { return v - std::trunc(v); };
+    auto smoother = [](double x) { return ((6.0 * x - 15.0) * x + 10.0) * x * x * x; };
+    const V3 w{smoother(fract(p.x)), smoother(fract(p.y)), smoother(fract(p.z))};
+    const size_t fx = as_u64(std::floor(p.x)), fy = as_u64(std::floor(p.y)), fz = as_u64(std::floor(p.z));
+    double acc = 0.0;
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j)
+            for (int k = 0; k < 2; ++k) {
+                const int hash = pn.perm[0][(fx + i) % 256] ^ pn.perm[1][(fy + j) % 256] ^ pn.perm[2][(fz + k) % 256];
+                const V3 norm{pn.lattice[hash][0], pn.lattice[hash][1], pn.lattice[hash][2]};
+                const V3 idx{(double)i, (double)j, (double)k};
+                const V3 widx = 2.0 * w * idx + V3{1.0, 1.0, 1.0} - w - idx;
+                acc = acc + widx.x * widx.y * widx.z * dot(norm, w - idx);
+            }
+    return acc;
+}
+double turbulence(const lumo_perlin& pn, double acc, V3 p, int depth) {  // texture.rs:105-112
+    if (depth >= 6) return acc;
+    double w = 1.0;  // 0.5.powi(depth)
+    for (int i = 0; i < depth; ++i) w *= 0.5;
+    return turbulence(pn, acc + w * fabs(perlin_noise_at(pn, p)), 2.0 * p, depth + 1);
+}
+// Texture::albedo_at (texture.rs:53-92); tex == -1 is the material's solid spectrum
+Color albedo_at(const Scene& sc, int tex, const lumo_spectrum& solid, const Lambda& L, V2 uv) {
+    if (tex < 0) return spec_sample(solid, L);
+    const lumo_texture& t = sc.d->textures[tex];
+    switch (t.kind) {
+        case LUMO_TEX_SOLID: return spec_sample(t.spec, L);
+        case LUMO_TEX_MARBLE: {
+            const V3 uvw{uv.x, uv.y, 0.0};
+            const double turb = turbulence(sc.d->perlin[t.first], 0.0, 4.0 * vabs(uvw), 0);
+            const double b = 0.5 + 0.5 * O_SIN(60.0 * uvw.x + 20.0 * turb);
+            const double b2 = b * b;
+            const double scaled = 1.0 - b2 * (b2 * b2);  // powi(6) as LLVM expands it
+            return spec_sample(t.spec, L) * scaled;
+        }
+        case LUMO_TEX_CHECKERBOARD: {
+            const V2 uvs{uv.x * t.scale, uv.y * t.scale};
+            const bool even = as_u64(std::floor(uvs.x) + std::floor(uvs.y)) % 2 == 0;
+            return albedo_at(sc, even ? t.first : t.second, solid, L, uv);
+        }
+        case LUMO_TEX_IMAGE: {  // image.rs:175-184
+            const Corners c = bilin_interp((uint32_t)t.width, (uint32_t)t.height, uv);
+            const lumo_spectrum* px = sc.d->texels + t.first;
+            const Color y0 = spec_sample(px[c.xy00], L) * c.x0 + spec_sample(px[c.xy10], L) * (1.0 - c.x0);
+            const Color y1 = spec_sample(px[c.xy01], L) * c.x0 + spec_sample(px[c.xy11], L) * (1.0 - c.x0);
+            return y0 * c.y0 + y1 * (1.0 - c.y0);
+        }
+        default: {  // Mandelbrot: c = 2 (uv - (0.75, 0.5)), z <- z^2 + c, 256 steps, |z| < 64
+            const double cre = 2.0 * (uv.x - 0.75), cim = 2.0 * (uv.y - 0.5);
+            double re = 0.0, im = 0.0;
+            size_t depth = 0;
+            while (depth < 256 && re * re + im * im < 64.0 * 64.0) {
+                const double nre = re * re - im * im, nim = re * im + im * re;
+                re = nre + cre;
+                im = nim + cim;
+                depth += 1;
+            }
+            return cconst(depth == 256 ? 1.0 : 0.0);
+        }
+    }
+}
+// Image<Normal>::value_at (image.rs:131-140)
+V3 normal_at(const Scene& sc, const lumo_normal_map& nm, V2 uv) {
+    const Corners c = bilin_interp((uint32_t)nm.width, (uint32_t)nm.height, uv);
+    const double* px = sc.d->normal_texels + 3 * (size_t)nm.first;
+    auto n = [&](size_t i) { return V3{px[3 * i], px[3 * i + 1], px[3 * i + 2]}; };
+    auto lerp = [](V3 a, V3 b, double v) { return normalize(a * v + b * (1.0 - v)); };
+    return lerp(lerp(n(c.xy00), n(c.xy10), c.x0), lerp(n(c.xy01), n(c.xy11), c.x0), c.y0);
+}
+
 struct Ray {
     V3 origin, dir;
 };
@@ -685,12 +783,17 @@ struct Mfd {
     const double* eta;
     const double* k;
     bool constant_eta;
-    lumo_spectrum kd, ks, tf;
+    const Scene* sc;
+    const lumo_material* m;
+    V2 uv;  // the hit's uv at which kd / ks / tf are evaluated (microfacet.rs:118-134)
 };
-Mfd mfd_of(const Scene& sc, const lumo_material& m) {
+Mfd mfd_of(const Scene& sc, const lumo_material& m, V2 uv = V2{0.0, 0.0}) {
     return Mfd{m.roughness, m.roughness, sc.dense(m.eta_idx), sc.dense(m.k_idx), (m.flags & LUMO_MATF_CONSTANT_ETA) != 0,
-               m.albedo, m.ks, m.tf};
+               &sc, &m, uv};
 }
+Color mfd_kd(const Mfd& d, const Lambda& L) { return albedo_at(*d.sc, d.m->albedo_tex, d.m->albedo, L, d.uv); }
+Color mfd_ks(const Mfd& d, const Lambda& L) { return albedo_at(*d.sc, d.m->ks_tex, d.m->ks, L, d.uv); }
+Color mfd_tf(const Mfd& d, const Lambda& L) { return albedo_at(*d.sc, d.m->tf_tex, d.m->tf, L, d.uv); }
 bool mfd_is_specular(const Mfd& d) { return (d.rx + d.ry) / 2.0 < 0.01; }   // microfacet.rs:73-77
 bool mfd_is_delta(const Mfd& d) { return (d.rx + d.ry) / 2.0 < 1e-3; }      // :80-84
 double eta_at(const Mfd& d, double wl) { return dense_one(d.eta, wl); }
@@ -832,12 +935,11 @@ double lambertian_pdf(V3 wo, V3 wi) {  // scatter.rs:14-26
     const double c = wi.z;
     return c > 0.0 ? c / PI : 0.0;
 }
-Color spec_c(const lumo_spectrum& s, const Lambda& L) { return spec_sample(s, L); }
 const Color WHITE_C = Color{{1.0, 1.0, 1.0, 1.0}};
 
 // conductor (:66-118)
 Color conductor_f(const Mfd& d, V3 wo, V3 wi, const Lambda& L) {
-    const Color ks = spec_c(d.ks, L);
+    const Color ks = mfd_ks(d, L);
     if (mfd_is_delta(d)) return ks * f_fresnel(d, wo, V3{0.0, 0.0, 1.0}, L) / fabs(wi.z);
     return ks * reflect_coeff(d, wo, wi, L);
 }
@@ -864,8 +966,8 @@ Color diffuse_f(const Mfd& d, V3 wo, V3 wi, const Lambda& L) {
     const double G = mf_g(d, wo, wi, wh);
     const Color fr = D * F * G / (4.0 * fabs(cwo) * fabs(cwi));
     const double fd = disney_diffuse(d, cwo, cwi, cwh);
-    const Color ks = spec_c(d.ks, L);
-    const Color kd = spec_c(d.kd, L);
+    const Color ks = mfd_ks(d, L);
+    const Color kd = mfd_kd(d, L);
     return fr * ks + kd * (WHITE_C - F) * fd / PI;
 }
 bool diffuse_sample(const Mfd& d, V3 wo, double rand_u, V2 sq, V3* wi) {
@@ -898,14 +1000,14 @@ Color dielectric_f(const Mfd& d, V3 wo, V3 wi, const Lambda& L, bool reflection,
     const bool flat = eta == 1.0 || mfd_is_delta(d);
     V3 wh = flat ? V3{0.0, 0.0, 1.0} : normalize(wi * eta_ratio + wo);
     if (reflection) {
-        const Color ks = spec_c(d.ks, L);
+        const Color ks = mfd_ks(d, L);
         if (flat) return ks * f_fresnel(d, wo, wh, L) / fabs(cwi);
         return ks * reflect_coeff(d, wo, wi, L);
     }
     const Color F = f_fresnel(d, wo, wh, L);
     if (wh.z < 0.0) wh = -wh;
     const double scale = importance ? 1.0 : eta_ratio * eta_ratio;  // Transport::Importance / Radiance
-    const Color tf = spec_c(d.tf, L);
+    const Color tf = mfd_tf(d, L);
     if (flat) return tf * (WHITE_C - F) / (scale * fabs(cwi));
     const double D = mf_d(d, wh);
     const double G = mf_g(d, wo, wi, wh);
@@ -953,12 +1055,17 @@ bool is_standard(int kind) {
            kind == LUMO_MAT_MF_DIELECTRIC;
 }
 bool is_reflection_bxdf(int kind) { return kind != LUMO_MAT_MF_DIELECTRIC; }  // bxdf.rs:46-54
+// Material::map_normal (material.rs:323-331)
+V3 map_normal(const Scene& sc, const lumo_material& m, const Hit& h) {
+    if (m.normal_map < 0) return h.ns;
+    return normalize(onb_to_world(onb_new(h.ns), normal_at(sc, sc.d->normal_maps[m.normal_map], h.uv)));
+}
 
 // material.rs:273-289 -> bsdf.rs:51-67 -> bxdf.rs:104-124
 bool bsdf_sample(const Scene& sc, const Hit& h, V3 wo, Lambda& L, double rand_u, V2 rand_sq, V3* wi) {
     const lumo_material& m = mat(sc, h.material);
     if (!is_standard(m.kind)) return false;  // Light / Blank -> None
-    const Onb uvw = onb_new(h.ns);
+    const Onb uvw = onb_new(map_normal(sc, m, h));
     const V3 wol = onb_to_local(uvw, wo);
     if (h.backface && is_reflection_bxdf(m.kind)) return false;
     V3 w;
@@ -968,9 +1075,9 @@ bool bsdf_sample(const Scene& sc, const Hit& h, V3 wo, Lambda& L, double rand_u,
             w = square_to_cos_hemisphere(rand_sq);
             ok = true;
             break;
-        case LUMO_MAT_MF_DIFFUSE: ok = diffuse_sample(mfd_of(sc, m), wol, rand_u, rand_sq, &w); break;
-        case LUMO_MAT_MF_CONDUCTOR: ok = conductor_sample(mfd_of(sc, m), wol, rand_sq, &w); break;
-        default: ok = dielectric_sample(mfd_of(sc, m), wol, L, rand_u, rand_sq, &w); break;
+        case LUMO_MAT_MF_DIFFUSE: ok = diffuse_sample(mfd_of(sc, m, h.uv), wol, rand_u, rand_sq, &w); break;
+        case LUMO_MAT_MF_CONDUCTOR: ok = conductor_sample(mfd_of(sc, m, h.uv), wol, rand_sq, &w); break;
+        default: ok = dielectric_sample(mfd_of(sc, m, h.uv), wol, L, rand_u, rand_sq, &w); break;
     }
     if (!ok) return false;
     *wi = onb_to_world(uvw, w);
@@ -981,14 +1088,14 @@ double bsdf_pdf(const Scene& sc, const Hit& h, V3 wo, V3 wi, const Lambda& L) {
     const lumo_material& m = mat(sc, h.material);
     if (!is_standard(m.kind)) return 0.0;
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
-    const Onb uvw = onb_new(h.ns);
+    const Onb uvw = onb_new(map_normal(sc, m, h));
     const V3 wol = onb_to_local(uvw, wo), wil = onb_to_local(uvw, wi);
     if (!reflection && is_reflection_bxdf(m.kind)) return 0.0;
     switch (m.kind) {
         case LUMO_MAT_LAMBERTIAN: return lambertian_pdf(wol, wil);
-        case LUMO_MAT_MF_DIFFUSE: return diffuse_pdf(mfd_of(sc, m), wol, wil);
-        case LUMO_MAT_MF_CONDUCTOR: return conductor_pdf(mfd_of(sc, m), wol, wil);
-        default: return dielectric_pdf(mfd_of(sc, m), wol, wil, reflection, L);
+        case LUMO_MAT_MF_DIFFUSE: return diffuse_pdf(mfd_of(sc, m, h.uv), wol, wil);
+        case LUMO_MAT_MF_CONDUCTOR: return conductor_pdf(mfd_of(sc, m, h.uv), wol, wil);
+        default: return dielectric_pdf(mfd_of(sc, m, h.uv), wol, wil, reflection, L);
     }
 }
 // material.rs:254-270 -> bsdf.rs:28-48 -> bxdf.rs:71-100
@@ -996,14 +1103,14 @@ Color bsdf_f(const Scene& sc, const Hit& h, V3 wo, V3 wi, const Lambda& L, bool 
     const lumo_material& m = mat(sc, h.material);
     if (!is_standard(m.kind)) return cconst(0.0);
     const bool reflection = dot(h.ng, wi) * dot(h.ng, wo) >= 0.0;
-    const Onb uvw = onb_new(h.ns);
+    const Onb uvw = onb_new(map_normal(sc, m, h));
     const V3 wol = onb_to_local(uvw, wo), wil = onb_to_local(uvw, wi);
     if ((!reflection || h.backface) && is_reflection_bxdf(m.kind)) return cconst(0.0);
     switch (m.kind) {
         case LUMO_MAT_LAMBERTIAN: return spec_sample(m.albedo, L) / PI;
-        case LUMO_MAT_MF_DIFFUSE: return diffuse_f(mfd_of(sc, m), wol, wil, L);
-        case LUMO_MAT_MF_CONDUCTOR: return conductor_f(mfd_of(sc, m), wol, wil, L);
-        default: return dielectric_f(mfd_of(sc, m), wol, wil, L, reflection, importance);
+        case LUMO_MAT_MF_DIFFUSE: return diffuse_f(mfd_of(sc, m, h.uv), wol, wil, L);
+        case LUMO_MAT_MF_CONDUCTOR: return conductor_f(mfd_of(sc, m, h.uv), wol, wil, L);
+        default: return dielectric_f(mfd_of(sc, m, h.uv), wol, wil, L, reflection, importance);
     }
 }
 double shading_cosine(const Scene& sc, int material, V3 wi, V3 ns) {  // material.rs:315-320
@@ -1029,7 +1136,7 @@ Color emit(const Scene& sc, int material, const Lambda& L, const Hit& h) {
     const lumo_material& m = mat(sc, material);
     if (m.kind != LUMO_MAT_LIGHT) return cconst(0.0);
     if (!m.two_sided && h.backface) return cconst(0.0);
-    return m.scale * spec_sample(m.albedo, L) * dense_sample(sc.dense(m.illuminant), L);
+    return m.scale * albedo_at(sc, m.albedo_tex, m.albedo, L, h.uv) * dense_sample(sc.dense(m.illuminant), L);
 }
 
 // lights (bvh.rs:51-86, rectangle.rs:113-134, object.rs:138-156)

@@ -126,11 +126,12 @@ def _tmp_obj(data):
     return f.name
 
 
-def test_texture_maps_rejected():
+def test_texture_map_missing_file():
+    """parser.rs:_extract_zip: a map_Kd naming a file the archive lacks is an error."""
     mtl = b"newmtl t\nKd 1 1 1\nmap_Kd wall.png\n"
     import tempfile
     with tempfile.TemporaryDirectory() as d:
         open(d + "/a.obj", "wb").write(b"v 0 0 0\nv 1 0 0\nv 0 1 0\nusemtl t\nf 1 2 3\n")
         open(d + "/a.mtl", "wb").write(mtl)
-        with pytest.raises(ValueError, match="texture"):
+        with pytest.raises(ValueError, match="wall.png"):
             L.Scene.from_file(d + "/a.obj", mtllib=d + "/a.mtl")
