@@ -428,8 +428,10 @@ class Scene:
                 name = tok[1]
                 if str(path).lower().endswith(".zip"):
                     mtls.append(_read_source((path, name), ".mtl"))
-                else:
-                    mtls.append(_read_source(os.path.join(os.path.dirname(os.path.abspath(path)), name), ".mtl"))
+                else:  # plain files (not a lumo mode): follow the statement when the file is there
+                    f = os.path.join(os.path.dirname(os.path.abspath(path)), name)
+                    if os.path.exists(f):
+                        mtls.append(_read_source(f, ".mtl"))
         mtl = b"\n".join(mtls) if mtls else None
         check(L.lumo_builder_set_map_ks(s._b, int(bool(map_ks))), "map_ks")
         st = L.lumo_builder_load_obj_scene(s._b, obj, len(obj), mtl, len(mtl) if mtl else 0)

@@ -242,7 +242,7 @@ __device__ DHit light_sample_on_hit(const DScene& sc, const lumo_object& L, V2 r
 __device__ __forceinline__ double sa_to_area(double pdf, V3 xo, V3 xi, V3 wi, V3 ngi) {
     return pdf * fabs(dot(wi, ngi)) / distance_squared(xo, xi);
 }
-template <bool FX>
+template <int FX>
 __device__ __forceinline__ bool v_is_delta(const DScene& sc, const BVtx& v, const double* L) {
     return !v.blank && mat_is_delta<FX>(sc, sc.mats[v.mat], L);
 }
@@ -253,19 +253,19 @@ __device__ double v_shading_correction(const DScene& sc, const BVtx& v, V3 wi) {
     return v_shading_cosine(sc, v, wi, v.ng) * v_shading_cosine(sc, v, v.wo, v.ns) /
            (v_shading_cosine(sc, v, v.wo, v.ng) * v_shading_cosine(sc, v, wi, v.ns));
 }
-template <bool FX>
+template <int FX>
 __device__ DColor v_f(const DScene& sc, const BVtx& v, V3 next_p, const double* L, int mode) {
     if (v.blank) return cfill(0.0);
     const V3 wi = normalize(next_p - v.p);
     return bsdf_f<FX>(sc, sc.mats[v.mat], vtx_hit(v), v.wo, wi, L, mode == TR_IMPORTANCE);
 }
-template <bool FX>
+template <int FX>
 __device__ double v_bsdf_pdf(const DScene& sc, const BVtx& v, V3 wi, const double* L, bool swap) {
     if (v.blank) return 0.0;
     const lumo_material m = sc.mats[v.mat];
     return swap ? bsdf_pdf<FX>(sc, m, vtx_hit(v), wi, v.wo, L) : bsdf_pdf<FX>(sc, m, vtx_hit(v), v.wo, wi, L);
 }
-template <bool FX>
+template <int FX>
 __device__ double v_pdf_prev(const DScene& sc, const BVtx& v, const BVtx& prev, V3 wi, const double* L) {  // vertex.rs:119-134
     if (v_is_delta<FX>(sc, v, L) || v_is_delta<FX>(sc, prev, L)) return 0.0;
     const double pdf_sa = v_bsdf_pdf<FX>(sc, v, wi, L, true);
@@ -308,7 +308,7 @@ __device__ __forceinline__ BVtx vtx_of_hit(const DHit& h, DColor gathered, doubl
 }
 
 // BVH::get_light_at (bvh.rs:97-102): the light hit along -ng from just outside the hit
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ int get_light_at(const DScene& sc, const BVtx& v, Counters& C) {
     const Ray ri = ray_new(ray_origin(vtx_hit(v), true), -v.ng);
     return bvh_traverse<true, STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, rayx(ri), 0.0, DINF, C);
@@ -316,7 +316,7 @@ __device__ int get_light_at(const DScene& sc, const BVtx& v, Counters& C) {
 
 // path_gen.rs:52-157.  Returns the number of vertices stored (root included), or -1 when the
 // subpath does not fit the store.
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ int bdpt_walk(const DScene& sc, const VStore& st, int slot, Ray ro, Xorshift& rng, double* L, double delta,
                          const BVtx& root, DColor gathered, double pdf_dir, int mode, Counters& C, uint32_t& queries) {
     int depth = 0;
@@ -387,7 +387,7 @@ struct PView {
     __device__ __forceinline__ MisE plain(const DScene& sc, int i, const double* L, bool light_side) const;
 };
 
-template <bool FX>
+template <int FX>
 __device__ MisE mis_plain(const DScene& sc, const PView& pv, int i, const double* L, bool light_side) {
     if (pv.one) {
         const BVtx& v = *pv.one;
@@ -400,7 +400,7 @@ __device__ MisE mis_plain(const DScene& sc, const PView& pv, int i, const double
     return light_side ? MisE{bck, fwd, del} : MisE{fwd, bck, del};
 }
 
-template <bool FX>
+template <int FX>
 __device__ double pdf_light_leaving(const DScene& sc, const BVtx& curr, const BVtx& next, const double* L) {
     if (v_is_delta<FX>(sc, next, L)) return 0.0;
     if (curr.light < 0) return 0.0;
@@ -411,7 +411,7 @@ __device__ double pdf_light_leaving(const DScene& sc, const BVtx& curr, const BV
     const V3 ngi = next.blank ? wi : next.ng;
     return sa_to_area(pdf_dir, xo, xi, wi, ngi);
 }
-template <bool FX>
+template <int FX>
 __device__ double pdf_camera_leaving(const DCam& cam, const DScene& sc, const BVtx& curr, const BVtx& next,
                                      const double* L) {
     if (v_is_delta<FX>(sc, next, L)) return 0.0;
@@ -425,7 +425,7 @@ __device__ __forceinline__ double pdf_light_origin(const DScene& sc, const BVtx&
     if (v.light < 0) return 0.0;
     return sc.alias_pdf[v.light] / light_area(sc, sc.lights[v.light]);
 }
-template <bool FX>
+template <int FX>
 __device__ double pdf_connection(const DScene& sc, const BVtx& curr, const BVtx& next, const double* L,
                                  const BVtx* prev) {
     if (v_is_delta<FX>(sc, next, L)) return 0.0;
@@ -444,7 +444,7 @@ __device__ double pdf_connection(const DScene& sc, const BVtx& curr, const BVtx&
     return sa_to_area(pdf_sa, xo, xi, wi, ngi);
 }
 
-template <bool FX>
+template <int FX>
 __device__ double mis_weight(const DScene& sc, const DCam& cam, const double* L, const PView& lp, int s, const PView& cp,
                              int t) {
     if (s + t == 2) return 1.0;
@@ -504,7 +504,7 @@ __device__ double mis_weight(const DScene& sc, const DCam& cam, const double* L,
 }
 
 // bd_path_trace.rs:279-290: visible() tests with Scene::hit_t (any-hit first, objects then lights)
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ bool bdpt_visible(const DScene& sc, const BVtx& a, const BVtx& b, Counters& C) {
     const V3 xo = a.p, xi = b.p;
     const Ray ri = spawn(vtx_hit(a), xi - xo);
@@ -519,7 +519,7 @@ __device__ bool bdpt_visible(const DScene& sc, const BVtx& a, const BVtx& b, Cou
 // bd_path_trace.rs:77-145 (t = 1): returns true with the splat.  `rs` is the lens sample the
 // reference draws here (only for a non-delta ll; the caller draws it).  `trace(rx)` is
 // Scene::hit of the camera ray: done inline, or looked up from k_bdpt_trace_a.
-template <bool FX, typename Trace>
+template <int FX, typename Trace>
 __device__ bool connect_light_path(const DScene& sc, const DCam& cam, V2 rs, const double* L, const PView& lp,
                                    int s, const BVtx& ll, V2* raster_out, DColor* color_out, uint32_t& queries,
                                    Trace&& trace) {
@@ -553,11 +553,11 @@ __device__ bool connect_light_path(const DScene& sc, const DCam& cam, V2 rs, con
     *color_out = color;
     return true;
 }
-template <bool FX>
+template <int FX>
 __device__ DColor add_camera_path(const DScene& sc, const DCam& cam, const double* L, const PView& cp, int t) {
     const BVtx ct = cp.get(t - 1);
     if (ct.light < 0) return cfill(0.0);
-    const DColor rad = ct.gath * emit(sc, sc.mats[ct.mat], L, ct.backface, ct.uv);
+    const DColor rad = ct.gath * emit<FX>(sc, sc.mats[ct.mat], L, ct.backface, ct.uv);
     if (rad.s[0] == 0.0 && rad.s[1] == 0.0 && rad.s[2] == 0.0 && rad.s[3] == 0.0) return cfill(0.0);
     const PView none{nullptr, 0, nullptr};
     return rad * mis_weight<FX>(sc, cam, L, none, 0, cp, t);
@@ -565,7 +565,7 @@ __device__ DColor add_camera_path(const DScene& sc, const DCam& cam, const doubl
 // bd_path_trace.rs:147-210 (s = 1).  `u`, `rs`: the light pick and light sample the reference
 // draws here (only when cl is neither delta nor on a light; the caller draws them).
 // `vis(rx, li)` is Scene::hit_light: the light triangle hit, or -1 when occluded / missed.
-template <bool FX, typename Vis>
+template <int FX, typename Vis>
 __device__ DColor connect_camera_path(const DScene& sc, const DCam& cam, double u, V2 rs, const double* L,
                                       const PView& cp, int t, const BVtx& cl, uint32_t& queries, Vis&& vis) {
     if (v_is_delta<FX>(sc, cl, L) || cl.light >= 0) return cfill(0.0);
@@ -589,7 +589,7 @@ __device__ DColor connect_camera_path(const DScene& sc, const DCam& cam, double 
     if (p_lig == 0.0) return cfill(0.0);
     wi = ri.d;
     const double pdf_origin = sa_to_area(p_lig, xo, xi, wi, ngi);
-    const DColor em = emit(sc, sc.mats[hi.material], L, hi.backface, hi.uv);
+    const DColor em = emit<FX>(sc, sc.mats[hi.material], L, hi.backface, hi.uv);
     const BVtx ll = vtx_of_hit(hi, em, pdf_origin, V3{0.0, 0.0, 0.0}, li);
     const DColor bsdf = v_f<FX>(sc, cl, ll.p, L, TR_RADIANCE);
     const double cos_wi = v_shading_cosine(sc, cl, wi, cl.ns);
@@ -601,7 +601,7 @@ __device__ DColor connect_camera_path(const DScene& sc, const DCam& cam, double 
 // connect_paths with the visibility test (bdpt_visible, the last condition of lumo's guard) done
 // beforehand by k_bdpt_vis: `visible` is its result, evaluated only when the other conditions
 // pass, exactly as the short-circuit guard does.
-template <bool FX>
+template <int FX>
 __device__ DColor connect_paths(const DScene& sc, const DCam& cam, const double* L, const PView& lp, int s,
                                 const PView& cp, int t, const BVtx& ll, const BVtx& cl, bool visible) {
     if (v_is_delta<FX>(sc, cl, L) || cl.light >= 0 || v_is_delta<FX>(sc, ll, L) || !visible) return cfill(0.0);
@@ -682,7 +682,7 @@ __device__ void bdpt_post_walks(const Bdpt& X, int si, const Paths& S, const BIt
 
 // Sample start: saves the re-run state, draws the light vertex (path_gen.rs:4-50) and queues the
 // light subpath.
-template <bool FX>
+template <int FX>
 __global__ __launch_bounds__(BLOCK) void k_bdpt_light_init(DScene sc, Paths S, Bdpt B, BItems I, int n) {
     const int slot = blockIdx.x * blockDim.x + threadIdx.x;
     bool go = false;
@@ -710,7 +710,7 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_light_init(DScene sc, Paths S, B
         const Ray ri = spawn(ho, onb_world(onb_new(ho.ns), wi_l));
         const double pdf_origin = 1.0 / light_area(sc, light);
         const double pdf_dir = dot(ho.ng, ri.d) / PI;
-        const DColor em = emit(sc, sc.mats[ho.material], L, ho.backface, ho.uv);
+        const DColor em = emit<FX>(sc, sc.mats[ho.material], L, ho.backface, ho.uv);
         B.lp.store(0, slot, vtx_of_hit(ho, em, pdf_origin * pdf_light, V3{0.0, 0.0, 0.0}, li));
         stc(S.gath, slot, em * fabs(dot(ri.d, ho.ns)) / (pdf_light * pdf_origin * pdf_dir));
         stv3(S.ro, slot, ri.o);
@@ -746,7 +746,7 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_cam_init(Paths S, Bdpt B, BItems
 #endif  // LUMO_MAIN_TU
 
 // One walk step (the loop body of path_gen.rs:52-157) after k_closest found the hit.
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ void bdpt_step_one(const DScene& sc, const Paths& S, const Tasks& T, const Bdpt& B, const BItems& I,
                               int mode, int slot, bool& alive, Counters& C) {
     const VStore& st = mode == TR_IMPORTANCE ? B.lp : B.cp;
@@ -842,7 +842,7 @@ __device__ void bdpt_step_one(const DScene& sc, const Paths& S, const Tasks& T, 
         }
     }
 }
-template <int STK, bool FX>
+template <int STK, int FX>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_bdpt_step(DScene sc, Paths S, Tasks T, Bdpt B, BItems I,
                                                                        int mode, const int32_t* queue, int32_t* next_queue) {
     const uint32_t count = S.counts[CNT_CUR];
@@ -862,7 +862,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_bdpt_step(DScene sc
 
 // The same two walks in one thread (path_gen.rs as written), from the slot's saved start state
 // into store X at `si`: used to re-run the samples whose subpaths did not fit the main store.
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ bool bdpt_walks(const DScene& sc, const Paths& S, const Tasks& T, const DCam& cam, const BItems& I,
                            const Bdpt& X, int slot, int si, Xorshift& rng, double* L, Counters& C, uint32_t& queries,
                            int& n_l, int& n_c) {
@@ -881,7 +881,7 @@ __device__ bool bdpt_walks(const DScene& sc, const Paths& S, const Tasks& T, con
         const Ray ri = spawn(ho, onb_world(onb_new(ho.ns), wi_l));
         const double pdf_origin = 1.0 / light_area(sc, light);
         const double pdf_dir = dot(ho.ng, ri.d) / PI;
-        const DColor em = emit(sc, sc.mats[ho.material], L, ho.backface, ho.uv);
+        const DColor em = emit<FX>(sc, sc.mats[ho.material], L, ho.backface, ho.uv);
         const BVtx root = vtx_of_hit(ho, em, pdf_origin * pdf_light, V3{0.0, 0.0, 0.0}, li);
         const DColor gathered = em * fabs(dot(ri.d, ho.ns)) / (pdf_light * pdf_origin * pdf_dir);
         n_l = bdpt_walk<STK, FX>(sc, X.lp, si, ri, rng, L, delta, root, gathered, pdf_dir, TR_IMPORTANCE, C, queries);
@@ -899,7 +899,7 @@ __device__ bool bdpt_walks(const DScene& sc, const Paths& S, const Tasks& T, con
 
 // Re-run of the samples whose subpaths did not fit: the walks into R, then the same post-walk
 // bookkeeping; their connections go through the item kernels like every other sample.
-template <int STK, bool LDS, bool FX>
+template <int STK, bool LDS, int FX>
 __global__ __launch_bounds__(BLOCK) void k_bdpt_redo(DScene sc0, Paths S, Tasks T, DCam cam, Bdpt B, Bdpt R, BItems I) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = min(*B.redo_count, B.redo_cap);
@@ -945,7 +945,7 @@ __device__ __forceinline__ ItemSel item_store(const Bdpt& B, const Bdpt& R, int 
 // (a) items, traversal part: the camera ray of each t = 1 connection and the light ray of each
 // s = 1 connection, traced whenever the ray exists (before lumo's BSDF-pdf guards, which
 // k_bdpt_eval_a evaluates; a ray the guards reject is never read and not counted as a query).
-template <int STK, bool LDS, bool FX>
+template <int STK, bool LDS, int FX>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_trace_a(DScene sc0, Paths S, DCam cam, Bdpt B, Bdpt R,
                                                                            BItems I, int n, const uint32_t* totals) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
@@ -987,7 +987,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_trace_a(DScen
 }
 
 // (a) items, evaluation: lumo's connection code with the traces looked up
-template <bool FX>
+template <int FX>
 __global__ __launch_bounds__(BLOCK) void k_bdpt_eval_a(DScene sc, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n,
                                                         const uint32_t* totals) {
     const uint32_t total = totals[0];
@@ -1042,7 +1042,7 @@ __device__ __forceinline__ void item_b_st(const BItems& I, int slot, uint32_t q,
 }
 
 // bdpt_visible of every (b) item whose guard reaches it (bd_path_trace.rs:279-290)
-template <int STK, bool LDS, bool FX>
+template <int STK, bool LDS, int FX>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_vis(DScene sc0, Paths S, Bdpt B, Bdpt R, BItems I,
                                                                        int n, const uint32_t* totals) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_vis(DScene sc
 }
 
 // MIS weight and contribution of every (b) item (bd_path_trace.rs:148-277), visibility from k_bdpt_vis
-template <bool FX>
+template <int FX>
 __global__ __launch_bounds__(BLOCK) void k_bdpt_paths(DScene sc, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n,
                                                        const uint32_t* totals) {
     const uint32_t total = totals[1];

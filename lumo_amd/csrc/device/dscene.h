@@ -665,7 +665,7 @@ constexpr int PRIM_SPHERE = -2;
 // Object::hit_t of the shape (kdtree.rs:178-180, rectangle.rs:87-89, triangle.rs:195-197)
 // FX: full feature set (instances, spheres, triangle objects, microfacet materials); scenes made
 // only of kd meshes / rectangles with Lambertian + Light materials run the FX = false kernels.
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ __forceinline__ double shape_hit_t(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                               double t_max, Counters& C) {
     if constexpr (FX) {
@@ -674,7 +674,7 @@ __device__ __forceinline__ double shape_hit_t(const DScene& sc, const lumo_objec
     }
     return kd_traverse<false, STK>(sc, ob, r, t_min, t_max, nullptr, C);
 }
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ __forceinline__ double object_hit_t(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                                double t_max, Counters& C) {
     if constexpr (FX) {
@@ -685,7 +685,7 @@ __device__ __forceinline__ double object_hit_t(const DScene& sc, const lumo_obje
 
 // Object::hit: kd GEO traversal, then the winner's GEO test (acceptance + t only; the record is
 // rebuilt by object_record).  Returns the global triangle index, PRIM_SPHERE, or -1 (miss).
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ __forceinline__ int shape_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                              double t_max, Counters& C, DHit& out) {
     if constexpr (FX) {
@@ -702,7 +702,7 @@ __device__ __forceinline__ int shape_hit_tri(const DScene& sc, const lumo_object
     if (!tri_hit_geo<false>(sc, ob.tri_base + idx, r, t_min, t_max, out)) return -1;
     return ob.tri_base + idx;
 }
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ __forceinline__ int object_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
                                               double t_max, Counters& C, DHit& out) {
     if constexpr (FX) {
@@ -714,7 +714,7 @@ __device__ __forceinline__ int object_hit_tri(const DScene& sc, const lumo_objec
 // Full hit record of triangle `tri` of object `ob` for world ray r (the GEO test is
 // deterministic, so re-running it reproduces the accepted hit), incl. Rectangle uv
 // (rectangle.rs:74-85) and the instance transform.
-template <bool FX>
+template <int FX>
 __device__ void object_record(const DScene& sc, const lumo_object& ob, int tri, const RayX& r, DHit& h) {
     if constexpr (!FX) {
         tri_hit_geo<true>(sc, tri, r, 0.0, DINF, h);
@@ -731,7 +731,7 @@ __device__ void object_record(const DScene& sc, const lumo_object& ob, int tri, 
 }
 
 // bvh.rs:315-362 (stackless, see DBvh): returns object index or -1
-template <bool GEO, int STK, bool FX>
+template <bool GEO, int STK, int FX>
 __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, const int32_t* items,
                             const lumo_object* objs, const RayX& r, double t_min, double t_max, Counters& C,
                             double* t_found = nullptr) {
@@ -772,7 +772,7 @@ __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, co
 }
 
 // BVH::hit_t (bvh.rs:371-374)
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ __forceinline__ double bvh_hit_t(const DScene& sc, const DBvh* nodes, int n, const int32_t* items,
                                             const lumo_object* objs, const RayX& r, double t_min, double t_max,
                                             Counters& C) {
@@ -789,7 +789,7 @@ struct HitRef {
     double t;
     int kind, obj, tri;
 };
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     HitRef h{DINF, 0, -1, -1};
     double t_max = DINF;
@@ -811,14 +811,14 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
 }
 
 // Rebuild the full hit record of a closest hit (the GEO test is deterministic).
-template <bool FX>
+template <int FX>
 __device__ __forceinline__ void hit_record(const DScene& sc, const HitRef& hr, const RayX& r, DHit& h) {
     const lumo_object& ob = hr.kind == 1 ? sc.objs[hr.obj] : sc.lights[hr.obj];
     object_record<FX>(sc, ob, hr.tri, r, h);
 }
 
 // Scene::hit_light (scene.rs:165-189): returns true and the light hit if visible.
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit& lh, Counters& C) {
     const lumo_object& L = sc.lights[light];
     const int tri = object_hit_tri<STK, FX>(sc, L, r, 0.0, DINF, C, lh);
@@ -833,7 +833,7 @@ __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit
 
 // Scene::hit_light without the record: the light triangle (or PRIM_SPHERE) when visible, else -1;
 // object_record rebuilds the record (the same GEO test).
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ int scene_hit_light_tri(const DScene& sc, const RayX& r, int light, Counters& C) {
     const lumo_object& L = sc.lights[light];
     DHit lh;
@@ -1015,27 +1015,35 @@ __device__ __forceinline__ bool standard_kind(int k) {
            k == LUMO_MAT_MF_DIELECTRIC;
 }
 
+// Feature classes FX: 0 lean (Lambertian / Light, kd meshes + rectangles), 1 full (every
+// material / shape / instance), 2 full + textures and bump maps (texture code compiled only here).
 // Material::map_normal (material.rs:323-331): the bump-mapped shading normal of Standard materials
-template <bool FX>
+template <int FX>
 __device__ __forceinline__ V3 mapped_ns(const DScene& sc, const lumo_material& m, const DHit& h) {
-    if constexpr (FX) {
+    if constexpr (FX >= 2) {
         if (m.normal_map >= 0) return normalize(onb_world(onb_new(h.ns), nmap_at(sc, sc.nmaps[m.normal_map], h.uv)));
     }
     return h.ns;
 }
 // MfDistribution::kd / ks / tf (microfacet.rs:118-134): Texture::albedo_at at the hit's uv
+template <int FX>
 __device__ __forceinline__ DColor mat_kd(const DScene& sc, const lumo_material& m, V2 uv, const double* L) {
-    return tex_at(sc, m.albedo_tex, m.albedo, uv, L);
+    if constexpr (FX >= 2) return tex_at(sc, m.albedo_tex, m.albedo, uv, L);
+    return spec_sample(m.albedo, L);
 }
+template <int FX>
 __device__ __forceinline__ DColor mat_ks(const DScene& sc, const lumo_material& m, V2 uv, const double* L) {
-    return tex_at(sc, m.ks_tex, m.ks, uv, L);
+    if constexpr (FX >= 2) return tex_at(sc, m.ks_tex, m.ks, uv, L);
+    return spec_sample(m.ks, L);
 }
+template <int FX>
 __device__ __forceinline__ DColor mat_tf(const DScene& sc, const lumo_material& m, V2 uv, const double* L) {
-    return tex_at(sc, m.tf_tex, m.tf, uv, L);
+    if constexpr (FX >= 2) return tex_at(sc, m.tf_tex, m.tf, uv, L);
+    return spec_sample(m.tf, L);
 }
 
 // Material::bsdf_sample (material.rs:273-289 -> bsdf.rs -> bxdf.rs:104-124); may terminate L
-template <bool FX>
+template <int FX>
 __device__ bool bsdf_sample(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, double* L,
                             double rand_u, V2 rs, V3& wi) {
     if constexpr (!FX) {  // Lambertian / Light only
@@ -1085,7 +1093,7 @@ __device__ bool bsdf_sample(const DScene& sc, const lumo_material& m, const DHit
     return true;
 }
 // Material::bsdf_pdf (material.rs:292-306 -> bsdf.rs:70-84 -> bxdf.rs:127-150)
-template <bool FX>
+template <int FX>
 __device__ double bsdf_pdf(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, V3 wi, const double* L) {
     if constexpr (!FX) {
         if (m.kind != LUMO_MAT_LAMBERTIAN) return 0.0;
@@ -1134,7 +1142,7 @@ __device__ double bsdf_pdf(const DScene& sc, const lumo_material& m, const DHit&
 }
 // Material::bsdf_f (material.rs:254-270 -> bsdf.rs:28-48 -> bxdf.rs:71-100); `importance` selects
 // Transport::Importance (BDPT light subpaths), which only changes dielectric transmission.
-template <bool FX>
+template <int FX>
 __device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h, V3 wo, V3 wi, const double* L,
                          bool importance = false) {
     if constexpr (!FX) {
@@ -1157,10 +1165,10 @@ __device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h
         const double r2 = sq(d.a);
         const double fd90 = 0.5 * r2 + 2.0 * sq(wh.z) * r2;
         const double fd = schlick(1.0, fd90, o.z) * schlick(1.0, fd90, i.z) * (1.0 + r2 * (1.0 / 1.51 - 1.0));
-        return fr * mat_ks(sc, m, h.uv, L) + mat_kd(sc, m, h.uv, L) * (cfill(1.0) - F) * fd / PI;
+        return fr * mat_ks<FX>(sc, m, h.uv, L) + mat_kd<FX>(sc, m, h.uv, L) * (cfill(1.0) - F) * fd / PI;
     }
     if (m.kind == LUMO_MAT_MF_CONDUCTOR) {
-        const DColor ks = mat_ks(sc, m, h.uv, L);
+        const DColor ks = mat_ks<FX>(sc, m, h.uv, L);
         if (mf_delta(d)) return ks * fresnel(d, o, V3{0.0, 0.0, 1.0}, L) / fabs(i.z);
         return ks * reflect_coeff(d, o, i, L);
     }
@@ -1169,14 +1177,14 @@ __device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h
     const bool flat = eta == 1.0 || mf_delta(d);
     V3 wh = flat ? V3{0.0, 0.0, 1.0} : normalize(i * er + o);
     if (reflection) {
-        const DColor ks = mat_ks(sc, m, h.uv, L);
+        const DColor ks = mat_ks<FX>(sc, m, h.uv, L);
         if (flat) return ks * fresnel(d, o, wh, L) / fabs(i.z);
         return ks * reflect_coeff(d, o, i, L);
     }
     const DColor F = fresnel(d, o, wh, L);
     if (wh.z < 0.0) wh = -wh;
     const double scale = importance ? 1.0 : er * er;
-    const DColor tf = mat_tf(sc, m, h.uv, L);
+    const DColor tf = mat_tf<FX>(sc, m, h.uv, L);
     if (flat) return tf * (cfill(1.0) - F) / (scale * fabs(i.z));
     const double hwo = dot(wh, o), hwi = dot(wh, i);
     return tf * mf_D(d, wh) * (cfill(1.0) - F) * mf_G(d, o, i, wh) / scale * fabs(hwi * hwo / (i.z * o.z)) /
@@ -1185,14 +1193,14 @@ __device__ DColor bsdf_f(const DScene& sc, const lumo_material& m, const DHit& h
 __device__ __forceinline__ double shading_cosine(const lumo_material& m, V3 wi, V3 ns) {
     return standard_kind(m.kind) ? fabs(dot(ns, wi)) : 1.0;
 }
-template <bool FX>
+template <int FX>
 __device__ __forceinline__ bool mat_is_specular(const lumo_material& m) {  // bxdf.rs:33-40
     if constexpr (!FX) return false;
     if (m.kind == LUMO_MAT_MF_DIELECTRIC) return true;
     if (m.kind == LUMO_MAT_MF_CONDUCTOR) return (m.roughness + m.roughness) / 2.0 < 0.01;
     return false;
 }
-template <bool FX>
+template <int FX>
 __device__ __forceinline__ bool mat_is_delta(const DScene& sc, const lumo_material& m, const double* L) {
     if constexpr (!FX) return false;
     if (m.kind == LUMO_MAT_MF_CONDUCTOR) return (m.roughness + m.roughness) / 2.0 < 1e-3;
@@ -1201,10 +1209,11 @@ __device__ __forceinline__ bool mat_is_delta(const DScene& sc, const lumo_materi
     return false;
 }
 // Material::emit (material.rs:221-234): Texture::albedo_at of the emission texture at the hit's uv
+template <int FX>
 __device__ __forceinline__ DColor emit(const DScene& sc, const lumo_material& m, const double* L, bool backface, V2 uv) {
     if (m.kind != LUMO_MAT_LIGHT) return cfill(0.0);
     if (!m.two_sided && backface) return cfill(0.0);
-    return m.scale * tex_at(sc, m.albedo_tex, m.albedo, uv, L) * dense_sample(sc.dense + 95 * m.illuminant, L);
+    return m.scale * mat_kd<FX>(sc, m, uv, L) * dense_sample(sc.dense + 95 * m.illuminant, L);
 }
 
 // lights (bvh.rs:51-86; Rectangle sample_on / sample_towards_pdf)
@@ -1263,7 +1272,7 @@ __device__ V3 shape_sample_towards(const DScene& sc, const lumo_object& L, V3 xo
     return normalize(xi - xo);
 }
 // Sampleable::sample_towards (Instance: instance.rs:162-167)
-template <bool FX>
+template <int FX>
 __device__ V3 light_sample_towards(const DScene& sc, const lumo_object& L, V3 xo, V2 rs) {
     if constexpr (!FX) return normalize(ld3(L.origin) + rs.x * ld3(L.b0) + rs.y * ld3(L.b1) - xo);  // Rectangle
     if (L.xform < 0) return shape_sample_towards(sc, L, xo, rs);
@@ -1273,7 +1282,7 @@ __device__ V3 light_sample_towards(const DScene& sc, const lumo_object& L, V3 xo
     return normalize(xf_apply(T.m, dl, 0.0));
 }
 // Sampleable::sample_towards_pdf (object.rs:149-156; Instance: instance.rs:169-199)
-template <bool FX>
+template <int FX>
 __device__ double light_pdf(const DScene& sc, const lumo_object& L, const RayX& ri, V3 xi, V3 ng) {
     if constexpr (!FX) {
         const double p_area = 1.0 / L.area;

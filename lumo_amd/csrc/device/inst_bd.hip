@@ -10,15 +10,18 @@ namespace lumo {
 namespace dev {
 
 template <int STK>
-void launch_bdpt_step(int grid, hipStream_t sm, bool fx, const DScene& sc, const Paths& S, const Tasks& T,
+void launch_bdpt_step(int grid, hipStream_t sm, int fx, const DScene& sc, const Paths& S, const Tasks& T,
                       const Bdpt& B, const BItems& I, int mode, const int32_t* queue, int32_t* next_queue) {
-    if (fx) k_bdpt_step<STK, true><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue);
-    else k_bdpt_step<STK, false><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue);
+    if (fx == 2) k_bdpt_step<STK, 2><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue);
+    else if (fx) k_bdpt_step<STK, 1><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue);
+    else k_bdpt_step<STK, 0><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue);
 }
 
 #define LUMO_TRAV_LAUNCH(KERNEL, ...)                                                        \
     do {                                                                                     \
-        if (l.lds) {                                                                         \
+        if (l.fx == 2) {                                                                     \
+            KERNEL<STK, false, 2><<<l.grid, BLOCK, 0, l.sm>>>(__VA_ARGS__);                  \
+        } else if (l.lds) {                                                                  \
             if (l.fx) KERNEL<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(__VA_ARGS__);  \
             else KERNEL<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(__VA_ARGS__);     \
         } else {                                                                             \
@@ -45,7 +48,7 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
     LUMO_TRAV_LAUNCH(k_bdpt_vis, sc, S, B, R, I, n, totals);
 }
 
-template void launch_bdpt_step<LUMO_STK>(int, hipStream_t, bool, const DScene&, const Paths&, const Tasks&,
+template void launch_bdpt_step<LUMO_STK>(int, hipStream_t, int, const DScene&, const Paths&, const Tasks&,
                                          const Bdpt&, const BItems&, int, const int32_t*, int32_t*);
 template void launch_bdpt_redo<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Tasks&, const DCam&,
                                          const Bdpt&, const Bdpt&, const BItems&);

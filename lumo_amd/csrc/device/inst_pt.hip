@@ -34,7 +34,9 @@ void launch_closest_q(const TravLaunch& l, const DScene& sc, const Paths& S, con
 
 template <int STK, bool NS1>
 void launch_shadow_q_ns(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& nxt) {
-    if (l.lds) {
+    if (l.fx == 2) {  // textured scenes: emission textures (no LDS staging variant)
+        k_shadow_q<STK, false, 2, NS1><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, nxt);
+    } else if (l.lds) {
         if (l.fx) k_shadow_q<STK, true, true, NS1><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, nxt);
         else k_shadow_q<STK, true, false, NS1><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, nxt);
     } else {

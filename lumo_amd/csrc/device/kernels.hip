@@ -678,7 +678,7 @@ void launch_trav(Ctx& c, uint64_t count, F&& f) {
     const bool lds = g_lds && c.sc.hot_bytes > 0;
     const int grid_full = ceil_div(count, BLOCK);
     const TravLaunch l{lds ? std::min(grid_full, c.lds_grid_cap) : grid_full, lds ? (size_t)c.sc.hot_bytes : 0, lds,
-                       c.sc.full != 0, c.stream};
+                       c.sc.full, c.stream};
     by_stack_class(c.sc.stack_class, [&](auto K) { f(K, l); });
 }
 
@@ -944,10 +944,12 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 }
                 {
                     StageTimer tm(c, g_timing, ST_SHADE);
-                    if (c.sc.full)
-                        k_shade_q<true><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                    if (c.sc.full == 2)
+                        k_shade_q<2><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                    else if (c.sc.full)
+                        k_shade_q<1><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
                     else
-                        k_shade_q<false><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                        k_shade_q<0><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
                 }
                 {
                     StageTimer tm(c, g_timing, ST_SHADOW);
@@ -972,16 +974,18 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                     }
                     StageTimer tm(c, g_timing, ST_SHADE);
                     by_stack_class(c.sc.stack_class, [&](auto K) {
-                        launch_bdpt_step<decltype(K)::value>(ceil_div(ub, BLOCK), sm, c.sc.full != 0, c.sc, S, T, B, BI, mode, qa, qb);
+                        launch_bdpt_step<decltype(K)::value>(ceil_div(ub, BLOCK), sm, c.sc.full, c.sc, S, T, B, BI, mode, qa, qb);
                     });
                 };
             };
             HIPCHK(hipMemsetAsync(B.redo_count, 0, sizeof(uint32_t), sm));
             HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));  // drop k_camera's queue
-            if (c.sc.full)
-                k_bdpt_light_init<true><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BI, N);
+            if (c.sc.full == 2)
+                k_bdpt_light_init<2><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BI, N);
+            else if (c.sc.full)
+                k_bdpt_light_init<1><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BI, N);
             else
-                k_bdpt_light_init<false><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BI, N);
+                k_bdpt_light_init<0><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BI, N);
             bst = bounce_loop(walk_step(TR_IMPORTANCE));
             if (bst) return bst;
             HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));
@@ -1025,10 +1029,12 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 }
                 StageTimer tm(c, g_timing, ST_BD_EVAL_A);
                 const int grid = std::min(ceil_div(totals[0], BLOCK), 1 << 16);
-                if (c.sc.full)
-                    k_bdpt_eval_a<true><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                if (c.sc.full == 2)
+                    k_bdpt_eval_a<2><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                else if (c.sc.full)
+                    k_bdpt_eval_a<1><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
                 else
-                    k_bdpt_eval_a<false><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                    k_bdpt_eval_a<0><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
             }
             if (totals[1] > 0) {
                 {
@@ -1039,10 +1045,12 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 }
                 StageTimer tm(c, g_timing, ST_BD_PATHS);
                 const int grid = std::min(ceil_div(totals[1], BLOCK), 1 << 16);
-                if (c.sc.full)
-                    k_bdpt_paths<true><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                if (c.sc.full == 2)
+                    k_bdpt_paths<2><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                else if (c.sc.full)
+                    k_bdpt_paths<1><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
                 else
-                    k_bdpt_paths<false><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                    k_bdpt_paths<0><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
             }
             {
                 StageTimer tm(c, g_timing, ST_RESOLVE);
@@ -1471,12 +1479,13 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     for (int i = 0; i < d->num_objects; ++i)
         full = full || (d->objects[i].type != LUMO_OBJ_KDMESH && d->objects[i].type != LUMO_OBJ_RECTANGLE);
     for (int i = 0; i < d->num_lights; ++i) full = full || d->lights[i].type != LUMO_OBJ_RECTANGLE;
-    for (int i = 0; i < d->num_materials; ++i) {  // textures and bump maps are sampled by the full kernels only
+    bool textured = false;  // textures and bump maps: feature class 2 (the only kernels that sample them)
+    for (int i = 0; i < d->num_materials; ++i) {
         const lumo_material& m = d->materials[i];
-        full = full || m.albedo_tex >= 0 || m.ks_tex >= 0 || m.tf_tex >= 0 || m.normal_map >= 0;
+        textured = textured || m.albedo_tex >= 0 || m.ks_tex >= 0 || m.tf_tex >= 0 || m.normal_map >= 0;
     }
     if (const char* e = std::getenv("LUMO_FULL_KERNELS")) full = full || std::atoi(e) != 0;  // A/B switch
-    s.full = full ? 1 : 0;
+    s.full = textured ? 2 : (full ? 1 : 0);
     c->has_scene = true;
     return LUMO_OK;
 }

@@ -17,7 +17,7 @@ struct TravLaunch {
     int grid;
     size_t shm;
     bool lds;
-    bool fx;
+    int fx;  // feature class (dscene.h): 0 lean, 1 full, 2 full + textures
     hipStream_t sm;
 };
 
@@ -33,7 +33,7 @@ void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, c
                   unsigned long long* tcount);
 
 template <int STK>
-void launch_bdpt_step(int grid, hipStream_t sm, bool fx, const DScene& sc, const Paths& S, const Tasks& T,
+void launch_bdpt_step(int grid, hipStream_t sm, int fx, const DScene& sc, const Paths& S, const Tasks& T,
                       const Bdpt& B, const BItems& I, int mode, const int32_t* queue, int32_t* next_queue);
 template <int STK>
 void launch_bdpt_redo(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const DCam& cam,
@@ -52,7 +52,7 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
     extern template void launch_trace<K>(int, hipStream_t, const DScene&, const double*, const double*,          \
                                          const int32_t*, int, int, double*, int32_t*, int32_t*, int32_t*,         \
                                          unsigned long long*);                                                    \
-    extern template void launch_bdpt_step<K>(int, hipStream_t, bool, const DScene&, const Paths&, const Tasks&,   \
+    extern template void launch_bdpt_step<K>(int, hipStream_t, int, const DScene&, const Paths&, const Tasks&,   \
                                              const Bdpt&, const BItems&, int, const int32_t*, int32_t*);          \
     extern template void launch_bdpt_redo<K>(const TravLaunch&, const DScene&, const Paths&, const Tasks&,        \
                                              const DCam&, const Bdpt&, const Bdpt&, const BItems&);               \

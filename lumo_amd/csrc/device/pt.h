@@ -9,7 +9,7 @@ namespace lumo {
 namespace dev {
 
 // ------------------------------------------------------------------ closest hit
-template <int STK, bool LDS, bool FX>
+template <int STK, bool LDS, int FX>
 __global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc0, Paths S, const int32_t* queue) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
@@ -51,7 +51,7 @@ __device__ __forceinline__ void qc(const QState& Q, int k, size_t q, const DColo
 }
 
 // Scene::hit (scene.rs:119-147) of every queued ray.
-template <int STK, bool LDS, bool FX>
+template <int STK, bool LDS, int FX>
 __global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest_q(DScene sc0, Paths S, QState cur) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
@@ -90,7 +90,7 @@ __device__ __forceinline__ void put_record(const ShadowQ& Q, int b, size_t r, co
 // (n_shadow x [light pick, light direction, BSDF sample]), the continuation and Russian
 // roulette.  Continuing paths are compacted into `nxt`; ending ones write their final values
 // per slot (the radiance after k_shadow_q when the path still has shadow rays pending).
-template <bool FX>
+template <int FX>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade_q(DScene sc, Paths S, Tasks T, QState cur, QState nxt,
                                                                       int buckets) {
     const uint32_t count = S.counts[CNT_CUR];
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade_q(DScene sc, 
                 const V2 rsq = xs_vec2(rng);
                 sampled = bsdf_sample<FX>(sc, m, ho, wo, L, rand_u, rsq, wi);  // may terminate L
                 if (!sampled) {
-                    if (flags & QF_SPECULAR) radiance = radiance + gathered * emit(sc, m, L, ho.backface, ho.uv);
+                    if (flags & QF_SPECULAR) radiance = radiance + gathered * emit<FX>(sc, m, L, ho.backface, ho.uv);
                 } else {
                     resolve = !mat_is_delta<FX>(sc, m, L);
                     if (resolve && buckets > 1) {  // origin object of the shadow rays (objects, then lights)
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade_q(DScene sc, 
 // Scene::hit_light + mis_sample of one NEE record (integrator.rs:100-184); plane base b.  The
 // path's wavelengths (header p) are read only after a visible hit, so they are not live across
 // the traversal.
-template <int STK, bool FX>
+template <int STK, int FX>
 __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const ShadowQ& Q, int b, size_t r, bool li_mode,
                                                   uint32_t p, Counters& C) {
     const RayX ri = rayx(Ray{V3{Q.D(b, r), Q.D(b + 1, r), Q.D(b + 2, r)}, V3{Q.D(b + 3, r), Q.D(b + 4, r), Q.D(b + 5, r)}});
@@ -252,7 +252,7 @@ __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const Shadow
             const double p_denom = li_mode ? p_lig : p_sct;
             const lumo_material hm = sc.mats[hi.material];
             const DColor f{{Q.D(b + 6, r), Q.D(b + 7, r), Q.D(b + 8, r), Q.D(b + 9, r)}};
-            out = f * cfill(1.0) * emit(sc, hm, L, hi.backface, hi.uv) * Q.D(b + 11, r) * weight / p_denom;
+            out = f * cfill(1.0) * emit<FX>(sc, hm, L, hi.backface, hi.uv) * Q.D(b + 11, r) * weight / p_denom;
         }
     }
     return out;
@@ -277,7 +277,7 @@ __device__ __forceinline__ void deliver_nee(const Paths& S, const ShadowQ& Q, co
 // the path's NEE term; otherwise it stores single_i over the pair's (consumed) L-record bsdf_f
 // planes and k_nee_fold adds the path's singles in i order.  No block barrier: a wave that
 // finishes its traversals early moves on to its next pairs.
-template <int STK, bool LDS, bool FX, bool NS1>
+template <int STK, bool LDS, int FX, bool NS1>
 __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc0, Paths S, QState nxt) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const int ns = NS1 ? 1 : sc0.n_shadow;

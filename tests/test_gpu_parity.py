@@ -158,3 +158,33 @@ def test_nan_pdf_continues_path(dev):
     assert np.isnan(g["radiance"]).any()  # the NaN pdf was reached (and counted, below)
     st = dev.stats()
     assert st.samples_nan > 0
+
+
+@pytest.mark.parametrize("max_paths", [0, 3000])
+def test_separate_result_buffers_match_oracle(dev, cornell, max_paths):
+    """lumo_render_tiles with each task's rgb_w a separate allocation, in reverse address order
+    and with gaps (how a C / Rust caller passes lumo's FilmTile buffers): the
+    device's host-copy path (not the single-transfer path the Python wrapper's one allocation
+    takes), alone and with the run split into chunks by max_paths."""
+    import ctypes as C
+
+    from lumo_amd import _ffi
+    cam = L.Camera.cornell_box((48, 48))
+    dev.upload(cornell, cam)
+    tasks = L.make_tasks(48, 48, 8, SEED)
+    n = len(tasks)
+    arr = (_ffi.TileTask * n)(*tasks)
+    res = (_ffi.TileResult * n)()
+    bufs = [None] * n
+    for i in reversed(range(n)):  # later tasks at lower addresses, padding between them
+        t = tasks[i]
+        P = (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1])
+        bufs[i] = np.full(4 * P + 17, np.nan)
+        res[i].rgb_w = bufs[i].ctypes.data_as(_ffi.c_double_p)
+    cfg = _ffi.RenderCfg(0, 0, max_paths, 0, 0.0, 0, 0, None)
+    _ffi.check(_ffi.load().lumo_render_tiles(dev.ctx, arr, n, C.byref(cfg), res), "render_tiles")
+    obufs, ores, _ = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        np.testing.assert_array_equal(b[:len(ob)], ob)
+        assert np.isnan(b[len(ob):]).all()  # nothing written past the tile
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)

@@ -34,11 +34,11 @@ def _cmp(g, o):
         np.testing.assert_array_equal(g[k], o[k], err_msg=k)
 
 
-@pytest.mark.parametrize("tile", [0, 5, 9, 14])
+@pytest.mark.parametrize("tile", [0, 5, 9, 11])
 def test_texture_zoo_paths(dev, zoo, tile):
     cam = default_camera((64, 48))
     dev.upload(zoo, cam)
-    assert dev.scene_info().full_kernels == 1
+    assert dev.scene_info().full_kernels == 2  # the texture feature class
     task = L.make_tasks(64, 48, 16, SEED)[tile]
     _cmp(gpu_paths(dev, task), O.trace_paths(zoo.desc(), cam.desc, task))
 
@@ -54,7 +54,7 @@ def test_texture_zoo_tiles(dev, zoo):
         assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
 
 
-@pytest.mark.parametrize("tile", [0, 6])
+@pytest.mark.parametrize("tile", [0, 3])
 def test_texture_zoo_bdpt_paths(dev, zoo, tile):
     cam = default_camera((32, 32))
     dev.upload(zoo, cam)
@@ -88,7 +88,7 @@ def test_textured_obj_scene(dev, tmp_path):
     sc = L.Scene.from_file(str(p), "scene.obj").build()
     cam = default_camera((32, 32))
     dev.upload(sc, cam)
-    assert dev.scene_info().full_kernels == 1
+    assert dev.scene_info().full_kernels == 2  # the texture feature class
     tasks = L.make_tasks(32, 32, 8, SEED)
     bufs, res = dev.render_tasks(tasks)
     obufs, ores, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
