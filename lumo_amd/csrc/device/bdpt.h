@@ -843,7 +843,7 @@ __device__ void bdpt_step_one(const DScene& sc, const Paths& S, const Tasks& T, 
     }
 }
 template <int STK, int FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_bdpt_step(DScene sc, Paths S, Tasks T, Bdpt B, BItems I,
+__global__ __launch_bounds__(BLOCK, LUMO_BDPT_STEP_WAVES) void k_bdpt_step(DScene sc, Paths S, Tasks T, Bdpt B, BItems I,
                                                                        int mode, const int32_t* queue, int32_t* next_queue) {
     const uint32_t count = S.counts[CNT_CUR];
     Counters C{0, 0, 0};

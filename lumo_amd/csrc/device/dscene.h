@@ -473,8 +473,12 @@ __device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_mi
 }
 
 // kdtree.rs:101-169.  GEO: returns the winning local triangle index (or -1);
-// !GEO: returns t of the first hit found (or INF).  The (node, t0, t1) stack is sized by the
-// stack class STK (lumo: 64); it lives in scratch for the classes above ~8.  Keeping its top 2 /
+// !GEO: returns t of the first hit found (or INF).  lumo's (node, t0, t1) stack is sized by the
+// stack class STK (lumo: 64); it lives in scratch for the classes above ~8.  Only (node, t0) is
+// stored: the t1 of entry k is always t0 of entry k-1 (the root interval's end for k = 0).  A
+// push happens at an interior node whose interval end is the t0 of the entry below (set by
+// that entry's push, restored by every pop, and changed by a hit only in a leaf, which always
+// pops next), so the restored values are lumo's bit for bit with 12 instead of 20 B per entry.  Keeping its top 2 /
 // 4 / 8 entries in registers as a shift register measured 6 / 27 / 92 % slower on C3 (the extra
 // VGPRs push more of the traversal state into scratch at 4 waves/SIMD).
 #ifdef LUMO_NOINLINE_KD
@@ -488,7 +492,7 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
     const double origin[3] = {r.o.x, r.o.y, r.o.z};
     const double inv_dir[3] = {r.inv.x, r.inv.y, r.inv.z};
     int st_node[STK];
-    double st_ts[STK], st_te[STK];
+    double st_ts[STK];
     int sp = 0;
     double t_hit = DINF;
     int curr = ob.kd_root;
@@ -497,6 +501,7 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
     C.aabb++;
     slab(ob.bmin, ob.bmax, r.o, r.inv, ts, te);
     double t_start = rmax(ts, t_min), t_end = rmin(te, t_max);
+    const double t_end0 = t_end;
     for (;;) {
         if (t_hit < t_start) break;
         const DKd node = sc.kdp[curr];
@@ -520,7 +525,7 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
             sp--;
             curr = st_node[sp];
             t_start = st_ts[sp];
-            t_end = st_te[sp];
+            t_end = sp == 0 ? t_end0 : st_ts[sp - 1];
         } else {
             C.kd++;
             const int ax = axis;
@@ -538,7 +543,6 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
                 curr = first;
                 st_node[sp] = second;
                 st_ts[sp] = t_split;
-                st_te[sp] = t_end;
                 t_end = t_split;
                 sp++;
             }
