@@ -85,6 +85,9 @@ int oracle_furnace(const lumo_scene_desc* scene, int material, const double* wo,
  * (Object::hit from xo), else 0. */
 int oracle_light_sample(const lumo_scene_desc* scene, int light, const double* xo, size_t n, uint64_t seed,
                         double* wi3);
+/* Math probes (spherical_utils / onb / complex / vec3 tests): see oracle.cpp oracle_math. */
+int oracle_math(int op, const double* in, size_t n, double* out);
+
 int oracle_light_pdf(const lumo_scene_desc* scene, int light, const double* xo, const double* wi3, size_t n,
                      double* pdf);
 

@@ -2519,3 +2519,48 @@ extern "C" int oracle_mis_sums(const lumo_scene_desc* scene, const lumo_camera_d
     }
     return LUMO_OK;
 }
+
+// ---- math probes for the known-value / property tests of lumo's math modules
+// (spherical_utils_tests.rs, onb.rs tests, complex_tests.rs, vec3_tests.rs), evaluated with the
+// oracle's own helpers (the vector algebra of common/vec.h is the device's as well).
+//   op 0: w (3)    -> cos_phi, sin_phi, cos2_theta, sin2_theta, sin_theta, tan2_theta   (6)
+//   op 1: w, v (6) -> Onb::new(w).to_world(to_local(v))                               (3)
+//   op 2: a, b (4) -> a / b, a / 0.0, 1 / b, sqrt(a), a - a                           (10)
+//   op 3: v (3)    -> normalize(v), its squared length                                (4)
+//   op 4: u, v (6) -> same_hemisphere(u, v)                                           (1)
+extern "C" int oracle_math(int op, const double* in, size_t n, double* out) {
+    static const int IN[] = {3, 6, 4, 3, 6}, OUT[] = {6, 3, 10, 4, 1};
+    if (op < 0 || op > 4 || (n && (!in || !out))) return LUMO_ERR_INVALID;
+    for (size_t i = 0; i < n; ++i) {
+        const double* x = in + IN[op] * i;
+        double* y = out + OUT[op] * i;
+        const V3 a{x[0], x[1], x[2]};
+        if (op == 0) {
+            const double r[6] = {sph_cos_phi(a), sph_sin_phi(a), sph_cos2(a), sph_sin2(a), sph_sin(a), sph_tan2(a)};
+            std::memcpy(y, r, sizeof(r));
+        } else if (op == 1) {
+            const Onb o = onb_new(a);
+            const V3 v = onb_to_world(o, onb_to_local(o, V3{x[3], x[4], x[5]}));
+            y[0] = v.x;
+            y[1] = v.y;
+            y[2] = v.z;
+        } else if (op == 2) {
+            const Cx ca{x[0], x[1]}, cb{x[2], x[3]};
+            const Cx r[5] = {cx_div(ca, cb), cx_div_f(ca, 0.0), f_div_cx(1.0, cb), cx_sqrt(ca),
+                             Cx{ca.re - ca.re, ca.im - ca.im}};
+            for (int k = 0; k < 5; ++k) {
+                y[2 * k] = r[k].re;
+                y[2 * k + 1] = r[k].im;
+            }
+        } else if (op == 3) {
+            const V3 v = normalize(a);
+            y[0] = v.x;
+            y[1] = v.y;
+            y[2] = v.z;
+            y[3] = length_squared(v);
+        } else {
+            y[0] = same_hemisphere(a, V3{x[3], x[4], x[5]}) ? 1.0 : 0.0;
+        }
+    }
+    return LUMO_OK;
+}

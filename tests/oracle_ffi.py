@@ -53,6 +53,8 @@ def load(path=None):
         lib.oracle_light_sample.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, C.c_size_t, C.c_uint64, dp]
         lib.oracle_light_pdf.restype = C.c_int
         lib.oracle_light_pdf.argtypes = [C.POINTER(_ffi.SceneDesc), C.c_int, dp, dp, C.c_size_t, dp]
+        lib.oracle_math.restype = C.c_int
+        lib.oracle_math.argtypes = [C.c_int, dp, C.c_size_t, dp]
         lib.oracle_mis_sums.restype = C.c_int
         lib.oracle_mis_sums.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(_ffi.CameraDesc), C.c_size_t, C.c_uint64,
                                         dp, _ffi.c_int32_p]
@@ -194,3 +196,15 @@ def mis_sums(scene_desc, camera_desc, n, seed):
                              lens.ctypes.data_as(_ffi.c_int32_p))
     assert st == 0, st
     return sums, lens
+
+
+MATH_IO = {0: (3, 6), 1: (6, 3), 2: (4, 10), 3: (3, 4), 4: (6, 1)}
+
+
+def math(op, x):
+    """oracle_math probe `op` over the rows of x (see oracle.cpp)."""
+    ni, no = MATH_IO[op]
+    x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1, ni)
+    out = np.zeros((len(x), no))
+    assert load().oracle_math(op, _dp(x), len(x), _dp(out)) == 0
+    return out
