@@ -56,6 +56,19 @@ $(ORACLE_G): oracle/src/oracle.cpp oracle/oracle.h $(COMMON_H)
 	@mkdir -p oracle/_build
 	$(CXX) $(CXXFLAGS) -O2 -DLUMO_ORACLE_GLIBC -shared -o $@ oracle/src/oracle.cpp -lpthread
 
+# Sanitizer build (CPU only): the host library sources and the oracle under ASan + UBSan, driven by
+# tools/sanitize/main.cpp (scene builds, both integrators, textures, hostile PNG / HDR / OBJ input).
+SAN_FLAGS := -O1 -g -std=c++17 $(FPFLAGS) -fsanitize=address,undefined -fno-sanitize-recover=all \
+             -fno-omit-frame-pointer -Wall -Wno-unused-parameter
+build/sanitize/lumo_sanitize: tools/sanitize/main.cpp $(HOST_SRC) oracle/src/oracle.cpp oracle/oracle.h $(COMMON_H) \
+                              $(wildcard lumo_amd/csrc/host/*.h)
+	@mkdir -p build/sanitize
+	$(CXX) $(SAN_FLAGS) -o $@ tools/sanitize/main.cpp $(HOST_SRC) oracle/src/oracle.cpp -lpthread -lz
+
+sanitize: build/sanitize/lumo_sanitize
+	ASAN_OPTIONS=halt_on_error=1:detect_leaks=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
+	    ./build/sanitize/lumo_sanitize
+
 # A/B builds of the device code (perf experiments, loaded with LUMO_AMD_LIB=<path>):
 #   make variant NAME=rs0 DEVFLAGS=-DLUMO_KD_REG=0   ->  lumo_amd/var/liblumo_amd_rs0.so
 variant:
@@ -66,4 +79,4 @@ variant:
 clean:
 	rm -rf build $(LIB) oracle/_build lumo_amd/var
 
-.PHONY: all clean variant
+.PHONY: all clean variant sanitize

@@ -96,6 +96,12 @@ bool png_raw(const uint8_t* d, size_t n, PngRaw& out, std::string& err) {
     }
     const size_t bits = (size_t)out.width * (size_t)channels * (size_t)out.bit_depth;
     out.stride = (bits + 7) / 8;
+    // png 0.17's default Limits (64 MiB of decoded image data): larger images are an error there
+    constexpr size_t PNG_LIMIT_BYTES = (size_t)64 << 20;
+    if (out.stride > PNG_LIMIT_BYTES || out.stride * (size_t)out.height > PNG_LIMIT_BYTES) {
+        err = "PNG image exceeds the decoder's 64 MiB limit";
+        return false;
+    }
     const size_t bpp = std::max<size_t>(1, (size_t)channels * (size_t)out.bit_depth / 8);
     std::vector<uint8_t> raw((out.stride + 1) * (size_t)out.height);
     z_stream zs{};
