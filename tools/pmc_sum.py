@@ -15,7 +15,8 @@ def short(name):
             return k
     return name[:40]
 
-root, names = sys.argv[1], sys.argv[2:]
+root, names = sys.argv[1], [a for a in sys.argv[2:] if a != "--all"]
+ALL = "--all" in sys.argv
 for v in names:
     acc = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
@@ -27,6 +28,9 @@ for v in names:
                 disp[k].add(r.get("Dispatch_Id", ""))
     for k in sorted(acc, key=lambda k: -acc[k].get("SQ_WAVE_CYCLES", 0))[:6]:
         c = acc[k]
+        if ALL:
+            print(v, k, " ".join(f"{n}={x:.4g}" for n, x in sorted(c.items())))
+            continue
         hit = c.get("TCC_HIT_sum", 0)
         miss = c.get("TCC_MISS_sum", 0)
         print(f"{v:6s} {k:14s} waves={c.get('SQ_WAVES', 0):.3g} valu={c.get('SQ_INSTS_VALU', 0):.4g} "
