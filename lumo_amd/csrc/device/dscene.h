@@ -27,6 +27,10 @@ constexpr double SVI = 253.819;  // SAMPLE_VISIBLE_INTEGRAL
 
 // kd node packed to 16 B for the device (lumo_kd_node is 32 B): interior nodes hold the split
 // point, leaves {first, count}; meta = right << 2 | axis, axis == 3 marks a leaf.
+// kd node as the device walks it (16 B): split point or leaf range, (right << 2) | axis (axis 3 =
+// leaf), and the left child's index, explicit so that the upload can lay each tree out in
+// cache-line treelets (a node and its nearest descendants in one 128-B line) instead of lumo's
+// preorder (left = i + 1, right child far away).  The traversal visits the same logical nodes.
 struct alignas(16) DKd {
     union {
         double point;
@@ -35,7 +39,7 @@ struct alignas(16) DKd {
         } leaf;
     } u;
     int32_t meta;
-    int32_t pad;
+    int32_t left;
 };
 constexpr int TV_STRIDE = 10;  // doubles per triangle in the vertex soup (A, B, C, pad) -> 80 B
 
@@ -533,8 +537,8 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
             const int right = node.meta >> 2;
             const double t_split = (point - origin[ax]) * inv_dir[ax];
             const bool left_first = origin[ax] < point || (origin[ax] == point && inv_dir[ax] <= 0.0);
-            const int first = left_first ? curr + 1 : right;
-            const int second = left_first ? right : curr + 1;
+            const int first = left_first ? node.left : right;
+            const int second = left_first ? right : node.left;
             if (t_split > t_end || t_split <= 0.0) {
                 curr = first;
             } else if (t_split < t_start) {

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <new>
 #include <type_traits>
 #include <vector>
@@ -1318,7 +1319,6 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     chk(upload(*c, d->triangles, (size_t)d->num_triangles, &s.tris));
     chk(upload(*c, d->kd_nodes, (size_t)d->num_kd_nodes, &s.kd));
     chk(upload(*c, d->kd_items, (size_t)d->num_kd_items, &s.kd_items));
-    chk(upload(*c, d->objects, (size_t)d->num_objects, &s.objs));
     // device BVHs: right child -> escape index (DBvh, dscene.h)
     auto escapes = [&](const lumo_bvh_node* nodes, int n, std::vector<DBvh>& out) {
         out.assign(n > 0 ? n : 0, DBvh{});
@@ -1346,7 +1346,6 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     escapes(d->light_nodes, d->num_light_nodes, lbvh);
     chk(upload(*c, obvh.data(), obvh.size(), &s.onodes));
     chk(upload(*c, d->object_items, (size_t)d->num_object_items, &s.oitems));
-    chk(upload(*c, d->lights, (size_t)d->num_lights, &s.lights));
     chk(upload(*c, lbvh.data(), lbvh.size(), &s.lnodes));
     chk(upload(*c, d->light_items, (size_t)d->num_light_items, &s.litems));
     chk(upload(*c, d->alias_prob, (size_t)d->num_lights, &s.alias_prob));
@@ -1365,21 +1364,92 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     for (int i = 0; i < d->num_triangles; ++i)
         for (int k = 0; k < 3; ++k)
             for (int a = 0; a < 3; ++a) tv[(size_t)TV_STRIDE * i + 3 * k + a] = d->vertices[3 * d->triangles[i].v[k] + a];
-    std::vector<DKd> kdp(d->num_kd_nodes);
-    for (int i = 0; i < d->num_kd_nodes; ++i) {
-        const lumo_kd_node& n = d->kd_nodes[i];
-        DKd k{};
-        if (n.leaf) {
-            k.u.leaf.first = n.first;
-            k.u.leaf.count = n.count;
-            k.meta = 3;
-        } else {
-            if (n.right < 0 || n.right >= (1 << 29) || n.axis < 0 || n.axis > 2) chk(LUMO_ERR_INVALID);
-            k.u.point = n.point;
-            k.meta = (n.right << 2) | n.axis;
+    // kd trees in cache-line treelets: each tree (from each distinct kd_root) is cut into groups of
+    // up to 8 nodes (128 B) taken breadth-first from a group root, so a node's children and
+    // grandchildren are usually in the line the node itself came in; trees under 8 nodes are
+    // packed without alignment.  Children are stored as explicit indices (DKd::left).
+    std::vector<int32_t> kd_new(d->num_kd_nodes, -1);
+    std::vector<DKd> kdp;
+    {
+        std::vector<int32_t> order;  // old indices in new order (-1: padding)
+        auto kid = [&](int i, int which) { return which == 0 ? i + 1 : d->kd_nodes[i].right; };
+        auto valid = [&](int i) { return i >= 0 && i < d->num_kd_nodes; };
+        auto place_tree = [&](int root) {
+            if (!valid(root) || kd_new[root] >= 0) return;
+            int size = 0;  // nodes of the tree (bounded walk)
+            {
+                std::vector<int32_t> st{root};
+                while (!st.empty() && size <= 8) {
+                    const int i = st.back();
+                    st.pop_back();
+                    size++;
+                    if (!d->kd_nodes[i].leaf) {
+                        for (int w = 0; w < 2; ++w)
+                            if (valid(kid(i, w))) st.push_back(kid(i, w));
+                    }
+                }
+            }
+            std::deque<int32_t> groups{root};
+            while (!groups.empty()) {
+                const int g = groups.front();
+                groups.pop_front();
+                if (size > 8)
+                    while (order.size() % 8) order.push_back(-1);  // start a 128-B line
+                std::deque<int32_t> bfs{g};
+                int used = 0;
+                while (!bfs.empty()) {
+                    const int i = bfs.front();
+                    bfs.pop_front();
+                    if (used == 8) {
+                        groups.push_back(i);
+                        continue;
+                    }
+                    kd_new[i] = (int32_t)order.size();
+                    order.push_back(i);
+                    used++;
+                    if (!d->kd_nodes[i].leaf)
+                        for (int w = 0; w < 2; ++w)
+                            if (valid(kid(i, w)) && kd_new[kid(i, w)] < 0) bfs.push_back(kid(i, w));
+                }
+            }
+        };
+        for (int i = 0; i < d->num_objects; ++i)
+            if (d->objects[i].type == LUMO_OBJ_KDMESH || d->objects[i].type == LUMO_OBJ_RECTANGLE) place_tree(d->objects[i].kd_root);
+        for (int i = 0; i < d->num_lights; ++i)
+            if (d->lights[i].type == LUMO_OBJ_KDMESH || d->lights[i].type == LUMO_OBJ_RECTANGLE) place_tree(d->lights[i].kd_root);
+        kdp.assign(order.size(), DKd{});
+        for (size_t j = 0; j < order.size(); ++j) {
+            const int i = order[j];
+            if (i < 0) continue;
+            const lumo_kd_node& n = d->kd_nodes[i];
+            DKd k{};
+            if (n.leaf) {
+                k.u.leaf.first = n.first;
+                k.u.leaf.count = n.count;
+                k.meta = 3;
+                k.left = -1;
+            } else {
+                if (!valid(n.right) || !valid(i + 1) || n.axis < 0 || n.axis > 2 || kd_new[n.right] >= (1 << 29))
+                    chk(LUMO_ERR_INVALID);
+                k.u.point = n.point;
+                k.meta = (kd_new[n.right] << 2) | n.axis;
+                k.left = kd_new[i + 1];
+            }
+            kdp[j] = k;
         }
-        kdp[i] = k;
     }
+    auto relaid = [&](const lumo_object* src, int n) {  // objects / lights with their new kd roots
+        std::vector<lumo_object> v(src, src + n);
+        for (lumo_object& o : v)
+            if ((o.type == LUMO_OBJ_KDMESH || o.type == LUMO_OBJ_RECTANGLE) && o.kd_root >= 0 &&
+                o.kd_root < d->num_kd_nodes)
+                o.kd_root = kd_new[o.kd_root];
+        return v;
+    };
+    const std::vector<lumo_object> objs_dev = relaid(d->objects, d->num_objects);
+    const std::vector<lumo_object> lights_dev = relaid(d->lights, d->num_lights);
+    chk(upload(*c, objs_dev.data(), objs_dev.size(), &s.objs));
+    chk(upload(*c, lights_dev.data(), lights_dev.size(), &s.lights));
     chk(upload(*c, tv.data(), tv.size(), &s.tv));
     chk(upload(*c, kdp.data(), kdp.size(), &s.kdp));
     if (st) {
@@ -1402,8 +1472,8 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         s.off_oitems = put(d->object_items, sizeof(int32_t) * d->num_object_items);
         s.off_lnodes = put(lbvh.data(), sizeof(DBvh) * lbvh.size());
         s.off_litems = put(d->light_items, sizeof(int32_t) * d->num_light_items);
-        s.off_objs = put(d->objects, sizeof(lumo_object) * d->num_objects);
-        s.off_lights = put(d->lights, sizeof(lumo_object) * d->num_lights);
+        s.off_objs = put(objs_dev.data(), sizeof(lumo_object) * objs_dev.size());
+        s.off_lights = put(lights_dev.data(), sizeof(lumo_object) * lights_dev.size());
         s.off_kdp = put(kdp.data(), sizeof(DKd) * kdp.size());
         s.off_kd_items = put(d->kd_items, sizeof(int32_t) * d->num_kd_items);
         s.off_tris = put(d->triangles, sizeof(lumo_triangle) * d->num_triangles);
