@@ -589,7 +589,7 @@ enum WorkId {
     W_BDR_SPN, W_BD_NL, W_BD_NC, W_BD_NITEMS, W_BD_IOFF, W_BD_DRAWS, W_BD_OK, W_BD_ITOTAL, W_BD_TERM, W_BD_PDF, W_BD_WDEPTH,
     W_BD_CAMO, W_BD_CAMD, W_BD_RNG0, W_BD_LAM0, W_BDR_DRAWS, W_BDR_OK, W_BD_NB, W_BD_OFFB, W_BD_TERMB, W_BD_VIS, W_BD_AT, W_BD_AKIND, W_BD_AOBJ,
     W_BD_ATRI, W_CHECKS, W_QS0_D, W_QS0_R, W_QS0_I, W_QS1_D, W_QS1_R, W_QS1_I, W_HQ_T, W_HQ_I, W_SQ_D, W_SQ_I,
-    W_SQ_HD, W_SQ_HI, W_COUNT
+    W_SQ_HD, W_SQ_HI, W_SQ_HR, W_COUNT
 };
 
 template <typename T>
@@ -760,8 +760,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         S.sq.cap = S.sq.hcap * (size_t)ns;
         S.sq.d = wbuf<double>(c, W_SQ_D, SD_N * S.sq.cap, st);
         S.sq.i = wbuf<int32_t>(c, W_SQ_I, SI_N * S.sq.cap, st);
-        S.sq.hd = wbuf<double>(c, W_SQ_HD, SH_N * S.sq.hcap, st);
+        S.sq.hd = wbuf<double>(c, W_SQ_HD, (ns > 1 ? SH_N : SH_N1) * S.sq.hcap, st);
         S.sq.hi = wbuf<int32_t>(c, W_SQ_HI, SHI_N * S.sq.hcap, st);
+        S.sq.hr = ns > 1 ? wbuf<uint64_t>(c, W_SQ_HR, 2 * S.sq.hcap, st) : nullptr;
     }
     S.p_rgb = wbuf<double>(c, W_P_RGB, 3 * (size_t)N, st);
     S.p_lum = wbuf<double>(c, W_P_LUM, N, st);
@@ -945,12 +946,26 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 }
                 {
                     StageTimer tm(c, g_timing, ST_SHADE);
-                    if (c.sc.full == 2)
-                        k_shade_q<2><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
-                    else if (c.sc.full)
-                        k_shade_q<1><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
-                    else
-                        k_shade_q<0><<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                    const int g = ceil_div(ub, BLOCK);
+                    if (ns > 1) {  // NEE pairs by k_nee_gen, one thread per pair
+                        const int gp = std::min(ceil_div((uint64_t)ub * (uint32_t)ns, BLOCK), 1 << 16);
+                        if (c.sc.full == 2) {
+                            k_shade_q<2, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                            k_nee_gen<2><<<gp, BLOCK, 0, sm>>>(c.sc, S);
+                        } else if (c.sc.full) {
+                            k_shade_q<1, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                            k_nee_gen<1><<<gp, BLOCK, 0, sm>>>(c.sc, S);
+                        } else {
+                            k_shade_q<0, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                            k_nee_gen<0><<<gp, BLOCK, 0, sm>>>(c.sc, S);
+                        }
+                    } else if (c.sc.full == 2) {
+                        k_shade_q<2, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                    } else if (c.sc.full) {
+                        k_shade_q<1, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                    } else {
+                        k_shade_q<0, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                    }
                 }
                 {
                     StageTimer tm(c, g_timing, ST_SHADOW);

@@ -85,13 +85,43 @@ __device__ __forceinline__ void put_record(const ShadowQ& Q, int b, size_t r, co
     Q.D(b + 11, r) = cosv;
 }
 
+// One (light sample, BSDF sample) pair of NEE records (integrator.rs:87-137) at pair index r:
+// the light pick, its direction, bsdf_f / pdf / cosine, then the BSDF-sampled direction (6 RNG
+// draws).  Returns whether the BSDF sample exists (SI_BVALID).
+template <int FX>
+__device__ __forceinline__ bool nee_pair(const DScene& sc, const ShadowQ& sq, size_t r, const DHit& ho,
+                                         const lumo_material& m, V3 wo, double* L, Xorshift& rng) {
+    const int li = sample_light(sc, xs_float(rng));
+    const lumo_object& Lo = sc.lights[li];
+    sq.D(SD_PDFL, r) = sc.alias_pdf[li];
+    sq.I(SI_LIGHT, r) = li;
+    {
+        const V2 rs = xs_vec2(rng);
+        const V3 w = light_sample_towards<FX>(sc, Lo, ho.p, rs);
+        put_record(sq, SD_LO, r, spawn(ho, w), bsdf_f<FX>(sc, m, ho, wo, w, L), bsdf_pdf<FX>(sc, m, ho, wo, w, L),
+                   shading_cosine(m, w, ho.ns));
+    }
+    const double ru = xs_float(rng);
+    const V2 rsq = xs_vec2(rng);
+    V3 w;
+    const bool ok = bsdf_sample<FX>(sc, m, ho, wo, L, ru, rsq, w);
+    sq.I(SI_BVALID, r) = ok ? 1 : 0;
+    if (ok)
+        put_record(sq, SD_BO, r, spawn(ho, w), bsdf_f<FX>(sc, m, ho, wo, w, L), bsdf_pdf<FX>(sc, m, ho, wo, w, L),
+                   shading_cosine(m, w, ho.ns));
+    return ok;
+}
+constexpr int NEE_DRAWS = 6;  // RNG draws per pair in nee_pair
+
 // The bounce of every queued path (path_trace.rs:18-77): the pending NEE term of the previous
 // bounce, the hit record, emission, BSDF sample, the NEE records of integrator.rs:87-137
 // (n_shadow x [light pick, light direction, BSDF sample]), the continuation and Russian
 // roulette.  Continuing paths are compacted into `nxt`; ending ones write their final values
 // per slot (the radiance after k_shadow_q when the path still has shadow rays pending).
-template <int FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade_q(DScene sc, Paths S, Tasks T, QState cur, QState nxt,
+// SPLIT (n_shadow > 1): the path's hit record and RNG state go to its NEE header and k_nee_gen
+// generates the pairs, one thread each; this kernel steps its RNG past their draws.
+template <int FX, bool SPLIT>
+__global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE_WAVES) void k_shade_q(DScene sc, Paths S, Tasks T, QState cur, QState nxt,
                                                                       int buckets) {
     const uint32_t count = S.counts[CNT_CUR];
     const int ns = sc.n_shadow;
@@ -147,31 +177,24 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADE_WAVES) void k_shade_q(DScene sc, 
         const uint32_t sp = key * sq.seg + block_slot_bucket(resolve, key, S.counts + CNT_BUCKET0);
         if (resolve) {
             uint32_t n_sh = 0;
-            for (int i = 0; i < ns; ++i) {
-                const size_t r = (size_t)sp * ns + i;
-                const int li = sample_light(sc, xs_float(rng));
-                const lumo_object& Lo = sc.lights[li];
-                sq.D(SD_PDFL, r) = sc.alias_pdf[li];
-                sq.I(SI_LIGHT, r) = li;
-                {
-                    const V2 rs = xs_vec2(rng);
-                    const V3 w = light_sample_towards<FX>(sc, Lo, ho.p, rs);
-                    put_record(sq, SD_LO, r, spawn(ho, w), bsdf_f<FX>(sc, m, ho, wo, w, L),
-                               bsdf_pdf<FX>(sc, m, ho, wo, w, L), shading_cosine(m, w, ho.ns));
-                    n_sh++;
+            if constexpr (SPLIT) {
+                for (int k = 0; k < 3; ++k) {
+                    sq.HD(SH_P + k, sp) = (&ho.p.x)[k];
+                    sq.HD(SH_E + k, sp) = (&ho.err.x)[k];
+                    sq.HD(SH_NS + k, sp) = (&ho.ns.x)[k];
+                    sq.HD(SH_NG + k, sp) = (&ho.ng.x)[k];
+                    sq.HD(SH_WO + k, sp) = (&wo.x)[k];
                 }
-                {
-                    const double ru = xs_float(rng);
-                    const V2 rsq = xs_vec2(rng);
-                    V3 w;
-                    const bool ok = bsdf_sample<FX>(sc, m, ho, wo, L, ru, rsq, w);
-                    sq.I(SI_BVALID, r) = ok ? 1 : 0;
-                    if (ok) {
-                        put_record(sq, SD_BO, r, spawn(ho, w), bsdf_f<FX>(sc, m, ho, wo, w, L),
-                                   bsdf_pdf<FX>(sc, m, ho, wo, w, L), shading_cosine(m, w, ho.ns));
-                        n_sh++;
-                    }
-                }
+                sq.HD(SH_UV, sp) = ho.uv.x;
+                sq.HD(SH_UV + 1, sp) = ho.uv.y;
+                sq.HI(SHI_MAT, sp) = ho.material;
+                sq.HI(SHI_BACK, sp) = ho.backface ? 1 : 0;
+                sq.HR(0, sp) = rng.hi;
+                sq.HR(1, sp) = rng.lo;
+                for (int k = 0; k < NEE_DRAWS * ns; ++k) xs_step(rng);
+                n_sh = (uint32_t)ns;  // the L records; k_nee_fold adds the valid B records
+            } else {
+                for (int i = 0; i < ns; ++i) n_sh += 1u + (nee_pair<FX>(sc, sq, (size_t)sp * ns + i, ho, m, wo, L, rng) ? 1u : 0u);
             }
             for (int k = 0; k < NS; ++k) {
                 sq.HD(SH_G + k, sp) = gathered.s[k];
@@ -312,9 +335,48 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc
     flush_counters(C, S.tcount + TC_N);
 }
 
+// n_shadow > 1: the NEE pairs of this bounce, one thread per pair (path p, light sample i), from the
+// header k_shade_q wrote; the path's RNG is stepped past the draws of pairs 0..i-1 (6 each), so
+// every pair draws exactly what the path's loop over i would have drawn.
+template <int FX>
+__global__ __launch_bounds__(BLOCK, LUMO_NEE_WAVES) void k_nee_gen(DScene sc, Paths S) {
+    const int ns = sc.n_shadow;
+    uint32_t bc[NB], count = 0;  // pairs per bucket
+    for (int b = 0; b < NB; ++b) {
+        bc[b] = S.counts[CNT_BUCKET0 + b] * (uint32_t)ns;
+        count += bc[b];
+    }
+    const ShadowQ sq = S.sq;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
+        uint32_t lj = j;
+        int bk = 0;
+        while (lj >= bc[bk]) lj -= bc[bk++];
+        const size_t r = (size_t)bk * sq.seg * ns + lj;
+        const uint32_t p = (uint32_t)(r / (size_t)ns);
+        const int i = (int)(r - (size_t)p * ns);
+        DHit ho;
+        ho.t = 0.0;
+        ho.p = V3{sq.HD(SH_P, p), sq.HD(SH_P + 1, p), sq.HD(SH_P + 2, p)};
+        ho.err = V3{sq.HD(SH_E, p), sq.HD(SH_E + 1, p), sq.HD(SH_E + 2, p)};
+        ho.ns = V3{sq.HD(SH_NS, p), sq.HD(SH_NS + 1, p), sq.HD(SH_NS + 2, p)};
+        ho.ng = V3{sq.HD(SH_NG, p), sq.HD(SH_NG + 1, p), sq.HD(SH_NG + 2, p)};
+        ho.uv = V2{sq.HD(SH_UV, p), sq.HD(SH_UV + 1, p)};
+        ho.material = sq.HI(SHI_MAT, p);
+        ho.backface = sq.HI(SHI_BACK, p) != 0;
+        const V3 wo{sq.HD(SH_WO, p), sq.HD(SH_WO + 1, p), sq.HD(SH_WO + 2, p)};
+        double L[NS];
+        for (int k = 0; k < NS; ++k) L[k] = sq.HD(SH_L + k, p);
+        Xorshift rng{sq.HR(0, p), sq.HR(1, p)};
+        for (int k = 0; k < NEE_DRAWS * i; ++k) xs_step(rng);
+        const lumo_material m = sc.mats[ho.material];
+        nee_pair<FX>(sc, sq, r, ho, m, wo, L, rng);
+    }
+}
+
 #ifdef LUMO_MAIN_TU
 // n_shadow > 1: radiance += (0 + gathered * single_0 + ... + gathered * single_{n-1}) / n_shadow
-// per path, in lumo's order (integrator.rs:74-85).
+// per path, in lumo's order (integrator.rs:74-85); the path's query count gains its valid B
+// records (k_nee_gen produced them after k_shade_q counted the L records).
 __global__ __launch_bounds__(BLOCK) void k_nee_fold(Paths S, QState nxt, int ns) {
     uint32_t bc[NB], count = 0;  // paths per bucket
     for (int b = 0; b < NB; ++b) {
@@ -329,12 +391,19 @@ __global__ __launch_bounds__(BLOCK) void k_nee_fold(Paths S, QState nxt, int ns)
         const uint32_t p = bk * Q.seg + lj;
         const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};
         DColor acc = cfill(0.0);
+        int32_t nb = 0;
         for (int i = 0; i < ns; ++i) {
             const size_t r = (size_t)p * ns + i;
             const DColor single{{Q.D(SD_LF, r), Q.D(SD_LF + 1, r), Q.D(SD_LF + 2, r), Q.D(SD_LF + 3, r)}};
             acc = acc + g * single;
+            nb += Q.I(SI_BVALID, r);
         }
         deliver_nee(S, Q, nxt, p, acc / (double)ns);
+        const int next = Q.HI(SHI_NEXT, p);
+        if (next >= 0)
+            nxt.I(QI_QUERIES, (size_t)next) += nb;
+        else
+            S.queries[Q.HI(SHI_SLOT, p)] += (uint32_t)nb;
     }
 }
 #endif  // LUMO_MAIN_TU

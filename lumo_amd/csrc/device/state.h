@@ -24,6 +24,12 @@ constexpr int BLOCK = 256;
 #ifndef LUMO_SHADE_WAVES  // k_shade_q: 2 waves/SIMD measured best (C3 shade 411 -> 337 ms, C1 neutral)
 #define LUMO_SHADE_WAVES 2
 #endif
+#ifndef LUMO_SHADE_WAVES_LEAN  // feature class 0 (Cornell): 171 -> <= 168 VGPRs buys a third wave
+#define LUMO_SHADE_WAVES_LEAN 3
+#endif
+#ifndef LUMO_NEE_WAVES
+#define LUMO_NEE_WAVES 3
+#endif
 #ifndef LUMO_BDPT_STEP_WAVES
 #define LUMO_BDPT_STEP_WAVES 1
 #endif
@@ -82,20 +88,25 @@ struct HitQ {
 enum { SD_LO = 0, SD_LD = 3, SD_LF = 6, SD_LPS = 10, SD_LCOS = 11, SD_BO = 12, SD_BD = 15, SD_BF = 18,
        SD_BPS = 22, SD_BCOS = 23, SD_PDFL = 24, SD_N = 25 };
 enum { SI_LIGHT = 0, SI_BVALID, SI_N };
-enum { SH_G = 0, SH_L = 4, SH_R = 8, SH_N = 12 };
-enum { SHI_SLOT = 0, SHI_NEXT, SHI_N };
+enum { SH_G = 0, SH_L = 4, SH_R = 8, SH_N1 = 12 };
+// n_shadow > 1: the NEE records are generated per pair by k_nee_gen, from the path's hit record
+// (point, error bounds, shading / geometric normals, wo, uv), material, face and RNG state.
+enum { SH_P = 12, SH_E = 15, SH_NS = 18, SH_NG = 21, SH_WO = 24, SH_UV = 27, SH_N = 29 };
+enum { SHI_SLOT = 0, SHI_NEXT, SHI_MAT, SHI_BACK, SHI_N };
 struct ShadowQ {
     double* d;   // SD_* planes, cap pairs
     int32_t* i;  // SI_* planes
     size_t cap;
-    double* hd;   // SH_* planes, hcap paths
-    int32_t* hi;  // SHI_* planes
+    double* hd;    // SH_* planes, hcap paths
+    int32_t* hi;   // SHI_* planes
+    uint64_t* hr;  // path RNG at the start of its NEE draws (hi, lo), n_shadow > 1
     size_t hcap;
     uint32_t seg;  // paths per bucket segment
     __device__ __forceinline__ double& D(int k, size_t r) const { return d[(size_t)k * cap + r]; }
     __device__ __forceinline__ int32_t& I(int k, size_t r) const { return i[(size_t)k * cap + r]; }
     __device__ __forceinline__ double& HD(int k, size_t p) const { return hd[(size_t)k * hcap + p]; }
     __device__ __forceinline__ int32_t& HI(int k, size_t p) const { return hi[(size_t)k * hcap + p]; }
+    __device__ __forceinline__ uint64_t& HR(int k, size_t p) const { return hr[(size_t)k * hcap + p]; }
 };
 
 // Per-slot state.  The path tracer keeps only the camera sampler state, the raster position and
