@@ -56,12 +56,18 @@ int lumo_builder_set_environment_texture(void* b, int texture, double scale);
 int lumo_builder_texture_solid(void* b, lumo_spectrum spec);
 int lumo_builder_texture_image(void* b, const char* png, size_t n);
 int lumo_builder_texture_hdr(void* b, const char* hdr, size_t n);
+/* An already decoded Image<Spectrum> (image.rs:7-16): width x height texel spectra, row-major from
+ * the image's top row as Image::buffer holds them, and its mean (Texture::power).  For callers
+ * that keep lumo's decoded images rather than the files. */
+int lumo_builder_texture_texels(void* b, int width, int height, const lumo_spectrum* texels, lumo_spectrum mean);
 int lumo_builder_texture_checkerboard(void* b, int even, int odd, double scale);
 int lumo_builder_texture_marble(void* b, uint64_t seed, lumo_spectrum spec);
 int lumo_builder_texture_mandelbrot(void* b);
 /* A bump map from a PNG file's bytes (Image::bump_from_file, image.rs:142-166); returns its
  * index or -1. */
 int lumo_builder_normal_map(void* b, const char* png, size_t n);
+/* An already decoded Image<Normal> bump map: width x height unit normals (xyz f64), row-major. */
+int lumo_builder_normal_map_texels(void* b, int width, int height, const double* normals);
 /* Copy of material `base` with textured slots: albedo (microfacet kd / Light texture), ks, tf
  * (texture indices, -1 keeps the solid spectrum) and a bump map (-1: none).  Returns the new
  * material index or -1. */

@@ -101,6 +101,17 @@ class Texture:
         return Texture("hdr", data=_read_source(source, ".hdr"))
 
     @staticmethod
+    def texels(width, height, spectra, mean):
+        """An already decoded Image<Spectrum>: width x height Spectra (row-major from the top row,
+        as Image::buffer) or an (N, 4) float32 array of (c0, c1, c2, scale), and the mean Spectrum."""
+        arr = np.ascontiguousarray(
+            [(x._s.c0, x._s.c1, x._s.c2, x._s.scale) for x in spectra] if not isinstance(spectra, np.ndarray)
+            else spectra, dtype=np.float32).reshape(-1, 4)
+        if len(arr) != width * height:
+            raise ValueError("texels: width * height spectra expected")
+        return Texture("texels", width=int(width), height=int(height), arr=arr, mean=mean)
+
+    @staticmethod
     def checkerboard(even, odd, scale):
         """Texture::Checkerboard(even, odd, scale): `even` where floor(u s) + floor(v s) is even."""
         return Texture("checkerboard", even=_as_texture(even), odd=_as_texture(odd), scale=float(scale))
@@ -128,6 +139,9 @@ class Texture:
             i = L.lumo_builder_texture_image(b, k["data"], len(k["data"]))
         elif self.kind == "hdr":
             i = L.lumo_builder_texture_hdr(b, k["data"], len(k["data"]))
+        elif self.kind == "texels":
+            i = L.lumo_builder_texture_texels(b, k["width"], k["height"],
+                                              k["arr"].ctypes.data_as(C.POINTER(_ffi.Spectrum)), k["mean"]._s)
         elif self.kind == "checkerboard":
             i = L.lumo_builder_texture_checkerboard(b, k["even"]._add(b, cache), k["odd"]._add(b, cache), k["scale"])
         elif self.kind == "marble":
@@ -144,11 +158,26 @@ class NormalMap:
     """A bump map, Image<Normal> (image.rs:142-166): n = normalize(rgb / 128 - 1) of a PNG."""
 
     def __init__(self, source):
-        self.data = _read_source(source, ".png")
+        self.data = _read_source(source, ".png") if source is not None else None
+        self.normals = None
+
+    @staticmethod
+    def from_normals(width, height, normals):
+        """An already decoded Image<Normal>: width x height unit normals (N, 3), row-major."""
+        nm = NormalMap(None)
+        nm.normals = np.ascontiguousarray(normals, dtype=np.float64).reshape(-1, 3)
+        if len(nm.normals) != width * height:
+            raise ValueError("normal map: width * height normals expected")
+        nm.size = (int(width), int(height))
+        return nm
 
     def _add(self, b, cache):
         if id(self) not in cache:
-            i = lib().lumo_builder_normal_map(b, self.data, len(self.data))
+            if self.normals is not None:
+                i = lib().lumo_builder_normal_map_texels(b, self.size[0], self.size[1],
+                                                         self.normals.ctypes.data_as(_ffi.c_double_p))
+            else:
+                i = lib().lumo_builder_normal_map(b, self.data, len(self.data))
             if i < 0:
                 raise ValueError("normal map: " + lib().lumo_builder_error(b).decode())
             cache[id(self)] = (self, i)

@@ -220,10 +220,12 @@ HOST_API = [
     ("lumo_builder_texture_solid", C.c_int, [C.c_void_p, Spectrum]),
     ("lumo_builder_texture_image", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
     ("lumo_builder_texture_hdr", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    ("lumo_builder_texture_texels", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(Spectrum), Spectrum]),
     ("lumo_builder_texture_checkerboard", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double]),
     ("lumo_builder_texture_marble", C.c_int, [C.c_void_p, C.c_uint64, Spectrum]),
     ("lumo_builder_texture_mandelbrot", C.c_int, [C.c_void_p]),
     ("lumo_builder_normal_map", C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    ("lumo_builder_normal_map_texels", C.c_int, [C.c_void_p, C.c_int, C.c_int, c_double_p]),
     ("lumo_builder_material_textured", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     ("lumo_builder_add_file", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t]),
     ("lumo_builder_set_map_ks", C.c_int, [C.c_void_p, C.c_int]),

@@ -157,6 +157,17 @@ int lumo_builder_texture_hdr(void* b, const char* hdr, size_t n) {
     if (!texture_from_hdr(reinterpret_cast<const uint8_t*>(hdr), n, t, sb->error)) return -1;
     return push_texture(sb, t);
 }
+int lumo_builder_texture_texels(void* b, int width, int height, const lumo_spectrum* texels, lumo_spectrum mean) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || width <= 0 || height <= 0 || !texels || (int64_t)width * height > (int64_t)INT32_MAX) return -1;
+    HostTexture t;
+    t.t.kind = LUMO_TEX_IMAGE;
+    t.t.width = width;
+    t.t.height = height;
+    t.t.spec = mean;
+    t.texels.assign(texels, texels + (size_t)width * height);
+    return push_texture(sb, t);
+}
 int lumo_builder_texture_checkerboard(void* b, int even, int odd, double scale) {
     SceneBuilder* sb = static_cast<SceneBuilder*>(b);
     // children must already exist: the texture graph stays acyclic (Box<Texture> in texture.rs:30)
@@ -190,6 +201,16 @@ int lumo_builder_normal_map(void* b, const char* png, size_t n) {
     if (!sb || !png) return -1;
     HostNormalMap m;
     if (!normal_map_from_png(reinterpret_cast<const uint8_t*>(png), n, m, sb->error)) return -1;
+    sb->normal_maps.push_back(std::move(m));
+    return (int)sb->normal_maps.size() - 1;
+}
+int lumo_builder_normal_map_texels(void* b, int width, int height, const double* normals) {
+    SceneBuilder* sb = static_cast<SceneBuilder*>(b);
+    if (!sb || width <= 0 || height <= 0 || !normals || (int64_t)width * height > (int64_t)INT32_MAX) return -1;
+    HostNormalMap m;
+    m.width = width;
+    m.height = height;
+    m.n.assign(normals, normals + 3 * (size_t)width * height);
     sb->normal_maps.push_back(std::move(m));
     return (int)sb->normal_maps.size() - 1;
 }

@@ -354,3 +354,41 @@ def test_oracle_renders_textured_obj_zip(tmp_path):
     cam = default_camera((16, 16))
     bufs, _, _ = O.render_tasks(d, cam.desc, L.make_tasks(16, 16, 4, 3), O.WAVEFRONT, 4)
     assert sum(float(b.reshape(-1, 4)[:, :3].sum()) for b in bufs) > 0.0
+
+
+def test_decoded_texels_match_the_file_decoders():
+    """lumo_builder_texture_texels / normal_map_texels (a binding that holds lumo's decoded
+    Image<Spectrum> / Image<Normal>) give the same tables, and the same oracle render, as the
+    PNG decoders."""
+    import oracle_ffi as O
+    from scenes import default_camera
+    rng = np.random.default_rng(21)
+    kd_png, _ = random_png(rng, 6, 4, 2, 8)
+    bump_png, _ = random_png(rng, 5, 3, 2, 8)
+
+    def scene(kd, bump):
+        return L.Scene.empty_box(L.Spectrum.from_srgb(242, 242, 242),
+                                 L.Material.microfacet(0.5, 1.5, 0.0, False, False, kd, L.Spectrum.from_rgb(1, 1, 1),
+                                                       L.Spectrum.black(), bump_map=bump),
+                                 L.Material.diffuse(L.Spectrum.from_rgb(0.5, 0.5, 0.5))).build()
+    a = scene(L.Texture.image(kd_png), L.NormalMap(bump_png))
+    da = a.desc()
+    tex, texels = _tables(da)
+    t = [x for x in tex if x["kind"] == _ffi.TEX_IMAGE][0]
+    arr = np.array([list(_spec_tuple(x)) for x in texels[t["first"]:t["first"] + 24]], dtype=np.float32)
+    mean = L.Spectrum(_ffi.Spectrum(*_spec_tuple(t["spec"])))
+    nm = np.ctypeslib.as_array(da.normal_maps, shape=(da.num_normal_maps,))[0]
+    normals = np.ctypeslib.as_array(da.normal_texels, shape=(da.num_normal_texels, 3))[nm["first"]:nm["first"] + 15]
+    b = scene(L.Texture.texels(6, 4, arr, mean), L.NormalMap.from_normals(5, 3, normals.copy()))
+    db = b.desc()
+    tb, texb = _tables(db)
+    tt = [x for x in tb if x["kind"] == _ffi.TEX_IMAGE][0]
+    assert _spec_tuple(tt["spec"]) == _spec_tuple(t["spec"])
+    assert [_spec_tuple(x) for x in texb[tt["first"]:tt["first"] + 24]] == \
+           [_spec_tuple(x) for x in texels[t["first"]:t["first"] + 24]]
+    cam = default_camera((16, 16))
+    tasks = L.make_tasks(16, 16, 4, 8)
+    ra, _, _ = O.render_tasks(da, cam.desc, tasks, O.WAVEFRONT, 4)
+    rb, _, _ = O.render_tasks(db, cam.desc, tasks, O.WAVEFRONT, 4)
+    for x, y in zip(ra, rb):
+        np.testing.assert_array_equal(x, y)
