@@ -14,7 +14,10 @@ With N ranks (one per GPU, launched by torch.distributed.run) the tasks are shar
 touches the data path; only the timing barriers and the final max/sum of scalars use the group.
 
 `value` is whole-job Mrays/s = (closest-hit + shadow-visibility queries of all ranks) / max-over-
-ranks wall time of the timed frames.  Also reported: Msamples/s (camera paths), lumo's own "total
+ranks wall time of the timed frames: lumo's Scene::hit / hit_light calls for the frame, including
+the shadow records the device answers without a traversal because their contribution is 0
+whatever the visibility (`shadow_resolved_per_step`; `mrays_traversed_per_s` excludes them).
+Also reported: Msamples/s (camera paths), lumo's own "total
 rays" rate (sum of path depths, task.rs:65), the roofline of the dominant kernel (algorithmic
 bytes from the kernels' own traversal counters over live HIP-event kernel time, DESIGN.md
 §Roofline), and the CPU baseline (the f64 oracle in lumo's tile-serial order on this host's
@@ -91,7 +94,8 @@ def main():
         if c3 is not None:
             out["c3"] = {k: c3[k] for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype",
                                             "data", "config", "msamples_per_s", "lumo_total_rays_per_s_M",
-                                            "queries_per_step", "scene_build_s", "sample_checks", "roofline",
+                                            "queries_per_step", "shadow_resolved_per_step",
+                                            "mrays_traversed_per_s", "scene_build_s", "sample_checks", "roofline",
                                             "cpu_baseline")}
         print(json.dumps(out))
     if pg is not None:
@@ -152,6 +156,7 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
     lib.lumo_set_timing(0)
     st = dev.stats()
     checks = [st.samples_nan, st.samples_neg, st.samples_large]
+    resolved = st.shadow_resolved
 
     if pg is not None:
         import torch
@@ -159,10 +164,10 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
         elapsed = float(t.item())
-        s = torch.tensor([q, cams, rays] + checks, dtype=torch.float64, device=dev_t)
+        s = torch.tensor([q, cams, rays, resolved] + checks, dtype=torch.float64, device=dev_t)
         pg.all_reduce(s, op=pg.ReduceOp.SUM)
-        q, cams, rays = (float(x) for x in s.tolist()[:3])
-        checks = [int(x) for x in s.tolist()[3:]]
+        q, cams, rays, resolved = (float(x) for x in s.tolist()[:4])
+        checks = [int(x) for x in s.tolist()[4:]]
     dev.close()
 
     out = None
@@ -196,6 +201,10 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
             "msamples_per_s": round(cams / elapsed / 1e6, 3),
             "lumo_total_rays_per_s_M": round(rays / elapsed / 1e6, 3),
             "queries_per_step": q / steps,
+            # of which shadow records answered without a traversal (their BSDF pdf is 0, so
+            # mis_sample returns 0 whatever the visibility, integrator.rs:146)
+            "shadow_resolved_per_step": resolved / steps,
+            "mrays_traversed_per_s": round((q - resolved) / elapsed / 1e6, 3),
             "scene_build_s": wl["scene_build_s"],
             # tone_mapping.rs:42-56 debug checks over the timed camera samples: NaN, negative, > 1000
             "sample_checks": {"nan": checks[0], "negative": checks[1], "large": checks[2]},
@@ -263,7 +272,10 @@ def roofline(st, n_shadow, bdpt=False, workload="c1"):
     ms = list(st.kernel_ms)
     launches = list(st.launches)
     per_stage = {STAGES[i]: {"ms": round(ms[i], 3), "launches": int(launches[i])} for i in range(len(STAGES))}
-    cq, sq = max(st.closest_queries, 1), max(st.shadow_queries, 1)
+    cq = max(st.closest_queries, 1)
+    # shadow records resolved without traversal (p_sct == 0) read only their pdf
+    traversed = st.shadow_queries - st.shadow_resolved
+    sq = max(traversed, 1)
     closest_bytes = (st.closest_queries * B_CLOSEST_IO + st.aabb_tests[0] * B_AABB + st.kd_nodes[0] * B_KD +
                      st.tri_tests[0] * B_TRI)
     trav1 = st.aabb_tests[1] * B_AABB + st.kd_nodes[1] * B_KD + st.tri_tests[1] * B_TRI
@@ -276,7 +288,7 @@ def roofline(st, n_shadow, bdpt=False, workload="c1"):
     else:
         b_io = B_RECORD + B_FOLD / (2 * n_shadow)
         cands = {"k_closest": (ms[1], launches[1], closest_bytes),
-                 "k_shadow": (ms[3], launches[3], st.shadow_queries * b_io + trav1)}
+                 "k_shadow": (ms[3], launches[3], traversed * b_io + st.shadow_resolved * 8 + trav1)}
     # the dominant kernel of the step: the longest of all timed stages; if that is not a
     # traversal kernel, the roofline is still reported for the longest traversal kernel
     dom_stage = STAGES[max(range(len(STAGES)), key=lambda i: ms[i])]

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define LUMO_ABI_VERSION 4
+#define LUMO_ABI_VERSION 5
 
 typedef int32_t lumo_status;
 enum {
@@ -302,6 +302,10 @@ typedef struct {
     uint64_t closest_queries, shadow_queries, bounces;
     uint64_t aabb_tests[2], kd_nodes[2], tri_tests[2];
     uint64_t samples_nan, samples_neg, samples_large;
+    /* shadow queries (included in shadow_queries) whose contribution is zero whatever the
+     * visibility: the record's BSDF pdf is 0, so mis_sample returns 0 before using the hit
+     * (integrator.rs:146); the device answers them without traversing the scene. */
+    uint64_t shadow_resolved;
 } lumo_stats;
 
 /* Per-path dump of one task (test hook for per-path parity): arrays sized samples x pixels

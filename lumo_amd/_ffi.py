@@ -8,6 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+ABI_VERSION = 5  # include/lumo_amd.h LUMO_ABI_VERSION
 LIB_PATH = os.environ.get("LUMO_AMD_LIB") or os.path.join(_HERE, "liblumo_amd.so")
 
 c_double_p = C.POINTER(C.c_double)
@@ -155,7 +156,8 @@ class Stats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double * STAGE_COUNT), ("launches", C.c_uint64 * STAGE_COUNT),
                 ("closest_queries", C.c_uint64), ("shadow_queries", C.c_uint64), ("bounces", C.c_uint64),
                 ("aabb_tests", C.c_uint64 * 2), ("kd_nodes", C.c_uint64 * 2), ("tri_tests", C.c_uint64 * 2),
-                ("samples_nan", C.c_uint64), ("samples_neg", C.c_uint64), ("samples_large", C.c_uint64)]
+                ("samples_nan", C.c_uint64), ("samples_neg", C.c_uint64), ("samples_large", C.c_uint64),
+                ("shadow_resolved", C.c_uint64)]
 
 
 class CameraParams(C.Structure):
@@ -263,6 +265,8 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.lumo_abi_version() != ABI_VERSION:  # a stale build: struct layouts would not match
+        raise OSError(f"lumo_amd: {p} has ABI version {lib.lumo_abi_version()}, expected {ABI_VERSION}; rebuild")
     if path is None:
         _lib = lib
     return lib

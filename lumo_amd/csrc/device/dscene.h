@@ -111,6 +111,7 @@ __device__ __forceinline__ DScene stage_scene_lds(const DScene& sc, char* lds) {
 
 struct Counters {
     uint32_t aabb, kd, tri;
+    uint32_t resolved;  // k_shadow_q: records answered without traversal (LUMO_SKIP_DEAD)
 };
 
 struct Ray {

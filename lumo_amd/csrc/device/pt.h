@@ -259,6 +259,14 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
 template <int STK, int FX>
 __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const ShadowQ& Q, int b, size_t r, bool li_mode,
                                                   uint32_t p, Counters& C) {
+#if LUMO_SKIP_DEAD
+    // integrator.rs:146: mis_sample returns 0 when p_sct == 0, before the hit is used, so the
+    // record contributes 0 whether or not the light is visible: no traversal.
+    if (Q.D(b + 10, r) == 0.0) {
+        C.resolved++;
+        return cfill(0.0);
+    }
+#endif
     const RayX ri = rayx(Ray{V3{Q.D(b, r), Q.D(b + 1, r), Q.D(b + 2, r)}, V3{Q.D(b + 3, r), Q.D(b + 4, r), Q.D(b + 5, r)}});
     const int li = Q.I(SI_LIGHT, r);
     DHit hi;
@@ -333,6 +341,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc
         }
     }
     flush_counters(C, S.tcount + TC_N);
+    if (LUMO_SKIP_DEAD) flush_resolved(C.resolved, S.tcount + TC_RESOLVED);
 }
 
 // n_shadow > 1: the NEE pairs of this bounce, one thread per pair (path p, light sample i), from the

@@ -30,8 +30,11 @@ constexpr int BLOCK = 256;
 #ifndef LUMO_NEE_WAVES
 #define LUMO_NEE_WAVES 3
 #endif
-#ifndef LUMO_BDPT_STEP_WAVES
-#define LUMO_BDPT_STEP_WAVES 1
+#ifndef LUMO_SKIP_DEAD  // shadow records with p_sct == 0 answered without traversal (C3 shadow -16 %)
+#define LUMO_SKIP_DEAD 1
+#endif
+#ifndef LUMO_BDPT_STEP_WAVES  // k_bdpt_step: 2 waves measured best (C4 step 187 -> 153 ms)
+#define LUMO_BDPT_STEP_WAVES 2
 #endif
 constexpr uint64_t SAMPLES_INCREMENT = 256;
 constexpr int RR_DEPTH = 5;
@@ -51,6 +54,8 @@ enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_BUCKET0, CNT_N = CNT_
 // (LUMO_BUCKETS=0: one bucket).  k_shadow_q walks the buckets in order.
 constexpr int NB = 8;
 enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
+constexpr int TC_RESOLVED = 2 * TC_N;  // + shadow records answered without traversal; W_TCOUNT has TC_ALL
+constexpr int TC_ALL = 2 * TC_N + 1;
 
 struct DCam {
     Xform wtc, sctr, cts;
@@ -127,7 +132,7 @@ struct Paths {
     double* film;
     int32_t *q0, *q1;  // BDPT walk queues (slot ids)
     uint32_t* counts;
-    unsigned long long* tcount;  // [2][TC_N]
+    unsigned long long* tcount;  // [2][TC_N] + resolved shadow records
     unsigned long long* checks;  // sample checks: NaN, negative, large (tone_mapping.rs:42-56)
     // path tracer: queue-order state (ping-pong by bounce parity), hits, NEE records
     QState qs[2];
@@ -233,6 +238,11 @@ __device__ __forceinline__ void flush_counters(const Counters& C, unsigned long 
         if (k) atomicAdd(dst + TC_KD, k);
         if (t) atomicAdd(dst + TC_TRI, t);
     }
+}
+__device__ __forceinline__ void flush_resolved(uint32_t n, unsigned long long* dst) {
+    unsigned long long a = n;
+    for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off);
+    if (lane_id() == 0 && a) atomicAdd(dst, a);
 }
 
 __device__ __forceinline__ V3 ldv3(const double* p, int i) { return V3{p[3 * i], p[3 * i + 1], p[3 * i + 2]}; }
