@@ -13,6 +13,10 @@
 #include "../common/rng.h"
 #include "../common/vec.h"
 
+#ifndef LUMO_WHILE_WHILE  // traversal loops as while-while (bvh_traverse, kd_traverse)
+#define LUMO_WHILE_WHILE 1
+#endif
+
 namespace lumo {
 namespace dev {
 
@@ -509,7 +513,35 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob,
     const double t_end0 = t_end;
     for (;;) {
         if (t_hit < t_start) break;
-        const DKd node = sc.kdp[curr];
+        DKd node = sc.kdp[curr];
+#if LUMO_WHILE_WHILE
+        // while-while (Aila & Laine 2009): descend interior nodes until this lane is at a leaf
+        // before any lane tests triangles, so the leaves of a wave's lanes are processed together.
+        // t_start and t_hit change only at a leaf or a pop, so the check above still runs before
+        // every node lumo checks it at; each lane's own node / triangle sequence is lumo's.
+        while ((node.meta & 3) != 3) {
+            C.kd++;
+            const int ax = node.meta & 3;
+            const double point = node.u.point;
+            const int right = node.meta >> 2;
+            const double t_split = (point - origin[ax]) * inv_dir[ax];
+            const bool left_first = origin[ax] < point || (origin[ax] == point && inv_dir[ax] <= 0.0);
+            const int first = left_first ? node.left : right;
+            const int second = left_first ? right : node.left;
+            if (t_split > t_end || t_split <= 0.0) {
+                curr = first;
+            } else if (t_split < t_start) {
+                curr = second;
+            } else {
+                curr = first;
+                st_node[sp] = second;
+                st_ts[sp] = t_split;
+                t_end = t_split;
+                sp++;
+            }
+            node = sc.kdp[curr];
+        }
+#endif
         const int axis = node.meta & 3;
         if (axis == 3) {
             const int first = node.u.leaf.first, count = node.u.leaf.count;
@@ -748,6 +780,33 @@ __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, co
     const V3 inv_dir = r.inv;
     int curr = 0, idx = -1;
     double tt = t_max;
+#if LUMO_WHILE_WHILE
+    // while-while (Aila & Laine 2009): every lane first advances to its next leaf whose box
+    // passes (tt changes only in a leaf), then the lanes' object tests (kd traversals) run
+    // together instead of one lane's at a time.  Each lane's node / object sequence is lumo's.
+    for (;;) {
+        int count = 0;
+        while (curr >= 0) {
+            const DBvh& node = nodes[curr];
+            double ts, te;
+            C.aabb++;
+            slab(node.bmin, node.bmax, r.o, inv_dir, ts, te);
+            ts = rmax(ts, t_min);
+            te = rmin(te, tt);
+            if (ts <= te) {
+                count = node.count;
+                if (count == 0) {
+                    curr += 1;
+                    continue;
+                }
+                break;
+            }
+            curr = node.escape;
+        }
+        if (curr < 0) break;
+        const DBvh& node = nodes[curr];
+        {
+#else
     while (curr >= 0) {
         const DBvh& node = nodes[curr];
         double ts, te;
@@ -761,6 +820,7 @@ __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, co
                 curr += 1;
                 continue;
             }
+#endif
             for (int k = 0; k < count; ++k) {
                 const int i = items[node.first + k];
                 const double t = object_hit_t<STK, FX>(sc, objs[i], r, t_min, tt, C);

@@ -770,7 +770,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     S.p_valid = wbuf<uint32_t>(c, W_P_VALID, N, st);
     S.film = wbuf<double>(c, W_FILM, 4 * (size_t)N, st);
     S.counts = wbuf<uint32_t>(c, W_COUNTS, CNT_N, st);
-    S.tcount = wbuf<unsigned long long>(c, W_TCOUNT, TC_ALL, st);
+    S.tcount = wbuf<unsigned long long>(c, W_TCOUNT, TC_ALL + TC_STATS, st);
     S.checks = wbuf<unsigned long long>(c, W_CHECKS, 3, st);
     Tasks T{};
     T.t = wbuf<lumo_tile_task>(c, W_TASKS, n_tasks, st);
@@ -866,7 +866,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     HIPCHK(hipMemsetAsync(T.num_rays, 0, sizeof(unsigned long long) * n_tasks, sm));
     HIPCHK(hipMemsetAsync(T.queries, 0, sizeof(unsigned long long) * n_tasks, sm));
     HIPCHK(hipMemsetAsync(S.film, 0, sizeof(double) * 4 * N, sm));
-    HIPCHK(hipMemsetAsync(S.tcount, 0, sizeof(unsigned long long) * TC_ALL, sm));
+    HIPCHK(hipMemsetAsync(S.tcount, 0, sizeof(unsigned long long) * (TC_ALL + TC_STATS), sm));
     HIPCHK(hipMemsetAsync(S.checks, 0, sizeof(unsigned long long) * 3, sm));
 
     const int gT = ceil_div(n_tasks, BLOCK), gN = ceil_div(N, BLOCK);
@@ -1203,6 +1203,15 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         c.stats.tri_tests[k] += tc[k * TC_N + TC_TRI];
     }
     c.stats.shadow_resolved += tc[TC_RESOLVED];
+#if LUMO_SHADOW_STATS
+    {
+        unsigned long long ss[TC_STATS];
+        HIPCHK(hipMemcpy(ss, S.tcount + TC_ALL, sizeof(ss), hipMemcpyDeviceToHost));
+        fprintf(stderr, "LUMO_SHADOW_STATS");
+        for (int k = 0; k < TC_STATS; ++k) fprintf(stderr, " %llu", ss[k]);
+        fprintf(stderr, "\n");
+    }
+#endif
     return splat_oom ? LUMO_ERR_OOM : LUMO_OK;
 }
 
@@ -1677,13 +1686,13 @@ lumo_status lumo_trace(void* ctx, const lumo_ray_soa* rays, size_t n, lumo_hit_s
     int32_t* kind = wbuf<int32_t>(*c, W_HIT_KIND, n, st);
     int32_t* obj = wbuf<int32_t>(*c, W_HIT_OBJ, n, st);
     int32_t* prim = wbuf<int32_t>(*c, W_HIT_TRI, n, st);
-    unsigned long long* tc = wbuf<unsigned long long>(*c, W_TCOUNT, TC_ALL, st);
+    unsigned long long* tc = wbuf<unsigned long long>(*c, W_TCOUNT, TC_ALL + TC_STATS, st);
     if (st) return st;
     hipStream_t sm = c->stream;
     HIPCHK(hipMemcpyAsync(o, rays->origin, sizeof(double) * 3 * n, hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemcpyAsync(d, rays->dir, sizeof(double) * 3 * n, hipMemcpyHostToDevice, sm));
     if (any_hit) HIPCHK(hipMemcpyAsync(light, rays->light, sizeof(int32_t) * n, hipMemcpyHostToDevice, sm));
-    HIPCHK(hipMemsetAsync(tc, 0, sizeof(unsigned long long) * TC_ALL, sm));
+    HIPCHK(hipMemsetAsync(tc, 0, sizeof(unsigned long long) * (TC_ALL + TC_STATS), sm));
     by_stack_class(c->sc.stack_class, [&](auto K) {
         launch_trace<decltype(K)::value>(ceil_div(n, BLOCK), sm, c->sc, o, d, light, (int)n, any_hit, t, kind, obj, prim, tc);
     });

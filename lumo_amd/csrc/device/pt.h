@@ -258,7 +258,7 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
 // the traversal.
 template <int STK, int FX>
 __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const ShadowQ& Q, int b, size_t r, bool li_mode,
-                                                  uint32_t p, Counters& C) {
+                                                  uint32_t p, Counters& C, bool* visible = nullptr) {
 #if LUMO_SKIP_DEAD
     // integrator.rs:146: mis_sample returns 0 when p_sct == 0, before the hit is used, so the
     // record contributes 0 whether or not the light is visible: no traversal.
@@ -272,6 +272,7 @@ __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const Shadow
     DHit hi;
     DColor out = cfill(0.0);
     if (scene_hit_light<STK, FX>(sc, ri, li, hi, C)) {
+        if (visible) *visible = true;
         const lumo_object& Lo = sc.lights[li];
         const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
         const double p_sct = Q.D(b + 10, r);
@@ -330,8 +331,44 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc
         }
         const size_t r = (size_t)bk * Q.seg * ns + lj;  // pair index
         const uint32_t p = (uint32_t)(NS1 ? r : r / (size_t)ns);
+#if LUMO_SHADOW_STATS
+        // diagnostics build: per-record traversal cost (AABB + kd + triangle steps) by class
+        // (record L/B x environment light x light missed / occluded / visible), cost histogram
+        // (log2 bins) and the pair loop's lane efficiency (sum of lane costs / 64 x wave max)
+        uint32_t pc = 0;
+        DColor a, b = cfill(0.0);
+        for (int rec = 0; rec < 2; ++rec) {
+            if (rec == 1 && !Q.I(SI_BVALID, r)) break;
+            const uint32_t c0 = C.aabb + C.kd + C.tri, a0 = C.aabb;
+            bool vis = false;
+            const DColor x = shadow_record_q<STK, FX>(sc, Q, rec ? SD_BO : SD_LO, r, rec == 0, p, C, &vis);
+            if (rec) b = x; else a = x;
+            const uint32_t cost = C.aabb + C.kd + C.tri - c0;
+            pc += cost;
+            const int env = sc.lights[Q.I(SI_LIGHT, r)].type == LUMO_OBJ_SPHERE;
+            const int outc = vis ? 2 : (C.aabb == a0 ? 0 : 1);
+            unsigned long long* st = S.tcount + TC_ALL + 18 * (rec * 6 + env * 3 + outc);
+            atomicAdd(st, 1ull);
+            atomicAdd(st + 1, (unsigned long long)cost);
+            const int bin = 31 - __builtin_clz(cost | 1u);
+            atomicAdd(st + 2 + (bin > 15 ? 15 : bin), 1ull);
+        }
+        {
+            unsigned long long sum = pc, mx = pc;
+            for (int off = 32; off > 0; off >>= 1) {
+                sum += __shfl_xor(sum, off);
+                const unsigned long long o = __shfl_xor(mx, off);
+                mx = o > mx ? o : mx;
+            }
+            if (lane_id() == 0) {
+                atomicAdd(S.tcount + TC_ALL + 216, sum);
+                atomicAdd(S.tcount + TC_ALL + 217, 64ull * mx);
+            }
+        }
+#else
         const DColor a = shadow_record_q<STK, FX>(sc, Q, SD_LO, r, true, p, C);
         const DColor b = Q.I(SI_BVALID, r) ? shadow_record_q<STK, FX>(sc, Q, SD_BO, r, false, p, C) : cfill(0.0);
+#endif
         const DColor single = (cfill(0.0) + a + b) / Q.D(SD_PDFL, r);
         if (NS1) {
             const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};

@@ -56,6 +56,10 @@ constexpr int NB = 8;
 enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
 constexpr int TC_RESOLVED = 2 * TC_N;  // + shadow records answered without traversal; W_TCOUNT has TC_ALL
 constexpr int TC_ALL = 2 * TC_N + 1;
+#ifndef LUMO_SHADOW_STATS
+#define LUMO_SHADOW_STATS 0
+#endif
+constexpr int TC_STATS = LUMO_SHADOW_STATS ? 218 : 0;  // diagnostics build: k_shadow_q cost classes
 
 struct DCam {
     Xform wtc, sctr, cts;
