@@ -369,6 +369,14 @@ lumo_status lumo_debug_stream(void* ctx, size_t n);
 /* Perf switch: stage the packed scene in LDS inside the traversal kernels (default on; also
  * LUMO_LDS=0 in the environment). */
 void lumo_set_lds_staging(int on);
+/* Perf switch (path tracer, one light sample per bounce).  fused = 0: each bounce is three
+ * kernels (closest hit / shading / visibility); fused = 1: one kernel (closest hit + shading +
+ * the NEE pair traced from registers); fused = -1 (default): fused when the scene is staged in
+ * LDS (small scenes), else three kernels.  Every bounce is preceded by a tail kernel that takes
+ * it instead when fewer than tail_below paths are alive and runs each of them to its end in that
+ * launch (tail_below = 0: never; default 262144).  Every mode gives bit-identical paths.  Also
+ * LUMO_FUSED / LUMO_TAIL in the environment. */
+void lumo_set_bounce_mode(int fused, uint32_t tail_below);
 
 #ifdef __cplusplus
 }

@@ -22,13 +22,13 @@ void launch_closest(const TravLaunch& l, const DScene& sc, const Paths& S, const
 }
 
 template <int STK>
-void launch_closest_q(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& cur) {
+void launch_closest_q(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& cur, uint32_t skip_below) {
     if (l.lds) {
-        if (l.fx) k_closest_q<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, cur);
-        else k_closest_q<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, cur);
+        if (l.fx) k_closest_q<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, cur, skip_below);
+        else k_closest_q<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, cur, skip_below);
     } else {
-        if (l.fx) k_closest_q<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, cur);
-        else k_closest_q<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, cur);
+        if (l.fx) k_closest_q<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, cur, skip_below);
+        else k_closest_q<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, cur, skip_below);
     }
 }
 
@@ -54,6 +54,27 @@ void launch_shadow_q(const TravLaunch& l, const DScene& sc, const Paths& S, cons
 }
 
 template <int STK>
+void launch_bounce_q(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const QState& cur,
+                     const QState& nxt, uint32_t tail_below, bool tail_only) {
+    auto go = [&](auto TL) {
+        constexpr bool TAIL = decltype(TL)::value;
+        if (l.fx == 2) {  // textured scenes: no LDS staging variant (as k_shadow_q)
+            k_bounce_q<STK, false, 2, TAIL><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, T, cur, nxt, tail_below);
+        } else if (l.lds) {
+            if (l.fx) k_bounce_q<STK, true, 1, TAIL><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, T, cur, nxt, tail_below);
+            else k_bounce_q<STK, true, 0, TAIL><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, T, cur, nxt, tail_below);
+        } else {
+            if (l.fx) k_bounce_q<STK, false, 1, TAIL><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, T, cur, nxt, tail_below);
+            else k_bounce_q<STK, false, 0, TAIL><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, T, cur, nxt, tail_below);
+        }
+    };
+    if (tail_only)
+        go(std::true_type{});
+    else
+        go(std::false_type{});
+}
+
+template <int STK>
 void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, const double* d, const int32_t* light,
                   int n, int any_hit, double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
                   unsigned long long* tcount) {
@@ -61,8 +82,10 @@ void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, c
 }
 
 template void launch_closest<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const int32_t*);
-template void launch_closest_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const QState&);
+template void launch_closest_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const QState&, uint32_t);
 template void launch_shadow_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const QState&);
+template void launch_bounce_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Tasks&, const QState&,
+                                        const QState&, uint32_t, bool);
 template void launch_trace<LUMO_STK>(int, hipStream_t, const DScene&, const double*, const double*, const int32_t*,
                                      int, int, double*, int32_t*, int32_t*, int32_t*, unsigned long long*);
 

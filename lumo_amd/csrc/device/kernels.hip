@@ -674,6 +674,9 @@ void by_stack_class(int cls, F&& f) {
 // grid-stride loop) so each workgroup copies the packed scene once per launch.
 bool g_lds = true;
 int g_buckets = NB;  // LUMO_BUCKETS=0: NEE records not grouped by origin object
+int g_fused = -1;  // n_shadow == 1: k_bounce_q instead of closest / shade / shadow (-1: when the scene is LDS-staged)
+uint32_t g_tail_below = 1u << 18;  // n_shadow == 1: k_bounce_q tail mode below this many live paths
+int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
 template <typename F>
 void launch_trav(Ctx& c, uint64_t count, F&& f) {
     const bool lds = g_lds && c.sc.hot_bytes > 0;
@@ -940,9 +943,28 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             bst = bounce_loop([&](uint32_t ub, int b, int32_t*, int32_t*) {
                 const QState& cur = S.qs[b & 1];
                 const QState& nxt = S.qs[(b + 1) & 1];
+                // n_shadow == 1: the tail kernel takes the bounce when fewer than g_tail_below paths
+                // are alive (decided on the device from the exact count); the bounce kernels skip it
+                const uint32_t skip = ns == 1 ? g_tail_below : 0u;
+                if (skip > 0) {
+                    StageTimer tm(c, g_timing, ST_RESOLVE);
+                    launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
+                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true);
+                    });
+                }
+                const bool fused = g_fused < 0 ? (g_lds && c.sc.hot_bytes > 0) : g_fused != 0;
+                if (ns == 1 && fused) {  // one fused kernel per bounce (pt.h k_bounce_q)
+                    StageTimer tm(c, g_timing, ST_CLOSEST);
+                    launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
+                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, false);
+                    });
+                    return;
+                }
                 {
                     StageTimer tm(c, g_timing, ST_CLOSEST);
-                    launch_trav(c, ub, [&](auto K, const TravLaunch& l) { launch_closest_q<decltype(K)::value>(l, c.sc, S, cur); });
+                    launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
+                        launch_closest_q<decltype(K)::value>(l, c.sc, S, cur, skip);
+                    });
                 }
                 {
                     StageTimer tm(c, g_timing, ST_SHADE);
@@ -950,21 +972,21 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                     if (ns > 1) {  // NEE pairs by k_nee_gen, one thread per pair
                         const int gp = std::min(ceil_div((uint64_t)ub * (uint32_t)ns, BLOCK), 1 << 16);
                         if (c.sc.full == 2) {
-                            k_shade_q<2, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                            k_shade_q<2, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
                             k_nee_gen<2><<<gp, BLOCK, 0, sm>>>(c.sc, S);
                         } else if (c.sc.full) {
-                            k_shade_q<1, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                            k_shade_q<1, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
                             k_nee_gen<1><<<gp, BLOCK, 0, sm>>>(c.sc, S);
                         } else {
-                            k_shade_q<0, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                            k_shade_q<0, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
                             k_nee_gen<0><<<gp, BLOCK, 0, sm>>>(c.sc, S);
                         }
                     } else if (c.sc.full == 2) {
-                        k_shade_q<2, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                        k_shade_q<2, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
                     } else if (c.sc.full) {
-                        k_shade_q<1, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                        k_shade_q<1, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
                     } else {
-                        k_shade_q<0, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets);
+                        k_shade_q<0, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
                     }
                 }
                 {
@@ -1189,8 +1211,10 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         for (size_t i = 0; i < n_tasks; ++i) total_q += queries[i];
         // per-slot query counters: PT 1 per closest + 1 per valid record; BDPT walk traces (the
         // bounce snapshots) + connection / re-run queries
-        shadow_q = total_q >= closest_q ? total_q - closest_q : 0;
+        const unsigned long long all_closest = closest_q + tc[TC_TAILQ];
+        shadow_q = total_q >= all_closest ? total_q - all_closest : 0;
     }
+    closest_q += tc[TC_TAILQ];  // k_bounce_q tail mode: the bounces past its first
     c.stats.closest_queries += closest_q;
     c.stats.shadow_queries += shadow_q;
     c.stats.bounces += bounces;
@@ -1270,6 +1294,9 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_LDS")) g_lds = e[0] != '0';
     if (const char* e = std::getenv("LUMO_BUCKETS")) g_buckets = e[0] == '0' ? 1 : NB;
     if (const char* e = std::getenv("LUMO_LDS_GRID")) c->lds_grid_cap = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("LUMO_FUSED")) g_fused = std::atoi(e);
+    if (const char* e = std::getenv("LUMO_QSORT")) g_qsort = std::atoi(e) & 3;
+    if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
     const char* tm = std::getenv("LUMO_TIMING");
     g_timing = tm && tm[0] == '1';
     *ctx_out = c;
@@ -1748,6 +1775,10 @@ lumo_status lumo_debug_stream(void* ctx, size_t n) {
 
 void lumo_set_timing(int on) { g_timing = on != 0; }
 void lumo_set_lds_staging(int on) { g_lds = on != 0; }
+void lumo_set_bounce_mode(int fused, uint32_t tail_below) {
+    g_fused = fused < 0 ? -1 : (fused != 0 ? 1 : 0);
+    g_tail_below = tail_below;
+}
 
 lumo_status lumo_stats_reset(void* ctx) {
     Ctx* c = static_cast<Ctx*>(ctx);

@@ -52,9 +52,11 @@ __device__ __forceinline__ void qc(const QState& Q, int k, size_t q, const DColo
 
 // Scene::hit (scene.rs:119-147) of every queued ray.
 template <int STK, bool LDS, int FX>
-__global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest_q(DScene sc0, Paths S, QState cur) {
+__global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest_q(DScene sc0, Paths S, QState cur,
+                                                                         uint32_t skip_below) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
+    if (count < skip_below) return;                // k_bounce_q<TAIL> ran this bounce's paths to their end
     if (count <= blockIdx.x * blockDim.x) return;  // before staging: whole block idle
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     const HitQ hq = S.hq;
@@ -122,8 +124,9 @@ constexpr int NEE_DRAWS = 6;  // RNG draws per pair in nee_pair
 // generates the pairs, one thread each; this kernel steps its RNG past their draws.
 template <int FX, bool SPLIT>
 __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE_WAVES) void k_shade_q(DScene sc, Paths S, Tasks T, QState cur, QState nxt,
-                                                                      int buckets) {
+                                                                      int buckets, uint32_t skip_below, int qsort) {
     const uint32_t count = S.counts[CNT_CUR];
+    if (count < skip_below) return;  // k_bounce_q<TAIL> ran this bounce's paths to their end
     const int ns = sc.n_shadow;
     const HitQ hq = S.hq;
     const ShadowQ sq = S.sq;
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
         const uint32_t q = base + threadIdx.x;
         const bool live = q < count;
-        int slot = 0, task = 0, key = 0;
+        int slot = 0, task = 0, key = 0, origin = 0;
         uint32_t depth = 0, flags = 0, queries = 0;
         double L[NS] = {0.0, 0.0, 0.0, 0.0};
         DColor gathered = cfill(0.0), radiance = cfill(0.0);
@@ -166,10 +169,8 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
                     if (flags & QF_SPECULAR) radiance = radiance + gathered * emit<FX>(sc, m, L, ho.backface, ho.uv);
                 } else {
                     resolve = !mat_is_delta<FX>(sc, m, L);
-                    if (resolve && buckets > 1) {  // origin object of the shadow rays (objects, then lights)
-                        const int k = kind == 2 ? sc.n_objs + hr.obj : hr.obj;
-                        key = k % NB;
-                    }
+                    origin = kind == 2 ? sc.n_objs + hr.obj : hr.obj;  // objects, then lights
+                    if (resolve && buckets > 1) key = origin % NB;    // bucket of the shadow rays
                 }
             }
         }
@@ -224,7 +225,16 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
                 alive = cont;
             }
         }
-        const uint32_t np = block_slot(alive, S.counts + CNT_NEXT);
+        // next ray queue: grouped within the block by origin object and / or direction octant
+        // (qsort 1 / 2 / 3; 0: lane order), see block_slot_sorted
+        uint32_t np;
+        if (qsort) {
+            const int oct = (rn.d.x < 0.0 ? 1 : 0) | (rn.d.y < 0.0 ? 2 : 0) | (rn.d.z < 0.0 ? 4 : 0);
+            const int ck = qsort == 1 ? (origin & 63) : (qsort == 2 ? oct : ((origin & 7) << 3 | oct));
+            np = block_slot_sorted<64>(alive, ck, S.counts + CNT_NEXT);
+        } else {
+            np = block_slot(alive, S.counts + CNT_NEXT);
+        }
         if (alive) {
             qv3(nxt, QD_O, np, rn.o);
             qv3(nxt, QD_D, np, rn.d);
@@ -453,6 +463,325 @@ __global__ __launch_bounds__(BLOCK) void k_nee_fold(Paths S, QState nxt, int ns)
     }
 }
 #endif  // LUMO_MAIN_TU
+
+// ------------------------------------------------------------------ fused bounce (n_shadow == 1)
+// With one light sample per bounce (the Cornell box) the three bounce kernels are fused into
+// k_bounce_q: each thread takes its queued path through the closest hit, the shading, and the
+// NEE pair traced at once from registers, so neither the closest hits nor the NEE records go
+// through HBM, and a bounce is one launch instead of three.  Every per-path operation is the
+// one k_closest_q / k_shade_q / k_shadow_q perform, in the same order, so each path's values
+// are bit for bit those of the three-kernel bounce (tests/test_gpu_parity.py runs both).
+//
+// Tail mode: once fewer than `tail_below` paths are alive (after Russian roulette starts, a pass
+// keeps ~10 bounces of a few thousand paths each, each bounce a few latency-bound launches), a
+// thread runs its path to the end inside one launch; per-path results do not depend on the
+// other paths, so they are unchanged.
+
+// One NEE record (integrator.rs:100-137) held in registers: spawned ray, bsdf_f, bsdf_pdf and
+// the shading cosine towards its direction.
+struct NeeRec {
+    Ray ray;
+    DColor f;
+    double pdf, cosv;
+};
+template <int FX>
+__device__ __forceinline__ NeeRec nee_record(const DScene& sc, const lumo_material& m, const DHit& ho, V3 wo, V3 w,
+                                             const double* L) {
+    return NeeRec{spawn(ho, w), bsdf_f<FX>(sc, m, ho, wo, w, L), bsdf_pdf<FX>(sc, m, ho, wo, w, L),
+                  shading_cosine(m, w, ho.ns)};
+}
+
+// shadow_record_q on a record held in registers (Scene::hit_light + mis_sample,
+// integrator.rs:100-184); L is the path's wavelengths after the pair was generated.
+template <int STK, int FX>
+__device__ __forceinline__ DColor shadow_record_r(const DScene& sc, const NeeRec& R, int li, bool li_mode,
+                                                  const double* L, Counters& C) {
+#if LUMO_SKIP_DEAD
+    if (R.pdf == 0.0) {  // integrator.rs:146: p_sct == 0 contributes 0 whatever the visibility
+        C.resolved++;
+        return cfill(0.0);
+    }
+#endif
+    const RayX ri = rayx(R.ray);
+    DHit hi;
+    DColor out = cfill(0.0);
+    if (scene_hit_light<STK, FX>(sc, ri, li, hi, C)) {
+        const lumo_object& Lo = sc.lights[li];
+        const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
+        const double p_sct = R.pdf;
+        if (!(p_lig == 0.0 || p_sct == 0.0)) {
+            const double denom = p_lig * p_lig + p_sct * p_sct;
+            const double weight = li_mode ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
+            const double p_denom = li_mode ? p_lig : p_sct;
+            const lumo_material hm = sc.mats[hi.material];
+            out = R.f * cfill(1.0) * emit<FX>(sc, hm, L, hi.backface, hi.uv) * R.cosv * weight / p_denom;
+        }
+    }
+    return out;
+}
+
+// A path between bounces, in registers (one QState entry).
+struct PathReg {
+    Ray ro;
+    DColor g, rad;
+    double L[NS];
+    Xorshift rng;
+    int32_t slot, task;
+    uint32_t depth, flags, queries;
+};
+
+// One bounce of one path with n_shadow == 1 (path_trace.rs:18-77, integrator.rs:74-184).
+// Returns whether the path continues; P then holds the next bounce's ray, throughput, flags and
+// depth, and its radiance includes this bounce's NEE term (the three-kernel bounce adds that
+// term at the start of the next bounce: the same addition).  When it ends, P holds its final
+// radiance, wavelengths, depth and query count (FilmSample, path_trace.rs:79-81).
+template <int STK, int FX>
+__device__ __forceinline__ bool bounce_path(const DScene& sc, const double* delta, PathReg& P, Counters& Cc,
+                                            Counters& Cs) {
+    const RayX rx = rayx(P.ro);
+    const HitRef hr = scene_hit<STK, FX>(sc, rx, Cc);  // Scene::hit (k_closest_q)
+    P.queries += 1u;
+    if (hr.kind == 0) return false;
+    DHit ho;
+    hit_record<FX>(sc, hr, rx, ho);
+    const lumo_material m = sc.mats[ho.material];
+    const V3 wo = -P.ro.d;
+    const double rand_u = xs_float(P.rng);
+    const V2 rsq = xs_vec2(P.rng);
+    V3 wi;
+    if (!bsdf_sample<FX>(sc, m, ho, wo, P.L, rand_u, rsq, wi)) {  // may terminate L
+        if (P.flags & QF_SPECULAR) P.rad = P.rad + P.g * emit<FX>(sc, m, P.L, ho.backface, ho.uv);
+        return false;
+    }
+    const bool resolve = !mat_is_delta<FX>(sc, m, P.L);
+    // the NEE pair (nee_pair): both records generated first, traced after the continuation, so
+    // the hit record and material are dead during the traversals (the traversals draw nothing,
+    // so the RNG sequence is lumo's: BSDF sample, light pick + direction, BSDF sample, RR)
+    NeeRec RL, RB;
+    int li = 0;
+    double pdf_light = 1.0;
+    bool ok = false;
+    const DColor g_nee = P.g;
+    if (resolve) {
+        li = sample_light(sc, xs_float(P.rng));
+        pdf_light = sc.alias_pdf[li];
+        const V2 rs = xs_vec2(P.rng);
+        RL = nee_record<FX>(sc, m, ho, wo, light_sample_towards<FX>(sc, sc.lights[li], ho.p, rs), P.L);
+        const double ru = xs_float(P.rng);
+        const V2 rsq2 = xs_vec2(P.rng);
+        V3 wb;
+        ok = bsdf_sample<FX>(sc, m, ho, wo, P.L, ru, rsq2, wb);  // may terminate L
+        if (ok) RB = nee_record<FX>(sc, m, ho, wo, wb, P.L);
+        P.queries += 1u + (ok ? 1u : 0u);
+    }
+    // continuation (path_trace.rs:42-77)
+    const Ray rn = spawn(ho, wi);
+    const double p_scatter = bsdf_pdf<FX>(sc, m, ho, wo, rn.d, P.L);
+    bool alive = false;
+    if (!(p_scatter <= 0.0)) {  // path_trace.rs:47: a NaN pdf continues the path
+        const DColor bsdf = bsdf_f<FX>(sc, m, ho, wo, rn.d, P.L);
+        P.g = P.g * (bsdf * shading_cosine(m, rn.d, ho.ns) / p_scatter);
+        alive = true;
+        if ((int)P.depth >= RR_DEPTH) {
+            const double lum = luminance(sc, P.g, P.L);
+            const double rr_prob = rmin(lum / delta[P.task], 1.0);
+            if (xs_float(P.rng) > rr_prob)
+                alive = false;
+            else
+                P.g = P.g / rr_prob;
+        }
+    }
+    if (resolve) {  // k_shadow_q (NS1): single = (0 + L-record + B-record) / pdf_light
+        // one inlined traversal for both records (selects, not an indexed array: no scratch)
+        DColor a = cfill(0.0), b = cfill(0.0);
+#pragma unroll 1
+        for (int k = 0; k < (ok ? 2 : 1); ++k) {
+            const NeeRec Rk = k == 0 ? RL : RB;
+            const DColor x = shadow_record_r<STK, FX>(sc, Rk, li, k == 0, P.L, Cs);
+            if (k == 0)
+                a = x;
+            else
+                b = x;
+        }
+        const DColor single = (cfill(0.0) + a + b) / pdf_light;
+        P.rad = P.rad + (cfill(0.0) + g_nee * single) / 1.0;
+    }
+    if (alive) {
+        P.ro = rn;
+        P.flags = mat_is_specular<FX>(m) ? QF_SPECULAR : 0u;
+        P.depth += 1u;
+    }
+    return alive;
+}
+
+__device__ __forceinline__ PathReg load_path(const QState& cur, uint32_t q) {
+    PathReg P;
+    P.slot = cur.I(QI_SLOT, q);
+    P.task = cur.I(QI_TASK, q);
+    P.depth = (uint32_t)cur.I(QI_DEPTH, q);
+    P.flags = (uint32_t)cur.I(QI_FLAGS, q);
+    P.queries = (uint32_t)cur.I(QI_QUERIES, q);
+    P.ro = Ray{qv3(cur, QD_O, q), qv3(cur, QD_D, q)};
+    P.g = qc(cur, QD_G, q);
+    P.rad = qc(cur, QD_R, q);
+    if (P.flags & QF_PENDING) P.rad = P.rad + qc(cur, QD_P, q);  // the previous bounce's NEE term
+    for (int i = 0; i < NS; ++i) P.L[i] = cur.D(QD_L + i, q);
+    P.rng = Xorshift{cur.R(0, q), cur.R(1, q)};
+    return P;
+}
+__device__ __forceinline__ void store_final(const Paths& S, const PathReg& P) {  // FilmSample (path_trace.rs:79-81)
+    for (int i = 0; i < NS; ++i) S.lam[4 * P.slot + i] = P.L[i];
+    S.depth[P.slot] = P.depth;
+    S.queries[P.slot] = P.queries;
+    stc(S.rad, P.slot, P.rad);
+}
+
+// TAIL = true: launched ahead of every bounce of an n_shadow == 1 pass; when fewer than
+// tail_below paths are alive it runs each of them to its end in this launch (the bounce kernels,
+// given the same threshold, then skip the bounce), so the switch is made on the device from the
+// exact count.  TAIL = false (fused mode): one bounce in three phases whose live registers do not
+// overlap: the closest hit from the ray alone; the shading, the NEE pair's records and the
+// continuation, compacted into `nxt` at once (with the NEE term pending, as k_shade_q); then the
+// pair's two traversals from registers, the term delivered into the continuation's entry or the
+// final radiance (as k_shadow_q).  Neither hits nor records go through HBM.
+template <int STK, bool LDS, int FX, bool TAIL>
+__global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_q(DScene sc0, Paths S, Tasks T,
+                                                                                  QState cur, QState nxt,
+                                                                                  uint32_t tail_below) {
+    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+    const uint32_t count = S.counts[CNT_CUR];
+    if ((count < tail_below) != TAIL) return;      // the other kernel takes this bounce
+    if (count <= blockIdx.x * blockDim.x) return;  // before staging: whole block idle
+    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    Counters Cc{0, 0, 0, 0}, Cs{0, 0, 0, 0};
+    if constexpr (TAIL) {
+        uint32_t tailq = 0;
+        for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
+            PathReg P = load_path(cur, q);
+            while (bounce_path<STK, FX>(sc, T.delta, P, Cc, Cs)) tailq++;
+            store_final(S, P);
+        }
+        flush_resolved(tailq, S.tcount + TC_TAILQ);
+    } else {
+        // grid-stride over whole blocks: block_slot needs every thread of the block each round
+        for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
+            const uint32_t q = base + threadIdx.x;
+            const bool live = q < count;
+            // phase 1: Scene::hit (k_closest_q)
+            HitRef hr{DINF, 0, -1, -1};
+            if (live) hr = scene_hit<STK, FX>(sc, rayx(Ray{qv3(cur, QD_O, q), qv3(cur, QD_D, q)}), Cc);
+            // phase 2: the bounce of k_shade_q (NS1) with the pair's records kept in registers
+            PathReg P{};
+            bool resolve = false, alive = false, ok = false;
+            NeeRec RL;
+            int li = 0;
+            double pdf_light = 1.0;
+            DColor g_nee = cfill(0.0);
+            Ray rn{V3{0, 0, 0}, V3{0, 0, 0}};
+            __shared__ double rb_lds[12][BLOCK];  // the B record waits here (not in VGPRs) for phase 3
+            if (live) {
+                P = load_path(cur, q);
+                P.queries += 1u;
+                if (hr.kind != 0) {
+                    DHit ho;
+                    hit_record<FX>(sc, hr, rayx(P.ro), ho);
+                    const lumo_material m = sc.mats[ho.material];
+                    const V3 wo = -P.ro.d;
+                    const double rand_u = xs_float(P.rng);
+                    const V2 rsq = xs_vec2(P.rng);
+                    V3 wi;
+                    if (!bsdf_sample<FX>(sc, m, ho, wo, P.L, rand_u, rsq, wi)) {  // may terminate L
+                        if (P.flags & QF_SPECULAR) P.rad = P.rad + P.g * emit<FX>(sc, m, P.L, ho.backface, ho.uv);
+                    } else {
+                        resolve = !mat_is_delta<FX>(sc, m, P.L);
+                        g_nee = P.g;
+                        if (resolve) {  // nee_pair
+                            li = sample_light(sc, xs_float(P.rng));
+                            pdf_light = sc.alias_pdf[li];
+                            const V2 rs = xs_vec2(P.rng);
+                            RL = nee_record<FX>(sc, m, ho, wo, light_sample_towards<FX>(sc, sc.lights[li], ho.p, rs),
+                                                P.L);
+                            const double ru = xs_float(P.rng);
+                            const V2 rsq2 = xs_vec2(P.rng);
+                            V3 wb;
+                            ok = bsdf_sample<FX>(sc, m, ho, wo, P.L, ru, rsq2, wb);  // may terminate L
+                            if (ok) {
+                                const NeeRec RB = nee_record<FX>(sc, m, ho, wo, wb, P.L);
+                                const double v[12] = {RB.ray.o.x, RB.ray.o.y, RB.ray.o.z, RB.ray.d.x, RB.ray.d.y,
+                                                      RB.ray.d.z, RB.f.s[0], RB.f.s[1], RB.f.s[2], RB.f.s[3],
+                                                      RB.pdf, RB.cosv};
+#pragma unroll
+                                for (int k = 0; k < 12; ++k) rb_lds[k][threadIdx.x] = v[k];
+                            }
+                            P.queries += 1u + (ok ? 1u : 0u);
+                        }
+                        // continuation (path_trace.rs:42-77)
+                        rn = spawn(ho, wi);
+                        const double p_scatter = bsdf_pdf<FX>(sc, m, ho, wo, rn.d, P.L);
+                        if (!(p_scatter <= 0.0)) {  // path_trace.rs:47: a NaN pdf continues the path
+                            const DColor bsdf = bsdf_f<FX>(sc, m, ho, wo, rn.d, P.L);
+                            P.g = P.g * (bsdf * shading_cosine(m, rn.d, ho.ns) / p_scatter);
+                            alive = true;
+                            if ((int)P.depth >= RR_DEPTH) {
+                                const double lum = luminance(sc, P.g, P.L);
+                                const double rr_prob = rmin(lum / T.delta[P.task], 1.0);
+                                if (xs_float(P.rng) > rr_prob)
+                                    alive = false;
+                                else
+                                    P.g = P.g / rr_prob;
+                            }
+                        }
+                        P.flags = mat_is_specular<FX>(m) ? QF_SPECULAR : 0u;
+                    }
+                }
+            }
+            const uint32_t np = block_slot(alive, S.counts + CNT_NEXT);
+            if (alive) {
+                qv3(nxt, QD_O, np, rn.o);
+                qv3(nxt, QD_D, np, rn.d);
+                qc(nxt, QD_G, np, P.g);
+                qc(nxt, QD_R, np, P.rad);
+                for (int i = 0; i < NS; ++i) nxt.D(QD_L + i, np) = P.L[i];
+                nxt.R(0, np) = P.rng.hi;
+                nxt.R(1, np) = P.rng.lo;
+                nxt.I(QI_SLOT, np) = P.slot;
+                nxt.I(QI_TASK, np) = P.task;
+                nxt.I(QI_DEPTH, np) = (int32_t)(P.depth + 1u);
+                nxt.I(QI_FLAGS, np) = (int32_t)(P.flags | (resolve ? (uint32_t)QF_PENDING : 0u));
+                nxt.I(QI_QUERIES, np) = (int32_t)P.queries;
+            } else if (live) {  // the path ends here (its radiance gains the NEE term below)
+                for (int i = 0; i < NS; ++i) S.lam[4 * P.slot + i] = P.L[i];
+                S.depth[P.slot] = P.depth;
+                S.queries[P.slot] = P.queries;
+                stc(S.rad, P.slot, P.rad);
+            }
+            // phase 3: the pair's visibility + MIS (k_shadow_q, NS1)
+            if (resolve) {
+                const DColor a = shadow_record_r<STK, FX>(sc, RL, li, true, P.L, Cs);
+                DColor b = cfill(0.0);
+                if (ok) {
+                    NeeRec RB;
+                    RB.ray = Ray{V3{rb_lds[0][threadIdx.x], rb_lds[1][threadIdx.x], rb_lds[2][threadIdx.x]},
+                                 V3{rb_lds[3][threadIdx.x], rb_lds[4][threadIdx.x], rb_lds[5][threadIdx.x]}};
+                    RB.f = DColor{{rb_lds[6][threadIdx.x], rb_lds[7][threadIdx.x], rb_lds[8][threadIdx.x],
+                                   rb_lds[9][threadIdx.x]}};
+                    RB.pdf = rb_lds[10][threadIdx.x];
+                    RB.cosv = rb_lds[11][threadIdx.x];
+                    b = shadow_record_r<STK, FX>(sc, RB, li, false, P.L, Cs);
+                }
+                const DColor single = (cfill(0.0) + a + b) / pdf_light;
+                const DColor X = (cfill(0.0) + g_nee * single) / 1.0;
+                if (alive)
+                    qc(nxt, QD_P, np, X);
+                else  // the radiance stored above, re-read by the thread that wrote it
+                    stc(S.rad, P.slot, ldc(S.rad, P.slot) + X);
+            }
+        }
+    }
+    flush_counters(Cc, S.tcount);
+    flush_counters(Cs, S.tcount + TC_N);
+    if (LUMO_SKIP_DEAD) flush_resolved(Cs.resolved, S.tcount + TC_RESOLVED);
+}
 
 // ------------------------------------------------------------------ traversal-only entry (lumo_trace)
 template <int STK>

@@ -33,6 +33,9 @@ constexpr int BLOCK = 256;
 #ifndef LUMO_SKIP_DEAD  // shadow records with p_sct == 0 answered without traversal (C3 shadow -16 %)
 #define LUMO_SKIP_DEAD 1
 #endif
+#ifndef LUMO_BOUNCE_WAVES  // k_bounce_q (fused bounce, n_shadow == 1)
+#define LUMO_BOUNCE_WAVES 3
+#endif
 #ifndef LUMO_BDPT_STEP_WAVES  // k_bdpt_step: 2 waves measured best (C4 step 187 -> 153 ms)
 #define LUMO_BDPT_STEP_WAVES 2
 #endif
@@ -55,7 +58,8 @@ enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_BUCKET0, CNT_N = CNT_
 constexpr int NB = 8;
 enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
 constexpr int TC_RESOLVED = 2 * TC_N;  // + shadow records answered without traversal; W_TCOUNT has TC_ALL
-constexpr int TC_ALL = 2 * TC_N + 1;
+constexpr int TC_TAILQ = 2 * TC_N + 1;  // + closest queries run by k_bounce_q in tail mode past its first bounce
+constexpr int TC_ALL = 2 * TC_N + 2;
 #ifndef LUMO_SHADOW_STATS
 #define LUMO_SHADOW_STATS 0
 #endif
@@ -225,6 +229,35 @@ __device__ __forceinline__ uint32_t block_slot_bucket(bool pred, int key, uint32
     }
     __syncthreads();
     const uint32_t pos = pred ? base_s[key] + cnt[key][w] + rank : 0u;
+    __syncthreads();
+    return pos;
+}
+
+// block_slot with the block's entries grouped by key (0 <= key < NK) inside its segment of the
+// queue: an LDS histogram gives each entry its rank within its key, the keys' offsets are
+// scanned, and one atomic per workgroup reserves the segment.  Which path lands in which lane of
+// the consuming kernel does not change any path's result, only how alike the paths of a wave
+// are (rays leaving the same surface in the same octant walk similar BVH / kd nodes).  The
+// order within a key is that of the LDS atomics.  Every thread of the block must call it.
+template <int NK>
+__device__ __forceinline__ uint32_t block_slot_sorted(bool pred, int key, uint32_t* counter) {
+    __shared__ uint32_t hist[NK];
+    __shared__ uint32_t base_s;
+    for (int k = threadIdx.x; k < NK; k += blockDim.x) hist[k] = 0u;
+    __syncthreads();
+    const uint32_t rank = pred ? atomicAdd(&hist[key], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int k = 0; k < NK; ++k) {
+            const uint32_t c = hist[k];
+            hist[k] = t;
+            t += c;
+        }
+        base_s = t ? atomicAdd(counter, t) : 0u;
+    }
+    __syncthreads();
+    const uint32_t pos = pred ? base_s + hist[key] + rank : 0u;
     __syncthreads();
     return pos;
 }

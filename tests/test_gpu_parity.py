@@ -188,3 +188,32 @@ def test_separate_result_buffers_match_oracle(dev, cornell, max_paths):
         np.testing.assert_array_equal(b[:len(ob)], ob)
         assert np.isnan(b[len(ob):]).all()  # nothing written past the tile
         assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+
+
+@pytest.mark.parametrize("fused,tail", [(0, 0), (0, 300), (0, 1 << 30), (1, 0), (1, 300), (1, 1 << 30)])
+def test_bounce_modes_match_oracle(dev, cornell, fused, tail):
+    """The three-kernel bounce and the fused bounce kernel (k_bounce_q: closest hit + shading +
+    NEE pair in one launch), each without the tail kernel (tail 0), with the tail entered
+    mid-pass (tail 300) and with every path run to its end in one launch (tail 2^30): paths,
+    tiles and the closest / shadow query counts all equal the oracle's.  (Traversal counters are
+    not compared here: the device answers p_sct == 0 records without traversal, the oracle
+    traces them; lumo_trace's counter parity is in test_gpu_trace / test_gpu_scale.)"""
+    from lumo_amd import _ffi
+    lib = _ffi.load()
+    lib.lumo_set_bounce_mode(fused, tail)
+    try:
+        cam = L.Camera.cornell_box((48, 40))
+        dev.upload(cornell, cam)
+        tasks = L.make_tasks(48, 40, 24, SEED)
+        _cmp_paths(gpu_paths(dev, tasks[4]), O.trace_paths(cornell.desc(), cam.desc, tasks[4]))
+        before = dev.stats()
+        bufs, res = dev.render_tasks(tasks)
+        after = dev.stats()
+        obufs, ores, cnt = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+        for b, ob, r, orr in zip(bufs, obufs, res, ores):
+            np.testing.assert_array_equal(b, ob)
+            assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+        assert after.closest_queries - before.closest_queries == cnt.closest_queries
+        assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
+    finally:
+        lib.lumo_set_bounce_mode(-1, 1 << 18)

@@ -196,3 +196,27 @@ def test_kernel_variants(dev, variant_env, name, cls, lds, full):
     for b, ob, r, orr in zip(bufs, obufs, res, ores):
         np.testing.assert_array_equal(b, ob)
         assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+
+
+@pytest.mark.parametrize("fused,tail", [(1, 0), (1, 300), (0, 1 << 30)])
+def test_bounce_modes_small_dragon(dev, fused, tail):
+    """The fused bounce kernel and the tail kernel on an instanced glass mesh (feature class 1,
+    no LDS staging, deep kd stack): paths and tiles equal the oracle's."""
+    lib = _ffi.load()
+    lib.lumo_set_bounce_mode(fused, tail)
+    try:
+        sc, cam, tasks = _variant_scene("small_dragon")
+        sc.build()
+        dev.upload(sc, cam)
+        g = gpu_paths(dev, tasks[1])
+        o = O.trace_paths(sc.desc(), cam.desc, tasks[1])
+        for k in ("depth", "raster", "lam", "radiance", "delta"):
+            np.testing.assert_array_equal(g[k], o[k], err_msg=k)
+        sub = list(tasks)[:6]
+        bufs, res = dev.render_tasks(sub)
+        obufs, ores, _ = O.render_tasks(sc.desc(), cam.desc, sub, O.WAVEFRONT, 8)
+        for b, ob, r, orr in zip(bufs, obufs, res, ores):
+            np.testing.assert_array_equal(b, ob)
+            assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+    finally:
+        lib.lumo_set_bounce_mode(-1, 1 << 18)
