@@ -287,8 +287,14 @@ def roofline(st, n_shadow, bdpt=False, workload="c1"):
                  "k_bdpt_trace_a+k_bdpt_vis": (conn_ms, conn_launches, st.shadow_queries * B_CONN_IO + trav1)}
     else:
         b_io = B_RECORD + B_FOLD / (2 * n_shadow)
-        cands = {"k_closest": (ms[1], launches[1], closest_bytes),
-                 "k_shadow": (ms[3], launches[3], traversed * b_io + st.shadow_resolved * 8 + trav1)}
+        shadow_bytes = traversed * b_io + st.shadow_resolved * 8 + trav1
+        if n_shadow == 1 and ms[1] > 0 and ms[2] == 0:
+            # fused bounce (k_bounce_q: closest hit + shading + the NEE pair, 'closest' stage) and
+            # its tail kernel ('resolve' stage for n_shadow == 1): one unit carrying every query,
+            # priced with the same per-query model as the three-kernel bounce
+            cands = {"k_bounce_q+k_bounce_tail": (ms[1] + ms[4], launches[1] + launches[4], closest_bytes + shadow_bytes)}
+        else:
+            cands = {"k_closest": (ms[1], launches[1], closest_bytes), "k_shadow": (ms[3], launches[3], shadow_bytes)}
     # the dominant kernel of the step: the longest of all timed stages; if that is not a
     # traversal kernel, the roofline is still reported for the longest traversal kernel
     dom_stage = STAGES[max(range(len(STAGES)), key=lambda i: ms[i])]

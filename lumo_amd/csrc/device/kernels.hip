@@ -250,6 +250,17 @@ __global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, 
     count_checks(cat, S.checks);
 }
 
+// Filter footprints up to FILM_R pixels: each source sample's separable Gaussian terms
+// max(gauss(v) - gauss(r), 0) for its 2r+1 columns / rows are computed once per sample (by the
+// sample's own thread, into LDS) instead of once per (sample, destination) pair; the gather reads
+// them in the same order, so the film is bit-identical.
+constexpr int FILM_R = 2;
+struct FilmTerms {
+    const double* wx;  // [2 * FILM_R + 1][BLOCK]: column term of source k at gx = px_k - r + i
+    const double* wy;
+    int r;
+};
+
 __device__ __forceinline__ double gauss(double x, double sigma) {
     return lm_exp(-(x * x) / (2.0 * sigma * sigma)) / sqrt(rmax(2.0 * PI * sigma * sigma, 0.0));
 }
@@ -259,7 +270,7 @@ __device__ __forceinline__ double gauss(double x, double sigma) {
 // than 2 px cannot.  `src` reads a source sample by its pixel index within the tile.
 template <class Src>
 __device__ __forceinline__ void film_gather(const Paths& S, const lumo_tile_task& t, const DCam& cam, int s, int j,
-                                            const Src& src) {
+                                            const Src& src, const FilmTerms* terms = nullptr) {
     const int W = (int)(t.px_max[0] - t.px_min[0]), H = (int)(t.px_max[1] - t.px_min[1]);
     const int dx = j % W, dy = j / W;
     const uint64_t gx = t.px_min[0] + dx, gy = t.px_min[1] + dy;
@@ -278,8 +289,13 @@ __device__ __forceinline__ void film_gather(const Paths& S, const lumo_tile_task
             const uint64_t miy = std::max(py >= r ? py - r : 0, t.px_min[1]);
             const uint64_t mxx = std::min(px + r, t.px_max[0] - 1), mxy = std::min(py + r, t.px_max[1] - 1);
             if (gx < mix || gx > mxx || gy < miy || gy > mxy) continue;
-            const double vx = rx - (0.5 + (double)gx), vy = ry - (0.5 + (double)gy);
-            const double w = rmax(gauss(vx, cam.fsig) - gr, 0.0) * rmax(gauss(vy, cam.fsig) - gr, 0.0);
+            double w;
+            if (terms) {  // the source's precomputed terms (px - r <= gx <= px + r)
+                w = terms->wx[(int)(gx + r - px) * BLOCK + k] * terms->wy[(int)(gy + r - py) * BLOCK + k];
+            } else {
+                const double vx = rx - (0.5 + (double)gx), vy = ry - (0.5 + (double)gy);
+                w = rmax(gauss(vx, cam.fsig) - gr, 0.0) * rmax(gauss(vy, cam.fsig) - gr, 0.0);
+            }
             if (w != 0.0) {
                 const V3 c = src.rgb(k) * w;
                 acc[0] += c.x;
@@ -318,6 +334,7 @@ struct LdsSrc {  // sources staged in LDS by k_finish_film
     __device__ V3 rgb(int k) const { return V3{rgb_[3 * k], rgb_[3 * k + 1], rgb_[3 * k + 2]}; }
 };
 
+
 // k_finish + k_film for tasks of at most BLOCK pixels (lumo's 16x16 tiles): one block per task,
 // the tile's sample RGB and raster positions staged in LDS instead of a round trip through HBM.
 // Same arithmetic as the two kernels, so the film is bit-identical.
@@ -326,11 +343,14 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S, Tasks
     __shared__ double l_rgb[3 * BLOCK];
     __shared__ double l_ras[2 * BLOCK];
     __shared__ uint32_t l_ok[BLOCK];
+    __shared__ double l_wx[(2 * FILM_R + 1) * BLOCK], l_wy[(2 * FILM_R + 1) * BLOCK];
     const int ti = blockIdx.x;
     const int first = T.first[ti];
     const int P = T.first[ti + 1] - first;
     const int j = threadIdx.x;
     const int s = first + j;
+    const int r = (int)ceil(cam.fr - 0.5);
+    const bool pre = r <= FILM_R;  // uniform
     if (j < P) {
         const bool ok = S.p_valid[s] != 0;
         l_ok[j] = ok ? 1u : 0u;
@@ -339,13 +359,24 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S, Tasks
             l_rgb[3 * j] = rgb.x;
             l_rgb[3 * j + 1] = rgb.y;
             l_rgb[3 * j + 2] = rgb.z;
-            l_ras[2 * j] = S.raster[2 * s];
-            l_ras[2 * j + 1] = S.raster[2 * s + 1];
+            const double rx = S.raster[2 * s], ry = S.raster[2 * s + 1];
+            l_ras[2 * j] = rx;
+            l_ras[2 * j + 1] = ry;
+            if (pre) {  // this sample's column / row terms, as film_gather computes them
+                const double gr = gauss(cam.fr, cam.fsig);
+                const int64_t px = rx > 0.0 ? (int64_t)floor(rx) : 0, py = ry > 0.0 ? (int64_t)floor(ry) : 0;
+                for (int i = 0; i <= 2 * r; ++i) {
+                    const double gx = (double)(px - r + i), gy = (double)(py - r + i);
+                    l_wx[i * BLOCK + j] = rmax(gauss(rx - (0.5 + gx), cam.fsig) - gr, 0.0);
+                    l_wy[i * BLOCK + j] = rmax(gauss(ry - (0.5 + gy), cam.fsig) - gr, 0.0);
+                }
+            }
         }
     }
     __syncthreads();
     count_checks(j < P && l_ok[j] ? sample_check(ldc(S.rad, s)) : 0, S.checks);
-    if (j < P) film_gather(S, T.t[ti], cam, s, j, LdsSrc{l_rgb, l_ras, l_ok});
+    const FilmTerms terms{l_wx, l_wy, r};
+    if (j < P) film_gather(S, T.t[ti], cam, s, j, LdsSrc{l_rgb, l_ras, l_ok}, pre ? &terms : nullptr);
 }
 
 // task.rs:42-53 + 64-69: ring update in pixel order, then delta for the next pass.
@@ -932,10 +963,10 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 issued++;
                 std::swap(qa, qb);
             }
-            while (consumed < issued) {  // trailing empty bounces
-                HIPCHK(hipEventSynchronize(c.snap_ev[consumed % Ctx::SNAP_RING]));
-                consumed++;
-            }
+            // The bounces issued past the first empty snapshot see empty queues; nothing waits for
+            // them: the stream orders them before the film kernels launched next (waiting here
+            // left the GPU idle for a host round trip per pass), and their snapshot slots and
+            // events are simply re-recorded by the next pass.
             return LUMO_OK;
         };
         lumo_status bst = LUMO_OK;
@@ -945,7 +976,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 const QState& nxt = S.qs[(b + 1) & 1];
                 // n_shadow == 1: the tail kernel takes the bounce when fewer than g_tail_below paths
                 // are alive (decided on the device from the exact count); the bounce kernels skip it
-                const uint32_t skip = ns == 1 ? g_tail_below : 0u;
+                // (launched only once the last count the host has seen is below 4x the threshold:
+                // before that the bounce kernels get threshold 0 and take every path)
+                const uint32_t skip = (ns == 1 && (uint64_t)ub < 4ull * g_tail_below) ? g_tail_below : 0u;
                 if (skip > 0) {
                     StageTimer tm(c, g_timing, ST_RESOLVE);
                     launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {

@@ -37,6 +37,14 @@ if "k_bdpt_trace_a" in out and "k_bdpt_vis" in out:  # bench.py's BDPT connectio
         kk: (a[kk] * a["launches"] + b[kk] * b["launches"]) / n
         for kk in ("hbm_bytes_per_launch", "hbm_bytes_per_launch_raw", "avg_us")}
     out["k_bdpt_trace_a+k_bdpt_vis"]["launches"] = n
+for a_k, b_k in (("k_bounce_q", "k_bounce_tail"),):  # bench.py's fused unit: both kernels
+    if a_k in out and b_k in out:
+        a, b = out[a_k], out[b_k]
+        n = a["launches"] + b["launches"]
+        out[a_k + "+" + b_k] = {
+            kk: (a[kk] * a["launches"] + b[kk] * b["launches"]) / n
+            for kk in ("hbm_bytes_per_launch", "hbm_bytes_per_launch_raw", "avg_us")}
+        out[a_k + "+" + b_k]["launches"] = n
 table[workload] = out
 json.dump(table, open(path, "w"), indent=1, sort_keys=True)
 print("updated", dst)
