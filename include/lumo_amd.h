@@ -372,11 +372,13 @@ void lumo_set_lds_staging(int on);
 /* Perf switch (path tracer, one light sample per bounce).  fused = 0: each bounce is three
  * kernels (closest hit / shading / visibility); fused = 1: one kernel (closest hit + shading +
  * the NEE pair traced from registers); fused = -1 (default): fused when the scene is staged in
- * LDS (small scenes), else three kernels.  Every bounce is preceded by a tail kernel that takes
- * it instead when fewer than tail_below paths are alive and runs each of them to its end in that
- * launch (tail_below = 0: never; default 262144).  Every mode gives bit-identical paths.  Also
- * LUMO_FUSED / LUMO_TAIL in the environment. */
-void lumo_set_bounce_mode(int fused, uint32_t tail_below);
+ * LDS (small scenes), else three kernels.  Bounces are preceded by a tail kernel that takes the
+ * bounce instead when fewer than tail_below paths are alive and runs each of them to its end in
+ * that launch (tail_below = 0: never; default 262144).  pipeline = 1 (default), with fused
+ * bounces: each pass runs its first bounces on one stream and hands the rest (tail kernel, film,
+ * ring) to a second stream while the next pass starts.  Every mode gives bit-identical results.
+ * Also LUMO_FUSED / LUMO_TAIL / LUMO_PIPELINE in the environment. */
+void lumo_set_bounce_mode(int fused, uint32_t tail_below, int pipeline);
 
 #ifdef __cplusplus
 }

@@ -189,7 +189,7 @@ DEVICE_API = [
     ("lumo_stats_reset", C.c_int32, [C.c_void_p]),
     ("lumo_set_timing", None, [C.c_int]),
     ("lumo_set_lds_staging", None, [C.c_int]),
-    ("lumo_set_bounce_mode", None, [C.c_int, C.c_uint32]),
+    ("lumo_set_bounce_mode", None, [C.c_int, C.c_uint32, C.c_int]),
     ("lumo_debug_stream", C.c_int32, [C.c_void_p, C.c_size_t]),
     ("lumo_scene_info", C.c_int32, [C.c_void_p, C.POINTER(SceneInfo)]),
     ("lumo_debug_set_integrator", C.c_int32, [C.c_void_p, C.c_int]),

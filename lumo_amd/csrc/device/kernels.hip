@@ -165,8 +165,9 @@ __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, in
 }
 
 // Start of a bounce: the alive queue just built becomes the current one.
-__global__ void k_bounce_begin(uint32_t* counts) {
+__global__ void k_bounce_begin(uint32_t* counts, unsigned long long* headq) {
     if (threadIdx.x == 0) {
+        *headq += counts[CNT_NEXT];  // this bounce's closest queries (one per queued path)
         counts[CNT_CUR] = counts[CNT_NEXT];
         counts[CNT_NEXT] = 0;
         counts[CNT_SHADOW] = 0;
@@ -555,6 +556,8 @@ struct DevBuf {
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;  // pipelined passes: each pass's tail, film and ring
+    hipEvent_t pass_ev[2] = {nullptr, nullptr}, tail_ev[2] = {nullptr, nullptr};
     bool has_scene = false, has_camera = false;
     DScene sc{};
     DCam cam{};
@@ -620,7 +623,8 @@ enum WorkId {
     W_BDR_SPN, W_BD_NL, W_BD_NC, W_BD_NITEMS, W_BD_IOFF, W_BD_DRAWS, W_BD_OK, W_BD_ITOTAL, W_BD_TERM, W_BD_PDF, W_BD_WDEPTH,
     W_BD_CAMO, W_BD_CAMD, W_BD_RNG0, W_BD_LAM0, W_BDR_DRAWS, W_BDR_OK, W_BD_NB, W_BD_OFFB, W_BD_TERMB, W_BD_VIS, W_BD_AT, W_BD_AKIND, W_BD_AOBJ,
     W_BD_ATRI, W_CHECKS, W_QS0_D, W_QS0_R, W_QS0_I, W_QS1_D, W_QS1_R, W_QS1_I, W_HQ_T, W_HQ_I, W_SQ_D, W_SQ_I,
-    W_SQ_HD, W_SQ_HI, W_SQ_HR, W_COUNT
+    W_SQ_HD, W_SQ_HI, W_SQ_HR, W_RAD2, W_LAM2, W_RASTER2, W_DEPTH2, W_QUERIES2, W_P_VALID2, W_COUNTS2, W_QS2_D,
+    W_QS2_R, W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I, W_COUNT
 };
 
 template <typename T>
@@ -656,33 +660,41 @@ struct StageTimer {
     Ctx& c;
     bool on;
     int stage;
+    hipStream_t sm;
     hipEvent_t a{}, b{};
-    StageTimer(Ctx& cc, bool enable, int st) : c(cc), on(enable), stage(st) {
+    StageTimer(Ctx& cc, bool enable, int st, hipStream_t stream = nullptr)
+        : c(cc), on(enable), stage(st), sm(stream ? stream : cc.stream) {
         if (on) {
             a = timing().get();
             b = timing().get();
-            (void)hipEventRecord(a, c.stream);
+            (void)hipEventRecord(a, sm);
         }
         c.stats.launches[stage] += 1;
     }
     ~StageTimer() {
         if (on) {
-            (void)hipEventRecord(b, c.stream);
+            (void)hipEventRecord(b, sm);
             timing().pending.push_back({stage, {a, b}});
         }
     }
 };
 
-// Call after the stream has been synchronised.
+// Adds the elapsed time of every completed timer pair; pairs still in flight stay pending (the
+// end of lumo_render_tiles synchronises, so all are resolved by its last call).
 void resolve_timers(Ctx& c) {
     Timing& t = timing();
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> still;
     for (auto& p : t.pending) {
+        if (hipEventQuery(p.second.second) != hipSuccess) {
+            still.push_back(p);
+            continue;
+        }
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, p.second.first, p.second.second) == hipSuccess) c.stats.kernel_ms[p.first] += ms;
         t.free_ev.push_back(p.second.first);
         t.free_ev.push_back(p.second.second);
     }
-    t.pending.clear();
+    t.pending.swap(still);
 }
 
 bool g_timing = false;
@@ -707,14 +719,108 @@ bool g_lds = true;
 int g_buckets = NB;  // LUMO_BUCKETS=0: NEE records not grouped by origin object
 int g_fused = -1;  // n_shadow == 1: k_bounce_q instead of closest / shade / shadow (-1: when the scene is LDS-staged)
 uint32_t g_tail_below = 1u << 18;  // n_shadow == 1: k_bounce_q tail mode below this many live paths
+bool g_pipeline = true;            // fused passes overlapped on two streams (render_pipelined)
 int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
 template <typename F>
-void launch_trav(Ctx& c, uint64_t count, F&& f) {
+void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr) {
     const bool lds = g_lds && c.sc.hot_bytes > 0;
     const int grid_full = ceil_div(count, BLOCK);
     const TravLaunch l{lds ? std::min(grid_full, c.lds_grid_cap) : grid_full, lds ? (size_t)c.sc.hot_bytes : 0, lds,
-                       c.sc.full, c.stream};
+                       c.sc.full, stream ? stream : c.stream};
     by_stack_class(c.sc.stack_class, [&](auto K) { f(K, l); });
+}
+
+// Pipelined passes (n_shadow == 1, fused bounces).  Russian roulette reads the pass's adaptive
+// delta only from depth RR_DEPTH on (path_trace.rs:60-69), and that delta needs the previous
+// pass's film + ring.  So on stream A each pass runs its camera and its first RR_DEPTH + 1 bounces
+// as fused launches (waiting for the previous pass's ring only before bounce RR_DEPTH), then hands
+// its queue to stream B, which runs the tail kernel (every remaining path to its end), the film and
+// the ring; meanwhile A starts the next pass.  The latency-bound tail, film and ring of pass p thus
+// overlap the heavy first bounces of pass p + 1.  Each pass parity has its own queues, counters and
+// per-slot outputs; every per-path operation and every film / ring sum is the same as in the
+// sequential loop, so the result is bit-identical.
+lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump_p, int N, int n_tasks, int dim_stride,
+                             uint64_t max_samples, uint64_t max_P, lumo_status& st) {
+    Paths S1 = S;  // odd passes
+    S1.rad = wbuf<double>(c, W_RAD2, 4 * (size_t)N, st);
+    S1.lam = wbuf<double>(c, W_LAM2, 4 * (size_t)N, st);
+    S1.raster = wbuf<double>(c, W_RASTER2, 2 * (size_t)N, st);
+    S1.depth = wbuf<uint32_t>(c, W_DEPTH2, N, st);
+    S1.queries = wbuf<uint32_t>(c, W_QUERIES2, N, st);
+    S1.p_valid = wbuf<uint32_t>(c, W_P_VALID2, N, st);
+    S1.counts = wbuf<uint32_t>(c, W_COUNTS2, CNT_N, st);
+    for (int k = 0; k < 2; ++k) {
+        S1.qs[k].cap = (size_t)N;
+        S1.qs[k].d = wbuf<double>(c, k ? W_QS3_D : W_QS2_D, QD_N * (size_t)N, st);
+        S1.qs[k].r = wbuf<uint64_t>(c, k ? W_QS3_R : W_QS2_R, 2 * (size_t)N, st);
+        S1.qs[k].i = wbuf<int32_t>(c, k ? W_QS3_I : W_QS2_I, QI_N * (size_t)N, st);
+    }
+    if (st) return st;
+    hipStream_t A = c.stream, B = c.stream2;
+    // "pass -1": the setup enqueued on A so far (tasks, memsets, the initial ring); B first waits
+    // for pass 0's heads on A, so it sees the setup too
+    HIPCHK(hipEventRecord(c.pass_ev[1], A));
+    const int gN = ceil_div(N, BLOCK);
+    const int heads = RR_DEPTH + 1;  // bounces 0..RR_DEPTH on A
+    for (uint64_t pass = 0; pass < max_samples; ++pass) {
+        const int par = (int)(pass & 1);
+        Paths& P = par ? S1 : S;
+        // ---- stream A: camera + the first bounces
+        HIPCHK(hipMemsetAsync(P.counts, 0, sizeof(uint32_t) * CNT_N, A));
+        {
+            StageTimer tm(c, g_timing, ST_CAMERA, A);
+            k_camera<true><<<gN, BLOCK, 0, A>>>(T, P, c.cam, N, dim_stride, (uint32_t)pass);
+        }
+        for (int b = 0; b < heads; ++b) {
+            if (b == RR_DEPTH) HIPCHK(hipStreamWaitEvent(A, c.pass_ev[par ^ 1], 0));  // this pass's delta
+            k_bounce_begin<<<1, 64, 0, A>>>(P.counts, P.tcount + TC_HEADQ);
+            StageTimer tm(c, g_timing, ST_CLOSEST, A);
+            launch_trav(
+                c, (uint64_t)N,
+                [&](auto K, const TravLaunch& l) {
+                    launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[b & 1], P.qs[(b + 1) & 1], 0u, false);
+                },
+                A);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c.tail_ev[par], A));
+        // ---- stream B: the rest of the pass, film, ring
+        HIPCHK(hipStreamWaitEvent(B, c.tail_ev[par], 0));
+        if (D.delta) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, B));
+        k_bounce_begin<<<1, 64, 0, B>>>(P.counts, P.tcount + TC_HEADQ);
+        {
+            StageTimer tm(c, g_timing, ST_RESOLVE, B);
+            launch_trav(
+                c, (uint64_t)N,
+                [&](auto K, const TravLaunch& l) {
+                    launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[heads & 1], P.qs[(heads + 1) & 1],
+                                                        0xffffffffu, true);
+                },
+                B);
+        }
+        if (max_P <= BLOCK) {
+            StageTimer tm(c, g_timing, ST_FILM, B);
+            k_finish_film<<<n_tasks, BLOCK, 0, B>>>(c.sc, P, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
+                                                    c.tone_arg);
+        } else {
+            {
+                StageTimer tm(c, g_timing, ST_FINISH, B);
+                k_finish<<<gN, BLOCK, 0, B>>>(c.sc, P, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg);
+            }
+            StageTimer tm(c, g_timing, ST_FILM, B);
+            k_film<<<gN, BLOCK, 0, B>>>(P, T, c.cam, N);
+        }
+        {
+            StageTimer tm(c, g_timing, ST_RING, B);
+            k_ring<<<n_tasks, 64, 0, B>>>(P, T, n_tasks, 1);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c.pass_ev[par], B));
+        if (g_timing) resolve_timers(c);
+    }
+    // the results are copied on A: after the last pass's ring
+    HIPCHK(hipStreamWaitEvent(A, c.pass_ev[(max_samples - 1) & 1], 0));
+    return LUMO_OK;
 }
 
 lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lumo_tile_result* out, Dump* dump_host,
@@ -917,7 +1023,14 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     // device memory.  A pass ends once a snapshot shows no path alive; the bounces enqueued past
     // that point see empty queues and exit at once.
     const int ahead = c.bounce_ahead;
-    for (uint64_t pass = 0; pass < max_samples; ++pass) {
+    const bool fused_now = ns == 1 && (g_fused < 0 ? (g_lds && c.sc.hot_bytes > 0) : g_fused != 0);
+    const bool pipe = !bdpt && fused_now && g_pipeline;
+    if (pipe) {
+        const lumo_status ps = render_pipelined(c, S, T, D, dump_p, N, (int)n_tasks, dim_stride, max_samples, max_P, st);
+        if (ps) return ps;
+        if (st) return st;
+    }
+    for (uint64_t pass = 0; pass < (pipe ? 0 : max_samples); ++pass) {
         if (dump_host) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, sm));
         HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));
         {
@@ -947,14 +1060,13 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                         break;
                     }
                     const uint32_t* k = c.snap + CNT_N * (consumed % Ctx::SNAP_RING);
-                    closest_q += k[CNT_CUR];
                     bounces += k[CNT_CUR] > 0 ? 1 : 0;
                     ub = k[CNT_NEXT];
                     done = done || ub == 0;
                     consumed++;
                 }
                 if (done) break;
-                k_bounce_begin<<<1, 64, 0, sm>>>(S.counts);
+                k_bounce_begin<<<1, 64, 0, sm>>>(S.counts, S.tcount + TC_HEADQ);
                 step(ub, issued, qa, qb);
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipMemcpyAsync(c.snap + CNT_N * (issued % Ctx::SNAP_RING), S.counts, sizeof(uint32_t) * CNT_N,
@@ -985,8 +1097,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                         launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true);
                     });
                 }
-                const bool fused = g_fused < 0 ? (g_lds && c.sc.hot_bytes > 0) : g_fused != 0;
-                if (ns == 1 && fused) {  // one fused kernel per bounce (pt.h k_bounce_q)
+                if (fused_now) {  // one fused kernel per bounce (pt.h k_bounce_q)
                     StageTimer tm(c, g_timing, ST_CLOSEST);
                     launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
                         launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, false);
@@ -1244,10 +1355,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         for (size_t i = 0; i < n_tasks; ++i) total_q += queries[i];
         // per-slot query counters: PT 1 per closest + 1 per valid record; BDPT walk traces (the
         // bounce snapshots) + connection / re-run queries
-        const unsigned long long all_closest = closest_q + tc[TC_TAILQ];
-        shadow_q = total_q >= all_closest ? total_q - all_closest : 0;
+        closest_q = tc[TC_HEADQ] + tc[TC_TAILQ];  // bounce heads + the tail kernel's further bounces
+        shadow_q = total_q >= closest_q ? total_q - closest_q : 0;
     }
-    closest_q += tc[TC_TAILQ];  // k_bounce_q tail mode: the bounces past its first
     c.stats.closest_queries += closest_q;
     c.stats.shadow_queries += shadow_q;
     c.stats.bounces += bounces;
@@ -1315,6 +1425,15 @@ lumo_status lumo_create(int device, void** ctx_out) {
         delete c;
         return LUMO_ERR_HIP;
     }
+    if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return LUMO_ERR_HIP;
+    }
+    for (int i = 0; i < 2; ++i) {
+        (void)hipEventCreateWithFlags(&c->pass_ev[i], hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&c->tail_ev[i], hipEventDisableTiming);
+    }
     for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventCreate(&c->ev[i]);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventCreateWithFlags(&c->snap_ev[i], hipEventDisableTiming);
     if (hipHostMalloc(reinterpret_cast<void**>(&c->snap), sizeof(uint32_t) * CNT_N * Ctx::SNAP_RING) != hipSuccess) {
@@ -1330,6 +1449,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_FUSED")) g_fused = std::atoi(e);
     if (const char* e = std::getenv("LUMO_QSORT")) g_qsort = std::atoi(e) & 3;
     if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("LUMO_PIPELINE")) g_pipeline = e[0] != '0';
     const char* tm = std::getenv("LUMO_TIMING");
     g_timing = tm && tm[0] == '1';
     *ctx_out = c;
@@ -1341,12 +1461,18 @@ void lumo_destroy(void* ctx) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream2);
     free_scene(*c);
     for (DevBuf& b : c->work)
         if (b.p) (void)hipFree(b.p);
     for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventDestroy(c->ev[i]);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventDestroy(c->snap_ev[i]);
     if (c->snap) (void)hipHostFree(c->snap);
+    for (int i = 0; i < 2; ++i) {
+        (void)hipEventDestroy(c->pass_ev[i]);
+        (void)hipEventDestroy(c->tail_ev[i]);
+    }
+    (void)hipStreamDestroy(c->stream2);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1808,9 +1934,10 @@ lumo_status lumo_debug_stream(void* ctx, size_t n) {
 
 void lumo_set_timing(int on) { g_timing = on != 0; }
 void lumo_set_lds_staging(int on) { g_lds = on != 0; }
-void lumo_set_bounce_mode(int fused, uint32_t tail_below) {
+void lumo_set_bounce_mode(int fused, uint32_t tail_below, int pipeline) {
     g_fused = fused < 0 ? -1 : (fused != 0 ? 1 : 0);
     g_tail_below = tail_below;
+    g_pipeline = pipeline != 0;
 }
 
 lumo_status lumo_stats_reset(void* ctx) {

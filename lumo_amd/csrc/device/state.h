@@ -59,7 +59,8 @@ constexpr int NB = 8;
 enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
 constexpr int TC_RESOLVED = 2 * TC_N;  // + shadow records answered without traversal; W_TCOUNT has TC_ALL
 constexpr int TC_TAILQ = 2 * TC_N + 1;  // + closest queries run by k_bounce_q in tail mode past its first bounce
-constexpr int TC_ALL = 2 * TC_N + 2;
+constexpr int TC_HEADQ = 2 * TC_N + 2;  // + closest queries of the bounce heads (k_bounce_begin)
+constexpr int TC_ALL = 2 * TC_N + 3;
 #ifndef LUMO_SHADOW_STATS
 #define LUMO_SHADOW_STATS 0
 #endif

@@ -198,12 +198,12 @@ def test_kernel_variants(dev, variant_env, name, cls, lds, full):
         assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
 
 
-@pytest.mark.parametrize("fused,tail", [(1, 0), (1, 300), (0, 1 << 30)])
-def test_bounce_modes_small_dragon(dev, fused, tail):
+@pytest.mark.parametrize("fused,tail,pipe", [(1, 0, 0), (1, 300, 0), (0, 1 << 30, 0), (1, 0, 1)])
+def test_bounce_modes_small_dragon(dev, fused, tail, pipe):
     """The fused bounce kernel and the tail kernel on an instanced glass mesh (feature class 1,
     no LDS staging, deep kd stack): paths and tiles equal the oracle's."""
     lib = _ffi.load()
-    lib.lumo_set_bounce_mode(fused, tail)
+    lib.lumo_set_bounce_mode(fused, tail, pipe)
     try:
         sc, cam, tasks = _variant_scene("small_dragon")
         sc.build()
@@ -219,4 +219,4 @@ def test_bounce_modes_small_dragon(dev, fused, tail):
             np.testing.assert_array_equal(b, ob)
             assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
     finally:
-        lib.lumo_set_bounce_mode(-1, 1 << 18)
+        lib.lumo_set_bounce_mode(-1, 1 << 18, 1)
