@@ -170,8 +170,9 @@ __global__ void k_bounce_begin(uint32_t* counts, unsigned long long* headq) {
         *headq += counts[CNT_NEXT];  // this bounce's closest queries (one per queued path)
         counts[CNT_CUR] = counts[CNT_NEXT];
         counts[CNT_NEXT] = 0;
-        counts[CNT_SHADOW] = 0;
-        counts[CNT_RESOLVE] = 0;
+        counts[CNT_FETCH_B] = 0;
+        counts[CNT_FETCH_C] = 0;
+        counts[CNT_FETCH_T] = 0;
         for (int b = 0; b < NB; ++b) counts[CNT_BUCKET0 + b] = 0;
     }
 }
@@ -720,6 +721,7 @@ int g_buckets = NB;  // LUMO_BUCKETS=0: NEE records not grouped by origin object
 int g_fused = -1;  // n_shadow == 1: k_bounce_q instead of closest / shade / shadow (-1: when the scene is LDS-staged)
 uint32_t g_tail_below = 1u << 18;  // n_shadow == 1: k_bounce_q tail mode below this many live paths
 bool g_pipeline = true;            // fused passes overlapped on two streams (render_pipelined)
+int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from a counter
 int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
 template <typename F>
 void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr) {
@@ -778,7 +780,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
             launch_trav(
                 c, (uint64_t)N,
                 [&](auto K, const TravLaunch& l) {
-                    launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[b & 1], P.qs[(b + 1) & 1], 0u, false);
+                    launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[b & 1], P.qs[(b + 1) & 1], 0u, false, g_dyn);
                 },
                 A);
         }
@@ -794,7 +796,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
                 c, (uint64_t)N,
                 [&](auto K, const TravLaunch& l) {
                     launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[heads & 1], P.qs[(heads + 1) & 1],
-                                                        0xffffffffu, true);
+                                                        0xffffffffu, true, 0);
                 },
                 B);
         }
@@ -1094,13 +1096,13 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 if (skip > 0) {
                     StageTimer tm(c, g_timing, ST_RESOLVE);
                     launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
-                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true);
+                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true, 0);
                     });
                 }
                 if (fused_now) {  // one fused kernel per bounce (pt.h k_bounce_q)
                     StageTimer tm(c, g_timing, ST_CLOSEST);
                     launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
-                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, false);
+                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, false, g_dyn);
                     });
                     return;
                 }
@@ -1450,6 +1452,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_QSORT")) g_qsort = std::atoi(e) & 3;
     if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("LUMO_PIPELINE")) g_pipeline = e[0] != '0';
+    if (const char* e = std::getenv("LUMO_DYN")) g_dyn = std::atoi(e);
     const char* tm = std::getenv("LUMO_TIMING");
     g_timing = tm && tm[0] == '1';
     *ctx_out = c;

@@ -61,7 +61,9 @@ __global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest_q(DScene 
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     const HitQ hq = S.hq;
     Counters C{0, 0, 0};
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
+    for (uint32_t w0 = wave_fetch(S.counts + CNT_FETCH_C); w0 < count; w0 = wave_fetch(S.counts + CNT_FETCH_C)) {
+        const uint32_t q = w0 + lane_id();
+        if (q >= count) continue;
         const RayX r = rayx(Ray{qv3(cur, QD_O, q), qv3(cur, QD_D, q)});
         const HitRef h = scene_hit<STK, FX>(sc, r, C);
         hq.t[q] = h.t;
@@ -330,6 +332,8 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc
     const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
     const ShadowQ Q = S.sq;
     Counters C{0, 0, 0};
+    // static stride: with 11 pairs per path, one fetch atomic per wave (~350 k per C3 bounce on one
+    // counter) cost more than the balance gained (C3 shadow 560 -> 639 ms per 8-spp frame)
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
         uint32_t lj = j;
         int bk = 0;
@@ -647,7 +651,7 @@ __device__ __forceinline__ void store_final(const Paths& S, const PathReg& P) { 
 template <int STK, bool LDS, int FX, bool TAIL>
 __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_q(DScene sc0, Paths S, Tasks T,
                                                                                   QState cur, QState nxt,
-                                                                                  uint32_t tail_below) {
+                                                                                  uint32_t tail_below, int dyn) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
     if ((count < tail_below) != TAIL) return;      // the other kernel takes this bounce
@@ -656,15 +660,26 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
     Counters Cc{0, 0, 0, 0}, Cs{0, 0, 0, 0};
     if constexpr (TAIL) {
         uint32_t tailq = 0;
-        for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
+        for (uint32_t w0 = wave_fetch(S.counts + CNT_FETCH_T); w0 < count; w0 = wave_fetch(S.counts + CNT_FETCH_T)) {
+            const uint32_t q = w0 + lane_id();
+            if (q >= count) continue;
             PathReg P = load_path(cur, q);
             while (bounce_path<STK, FX>(sc, T.delta, P, Cc, Cs)) tailq++;
             store_final(S, P);
         }
         flush_resolved(tailq, S.tcount + TC_TAILQ);
     } else {
-        // grid-stride over whole blocks: block_slot needs every thread of the block each round
-        for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
+        // Whole blocks of the queue; block_slot needs every thread of the block each round.  With
+        // `dyn`, a persistent block takes its next 256 paths from a counter (CNT_FETCH_B, zeroed by
+        // k_bounce_begin) instead of a fixed grid stride, so CUs whose paths ran long take fewer.
+        __shared__ uint32_t next_base;
+        uint32_t base = blockIdx.x * blockDim.x;
+        if (dyn) {
+            if (threadIdx.x == 0) next_base = atomicAdd(S.counts + CNT_FETCH_B, (uint32_t)blockDim.x);
+            __syncthreads();
+            base = next_base;
+        }
+        while (base < count) {
             const uint32_t q = base + threadIdx.x;
             const bool live = q < count;
             // phase 1: Scene::hit (k_closest_q)
@@ -775,6 +790,14 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                     qc(nxt, QD_P, np, X);
                 else  // the radiance stored above, re-read by the thread that wrote it
                     stc(S.rad, P.slot, ldc(S.rad, P.slot) + X);
+            }
+            if (dyn) {
+                __syncthreads();  // every thread has read next_base
+                if (threadIdx.x == 0) next_base = atomicAdd(S.counts + CNT_FETCH_B, (uint32_t)blockDim.x);
+                __syncthreads();
+                base = next_base;
+            } else {
+                base += gridDim.x * blockDim.x;
             }
         }
     }

@@ -50,7 +50,9 @@ enum Stage {
 static_assert(ST_COUNT == LUMO_STAGE_COUNT, "stage slots match lumo_stats");
 // Device-side queue counters: the bounce kernels read their counts from here, so the host never
 // waits for a count before launching the next stage.
-enum { CNT_NEXT = 0, CNT_SHADOW, CNT_RESOLVE, CNT_CUR, CNT_BUCKET0, CNT_N = CNT_BUCKET0 + 8 };
+// CNT_FETCH_*: work counters from which the kernels' waves / blocks take their next paths
+// (dynamic load balance; k_bounce_begin zeroes them every bounce).
+enum { CNT_NEXT = 0, CNT_FETCH_B, CNT_FETCH_C, CNT_FETCH_T, CNT_CUR, CNT_BUCKET0, CNT_N = CNT_BUCKET0 + 8 };
 // k_shade_q files each path's NEE records into one of NB buckets by the shadow rays' origin
 // object (objects, then lights, mod NB), each bucket a contiguous segment of the record queue, so
 // that a wave's visibility queries start on the same surface and walk the same BVH / kd nodes
@@ -261,6 +263,15 @@ __device__ __forceinline__ uint32_t block_slot_sorted(bool pred, int key, uint32
     const uint32_t pos = pred ? base_s + hist[key] + rank : 0u;
     __syncthreads();
     return pos;
+}
+
+// The wave's next 64 work items from counter `ctr` (one atomic per wave): waves whose items ran
+// long take fewer, so a kernel's waves finish together instead of waiting for the slowest
+// statically assigned stripe.  Returns the first item index (uniform over the wave).
+__device__ __forceinline__ uint32_t wave_fetch(uint32_t* ctr) {
+    uint32_t b = 0;
+    if (lane_id() == 0) b = atomicAdd(ctr, 64u);
+    return __shfl(b, 0, 64);
 }
 
 // Wave-reduced traversal counters (one atomic per wavefront).
