@@ -374,9 +374,10 @@ void lumo_set_lds_staging(int on);
  * the NEE pair traced from registers); fused = -1 (default): fused when the scene is staged in
  * LDS (small scenes), else three kernels.  Bounces are preceded by a tail kernel that takes the
  * bounce instead when fewer than tail_below paths are alive and runs each of them to its end in
- * that launch (tail_below = 0: never; default 262144).  pipeline = 1 (default), with fused
- * bounces: each pass runs its first bounces on one stream and hands the rest (tail kernel, film,
- * ring) to a second stream while the next pass starts.  Every mode gives bit-identical results.
+ * that launch (tail_below = 0: never; default 262144).  pipeline (with fused bounces): 1 each
+ * pass runs its first bounces on a head stream and hands the rest (tail kernel, film, ring) to a
+ * second stream while the next pass starts; 2 (default) alternates two head streams so
+ * consecutive passes' first bounces also overlap; 0 off.  Every mode gives bit-identical results.
  * Also LUMO_FUSED / LUMO_TAIL / LUMO_PIPELINE in the environment. */
 void lumo_set_bounce_mode(int fused, uint32_t tail_below, int pipeline);
 

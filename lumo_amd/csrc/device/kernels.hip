@@ -167,7 +167,7 @@ __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, in
 // Start of a bounce: the alive queue just built becomes the current one.
 __global__ void k_bounce_begin(uint32_t* counts, unsigned long long* headq) {
     if (threadIdx.x == 0) {
-        *headq += counts[CNT_NEXT];  // this bounce's closest queries (one per queued path)
+        atomicAdd(headq, (unsigned long long)counts[CNT_NEXT]);  // this bounce's closest queries (streams run concurrently)
         counts[CNT_CUR] = counts[CNT_NEXT];
         counts[CNT_NEXT] = 0;
         counts[CNT_FETCH_B] = 0;
@@ -558,7 +558,8 @@ struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // pipelined passes: each pass's tail, film and ring
-    hipEvent_t pass_ev[2] = {nullptr, nullptr}, tail_ev[2] = {nullptr, nullptr};
+    hipStream_t stream3 = nullptr;  // pipelined passes (2 head streams): odd passes' first bounces
+    hipEvent_t pass_ev[3] = {}, tail_ev[3] = {}, cam_ev[3] = {};
     bool has_scene = false, has_camera = false;
     DScene sc{};
     DCam cam{};
@@ -625,7 +626,8 @@ enum WorkId {
     W_BD_CAMO, W_BD_CAMD, W_BD_RNG0, W_BD_LAM0, W_BDR_DRAWS, W_BDR_OK, W_BD_NB, W_BD_OFFB, W_BD_TERMB, W_BD_VIS, W_BD_AT, W_BD_AKIND, W_BD_AOBJ,
     W_BD_ATRI, W_CHECKS, W_QS0_D, W_QS0_R, W_QS0_I, W_QS1_D, W_QS1_R, W_QS1_I, W_HQ_T, W_HQ_I, W_SQ_D, W_SQ_I,
     W_SQ_HD, W_SQ_HI, W_SQ_HR, W_RAD2, W_LAM2, W_RASTER2, W_DEPTH2, W_QUERIES2, W_P_VALID2, W_COUNTS2, W_QS2_D,
-    W_QS2_R, W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I, W_COUNT
+    W_QS2_R, W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I, W_RAD3, W_LAM3, W_RASTER3, W_DEPTH3, W_QUERIES3, W_P_VALID3,
+    W_COUNTS3, W_QS4_D, W_QS4_R, W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I, W_COUNT
 };
 
 template <typename T>
@@ -720,8 +722,9 @@ bool g_lds = true;
 int g_buckets = NB;  // LUMO_BUCKETS=0: NEE records not grouped by origin object
 int g_fused = -1;  // n_shadow == 1: k_bounce_q instead of closest / shade / shadow (-1: when the scene is LDS-staged)
 uint32_t g_tail_below = 1u << 18;  // n_shadow == 1: k_bounce_q tail mode below this many live paths
-bool g_pipeline = true;            // fused passes overlapped on two streams (render_pipelined)
+int g_pipeline = 2;                // fused passes overlapped (render_pipelined): 0 off, 1 one head stream, 2 two
 int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from a counter
+int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
 int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
 template <typename F>
 void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr) {
@@ -743,51 +746,75 @@ void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr) {
 // sequential loop, so the result is bit-identical.
 lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump_p, int N, int n_tasks, int dim_stride,
                              uint64_t max_samples, uint64_t max_P, lumo_status& st) {
-    Paths S1 = S;  // odd passes
-    S1.rad = wbuf<double>(c, W_RAD2, 4 * (size_t)N, st);
-    S1.lam = wbuf<double>(c, W_LAM2, 4 * (size_t)N, st);
-    S1.raster = wbuf<double>(c, W_RASTER2, 2 * (size_t)N, st);
-    S1.depth = wbuf<uint32_t>(c, W_DEPTH2, N, st);
-    S1.queries = wbuf<uint32_t>(c, W_QUERIES2, N, st);
-    S1.p_valid = wbuf<uint32_t>(c, W_P_VALID2, N, st);
-    S1.counts = wbuf<uint32_t>(c, W_COUNTS2, CNT_N, st);
-    for (int k = 0; k < 2; ++k) {
-        S1.qs[k].cap = (size_t)N;
-        S1.qs[k].d = wbuf<double>(c, k ? W_QS3_D : W_QS2_D, QD_N * (size_t)N, st);
-        S1.qs[k].r = wbuf<uint64_t>(c, k ? W_QS3_R : W_QS2_R, 2 * (size_t)N, st);
-        S1.qs[k].i = wbuf<int32_t>(c, k ? W_QS3_I : W_QS2_I, QI_N * (size_t)N, st);
+    // NA head streams (1 or 2, g_pipeline): with 2, the first bounces of consecutive passes also
+    // run concurrently (filling the GPU when a rank holds few slots); NS = NA + 1 sets of queues,
+    // counters and per-slot outputs, so a set is reused only after the pass three back has
+    // finished its film.
+    const int NA = g_pipeline >= 2 ? 2 : 1, NSETS = NA + 1;
+    Paths P3[3] = {S, S, S};
+    const int wid[2][16] = {{W_RAD2, W_LAM2, W_RASTER2, W_DEPTH2, W_QUERIES2, W_P_VALID2, W_COUNTS2, W_QS2_D, W_QS2_R,
+                             W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I},
+                            {W_RAD3, W_LAM3, W_RASTER3, W_DEPTH3, W_QUERIES3, W_P_VALID3, W_COUNTS3, W_QS4_D, W_QS4_R,
+                             W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I}};
+    for (int k = 1; k < NSETS; ++k) {
+        const int* w = wid[k - 1];
+        Paths& Q = P3[k];
+        Q.rad = wbuf<double>(c, w[0], 4 * (size_t)N, st);
+        Q.lam = wbuf<double>(c, w[1], 4 * (size_t)N, st);
+        Q.raster = wbuf<double>(c, w[2], 2 * (size_t)N, st);
+        Q.depth = wbuf<uint32_t>(c, w[3], N, st);
+        Q.queries = wbuf<uint32_t>(c, w[4], N, st);
+        Q.p_valid = wbuf<uint32_t>(c, w[5], N, st);
+        Q.counts = wbuf<uint32_t>(c, w[6], CNT_N, st);
+        for (int h = 0; h < 2; ++h) {
+            Q.qs[h].cap = (size_t)N;
+            Q.qs[h].d = wbuf<double>(c, w[7 + 3 * h], QD_N * (size_t)N, st);
+            Q.qs[h].r = wbuf<uint64_t>(c, w[8 + 3 * h], 2 * (size_t)N, st);
+            Q.qs[h].i = wbuf<int32_t>(c, w[9 + 3 * h], QI_N * (size_t)N, st);
+        }
     }
     if (st) return st;
-    hipStream_t A = c.stream, B = c.stream2;
-    // "pass -1": the setup enqueued on A so far (tasks, memsets, the initial ring); B first waits
-    // for pass 0's heads on A, so it sees the setup too
-    HIPCHK(hipEventRecord(c.pass_ev[1], A));
+    hipStream_t As[2] = {c.stream, c.stream3}, B = c.stream2;
+    // every event starts "done" after the setup enqueued on stream 0 (tasks, memsets, the initial
+    // ring): pass p waits for pass p - NSETS's film before reusing its set, for pass p - 1's camera
+    // (the sampler state is per slot) and, before bounce RR_DEPTH, for pass p - 1's ring
+    for (int k = 0; k < 3; ++k) {
+        HIPCHK(hipEventRecord(c.pass_ev[k], As[0]));
+        HIPCHK(hipEventRecord(c.cam_ev[k], As[0]));
+    }
     const int gN = ceil_div(N, BLOCK);
-    const int heads = RR_DEPTH + 1;  // bounces 0..RR_DEPTH on A
+    const int heads = RR_DEPTH + 1;  // bounces 0..RR_DEPTH on the head stream
     for (uint64_t pass = 0; pass < max_samples; ++pass) {
-        const int par = (int)(pass & 1);
-        Paths& P = par ? S1 : S;
-        // ---- stream A: camera + the first bounces
+        const int set = (int)(pass % NSETS), prev = (int)((pass + NSETS - 1) % NSETS);
+        hipStream_t A = As[pass % NA];
+        Paths& P = P3[set];
+        // ---- head stream: camera + the first bounces
+        if (NA > 1) {
+            HIPCHK(hipStreamWaitEvent(A, c.pass_ev[set], 0));  // pass - NSETS done with this set
+            HIPCHK(hipStreamWaitEvent(A, c.cam_ev[prev], 0));  // pass - 1's camera (sampler state)
+        }
         HIPCHK(hipMemsetAsync(P.counts, 0, sizeof(uint32_t) * CNT_N, A));
         {
             StageTimer tm(c, g_timing, ST_CAMERA, A);
             k_camera<true><<<gN, BLOCK, 0, A>>>(T, P, c.cam, N, dim_stride, (uint32_t)pass);
         }
+        HIPCHK(hipEventRecord(c.cam_ev[set], A));
         for (int b = 0; b < heads; ++b) {
-            if (b == RR_DEPTH) HIPCHK(hipStreamWaitEvent(A, c.pass_ev[par ^ 1], 0));  // this pass's delta
+            if (b == RR_DEPTH) HIPCHK(hipStreamWaitEvent(A, c.pass_ev[prev], 0));  // this pass's delta
             k_bounce_begin<<<1, 64, 0, A>>>(P.counts, P.tcount + TC_HEADQ);
             StageTimer tm(c, g_timing, ST_CLOSEST, A);
             launch_trav(
                 c, (uint64_t)N,
                 [&](auto K, const TravLaunch& l) {
-                    launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[b & 1], P.qs[(b + 1) & 1], 0u, false, g_dyn);
+                    launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[b & 1], P.qs[(b + 1) & 1], 0u, false,
+                                                        g_dyn, g_bounce_threads);
                 },
                 A);
         }
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c.tail_ev[par], A));
+        HIPCHK(hipEventRecord(c.tail_ev[set], A));
         // ---- stream B: the rest of the pass, film, ring
-        HIPCHK(hipStreamWaitEvent(B, c.tail_ev[par], 0));
+        HIPCHK(hipStreamWaitEvent(B, c.tail_ev[set], 0));
         if (D.delta) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, B));
         k_bounce_begin<<<1, 64, 0, B>>>(P.counts, P.tcount + TC_HEADQ);
         {
@@ -796,7 +823,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
                 c, (uint64_t)N,
                 [&](auto K, const TravLaunch& l) {
                     launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[heads & 1], P.qs[(heads + 1) & 1],
-                                                        0xffffffffu, true, 0);
+                                                        0xffffffffu, true, 0, BLOCK);
                 },
                 B);
         }
@@ -817,11 +844,11 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
             k_ring<<<n_tasks, 64, 0, B>>>(P, T, n_tasks, 1);
         }
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c.pass_ev[par], B));
+        HIPCHK(hipEventRecord(c.pass_ev[set], B));
         if (g_timing) resolve_timers(c);
     }
-    // the results are copied on A: after the last pass's ring
-    HIPCHK(hipStreamWaitEvent(A, c.pass_ev[(max_samples - 1) & 1], 0));
+    // the results are copied on stream 0: after the last pass's ring
+    HIPCHK(hipStreamWaitEvent(As[0], c.pass_ev[(max_samples - 1) % NSETS], 0));
     return LUMO_OK;
 }
 
@@ -1096,13 +1123,13 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 if (skip > 0) {
                     StageTimer tm(c, g_timing, ST_RESOLVE);
                     launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
-                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true, 0);
+                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true, 0, BLOCK);
                     });
                 }
                 if (fused_now) {  // one fused kernel per bounce (pt.h k_bounce_q)
                     StageTimer tm(c, g_timing, ST_CLOSEST);
                     launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
-                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, false, g_dyn);
+                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, false, g_dyn, g_bounce_threads);
                     });
                     return;
                 }
@@ -1427,14 +1454,16 @@ lumo_status lumo_create(int device, void** ctx_out) {
         delete c;
         return LUMO_ERR_HIP;
     }
-    if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
         delete c;
         return LUMO_ERR_HIP;
     }
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
         (void)hipEventCreateWithFlags(&c->pass_ev[i], hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&c->tail_ev[i], hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&c->cam_ev[i], hipEventDisableTiming);
     }
     for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventCreate(&c->ev[i]);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventCreateWithFlags(&c->snap_ev[i], hipEventDisableTiming);
@@ -1451,8 +1480,12 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_FUSED")) g_fused = std::atoi(e);
     if (const char* e = std::getenv("LUMO_QSORT")) g_qsort = std::atoi(e) & 3;
     if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("LUMO_PIPELINE")) g_pipeline = e[0] != '0';
+    if (const char* e = std::getenv("LUMO_PIPELINE")) g_pipeline = std::atoi(e);
     if (const char* e = std::getenv("LUMO_DYN")) g_dyn = std::atoi(e);
+    if (const char* e = std::getenv("LUMO_BOUNCE_THREADS")) {
+        const int t = std::atoi(e);
+        g_bounce_threads = (t == 64 || t == 128) ? t : BLOCK;
+    }
     const char* tm = std::getenv("LUMO_TIMING");
     g_timing = tm && tm[0] == '1';
     *ctx_out = c;
@@ -1465,16 +1498,19 @@ void lumo_destroy(void* ctx) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->stream2);
+    (void)hipStreamSynchronize(c->stream3);
     free_scene(*c);
     for (DevBuf& b : c->work)
         if (b.p) (void)hipFree(b.p);
     for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventDestroy(c->ev[i]);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventDestroy(c->snap_ev[i]);
     if (c->snap) (void)hipHostFree(c->snap);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
         (void)hipEventDestroy(c->pass_ev[i]);
         (void)hipEventDestroy(c->tail_ev[i]);
+        (void)hipEventDestroy(c->cam_ev[i]);
     }
+    (void)hipStreamDestroy(c->stream3);
     (void)hipStreamDestroy(c->stream2);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1940,7 +1976,7 @@ void lumo_set_lds_staging(int on) { g_lds = on != 0; }
 void lumo_set_bounce_mode(int fused, uint32_t tail_below, int pipeline) {
     g_fused = fused < 0 ? -1 : (fused != 0 ? 1 : 0);
     g_tail_below = tail_below;
-    g_pipeline = pipeline != 0;
+    g_pipeline = pipeline;
 }
 
 lumo_status lumo_stats_reset(void* ctx) {

@@ -673,6 +673,10 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
         // `dyn`, a persistent block takes its next 256 paths from a counter (CNT_FETCH_B, zeroed by
         // k_bounce_begin) instead of a fixed grid stride, so CUs whose paths ran long take fewer.
         __shared__ uint32_t next_base;
+        // the B record waits here (not in VGPRs) for phase 3: 12 planes of blockDim.x doubles in the
+        // dynamic LDS after the staged scene
+        double* rb_lds = reinterpret_cast<double*>(lds_scene + (LDS ? (sc0.hot_bytes + 15u) / 16u * 16u : 0u));
+        const uint32_t nt = blockDim.x;
         uint32_t base = blockIdx.x * blockDim.x;
         if (dyn) {
             if (threadIdx.x == 0) next_base = atomicAdd(S.counts + CNT_FETCH_B, (uint32_t)blockDim.x);
@@ -693,7 +697,6 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
             double pdf_light = 1.0;
             DColor g_nee = cfill(0.0);
             Ray rn{V3{0, 0, 0}, V3{0, 0, 0}};
-            __shared__ double rb_lds[12][BLOCK];  // the B record waits here (not in VGPRs) for phase 3
             if (live) {
                 P = load_path(cur, q);
                 P.queries += 1u;
@@ -726,7 +729,7 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                                                       RB.ray.d.z, RB.f.s[0], RB.f.s[1], RB.f.s[2], RB.f.s[3],
                                                       RB.pdf, RB.cosv};
 #pragma unroll
-                                for (int k = 0; k < 12; ++k) rb_lds[k][threadIdx.x] = v[k];
+                                for (int k = 0; k < 12; ++k) rb_lds[k * nt + threadIdx.x] = v[k];
                             }
                             P.queries += 1u + (ok ? 1u : 0u);
                         }
@@ -776,12 +779,11 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                 DColor b = cfill(0.0);
                 if (ok) {
                     NeeRec RB;
-                    RB.ray = Ray{V3{rb_lds[0][threadIdx.x], rb_lds[1][threadIdx.x], rb_lds[2][threadIdx.x]},
-                                 V3{rb_lds[3][threadIdx.x], rb_lds[4][threadIdx.x], rb_lds[5][threadIdx.x]}};
-                    RB.f = DColor{{rb_lds[6][threadIdx.x], rb_lds[7][threadIdx.x], rb_lds[8][threadIdx.x],
-                                   rb_lds[9][threadIdx.x]}};
-                    RB.pdf = rb_lds[10][threadIdx.x];
-                    RB.cosv = rb_lds[11][threadIdx.x];
+                    const double* v = rb_lds + threadIdx.x;
+                    RB.ray = Ray{V3{v[0], v[nt], v[2 * nt]}, V3{v[3 * nt], v[4 * nt], v[5 * nt]}};
+                    RB.f = DColor{{v[6 * nt], v[7 * nt], v[8 * nt], v[9 * nt]}};
+                    RB.pdf = v[10 * nt];
+                    RB.cosv = v[11 * nt];
                     b = shadow_record_r<STK, FX>(sc, RB, li, false, P.L, Cs);
                 }
                 const DColor single = (cfill(0.0) + a + b) / pdf_light;

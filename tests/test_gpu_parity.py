@@ -191,12 +191,12 @@ def test_separate_result_buffers_match_oracle(dev, cornell, max_paths):
 
 
 @pytest.mark.parametrize("fused,tail,pipe", [(0, 0, 0), (0, 300, 0), (0, 1 << 30, 0), (1, 0, 0), (1, 300, 0),
-                                             (1, 1 << 30, 0), (1, 0, 1), (-1, 1 << 18, 1)])
+                                             (1, 1 << 30, 0), (1, 0, 1), (-1, 1 << 18, 1), (-1, 1 << 18, 2)])
 def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
     """The three-kernel bounce and the fused bounce kernel (k_bounce_q: closest hit + shading +
     NEE pair in one launch), each without the tail kernel (tail 0), with the tail entered
     mid-pass (tail 300) and with every path run to its end in one launch (tail 2^30), and the
-    pipelined passes (fused bounces on one stream, tail / film / ring on another): paths,
+    pipelined passes (fused bounces on one or two head streams, tail / film / ring on another): paths,
     tiles and the closest / shadow query counts all equal the oracle's.  (Traversal counters are
     not compared here: the device answers p_sct == 0 records without traversal, the oracle
     traces them; lumo_trace's counter parity is in test_gpu_trace / test_gpu_scale.)"""
@@ -218,4 +218,4 @@ def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
         assert after.closest_queries - before.closest_queries == cnt.closest_queries
         assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
     finally:
-        lib.lumo_set_bounce_mode(-1, 1 << 18, 1)
+        lib.lumo_set_bounce_mode(-1, 1 << 18, 2)
