@@ -558,8 +558,9 @@ struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // pipelined passes: each pass's tail, film and ring
-    hipStream_t stream3 = nullptr;  // pipelined passes (2 head streams): odd passes' first bounces
-    hipEvent_t pass_ev[3] = {}, tail_ev[3] = {}, cam_ev[3] = {};
+    hipStream_t stream3 = nullptr;  // pipelined passes (2-3 head streams): further head streams
+    hipStream_t stream4 = nullptr;
+    hipEvent_t pass_ev[4] = {}, tail_ev[4] = {}, cam_ev[4] = {};
     bool has_scene = false, has_camera = false;
     DScene sc{};
     DCam cam{};
@@ -627,7 +628,8 @@ enum WorkId {
     W_BD_ATRI, W_CHECKS, W_QS0_D, W_QS0_R, W_QS0_I, W_QS1_D, W_QS1_R, W_QS1_I, W_HQ_T, W_HQ_I, W_SQ_D, W_SQ_I,
     W_SQ_HD, W_SQ_HI, W_SQ_HR, W_RAD2, W_LAM2, W_RASTER2, W_DEPTH2, W_QUERIES2, W_P_VALID2, W_COUNTS2, W_QS2_D,
     W_QS2_R, W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I, W_RAD3, W_LAM3, W_RASTER3, W_DEPTH3, W_QUERIES3, W_P_VALID3,
-    W_COUNTS3, W_QS4_D, W_QS4_R, W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I, W_COUNT
+    W_COUNTS3, W_QS4_D, W_QS4_R, W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I, W_RAD4, W_LAM4, W_RASTER4, W_DEPTH4,
+    W_QUERIES4, W_P_VALID4, W_COUNTS4, W_QS6_D, W_QS6_R, W_QS6_I, W_QS7_D, W_QS7_R, W_QS7_I, W_COUNT
 };
 
 template <typename T>
@@ -722,7 +724,7 @@ bool g_lds = true;
 int g_buckets = NB;  // LUMO_BUCKETS=0: NEE records not grouped by origin object
 int g_fused = -1;  // n_shadow == 1: k_bounce_q instead of closest / shade / shadow (-1: when the scene is LDS-staged)
 uint32_t g_tail_below = 1u << 18;  // n_shadow == 1: k_bounce_q tail mode below this many live paths
-int g_pipeline = 2;                // fused passes overlapped (render_pipelined): 0 off, 1 one head stream, 2 two
+int g_pipeline = 3;                // fused passes overlapped (render_pipelined): 0 off, else the number of head streams (1-3)
 int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from a counter
 int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
 int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
@@ -746,16 +748,18 @@ void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr) {
 // sequential loop, so the result is bit-identical.
 lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump_p, int N, int n_tasks, int dim_stride,
                              uint64_t max_samples, uint64_t max_P, lumo_status& st) {
-    // NA head streams (1 or 2, g_pipeline): with 2, the first bounces of consecutive passes also
-    // run concurrently (filling the GPU when a rank holds few slots); NS = NA + 1 sets of queues,
-    // counters and per-slot outputs, so a set is reused only after the pass three back has
-    // finished its film.
-    const int NA = g_pipeline >= 2 ? 2 : 1, NSETS = NA + 1;
-    Paths P3[3] = {S, S, S};
-    const int wid[2][16] = {{W_RAD2, W_LAM2, W_RASTER2, W_DEPTH2, W_QUERIES2, W_P_VALID2, W_COUNTS2, W_QS2_D, W_QS2_R,
+    // NA head streams (1 to 3, g_pipeline): with more than one, the first bounces of consecutive
+    // passes also run concurrently (filling the GPU when a rank holds few slots); NSETS = NA + 1
+    // sets of queues, counters and per-slot outputs, so a set is reused only after the pass
+    // NSETS back has finished its film.
+    const int NA = std::min(std::max(g_pipeline, 1), 3), NSETS = NA + 1;
+    Paths P3[4] = {S, S, S, S};
+    const int wid[3][16] = {{W_RAD2, W_LAM2, W_RASTER2, W_DEPTH2, W_QUERIES2, W_P_VALID2, W_COUNTS2, W_QS2_D, W_QS2_R,
                              W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I},
                             {W_RAD3, W_LAM3, W_RASTER3, W_DEPTH3, W_QUERIES3, W_P_VALID3, W_COUNTS3, W_QS4_D, W_QS4_R,
-                             W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I}};
+                             W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I},
+                            {W_RAD4, W_LAM4, W_RASTER4, W_DEPTH4, W_QUERIES4, W_P_VALID4, W_COUNTS4, W_QS6_D, W_QS6_R,
+                             W_QS6_I, W_QS7_D, W_QS7_R, W_QS7_I}};
     for (int k = 1; k < NSETS; ++k) {
         const int* w = wid[k - 1];
         Paths& Q = P3[k];
@@ -774,11 +778,11 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         }
     }
     if (st) return st;
-    hipStream_t As[2] = {c.stream, c.stream3}, B = c.stream2;
+    hipStream_t As[3] = {c.stream, c.stream3, c.stream4}, B = c.stream2;
     // every event starts "done" after the setup enqueued on stream 0 (tasks, memsets, the initial
     // ring): pass p waits for pass p - NSETS's film before reusing its set, for pass p - 1's camera
     // (the sampler state is per slot) and, before bounce RR_DEPTH, for pass p - 1's ring
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 4; ++k) {
         HIPCHK(hipEventRecord(c.pass_ev[k], As[0]));
         HIPCHK(hipEventRecord(c.cam_ev[k], As[0]));
     }
@@ -1455,12 +1459,13 @@ lumo_status lumo_create(int device, void** ctx_out) {
         return LUMO_ERR_HIP;
     }
     if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
         delete c;
         return LUMO_ERR_HIP;
     }
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 4; ++i) {
         (void)hipEventCreateWithFlags(&c->pass_ev[i], hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&c->tail_ev[i], hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&c->cam_ev[i], hipEventDisableTiming);
@@ -1499,17 +1504,19 @@ void lumo_destroy(void* ctx) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamSynchronize(c->stream2);
     (void)hipStreamSynchronize(c->stream3);
+    (void)hipStreamSynchronize(c->stream4);
     free_scene(*c);
     for (DevBuf& b : c->work)
         if (b.p) (void)hipFree(b.p);
     for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventDestroy(c->ev[i]);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventDestroy(c->snap_ev[i]);
     if (c->snap) (void)hipHostFree(c->snap);
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 4; ++i) {
         (void)hipEventDestroy(c->pass_ev[i]);
         (void)hipEventDestroy(c->tail_ev[i]);
         (void)hipEventDestroy(c->cam_ev[i]);
     }
+    (void)hipStreamDestroy(c->stream4);
     (void)hipStreamDestroy(c->stream3);
     (void)hipStreamDestroy(c->stream2);
     (void)hipStreamDestroy(c->stream);

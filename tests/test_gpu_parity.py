@@ -191,7 +191,7 @@ def test_separate_result_buffers_match_oracle(dev, cornell, max_paths):
 
 
 @pytest.mark.parametrize("fused,tail,pipe", [(0, 0, 0), (0, 300, 0), (0, 1 << 30, 0), (1, 0, 0), (1, 300, 0),
-                                             (1, 1 << 30, 0), (1, 0, 1), (-1, 1 << 18, 1), (-1, 1 << 18, 2)])
+                                             (1, 1 << 30, 0), (1, 0, 1), (-1, 1 << 18, 1), (-1, 1 << 18, 2), (-1, 1 << 18, 3)])
 def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
     """The three-kernel bounce and the fused bounce kernel (k_bounce_q: closest hit + shading +
     NEE pair in one launch), each without the tail kernel (tail 0), with the tail entered
@@ -218,4 +218,4 @@ def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
         assert after.closest_queries - before.closest_queries == cnt.closest_queries
         assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
     finally:
-        lib.lumo_set_bounce_mode(-1, 1 << 18, 2)
+        lib.lumo_set_bounce_mode(-1, 1 << 18, 3)

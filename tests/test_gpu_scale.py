@@ -198,7 +198,7 @@ def test_kernel_variants(dev, variant_env, name, cls, lds, full):
         assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
 
 
-@pytest.mark.parametrize("fused,tail,pipe", [(1, 0, 0), (1, 300, 0), (0, 1 << 30, 0), (1, 0, 1), (1, 0, 2)])
+@pytest.mark.parametrize("fused,tail,pipe", [(1, 0, 0), (1, 300, 0), (0, 1 << 30, 0), (1, 0, 1), (1, 0, 2), (1, 0, 3)])
 def test_bounce_modes_small_dragon(dev, fused, tail, pipe):
     """The fused bounce kernel and the tail kernel on an instanced glass mesh (feature class 1,
     no LDS staging, deep kd stack): paths and tiles equal the oracle's."""
@@ -219,4 +219,4 @@ def test_bounce_modes_small_dragon(dev, fused, tail, pipe):
             np.testing.assert_array_equal(b, ob)
             assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
     finally:
-        lib.lumo_set_bounce_mode(-1, 1 << 18, 2)
+        lib.lumo_set_bounce_mode(-1, 1 << 18, 3)
