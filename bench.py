@@ -77,7 +77,12 @@ def main():
     if ws > 1:
         import torch
         import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # LUMO_BENCH_BACKEND=gloo with more ranks than GPUs rehearses the multi-rank path on one
+        # GPU (RCCL refuses two ranks on one device); the driver's runs use RCCL, one GPU per rank
+        backend = os.environ.get("LUMO_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        n_dev = torch.cuda.device_count()
+        if n_dev > 0:
+            local = local % n_dev
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
@@ -160,7 +165,7 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
 
     if pg is not None:
         import torch
-        dev_t = "cuda" if torch.cuda.is_available() else "cpu"
+        dev_t = "cuda" if pg.get_backend() == "nccl" else "cpu"
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
         elapsed = float(t.item())
