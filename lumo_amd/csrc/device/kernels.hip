@@ -727,6 +727,7 @@ uint32_t g_tail_below = 1u << 18;  // n_shadow == 1: k_bounce_q tail mode below 
 int g_pipeline = 3;                // fused passes overlapped (render_pipelined): 0 off, else the number of head streams (1-3)
 int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from a counter
 int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
+int g_heads = 0;                   // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
 int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
 template <typename F>
 void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr) {
@@ -787,16 +788,17 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         HIPCHK(hipEventRecord(c.cam_ev[k], As[0]));
     }
     const int gN = ceil_div(N, BLOCK);
-    const int heads = RR_DEPTH + 1;  // bounces 0..RR_DEPTH on the head stream
+    // bounces 0..heads-1 on the head stream: through the RR bounce when a pass holds many paths;
+    // with few (a rank's share of a multi-GPU run) the RR bounce goes to the tail kernel too, so
+    // the head stream never waits for the previous pass's ring (362^2: 509 -> 434 ms per frame)
+    const int heads = g_heads > 0 ? g_heads : (N >= (1 << 21) ? RR_DEPTH + 1 : RR_DEPTH);
     for (uint64_t pass = 0; pass < max_samples; ++pass) {
         const int set = (int)(pass % NSETS), prev = (int)((pass + NSETS - 1) % NSETS);
         hipStream_t A = As[pass % NA];
         Paths& P = P3[set];
         // ---- head stream: camera + the first bounces
-        if (NA > 1) {
-            HIPCHK(hipStreamWaitEvent(A, c.pass_ev[set], 0));  // pass - NSETS done with this set
-            HIPCHK(hipStreamWaitEvent(A, c.cam_ev[prev], 0));  // pass - 1's camera (sampler state)
-        }
+        HIPCHK(hipStreamWaitEvent(A, c.pass_ev[set], 0));  // pass - NSETS done with this set
+        if (NA > 1) HIPCHK(hipStreamWaitEvent(A, c.cam_ev[prev], 0));  // pass - 1's camera (sampler state)
         HIPCHK(hipMemsetAsync(P.counts, 0, sizeof(uint32_t) * CNT_N, A));
         {
             StageTimer tm(c, g_timing, ST_CAMERA, A);
@@ -1487,6 +1489,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("LUMO_PIPELINE")) g_pipeline = std::atoi(e);
     if (const char* e = std::getenv("LUMO_DYN")) g_dyn = std::atoi(e);
+    if (const char* e = std::getenv("LUMO_HEADS")) g_heads = std::min(std::max(std::atoi(e), 0), 64);
     if (const char* e = std::getenv("LUMO_BOUNCE_THREADS")) {
         const int t = std::atoi(e);
         g_bounce_threads = (t == 64 || t == 128) ? t : BLOCK;
