@@ -219,3 +219,26 @@ def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
         assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
     finally:
         lib.lumo_set_bounce_mode(-1, 1 << 18, 3)
+
+
+@pytest.mark.parametrize("heads", [4, 5, 8])
+def test_head_bounce_counts_match_oracle(cornell, heads):
+    """Pipelined passes handing over to the tail kernel after 4, 5 or 8 head bounces (the choice
+    between the RR bounce on the head stream or in the tail kernel is a size heuristic; every
+    count must give the oracle's tiles)."""
+    import os
+    os.environ["LUMO_HEADS"] = str(heads)  # read when a device context is created
+    try:
+        d = L.Device(0)
+        cam = L.Camera.cornell_box((48, 40))
+        d.upload(cornell, cam)
+        tasks = L.make_tasks(48, 40, 24, SEED)
+        bufs, res = d.render_tasks(tasks)
+        d.close()
+        obufs, ores, _ = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+        for b, ob, r, orr in zip(bufs, obufs, res, ores):
+            np.testing.assert_array_equal(b, ob)
+            assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+    finally:
+        os.environ["LUMO_HEADS"] = "0"
+        L.Device(0).close()  # back to the automatic count
