@@ -177,6 +177,12 @@ __global__ void k_bounce_begin(uint32_t* counts, unsigned long long* headq) {
     }
 }
 
+// Queue counters (and optionally one more word) zeroed in-stream: a kernel instead of a fill.
+__global__ void k_zero_counts(uint32_t* counts, uint32_t* extra) {
+    if (threadIdx.x < CNT_N) counts[threadIdx.x] = 0u;
+    if (extra && threadIdx.x == 0) *extra = 0u;
+}
+
 // ------------------------------------------------------------------ finish + film + ring
 // ToneMap::map (tone_mapping.rs:38-63), then XYZ -> white balance -> colour space
 // (film/tile.rs:65-66, space.rs:125-151)
@@ -385,10 +391,14 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S, Tasks
 // One wave per task.  The pass's samples land in ring slots (ptr + j) % n; when a tile has more
 // pixels than ring slots only the last writer of a slot (no j + n < P) stores.  The variance
 // sums stay sequential in slot order (lane 0, from LDS) so they round exactly like task.rs.
-__global__ __launch_bounds__(64) void k_ring(Paths S, Tasks T, int n_tasks, int update) {
+// `zero_counts` (when set): the pass's queue counters, zeroed by block 0 for the next pass that
+// uses them (every kernel of the pass that reads them precedes the ring on its stream), so a pass
+// starts without a fill of its own.
+__global__ __launch_bounds__(64) void k_ring(Paths S, Tasks T, int n_tasks, int update, uint32_t* zero_counts) {
     const int ti = blockIdx.x;
     if (ti >= n_tasks) return;
     const int lane = threadIdx.x;
+    if (zero_counts && ti == 0 && lane < CNT_N) zero_counts[lane] = 0u;
     __shared__ double lum[SAMPLES_INCREMENT];
     __shared__ unsigned long long cst[SAMPLES_INCREMENT];
     const lumo_tile_task& t = T.t[ti];
@@ -754,6 +764,17 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
     // sets of queues, counters and per-slot outputs, so a set is reused only after the pass
     // NSETS back has finished its film.
     const int NA = std::min(std::max(g_pipeline, 1), 3), NSETS = NA + 1;
+    // On an error return, work already queued on the other streams may still use the buffers the
+    // next call re-initialises on stream 0: drain every stream before reporting the error.
+    struct JoinOnError {
+        Ctx& c;
+        bool ok = false;
+        ~JoinOnError() {
+            if (ok) return;
+            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream})
+                if (s) (void)hipStreamSynchronize(s);
+        }
+    } join{c};
     Paths P3[4] = {S, S, S, S};
     const int wid[3][16] = {{W_RAD2, W_LAM2, W_RASTER2, W_DEPTH2, W_QUERIES2, W_P_VALID2, W_COUNTS2, W_QS2_D, W_QS2_R,
                              W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I},
@@ -783,6 +804,8 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
     // every event starts "done" after the setup enqueued on stream 0 (tasks, memsets, the initial
     // ring): pass p waits for pass p - NSETS's film before reusing its set, for pass p - 1's camera
     // (the sampler state is per slot) and, before bounce RR_DEPTH, for pass p - 1's ring
+    // each set's counters start zeroed; from then on every pass's ring zeroes its set's counters
+    for (int k = 1; k < NSETS; ++k) HIPCHK(hipMemsetAsync(P3[k].counts, 0, sizeof(uint32_t) * CNT_N, As[0]));
     for (int k = 0; k < 4; ++k) {
         HIPCHK(hipEventRecord(c.pass_ev[k], As[0]));
         HIPCHK(hipEventRecord(c.cam_ev[k], As[0]));
@@ -797,9 +820,8 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         hipStream_t A = As[pass % NA];
         Paths& P = P3[set];
         // ---- head stream: camera + the first bounces
-        HIPCHK(hipStreamWaitEvent(A, c.pass_ev[set], 0));  // pass - NSETS done with this set
+        HIPCHK(hipStreamWaitEvent(A, c.pass_ev[set], 0));  // pass - NSETS done with this set (its ring zeroed the counters)
         if (NA > 1) HIPCHK(hipStreamWaitEvent(A, c.cam_ev[prev], 0));  // pass - 1's camera (sampler state)
-        HIPCHK(hipMemsetAsync(P.counts, 0, sizeof(uint32_t) * CNT_N, A));
         {
             StageTimer tm(c, g_timing, ST_CAMERA, A);
             k_camera<true><<<gN, BLOCK, 0, A>>>(T, P, c.cam, N, dim_stride, (uint32_t)pass);
@@ -847,7 +869,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         }
         {
             StageTimer tm(c, g_timing, ST_RING, B);
-            k_ring<<<n_tasks, 64, 0, B>>>(P, T, n_tasks, 1);
+            k_ring<<<n_tasks, 64, 0, B>>>(P, T, n_tasks, 1, P.counts);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.pass_ev[set], B));
@@ -855,6 +877,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
     }
     // the results are copied on stream 0: after the last pass's ring
     HIPCHK(hipStreamWaitEvent(As[0], c.pass_ev[(max_samples - 1) % NSETS], 0));
+    join.ok = true;
     return LUMO_OK;
 }
 
@@ -1043,11 +1066,12 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     HIPCHK(hipMemsetAsync(S.film, 0, sizeof(double) * 4 * N, sm));
     HIPCHK(hipMemsetAsync(S.tcount, 0, sizeof(unsigned long long) * (TC_ALL + TC_STATS), sm));
     HIPCHK(hipMemsetAsync(S.checks, 0, sizeof(unsigned long long) * 3, sm));
+    HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));
 
     const int gT = ceil_div(n_tasks, BLOCK), gN = ceil_div(N, BLOCK);
     k_init_seeds<<<gT, BLOCK, 0, sm>>>(T, S, (int)n_tasks);
     k_init_mj<<<gN, BLOCK, 0, sm>>>(T, S, N, dim_stride);
-    k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 0);
+    k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 0, nullptr);
     HIPCHK(hipGetLastError());
 
     uint64_t bounces = 0, closest_q = 0, shadow_q = 0;
@@ -1067,7 +1091,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     }
     for (uint64_t pass = 0; pass < (pipe ? 0 : max_samples); ++pass) {
         if (dump_host) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, sm));
-        HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));
+        // S.counts: zeroed at setup, then by the ring at the end of every pass
         {
             StageTimer tm(c, g_timing, ST_CAMERA);
             if (bdpt)
@@ -1195,8 +1219,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                     });
                 };
             };
-            HIPCHK(hipMemsetAsync(B.redo_count, 0, sizeof(uint32_t), sm));
-            HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));  // drop k_camera's queue
+            k_zero_counts<<<1, 64, 0, sm>>>(S.counts, B.redo_count);  // drop k_camera's queue; no re-runs yet
             if (c.sc.full == 2)
                 k_bdpt_light_init<2><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BI, N);
             else if (c.sc.full)
@@ -1205,7 +1228,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 k_bdpt_light_init<0><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BI, N);
             bst = bounce_loop(walk_step(TR_IMPORTANCE));
             if (bst) return bst;
-            HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));
+            k_zero_counts<<<1, 64, 0, sm>>>(S.counts, nullptr);
             k_bdpt_cam_init<<<gN, BLOCK, 0, sm>>>(S, B, BI, c.cam, N);
             bst = bounce_loop(walk_step(TR_RADIANCE));
             if (bst) return bst;
@@ -1293,7 +1316,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         }
         {
             StageTimer tm(c, g_timing, ST_RING);
-            k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 1);
+            k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 1, S.counts);
         }
         HIPCHK(hipGetLastError());
         if (bdpt && dfilm) {

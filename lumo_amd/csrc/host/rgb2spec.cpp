@@ -4,6 +4,15 @@
 // (src/tracer/color/spectrum/tables.rs:6).  Same CIE tables (lumo color/samples.rs),
 // same 3/8-Simpson fine grid, CIELAB residual, central-difference Jacobian, LUP solve,
 // 15 Gauss-Newton iterations with the |c|<=200 rescale and the res/5 warm-start sweep.
+//
+// Upstream notice.  The algorithm restated here is that of `rgb2spec_opt.cpp` in
+// https://github.com/mitsuba-renderer/rgb2spec, Copyright (c) 2019 Wenzel Jakob and Johannes
+// Hanika, distributed under a 3-clause BSD-style licence (redistribution in source and binary
+// forms permitted provided the copyright notice, the conditions and the disclaimer are retained;
+// the authors' names may not be used to endorse derived products; provided "as is", without
+// warranty).  No upstream source text is included: this file was written from the published
+// method and from lumo's use of its output.  The upstream LICENSE file, not this summary, governs;
+// it is not in this image (no network), so a redistribution should add it verbatim beside this file.
 #include "rgb2spec.h"
 
 #include <array>

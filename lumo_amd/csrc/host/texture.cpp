@@ -1,5 +1,6 @@
 // Host side of lumo's textures: PNG (zlib inflate + PNG row filters) and Radiance HDR decoding,
 // per-texel spectra, bump maps, Perlin lattices.  Restates image.rs:17-276 and perlin.rs:31-47.
+#include <climits>
 #include "texture.h"
 
 #include <zlib.h>
@@ -254,6 +255,12 @@ bool texture_from_hdr(const uint8_t* data, size_t n, HostTexture& out, std::stri
     }
     if (width <= 0 || height <= 0) {
         err = "HDR file without resolution";
+        return false;
+    }
+    // lumo parses the sizes as u32 (image.rs:214-230); the device indexes texels with int32, so
+    // each side and the texel count must fit in [1, INT32_MAX] (checked without overflow)
+    if (width > INT32_MAX || height > INT32_MAX || width > INT32_MAX / height) {
+        err = "HDR resolution too large";
         return false;
     }
     const size_t count = (size_t)width * (size_t)height;

@@ -18,3 +18,18 @@ def gpu_paths(dev, task):
     _ffi.check(_ffi.load().lumo_debug_paths(dev.ctx, C.byref(task), C.byref(dump)), "debug_paths")
     return dict(radiance=rad.reshape(-1, 4), lam=lam.reshape(-1, 4), raster=ras.reshape(-1, 2), depth=depth,
                 delta=delta)
+
+
+def oracle_threads():
+    """Threads for the CPU oracle in a parity test: the cores this process may use (the affinity
+    mask, capped by a cgroup v2 quota: on the GPU box os.cpu_count() is the whole machine)."""
+    import math
+    import os
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, math.floor(int(q) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(n, 32))

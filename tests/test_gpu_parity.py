@@ -9,7 +9,7 @@ import pytest
 
 import lumo_amd as L
 import oracle_ffi as O
-from parity import gpu_paths
+from parity import gpu_paths, oracle_threads
 
 pytestmark = pytest.mark.gpu
 
@@ -221,9 +221,9 @@ def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
         lib.lumo_set_bounce_mode(-1, 1 << 18, 3)
 
 
-@pytest.mark.parametrize("heads", [4, 5, 8])
+@pytest.mark.parametrize("heads", [4, 5, 6, 8])
 def test_head_bounce_counts_match_oracle(cornell, heads):
-    """Pipelined passes handing over to the tail kernel after 4, 5 or 8 head bounces (the choice
+    """Pipelined passes handing over to the tail kernel after 4, 5, 6 or 8 head bounces (the choice
     between the RR bounce on the head stream or in the tail kernel is a size heuristic; every
     count must give the oracle's tiles)."""
     import os
@@ -242,3 +242,96 @@ def test_head_bounce_counts_match_oracle(cornell, heads):
     finally:
         os.environ["LUMO_HEADS"] = "0"
         L.Device(0).close()  # back to the automatic count
+
+
+HEADLINE = (1536, 1536, 8)  # 2.36 M slots per pass >= 2^21: the automatic head count is 6, as at 1024^2
+
+
+def test_headline_schedule_matches_oracle(cornell):
+    """The exact schedule behind the C1 bench line, at a size where the device picks it by itself:
+    a pass of >= 2^21 slots (6 head bounces, the RR bounce on the head stream), 3 head streams
+    rotating 4 sets of queues / counters / per-slot outputs (8 passes: every set is reused),
+    dynamic work fetch, max_paths = 2^23 (bench.py --max-paths).  Every tile's pixels, ray and
+    query counts, and the frame's closest / shadow query totals equal the oracle's (wavefront
+    order).  Then the same frame without pipelining (pipeline 0: passes in sequence, one stream)
+    must give the same bits: the cross-stream machinery adds nothing to any per-path result."""
+    from lumo_amd import _ffi
+    W, H, spp = HEADLINE
+    lib = _ffi.load()
+    lib.lumo_set_bounce_mode(-1, 1 << 18, 3)
+    d = L.Device(0)
+    try:
+        cam = L.Camera.cornell_box((W, H))
+        d.upload(cornell, cam)
+        assert d.scene_info().lds_bytes > 0  # the fused, LDS-staged kernels (C1's)
+        tasks = L.make_tasks(W, H, spp, SEED)
+        before = d.stats()
+        bufs, res = d.render_tasks(tasks, max_paths=1 << 23)
+        after = d.stats()
+        assert after.launches[1] - before.launches[1] == 6 * spp  # 6 fused head bounces per pass
+        lib.lumo_set_bounce_mode(-1, 1 << 18, 0)
+        seq, seq_res = d.render_tasks(tasks, max_paths=1 << 23)
+    finally:
+        lib.lumo_set_bounce_mode(-1, 1 << 18, 3)
+        d.close()
+    for b, s, r, sr in zip(bufs, seq, res, seq_res):
+        np.testing.assert_array_equal(b, s)
+        assert (r.num_rays, r.num_queries) == (sr.num_rays, sr.num_queries)
+    obufs, ores, cnt = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, oracle_threads())
+    bad = [i for i, (b, ob) in enumerate(zip(bufs, obufs)) if not np.array_equal(b, ob)]
+    assert not bad, f"{len(bad)} of {len(tasks)} tiles differ, first {bad[:8]}"
+    for r, orr in zip(res, ores):
+        assert (r.num_rays, r.num_queries, r.num_camera_rays) == (orr.num_rays, orr.num_queries,
+                                                                  orr.num_camera_rays)
+    assert after.closest_queries - before.closest_queries == cnt.closest_queries
+    assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
+
+
+def dof_scene():
+    """examples/dof.rs's layout without its downloaded teapots: the 20 x 20 floor at y = -1, the
+    3 x 3 light rotated to face down at y = 8, and three spheres in a row along -z (the teapots'
+    places) for the focus to fall on."""
+    s = L.Scene()
+    grey = L.Material.diffuse(L.Spectrum.from_srgb(200, 200, 200))
+    s.add_rectangle((-10, -1, 10), (10, -1, 10), (10, -1, -10), grey)  # normal +y
+    s.add_rectangle((-1.5, 8, -3.0), (1.5, 8, -3.0), (1.5, 8, 0.0), L.Material.light(L.named_spectrum("WHITE"),
+                                                                                     scale=0.25), light=True)
+    for i in range(3):
+        s.add_sphere(0.25, L.Material.diffuse(L.Spectrum.from_srgb(255, 245, 255))).translate(0.0, -0.75, -1.0 * i)
+    s.build()
+    return s
+
+
+def dof_camera(res, lens=0.03):
+    """dof.rs:15-22: origin 0.75 (-X) + 0.25 Y, towards 0.75 (-Y) - Z, lens_radius(0.03),
+    focal_length(|o - t|) (perspective: the orthographic variant is test_orthographic_*)."""
+    o, t = np.array([-0.75, 0.25, 0.0]), np.array([0.0, -0.75, -1.0])
+    return (L.Camera.builder().origin(*o).towards(*t).lens_radius(lens)
+            .focal_length(float(np.linalg.norm(o - t))).resolution(res).build())
+
+
+@pytest.mark.parametrize("which", ["cornell", "dof"])
+def test_thin_lens_matches_oracle(dev, cornell, which):
+    """Camera::add_dof (camera.rs:221-243) with lens_radius != 0: the lens sample (drawn for every
+    camera ray, integrator.rs:56) moves the origin on the lens and aims at the focal plane.  Paths
+    and tiles equal the oracle's, for the Cornell camera with an 8-unit lens focused at z = 280
+    and for dof.rs's camera (lens 0.03, focal length |origin - towards|)."""
+    res = (40, 32)
+    if which == "cornell":
+        scene, cam = cornell, L.Camera.cornell_box_builder().lens_radius(8.0).focal_length(1080.0).resolution(res).build()
+    else:
+        scene, cam = dof_scene(), dof_camera(res)
+    assert cam.desc.lens_radius > 0
+    dev.upload(scene, cam)
+    tasks = L.make_tasks(res[0], res[1], 12, SEED)
+    _cmp_paths(gpu_paths(dev, tasks[3]), O.trace_paths(scene.desc(), cam.desc, tasks[3]))
+    bufs, res_ = dev.render_tasks(tasks)
+    obufs, ores, _ = O.render_tasks(scene.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+    for b, ob, r, orr in zip(bufs, obufs, res_, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+    # the lens matters: the same frame through a pinhole differs
+    pin = dof_camera(res, 0.0) if which == "dof" else L.Camera.cornell_box(res)
+    dev.upload(scene, pin)
+    flat, _ = dev.render_tasks(tasks)
+    assert not np.array_equal(np.concatenate(flat), np.concatenate(bufs))

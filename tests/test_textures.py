@@ -126,7 +126,10 @@ def test_hdr_environment_texels_and_mean():
 
 
 @pytest.mark.parametrize("bad", [b"#?RGBE\n-Y 1 +X 1\n\x01\x01\x01\x80", b"#?RADIANCE\n-Y 2 +X 2\n\x01\x01\x01\x80",
-                                 b"#?RADIANCE\n+X 1 -Y 1\n\x01\x01\x01\x80"])
+                                 b"#?RADIANCE\n+X 1 -Y 1\n\x01\x01\x01\x80",
+                                 # sizes whose product wraps to 0 (an empty body would pass the size
+                                 # check) or overflows int32 texel indexing: rejected as lumo's u32 parse
+                                 b"#?RADIANCE\n-Y 4 +X 4611686018427387904\n", b"#?RADIANCE\n-Y 65536 +X 65536\n"])
 def test_hdr_rejections(bad):
     """image.rs:214-238 asserts: the magic line, the '-Y h +X w' order, w * h * 4 data bytes."""
     with pytest.raises(ValueError):

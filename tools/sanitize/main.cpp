@@ -212,6 +212,14 @@ void hostile() {
         lumo_builder_free(b);
     }
     CHECK(ok > 0 && bad > 0);
+    // HDR headers whose sizes overflow the texel count (the count wraps to 0, so the data-size
+    // check alone would pass an empty body) or exceed the int32 texel indexing
+    for (const char* hd : {"#?RADIANCE\n-Y 4 +X 4611686018427387904\n", "#?RADIANCE\n-Y 4611686018427387904 +X 4\n",
+                           "#?RADIANCE\n-Y 65536 +X 65536\n", "#?RADIANCE\n-Y 1 +X 2147483648\n"}) {
+        void* b = lumo_builder_new();
+        CHECK(lumo_builder_texture_hdr(b, hd, std::strlen(hd)) < 0);
+        lumo_builder_free(b);
+    }
     // mangled OBJ / MTL text
     const std::string obj = "mtllib a.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\nv 1 1 0\nvt 0 0\nvt 1 0\nvt 0 1\nvn 0 0 1\n"
                             "usemtl m\nf 1/1/1 2/2/1 3/3/1\nf 2 4 3\nusemtl l\nf -1 -2 -3\n";
