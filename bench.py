@@ -43,6 +43,14 @@ B_CLOSEST_IO = 48 + 20  # ray in + hit out
 B_RECORD, B_FOLD = 104, 104  # shadow record in; per path: gathered + pdf_light + radiance read/write
 B_CONN_IO = 104  # BDPT connection query: the two vertices' position / error / normal in, result out
 LUMO_DEFAULT_THREADS = 4  # renderer.rs:21
+# f64 VALU peak in lane-operations per second (an FMA counts once): 256 CUs x 4 SIMDs x 16 f64
+# lanes per cycle x 2.4 GHz = 78.6 TFLOP/s / 2 (MI355X FP64 vector rate).  The VALU bound prices
+# every VALU lane-operation at this rate (integer / f32 ops issue at twice it, so the fraction is
+# an upper bound on how busy the f64 pipe is).
+VALU_PEAK_LANE_OPS = 256 * 4 * 16 * 2.4e9
+# timed stages (lumo_amd._ffi.STAGES indices) of each roofline unit
+UNIT_STAGES = {"k_bounce_q+k_bounce_tail": [1, 4], "k_closest": [1], "k_shadow": [3],
+               "k_bdpt_trace_a+k_bdpt_vis": [8, 10], "frame": list(range(12))}
 
 
 def dist_env():
@@ -100,7 +108,7 @@ def main():
             out["c3"] = {k: c3[k] for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype",
                                             "data", "config", "msamples_per_s", "lumo_total_rays_per_s_M",
                                             "queries_per_step", "shadow_resolved_per_step",
-                                            "mrays_traversed_per_s", "scene_build_s", "sample_checks", "roofline",
+                                            "mrays_traversed_per_s", "mrays_lumo_equivalent_per_s", "scene_build_s", "sample_checks", "roofline",
                                             "cpu_baseline")}
         print(json.dumps(out))
     if pg is not None:
@@ -160,6 +168,9 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
     elapsed = time.perf_counter() - t0
     lib.lumo_set_timing(0)
     st = dev.stats()
+    # busy time (union of launch intervals) of every stage and of the roofline units
+    busy = {name: dev.busy_ms(stages) for name, stages in UNIT_STAGES.items()}
+    busy["_stages"] = [dev.busy_ms([k]) for k in range(len(_ffi.STAGES))]
     checks = [st.samples_nan, st.samples_neg, st.samples_large]
     resolved = st.shadow_resolved
 
@@ -177,11 +188,13 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
 
     out = None
     if rank == 0:
-        roof = roofline(st, n_shadow_rays(scene), bdpt=bdpt, workload=config, elapsed=elapsed)
+        roof = roofline(st, n_shadow_rays(scene), bdpt=bdpt, workload=config, elapsed=elapsed, busy=busy)
         cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl) if (args.cpu_baseline and ws == 1) else None
         out = {
             "metric": "Mrays/s",
-            "value": round(q / elapsed / 1e6, 3),
+            # traversed queries only: the shadow records answered without a traversal (their BSDF
+            # pdf is 0, integrator.rs:146) are in the lumo-equivalent rate below, not here
+            "value": round((q - resolved) / elapsed / 1e6, 3),
             "unit": "Mrays/s",
             "n_gpus": ws,
             "steps": steps,
@@ -210,6 +223,9 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
             # mis_sample returns 0 whatever the visibility, integrator.rs:146)
             "shadow_resolved_per_step": resolved / steps,
             "mrays_traversed_per_s": round((q - resolved) / elapsed / 1e6, 3),
+            # every Scene::hit / hit_light call lumo would make for the frame (the traversed ones +
+            # the shadow records the device resolves without traversal)
+            "mrays_lumo_equivalent_per_s": round(q / elapsed / 1e6, 3),
             "scene_build_s": wl["scene_build_s"],
             # tone_mapping.rs:42-56 debug checks over the timed camera samples: NaN, negative, > 1000
             "sample_checks": {"nan": checks[0], "negative": checks[1], "large": checks[2]},
@@ -265,18 +281,28 @@ def build_config(name, res=None, spp_override=None):
     return scene, cam, (W, H), spp, wl
 
 
-def roofline(st, n_shadow, bdpt=False, workload="c1", elapsed=None):
-    """Dominant-kernel roofline from live per-launch HIP-event times and traversal counters.
+def roofline(st, n_shadow, bdpt=False, workload="c1", elapsed=None, busy=None):
+    """Dominant-kernel roofline from live HIP-event launch intervals and traversal counters.
 
     Unit = one ray query; bytes = IO + 48 per AABB test + 16 per kd split visit + 84 per triangle
     test (f64), the counters being the kernels' own (identical to the oracle's on the same rays).
     PathTrace: k_closest (closest IO) or k_shadow (shadow record + the per-path fold amortised
-    over its 2 n_shadow queries).  BDPT: the walk traces (k_closest) or the connection
-    traversals (k_bdpt_trace_a + k_bdpt_vis, one query each)."""
+    over its 2 n_shadow queries), or, with fused bounces, k_bounce_q + its tail kernel as one unit.
+    BDPT: the walk traces (k_closest) or the connection traversals (k_bdpt_trace_a + k_bdpt_vis).
+
+    Time base: the unit's BUSY time, the union of its launches' [start, end] intervals (HIP events
+    on the streams they run on).  With pipelined passes launches of the unit overlap on several
+    streams, so the sum of launch durations exceeds the time the unit occupied the GPU (it can
+    exceed the frame time); the union never does.  `achieved` = algorithmic bytes / busy time.
+    The per-launch view (bytes per launch / average launch duration, what rocprofv3's average
+    duration checks) is reported beside it as `achieved_per_launch`."""
     from lumo_amd._ffi import STAGES
     ms = list(st.kernel_ms)
     launches = list(st.launches)
-    per_stage = {STAGES[i]: {"ms": round(ms[i], 3), "launches": int(launches[i])} for i in range(len(STAGES))}
+    busy = busy or {}
+    bst = busy.get("_stages", [None] * len(STAGES))
+    per_stage = {STAGES[i]: {"ms": round(ms[i], 3), "busy_ms": None if bst[i] is None else round(bst[i], 3),
+                             "launches": int(launches[i])} for i in range(len(STAGES))}
     cq = max(st.closest_queries, 1)
     # shadow records resolved without traversal (p_sct == 0, DESIGN.md §4) read only their pdf
     traversed = st.shadow_queries - st.shadow_resolved
@@ -284,27 +310,26 @@ def roofline(st, n_shadow, bdpt=False, workload="c1", elapsed=None):
     closest_bytes = (st.closest_queries * B_CLOSEST_IO + st.aabb_tests[0] * B_AABB + st.kd_nodes[0] * B_KD +
                      st.tri_tests[0] * B_TRI)
     trav1 = st.aabb_tests[1] * B_AABB + st.kd_nodes[1] * B_KD + st.tri_tests[1] * B_TRI
+
+    def unit(name, stages, nbytes):
+        return (sum(ms[i] for i in stages), sum(launches[i] for i in stages), nbytes, busy.get(name))
+
     if bdpt:
-        # candidates: walk traces; connection traversals (both item kernels as one unit)
-        conn_ms = ms[8] + ms[10]
-        conn_launches = launches[8] + launches[10]
-        cands = {"k_closest": (ms[1], launches[1], closest_bytes),
-                 "k_bdpt_trace_a+k_bdpt_vis": (conn_ms, conn_launches, st.shadow_queries * B_CONN_IO + trav1)}
+        cands = {"k_closest": unit("k_closest", [1], closest_bytes),
+                 "k_bdpt_trace_a+k_bdpt_vis": unit("k_bdpt_trace_a+k_bdpt_vis", [8, 10],
+                                                   st.shadow_queries * B_CONN_IO + trav1)}
     else:
         b_io = B_RECORD + B_FOLD / (2 * n_shadow)
         shadow_bytes = traversed * b_io + st.shadow_resolved * 8 + trav1
         if n_shadow == 1 and ms[1] > 0 and ms[2] == 0:
             # fused bounce (k_bounce_q: closest hit + shading + the NEE pair, 'closest' stage) and
-            # its tail kernel ('resolve' stage for n_shadow == 1): one unit carrying every query,
-            # priced with the same per-query model as the three-kernel bounce
-            cands = {"k_bounce_q+k_bounce_tail": (ms[1] + ms[4], launches[1] + launches[4], closest_bytes + shadow_bytes)}
+            # its tail kernel ('resolve' stage for n_shadow == 1): one unit carrying every query
+            cands = {"k_bounce_q+k_bounce_tail": unit("k_bounce_q+k_bounce_tail", [1, 4], closest_bytes + shadow_bytes)}
         else:
-            cands = {"k_closest": (ms[1], launches[1], closest_bytes), "k_shadow": (ms[3], launches[3], shadow_bytes)}
-    # the dominant kernel of the step: the longest of all timed stages; if that is not a
-    # traversal kernel, the roofline is still reported for the longest traversal kernel
+            cands = {"k_closest": unit("k_closest", [1], closest_bytes), "k_shadow": unit("k_shadow", [3], shadow_bytes)}
     dom_stage = STAGES[max(range(len(STAGES)), key=lambda i: ms[i])]
-    kname = max(cands, key=lambda k: cands[k][0])
-    kms, kl, nbytes = cands[kname]
+    kname = max(cands, key=lambda k: cands[k][3] if cands[k][3] is not None else cands[k][0])
+    kms, kl, nbytes, kbusy = cands[kname]
     pmc = pmc_traffic(workload, kname)
     out = {"bound": "hbm", "kernel": kname, "longest_stage": dom_stage, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "traffic": pmc.get("hbm_bytes_per_launch"), "traffic_raw": pmc.get("hbm_bytes_per_launch_raw"),
@@ -314,20 +339,27 @@ def roofline(st, n_shadow, bdpt=False, workload="c1", elapsed=None):
         ("connection" if bdpt else "shadow"): {"aabb": st.aabb_tests[1] / sq, "kd": st.kd_nodes[1] / sq,
                                                "tri": st.tri_tests[1] / sq}}
     if kms > 0 and kl > 0:
-        achieved = nbytes / (kms * 1e-3) / 1e9
+        t_busy = (kbusy if kbusy else kms) * 1e-3
+        achieved = nbytes / t_busy / 1e9
         avg_s = kms * 1e-3 / kl
         out.update({"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 5),
-                    "bytes_per_launch": nbytes / kl, "avg_launch_us": avg_s * 1e6})
+                    "bytes_per_launch": nbytes / kl, "launches": kl, "busy_ms": round(t_busy * 1e3, 3),
+                    "launch_ms_sum": round(kms, 3), "avg_launch_us": avg_s * 1e6,
+                    "achieved_per_launch": round(nbytes / (kms * 1e-3) / 1e9, 2),
+                    "frac_per_launch": round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)})
         if elapsed:
-            # the same bytes over the step's wall time: with pipelined passes the unit's launches
-            # overlap (two head streams + the tail stream), so per-launch durations include the
-            # time they share the GPU and `achieved` understates the unit's throughput
-            aw = nbytes / elapsed / 1e9
-            out.update({"achieved_wall": round(aw, 2), "frac_wall": round(aw / HBM_PEAK_GBS, 5)})
+            out["busy_over_wall"] = round(t_busy / elapsed, 4)
         if out["traffic"]:
-            # measured DRAM-side rate of the same kernel: PMC bytes per launch over live launch time
-            out["hbm_gbs_measured"] = round(out["traffic"] / avg_s / 1e9, 2)
+            # measured DRAM bytes of the same launches over the unit's busy time
+            out["hbm_gbs_measured"] = round(out["traffic"] * kl / t_busy / 1e9, 2)
             out["traffic_over_algorithmic"] = round(out["traffic"] / (nbytes / kl), 3)
+        lane_ops = pmc.get("valu_lane_ops_per_launch")
+        if lane_ops:
+            va = lane_ops * kl / t_busy
+            out["valu"] = {"bound": "valu", "achieved": round(va / 1e12, 3), "peak": round(VALU_PEAK_LANE_OPS / 1e12, 3),
+                           "unit": "T lane-op/s (f64 rate)", "frac": round(va / VALU_PEAK_LANE_OPS, 5),
+                           "lanes_active_per_valu_inst": pmc.get("lanes_active_per_valu_inst"),
+                           "source": out["traffic_source"]}
     else:
         out.update({"achieved": None, "frac": None})
     return out

@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define LUMO_ABI_VERSION 5
+#define LUMO_ABI_VERSION 6
 
 typedef int32_t lumo_status;
 enum {
@@ -344,6 +344,10 @@ lumo_status lumo_trace(void* ctx, const lumo_ray_soa* rays, size_t n, lumo_hit_s
 
 lumo_status lumo_stats_get(void* ctx, lumo_stats* stats);
 lumo_status lumo_stats_reset(void* ctx);
+/* Busy time of a set of stages (bit k = LUMO_STAGE k) since the last reset, with timing on: the
+ * length of the union of their launches' intervals.  kernel_ms sums launch durations, which counts
+ * twice the time that launches on concurrent streams overlap (pipelined passes); this does not. */
+lumo_status lumo_stats_busy_ms(void* ctx, uint32_t stage_mask, double* ms);
 /* Enable per-launch HIP-event timing of every stage (also LUMO_TIMING=1). */
 void lumo_set_timing(int on);
 

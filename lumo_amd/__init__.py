@@ -774,6 +774,16 @@ class Device:
         check(lib().lumo_stats_get(self.ctx, C.byref(s)), "stats")
         return s
 
+    def busy_ms(self, stages):
+        """Union of the timed launch intervals of `stages` (indices into _ffi.STAGES) since the
+        last stats reset: the time at least one of them was running (lumo_stats_busy_ms)."""
+        mask = 0
+        for k in stages:
+            mask |= 1 << int(k)
+        ms = C.c_double(0.0)
+        check(lib().lumo_stats_busy_ms(self.ctx, mask, C.byref(ms)), "stats_busy_ms")
+        return ms.value
+
     def close(self):
         if getattr(self, "ctx", None):
             lib().lumo_destroy(self.ctx)

@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 5  # include/lumo_amd.h LUMO_ABI_VERSION
+ABI_VERSION = 6  # include/lumo_amd.h LUMO_ABI_VERSION
 LIB_PATH = os.environ.get("LUMO_AMD_LIB") or os.path.join(_HERE, "liblumo_amd.so")
 
 c_double_p = C.POINTER(C.c_double)
@@ -187,6 +187,7 @@ DEVICE_API = [
     ("lumo_trace", C.c_int32, [C.c_void_p, C.POINTER(RaySoA), C.c_size_t, C.POINTER(HitSoA), C.c_int]),
     ("lumo_stats_get", C.c_int32, [C.c_void_p, C.POINTER(Stats)]),
     ("lumo_stats_reset", C.c_int32, [C.c_void_p]),
+    ("lumo_stats_busy_ms", C.c_int32, [C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]),
     ("lumo_set_timing", None, [C.c_int]),
     ("lumo_set_lds_staging", None, [C.c_int]),
     ("lumo_set_bounce_mode", None, [C.c_int, C.c_uint32, C.c_int]),

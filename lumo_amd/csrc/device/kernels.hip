@@ -177,6 +177,25 @@ __global__ void k_bounce_begin(uint32_t* counts, unsigned long long* headq) {
     }
 }
 
+// Setup zeroing of a render's accumulators and counters in one launch instead of a fill per
+// buffer (every buffer is a hipMalloc allocation or a whole field of one, 4-byte granular).
+struct ZeroList {
+    static constexpr int MAX = 16;
+    uint32_t* p[MAX];
+    uint64_t words[MAX];
+    int n = 0;
+    void add(void* ptr, size_t bytes) {
+        p[n] = static_cast<uint32_t*>(ptr);
+        words[n] = bytes / 4;
+        ++n;
+    }
+};
+__global__ __launch_bounds__(BLOCK) void k_zero_list(ZeroList z) {
+    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+    for (int k = 0; k < z.n; ++k)
+        for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < z.words[k]; i += stride) z.p[k][i] = 0u;
+}
+
 // Queue counters (and optionally one more word) zeroed in-stream: a kernel instead of a fill.
 __global__ void k_zero_counts(uint32_t* counts, uint32_t* extra) {
     if (threadIdx.x < CNT_N) counts[threadIdx.x] = 0u;
@@ -591,6 +610,12 @@ struct Ctx {
     int max_vertices = 64;
     double* splat_film = nullptr;
     int debug_integrator = LUMO_INTEGRATOR_PATH_TRACE;  // lumo_debug_paths
+    // Launch intervals of the timed stages (ms from ref_ev, recorded before the first timed launch
+    // after a stats reset): their union is a stage's busy time, which does not count twice the
+    // time that launches on different streams overlap (lumo_stats_busy_ms)
+    hipEvent_t ref_ev = nullptr;
+    bool ref_recorded = false;
+    std::vector<std::pair<float, float>> intervals[LUMO_STAGE_COUNT];
 };
 
 lumo_status dev_alloc(DevBuf& b, size_t bytes) {
@@ -654,7 +679,12 @@ T* wbuf(Ctx& c, int id, size_t count, lumo_status& st) {
 // has (queue-count readbacks), so timing adds no extra stalls.
 struct Timing {
     std::vector<hipEvent_t> free_ev;
-    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    struct Pending {
+        Ctx* c;
+        int stage;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
     hipEvent_t get() {
         if (free_ev.empty()) {
             hipEvent_t e;
@@ -682,6 +712,11 @@ struct StageTimer {
         if (on) {
             a = timing().get();
             b = timing().get();
+            if (!c.ref_recorded) {
+                if (!c.ref_ev) (void)hipEventCreate(&c.ref_ev);
+                (void)hipEventRecord(c.ref_ev, sm);
+                c.ref_recorded = true;
+            }
             (void)hipEventRecord(a, sm);
         }
         c.stats.launches[stage] += 1;
@@ -689,7 +724,7 @@ struct StageTimer {
     ~StageTimer() {
         if (on) {
             (void)hipEventRecord(b, sm);
-            timing().pending.push_back({stage, {a, b}});
+            timing().pending.push_back({&c, stage, a, b});
         }
     }
 };
@@ -698,18 +733,43 @@ struct StageTimer {
 // end of lumo_render_tiles synchronises, so all are resolved by its last call).
 void resolve_timers(Ctx& c) {
     Timing& t = timing();
-    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> still;
+    std::vector<Timing::Pending> still;
     for (auto& p : t.pending) {
-        if (hipEventQuery(p.second.second) != hipSuccess) {
+        if (p.c != &c || hipEventQuery(p.b) != hipSuccess) {
             still.push_back(p);
             continue;
         }
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, p.second.first, p.second.second) == hipSuccess) c.stats.kernel_ms[p.first] += ms;
-        t.free_ev.push_back(p.second.first);
-        t.free_ev.push_back(p.second.second);
+        float ms = 0.f, t0 = 0.f, t1 = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) c.stats.kernel_ms[p.stage] += ms;
+        if (c.ref_ev && hipEventElapsedTime(&t0, c.ref_ev, p.a) == hipSuccess &&
+            hipEventElapsedTime(&t1, c.ref_ev, p.b) == hipSuccess)
+            c.intervals[p.stage].push_back({t0, t1});
+        t.free_ev.push_back(p.a);
+        t.free_ev.push_back(p.b);
     }
     t.pending.swap(still);
+}
+
+// Union length of the launch intervals of the stages in `mask` (ms).
+double busy_ms(const Ctx& c, uint32_t mask) {
+    std::vector<std::pair<float, float>> iv;
+    for (int k = 0; k < LUMO_STAGE_COUNT; ++k)
+        if (mask & (1u << k)) iv.insert(iv.end(), c.intervals[k].begin(), c.intervals[k].end());
+    std::sort(iv.begin(), iv.end());
+    double total = 0.0, lo = 0.0, hi = 0.0;
+    bool open = false;
+    for (const auto& x : iv) {
+        if (open && x.first <= hi) {
+            hi = std::max(hi, (double)x.second);
+            continue;
+        }
+        if (open) total += hi - lo;
+        lo = x.first;
+        hi = x.second;
+        open = true;
+    }
+    if (open) total += hi - lo;
+    return total;
 }
 
 bool g_timing = false;
@@ -805,7 +865,11 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
     // ring): pass p waits for pass p - NSETS's film before reusing its set, for pass p - 1's camera
     // (the sampler state is per slot) and, before bounce RR_DEPTH, for pass p - 1's ring
     // each set's counters start zeroed; from then on every pass's ring zeroes its set's counters
-    for (int k = 1; k < NSETS; ++k) HIPCHK(hipMemsetAsync(P3[k].counts, 0, sizeof(uint32_t) * CNT_N, As[0]));
+    {
+        ZeroList z;
+        for (int k = 1; k < NSETS; ++k) z.add(P3[k].counts, sizeof(uint32_t) * CNT_N);
+        k_zero_list<<<1, BLOCK, 0, As[0]>>>(z);
+    }
     for (int k = 0; k < 4; ++k) {
         HIPCHK(hipEventRecord(c.pass_ev[k], As[0]));
         HIPCHK(hipEventRecord(c.cam_ev[k], As[0]));
@@ -1047,10 +1111,6 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     if (st) return st;
 
     hipStream_t sm = c.stream;
-    if (bdpt) {
-        HIPCHK(hipMemsetAsync(B.overflow, 0, sizeof(uint32_t), sm));
-        if (dfilm) HIPCHK(hipMemsetAsync(dfilm, 0, sizeof(double) * film_n, sm));
-    }
     std::vector<uint64_t> n_splats(n_tasks, 0);
     std::vector<lumo_splat> taps_h;
     std::vector<uint64_t> ranges_h(n_tasks + 1);
@@ -1058,15 +1118,23 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     HIPCHK(hipMemcpyAsync(T.first, first.data(), sizeof(int32_t) * (n_tasks + 1), hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemcpyAsync(S.task, task_of.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemcpyAsync(S.pix, pix_of.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, sm));
-    HIPCHK(hipMemsetAsync(T.ring_cost, 0, sizeof(uint64_t) * SAMPLES_INCREMENT * n_tasks, sm));
-    HIPCHK(hipMemsetAsync(T.ring_lum, 0, sizeof(double) * SAMPLES_INCREMENT * n_tasks, sm));
-    HIPCHK(hipMemsetAsync(T.ring_ptr, 0, sizeof(uint32_t) * n_tasks, sm));
-    HIPCHK(hipMemsetAsync(T.num_rays, 0, sizeof(unsigned long long) * n_tasks, sm));
-    HIPCHK(hipMemsetAsync(T.queries, 0, sizeof(unsigned long long) * n_tasks, sm));
-    HIPCHK(hipMemsetAsync(S.film, 0, sizeof(double) * 4 * N, sm));
-    HIPCHK(hipMemsetAsync(S.tcount, 0, sizeof(unsigned long long) * (TC_ALL + TC_STATS), sm));
-    HIPCHK(hipMemsetAsync(S.checks, 0, sizeof(unsigned long long) * 3, sm));
-    HIPCHK(hipMemsetAsync(S.counts, 0, sizeof(uint32_t) * CNT_N, sm));
+    {
+        ZeroList z;
+        z.add(T.ring_cost, sizeof(uint64_t) * SAMPLES_INCREMENT * n_tasks);
+        z.add(T.ring_lum, sizeof(double) * SAMPLES_INCREMENT * n_tasks);
+        z.add(T.ring_ptr, sizeof(uint32_t) * n_tasks);
+        z.add(T.num_rays, sizeof(unsigned long long) * n_tasks);
+        z.add(T.queries, sizeof(unsigned long long) * n_tasks);
+        z.add(S.film, sizeof(double) * 4 * N);
+        z.add(S.tcount, sizeof(unsigned long long) * (TC_ALL + TC_STATS));
+        z.add(S.checks, sizeof(unsigned long long) * 3);
+        z.add(S.counts, sizeof(uint32_t) * CNT_N);
+        if (bdpt) {
+            z.add(B.overflow, sizeof(uint32_t));
+            if (dfilm) z.add(dfilm, sizeof(double) * film_n);
+        }
+        k_zero_list<<<std::min(ceil_div((uint64_t)4 * N, BLOCK), 2048), BLOCK, 0, sm>>>(z);
+    }
 
     const int gT = ceil_div(n_tasks, BLOCK), gN = ceil_div(N, BLOCK);
     k_init_seeds<<<gT, BLOCK, 0, sm>>>(T, S, (int)n_tasks);
@@ -2016,6 +2084,15 @@ lumo_status lumo_stats_reset(void* ctx) {
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c) return LUMO_ERR_INVALID;
     std::memset(&c->stats, 0, sizeof(c->stats));
+    for (auto& v : c->intervals) v.clear();
+    c->ref_recorded = false;
+    return LUMO_OK;
+}
+
+lumo_status lumo_stats_busy_ms(void* ctx, uint32_t stage_mask, double* ms) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !ms) return LUMO_ERR_INVALID;
+    *ms = busy_ms(*c, stage_mask);
     return LUMO_OK;
 }
 

@@ -335,3 +335,29 @@ def test_thin_lens_matches_oracle(dev, cornell, which):
     dev.upload(scene, pin)
     flat, _ = dev.render_tasks(tasks)
     assert not np.array_equal(np.concatenate(flat), np.concatenate(bufs))
+
+
+def test_busy_time_is_a_union(dev, cornell):
+    """lumo_stats_busy_ms: the union of the timed launches' intervals.  With pipelined passes
+    (launches of one stage overlap on several streams) it is at most the sum of the launch
+    durations and at most the render's wall time; a stage set's union is at least each member's."""
+    import time
+    from lumo_amd import _ffi
+    lib = _ffi.load()
+    cam = L.Camera.cornell_box((256, 256))
+    dev.upload(cornell, cam)
+    tasks = L.make_tasks(256, 256, 32, SEED)
+    lib.lumo_set_timing(1)
+    try:
+        lib.lumo_stats_reset(dev.ctx)
+        t0 = time.perf_counter()
+        dev.render_tasks(tasks)
+        wall_ms = (time.perf_counter() - t0) * 1e3
+        st = dev.stats()
+        unit = dev.busy_ms([1, 4])
+        allst = dev.busy_ms(range(len(_ffi.STAGES)))
+    finally:
+        lib.lumo_set_timing(0)
+    assert 0 < unit <= st.kernel_ms[1] + st.kernel_ms[4] + 1e-3
+    assert max(dev.busy_ms([1]), dev.busy_ms([4])) <= unit + 1e-6
+    assert unit <= allst <= wall_ms

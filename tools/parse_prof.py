@@ -27,13 +27,70 @@ def short(name):
     return name[:60]
 
 
+UNITS = {"k_bounce_q+k_bounce_tail": ("k_bounce_q", "k_bounce_tail"),
+         "k_bdpt_trace_a+k_bdpt_vis": ("k_bdpt_trace_a", "k_bdpt_vis")}
+
+
+def union_ns(iv):
+    """Length of the union of [start, end] intervals: the time at least one launch ran."""
+    total, lo, hi = 0, None, None
+    for a, b in sorted(iv):
+        if hi is not None and a <= hi:
+            hi = max(hi, b)
+            continue
+        if hi is not None:
+            total += hi - lo
+        lo, hi = a, b
+    return total + (hi - lo if hi is not None else 0)
+
+
 res = defaultdict(lambda: {"launches": 0, "total_ns": 0})
+ivs = defaultdict(list)
 for r in rows("trace/**/*kernel_trace.csv"):
     k = short(r.get("Kernel_Name", ""))
+    a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     res[k]["launches"] += 1
-    res[k]["total_ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    res[k]["total_ns"] += b - a
+    ivs[k].append((a, b))
 for k, v in res.items():
     v["avg_us"] = v["total_ns"] / max(v["launches"], 1) / 1e3
+    v["busy_ms"] = union_ns(ivs[k]) / 1e6  # overlapping launches (several streams) counted once
+for u, parts in UNITS.items():
+    if all(p in res for p in parts):
+        iv = [x for p in parts for x in ivs[p]]
+        n = sum(res[p]["launches"] for p in parts)
+        tot = sum(res[p]["total_ns"] for p in parts)
+        res[u] = {"launches": n, "total_ns": tot, "avg_us": tot / n / 1e3, "busy_ms": union_ns(iv) / 1e6}
+if ivs:
+    allv = [x for v in ivs.values() for x in v]
+    res["_gpu"] = {"busy_ms": union_ns(allv) / 1e6, "span_ms": (max(b for _, b in allv) - min(a for a, _ in allv)) / 1e6}
+# SQ pass (tools/profile.sh "valu"): VALU lane activity, wave cycles and waits, per launch
+SQ = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+      "SQ_INSTS_FLAT", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR")
+sq = defaultdict(lambda: defaultdict(lambda: [0.0, set()]))
+for r in rows("valu/**/*counter_collection.csv"):
+    c = r.get("Counter_Name")
+    if c in SQ:
+        k = short(r.get("Kernel_Name", ""))
+        sq[k][c][0] += float(r["Counter_Value"])
+        sq[k][c][1].add(r.get("Dispatch_Id"))
+for k, d in sq.items():
+    n = max(len(d["SQ_INSTS_VALU"][1]), 1)
+    per = {c: d[c][0] / max(len(d[c][1]), 1) for c in d}
+    res[k]["sq_per_launch"] = per
+    if per.get("SQ_ACTIVE_INST_VALU"):
+        lanes = per["SQ_THREAD_CYCLES_VALU"] / per["SQ_ACTIVE_INST_VALU"]
+        res[k]["lanes_active_per_valu_inst"] = lanes
+        res[k]["valu_lane_ops_per_launch"] = per["SQ_INSTS_VALU"] * lanes
+    if per.get("SQ_WAVE_CYCLES"):
+        res[k]["wait_any_frac"] = per["SQ_WAIT_ANY"] / per["SQ_WAVE_CYCLES"]
+for u, parts in UNITS.items():
+    if all(p in res and "valu_lane_ops_per_launch" in res[p] for p in parts):
+        n = sum(res[p]["launches"] for p in parts)
+        ops = sum(res[p]["valu_lane_ops_per_launch"] * res[p]["launches"] for p in parts) / n
+        ins = sum(res[p]["sq_per_launch"]["SQ_INSTS_VALU"] * res[p]["launches"] for p in parts) / n
+        res[u]["valu_lane_ops_per_launch"] = ops
+        res[u]["lanes_active_per_valu_inst"] = ops / ins
 for tag, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
     acc = defaultdict(lambda: [0.0, 0])
     for r in rows(f"{tag}/**/*counter_collection.csv"):

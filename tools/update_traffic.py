@@ -14,7 +14,7 @@ os.makedirs(dst, exist_ok=True)
 summary = json.load(open(os.path.join(src, "summary.json")))
 shutil.copy(os.path.join(src, "summary.json"), os.path.join(dst, "rocprof_summary.json"))
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
-for name in ("bench_trace.json", "bench_fetch.json", "bench_write.json"):
+for name in ("bench_trace.json", "bench_fetch.json", "bench_write.json", "bench_valu.json"):
     p = os.path.join(src, name)
     if os.path.exists(p):
         shutil.copy(p, os.path.join(dst, name.replace("bench_", "bench_under_rocprof_")))
@@ -27,9 +27,11 @@ table["correction"] = ("hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950: FETCH_SIZE coun
                        "MI355X_MICROARCH.md HBM section); raw = FETCH_SIZE + WRITE_SIZE. Bytes per launch.")
 out = {"source": f"profiles/{rnd}/{workload}/rocprof_summary.json (tools/profile.sh: separate FETCH_SIZE and "
                  "WRITE_SIZE passes, no traces)"}
+KEYS = ("hbm_bytes_per_launch", "hbm_bytes_per_launch_raw", "avg_us", "launches", "busy_ms",
+        "valu_lane_ops_per_launch", "lanes_active_per_valu_inst", "wait_any_frac")
 for k, v in summary.items():
     if k.startswith("k_") and "hbm_bytes_per_launch" in v:
-        out[k] = {kk: v[kk] for kk in ("hbm_bytes_per_launch", "hbm_bytes_per_launch_raw", "avg_us", "launches")}
+        out[k] = {kk: v[kk] for kk in KEYS if kk in v}
 if "k_bdpt_trace_a" in out and "k_bdpt_vis" in out:  # bench.py's BDPT connection unit: both kernels
     a, b = out["k_bdpt_trace_a"], out["k_bdpt_vis"]
     n = a["launches"] + b["launches"]
@@ -45,6 +47,10 @@ for a_k, b_k in (("k_bounce_q", "k_bounce_tail"),):  # bench.py's fused unit: bo
             kk: (a[kk] * a["launches"] + b[kk] * b["launches"]) / n
             for kk in ("hbm_bytes_per_launch", "hbm_bytes_per_launch_raw", "avg_us")}
         out[a_k + "+" + b_k]["launches"] = n
+for u in ("k_bounce_q+k_bounce_tail", "k_bdpt_trace_a+k_bdpt_vis"):  # union busy time, VALU of the unit
+    if u in out and u in summary:
+        out[u].update({kk: summary[u][kk] for kk in ("busy_ms", "valu_lane_ops_per_launch", "lanes_active_per_valu_inst")
+                       if kk in summary[u]})
 table[workload] = out
 json.dump(table, open(path, "w"), indent=1, sort_keys=True)
 print("updated", dst)
