@@ -205,14 +205,17 @@ typedef struct {
 } lumo_scene_desc;
 
 /* Camera (camera.rs:17-38, CameraConfig): world_to_camera, screen_to_raster and
- * camera_to_screen transforms as (m, inv) row-major 4x4 pairs. Perspective only. */
+ * camera_to_screen transforms as (m, inv) row-major 4x4 pairs.  Camera::Perspective or
+ * Camera::Orthographic (camera.rs:127-132; generate_ray :257-268).  lumo's orthographic camera
+ * has no importance functions (camera.rs:348-351 `unimplemented!()`), so BDPT with it is
+ * LUMO_ERR_UNSUPPORTED, as it panics in lumo. */
 typedef struct {
     double world_to_camera[2][16];
     double screen_to_raster[2][16];
     double camera_to_screen[2][16];
     double lens_radius, focal_length;
     int64_t width, height;
-    int32_t orthographic; /* 0 = Perspective */
+    int32_t orthographic; /* 0 = Perspective, 1 = Orthographic */
     int32_t illuminant;   /* dense_spectra index used for white balance */
     double white_balance[9];   /* ColorSpace::wb_matrix (space.rs:144-151), row-major */
     double xyz_to_rgb[9];      /* colour space XYZ->RGB (default DCI-P3, space.rs:51-54) */
@@ -252,6 +255,10 @@ typedef struct {
 } lumo_tile_result;
 
 enum { LUMO_RNG_WAVEFRONT = 0, LUMO_RNG_LUMO_ORDER = 1 };
+/* SamplerType (samplers.rs:6-17), the pixel sampler of Renderer::sampler (renderer.rs:89-93).
+ * Sobol draws from a 10-bit sequence (samplers/sobol_seq.rs: SOBOL_MAX_LEN 1023): more than 1023
+ * samples per pixel panic in lumo and are LUMO_ERR_INVALID here. */
+enum { LUMO_SAMPLER_MULTI_JITTERED = 0, LUMO_SAMPLER_UNIFORM = 1, LUMO_SAMPLER_JITTERED = 2, LUMO_SAMPLER_SOBOL = 3 };
 enum { LUMO_INTEGRATOR_PATH_TRACE = 0, LUMO_INTEGRATOR_BDPT = 1 };
 
 typedef struct {
@@ -266,7 +273,8 @@ typedef struct {
      * row-major width x height x 3 array; when a task's result has no `splats` list, its
      * light-tracing taps are summed into it (film.rs:167-170; summation order unspecified, as
      * lumo's tile completion order). */
-    int32_t max_vertices, pad0;
+    int32_t max_vertices;
+    int32_t sampler;    /* LUMO_SAMPLER_* (0 = MultiJittered, lumo's default)                  */
     double* splat_film;
 } lumo_render_cfg;
 enum { LUMO_TONEMAP_NONE = 0, LUMO_TONEMAP_CLAMP = 1, LUMO_TONEMAP_REINHARD = 2 }; /* tone_mapping.rs */
@@ -355,6 +363,8 @@ void lumo_set_timing(int on);
 lumo_status lumo_debug_paths(void* ctx, const lumo_tile_task* task, lumo_path_dump* dump);
 /* Integrator of lumo_debug_paths (LUMO_INTEGRATOR_*; BDPT splats are not collected there). */
 lumo_status lumo_debug_set_integrator(void* ctx, int integrator);
+/* Pixel sampler of lumo_debug_paths (LUMO_SAMPLER_*). */
+lumo_status lumo_debug_set_sampler(void* ctx, int sampler);
 /* Diagnostics: per-bounce record (20 doubles per bounce, at most 64 bounces) of the path of
  * `pixel` in sample pass `pass` of `task`; *n_out = number of bounces recorded. */
 lumo_status lumo_debug_trace(void* ctx, const lumo_tile_task* task, int pass, int pixel, double* out,

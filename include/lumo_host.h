@@ -123,6 +123,8 @@ typedef struct {
     int32_t illuminant;  /* LUMO_DENSE_* */
     int32_t color_space; /* 0 sRGB, 1 DCI-P3 (default), 2 Rec. 2020 */
     double filter_radius, filter_sigma;
+    int32_t camera_type; /* CameraType (camera/builder.rs:4-9): 0 Perspective, 1 Orthographic */
+    int32_t pad0;
 } lumo_camera_params;
 void lumo_camera_params_default(lumo_camera_params* p);
 void lumo_camera_params_cornell_box(lumo_camera_params* p);

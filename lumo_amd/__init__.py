@@ -556,6 +556,11 @@ class Camera:
             self.p.illuminant = DENSE[name] if isinstance(name, str) else int(name)
             return self
 
+        def camera_type(self, t):
+            """CameraType (camera/builder.rs:4-9): CameraType.Perspective or CameraType.Orthographic."""
+            self.p.camera_type = int(t)
+            return self
+
         def color_space(self, cs):
             """0 sRGB, 1 DCI-P3 (default), 2 Rec. 2020 (color/space.rs)."""
             self.p.color_space = int(cs)
@@ -588,6 +593,20 @@ class Camera:
     @staticmethod
     def cornell_box(resolution=(512, 512)):
         return Camera.cornell_box_builder().resolution(resolution).build()
+
+
+class CameraType:
+    """camera/builder.rs:4-9."""
+    Perspective = 0
+    Orthographic = 1
+
+
+class SamplerType:
+    """samplers.rs:6-17: the pixel sampler of Renderer::sampler (renderer.rs:89-93)."""
+    MultiJittered = 0  # lumo's default
+    Uniform = 1
+    Jittered = 2
+    Sobol = 3  # at most 1023 samples per pixel (sobol_seq.rs SOBOL_MAX_LEN)
 
 
 class Integrator:
@@ -703,9 +722,10 @@ class Device:
         return np.split(big, off[1:-1]), [], res
 
     def render_tasks(self, tasks, max_paths=0, tone_map=None, integrator=0, splats_out=None, splat_film=None,
-                     max_vertices=0):
+                     max_vertices=0, sampler=0):
         """lumo_render_tiles over `tasks`; returns per-task (rgb_w array, result).
         tone_map: None, ToneMap.clamp(x) or ToneMap.REINHARD (tone_mapping.rs).
+        sampler: SamplerType (samplers.rs:6-17; default MultiJittered).
         integrator = Integrator.BDPathTrace: the light-tracing splats of each task are appended
         to `splats_out` (a list of (x, y, rgb) record arrays, lumo's order), or, when
         `splats_out` is None, summed into `splat_film` (an H x W x 3 float64 array)."""
@@ -729,7 +749,7 @@ class Device:
                     sbufs.append(sb)
                     res[i].splats = sb
                     res[i].splat_cap = caps[i]
-            cfg = _ffi.RenderCfg(integrator, 0, max_paths, tm[0], tm[1], max_vertices, 0,
+            cfg = _ffi.RenderCfg(integrator, 0, max_paths, tm[0], tm[1], max_vertices, int(sampler),
                                  splat_film.ctypes.data_as(_ffi.c_double_p) if (splat_film is not None and not lists)
                                  else None)
             st = L.lumo_render_tiles(self.ctx, arr, n, C.byref(cfg), res)
@@ -807,6 +827,7 @@ class Renderer:
         self._integrator = Integrator.PathTrace
         self._device = 0
         self._tone_map = ToneMap.NO_MAP
+        self._sampler = SamplerType.MultiJittered
 
     def samples(self, n):
         self._samples = int(n)
@@ -821,6 +842,13 @@ class Renderer:
         if i not in (Integrator.PathTrace, Integrator.BDPathTrace):
             raise ValueError(f"unknown integrator {i}")
         self._integrator = i
+        return self
+
+    def sampler(self, s):
+        """Renderer::sampler (renderer.rs:89-93): a SamplerType."""
+        if s not in (SamplerType.MultiJittered, SamplerType.Uniform, SamplerType.Jittered, SamplerType.Sobol):
+            raise ValueError(f"unknown sampler {s}")
+        self._sampler = s
         return self
 
     def tone_map(self, tm):
@@ -848,9 +876,9 @@ class Renderer:
         if self._integrator == Integrator.BDPathTrace:
             # light-tracing splats are summed on the device straight into the film's splat buffer
             bufs, res = dev.render_tasks(mine, tone_map=self._tone_map, integrator=self._integrator,
-                                         splat_film=film.splats)
+                                         splat_film=film.splats, sampler=self._sampler)
         else:
-            bufs, res = dev.render_tasks(mine, tone_map=self._tone_map)
+            bufs, res = dev.render_tasks(mine, tone_map=self._tone_map, sampler=self._sampler)
         for t, b in zip(mine, bufs):
             film.add_tile(t, b)
         self.num_rays = sum(r.num_rays for r in res)

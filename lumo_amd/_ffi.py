@@ -131,7 +131,7 @@ class TileResult(C.Structure):
 class RenderCfg(C.Structure):
     _fields_ = [("integrator", C.c_int32), ("rng_mode", C.c_int32), ("max_paths", C.c_int32),
                 ("tone_map", C.c_int32), ("tone_arg", C.c_double), ("max_vertices", C.c_int32),
-                ("pad0", C.c_int32), ("splat_film", c_double_p)]
+                ("sampler", C.c_int32), ("splat_film", c_double_p)]
 
 
 class RaySoA(C.Structure):
@@ -165,7 +165,8 @@ class CameraParams(C.Structure):
                 ("zoom", C.c_double), ("lens_radius", C.c_double), ("focal_length", C.c_double),
                 ("vfov", C.c_double), ("width", C.c_int64), ("height", C.c_int64),
                 ("illuminant", C.c_int32), ("color_space", C.c_int32),
-                ("filter_radius", C.c_double), ("filter_sigma", C.c_double)]
+                ("filter_radius", C.c_double), ("filter_sigma", C.c_double),
+                ("camera_type", C.c_int32), ("pad0", C.c_int32)]
 
 
 class PathDump(C.Structure):
@@ -194,6 +195,7 @@ DEVICE_API = [
     ("lumo_debug_stream", C.c_int32, [C.c_void_p, C.c_size_t]),
     ("lumo_scene_info", C.c_int32, [C.c_void_p, C.POINTER(SceneInfo)]),
     ("lumo_debug_set_integrator", C.c_int32, [C.c_void_p, C.c_int]),
+    ("lumo_debug_set_sampler", C.c_int32, [C.c_void_p, C.c_int]),
     ("lumo_debug_trace", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.c_int, C.c_int, c_double_p, C.POINTER(C.c_int)]),
     ("lumo_debug_paths", C.c_int32, [C.c_void_p, C.POINTER(TileTask), C.POINTER(PathDump)]),
 ]

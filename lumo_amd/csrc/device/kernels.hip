@@ -46,13 +46,22 @@ __global__ void k_init_seeds(Tasks T, Paths S, int n_tasks) {
     for (int s = T.first[ti]; s < T.first[ti + 1]; ++s) S.pseed[s] = xs_u64(r);
 }
 
-// MultiJitteredSampler::new (samplers.rs:148-171): two Fisher-Yates permutations per pixel.
+// SamplerType::new (samplers.rs:26-37) per pixel: the sampler's Xorshift::new(seed) (Uniform,
+// Jittered, MultiJittered) and, for MultiJitteredSampler::new (samplers.rs:148-171), its two
+// Fisher-Yates permutations; the state starts at the batch's first sample s0.  Sobol keeps no RNG
+// (its seed is the pixel seed, read by k_camera).
 __global__ void k_init_mj(Tasks T, Paths S, int n, int dim_stride) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     const lumo_tile_task& t = T.t[S.task[s]];
-    const uint64_t dim = (uint64_t)ceil(sqrt((double)t.total_samples));
+    S.mj_state[s] = t.batch * SAMPLES_INCREMENT;
     Xorshift r = xs_new(S.pseed[s]);
+    if (T.sampler != LUMO_SAMPLER_MULTI_JITTERED) {
+        S.mj_rng[2 * s] = r.hi;
+        S.mj_rng[2 * s + 1] = r.lo;
+        return;
+    }
+    const uint64_t dim = (uint64_t)ceil(sqrt((double)t.total_samples));
     uint16_t* px = S.perm + (size_t)s * 2 * dim_stride;
     uint16_t* py = px + dim_stride;
     for (int which = 0; which < 2; ++which) {
@@ -68,7 +77,45 @@ __global__ void k_init_mj(Tasks T, Paths S, int n, int dim_stride) {
     }
     S.mj_rng[2 * s] = r.hi;
     S.mj_rng[2 * s + 1] = r.lo;
-    S.mj_state[s] = t.batch * SAMPLES_INCREMENT;
+}
+
+// SobolSampler (samplers.rs:196-248, sobol_seq.rs): direction numbers m_i << (63 - i) of the two
+// dimensions (sobol_seq.rs:10-13, map_m_v :32-39).  The point after `n` steps from 0 is the XOR of
+// the directions at the set bits of the Gray code n ^ (n >> 1) (each step XORs the direction at
+// trailing_zeros(n), the bit in which consecutive Gray codes differ); BATCH_STATES[b] is the
+// point at n = 256 b, so the same closed form covers every batch.
+__device__ __forceinline__ uint64_t sobol_dir(int dimension, int i) {
+    const uint64_t m1[10] = {1, 1, 7, 15, 5, 19, 69, 51, 121, 695};
+    const uint64_t m2[10] = {1, 1, 7, 7, 7, 53, 57, 229, 473, 533};
+    return (dimension == 0 ? m1[i] : m2[i]) << (63 - i);
+}
+__device__ __forceinline__ uint64_t sobol_point(int dimension, uint64_t n) {
+    const uint64_t g = n ^ (n >> 1);
+    uint64_t x = 0;
+    for (int i = 0; i < 10; ++i)
+        if ((g >> i) & 1) x ^= sobol_dir(dimension, i);
+    return x;
+}
+
+// Sampler::next for the pixel's sampler (samplers.rs:61-248); `st` is the state before the call.
+__device__ __forceinline__ V2 sampler_next(int kind, const lumo_tile_task& t, const uint16_t* px, const uint16_t* py,
+                                           uint64_t st, Xorshift& mr, uint64_t pixel_seed) {
+    if (kind == LUMO_SAMPLER_UNIFORM) return xs_vec2(mr);  // UniformSampler::next (:73-84)
+    if (kind == LUMO_SAMPLER_SOBOL) {  // SobolSampler::next (:236-248): step, then shuffle the point
+        const uint64_t a = sobol_point(0, st + 1) ^ pixel_seed, b = sobol_point(1, st + 1) ^ pixel_seed;
+        const double s64 = 0x1p-64;  // Float::powi(2.0, -64)
+        return V2{(double)a * s64, (double)b * s64};
+    }
+    const uint64_t dim = (uint64_t)ceil(sqrt((double)t.total_samples));
+    const V2 scale0 = V2{1.0 / (double)dim, (double)dim / (double)t.total_samples};
+    const uint64_t x0 = st % dim, y0 = st / dim;
+    const V2 offset0 = scale0 * V2{(double)x0, (double)y0};
+    if (kind == LUMO_SAMPLER_JITTERED) return scale0 * xs_vec2(mr) + offset0;  // JitteredSampler::next (:113-131)
+    // MultiJitteredSampler::next (samplers.rs:174-193)
+    const V2 scale1 = scale0 / (double)dim;
+    const V2 offset1 = scale1 * V2{(double)px[y0], (double)py[x0]};
+    const V2 rsq = scale1 * xs_vec2(mr);
+    return offset0 + offset1 + rsq;
 }
 
 __device__ __forceinline__ uint64_t wf_path_seed(uint64_t pixel_seed, uint64_t k) {
@@ -92,31 +139,26 @@ __global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, in
         active = pass < t.samples;
         S.p_valid[s] = active ? 1u : 0u;
         if (active) {
-            // MultiJitteredSampler::next (samplers.rs:174-193)
-            const uint64_t dim = (uint64_t)ceil(sqrt((double)t.total_samples));
-            const V2 scale0 = V2{1.0 / (double)dim, (double)dim / (double)t.total_samples};
-            const V2 scale1 = scale0 / (double)dim;
             Xorshift mr{S.mj_rng[2 * s], S.mj_rng[2 * s + 1]};
             const uint64_t st = S.mj_state[s];
-            const uint64_t x0 = st % dim, y0 = st / dim;
             const uint16_t* px = S.perm + (size_t)s * 2 * dim_stride;
-            const uint16_t* py = px + dim_stride;
-            const V2 offset0 = scale0 * V2{(double)x0, (double)y0};
-            const V2 offset1 = scale1 * V2{(double)px[y0], (double)py[x0]};
-            const V2 rsq = scale1 * xs_vec2(mr);
+            const V2 rs = sampler_next(T.sampler, t, px, px + dim_stride, st, mr, S.pseed[s]);
             S.mj_state[s] = st + 1;
             S.mj_rng[2 * s] = mr.hi;
             S.mj_rng[2 * s + 1] = mr.lo;
             const int j = S.pix[s];
             const uint64_t W = t.px_max[0] - t.px_min[0];
             const V2 xy = V2{(double)(t.px_min[0] + (uint64_t)j % W), (double)(t.px_min[1] + (uint64_t)j / W)};
-            const V2 raster = xy + (offset0 + offset1 + rsq);
+            const V2 raster = xy + rs;
             // Integrator::integrate: lens sample (2 draws), then wavelengths (1 draw)
             r = xs_new(wf_path_seed(S.pseed[s], pass));
             const V2 lens = xs_vec2(r);
             const V3 screen = xf_pt_inv(cam.sctr, V3{raster.x, raster.y, 0.0});
-            const V3 wl0 = normalize(xf_pt_inv(cam.cts, screen));
-            V3 xo_local = V3{0, 0, 0}, wi_local = wl0;
+            // Camera::generate_ray (camera.rs:257-268): Perspective aims from the origin through the
+            // normalised camera-space point; Orthographic starts at the point, along +z
+            const V3 cpt = xf_pt_inv(cam.cts, screen);
+            const V3 wl0 = cam.orthographic ? V3{0.0, 0.0, 1.0} : normalize(cpt);
+            V3 xo_local = cam.orthographic ? cpt : V3{0, 0, 0}, wi_local = wl0;
             if (cam.lens_radius != 0.0) {  // camera.rs:221-243
                 const V2 lxy = cam.lens_radius * square_to_disk(lens);
                 const V3 lz = V3{lxy.x, lxy.y, 0.0};
@@ -610,6 +652,8 @@ struct Ctx {
     int max_vertices = 64;
     double* splat_film = nullptr;
     int debug_integrator = LUMO_INTEGRATOR_PATH_TRACE;  // lumo_debug_paths
+    int sampler = LUMO_SAMPLER_MULTI_JITTERED;          // of the lumo_render_tiles call in progress
+    int debug_sampler = LUMO_SAMPLER_MULTI_JITTERED;    // lumo_debug_paths
     // Launch intervals of the timed stages (ms from ref_ev, recorded before the first timed launch
     // after a stats reset): their union is a stage's busy time, which does not count twice the
     // time that launches on different streams overlap (lumo_stats_busy_ms)
@@ -1041,6 +1085,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     T.ring_lum = wbuf<double>(c, W_RING_LUM, SAMPLES_INCREMENT * n_tasks, st);
     T.ring_ptr = wbuf<uint32_t>(c, W_RING_PTR, n_tasks, st);
     T.delta = wbuf<double>(c, W_DELTA, n_tasks, st);
+    T.sampler = c.sampler;
     T.num_rays = wbuf<unsigned long long>(c, W_NUM_RAYS, n_tasks, st);
     T.queries = wbuf<unsigned long long>(c, W_TQUERIES, n_tasks, st);
     Dump D{};
@@ -1914,7 +1959,7 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
 lumo_status lumo_camera_set(void* ctx, const lumo_camera_desc* d) {
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c || !d) return LUMO_ERR_INVALID;
-    if (d->orthographic) return LUMO_ERR_UNSUPPORTED;
+    if (d->orthographic != 0 && d->orthographic != 1) return LUMO_ERR_INVALID;
     if (d->width <= 0 || d->height <= 0 || !(d->filter_radius > 0.0) || !(d->filter_sigma > 0.0)) return LUMO_ERR_INVALID;
     auto get = [](const double (&a)[2][16]) {
         Xform x;
@@ -1937,6 +1982,7 @@ lumo_status lumo_camera_set(void* ctx, const lumo_camera_desc* d) {
     c->cam.fsig = d->filter_sigma;
     c->cam.width = (double)d->width;
     c->cam.height = (double)d->height;
+    c->cam.orthographic = d->orthographic;
     {   // CameraConfig::new (camera.rs:47-76): image plane area at z = 1
         const DCam& k = c->cam;
         V3 p_min3 = xf_pt_inv(k.sctr, V3{0.0, 0.0, 0.0});
@@ -1962,6 +2008,12 @@ lumo_status lumo_render_tiles(void* ctx, const lumo_tile_task* tasks, size_t n, 
         return LUMO_ERR_UNSUPPORTED;
     if (cfg && (cfg->max_vertices < 0 || cfg->max_vertices > BDPT_MAX_DEPTH + 1)) return LUMO_ERR_INVALID;
     if (cfg && (cfg->tone_map < LUMO_TONEMAP_NONE || cfg->tone_map > LUMO_TONEMAP_REINHARD)) return LUMO_ERR_INVALID;
+    const int sampler = cfg ? cfg->sampler : LUMO_SAMPLER_MULTI_JITTERED;
+    if (sampler < LUMO_SAMPLER_MULTI_JITTERED || sampler > LUMO_SAMPLER_SOBOL) return LUMO_ERR_INVALID;
+    for (size_t i = 0; i < n && sampler == LUMO_SAMPLER_SOBOL; ++i)
+        if (tasks[i].total_samples > 1023) return LUMO_ERR_INVALID;  // sobol_seq.rs SOBOL_MAX_LEN (lumo panics)
+    if (cfg && cfg->integrator == LUMO_INTEGRATOR_BDPT && c->has_camera && c->cam.orthographic)
+        return LUMO_ERR_UNSUPPORTED;  // camera.rs:348-351: no importance for Orthographic (lumo panics)
     HIPCHK(hipSetDevice(c->device));
     struct CallScope {  // tone map and integrator settings apply to this call only
         Ctx* c;
@@ -1969,8 +2021,10 @@ lumo_status lumo_render_tiles(void* ctx, const lumo_tile_task* tasks, size_t n, 
             c->tone_map = LUMO_TONEMAP_NONE;
             c->integrator = LUMO_INTEGRATOR_PATH_TRACE;
             c->splat_film = nullptr;
+            c->sampler = LUMO_SAMPLER_MULTI_JITTERED;
         }
     } scope{c};
+    c->sampler = sampler;
     c->tone_map = cfg ? cfg->tone_map : LUMO_TONEMAP_NONE;
     c->tone_arg = cfg ? cfg->tone_arg : 0.0;
     c->integrator = cfg ? cfg->integrator : LUMO_INTEGRATOR_PATH_TRACE;
@@ -2111,10 +2165,22 @@ lumo_status lumo_debug_paths(void* ctx, const lumo_tile_task* task, lumo_path_du
     HIPCHK(hipSetDevice(c->device));
     Dump D{dump->radiance, dump->lambda_, dump->raster, dump->delta,
            reinterpret_cast<unsigned long long*>(dump->depth)};
+    if (c->debug_sampler == LUMO_SAMPLER_SOBOL && task->total_samples > 1023) return LUMO_ERR_INVALID;
+    if (c->debug_integrator == LUMO_INTEGRATOR_BDPT && c->has_camera && c->cam.orthographic) return LUMO_ERR_UNSUPPORTED;
     c->integrator = c->debug_integrator;
+    c->sampler = c->debug_sampler;
     const lumo_status st = render_impl(*c, task, 1, nullptr, &D, task->samples);
     c->integrator = LUMO_INTEGRATOR_PATH_TRACE;
+    c->sampler = LUMO_SAMPLER_MULTI_JITTERED;
     return st;
+}
+
+// Pixel sampler used by lumo_debug_paths (test hook).
+lumo_status lumo_debug_set_sampler(void* ctx, int sampler) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || sampler < LUMO_SAMPLER_MULTI_JITTERED || sampler > LUMO_SAMPLER_SOBOL) return LUMO_ERR_INVALID;
+    c->debug_sampler = sampler;
+    return LUMO_OK;
 }
 
 // Integrator used by lumo_debug_paths (test hook; BDPT splats are not collected there).

@@ -74,6 +74,7 @@ struct DCam {
     M3 wb, x2r;
     double fr, fsig;
     double width, height, image_plane_area;  // CameraConfig (camera.rs:47-76), for BDPT importance
+    int orthographic;                        // Camera::Orthographic (camera.rs:127-132)
 };
 
 // Path state (SoA)
@@ -159,6 +160,7 @@ struct Tasks {
     uint32_t* ring_ptr;
     double* delta;
     unsigned long long *num_rays, *queries;
+    int sampler;  // LUMO_SAMPLER_* of the call (samplers.rs:6-17)
 };
 
 struct Dump {

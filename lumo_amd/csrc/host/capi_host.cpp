@@ -307,13 +307,18 @@ static void params_from(const CameraParams& c, lumo_camera_params* p) {
     p->color_space = c.color_space;
     p->filter_radius = c.filter_radius;
     p->filter_sigma = c.filter_sigma;
+    p->camera_type = c.camera_type;
+    p->pad0 = 0;
 }
 void lumo_camera_params_default(lumo_camera_params* p) { params_from(CameraParams{}, p); }
 void lumo_camera_params_cornell_box(lumo_camera_params* p) { params_from(CameraParams::cornell_box(), p); }
 
 int lumo_camera_build(const lumo_camera_params* p, lumo_camera_desc* out) {
     if (!p || !out) return LUMO_ERR_INVALID;
-    if (p->width <= 0 || p->height <= 0 || !(p->zoom > 0.0) || !(p->vfov > 0.0 && p->vfov < 180.0) ||
+    // matrices.rs asserts: vfov in (0, 180) for the perspective projection only
+    if (p->camera_type != 0 && p->camera_type != 1) return LUMO_ERR_INVALID;
+    if (p->width <= 0 || p->height <= 0 || !(p->zoom > 0.0) ||
+        (p->camera_type == 0 && !(p->vfov > 0.0 && p->vfov < 180.0)) ||
         p->lens_radius < 0.0 || p->illuminant < 0 || p->illuminant >= DENSE_BUILTIN_COUNT ||
         !(p->filter_radius > 0.0) || !(p->filter_sigma > 0.0))
         return LUMO_ERR_INVALID;
@@ -332,6 +337,7 @@ int lumo_camera_build(const lumo_camera_params* p, lumo_camera_desc* out) {
     c.color_space = p->color_space;
     c.filter_radius = p->filter_radius;
     c.filter_sigma = p->filter_sigma;
+    c.camera_type = p->camera_type;
     *out = build_camera(c);
     return LUMO_OK;
 }

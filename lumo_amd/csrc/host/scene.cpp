@@ -1191,11 +1191,18 @@ CameraParams CameraParams::cornell_box() {
 }
 
 lumo_camera_desc build_camera(const CameraParams& p) {
-    // perspective_projection (matrices.rs:3-13)
-    const double near = 1e-2, far = 1e3;
-    const Xform projection = xf_perspective(near, far);
-    const double tan_vfov_inv = 1.0 / std::tan(p.vfov * (PI / 180.0) / 2.0);
-    const Xform cts = xf_mul(xf_scale(tan_vfov_inv, tan_vfov_inv, 1.0), projection);
+    Xform cts;
+    if (p.camera_type == 1) {
+        // orthographic_projection (matrices.rs:15-20): near 0, far 1
+        const double near = 0.0, far = 1.0;
+        cts = xf_mul(xf_scale(1.0, 1.0, 1.0 / (far - near)), xf_translation(0.0, 0.0, -near));
+    } else {
+        // perspective_projection (matrices.rs:3-13)
+        const double near = 1e-2, far = 1e3;
+        const Xform projection = xf_perspective(near, far);
+        const double tan_vfov_inv = 1.0 / std::tan(p.vfov * (PI / 180.0) / 2.0);
+        cts = xf_mul(xf_scale(tan_vfov_inv, tan_vfov_inv, 1.0), projection);
+    }
     // world_to_camera (matrices.rs:23-34)
     const V3 forward = normalize(p.towards - p.origin);
     const V3 right = normalize(cross(forward, p.up));
@@ -1225,7 +1232,7 @@ lumo_camera_desc build_camera(const CameraParams& p) {
     d.focal_length = p.focal_length;
     d.width = p.width;
     d.height = p.height;
-    d.orthographic = 0;
+    d.orthographic = p.camera_type == 1 ? 1 : 0;
     d.illuminant = p.illuminant;
     const M3 wb = cs_wb_matrix(p.color_space, builtin_dense(p.illuminant));
     const M3 x2r = cs_xyz_to_rgb(p.color_space);

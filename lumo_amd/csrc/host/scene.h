@@ -163,6 +163,7 @@ struct CameraParams {
     int illuminant = DENSE_D65;
     int color_space = CS_DCI_P3;
     double filter_radius = 1.5, filter_sigma = 1.5 / 4.0;
+    int camera_type = 0;  // 0 Perspective, 1 Orthographic (camera/builder.rs:4-9)
     static CameraParams cornell_box();  // camera.rs:139-148
 };
 lumo_camera_desc build_camera(const CameraParams& p);

@@ -52,6 +52,10 @@ int oracle_render_tiles(const lumo_scene_desc* scene, const lumo_camera_desc* ca
 void oracle_set_tone_map(int kind, double arg);
 /* Integrator for subsequent renders: LUMO_INTEGRATOR_PATH_TRACE or LUMO_INTEGRATOR_BDPT. */
 void oracle_set_integrator(int integrator);
+/* SamplerType of subsequent renders (LUMO_SAMPLER_*, samplers.rs:6-17; default MultiJittered). */
+void oracle_set_sampler(int sampler);
+/* The points SamplerType::new(batch, samples, seed) yields (x, y interleaved, at most cap). */
+int64_t oracle_sampler_points(uint64_t batch, uint64_t samples, uint64_t seed, double* out, int64_t cap);
 
 /* Per-path record of the wavefront order for one task (for per-path parity tests):
  * out arrays sized (pixels * samples), pixel-major within each pass (pass s, pixel j). */

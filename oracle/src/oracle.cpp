@@ -1354,6 +1354,7 @@ struct Cam {
     M3 wb, x2r;
     double fr, fsig;
     double width, height, image_plane_area;
+    int orthographic;  // Camera::Orthographic (camera.rs:127-132)
 };
 Cam cam_of(const lumo_camera_desc* c) {
     Cam k;
@@ -1378,6 +1379,7 @@ Cam cam_of(const lumo_camera_desc* c) {
     k.fsig = c->filter_sigma;
     k.width = (double)c->width;
     k.height = (double)c->height;
+    k.orthographic = c->orthographic;
     // CameraConfig::new (camera.rs:47-76): image plane area at z = 1
     V3 p_min3 = xf_pt_inv(k.sctr, V3{0.0, 0.0, 0.0});
     V3 p_max3 = xf_pt_inv(k.sctr, V3{k.width, k.height, 0.0});
@@ -1389,11 +1391,13 @@ Cam cam_of(const lumo_camera_desc* c) {
     k.image_plane_area = fabs(pd.x * pd.y);
     return k;
 }
-// camera.rs:257-268 (Perspective) + add_dof :221-243
+// camera.rs:257-268 (Perspective: from the lens centre through the normalised camera-space point;
+// Orthographic: from the camera-space point along Direction::Z) + add_dof :221-243
 Ray camera_ray(const Cam& k, V2 raster_xy, V2 rand_sq) {
     const V3 screen = xf_pt_inv(k.sctr, V3{raster_xy.x, raster_xy.y, 0.0});
-    const V3 wi_local0 = normalize(xf_pt_inv(k.cts, screen));
-    V3 xo_local = V3{0, 0, 0}, wi_local = wi_local0;
+    const V3 p_local = xf_pt_inv(k.cts, screen);  // CameraConfig::raster_to_camera (:111-115)
+    const V3 wi_local0 = k.orthographic ? V3{0.0, 0.0, 1.0} : normalize(p_local);
+    V3 xo_local = k.orthographic ? p_local : V3{0, 0, 0}, wi_local = wi_local0;
     if (k.lens_radius != 0.0) {
         const V2 lxy = k.lens_radius * square_to_disk(rand_sq);
         const V3 lens = V3{lxy.x, lxy.y, 0.0};
@@ -1912,32 +1916,101 @@ std::vector<size_t> gen_perm(Xorshift& rng, size_t n) {  // rng.rs:104-116
     }
     return p;
 }
+// SobolSampler's sequence (samplers/sobol_seq.rs): DEG = 10 direction numbers per dimension,
+// VS = map_m_v(m) = m_i << (64 - i - 1) (:10-13, 32-39); BATCH_STATES[b] = the point after 256 b
+// steps from 0 (get_batch_states :15-30, iterated here exactly as written).
+constexpr int SOBOL_DEG = 10;
+constexpr uint64_t SOBOL_MAX_LEN = (1u << SOBOL_DEG) - 1;
+struct SobolTables {
+    uint64_t vs1[SOBOL_DEG], vs2[SOBOL_DEG];
+    uint64_t batch_states[1 + SOBOL_MAX_LEN / SAMPLES_INCREMENT][2];
+    SobolTables() {
+        const uint64_t m1[SOBOL_DEG] = {1, 1, 7, 15, 5, 19, 69, 51, 121, 695};  // dim = 119
+        const uint64_t m2[SOBOL_DEG] = {1, 1, 7, 7, 7, 53, 57, 229, 473, 533};  // dim = 103
+        for (int i = 0; i < SOBOL_DEG; ++i) {
+            vs1[i] = m1[i] << (64 - i - 1);
+            vs2[i] = m2[i] << (64 - i - 1);
+        }
+        uint64_t state = 0, p0 = 0, p1 = 0;
+        while (state < SOBOL_MAX_LEN) {
+            if (state % SAMPLES_INCREMENT == 0) {
+                batch_states[state / SAMPLES_INCREMENT][0] = p0;
+                batch_states[state / SAMPLES_INCREMENT][1] = p1;
+            }
+            state += 1;
+            p0 ^= vs1[__builtin_ctzll(state)];
+            p1 ^= vs2[__builtin_ctzll(state)];
+        }
+    }
+};
+const SobolTables& sobol_tables() {
+    static const SobolTables t;
+    return t;
+}
+
+// Box<dyn Sampler> of SamplerType::new (samplers.rs:26-37): Uniform (:56-85), Jittered (:87-132),
+// MultiJittered (:134-193), Sobol (:195-248).
 struct MJ {
+    int kind = LUMO_SAMPLER_MULTI_JITTERED;
     uint64_t state, batch_end, dim;
     std::vector<size_t> px, py;
     V2 scale0, scale1;
     Xorshift rng;
+    uint64_t seed = 0, prev0 = 0, prev1 = 0;  // Sobol
 };
+int g_sampler = LUMO_SAMPLER_MULTI_JITTERED;  // set by oracle_set_sampler before a render
 MJ mj_new(uint64_t batch, uint64_t samples, uint64_t seed) {  // SamplerType::new (samplers.rs:26-37)
     const uint64_t s0 = batch * SAMPLES_INCREMENT;
     uint64_t s1 = (batch + 1) * SAMPLES_INCREMENT;
     s1 = std::min(s1, samples);
     MJ m;
-    m.rng = xs_new(seed);
-    m.dim = (uint64_t)std::ceil(std::sqrt((double)samples));
-    const V2 scale = V2{1.0 / (double)m.dim, (double)m.dim / (double)samples};
-    m.px = gen_perm(m.rng, m.dim);
-    m.py = gen_perm(m.rng, m.dim);
+    m.kind = g_sampler;
     m.state = s0;
     m.batch_end = s1;
+    if (m.kind == LUMO_SAMPLER_SOBOL) {  // SobolSampler::new (:204-218)
+        m.seed = seed;
+        m.prev0 = sobol_tables().batch_states[batch][0];
+        m.prev1 = sobol_tables().batch_states[batch][1];
+        return m;
+    }
+    m.rng = xs_new(seed);
+    if (m.kind == LUMO_SAMPLER_UNIFORM) {  // UniformSampler::new(s1 - s0, rng): state counts from 0
+        m.state = 0;
+        m.batch_end = s1 - s0;
+        return m;
+    }
+    m.dim = (uint64_t)std::ceil(std::sqrt((double)samples));
+    const V2 scale = V2{1.0 / (double)m.dim, (double)m.dim / (double)samples};
     m.scale0 = scale;
+    if (m.kind == LUMO_SAMPLER_JITTERED) return m;
+    m.px = gen_perm(m.rng, m.dim);
+    m.py = gen_perm(m.rng, m.dim);
     m.scale1 = scale / (double)m.dim;
     return m;
 }
 bool mj_next(MJ& m, V2* out) {
     if (m.state == m.batch_end) return false;
+    if (m.kind == LUMO_SAMPLER_UNIFORM) {
+        m.state += 1;
+        *out = xs_vec2(m.rng);
+        return true;
+    }
+    if (m.kind == LUMO_SAMPLER_SOBOL) {  // step (:220-226), then shuffle (:228-230) and scale
+        const SobolTables& tb = sobol_tables();
+        m.state += 1;
+        m.prev0 ^= tb.vs1[__builtin_ctzll(m.state)];
+        m.prev1 ^= tb.vs2[__builtin_ctzll(m.state)];
+        const double s64 = std::ldexp(1.0, -64);  // Float::powi(2.0, -64)
+        *out = V2{(double)(m.prev0 ^ m.seed) * s64, (double)(m.prev1 ^ m.seed) * s64};
+        return true;
+    }
     const uint64_t x0 = m.state % m.dim, y0 = m.state / m.dim;
     const V2 offset0 = m.scale0 * V2{(double)x0, (double)y0};
+    if (m.kind == LUMO_SAMPLER_JITTERED) {
+        m.state += 1;
+        *out = m.scale0 * xs_vec2(m.rng) + offset0;
+        return true;
+    }
     const V2 offset1 = m.scale1 * V2{(double)m.px[y0], (double)m.py[x0]};
     const V2 rand_sq = m.scale1 * xs_vec2(m.rng);
     m.state += 1;
@@ -2138,7 +2211,8 @@ void exec_wavefront(const Scene& sc, const Cam& k, const lumo_tile_task& t, lumo
 
 bool valid_task(const lumo_tile_task& t) {
     return t.px_max[0] > t.px_min[0] && t.px_max[1] > t.px_min[1] && t.samples >= 1 &&
-           t.samples <= SAMPLES_INCREMENT && t.total_samples >= 1;
+           t.samples <= SAMPLES_INCREMENT && t.total_samples >= 1 &&
+           (g_sampler != LUMO_SAMPLER_SOBOL || t.total_samples <= SOBOL_MAX_LEN);  // lumo panics past it
 }
 }  // namespace
 
@@ -2150,6 +2224,7 @@ extern "C" int oracle_render_tiles(const lumo_scene_desc* scene, const lumo_came
         if (!valid_task(tasks[i]) || !out[i].rgb_w) return LUMO_ERR_INVALID;
     const Scene sc{scene};
     const Cam k = cam_of(camera);
+    if (k.orthographic && g_integrator == LUMO_INTEGRATOR_BDPT) return LUMO_ERR_UNSUPPORTED;  // camera.rs:348-351
     if (threads < 1) threads = 1;
     g_splat_overflow = false;
     std::atomic<size_t> next{0};
@@ -2190,6 +2265,7 @@ extern "C" int oracle_trace_paths(const lumo_scene_desc* scene, const lumo_camer
     if (!scene || !camera || !task || !valid_task(*task)) return LUMO_ERR_INVALID;
     const Scene sc{scene};
     const Cam k = cam_of(camera);
+    if (k.orthographic && g_integrator == LUMO_INTEGRATOR_BDPT) return LUMO_ERR_UNSUPPORTED;
     Counters C;
     std::vector<Sample> paths;
     std::vector<double> deltas;
@@ -2375,6 +2451,22 @@ extern "C" int oracle_light_pdf(const lumo_scene_desc* scene, int light, const d
 extern "C" void oracle_set_tone_map(int kind, double arg) { g_tone = ToneMap{kind, arg}; }
 
 extern "C" void oracle_set_integrator(int integrator) { g_integrator = integrator; }
+extern "C" void oracle_set_sampler(int sampler) { g_sampler = sampler; }
+// Probe: the points a pixel sampler (SamplerType::new(batch, samples, seed) of the current
+// g_sampler) yields, x y interleaved; returns how many (at most cap).
+extern "C" int64_t oracle_sampler_points(uint64_t batch, uint64_t samples, uint64_t seed, double* out, int64_t cap) {
+    if (samples == 0 || batch * SAMPLES_INCREMENT >= samples) return -1;
+    if (g_sampler == LUMO_SAMPLER_SOBOL && samples > SOBOL_MAX_LEN) return -1;
+    MJ m = mj_new(batch, samples, seed);
+    V2 p;
+    int64_t k = 0;
+    while (k < cap && mj_next(m, &p)) {
+        out[2 * k] = p.x;
+        out[2 * k + 1] = p.y;
+        ++k;
+    }
+    return k;
+}
 
 // ------------------------------------------------------------------ MIS weights sum to one
 // bd_path_trace/mis_tests.rs:96-352 (test_scene, _from_light, _from_camera, _reverse): build a full

@@ -39,6 +39,10 @@ def load(path=None):
                                      C.POINTER(_ffi.HitSoA), C.c_int, C.POINTER(Counters)]
         lib.oracle_set_integrator.restype = None
         lib.oracle_set_integrator.argtypes = [C.c_int]
+        lib.oracle_set_sampler.restype = None
+        lib.oracle_set_sampler.argtypes = [C.c_int]
+        lib.oracle_sampler_points.restype = C.c_int64
+        lib.oracle_sampler_points.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, _ffi.c_double_p, C.c_int64]
         lib.oracle_set_tone_map.restype = None
         lib.oracle_set_tone_map.argtypes = [C.c_int, C.c_double]
         dp = _ffi.c_double_p
@@ -63,12 +67,14 @@ def load(path=None):
 
 
 def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path=None, tone_map=(0, 0.0),
-                 integrator=0, splats_out=None):
+                 integrator=0, splats_out=None, sampler=0):
     """Returns (list of rgb_w arrays, results array, counters).  With integrator = 1 (BDPT) the
-    per-task light-tracing splats are appended to `splats_out` (a list) as (x, y, rgb) arrays."""
+    per-task light-tracing splats are appended to `splats_out` (a list) as (x, y, rgb) arrays.
+    sampler: lumo_amd.SamplerType (samplers.rs:6-17)."""
     lib = load(path)
     lib.oracle_set_tone_map(*tone_map)
     lib.oracle_set_integrator(integrator)
+    lib.oracle_set_sampler(int(sampler))
     n = len(tasks)
     arr = tasks if isinstance(tasks, C.Array) else (_ffi.TileTask * n)(*tasks)
     caps = [16 * (t.px_max[0] - t.px_min[0]) * (t.px_max[1] - t.px_min[1]) * t.samples if integrator else 0
@@ -91,9 +97,13 @@ def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path
         if st == 7:  # LUMO_ERR_OOM: splat buffers too small, retry with the reported counts
             caps = [max(c, r.num_splats) for c, r in zip(caps, res)]
             continue
+        if st != 0:
+            lib.oracle_set_integrator(0)
+            lib.oracle_set_sampler(0)
         assert st == 0, st
         break
     lib.oracle_set_integrator(0)
+    lib.oracle_set_sampler(0)
     if splats_out is not None:
         for i in range(n):
             m = res[i].num_splats
@@ -103,9 +113,10 @@ def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path
     return bufs, res, cnt
 
 
-def trace_paths(scene_desc, camera_desc, task, path=None, integrator=0):
+def trace_paths(scene_desc, camera_desc, task, path=None, integrator=0, sampler=0):
     lib = load(path)
     lib.oracle_set_integrator(integrator)
+    lib.oracle_set_sampler(int(sampler))
     P = (task.px_max[0] - task.px_min[0]) * (task.px_max[1] - task.px_min[1])
     m = P * task.samples
     rad, lam, ras = np.zeros(4 * m), np.zeros(4 * m), np.zeros(2 * m)
@@ -115,6 +126,7 @@ def trace_paths(scene_desc, camera_desc, task, path=None, integrator=0):
                                 ras.ctypes.data_as(_ffi.c_double_p), depth.ctypes.data_as(_ffi.c_uint64_p),
                                 delta.ctypes.data_as(_ffi.c_double_p))
     lib.oracle_set_integrator(0)
+    lib.oracle_set_sampler(0)
     assert st == 0, st
     return dict(radiance=rad.reshape(-1, 4), lam=lam.reshape(-1, 4), raster=ras.reshape(-1, 2), depth=depth,
                 delta=delta)
@@ -208,3 +220,14 @@ def math(op, x):
     out = np.zeros((len(x), no))
     assert load().oracle_math(op, _dp(x), len(x), _dp(out)) == 0
     return out
+
+
+def sampler_points(sampler, batch, samples, seed):
+    """SamplerType::new(batch, samples, seed) of the oracle, all its points as an (n, 2) array."""
+    lib = load()
+    lib.oracle_set_sampler(int(sampler))
+    out = np.zeros(2 * 256)
+    n = lib.oracle_sampler_points(batch, samples, seed, out.ctypes.data_as(_ffi.c_double_p), 256)
+    lib.oracle_set_sampler(0)
+    assert n >= 0, n
+    return out[:2 * n].reshape(-1, 2)

@@ -6,7 +6,7 @@ import numpy as np
 from lumo_amd import _ffi
 
 
-def gpu_paths(dev, task):
+def gpu_paths(dev, task, sampler=0):
     """lumo_debug_paths: per-path radiance / wavelengths / raster / depth of one task."""
     P = (task.px_max[0] - task.px_min[0]) * (task.px_max[1] - task.px_min[1])
     m = P * task.samples
@@ -15,7 +15,12 @@ def gpu_paths(dev, task):
     dump = _ffi.PathDump(rad.ctypes.data_as(_ffi.c_double_p), lam.ctypes.data_as(_ffi.c_double_p),
                          ras.ctypes.data_as(_ffi.c_double_p), depth.ctypes.data_as(_ffi.c_uint64_p),
                          delta.ctypes.data_as(_ffi.c_double_p))
-    _ffi.check(_ffi.load().lumo_debug_paths(dev.ctx, C.byref(task), C.byref(dump)), "debug_paths")
+    lib = _ffi.load()
+    _ffi.check(lib.lumo_debug_set_sampler(dev.ctx, int(sampler)), "debug_set_sampler")
+    try:
+        _ffi.check(lib.lumo_debug_paths(dev.ctx, C.byref(task), C.byref(dump)), "debug_paths")
+    finally:
+        lib.lumo_debug_set_sampler(dev.ctx, 0)
     return dict(radiance=rad.reshape(-1, 4), lam=lam.reshape(-1, 4), raster=ras.reshape(-1, 2), depth=depth,
                 delta=delta)
 

@@ -68,3 +68,47 @@ def splitmix64(z):
     z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
     z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
     return z ^ (z >> 31)
+
+
+def sampler_points(kind, batch, total_samples, seed):
+    """SamplerType::new(batch, samples, seed) (samplers.rs:26-37) and every point it yields:
+    kind 1 Uniform (:56-85), 2 Jittered (:87-132), 3 Sobol (:195-248 with sobol_seq.rs);
+    0 MultiJittered is mj_offsets."""
+    s0 = batch * 256
+    s1 = min((batch + 1) * 256, total_samples)
+    if kind == 0:
+        return mj_offsets(batch, total_samples, seed, s1 - s0)
+    if kind == 1:
+        rng = Xorshift(seed)
+        return [rng.gen_vec2() for _ in range(s1 - s0)]
+    if kind == 2:
+        rng = Xorshift(seed)
+        dim = math.ceil(math.sqrt(float(total_samples)))
+        sc = (1.0 / dim, dim / total_samples)
+        out = []
+        for state in range(s0, s1):
+            off = (sc[0] * (state % dim), sc[1] * (state // dim))
+            u = rng.gen_vec2()
+            out.append((sc[0] * u[0] + off[0], sc[1] * u[1] + off[1]))
+        return out
+    # Sobol: sobol_seq.rs, written out as the const fns iterate
+    deg = 10
+    vs1 = [(m << (64 - i - 1)) & M64 for i, m in enumerate([1, 1, 7, 15, 5, 19, 69, 51, 121, 695])]
+    vs2 = [(m << (64 - i - 1)) & M64 for i, m in enumerate([1, 1, 7, 7, 7, 53, 57, 229, 473, 533])]
+    max_len = (1 << deg) - 1
+    batch_states = [(0, 0)] * (1 + max_len // 256)
+    state, prev = 0, (0, 0)
+    while state < max_len:
+        if state % 256 == 0:
+            batch_states[state // 256] = prev
+        state += 1
+        tz = (state & -state).bit_length() - 1
+        prev = (prev[0] ^ vs1[tz], prev[1] ^ vs2[tz])
+    state, prev = s0, batch_states[batch]
+    out = []
+    while state != s1:
+        state += 1
+        tz = (state & -state).bit_length() - 1
+        prev = (prev[0] ^ vs1[tz], prev[1] ^ vs2[tz])
+        out.append((float(prev[0] ^ seed) * 2.0 ** -64, float(prev[1] ^ seed) * 2.0 ** -64))
+    return out

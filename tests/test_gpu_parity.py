@@ -361,3 +361,55 @@ def test_busy_time_is_a_union(dev, cornell):
     assert 0 < unit <= st.kernel_ms[1] + st.kernel_ms[4] + 1e-3
     assert max(dev.busy_ms([1]), dev.busy_ms([4])) <= unit + 1e-6
     assert unit <= allst <= wall_ms
+
+
+@pytest.mark.parametrize("sampler", [L.SamplerType.Uniform, L.SamplerType.Jittered, L.SamplerType.Sobol,
+                                     L.SamplerType.MultiJittered])
+def test_samplers_match_oracle(dev, cornell, sampler):
+    """Renderer::sampler (samplers.rs:6-17): every SamplerType's raster positions, paths and tiles
+    equal the oracle's, over two 256-spp batches and a ragged one (300 spp: the batch offsets of
+    Jittered / MultiJittered strata and Sobol's BATCH_STATES)."""
+    cam = L.Camera.cornell_box((24, 16))
+    dev.upload(cornell, cam)
+    tasks = L.make_tasks(24, 16, 300, SEED)
+    for t in (tasks[0], tasks[-1]):
+        _cmp_paths(gpu_paths(dev, t, sampler), O.trace_paths(cornell.desc(), cam.desc, t, sampler=sampler))
+    bufs, res = dev.render_tasks(tasks, sampler=sampler)
+    obufs, ores, _ = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, oracle_threads(), sampler=sampler)
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+
+
+def test_sobol_length_limit(dev, cornell):
+    """sobol_seq.rs SOBOL_MAX_LEN = 1023: lumo panics past it; the device refuses the call."""
+    cam = L.Camera.cornell_box((16, 16))
+    dev.upload(cornell, cam)
+    with pytest.raises(Exception):
+        dev.render_tasks(L.make_tasks(16, 16, 1024, SEED), sampler=L.SamplerType.Sobol)
+    dev.render_tasks(L.make_tasks(16, 16, 1023, SEED)[:1], sampler=L.SamplerType.Sobol)
+
+
+@pytest.mark.parametrize("lens", [0.0, 0.03])
+def test_orthographic_matches_oracle(dev, lens):
+    """CameraType::Orthographic (camera.rs:257-268): dof.rs's own camera (orthographic, lens 0.03,
+    focal length |origin - towards|) and its pinhole variant: paths and tiles equal the oracle's."""
+    from test_samplers import ortho_camera
+    scene = dof_scene()
+    cam = ortho_camera((40, 32), lens)
+    dev.upload(scene, cam)
+    tasks = L.make_tasks(40, 32, 12, SEED)
+    _cmp_paths(gpu_paths(dev, tasks[2]), O.trace_paths(scene.desc(), cam.desc, tasks[2]))
+    bufs, res_ = dev.render_tasks(tasks)
+    obufs, ores, _ = O.render_tasks(scene.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+    for b, ob, r, orr in zip(bufs, obufs, res_, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+    assert np.concatenate(bufs).sum() > 0
+
+
+def test_orthographic_bdpt_refused(dev):
+    from test_samplers import ortho_camera
+    dev.upload(dof_scene(), ortho_camera((16, 16)))
+    with pytest.raises(Exception):
+        dev.render_tasks(L.make_tasks(16, 16, 1, SEED), integrator=L.Integrator.BDPathTrace, splats_out=[])
