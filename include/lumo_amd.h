@@ -371,9 +371,13 @@ lumo_status lumo_debug_trace(void* ctx, const lumo_tile_task* task, int pass, in
                              int* n_out);
 /* Kernel variant selected for the uploaded scene: kd stack class, bytes of scene staged in LDS
  * (0: no staging), feature class (1: instances / spheres / triangle lights / microfacet
- * materials), shadow rays per bounce (scene.rs:90-92). */
+ * materials), shadow rays per bounce (scene.rs:90-92).  Scenes too large to stage whole stage
+ * their TOP set in the closest-hit and visibility kernels: top_bytes of LDS per block (0: none),
+ * holding the first top_object_nodes / top_light_nodes nodes (breadth-first: the top levels) of
+ * the objects / lights BVH, the object items and the objects' traversal records. */
 typedef struct {
     int32_t stack_class, lds_bytes, full_kernels, n_shadow;
+    int32_t top_bytes, top_object_nodes, top_light_nodes, pad0;
 } lumo_scene_info_t;
 lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info);
 /* Diagnostics: one coalesced 8-B-per-lane read stream and one write stream over n doubles

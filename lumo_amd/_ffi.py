@@ -144,7 +144,8 @@ class HitSoA(C.Structure):
 
 class SceneInfo(C.Structure):
     _fields_ = [("stack_class", C.c_int32), ("lds_bytes", C.c_int32), ("full_kernels", C.c_int32),
-                ("n_shadow", C.c_int32)]
+                ("n_shadow", C.c_int32), ("top_bytes", C.c_int32), ("top_object_nodes", C.c_int32),
+                ("top_light_nodes", C.c_int32), ("pad0", C.c_int32)]
 
 
 STAGE_COUNT = 12  # LUMO_STAGE_COUNT

@@ -311,7 +311,7 @@ __device__ __forceinline__ BVtx vtx_of_hit(const DHit& h, DColor gathered, doubl
 template <int STK, int FX>
 __device__ int get_light_at(const DScene& sc, const BVtx& v, Counters& C) {
     const Ray ri = ray_new(ray_origin(vtx_hit(v), true), -v.ng);
-    return bvh_traverse<true, STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, rayx(ri), 0.0, DINF, C);
+    return bvh_traverse<true, STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, rayx(ri), 0.0, DINF, C);
 }
 
 // path_gen.rs:52-157.  Returns the number of vertices stored (root included), or -1 when the
@@ -511,8 +511,8 @@ __device__ bool bdpt_visible(const DScene& sc, const BVtx& a, const BVtx& b, Cou
     if (dot(ri.d, a.ng) < EPSILON) return false;
     const RayX rx = rayx(ri);
     double t = DINF;
-    t = rmin(t, bvh_hit_t<STK, FX>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, rx, 0.0, t, C));
-    t = rmin(t, bvh_hit_t<STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, rx, 0.0, t, C));
+    t = rmin(t, bvh_hit_t<STK, FX>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, rx, 0.0, t, C));
+    t = rmin(t, bvh_hit_t<STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, rx, 0.0, t, C));
     return fabs(sqrt(rmax(distance_squared(xo, xi), 0.0)) - t) < EPSILON;
 }
 

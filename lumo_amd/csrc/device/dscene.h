@@ -47,15 +47,30 @@ struct alignas(16) DKd {
 };
 constexpr int TV_STRIDE = 10;  // doubles per triangle in the vertex soup (A, B, C, pad) -> 80 B
 
-// BVH node as the device walks it: lumo's preorder layout (left child = i + 1) with the right
-// child replaced by the escape index, the next node in preorder after this node's subtree
-// (-1 past the end).  lumo's DFS (bvh.rs:315-362) pushes the right child and descends left; the
-// node it pops after a miss or a leaf is exactly the escape index, so the stackless walk visits
-// the same nodes in the same order with the same t_max at every test.
+// BVH node as the device walks it: lumo's node with the right child replaced by the escape
+// index, the next node in lumo's preorder after this node's subtree (-1 past the end), and the
+// left child stored explicitly (lumo: i + 1).  lumo's DFS (bvh.rs:315-362) pushes the right child
+// and descends left; the node it pops after a miss or a leaf is exactly the escape index, so the
+// stackless walk visits the same nodes in the same order with the same t_max at every test.  The
+// upload stores the nodes breadth-first (the explicit left child and escape index make the walk
+// independent of the storage order), so the top levels of a BVH are a prefix of its array: the
+// part that LDS staging of large scenes copies (TOP staging, below).
 struct DBvh {
     double bmin[3], bmax[3];
-    int32_t escape, first, count, pad0;
+    int32_t escape, first, count, left;
 };
+
+// Object as the traversal reads it (64 B; lumo_object, 168 B, stays the record for hit records,
+// Rectangle uv and light sampling): the kd tree's boundary, its root, the triangle and kd-item
+// bases, the shape type and the instance transform.  A Sphere keeps its radius in bmin[0].
+struct DObj {
+    double bmin[3], bmax[3];
+    int32_t kd_root, tri_base, item_base, tx;  // tx = (xform + 1) << 2 | type
+    __device__ __forceinline__ int type() const { return tx & 3; }
+    __device__ __forceinline__ int xform() const { return (tx >> 2) - 1; }
+};
+__device__ __forceinline__ double obj_radius(const DObj& o) { return o.bmin[0]; }
+__device__ __forceinline__ double obj_radius(const lumo_object& o) { return o.radius; }
 
 struct DScene {
     const double* vertices;
@@ -67,9 +82,11 @@ struct DScene {
     const lumo_kd_node* kd;
     const int32_t* kd_items;
     const lumo_object* objs;
+    const DObj* tobjs;  // traversal view of objs
     const DBvh* onodes;
     const int32_t* oitems;
     const lumo_object* lights;
+    const DObj* tlights;  // traversal view of lights
     const DBvh* lnodes;
     const int32_t* litems;
     const double* alias_prob;
@@ -89,8 +106,34 @@ struct DScene {
     const char* hot;
     uint32_t hot_bytes;
     uint32_t off_onodes, off_oitems, off_lnodes, off_litems, off_objs, off_lights, off_kd_items, off_tris, off_xforms,
-        off_tv, off_kdp;
+        off_tv, off_kdp, off_tobjs, off_tlights;
+    // TOP staging (large scenes, visibility and closest-hit kernels with LDS mode 2): the top levels
+    // of both BVHs (a prefix of their breadth-first arrays), the object items and the objects'
+    // traversal records, packed in `top` (top_bytes <= the LDS of one CU).  In a TOP view the
+    // first n_onodes_lds / n_lnodes_lds nodes are read from onodes_lds / lnodes_lds.
+    const char* top;
+    uint32_t top_bytes, off_top_onodes, off_top_lnodes, off_top_oitems, off_top_tobjs;
+    int32_t top_onodes, top_lnodes;  // nodes in the TOP set
+    const DBvh* onodes_lds;
+    const DBvh* lnodes_lds;
+    int32_t n_onodes_lds, n_lnodes_lds;
 };
+
+// TOP view: copy the packed top levels into LDS; the rest of the scene stays in HBM / L2.
+__device__ __forceinline__ DScene stage_top_lds(const DScene& sc, char* lds) {
+    const uint4* src = reinterpret_cast<const uint4*>(sc.top);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    for (uint32_t i = threadIdx.x; i < sc.top_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+    DScene v = sc;
+    v.onodes_lds = reinterpret_cast<const DBvh*>(lds + sc.off_top_onodes);
+    v.lnodes_lds = reinterpret_cast<const DBvh*>(lds + sc.off_top_lnodes);
+    v.n_onodes_lds = sc.top_onodes;
+    v.n_lnodes_lds = sc.top_lnodes;
+    v.oitems = reinterpret_cast<const int32_t*>(lds + sc.off_top_oitems);
+    v.tobjs = reinterpret_cast<const DObj*>(lds + sc.off_top_tobjs);
+    return v;
+}
 
 // Copy the packed traversal set into LDS and point a scene view at it.
 __device__ __forceinline__ DScene stage_scene_lds(const DScene& sc, char* lds) {
@@ -110,6 +153,8 @@ __device__ __forceinline__ DScene stage_scene_lds(const DScene& sc, char* lds) {
     v.xforms = reinterpret_cast<const lumo_transform*>(lds + sc.off_xforms);
     v.tv = reinterpret_cast<const double*>(lds + sc.off_tv);
     v.kdp = reinterpret_cast<const DKd*>(lds + sc.off_kdp);
+    v.tobjs = reinterpret_cast<const DObj*>(lds + sc.off_tobjs);
+    v.tlights = reinterpret_cast<const DObj*>(lds + sc.off_tlights);
     return v;
 }
 
@@ -496,7 +541,7 @@ __device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_mi
 #define KD_INLINE
 #endif
 template <bool GEO, int STK>
-__device__ KD_INLINE double kd_traverse(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min, double t_max,
+__device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const RayX& r, double t_min, double t_max,
                               int* idx_out, Counters& C) {
     const double origin[3] = {r.o.x, r.o.y, r.o.z};
     const double inv_dir[3] = {r.inv.x, r.inv.y, r.inv.z};
@@ -643,10 +688,11 @@ __device__ __forceinline__ EF ef_div(EF a, EF b) {
     return EF{a.v / b.v, previous_float(rmin(rmin(rmin(d0, d1), d2), d3)), next_float(rmax(rmax(rmax(d0, d1), d2), d3))};
 }
 // Sphere::hit (sphere.rs:27-78); FULL also builds the record
-template <bool FULL>
-__device__ bool sphere_hit(const lumo_object& ob, const RayX& r, double t_min, double t_max, DHit& out) {
+template <bool FULL, class OB>
+__device__ bool sphere_hit(const OB& ob, const RayX& r, double t_min, double t_max, DHit& out) {
+    const double radius = obj_radius(ob);
     const EF dx = ef(r.d.x), dy = ef(r.d.y), dz = ef(r.d.z), ox = ef(r.o.x), oy = ef(r.o.y), oz = ef(r.o.z);
-    const EF radius2 = ef_mul(ef(ob.radius), ef(ob.radius));
+    const EF radius2 = ef_mul(ef(radius), ef(radius));
     const EF a = ef_add(ef_add(ef_mul(dx, dx), ef_mul(dy, dy)), ef_mul(dz, dz));
     const EF b = ef_mul(ef(2.0), ef_add(ef_add(ef_mul(dx, ox), ef_mul(dy, oy)), ef_mul(dz, oz)));
     const EF c = ef_sub(ef_add(ef_add(ef_mul(ox, ox), ef_mul(oy, oy)), ef_mul(oz, oz)), radius2);
@@ -669,10 +715,12 @@ __device__ bool sphere_hit(const lumo_object& ob, const RayX& r, double t_min, d
         t = t1;
     }
     out.t = t.v;
-    if (!FULL) return true;
+    if constexpr (!FULL) {
+        return true;
+    } else {
     V3 xi = r.o + t.v * r.d;
-    xi = xi * ob.radius / length(xi);
-    const V3 ni = xi / ob.radius;
+    xi = xi * radius / length(xi);
+    const V3 ni = xi / radius;
     out.err = gamma_n(5) * vabs(xi);
     out.material = ob.material;
     out.backface = dot(r.d, ni) > 0.0;
@@ -681,12 +729,14 @@ __device__ bool sphere_hit(const lumo_object& ob, const RayX& r, double t_min, d
     out.ng = ni;
     out.uv = wrap_uv(V2{(lm_atan2(-ni.z, ni.x) + PI) / (2.0 * PI), lm_acos(-ni.y) / PI});
     return true;
+    }
 }
 // Sphere::hit_t (sphere.rs:80-97) with util::quadratic (object.rs:60-74)
-__device__ double sphere_hit_t(const lumo_object& ob, const RayX& r, double t_min, double t_max) {
+__device__ double sphere_hit_t(const DObj& ob, const RayX& r, double t_min, double t_max) {
     const double a = dot(r.d, r.d);
     const double b = 2.0 * dot(r.d, r.o);
-    const double c = dot(r.o, r.o) - ob.radius * ob.radius;
+    const double radius = obj_radius(ob);
+    const double c = dot(r.o, r.o) - radius * radius;
     const double disc = b * b - 4.0 * a * c;
     if (disc < 0.0) return DINF;
     const double root = sqrt(disc);
@@ -707,19 +757,19 @@ constexpr int PRIM_SPHERE = -2;
 // FX: full feature set (instances, spheres, triangle objects, microfacet materials); scenes made
 // only of kd meshes / rectangles with Lambertian + Light materials run the FX = false kernels.
 template <int STK, int FX>
-__device__ __forceinline__ double shape_hit_t(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
+__device__ __forceinline__ double shape_hit_t(const DScene& sc, const DObj& ob, const RayX& r, double t_min,
                                               double t_max, Counters& C) {
     if constexpr (FX) {
-        if (ob.type == LUMO_OBJ_TRIANGLE) return tri_hit_t(sc, ob.tri_base, r, t_min, t_max, C);
-        if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit_t(ob, r, t_min, t_max);
+        if (ob.type() == LUMO_OBJ_TRIANGLE) return tri_hit_t(sc, ob.tri_base, r, t_min, t_max, C);
+        if (ob.type() == LUMO_OBJ_SPHERE) return sphere_hit_t(ob, r, t_min, t_max);
     }
     return kd_traverse<false, STK>(sc, ob, r, t_min, t_max, nullptr, C);
 }
 template <int STK, int FX>
-__device__ __forceinline__ double object_hit_t(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
+__device__ __forceinline__ double object_hit_t(const DScene& sc, const DObj& ob, const RayX& r, double t_min,
                                                double t_max, Counters& C) {
     if constexpr (FX) {
-        if (ob.xform >= 0) return shape_hit_t<STK, FX>(sc, ob, ray_local(sc.xforms[ob.xform], r), t_min, t_max, C);
+        if (ob.xform() >= 0) return shape_hit_t<STK, FX>(sc, ob, ray_local(sc.xforms[ob.xform()], r), t_min, t_max, C);
     }
     return shape_hit_t<STK, FX>(sc, ob, r, t_min, t_max, C);
 }
@@ -727,14 +777,14 @@ __device__ __forceinline__ double object_hit_t(const DScene& sc, const lumo_obje
 // Object::hit: kd GEO traversal, then the winner's GEO test (acceptance + t only; the record is
 // rebuilt by object_record).  Returns the global triangle index, PRIM_SPHERE, or -1 (miss).
 template <int STK, int FX>
-__device__ __forceinline__ int shape_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
+__device__ __forceinline__ int shape_hit_tri(const DScene& sc, const DObj& ob, const RayX& r, double t_min,
                                              double t_max, Counters& C, DHit& out) {
     if constexpr (FX) {
-        if (ob.type == LUMO_OBJ_TRIANGLE) {
+        if (ob.type() == LUMO_OBJ_TRIANGLE) {
             C.tri++;  // the GEO test counts as a triangle test (triangle.rs:63, as the oracle counts it)
             return tri_hit_geo<false>(sc, ob.tri_base, r, t_min, t_max, out) ? ob.tri_base : -1;
         }
-        if (ob.type == LUMO_OBJ_SPHERE) return sphere_hit<false>(ob, r, t_min, t_max, out) ? PRIM_SPHERE : -1;
+        if (ob.type() == LUMO_OBJ_SPHERE) return sphere_hit<false>(ob, r, t_min, t_max, out) ? PRIM_SPHERE : -1;
     }
     int idx = -1;
     kd_traverse<true, STK>(sc, ob, r, t_min, t_max, &idx, C);
@@ -744,10 +794,10 @@ __device__ __forceinline__ int shape_hit_tri(const DScene& sc, const lumo_object
     return ob.tri_base + idx;
 }
 template <int STK, int FX>
-__device__ __forceinline__ int object_hit_tri(const DScene& sc, const lumo_object& ob, const RayX& r, double t_min,
+__device__ __forceinline__ int object_hit_tri(const DScene& sc, const DObj& ob, const RayX& r, double t_min,
                                               double t_max, Counters& C, DHit& out) {
     if constexpr (FX) {
-        if (ob.xform >= 0) return shape_hit_tri<STK, FX>(sc, ob, ray_local(sc.xforms[ob.xform], r), t_min, t_max, C, out);
+        if (ob.xform() >= 0) return shape_hit_tri<STK, FX>(sc, ob, ray_local(sc.xforms[ob.xform()], r), t_min, t_max, C, out);
     }
     return shape_hit_tri<STK, FX>(sc, ob, r, t_min, t_max, C, out);
 }
@@ -771,11 +821,12 @@ __device__ void object_record(const DScene& sc, const lumo_object& ob, int tri, 
     }
 }
 
-// bvh.rs:315-362 (stackless, see DBvh): returns object index or -1
-template <bool GEO, int STK, int FX>
+// bvh.rs:315-362 (stackless, see DBvh): returns object index or -1.  TOP: nodes below n_lds are
+// read from the LDS copy nodes_lds (TOP staging), the others from `nodes`.
+template <bool GEO, int STK, int FX, bool TOP = false>
 __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, const int32_t* items,
-                            const lumo_object* objs, const RayX& r, double t_min, double t_max, Counters& C,
-                            double* t_found = nullptr) {
+                            const DObj* objs, const RayX& r, double t_min, double t_max, Counters& C,
+                            double* t_found = nullptr, const DBvh* nodes_lds = nullptr, int n_lds = 0) {
     if (n_nodes == 0) return -1;
     const V3 inv_dir = r.inv;
     int curr = 0, idx = -1;
@@ -787,7 +838,7 @@ __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, co
     for (;;) {
         int count = 0;
         while (curr >= 0) {
-            const DBvh& node = nodes[curr];
+            const DBvh& node = (TOP && curr < n_lds) ? nodes_lds[curr] : nodes[curr];
             double ts, te;
             C.aabb++;
             slab(node.bmin, node.bmax, r.o, inv_dir, ts, te);
@@ -796,7 +847,7 @@ __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, co
             if (ts <= te) {
                 count = node.count;
                 if (count == 0) {
-                    curr += 1;
+                    curr = node.left;
                     continue;
                 }
                 break;
@@ -804,11 +855,11 @@ __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, co
             curr = node.escape;
         }
         if (curr < 0) break;
-        const DBvh& node = nodes[curr];
+        const DBvh& node = (TOP && curr < n_lds) ? nodes_lds[curr] : nodes[curr];
         {
 #else
     while (curr >= 0) {
-        const DBvh& node = nodes[curr];
+        const DBvh& node = (TOP && curr < n_lds) ? nodes_lds[curr] : nodes[curr];
         double ts, te;
         C.aabb++;
         slab(node.bmin, node.bmax, r.o, inv_dir, ts, te);
@@ -817,7 +868,7 @@ __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, co
         if (ts <= te) {
             const int count = node.count;
             if (count == 0) {
-                curr += 1;
+                curr = node.left;
                 continue;
             }
 #endif
@@ -841,14 +892,14 @@ __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, co
 }
 
 // BVH::hit_t (bvh.rs:371-374)
-template <int STK, int FX>
+template <int STK, int FX, bool TOP = false>
 __device__ __forceinline__ double bvh_hit_t(const DScene& sc, const DBvh* nodes, int n, const int32_t* items,
-                                            const lumo_object* objs, const RayX& r, double t_min, double t_max,
-                                            Counters& C) {
+                                            const DObj* objs, const RayX& r, double t_min, double t_max,
+                                            Counters& C, const DBvh* nodes_lds = nullptr, int n_lds = 0) {
     // bvh.rs:371-374 re-runs objects[idx].hit_t(r, t_min, t_max); in any-hit mode the traversal
     // called exactly that (tt == t_max), so its value is reused.
     double t = DINF;
-    const int idx = bvh_traverse<false, STK, FX>(sc, nodes, n, items, objs, r, t_min, t_max, C, &t);
+    const int idx = bvh_traverse<false, STK, FX, TOP>(sc, nodes, n, items, objs, r, t_min, t_max, C, &t, nodes_lds, n_lds);
     if (idx < 0) return DINF;
     return t;
 }
@@ -858,22 +909,24 @@ struct HitRef {
     double t;
     int kind, obj, tri;
 };
-template <int STK, int FX>
+template <int STK, int FX, bool TOP = false>
 __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     HitRef h{DINF, 0, -1, -1};
     double t_max = DINF;
     DHit g;
-    int oi = bvh_traverse<true, STK, FX>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C);
+    int oi = bvh_traverse<true, STK, FX, TOP>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, r, 0.0, t_max, C, nullptr,
+                                              sc.onodes_lds, sc.n_onodes_lds);
     if (oi >= 0) {
-        const int tri = object_hit_tri<STK, FX>(sc, sc.objs[oi], r, 0.0, t_max, C, g);
+        const int tri = object_hit_tri<STK, FX>(sc, sc.tobjs[oi], r, 0.0, t_max, C, g);
         if (tri != -1) {
             h = HitRef{g.t, 1, oi, tri};
             t_max = g.t;
         }
     }
-    const int li = bvh_traverse<true, STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C);
+    const int li = bvh_traverse<true, STK, FX, TOP>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, r, 0.0, t_max, C,
+                                                    nullptr, sc.lnodes_lds, sc.n_lnodes_lds);
     if (li >= 0) {
-        const int tri = object_hit_tri<STK, FX>(sc, sc.lights[li], r, 0.0, t_max, C, g);
+        const int tri = object_hit_tri<STK, FX>(sc, sc.tlights[li], r, 0.0, t_max, C, g);
         if (tri != -1) h = HitRef{g.t, 2, li, tri};
     }
     return h;
@@ -887,30 +940,36 @@ __device__ __forceinline__ void hit_record(const DScene& sc, const HitRef& hr, c
 }
 
 // Scene::hit_light (scene.rs:165-189): returns true and the light hit if visible.
-template <int STK, int FX>
+template <int STK, int FX, bool TOP = false>
 __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit& lh, Counters& C) {
-    const lumo_object& L = sc.lights[light];
-    const int tri = object_hit_tri<STK, FX>(sc, L, r, 0.0, DINF, C, lh);
+    const int tri = object_hit_tri<STK, FX>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
     if (tri == -1) return false;
     const double t_max = lh.t - EPSILON;
-    if (bvh_hit_t<STK, FX>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C) < t_max) return false;
-    if (bvh_hit_t<STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C) < t_max) return false;
+    if (bvh_hit_t<STK, FX, TOP>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, r, 0.0, t_max, C, sc.onodes_lds,
+                                sc.n_onodes_lds) < t_max)
+        return false;
+    if (bvh_hit_t<STK, FX, TOP>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, r, 0.0, t_max, C, sc.lnodes_lds,
+                                sc.n_lnodes_lds) < t_max)
+        return false;
     // visible: build the light hit record (same GEO test, now in full)
-    object_record<FX>(sc, L, tri, r, lh);
+    object_record<FX>(sc, sc.lights[light], tri, r, lh);
     return true;
 }
 
 // Scene::hit_light without the record: the light triangle (or PRIM_SPHERE) when visible, else -1;
 // object_record rebuilds the record (the same GEO test).
-template <int STK, int FX>
+template <int STK, int FX, bool TOP = false>
 __device__ int scene_hit_light_tri(const DScene& sc, const RayX& r, int light, Counters& C) {
-    const lumo_object& L = sc.lights[light];
     DHit lh;
-    const int tri = object_hit_tri<STK, FX>(sc, L, r, 0.0, DINF, C, lh);
+    const int tri = object_hit_tri<STK, FX>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
     if (tri == -1) return -1;
     const double t_max = lh.t - EPSILON;
-    if (bvh_hit_t<STK, FX>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.objs, r, 0.0, t_max, C) < t_max) return -1;
-    if (bvh_hit_t<STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.lights, r, 0.0, t_max, C) < t_max) return -1;
+    if (bvh_hit_t<STK, FX, TOP>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, r, 0.0, t_max, C, sc.onodes_lds,
+                                sc.n_onodes_lds) < t_max)
+        return -1;
+    if (bvh_hit_t<STK, FX, TOP>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, r, 0.0, t_max, C, sc.lnodes_lds,
+                                sc.n_lnodes_lds) < t_max)
+        return -1;
     return tri;
 }
 

@@ -23,7 +23,10 @@ void launch_closest(const TravLaunch& l, const DScene& sc, const Paths& S, const
 
 template <int STK>
 void launch_closest_q(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& cur, uint32_t skip_below) {
-    if (l.lds) {
+    if (l.top) {
+        if (l.fx) k_closest_q<STK, 2, true><<<l.grid, TOP_BLOCK, l.shm, l.sm>>>(sc, S, cur, skip_below);
+        else k_closest_q<STK, 2, false><<<l.grid, TOP_BLOCK, l.shm, l.sm>>>(sc, S, cur, skip_below);
+    } else if (l.lds) {
         if (l.fx) k_closest_q<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, cur, skip_below);
         else k_closest_q<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, cur, skip_below);
     } else {
@@ -34,7 +37,11 @@ void launch_closest_q(const TravLaunch& l, const DScene& sc, const Paths& S, con
 
 template <int STK, bool NS1>
 void launch_shadow_q_ns(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& nxt) {
-    if (l.fx == 2) {  // textured scenes: emission textures (no LDS staging variant)
+    if (l.top) {  // TOP staging: the BVHs' top levels and the object records in LDS
+        if (l.fx == 2) k_shadow_q<STK, 2, 2, NS1><<<l.grid, TOP_BLOCK, l.shm, l.sm>>>(sc, S, nxt);
+        else if (l.fx) k_shadow_q<STK, 2, 1, NS1><<<l.grid, TOP_BLOCK, l.shm, l.sm>>>(sc, S, nxt);
+        else k_shadow_q<STK, 2, 0, NS1><<<l.grid, TOP_BLOCK, l.shm, l.sm>>>(sc, S, nxt);
+    } else if (l.fx == 2) {  // textured scenes: emission textures (no whole-scene LDS staging variant)
         k_shadow_q<STK, false, 2, NS1><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, nxt);
     } else if (l.lds) {
         if (l.fx) k_shadow_q<STK, true, true, NS1><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, nxt);
@@ -83,8 +90,13 @@ void launch_bounce_q(const TravLaunch& l, const DScene& sc, const Paths& S, cons
 template <int STK>
 void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, const double* d, const int32_t* light,
                   int n, int any_hit, double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
-                  unsigned long long* tcount) {
-    k_trace<STK><<<grid, BLOCK, 0, sm>>>(sc, o, d, light, n, any_hit, t_out, kind_out, obj_out, prim_out, tcount);
+                  unsigned long long* tcount, bool top) {
+    if (top)
+        k_trace<STK, true><<<grid, TOP_BLOCK, sc.top_bytes, sm>>>(sc, o, d, light, n, any_hit, t_out, kind_out, obj_out,
+                                                                  prim_out, tcount);
+    else
+        k_trace<STK, false><<<grid, BLOCK, 0, sm>>>(sc, o, d, light, n, any_hit, t_out, kind_out, obj_out, prim_out,
+                                                    tcount);
 }
 
 template void launch_closest<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const int32_t*);
@@ -93,7 +105,7 @@ template void launch_shadow_q<LUMO_STK>(const TravLaunch&, const DScene&, const 
 template void launch_bounce_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Tasks&, const QState&,
                                         const QState&, uint32_t, bool, int, int);
 template void launch_trace<LUMO_STK>(int, hipStream_t, const DScene&, const double*, const double*, const int32_t*,
-                                     int, int, double*, int32_t*, int32_t*, int32_t*, unsigned long long*);
+                                     int, int, double*, int32_t*, int32_t*, int32_t*, unsigned long long*, bool);
 
 }  // namespace dev
 }  // namespace lumo

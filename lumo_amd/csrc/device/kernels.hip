@@ -640,6 +640,8 @@ struct Ctx {
     lumo_stats stats{};
     hipEvent_t ev[2 * ST_COUNT];
     int lds_grid_cap = 2048;
+    int top_grid_cap = 1024;  // TOP-staged traversal kernels: blocks of TOP_BLOCK threads (LUMO_TOP_GRID)
+    int top_lds_bytes = 160 * 1024 - 256;  // TOP set budget (LUMO_TOP_KB)
     int tone_map = LUMO_TONEMAP_NONE;  // of the lumo_render_tiles call in progress
     double tone_arg = 0.0;
     // per-bounce queue-count snapshots (pinned) and their completion events
@@ -843,12 +845,21 @@ int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from 
 int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
 int g_heads = 0;                   // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
 int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
+// allow_top: the kernel has a TOP-staged variant (k_closest_q, k_shadow_q); it is used when the
+// whole scene does not fit in LDS but its top levels were packed at upload (DScene::top).
+int g_top = 1;  // LUMO_TOP=0: no TOP staging
 template <typename F>
-void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr) {
+void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr, bool allow_top = false) {
     const bool lds = g_lds && c.sc.hot_bytes > 0;
+    const bool top = !lds && allow_top && g_top && c.sc.top_bytes > 0;
     const int grid_full = ceil_div(count, BLOCK);
-    const TravLaunch l{lds ? std::min(grid_full, c.lds_grid_cap) : grid_full, lds ? (size_t)c.sc.hot_bytes : 0, lds,
-                       c.sc.full, stream ? stream : c.stream};
+    TravLaunch l{lds ? std::min(grid_full, c.lds_grid_cap) : grid_full, lds ? (size_t)c.sc.hot_bytes : 0, lds,
+                 c.sc.full, stream ? stream : c.stream};
+    if (top) {
+        l.top = true;
+        l.grid = std::min(ceil_div(count, TOP_BLOCK), c.top_grid_cap);
+        l.shm = c.sc.top_bytes;
+    }
     by_stack_class(c.sc.stack_class, [&](auto K) { f(K, l); });
 }
 
@@ -1278,9 +1289,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 }
                 {
                     StageTimer tm(c, g_timing, ST_CLOSEST);
-                    launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
-                        launch_closest_q<decltype(K)::value>(l, c.sc, S, cur, skip);
-                    });
+                    launch_trav(
+                        c, ub, [&](auto K, const TravLaunch& l) { launch_closest_q<decltype(K)::value>(l, c.sc, S, cur, skip); },
+                        nullptr, true);
                 }
                 {
                     StageTimer tm(c, g_timing, ST_SHADE);
@@ -1307,8 +1318,10 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                 }
                 {
                     StageTimer tm(c, g_timing, ST_SHADOW);
-                    launch_trav(c, (uint64_t)ub * (uint32_t)ns,
-                                [&](auto K, const TravLaunch& l) { launch_shadow_q<decltype(K)::value>(l, c.sc, S, nxt); });
+                    launch_trav(
+                        c, (uint64_t)ub * (uint32_t)ns,
+                        [&](auto K, const TravLaunch& l) { launch_shadow_q<decltype(K)::value>(l, c.sc, S, nxt); }, nullptr,
+                        true);
                 }
                 if (ns > 1) {
                     StageTimer tm(c, g_timing, ST_RESOLVE);
@@ -1620,6 +1633,9 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_LDS")) g_lds = e[0] != '0';
     if (const char* e = std::getenv("LUMO_BUCKETS")) g_buckets = e[0] == '0' ? 1 : NB;
     if (const char* e = std::getenv("LUMO_LDS_GRID")) c->lds_grid_cap = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("LUMO_TOP_GRID")) c->top_grid_cap = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("LUMO_TOP")) g_top = std::atoi(e);
+    if (const char* e = std::getenv("LUMO_TOP_KB")) c->top_lds_bytes = std::max(0, std::atoi(e)) * 1024;
     if (const char* e = std::getenv("LUMO_FUSED")) g_fused = std::atoi(e);
     if (const char* e = std::getenv("LUMO_QSORT")) g_qsort = std::atoi(e) & 3;
     if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -1715,24 +1731,54 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     chk(upload(*c, d->triangles, (size_t)d->num_triangles, &s.tris));
     chk(upload(*c, d->kd_nodes, (size_t)d->num_kd_nodes, &s.kd));
     chk(upload(*c, d->kd_items, (size_t)d->num_kd_items, &s.kd_items));
-    // device BVHs: right child -> escape index (DBvh, dscene.h)
+    // device BVHs (DBvh, dscene.h): right child -> escape index (lumo's preorder successor of the
+    // subtree), left child explicit, nodes stored breadth-first so the top levels are a prefix
+    bool bvh_ok = true;
     auto escapes = [&](const lumo_bvh_node* nodes, int n, std::vector<DBvh>& out) {
         out.assign(n > 0 ? n : 0, DBvh{});
-        std::vector<int32_t> esc(n > 0 ? n : 1, -1);
+        if (n <= 0) return;
+        std::vector<int32_t> esc(n, -1);
         for (int i = 0; i < n; ++i) {  // parents precede children (preorder)
             const lumo_bvh_node& b = nodes[i];
             if (b.count == 0) {
-                if (i + 1 < n) esc[i + 1] = b.right >= 0 ? b.right : esc[i];
-                if (b.right >= 0 && b.right < n) esc[b.right] = esc[i];
+                if (i + 1 >= n || (b.right >= n)) {
+                    bvh_ok = false;
+                    return;
+                }
+                esc[i + 1] = b.right >= 0 ? b.right : esc[i];
+                if (b.right >= 0) esc[b.right] = esc[i];
             }
         }
-        for (int i = 0; i < n; ++i) {
-            DBvh& o = out[i];
+        std::vector<int32_t> order, at(n, -1);  // breadth-first order; at[old] = new index
+        order.reserve(n);
+        order.push_back(0);
+        at[0] = 0;
+        for (size_t h = 0; h < order.size(); ++h) {
+            const int i = order[h];
+            if (nodes[i].count != 0) continue;
+            for (const int ch : {i + 1, nodes[i].right}) {
+                if (ch < 0) continue;
+                if (at[ch] >= 0) {  // not a tree
+                    bvh_ok = false;
+                    return;
+                }
+                at[ch] = (int32_t)order.size();
+                order.push_back(ch);
+            }
+        }
+        if ((int)order.size() != n) {  // unreachable nodes: not lumo's layout
+            bvh_ok = false;
+            return;
+        }
+        for (int k = 0; k < n; ++k) {
+            const int i = order[k];
+            DBvh& o = out[k];
             for (int a = 0; a < 3; ++a) {
                 o.bmin[a] = nodes[i].bmin[a];
                 o.bmax[a] = nodes[i].bmax[a];
             }
-            o.escape = esc[i];
+            o.escape = esc[i] >= 0 ? at[esc[i]] : -1;
+            o.left = nodes[i].count == 0 ? at[i + 1] : -1;
             o.first = nodes[i].first;
             o.count = nodes[i].count;
         }
@@ -1740,6 +1786,10 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     std::vector<DBvh> obvh, lbvh;
     escapes(d->object_nodes, d->num_object_nodes, obvh);
     escapes(d->light_nodes, d->num_light_nodes, lbvh);
+    if (!bvh_ok) {
+        free_scene(*c);
+        return LUMO_ERR_INVALID;
+    }
     chk(upload(*c, obvh.data(), obvh.size(), &s.onodes));
     chk(upload(*c, d->object_items, (size_t)d->num_object_items, &s.oitems));
     chk(upload(*c, lbvh.data(), lbvh.size(), &s.lnodes));
@@ -1844,8 +1894,28 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     };
     const std::vector<lumo_object> objs_dev = relaid(d->objects, d->num_objects);
     const std::vector<lumo_object> lights_dev = relaid(d->lights, d->num_lights);
+    auto trav_view = [](const std::vector<lumo_object>& v) {  // DObj (dscene.h): what the walks read
+        std::vector<DObj> t(v.size());
+        for (size_t i = 0; i < v.size(); ++i) {
+            const lumo_object& o = v[i];
+            DObj& x = t[i];
+            for (int a = 0; a < 3; ++a) {
+                x.bmin[a] = o.bmin[a];
+                x.bmax[a] = o.bmax[a];
+            }
+            if (o.type == LUMO_OBJ_SPHERE) x.bmin[0] = o.radius;
+            x.kd_root = o.kd_root;
+            x.tri_base = o.tri_base;
+            x.item_base = o.item_base;
+            x.tx = ((o.xform + 1) << 2) | o.type;
+        }
+        return t;
+    };
+    const std::vector<DObj> tobjs = trav_view(objs_dev), tlights = trav_view(lights_dev);
     chk(upload(*c, objs_dev.data(), objs_dev.size(), &s.objs));
     chk(upload(*c, lights_dev.data(), lights_dev.size(), &s.lights));
+    chk(upload(*c, tobjs.data(), tobjs.size(), &s.tobjs));
+    chk(upload(*c, tlights.data(), tlights.size(), &s.tlights));
     chk(upload(*c, tv.data(), tv.size(), &s.tv));
     chk(upload(*c, kdp.data(), kdp.size(), &s.kdp));
     if (st) {
@@ -1875,6 +1945,8 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         s.off_tris = put(d->triangles, sizeof(lumo_triangle) * d->num_triangles);
         s.off_tv = put(tv.data(), sizeof(double) * tv.size());
         s.off_xforms = put(d->transforms, sizeof(lumo_transform) * d->num_transforms);
+        s.off_tobjs = put(tobjs.data(), sizeof(DObj) * tobjs.size());
+        s.off_tlights = put(tlights.data(), sizeof(DObj) * tlights.size());
         s.hot_bytes = 0;
         if (hot.size() <= 48 * 1024) {
             const char* dp = nullptr;
@@ -1885,6 +1957,43 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
             }
             s.hot = dp;
             s.hot_bytes = (uint32_t)hot.size();
+        }
+    }
+    {   // TOP set for larger scenes (DScene::top): the object items and traversal records, the
+        // objects BVH and as much of the lights BVH as fits, both breadth-first prefixes
+        s.top = nullptr;
+        s.top_bytes = 0;
+        s.top_onodes = s.top_lnodes = 0;
+        s.onodes_lds = s.lnodes_lds = nullptr;
+        s.n_onodes_lds = s.n_lnodes_lds = 0;
+        const size_t budget = (size_t)c->top_lds_bytes;
+        const size_t objs_b = ((sizeof(int32_t) * d->num_object_items + 15) & ~(size_t)15) + sizeof(DObj) * tobjs.size();
+        if (s.hot_bytes == 0 && budget >= 4096 && objs_b + 64 * sizeof(DBvh) <= budget) {
+            std::vector<char> top;
+            auto put = [&](const void* p, size_t bytes) -> uint32_t {
+                const size_t off = (top.size() + 15) & ~(size_t)15;
+                top.resize(off + ((bytes + 15) & ~(size_t)15), 0);
+                if (bytes) std::memcpy(top.data() + off, p, bytes);
+                return (uint32_t)off;
+            };
+            s.off_top_oitems = put(d->object_items, sizeof(int32_t) * d->num_object_items);
+            s.off_top_tobjs = put(tobjs.data(), sizeof(DObj) * tobjs.size());
+            size_t left = budget - top.size();
+            const size_t no = std::min(obvh.size(), left / sizeof(DBvh));
+            s.off_top_onodes = put(obvh.data(), sizeof(DBvh) * no);
+            left = budget - top.size();
+            const size_t nl = std::min(lbvh.size(), left / sizeof(DBvh));
+            s.off_top_lnodes = put(lbvh.data(), sizeof(DBvh) * nl);
+            s.top_onodes = (int32_t)no;
+            s.top_lnodes = (int32_t)nl;
+            const char* dp = nullptr;
+            chk(upload(*c, top.data(), top.size(), &dp));
+            if (st) {
+                free_scene(*c);
+                return st;
+            }
+            s.top = dp;
+            s.top_bytes = (uint32_t)top.size();
         }
     }
     int n = d->num_lights, lg = 0;
@@ -2073,8 +2182,10 @@ lumo_status lumo_trace(void* ctx, const lumo_ray_soa* rays, size_t n, lumo_hit_s
     HIPCHK(hipMemcpyAsync(d, rays->dir, sizeof(double) * 3 * n, hipMemcpyHostToDevice, sm));
     if (any_hit) HIPCHK(hipMemcpyAsync(light, rays->light, sizeof(int32_t) * n, hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemsetAsync(tc, 0, sizeof(unsigned long long) * (TC_ALL + TC_STATS), sm));
+    const bool top = g_top && c->sc.top_bytes > 0 && !(g_lds && c->sc.hot_bytes > 0);
+    const int grid = top ? std::min(ceil_div(n, TOP_BLOCK), c->top_grid_cap) : ceil_div(n, BLOCK);
     by_stack_class(c->sc.stack_class, [&](auto K) {
-        launch_trace<decltype(K)::value>(ceil_div(n, BLOCK), sm, c->sc, o, d, light, (int)n, any_hit, t, kind, obj, prim, tc);
+        launch_trace<decltype(K)::value>(grid, sm, c->sc, o, d, light, (int)n, any_hit, t, kind, obj, prim, tc, top);
     });
     HIPCHK(hipGetLastError());
     if (hits->t) HIPCHK(hipMemcpyAsync(hits->t, t, sizeof(double) * n, hipMemcpyDeviceToHost, sm));
@@ -2100,6 +2211,10 @@ lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info) {
     info->lds_bytes = g_lds ? (int32_t)c->sc.hot_bytes : 0;
     info->full_kernels = c->sc.full;
     info->n_shadow = c->sc.n_shadow;
+    const bool top = g_top && c->sc.top_bytes > 0 && !(g_lds && c->sc.hot_bytes > 0);
+    info->top_bytes = top ? (int32_t)c->sc.top_bytes : 0;
+    info->top_object_nodes = c->sc.top_onodes;
+    info->top_light_nodes = c->sc.top_lnodes;
     return LUMO_OK;
 }
 

@@ -19,6 +19,9 @@ struct TravLaunch {
     bool lds;
     int fx;  // feature class (dscene.h): 0 lean, 1 full, 2 full + textures
     hipStream_t sm;
+    // TOP staging (k_closest_q / k_shadow_q of scenes too large for `lds`): TOP_BLOCK threads per
+    // block, `shm` bytes of LDS (DScene::top_bytes), grid `grid`
+    bool top = false;
 };
 
 template <int STK>
@@ -33,7 +36,7 @@ void launch_bounce_q(const TravLaunch& l, const DScene& sc, const Paths& S, cons
 template <int STK>
 void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, const double* d, const int32_t* light,
                   int n, int any_hit, double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
-                  unsigned long long* tcount);
+                  unsigned long long* tcount, bool top);
 
 template <int STK>
 void launch_bdpt_step(int grid, hipStream_t sm, int fx, const DScene& sc, const Paths& S, const Tasks& T,
@@ -57,7 +60,7 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
                                             const QState&, const QState&, uint32_t, bool, int, int);              \
     extern template void launch_trace<K>(int, hipStream_t, const DScene&, const double*, const double*,          \
                                          const int32_t*, int, int, double*, int32_t*, int32_t*, int32_t*,         \
-                                         unsigned long long*);                                                    \
+                                         unsigned long long*, bool);                                              \
     extern template void launch_bdpt_step<K>(int, hipStream_t, int, const DScene&, const Paths&, const Tasks&,   \
                                              const Bdpt&, const BItems&, int, const int32_t*, int32_t*);          \
     extern template void launch_bdpt_redo<K>(const TravLaunch&, const DScene&, const Paths&, const Tasks&,        \

@@ -50,22 +50,25 @@ __device__ __forceinline__ void qc(const QState& Q, int k, size_t q, const DColo
     for (int i = 0; i < NS; ++i) Q.D(k + i, q) = c.s[i];
 }
 
-// Scene::hit (scene.rs:119-147) of every queued ray.
-template <int STK, bool LDS, int FX>
-__global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest_q(DScene sc0, Paths S, QState cur,
-                                                                         uint32_t skip_below) {
+// Scene::hit (scene.rs:119-147) of every queued ray.  LDS: 0 scene in HBM, 1 whole scene staged
+// in LDS (small scenes), 2 TOP staging (the BVHs' top levels and the object records in LDS,
+// TOP_BLOCK threads per block: one block fills a CU).
+template <int STK, int LDS, int FX>
+__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_CLOSEST_WAVES) void k_closest_q(DScene sc0, Paths S,
+                                                                                               QState cur,
+                                                                                               uint32_t skip_below) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
     if (count < skip_below) return;                // k_bounce_q<TAIL> ran this bounce's paths to their end
     if (count <= blockIdx.x * blockDim.x) return;  // before staging: whole block idle
-    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    const DScene sc = LDS == 1 ? stage_scene_lds(sc0, lds_scene) : (LDS == 2 ? stage_top_lds(sc0, lds_scene) : sc0);
     const HitQ hq = S.hq;
     Counters C{0, 0, 0};
     for (uint32_t w0 = wave_fetch(S.counts + CNT_FETCH_C); w0 < count; w0 = wave_fetch(S.counts + CNT_FETCH_C)) {
         const uint32_t q = w0 + lane_id();
         if (q >= count) continue;
         const RayX r = rayx(Ray{qv3(cur, QD_O, q), qv3(cur, QD_D, q)});
-        const HitRef h = scene_hit<STK, FX>(sc, r, C);
+        const HitRef h = scene_hit<STK, FX, LDS == 2>(sc, r, C);
         hq.t[q] = h.t;
         hq.i[q] = h.kind;
         hq.i[hq.cap + q] = h.obj;
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
 // Scene::hit_light + mis_sample of one NEE record (integrator.rs:100-184); plane base b.  The
 // path's wavelengths (header p) are read only after a visible hit, so they are not live across
 // the traversal.
-template <int STK, int FX>
+template <int STK, int FX, bool TOP = false>
 __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const ShadowQ& Q, int b, size_t r, bool li_mode,
                                                   uint32_t p, Counters& C, bool* visible = nullptr) {
 #if LUMO_SKIP_DEAD
@@ -283,7 +286,7 @@ __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const Shadow
     const int li = Q.I(SI_LIGHT, r);
     DHit hi;
     DColor out = cfill(0.0);
-    if (scene_hit_light<STK, FX>(sc, ri, li, hi, C)) {
+    if (scene_hit_light<STK, FX, TOP>(sc, ri, li, hi, C)) {
         if (visible) *visible = true;
         const lumo_object& Lo = sc.lights[li];
         const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
@@ -321,15 +324,16 @@ __device__ __forceinline__ void deliver_nee(const Paths& S, const ShadowQ& Q, co
 // the path's NEE term; otherwise it stores single_i over the pair's (consumed) L-record bsdf_f
 // planes and k_nee_fold adds the path's singles in i order.  No block barrier: a wave that
 // finishes its traversals early moves on to its next pairs.
-template <int STK, bool LDS, int FX, bool NS1>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc0, Paths S, QState nxt) {
+template <int STK, int LDS, int FX, bool NS1>
+__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc0, Paths S,
+                                                                                              QState nxt) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const int ns = NS1 ? 1 : sc0.n_shadow;
     uint32_t count = 0;  // pairs over all buckets
     for (int b = 0; b < NB; ++b) count += S.counts[CNT_BUCKET0 + b];
     count *= (uint32_t)ns;
     if (count <= blockIdx.x * blockDim.x) return;
-    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    const DScene sc = LDS == 1 ? stage_scene_lds(sc0, lds_scene) : (LDS == 2 ? stage_top_lds(sc0, lds_scene) : sc0);
     const ShadowQ Q = S.sq;
     Counters C{0, 0, 0};
     // static stride: with 11 pairs per path, one fetch atomic per wave (~350 k per C3 bounce on one
@@ -355,7 +359,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc
             if (rec == 1 && !Q.I(SI_BVALID, r)) break;
             const uint32_t c0 = C.aabb + C.kd + C.tri, a0 = C.aabb;
             bool vis = false;
-            const DColor x = shadow_record_q<STK, FX>(sc, Q, rec ? SD_BO : SD_LO, r, rec == 0, p, C, &vis);
+            const DColor x = shadow_record_q<STK, FX, LDS == 2>(sc, Q, rec ? SD_BO : SD_LO, r, rec == 0, p, C, &vis);
             if (rec) b = x; else a = x;
             const uint32_t cost = C.aabb + C.kd + C.tri - c0;
             pc += cost;
@@ -380,8 +384,8 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc
             }
         }
 #else
-        const DColor a = shadow_record_q<STK, FX>(sc, Q, SD_LO, r, true, p, C);
-        const DColor b = Q.I(SI_BVALID, r) ? shadow_record_q<STK, FX>(sc, Q, SD_BO, r, false, p, C) : cfill(0.0);
+        const DColor a = shadow_record_q<STK, FX, LDS == 2>(sc, Q, SD_LO, r, true, p, C);
+        const DColor b = Q.I(SI_BVALID, r) ? shadow_record_q<STK, FX, LDS == 2>(sc, Q, SD_BO, r, false, p, C) : cfill(0.0);
 #endif
         const DColor single = (cfill(0.0) + a + b) / Q.D(SD_PDFL, r);
         if (NS1) {
@@ -809,16 +813,21 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
 }
 
 // ------------------------------------------------------------------ traversal-only entry (lumo_trace)
-template <int STK>
-__global__ void k_trace(DScene sc, const double* o, const double* d, const int32_t* light, int n, int any_hit,
-                        double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
-                        unsigned long long* tcount) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// TOP: the scene's TOP set staged in LDS (as k_closest_q / k_shadow_q of large scenes), so the
+// traversal-only entry checks that walk too; grid-stride over the rays.
+template <int STK, bool TOP>
+__global__ __launch_bounds__(TOP ? TOP_BLOCK : BLOCK) void k_trace(DScene sc0, const double* o, const double* d,
+                                                                 const int32_t* light, int n, int any_hit,
+                                                                 double* t_out, int32_t* kind_out, int32_t* obj_out,
+                                                                 int32_t* prim_out, unsigned long long* tcount) {
+    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+    if (n <= (int)(blockIdx.x * blockDim.x)) return;
+    const DScene sc = TOP ? stage_top_lds(sc0, lds_scene) : sc0;
     Counters C{0, 0, 0};
-    if (i < n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const RayX r = rayx(Ray{ldv3(o, i), ldv3(d, i)});
         if (!any_hit) {
-            const HitRef h = scene_hit<STK, true>(sc, r, C);
+            const HitRef h = scene_hit<STK, true, TOP>(sc, r, C);
             t_out[i] = h.t;
             kind_out[i] = h.kind;
             obj_out[i] = h.obj;
@@ -826,7 +835,7 @@ __global__ void k_trace(DScene sc, const double* o, const double* d, const int32
         } else {
             DHit lh;
             const int li = light[i];
-            const bool vis = scene_hit_light<STK, true>(sc, r, li, lh, C);
+            const bool vis = scene_hit_light<STK, true, TOP>(sc, r, li, lh, C);
             t_out[i] = vis ? lh.t : DINF;
             kind_out[i] = vis ? 2 : 0;
             obj_out[i] = vis ? li : -1;

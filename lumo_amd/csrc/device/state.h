@@ -15,6 +15,9 @@ namespace dev {
 
 constexpr int BLOCK = 256;
 // Minimum waves per SIMD (register budget) per kernel, tuned by A/B on MI355X.
+// Threads per block of the TOP-staged traversal kernels (dscene.h stage_top_lds): one block holds
+// the LDS of a CU, so it must bring the CU's whole wave budget (16 waves at 4 per SIMD).
+constexpr int TOP_BLOCK = 1024;
 #ifndef LUMO_CLOSEST_WAVES
 #define LUMO_CLOSEST_WAVES 4
 #endif

@@ -220,3 +220,68 @@ def test_bounce_modes_small_dragon(dev, fused, tail, pipe):
             assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
     finally:
         lib.lumo_set_bounce_mode(-1, 1 << 18, 3)
+
+
+# ---------------------------------------------------------------------------- TOP staging
+@pytest.fixture(scope="module")
+def mid_bistro():
+    from lumo_amd.procedural import bistro_standin
+    return scenes.bistro(bistro_standin(groups=48, lamps=160, n=8)).build()
+
+
+def test_top_staging_selected_for_large_scenes(dev, c3):
+    """A scene too large to stage whole (C3) runs its closest-hit and visibility walks with the
+    TOP set in LDS: the whole objects BVH, the object records and the top of the lights BVH."""
+    dev.upload(c3)
+    info = dev.scene_info()
+    d = c3.desc()
+    assert info.lds_bytes == 0
+    assert 0 < info.top_bytes <= 160 * 1024
+    assert info.top_object_nodes == d.num_object_nodes
+    assert 0 < info.top_light_nodes < d.num_light_nodes
+
+
+@pytest.mark.parametrize("budget_kb,top", [(0, 0), (8, 1), (20, 1), (None, 1)])
+def test_top_staging_budgets(mid_bistro, budget_kb, top):
+    """The TOP walk reads node i from LDS when i is below the staged prefix of its BVH and from
+    HBM otherwise: with the staged prefix cutting the objects BVH (8 KiB), the lights BVH
+    (20 KiB), neither (default) or TOP off, lumo_trace (t / kind / object and the traversal
+    counters) and rendered tiles equal the oracle's."""
+    env = {"LUMO_TOP": str(top)}
+    if budget_kb is not None:
+        env["LUMO_TOP_KB"] = str(budget_kb)
+    saved = {k: os.environ.get(k) for k in ("LUMO_TOP", "LUMO_TOP_KB")}
+    os.environ.update(env)
+    try:
+        d = L.Device(0)  # the budget is read when a context is created
+        sc = mid_bistro
+        d.upload(sc)
+        info = d.scene_info()
+        desc = sc.desc()
+        if top == 0:
+            assert info.top_bytes == 0
+        elif budget_kb == 8:
+            assert 0 < info.top_object_nodes < desc.num_object_nodes and info.top_light_nodes == 0
+        elif budget_kb == 20:
+            assert info.top_object_nodes == desc.num_object_nodes and 0 < info.top_light_nodes < desc.num_light_nodes
+        else:
+            assert info.top_object_nodes == desc.num_object_nodes and info.top_light_nodes == desc.num_light_nodes
+        o, dd = _closest_rays(desc, (-16.0, 5.0, -1.0), 1 << 17, 21)
+        _trace_cmp(d, sc, o, dd)
+        o, dd, li = _visibility_rays(desc, 1 << 17, 22)
+        _trace_cmp(d, sc, o, dd, lights=li)
+        cam = scenes.bistro_camera((96, 64))
+        d.upload(sc, cam)
+        tasks = L.make_tasks(96, 64, 4, SEED)[8:14]
+        bufs, res = d.render_tasks(tasks)
+        obufs, ores, _ = O.render_tasks(desc, cam.desc, tasks, O.WAVEFRONT, 8)
+        for b, ob, r, orr in zip(bufs, obufs, res, ores):
+            np.testing.assert_array_equal(b, ob)
+            assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+        d.close()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
