@@ -78,6 +78,9 @@ def main():
     ap.add_argument("--max-vertices", type=int, default=0, help="BDPT vertex storage per subpath (0 = 128)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU work per baseline run")
+    ap.add_argument("--share", default=None,
+                    help="R/N: render only rank R's share of an N-rank run (tile %% N == R) in this single "
+                         "process, to time one rank's load of a multi-GPU run on one GPU")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -126,7 +129,12 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
     bdpt = wl.get("integrator") == L.Integrator.BDPathTrace
     tasks = L.make_tasks(W, H, spp, SEED)
     tiles = tiles_per_batch(W, H)
-    mine = shard_tasks(tasks, W, H, rank, ws)
+    share = getattr(args, "share", None) if config == args.config else None
+    if share:
+        sr, sn = (int(x) for x in share.split("/"))
+        mine = shard_tasks(tasks, W, H, sr, sn)
+    else:
+        mine = shard_tasks(tasks, W, H, rank, ws)
     mine_arr = (_ffi.TileTask * len(mine))(*mine)
     warm_arr = mine_arr
     if warm_spp is not None:
@@ -234,6 +242,8 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
         }
         if warm_spp is not None:
             out["warmup_spp"] = warm_spp
+        if share:
+            out["share"] = share  # one rank's load of an N-rank run, timed on this one GPU
     del scene
     return out
 

@@ -640,7 +640,9 @@ struct Ctx {
     lumo_stats stats{};
     hipEvent_t ev[2 * ST_COUNT];
     int lds_grid_cap = 2048;
-    int top_grid_cap = 1024;  // TOP-staged traversal kernels: blocks of TOP_BLOCK threads (LUMO_TOP_GRID)
+    // TOP-staged traversal kernels: blocks of TOP_BLOCK threads, one per CU (each holds a CU's LDS;
+    // C3 shadow 438 ms per 8-spp frame at one block per CU vs 446 at four, 817 at half the CUs)
+    int top_grid_cap = 256;  // set to the device's CU count at creation (LUMO_TOP_GRID)
     int top_lds_bytes = 160 * 1024 - 256;  // TOP set budget (LUMO_TOP_KB)
     int tone_map = LUMO_TONEMAP_NONE;  // of the lumo_render_tiles call in progress
     double tone_arg = 0.0;
@@ -1605,6 +1607,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
     Ctx* c = new (std::nothrow) Ctx();
     if (!c) return LUMO_ERR_OOM;
     c->device = device;
+    c->top_grid_cap = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return LUMO_ERR_HIP;

@@ -1,16 +1,23 @@
 #!/bin/bash
-# A/B of device-code variants on the GPU box (repo root): for each "name[:ENV=val]" argument run
-# C1 (1024^2 @ 64 spp, 4 frames) and C3 (1920x1080 @ 8 spp) with lumo_amd/var/liblumo_amd_<name>.so
-# (name "base": the in-tree library; "r01": the round-1 tree copied to ab_r01/).  Results: gpurun_out/ab/<name>_<cfg>.json.
+# A/B of device-code variants on the GPU box (repo root): for each "name[:ENV=val,ENV2=val]" argument
+# run C1 (1024^2 @ 64 spp, 4 frames), C2 (4 spp), C3 (1920x1080 @ 8 spp) and / or C4 (8 spp) with
+# lumo_amd/var/liblumo_amd_<name>.so (name "base": the in-tree library).  AB_CONFIGS picks the
+# configs (default "c1 c3").  Each run has its own time limit; results: gpurun_out/ab/<tag>_<cfg>.json.
 set -eo pipefail
 mkdir -p gpurun_out/ab
+CFGS=${AB_CONFIGS:-c1 c3}
 for v in "$@"; do
   name=${v%%:*}; envs=""; [ "$name" != "$v" ] && envs=${v#*:}
   lib=lumo_amd/var/liblumo_amd_${name}.so; [ "$name" = "base" ] && lib=lumo_amd/liblumo_amd.so
   tag=$(echo "$v" | tr ':=,' '___')
-  bench="bench.py"; extra="--bistro-frames 0"
-  if [ "$name" = "r01" ]; then bench="ab_r01/bench.py"; extra=""; lib=ab_r01/lumo_amd/liblumo_amd.so; fi  # round-1 tree
-  env $(echo $envs | tr ',' ' ') LUMO_AMD_LIB=$lib timeout -k 10 300 python3 $bench --res 1024 --spp 64 --steps 4 --warmup 1 $extra --cpu-baseline 0 > gpurun_out/ab/${tag}_c1.json
-  env $(echo $envs | tr ',' ' ') LUMO_AMD_LIB=$lib timeout -k 10 300 python3 $bench --config c3 --spp 8 --steps 1 --warmup 1 --cpu-baseline 0 > gpurun_out/ab/${tag}_c3.json
+  for cfg in $CFGS; do
+    case $cfg in
+      c1) args="--res 1024 --spp 64 --steps 4 --warmup 1 --bistro-frames 0 --cpu-baseline 0" ;;
+      c2) args="--config c2 --spp 4 --steps 1 --warmup 1 --cpu-baseline 0" ;;
+      c4) args="--config c4 --spp 8 --steps 1 --warmup 1 --cpu-baseline 0" ;;
+      *) args="--config c3 --spp 8 --steps 1 --warmup 1 --cpu-baseline 0" ;;
+    esac
+    env $(echo $envs | tr ',' ' ') LUMO_AMD_LIB=$lib timeout -k 10 300 python3 bench.py $args > gpurun_out/ab/${tag}_${cfg}.json
+    python3 -c "import json,sys; d=json.load(open('gpurun_out/ab/${tag}_${cfg}.json')); st=d['roofline']['stages']; print('$tag $cfg', d['ms_per_step'], 'ms', {k: v['ms'] for k, v in st.items() if v['ms'] > 0})"
+  done
 done
-python3 tools/ab_report.py
