@@ -395,7 +395,9 @@ void lumo_set_lds_staging(int on);
  * that launch (tail_below = 0: never; default 262144).  pipeline (with fused bounces): 1 each
  * pass runs its first bounces on a head stream and hands the rest (tail kernel, film, ring) to a
  * second stream while the next pass starts; 2 or 3 (default 3) rotate that many head streams so
- * consecutive passes' first bounces also overlap; 0 off.  Every mode gives bit-identical results.
+ * consecutive passes' first bounces also overlap; 0 off (also for the split schedule, which
+ * otherwise keeps up to LUMO_SPLIT_PIPE = 4 passes in flight on four streams when HBM allows).
+ * Every mode gives bit-identical results.
  * Also LUMO_FUSED / LUMO_TAIL / LUMO_PIPELINE in the environment. */
 void lumo_set_bounce_mode(int fused, uint32_t tail_below, int pipeline);
 

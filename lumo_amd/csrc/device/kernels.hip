@@ -658,6 +658,7 @@ struct Ctx {
     int debug_integrator = LUMO_INTEGRATOR_PATH_TRACE;  // lumo_debug_paths
     int sampler = LUMO_SAMPLER_MULTI_JITTERED;          // of the lumo_render_tiles call in progress
     int debug_sampler = LUMO_SAMPLER_MULTI_JITTERED;    // lumo_debug_paths
+    size_t split_sets_bytes = 0;  // work buffers already held by the extra pass sets (free-memory check)
     // Launch intervals of the timed stages (ms from ref_ev, recorded before the first timed launch
     // after a stats reset): their union is a stage's busy time, which does not count twice the
     // time that launches on different streams overlap (lumo_stats_busy_ms)
@@ -712,7 +713,9 @@ enum WorkId {
     W_SQ_HD, W_SQ_HI, W_SQ_HR, W_RAD2, W_LAM2, W_RASTER2, W_DEPTH2, W_QUERIES2, W_P_VALID2, W_COUNTS2, W_QS2_D,
     W_QS2_R, W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I, W_RAD3, W_LAM3, W_RASTER3, W_DEPTH3, W_QUERIES3, W_P_VALID3,
     W_COUNTS3, W_QS4_D, W_QS4_R, W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I, W_RAD4, W_LAM4, W_RASTER4, W_DEPTH4,
-    W_QUERIES4, W_P_VALID4, W_COUNTS4, W_QS6_D, W_QS6_R, W_QS6_I, W_QS7_D, W_QS7_R, W_QS7_I, W_COUNT
+    W_QUERIES4, W_P_VALID4, W_COUNTS4, W_QS6_D, W_QS6_R, W_QS6_I, W_QS7_D, W_QS7_R, W_QS7_I,
+    W_SPLIT_SET1,  // render_split_pipelined sets 1..3: hits + NEE records, 7 buffers each
+    W_COUNT = W_SPLIT_SET1 + 3 * 7
 };
 
 template <typename T>
@@ -846,6 +849,7 @@ int g_pipeline = 3;                // fused passes overlapped (render_pipelined)
 int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from a counter
 int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
 int g_heads = 0;                   // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
+int g_split_pipe = 4;              // split schedule: passes in flight (render_split_pipelined; 1 = sequential)
 int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
 // allow_top: the kernel has a TOP-staged variant (k_closest_q, k_shadow_q); it is used when the
 // whole scene does not fit in LDS but its top levels were packed at upload (DScene::top).
@@ -863,6 +867,48 @@ void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr, bo
         l.shm = c.sc.top_bytes;
     }
     by_stack_class(c.sc.stack_class, [&](auto K) { f(K, l); });
+}
+
+// Per-pass copies of the per-slot outputs, queue counters and queue-order state for the pipelined
+// schedules (pass set k = 1..3; set 0 is the render's own Paths).
+const int kSetWork[3][13] = {{W_RAD2, W_LAM2, W_RASTER2, W_DEPTH2, W_QUERIES2, W_P_VALID2, W_COUNTS2, W_QS2_D, W_QS2_R,
+                              W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I},
+                             {W_RAD3, W_LAM3, W_RASTER3, W_DEPTH3, W_QUERIES3, W_P_VALID3, W_COUNTS3, W_QS4_D, W_QS4_R,
+                              W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I},
+                             {W_RAD4, W_LAM4, W_RASTER4, W_DEPTH4, W_QUERIES4, W_P_VALID4, W_COUNTS4, W_QS6_D, W_QS6_R,
+                              W_QS6_I, W_QS7_D, W_QS7_R, W_QS7_I}};
+void alloc_pass_set(Ctx& c, Paths& Q, int k, int N, lumo_status& st) {
+    const int* w = kSetWork[k - 1];
+    Q.rad = wbuf<double>(c, w[0], 4 * (size_t)N, st);
+    Q.lam = wbuf<double>(c, w[1], 4 * (size_t)N, st);
+    Q.raster = wbuf<double>(c, w[2], 2 * (size_t)N, st);
+    Q.depth = wbuf<uint32_t>(c, w[3], N, st);
+    Q.queries = wbuf<uint32_t>(c, w[4], N, st);
+    Q.p_valid = wbuf<uint32_t>(c, w[5], N, st);
+    Q.counts = wbuf<uint32_t>(c, w[6], CNT_N, st);
+    for (int h = 0; h < 2; ++h) {
+        Q.qs[h].cap = (size_t)N;
+        Q.qs[h].d = wbuf<double>(c, w[7 + 3 * h], QD_N * (size_t)N, st);
+        Q.qs[h].r = wbuf<uint64_t>(c, w[8 + 3 * h], 2 * (size_t)N, st);
+        Q.qs[h].i = wbuf<int32_t>(c, w[9 + 3 * h], QI_N * (size_t)N, st);
+    }
+}
+// ... and, for the split schedule, the set's closest hits and NEE records (the sizes of set 0's)
+void alloc_split_set(Ctx& c, Paths& Q, const Paths& S, int k, int ns, lumo_status& st) {
+    const int w = W_SPLIT_SET1 + 7 * (k - 1);
+    Q.hq.t = wbuf<double>(c, w + 0, S.hq.cap, st);
+    Q.hq.i = wbuf<int32_t>(c, w + 1, 3 * S.hq.cap, st);
+    Q.sq.d = wbuf<double>(c, w + 2, SD_N * S.sq.cap, st);
+    Q.sq.i = wbuf<int32_t>(c, w + 3, SI_N * S.sq.cap, st);
+    Q.sq.hd = wbuf<double>(c, w + 4, (ns > 1 ? SH_N : SH_N1) * S.sq.hcap, st);
+    Q.sq.hi = wbuf<int32_t>(c, w + 5, SHI_N * S.sq.hcap, st);
+    Q.sq.hr = ns > 1 ? wbuf<uint64_t>(c, w + 6, 2 * S.sq.hcap, st) : nullptr;
+}
+// Device bytes of one extra pass set of the split schedule.
+size_t split_set_bytes(const Paths& S, int N, int ns) {
+    return (size_t)N * (4 + 4 + 2) * 8 + (size_t)N * 3 * 4 + 2 * (size_t)N * (QD_N * 8 + 16 + QI_N * 4) +
+           S.hq.cap * (8 + 12) + S.sq.cap * (SD_N * 8 + SI_N * 4) +
+           S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4 + (ns > 1 ? 16 : 0));
 }
 
 // Pipelined passes (n_shadow == 1, fused bounces).  Russian roulette reads the pass's adaptive
@@ -893,29 +939,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         }
     } join{c};
     Paths P3[4] = {S, S, S, S};
-    const int wid[3][16] = {{W_RAD2, W_LAM2, W_RASTER2, W_DEPTH2, W_QUERIES2, W_P_VALID2, W_COUNTS2, W_QS2_D, W_QS2_R,
-                             W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I},
-                            {W_RAD3, W_LAM3, W_RASTER3, W_DEPTH3, W_QUERIES3, W_P_VALID3, W_COUNTS3, W_QS4_D, W_QS4_R,
-                             W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I},
-                            {W_RAD4, W_LAM4, W_RASTER4, W_DEPTH4, W_QUERIES4, W_P_VALID4, W_COUNTS4, W_QS6_D, W_QS6_R,
-                             W_QS6_I, W_QS7_D, W_QS7_R, W_QS7_I}};
-    for (int k = 1; k < NSETS; ++k) {
-        const int* w = wid[k - 1];
-        Paths& Q = P3[k];
-        Q.rad = wbuf<double>(c, w[0], 4 * (size_t)N, st);
-        Q.lam = wbuf<double>(c, w[1], 4 * (size_t)N, st);
-        Q.raster = wbuf<double>(c, w[2], 2 * (size_t)N, st);
-        Q.depth = wbuf<uint32_t>(c, w[3], N, st);
-        Q.queries = wbuf<uint32_t>(c, w[4], N, st);
-        Q.p_valid = wbuf<uint32_t>(c, w[5], N, st);
-        Q.counts = wbuf<uint32_t>(c, w[6], CNT_N, st);
-        for (int h = 0; h < 2; ++h) {
-            Q.qs[h].cap = (size_t)N;
-            Q.qs[h].d = wbuf<double>(c, w[7 + 3 * h], QD_N * (size_t)N, st);
-            Q.qs[h].r = wbuf<uint64_t>(c, w[8 + 3 * h], 2 * (size_t)N, st);
-            Q.qs[h].i = wbuf<int32_t>(c, w[9 + 3 * h], QI_N * (size_t)N, st);
-        }
-    }
+    for (int k = 1; k < NSETS; ++k) alloc_pass_set(c, P3[k], k, N, st);
     if (st) return st;
     hipStream_t As[3] = {c.stream, c.stream3, c.stream4}, B = c.stream2;
     // every event starts "done" after the setup enqueued on stream 0 (tasks, memsets, the initial
@@ -998,6 +1022,240 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
     }
     // the results are copied on stream 0: after the last pass's ring
     HIPCHK(hipStreamWaitEvent(As[0], c.pass_ev[(max_samples - 1) % NSETS], 0));
+    join.ok = true;
+    return LUMO_OK;
+}
+
+// One path-tracing bounce of the split (not fused-LDS) schedule on stream `sm`: the tail kernel when
+// few paths are alive (n_shadow == 1), then the fused bounce (fused_now) or closest hit -> shading
+// (+ NEE pair generation when n_shadow > 1) -> visibility (+ the NEE fold).  `ub` is an upper bound
+// on the live count (grids); the kernels read the exact count from S.counts.
+void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, const QState& nxt, uint32_t ub,
+                        hipStream_t sm, bool fused_now) {
+    const int ns = c.sc.n_shadow;
+    // n_shadow == 1: the tail kernel takes the bounce when fewer than g_tail_below paths
+    // are alive (decided on the device from the exact count); the bounce kernels skip it
+    // (launched only once the last count the host has seen is below 4x the threshold:
+    // before that the bounce kernels get threshold 0 and take every path)
+    const uint32_t skip = (ns == 1 && (uint64_t)ub < 4ull * g_tail_below) ? g_tail_below : 0u;
+    if (skip > 0) {
+        StageTimer tm(c, g_timing, ST_RESOLVE, sm);
+        launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
+            launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true, 0, BLOCK);
+        }, sm);
+    }
+    if (fused_now) {  // one fused kernel per bounce (pt.h k_bounce_q)
+        StageTimer tm(c, g_timing, ST_CLOSEST, sm);
+        launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
+            launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, false, g_dyn, g_bounce_threads);
+        }, sm);
+        return;
+    }
+    {
+        StageTimer tm(c, g_timing, ST_CLOSEST, sm);
+        launch_trav(
+            c, ub, [&](auto K, const TravLaunch& l) { launch_closest_q<decltype(K)::value>(l, c.sc, S, cur, skip); },
+            sm, true);
+    }
+    {
+        StageTimer tm(c, g_timing, ST_SHADE, sm);
+        const int g = ceil_div(ub, BLOCK);
+        if (ns > 1) {  // NEE pairs by k_nee_gen, one thread per pair
+            const int gp = std::min(ceil_div((uint64_t)ub * (uint32_t)ns, BLOCK), 1 << 16);
+            if (c.sc.full == 2) {
+                k_shade_q<2, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+                k_nee_gen<2><<<gp, BLOCK, 0, sm>>>(c.sc, S);
+            } else if (c.sc.full) {
+                k_shade_q<1, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+                k_nee_gen<1><<<gp, BLOCK, 0, sm>>>(c.sc, S);
+            } else {
+                k_shade_q<0, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+                k_nee_gen<0><<<gp, BLOCK, 0, sm>>>(c.sc, S);
+            }
+        } else if (c.sc.full == 2) {
+            k_shade_q<2, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+        } else if (c.sc.full) {
+            k_shade_q<1, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+        } else {
+            k_shade_q<0, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+        }
+    }
+    {
+        StageTimer tm(c, g_timing, ST_SHADOW, sm);
+        launch_trav(
+            c, (uint64_t)ub * (uint32_t)ns,
+            [&](auto K, const TravLaunch& l) { launch_shadow_q<decltype(K)::value>(l, c.sc, S, nxt); }, sm,
+            true);
+    }
+    if (ns > 1) {
+        StageTimer tm(c, g_timing, ST_RESOLVE, sm);
+        k_nee_fold<<<std::min(ceil_div(ub, BLOCK), 1 << 14), BLOCK, 0, sm>>>(S, nxt, ns);
+    }
+}
+
+// Pipelined passes of the split schedule (closest hit / shading / visibility kernels: scenes too
+// large for the fused LDS kernel, n_shadow > 1).  A pass whose queue has shrunk to a few thousand
+// paths runs latency-bound launches (one long walk sets a kernel's duration: C3 at one rank's 1/8
+// share spent ~0.4 ms per closest / visibility launch for every bounce past the fifth), so K
+// passes run at once, pass p on stream p % K with pass set p % K (queues, counters, hits, NEE
+// records, per-slot outputs).  Russian roulette reads the pass's delta only from depth RR_DEPTH on
+// (path_trace.rs:60-69) and the sampler state is per slot, so pass p waits for pass p - 1's
+// camera before its own and for pass p - 1's ring before its bounce RR_DEPTH and its film; set
+// reuse (pass p + K) is ordered by its stream.  The host runs every in-flight pass's bounce loop
+// (count snapshots `ahead` launches back, as the sequential loop) and blocks only on the oldest
+// pass, which never waits for a younger one; a younger pass issues bounce RR_DEPTH and its film
+// only once the pass before it has issued its ring, so every wait is enqueued after the record it
+// waits for.  Every per-path operation and every film / ring sum is the sequential loop's:
+// bit-identical.
+lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int n_tasks, int dim_stride,
+                                   uint64_t max_samples, uint64_t max_P, bool fused_now, int K, uint64_t& bounces,
+                                   lumo_status& st) {
+    struct JoinOnError {
+        Ctx& c;
+        bool ok = false;
+        ~JoinOnError() {
+            if (ok) return;
+            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream})
+                if (s) (void)hipStreamSynchronize(s);
+        }
+    } join{c};
+    const int ns = c.sc.n_shadow;
+    Paths P[4] = {S, S, S, S};
+    for (int k = 1; k < K; ++k) {
+        alloc_pass_set(c, P[k], k, N, st);
+        alloc_split_set(c, P[k], S, k, ns, st);
+    }
+    if (st) return st;
+    hipStream_t Ss[4] = {c.stream, c.stream2, c.stream3, c.stream4};
+    {
+        ZeroList z;
+        for (int k = 1; k < K; ++k) z.add(P[k].counts, sizeof(uint32_t) * CNT_N);
+        if (z.n) k_zero_list<<<1, BLOCK, 0, Ss[0]>>>(z);
+    }
+    for (int k = 0; k < 4; ++k) HIPCHK(hipEventRecord(c.pass_ev[k], Ss[0]));
+    const int SEG = Ctx::SNAP_RING / 4;  // snapshot slots per set
+    const int ahead = std::max(1, std::min(c.bounce_ahead, SEG - 1));
+    const int gN = ceil_div(N, BLOCK);
+    struct PS {
+        uint64_t pass;
+        int set, issued, consumed;
+        uint32_t ub;
+        bool done, waited;
+    };
+    std::deque<PS> act;
+    uint64_t next = 0;
+    auto start = [&]() -> lumo_status {
+        const int set = (int)(next % K);
+        hipStream_t sm = Ss[set];
+        if (next > 0) HIPCHK(hipStreamWaitEvent(sm, c.cam_ev[(next - 1) % K], 0));  // sampler state per slot
+        {
+            StageTimer tm(c, g_timing, ST_CAMERA, sm);
+            k_camera<true><<<gN, BLOCK, 0, sm>>>(T, P[set], c.cam, N, dim_stride, (uint32_t)next);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c.cam_ev[set], sm));
+        act.push_back(PS{next, set, 0, 0, (uint32_t)N, false, next == 0});
+        next++;
+        return LUMO_OK;
+    };
+    auto wait_prev = [&](PS& ps) -> lumo_status {  // pass - 1's ring (issued: ps is the oldest pass)
+        if (!ps.waited) HIPCHK(hipStreamWaitEvent(Ss[ps.set], c.pass_ev[(ps.pass - 1) % K], 0));
+        ps.waited = true;
+        return LUMO_OK;
+    };
+    auto issue = [&](PS& ps) -> lumo_status {
+        hipStream_t sm = Ss[ps.set];
+        Paths& Q = P[ps.set];
+        if (ps.issued >= RR_DEPTH) {
+            const lumo_status w = wait_prev(ps);
+            if (w) return w;
+        }
+        k_bounce_begin<<<1, 64, 0, sm>>>(Q.counts, Q.tcount + TC_HEADQ);
+        issue_split_bounce(c, Q, T, Q.qs[ps.issued & 1], Q.qs[(ps.issued + 1) & 1], ps.ub, sm, fused_now);
+        HIPCHK(hipGetLastError());
+        const int slot = ps.set * SEG + ps.issued % SEG;
+        HIPCHK(hipMemcpyAsync(c.snap + CNT_N * slot, Q.counts, sizeof(uint32_t) * CNT_N, hipMemcpyDeviceToHost, sm));
+        HIPCHK(hipEventRecord(c.snap_ev[slot], sm));
+        ps.issued++;
+        return LUMO_OK;
+    };
+    auto poll = [&](PS& ps, bool block) -> lumo_status {
+        while (ps.consumed < ps.issued && !ps.done) {
+            const int slot = ps.set * SEG + ps.consumed % SEG;
+            if (hipEventQuery(c.snap_ev[slot]) != hipSuccess) {
+                if (!block) break;
+                HIPCHK(hipEventSynchronize(c.snap_ev[slot]));
+                block = false;
+            }
+            const uint32_t* k = c.snap + CNT_N * slot;
+            bounces += k[CNT_CUR] > 0 ? 1 : 0;
+            ps.ub = k[CNT_NEXT];
+            ps.done = ps.ub == 0;
+            ps.consumed++;
+        }
+        return LUMO_OK;
+    };
+    auto finish = [&](PS& ps) -> lumo_status {  // film + ring of the oldest pass
+        hipStream_t sm = Ss[ps.set];
+        Paths& Q = P[ps.set];
+        if (ps.pass > 0) {
+            const lumo_status w = wait_prev(ps);
+            if (w) return w;
+        }
+        if (max_P <= BLOCK) {
+            StageTimer tm(c, g_timing, ST_FILM, sm);
+            k_finish_film<<<n_tasks, BLOCK, 0, sm>>>(c.sc, Q, T, c.cam, (uint32_t)ps.pass, Dump{}, 0, c.tone_map,
+                                                     c.tone_arg);
+        } else {
+            {
+                StageTimer tm(c, g_timing, ST_FINISH, sm);
+                k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, Q, c.cam, N, (uint32_t)ps.pass, Dump{}, 0, c.tone_map, c.tone_arg);
+            }
+            StageTimer tm(c, g_timing, ST_FILM, sm);
+            k_film<<<gN, BLOCK, 0, sm>>>(Q, T, c.cam, N);
+        }
+        {
+            StageTimer tm(c, g_timing, ST_RING, sm);
+            k_ring<<<n_tasks, 64, 0, sm>>>(Q, T, n_tasks, 1, Q.counts);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c.pass_ev[ps.set], sm));
+        if (g_timing) resolve_timers(c);
+        return LUMO_OK;
+    };
+    lumo_status e = LUMO_OK;
+    while (next < max_samples || !act.empty()) {
+        bool progress = false;
+        if ((int)act.size() < K && next < max_samples) {
+            if ((e = start())) return e;
+            progress = true;
+        }
+        for (size_t i = 0; i < act.size(); ++i) {
+            PS& ps = act[i];
+            if ((e = poll(ps, false))) return e;
+            if (ps.done) {
+                if (i == 0) {
+                    if ((e = finish(ps))) return e;
+                    act.pop_front();
+                    progress = true;
+                    break;
+                }
+                continue;
+            }
+            // a younger pass stops before bounce RR_DEPTH until the pass before it has finished
+            const bool may = ps.issued < RR_DEPTH || ps.waited || i == 0;
+            if (may && ps.issued - ps.consumed < ahead) {
+                if ((e = issue(ps))) return e;
+                progress = true;
+            }
+        }
+        if (!progress) {
+            PS& f = act.front();  // the oldest pass waits for nothing the host has not issued
+            if ((e = poll(f, true))) return e;
+        }
+    }
+    // the results are copied on stream 0, after the last pass's ring
+    if (max_samples > 0) HIPCHK(hipStreamWaitEvent(Ss[0], c.pass_ev[(max_samples - 1) % K], 0));
     join.ok = true;
     return LUMO_OK;
 }
@@ -1215,7 +1473,25 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         if (ps) return ps;
         if (st) return st;
     }
-    for (uint64_t pass = 0; pass < (pipe ? 0 : max_samples); ++pass) {
+    // split schedule: passes in flight, as many as g_split_pipe and the free HBM allow
+    int K = 1;
+    if (!bdpt && !pipe && !dump_host && g_pipeline && g_split_pipe > 1 && max_samples > 1) {
+        size_t free_b = 0, total_b = 0;
+        const size_t per_set = split_set_bytes(S, N, ns);
+        const size_t margin = (size_t)8 << 30;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            K = std::min(std::min(g_split_pipe, 4), (int)std::min<uint64_t>(max_samples, 4));
+            while (K > 1 && (size_t)(K - 1) * per_set + margin > free_b + c.split_sets_bytes) K--;
+        }
+    }
+    if (K > 1) {
+        const lumo_status ps = render_split_pipelined(c, S, T, N, (int)n_tasks, dim_stride, max_samples, max_P,
+                                                      fused_now, K, bounces, st);
+        if (ps) return ps;
+        if (st) return st;
+        c.split_sets_bytes = std::max(c.split_sets_bytes, (size_t)(K - 1) * split_set_bytes(S, N, ns));
+    }
+    for (uint64_t pass = 0; pass < ((pipe || K > 1) ? 0 : max_samples); ++pass) {
         if (dump_host) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, sm));
         // S.counts: zeroed at setup, then by the ring at the end of every pass
         {
@@ -1269,66 +1545,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         lumo_status bst = LUMO_OK;
         if (!bdpt) {
             bst = bounce_loop([&](uint32_t ub, int b, int32_t*, int32_t*) {
-                const QState& cur = S.qs[b & 1];
-                const QState& nxt = S.qs[(b + 1) & 1];
-                // n_shadow == 1: the tail kernel takes the bounce when fewer than g_tail_below paths
-                // are alive (decided on the device from the exact count); the bounce kernels skip it
-                // (launched only once the last count the host has seen is below 4x the threshold:
-                // before that the bounce kernels get threshold 0 and take every path)
-                const uint32_t skip = (ns == 1 && (uint64_t)ub < 4ull * g_tail_below) ? g_tail_below : 0u;
-                if (skip > 0) {
-                    StageTimer tm(c, g_timing, ST_RESOLVE);
-                    launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
-                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true, 0, BLOCK);
-                    });
-                }
-                if (fused_now) {  // one fused kernel per bounce (pt.h k_bounce_q)
-                    StageTimer tm(c, g_timing, ST_CLOSEST);
-                    launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
-                        launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, false, g_dyn, g_bounce_threads);
-                    });
-                    return;
-                }
-                {
-                    StageTimer tm(c, g_timing, ST_CLOSEST);
-                    launch_trav(
-                        c, ub, [&](auto K, const TravLaunch& l) { launch_closest_q<decltype(K)::value>(l, c.sc, S, cur, skip); },
-                        nullptr, true);
-                }
-                {
-                    StageTimer tm(c, g_timing, ST_SHADE);
-                    const int g = ceil_div(ub, BLOCK);
-                    if (ns > 1) {  // NEE pairs by k_nee_gen, one thread per pair
-                        const int gp = std::min(ceil_div((uint64_t)ub * (uint32_t)ns, BLOCK), 1 << 16);
-                        if (c.sc.full == 2) {
-                            k_shade_q<2, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
-                            k_nee_gen<2><<<gp, BLOCK, 0, sm>>>(c.sc, S);
-                        } else if (c.sc.full) {
-                            k_shade_q<1, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
-                            k_nee_gen<1><<<gp, BLOCK, 0, sm>>>(c.sc, S);
-                        } else {
-                            k_shade_q<0, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
-                            k_nee_gen<0><<<gp, BLOCK, 0, sm>>>(c.sc, S);
-                        }
-                    } else if (c.sc.full == 2) {
-                        k_shade_q<2, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
-                    } else if (c.sc.full) {
-                        k_shade_q<1, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
-                    } else {
-                        k_shade_q<0, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
-                    }
-                }
-                {
-                    StageTimer tm(c, g_timing, ST_SHADOW);
-                    launch_trav(
-                        c, (uint64_t)ub * (uint32_t)ns,
-                        [&](auto K, const TravLaunch& l) { launch_shadow_q<decltype(K)::value>(l, c.sc, S, nxt); }, nullptr,
-                        true);
-                }
-                if (ns > 1) {
-                    StageTimer tm(c, g_timing, ST_RESOLVE);
-                    k_nee_fold<<<std::min(ceil_div(ub, BLOCK), 1 << 14), BLOCK, 0, sm>>>(S, nxt, ns);
-                }
+                issue_split_bounce(c, S, T, S.qs[b & 1], S.qs[(b + 1) & 1], ub, sm, fused_now);
             });
             if (bst) return bst;
         } else {
@@ -1638,6 +1855,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_LDS_GRID")) c->lds_grid_cap = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("LUMO_TOP_GRID")) c->top_grid_cap = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("LUMO_TOP")) g_top = std::atoi(e);
+    if (const char* e = std::getenv("LUMO_SPLIT_PIPE")) g_split_pipe = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("LUMO_TOP_KB")) c->top_lds_bytes = std::max(0, std::atoi(e)) * 1024;
     if (const char* e = std::getenv("LUMO_FUSED")) g_fused = std::atoi(e);
     if (const char* e = std::getenv("LUMO_QSORT")) g_qsort = std::atoi(e) & 3;

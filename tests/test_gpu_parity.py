@@ -190,7 +190,8 @@ def test_separate_result_buffers_match_oracle(dev, cornell, max_paths):
         assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
 
 
-@pytest.mark.parametrize("fused,tail,pipe", [(0, 0, 0), (0, 300, 0), (0, 1 << 30, 0), (1, 0, 0), (1, 300, 0),
+@pytest.mark.parametrize("fused,tail,pipe", [(0, 0, 0), (0, 300, 0), (0, 1 << 30, 0), (0, 0, 1), (0, 300, 1),
+                                             (1, 0, 0), (1, 300, 0),
                                              (1, 1 << 30, 0), (1, 0, 1), (-1, 1 << 18, 1), (-1, 1 << 18, 2), (-1, 1 << 18, 3)])
 def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
     """The three-kernel bounce and the fused bounce kernel (k_bounce_q: closest hit + shading +

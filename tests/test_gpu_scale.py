@@ -198,7 +198,8 @@ def test_kernel_variants(dev, variant_env, name, cls, lds, full):
         assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
 
 
-@pytest.mark.parametrize("fused,tail,pipe", [(1, 0, 0), (1, 300, 0), (0, 1 << 30, 0), (1, 0, 1), (1, 0, 2), (1, 0, 3)])
+@pytest.mark.parametrize("fused,tail,pipe", [(1, 0, 0), (1, 300, 0), (0, 1 << 30, 0), (1, 0, 1), (1, 0, 2), (1, 0, 3),
+                                             (0, 0, 1), (0, 1 << 18, 1)])
 def test_bounce_modes_small_dragon(dev, fused, tail, pipe):
     """The fused bounce kernel and the tail kernel on an instanced glass mesh (feature class 1,
     no LDS staging, deep kd stack): paths and tiles equal the oracle's."""
@@ -285,3 +286,34 @@ def test_top_staging_budgets(mid_bistro, budget_kb, top):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4])
+def test_split_pipeline_passes_in_flight(mid_bistro, k):
+    """render_split_pipelined (n_shadow > 1, three-kernel bounces): with 1 (sequential) to 4 passes
+    in flight on their own streams and pass sets, a 9-pass render's tiles, ray and query counts
+    equal the oracle's (passes wait for the previous pass's camera, its ring before bounce
+    RR_DEPTH and before their film; set reuse is ordered by stream)."""
+    saved = os.environ.get("LUMO_SPLIT_PIPE")
+    os.environ["LUMO_SPLIT_PIPE"] = str(k)
+    try:
+        d = L.Device(0)
+        cam = scenes.bistro_camera((64, 48))
+        d.upload(mid_bistro, cam)
+        assert d.scene_info().n_shadow > 1
+        tasks = L.make_tasks(64, 48, 9, SEED)
+        before = d.stats()
+        bufs, res = d.render_tasks(tasks)
+        after = d.stats()
+        d.close()
+    finally:
+        if saved is None:
+            os.environ.pop("LUMO_SPLIT_PIPE", None)
+        else:
+            os.environ["LUMO_SPLIT_PIPE"] = saved
+    obufs, ores, cnt = O.render_tasks(mid_bistro.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+    assert after.closest_queries - before.closest_queries == cnt.closest_queries
+    assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
