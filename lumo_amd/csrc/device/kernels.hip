@@ -1484,6 +1484,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             while (K > 1 && (size_t)(K - 1) * per_set + margin > free_b + c.split_sets_bytes) K--;
         }
     }
+    if (std::getenv("LUMO_DEBUG_SCHED"))
+        std::fprintf(stderr, "lumo: N=%d passes=%llu ns=%d fused=%d pipe=%d split K=%d g_pipeline=%d tail=%u\n", N,
+                     (unsigned long long)max_samples, ns, (int)fused_now, (int)pipe, K, g_pipeline, g_tail_below);
     if (K > 1) {
         const lumo_status ps = render_split_pipelined(c, S, T, N, (int)n_tasks, dim_stride, max_samples, max_P,
                                                       fused_now, K, bounces, st);
