@@ -1100,7 +1100,8 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
 // passes run at once, pass p on stream p % K with pass set p % K (queues, counters, hits, NEE
 // records, per-slot outputs).  Russian roulette reads the pass's delta only from depth RR_DEPTH on
 // (path_trace.rs:60-69) and the sampler state is per slot, so pass p waits for pass p - 1's
-// camera before its own and for pass p - 1's ring before its bounce RR_DEPTH and its film; set
+// camera before its own and for pass p - 1's ring before its bounce RR_DEPTH (or the first bounce
+// that may run the tail kernel, which takes paths through Russian roulette) and its film; set
 // reuse (pass p + K) is ordered by its stream.  The host runs every in-flight pass's bounce loop
 // (count snapshots `ahead` launches back, as the sequential loop) and blocks only on the oldest
 // pass, which never waits for a younger one; a younger pass issues bounce RR_DEPTH and its film
@@ -1163,10 +1164,15 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         ps.waited = true;
         return LUMO_OK;
     };
+    // the tail kernel (n_shadow == 1, launched once few paths are alive) runs paths to their end,
+    // through Russian roulette, in whatever bounce it is launched: such a bounce needs the delta too
+    auto tail_possible = [&](const PS& ps) {
+        return ns == 1 && g_tail_below > 0 && (uint64_t)ps.ub < 4ull * g_tail_below;
+    };
     auto issue = [&](PS& ps) -> lumo_status {
         hipStream_t sm = Ss[ps.set];
         Paths& Q = P[ps.set];
-        if (ps.issued >= RR_DEPTH) {
+        if (ps.issued >= RR_DEPTH || tail_possible(ps)) {
             const lumo_status w = wait_prev(ps);
             if (w) return w;
         }
@@ -1242,8 +1248,9 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
                 }
                 continue;
             }
-            // a younger pass stops before bounce RR_DEPTH until the pass before it has finished
-            const bool may = ps.issued < RR_DEPTH || ps.waited || i == 0;
+            // a younger pass stops before bounce RR_DEPTH (or a tail-kernel bounce) until the pass
+            // before it has finished
+            const bool may = (ps.issued < RR_DEPTH && !tail_possible(ps)) || ps.waited || i == 0;
             if (may && ps.issued - ps.consumed < ahead) {
                 if ((e = issue(ps))) return e;
                 progress = true;
