@@ -126,8 +126,9 @@ __device__ __forceinline__ uint64_t wf_path_seed(uint64_t pixel_seed, uint64_t k
 // QUEUE (path tracer): the camera paths enter the queue-order state qs[0]; otherwise (BDPT) the
 // ray, throughput, wavelengths and RNG stay per slot and the slot ids are queued in q0.
 template <bool QUEUE>
-__global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, int n, int dim_stride, uint32_t pass) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, int n, int dim_stride, uint32_t pass,
+                                                  int s0) {
+    const int s = s0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);  // slots [s0, n)
     bool active = false;
     Ray ray{V3{0, 0, 0}, V3{0, 0, 0}};
     double L[NS] = {0.0, 0.0, 0.0, 0.0};
@@ -309,8 +310,8 @@ __device__ __forceinline__ V3 finish_one(const DScene& sc, const Paths& S, const
 }
 
 __global__ __launch_bounds__(BLOCK) void k_finish(DScene sc, Paths S, DCam cam, int n, uint32_t pass, Dump dump,
-                                                   int dump_p, int tone_map, double tone_arg) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+                                                   int dump_p, int tone_map, double tone_arg, int s0) {
+    const int s = s0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);  // slots [s0, n)
     int cat = 0;
     if (s < n && S.p_valid[s]) {
         cat = sample_check(ldc(S.rad, s));
@@ -386,8 +387,8 @@ struct HbmSrc {  // sources read from the per-slot buffers k_finish wrote
     __device__ V3 rgb(int k) const { return ldv3(S.p_rgb, first + k); }
 };
 
-__global__ __launch_bounds__(BLOCK) void k_film(Paths S, Tasks T, DCam cam, int n) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(BLOCK) void k_film(Paths S, Tasks T, DCam cam, int n, int s0) {
+    const int s = s0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);  // slots [s0, n)
     if (s >= n) return;
     const int ti = S.task[s];
     film_gather(S, T.t[ti], cam, s, S.pix[s], HbmSrc{S, T.first[ti]});
@@ -408,12 +409,12 @@ struct LdsSrc {  // sources staged in LDS by k_finish_film
 // the tile's sample RGB and raster positions staged in LDS instead of a round trip through HBM.
 // Same arithmetic as the two kernels, so the film is bit-identical.
 __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S, Tasks T, DCam cam, uint32_t pass, Dump dump,
-                                                        int dump_p, int tone_map, double tone_arg) {
+                                                        int dump_p, int tone_map, double tone_arg, int t0) {
     __shared__ double l_rgb[3 * BLOCK];
     __shared__ double l_ras[2 * BLOCK];
     __shared__ uint32_t l_ok[BLOCK];
     __shared__ double l_wx[(2 * FILM_R + 1) * BLOCK], l_wy[(2 * FILM_R + 1) * BLOCK];
-    const int ti = blockIdx.x;
+    const int ti = t0 + (int)blockIdx.x;  // tasks [t0, t0 + gridDim.x)
     const int first = T.first[ti];
     const int P = T.first[ti + 1] - first;
     const int j = threadIdx.x;
@@ -455,11 +456,11 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S, Tasks
 // `zero_counts` (when set): the pass's queue counters, zeroed by block 0 for the next pass that
 // uses them (every kernel of the pass that reads them precedes the ring on its stream), so a pass
 // starts without a fill of its own.
-__global__ __launch_bounds__(64) void k_ring(Paths S, Tasks T, int n_tasks, int update, uint32_t* zero_counts) {
-    const int ti = blockIdx.x;
+__global__ __launch_bounds__(64) void k_ring(Paths S, Tasks T, int n_tasks, int update, uint32_t* zero_counts, int t0) {
+    const int ti = t0 + (int)blockIdx.x;  // tasks [t0, n_tasks)
     if (ti >= n_tasks) return;
     const int lane = threadIdx.x;
-    if (zero_counts && ti == 0 && lane < CNT_N) zero_counts[lane] = 0u;
+    if (zero_counts && blockIdx.x == 0 && lane < CNT_N) zero_counts[lane] = 0u;
     __shared__ double lum[SAMPLES_INCREMENT];
     __shared__ unsigned long long cst[SAMPLES_INCREMENT];
     const lumo_tile_task& t = T.t[ti];
@@ -850,6 +851,7 @@ int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from 
 int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
 int g_heads = 0;                   // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
 int g_split_pipe = 4;              // split schedule: passes in flight (render_split_pipelined; 1 = sequential)
+int g_split_groups = 2;            // split schedule: independent task groups (render_split_pipelined)
 int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
 // allow_top: the kernel has a TOP-staged variant (k_closest_q, k_shadow_q); it is used when the
 // whole scene does not fit in LDS but its top levels were packed at upload (DScene::top).
@@ -969,7 +971,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         if (NA > 1) HIPCHK(hipStreamWaitEvent(A, c.cam_ev[prev], 0));  // pass - 1's camera (sampler state)
         {
             StageTimer tm(c, g_timing, ST_CAMERA, A);
-            k_camera<true><<<gN, BLOCK, 0, A>>>(T, P, c.cam, N, dim_stride, (uint32_t)pass);
+            k_camera<true><<<gN, BLOCK, 0, A>>>(T, P, c.cam, N, dim_stride, (uint32_t)pass, 0);
         }
         HIPCHK(hipEventRecord(c.cam_ev[set], A));
         for (int b = 0; b < heads; ++b) {
@@ -1003,18 +1005,18 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         if (max_P <= BLOCK) {
             StageTimer tm(c, g_timing, ST_FILM, B);
             k_finish_film<<<n_tasks, BLOCK, 0, B>>>(c.sc, P, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
-                                                    c.tone_arg);
+                                                    c.tone_arg, 0);
         } else {
             {
                 StageTimer tm(c, g_timing, ST_FINISH, B);
-                k_finish<<<gN, BLOCK, 0, B>>>(c.sc, P, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg);
+                k_finish<<<gN, BLOCK, 0, B>>>(c.sc, P, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg, 0);
             }
             StageTimer tm(c, g_timing, ST_FILM, B);
-            k_film<<<gN, BLOCK, 0, B>>>(P, T, c.cam, N);
+            k_film<<<gN, BLOCK, 0, B>>>(P, T, c.cam, N, 0);
         }
         {
             StageTimer tm(c, g_timing, ST_RING, B);
-            k_ring<<<n_tasks, 64, 0, B>>>(P, T, n_tasks, 1, P.counts);
+            k_ring<<<n_tasks, 64, 0, B>>>(P, T, n_tasks, 1, P.counts, 0);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.pass_ev[set], B));
@@ -1096,21 +1098,25 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
 // Pipelined passes of the split schedule (closest hit / shading / visibility kernels: scenes too
 // large for the fused LDS kernel, n_shadow > 1).  A pass whose queue has shrunk to a few thousand
 // paths runs latency-bound launches (one long walk sets a kernel's duration: C3 at one rank's 1/8
-// share spent ~0.4 ms per closest / visibility launch for every bounce past the fifth), so K
-// passes run at once, pass p on stream p % K with pass set p % K (queues, counters, hits, NEE
-// records, per-slot outputs).  Russian roulette reads the pass's delta only from depth RR_DEPTH on
-// (path_trace.rs:60-69) and the sampler state is per slot, so pass p waits for pass p - 1's
-// camera before its own and for pass p - 1's ring before its bounce RR_DEPTH (or the first bounce
-// that may run the tail kernel, which takes paths through Russian roulette) and its film; set
-// reuse (pass p + K) is ordered by its stream.  The host runs every in-flight pass's bounce loop
-// (count snapshots `ahead` launches back, as the sequential loop) and blocks only on the oldest
-// pass, which never waits for a younger one; a younger pass issues bounce RR_DEPTH and its film
-// only once the pass before it has issued its ring, so every wait is enqueued after the record it
-// waits for.  Every per-path operation and every film / ring sum is the sequential loop's:
-// bit-identical.
+// share spent ~0.4 ms per closest / visibility launch for every bounce past the fifth), so several
+// passes run at once on their own streams and pass sets (queues, counters, hits, NEE records,
+// per-slot outputs).
+//
+// Russian roulette reads a task's adaptive delta from depth RR_DEPTH on (path_trace.rs:60-69) and
+// the delta of pass p needs the film and ring of pass p - 1 *of the same task* (task.rs:28-53); the
+// sampler state is per slot.  So the tasks are cut into G groups of consecutive tasks (about equal
+// slots) whose pass chains are independent, and the units of work are (group g, pass p), issued in
+// the order n = p * G + g on pass set / stream n % K (K >= G).  Unit (g, p) waits for unit (g, p - 1)'s
+// camera before its own, and for its ring before its bounce RR_DEPTH, before any bounce that may
+// run the tail kernel (n_shadow == 1: it takes paths through Russian roulette) and before its film.
+// Set reuse (unit n + K) is ordered by its stream.  The host runs every in-flight unit's bounce
+// loop (count snapshots `ahead` launches back, as the sequential loop), blocks only on the oldest
+// unit, which never waits for a unit the host has not finished issuing, and enqueues every wait
+// after the record it waits for.  Every per-path operation and every film / ring sum of a task is
+// the sequential loop's, in the same order: bit-identical.
 lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int n_tasks, int dim_stride,
-                                   uint64_t max_samples, uint64_t max_P, bool fused_now, int K, uint64_t& bounces,
-                                   lumo_status& st) {
+                                   uint64_t max_samples, uint64_t max_P, bool fused_now, int K, int G,
+                                   const std::vector<int32_t>& first, uint64_t& bounces, lumo_status& st) {
     struct JoinOnError {
         Ctx& c;
         bool ok = false;
@@ -1121,6 +1127,16 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         }
     } join{c};
     const int ns = c.sc.n_shadow;
+    G = std::max(1, std::min(G, std::min(K, n_tasks)));
+    // groups of consecutive tasks, about N / G slots each
+    std::vector<int> t_lo(G), t_hi(G);
+    for (int g = 0, t = 0; g < G; ++g) {
+        t_lo[g] = t;
+        const int64_t target = (int64_t)N * (g + 1) / G;
+        while (t < n_tasks && (g == G - 1 || first[t + 1] <= target || t == t_lo[g])) ++t;
+        t = std::max(std::min(t, n_tasks - (G - 1 - g)), t_lo[g] + 1);  // >= 1 task here and in every later group
+        t_hi[g] = t;
+    }
     Paths P[4] = {S, S, S, S};
     for (int k = 1; k < K; ++k) {
         alloc_pass_set(c, P[k], k, N, st);
@@ -1136,31 +1152,36 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
     for (int k = 0; k < 4; ++k) HIPCHK(hipEventRecord(c.pass_ev[k], Ss[0]));
     const int SEG = Ctx::SNAP_RING / 4;  // snapshot slots per set
     const int ahead = std::max(1, std::min(c.bounce_ahead, SEG - 1));
-    const int gN = ceil_div(N, BLOCK);
     struct PS {
-        uint64_t pass;
-        int set, issued, consumed;
+        uint64_t unit, pass;
+        int g, set, issued, consumed;
         uint32_t ub;
         bool done, waited;
     };
     std::deque<PS> act;
+    std::vector<uint64_t> finished(G, 0);  // passes of each group whose ring has been issued
+    const uint64_t units = max_samples * (uint64_t)G;
     uint64_t next = 0;
     auto start = [&]() -> lumo_status {
-        const int set = (int)(next % K);
+        const int set = (int)(next % K), g = (int)(next % G);
+        const uint64_t pass = next / G;
         hipStream_t sm = Ss[set];
-        if (next > 0) HIPCHK(hipStreamWaitEvent(sm, c.cam_ev[(next - 1) % K], 0));  // sampler state per slot
+        const int s0 = first[t_lo[g]], s1 = first[t_hi[g]];
+        if (pass > 0) HIPCHK(hipStreamWaitEvent(sm, c.cam_ev[(next - G) % K], 0));  // sampler state per slot
         {
             StageTimer tm(c, g_timing, ST_CAMERA, sm);
-            k_camera<true><<<gN, BLOCK, 0, sm>>>(T, P[set], c.cam, N, dim_stride, (uint32_t)next);
+            k_camera<true><<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(T, P[set], c.cam, s1, dim_stride, (uint32_t)pass,
+                                                                        s0);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.cam_ev[set], sm));
-        act.push_back(PS{next, set, 0, 0, (uint32_t)N, false, next == 0});
+        act.push_back(PS{next, pass, g, set, 0, 0, (uint32_t)(s1 - s0), false, pass == 0});
         next++;
         return LUMO_OK;
     };
-    auto wait_prev = [&](PS& ps) -> lumo_status {  // pass - 1's ring (issued: ps is the oldest pass)
-        if (!ps.waited) HIPCHK(hipStreamWaitEvent(Ss[ps.set], c.pass_ev[(ps.pass - 1) % K], 0));
+    auto ready = [&](const PS& ps) { return ps.waited || finished[ps.g] >= ps.pass; };
+    auto wait_prev = [&](PS& ps) -> lumo_status {  // unit (g, p - 1)'s ring, already issued
+        if (!ps.waited) HIPCHK(hipStreamWaitEvent(Ss[ps.set], c.pass_ev[(ps.unit - G) % K], 0));
         ps.waited = true;
         return LUMO_OK;
     };
@@ -1201,38 +1222,39 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         }
         return LUMO_OK;
     };
-    auto finish = [&](PS& ps) -> lumo_status {  // film + ring of the oldest pass
+    auto finish = [&](PS& ps) -> lumo_status {  // film + ring of the group's tasks
         hipStream_t sm = Ss[ps.set];
         Paths& Q = P[ps.set];
-        if (ps.pass > 0) {
-            const lumo_status w = wait_prev(ps);
-            if (w) return w;
-        }
+        const lumo_status w = wait_prev(ps);
+        if (w) return w;
+        const int t0 = t_lo[ps.g], t1 = t_hi[ps.g], s0 = first[t0], s1 = first[t1];
         if (max_P <= BLOCK) {
             StageTimer tm(c, g_timing, ST_FILM, sm);
-            k_finish_film<<<n_tasks, BLOCK, 0, sm>>>(c.sc, Q, T, c.cam, (uint32_t)ps.pass, Dump{}, 0, c.tone_map,
-                                                     c.tone_arg);
+            k_finish_film<<<t1 - t0, BLOCK, 0, sm>>>(c.sc, Q, T, c.cam, (uint32_t)ps.pass, Dump{}, 0, c.tone_map,
+                                                     c.tone_arg, t0);
         } else {
             {
                 StageTimer tm(c, g_timing, ST_FINISH, sm);
-                k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, Q, c.cam, N, (uint32_t)ps.pass, Dump{}, 0, c.tone_map, c.tone_arg);
+                k_finish<<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(c.sc, Q, c.cam, s1, (uint32_t)ps.pass, Dump{}, 0,
+                                                                     c.tone_map, c.tone_arg, s0);
             }
             StageTimer tm(c, g_timing, ST_FILM, sm);
-            k_film<<<gN, BLOCK, 0, sm>>>(Q, T, c.cam, N);
+            k_film<<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(Q, T, c.cam, s1, s0);
         }
         {
             StageTimer tm(c, g_timing, ST_RING, sm);
-            k_ring<<<n_tasks, 64, 0, sm>>>(Q, T, n_tasks, 1, Q.counts);
+            k_ring<<<t1 - t0, 64, 0, sm>>>(Q, T, t1, 1, Q.counts, t0);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.pass_ev[ps.set], sm));
+        finished[ps.g] = ps.pass + 1;
         if (g_timing) resolve_timers(c);
         return LUMO_OK;
     };
     lumo_status e = LUMO_OK;
-    while (next < max_samples || !act.empty()) {
+    while (next < units || !act.empty()) {
         bool progress = false;
-        if ((int)act.size() < K && next < max_samples) {
+        if ((int)act.size() < K && next < units) {
             if ((e = start())) return e;
             progress = true;
         }
@@ -1240,29 +1262,29 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
             PS& ps = act[i];
             if ((e = poll(ps, false))) return e;
             if (ps.done) {
-                if (i == 0) {
+                if (ready(ps)) {  // the group's previous pass has issued its ring
                     if ((e = finish(ps))) return e;
-                    act.pop_front();
+                    act.erase(act.begin() + (std::ptrdiff_t)i);
                     progress = true;
                     break;
                 }
                 continue;
             }
-            // a younger pass stops before bounce RR_DEPTH (or a tail-kernel bounce) until the pass
-            // before it has finished
-            const bool may = (ps.issued < RR_DEPTH && !tail_possible(ps)) || ps.waited || i == 0;
+            // a unit stops before bounce RR_DEPTH (or a tail-kernel bounce) until the group's
+            // previous pass has issued its ring
+            const bool may = (ps.issued < RR_DEPTH && !tail_possible(ps)) || ready(ps);
             if (may && ps.issued - ps.consumed < ahead) {
                 if ((e = issue(ps))) return e;
                 progress = true;
             }
         }
         if (!progress) {
-            PS& f = act.front();  // the oldest pass waits for nothing the host has not issued
+            PS& f = act.front();  // the oldest unit waits for nothing the host has not issued
             if ((e = poll(f, true))) return e;
         }
     }
-    // the results are copied on stream 0, after the last pass's ring
-    if (max_samples > 0) HIPCHK(hipStreamWaitEvent(Ss[0], c.pass_ev[(max_samples - 1) % K], 0));
+    // the results are copied on stream 0: after every set's last unit
+    for (int k = 1; k < K; ++k) HIPCHK(hipStreamWaitEvent(Ss[0], c.pass_ev[k], 0));
     join.ok = true;
     return LUMO_OK;
 }
@@ -1462,7 +1484,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     const int gT = ceil_div(n_tasks, BLOCK), gN = ceil_div(N, BLOCK);
     k_init_seeds<<<gT, BLOCK, 0, sm>>>(T, S, (int)n_tasks);
     k_init_mj<<<gN, BLOCK, 0, sm>>>(T, S, N, dim_stride);
-    k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 0, nullptr);
+    k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 0, nullptr, 0);
     HIPCHK(hipGetLastError());
 
     uint64_t bounces = 0, closest_q = 0, shadow_q = 0;
@@ -1482,12 +1504,13 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     }
     // split schedule: passes in flight, as many as g_split_pipe and the free HBM allow
     int K = 1;
-    if (!bdpt && !pipe && !dump_host && g_pipeline && g_split_pipe > 1 && max_samples > 1) {
+    const uint64_t units = max_samples * (uint64_t)std::max(1, std::min(g_split_groups, (int)n_tasks));
+    if (!bdpt && !pipe && !dump_host && g_pipeline && g_split_pipe > 1 && units > 1) {
         size_t free_b = 0, total_b = 0;
         const size_t per_set = split_set_bytes(S, N, ns);
         const size_t margin = (size_t)8 << 30;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-            K = std::min(std::min(g_split_pipe, 4), (int)std::min<uint64_t>(max_samples, 4));
+            K = std::min(std::min(g_split_pipe, 4), (int)std::min<uint64_t>(units, 4));
             while (K > 1 && (size_t)(K - 1) * per_set + margin > free_b + c.split_sets_bytes) K--;
         }
     }
@@ -1496,7 +1519,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                      (unsigned long long)max_samples, ns, (int)fused_now, (int)pipe, K, g_pipeline, g_tail_below);
     if (K > 1) {
         const lumo_status ps = render_split_pipelined(c, S, T, N, (int)n_tasks, dim_stride, max_samples, max_P,
-                                                      fused_now, K, bounces, st);
+                                                      fused_now, K, g_split_groups, first, bounces, st);
         if (ps) return ps;
         if (st) return st;
         c.split_sets_bytes = std::max(c.split_sets_bytes, (size_t)(K - 1) * split_set_bytes(S, N, ns));
@@ -1507,9 +1530,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         {
             StageTimer tm(c, g_timing, ST_CAMERA);
             if (bdpt)
-                k_camera<false><<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass);
+                k_camera<false><<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass, 0);
             else
-                k_camera<true><<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass);
+                k_camera<true><<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass, 0);
         }
         HIPCHK(hipGetLastError());
         // Bounce loop over the alive queue (filled by the producer just launched): `step` launches
@@ -1658,20 +1681,20 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         if (max_P <= BLOCK) {  // one block per tile (lumo's 16x16 tiles)
             StageTimer tm(c, g_timing, ST_FILM);
             k_finish_film<<<(int)n_tasks, BLOCK, 0, sm>>>(c.sc, S, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
-                                                          c.tone_arg);
+                                                          c.tone_arg, 0);
         } else {
             {
                 StageTimer tm(c, g_timing, ST_FINISH);
-                k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, S, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg);
+                k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, S, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg, 0);
             }
             {
                 StageTimer tm(c, g_timing, ST_FILM);
-                k_film<<<gN, BLOCK, 0, sm>>>(S, T, c.cam, N);
+                k_film<<<gN, BLOCK, 0, sm>>>(S, T, c.cam, N, 0);
             }
         }
         {
             StageTimer tm(c, g_timing, ST_RING);
-            k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 1, S.counts);
+            k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 1, S.counts, 0);
         }
         HIPCHK(hipGetLastError());
         if (bdpt && dfilm) {
@@ -1866,6 +1889,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_TOP_GRID")) c->top_grid_cap = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("LUMO_TOP")) g_top = std::atoi(e);
     if (const char* e = std::getenv("LUMO_SPLIT_PIPE")) g_split_pipe = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("LUMO_SPLIT_GROUPS")) g_split_groups = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("LUMO_TOP_KB")) c->top_lds_bytes = std::max(0, std::atoi(e)) * 1024;
     if (const char* e = std::getenv("LUMO_FUSED")) g_fused = std::atoi(e);
     if (const char* e = std::getenv("LUMO_QSORT")) g_qsort = std::atoi(e) & 3;

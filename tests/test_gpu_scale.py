@@ -288,14 +288,16 @@ def test_top_staging_budgets(mid_bistro, budget_kb, top):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("k", [1, 2, 3, 4])
-def test_split_pipeline_passes_in_flight(mid_bistro, k):
-    """render_split_pipelined (n_shadow > 1, three-kernel bounces): with 1 (sequential) to 4 passes
-    in flight on their own streams and pass sets, a 9-pass render's tiles, ray and query counts
-    equal the oracle's (passes wait for the previous pass's camera, its ring before bounce
-    RR_DEPTH and before their film; set reuse is ordered by stream)."""
-    saved = os.environ.get("LUMO_SPLIT_PIPE")
+@pytest.mark.parametrize("k,groups", [(1, 1), (2, 1), (3, 1), (4, 1), (2, 2), (4, 2), (3, 3), (4, 4)])
+def test_split_pipeline_passes_in_flight(mid_bistro, k, groups):
+    """render_split_pipelined (n_shadow > 1, three-kernel bounces): 1 (sequential) to 4 units of
+    (task group, pass) in flight on their own streams and pass sets, with the 12 tasks cut into 1-4
+    independent groups; a 9-pass render's tiles, ray and query counts equal the oracle's (a unit
+    waits for its group's previous pass's camera, and its ring before bounce RR_DEPTH and before
+    its film; set reuse is ordered by stream)."""
+    saved = {v: os.environ.get(v) for v in ("LUMO_SPLIT_PIPE", "LUMO_SPLIT_GROUPS")}
     os.environ["LUMO_SPLIT_PIPE"] = str(k)
+    os.environ["LUMO_SPLIT_GROUPS"] = str(groups)
     try:
         d = L.Device(0)
         cam = scenes.bistro_camera((64, 48))
@@ -307,10 +309,11 @@ def test_split_pipeline_passes_in_flight(mid_bistro, k):
         after = d.stats()
         d.close()
     finally:
-        if saved is None:
-            os.environ.pop("LUMO_SPLIT_PIPE", None)
-        else:
-            os.environ["LUMO_SPLIT_PIPE"] = saved
+        for v, x in saved.items():
+            if x is None:
+                os.environ.pop(v, None)
+            else:
+                os.environ[v] = x
     obufs, ores, cnt = O.render_tasks(mid_bistro.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
     for b, ob, r, orr in zip(bufs, obufs, res, ores):
         np.testing.assert_array_equal(b, ob)
