@@ -440,14 +440,6 @@ class Scene:
             obj = _read_source(path, ".obj")
             mtl = _read_source(mtllib, ".mtl") if mtllib else None
             base = os.path.dirname(os.path.abspath(mtllib if mtllib else path))
-            for root, _, files in os.walk(base):
-                for f in files:
-                    if f.lower().endswith((".png", ".hdr")):
-                        full = os.path.join(root, f)
-                        with open(full, "rb") as fh:
-                            data = fh.read()
-                        rel = os.path.relpath(full, base).replace(os.sep, "/")
-                        check(L.lumo_builder_add_file(s._b, rel.encode(), data, len(data)), "add_file")
             env = (_read_source(env_map[0], ".hdr"), env_map[1]) if env_map else None
         # parser.rs:219-249: the explicit mtllib, then every `mtllib` statement of the .obj
         mtls = [mtl] if mtl else []
@@ -462,6 +454,23 @@ class Scene:
                     if os.path.exists(f):
                         mtls.append(_read_source(f, ".mtl"))
         mtl = b"\n".join(mtls) if mtls else None
+        if not str(path).lower().endswith(".zip") and mtl:
+            # plain files: register only the files the MTL's map statements name (matched by
+            # _extract_zip's case-insensitive suffix rule under the MTL's directory), so the
+            # directory's other images are never read
+            wanted = set()
+            for line in mtl.decode("utf-8", "replace").splitlines():
+                tok = line.split()
+                if len(tok) >= 2 and (tok[0].lower().startswith("map_") or tok[0].lower() in ("bump", "norm")):
+                    wanted.add(tok[-1].replace("\\", "/").lower())
+            for root, _, files in os.walk(base) if wanted else ():
+                for f in files:
+                    full = os.path.join(root, f)
+                    rel = os.path.relpath(full, base).replace(os.sep, "/")
+                    if any(rel.lower().endswith(w) for w in wanted):
+                        with open(full, "rb") as fh:
+                            data = fh.read()
+                        check(L.lumo_builder_add_file(s._b, rel.encode(), data, len(data)), "add_file")
         check(L.lumo_builder_set_map_ks(s._b, int(bool(map_ks))), "map_ks")
         st = L.lumo_builder_load_obj_scene(s._b, obj, len(obj), mtl, len(mtl) if mtl else 0)
         if st != _ffi.LUMO_OK:

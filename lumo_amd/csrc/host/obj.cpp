@@ -181,8 +181,11 @@ bool parse_mtl(SceneBuilder& sb, const char* data, size_t n, std::vector<std::pa
         auto file_of = [&](const std::vector<std::string>& t) -> const std::vector<uint8_t>* {
             std::string nm;  // tokens[1..].join(" ")
             for (size_t i = 1; i < t.size(); ++i) nm += (i > 1 ? " " : "") + t[i];
-            const std::vector<uint8_t>* f = sb.find_file(nm);
-            if (!f) err = "material " + name + ": no file " + nm + " for " + t[0] + " (lumo_builder_add_file)";
+            int matches = 0;
+            const std::vector<uint8_t>* f = sb.find_file(nm, &matches);
+            if (!f)  // parser.rs:88-114: "Could not find" / "Found multiple"
+                err = "material " + name + ": " + (matches > 1 ? "several files match " : "no file ") + nm + " for " +
+                      t[0] + (matches > 1 ? "" : " (lumo_builder_add_file)");
             return f;
         };
         auto image = [&](const std::vector<std::string>& t, int& dst) -> bool {

@@ -795,7 +795,7 @@ lumo_scene_desc FlatScene::desc() const {
     return d;
 }
 
-const std::vector<uint8_t>* SceneBuilder::find_file(const std::string& name) const {
+const std::vector<uint8_t>* SceneBuilder::find_file(const std::string& name, int* matches) const {
     std::string n = name;
     for (char& ch : n) {
         if (ch == '\\') ch = '/';  // parser/mtl/task.rs: .replace('\\', "/")
@@ -804,15 +804,17 @@ const std::vector<uint8_t>* SceneBuilder::find_file(const std::string& name) con
     // parser.rs:88-114 _extract_zip: the one archive member whose lower-cased name ends with the
     // lower-cased request (none or several: an error)
     const std::vector<uint8_t>* hit = nullptr;
+    int count = 0;
     for (const auto& f : files) {
         std::string m = f.first;
         for (char& ch : m) ch = (char)std::tolower((unsigned char)ch);
         if (m.size() >= n.size() && m.compare(m.size() - n.size(), n.size(), n) == 0) {
-            if (hit) return nullptr;
             hit = &f.second;
+            count++;
         }
     }
-    return hit;
+    if (matches) *matches = count;
+    return count == 1 ? hit : nullptr;
 }
 
 namespace {

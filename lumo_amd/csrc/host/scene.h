@@ -121,7 +121,9 @@ class SceneBuilder {
     // named files for the MTL map_* statements (parser.rs _img_from_zip) and the map_ks flag
     std::vector<std::pair<std::string, std::vector<uint8_t>>> files;
     bool map_ks = false;
-    const std::vector<uint8_t>* find_file(const std::string& name) const;
+    // parser.rs _extract_zip: the one registered file whose name ends with `name` (case-insensitive);
+    // null when none or several match (*matches says how many)
+    const std::vector<uint8_t>* find_file(const std::string& name, int* matches = nullptr) const;
 
     // Scene::cornell_box (scene/cornell_box.rs:8-193)
     static SceneBuilder cornell_box();

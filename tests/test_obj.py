@@ -135,3 +135,29 @@ def test_texture_map_missing_file():
         open(d + "/a.mtl", "wb").write(mtl)
         with pytest.raises(ValueError, match="wall.png"):
             L.Scene.from_file(d + "/a.obj", mtllib=d + "/a.mtl")
+
+
+def test_plain_files_register_only_named_textures(tmp_path):
+    """Scene.from_file on plain files: the MTL's map_Kd name resolves by _extract_zip's
+    case-insensitive suffix rule under the MTL's directory (parser.rs:88-114); only named files are
+    read, an unrelated unreadable file is ignored, and a name two files match is reported as
+    ambiguous ("Found multiple"), not as missing."""
+    import numpy as np_
+    from imgdata import random_png
+    png = random_png(np_.random.default_rng(1), 4, 4, 2, 8)[0]
+    mtl = MTL.replace(b"newmtl red\n", b"newmtl red\nmap_Kd tex/Red.PNG\n")
+    (tmp_path / "scene.obj").write_bytes(OBJ)
+    (tmp_path / "scene.mtl").write_bytes(mtl)
+    (tmp_path / "tex").mkdir()
+    (tmp_path / "tex" / "red.png").write_bytes(png)
+    (tmp_path / "unrelated.png").mkdir()  # a directory with an image's name: never opened
+    s = L.Scene.from_file(str(tmp_path / "scene.obj"), mtllib=str(tmp_path / "scene.mtl"))
+    assert s.desc().num_textures >= 1
+    (tmp_path / "more").mkdir()
+    (tmp_path / "more" / "tex").mkdir()
+    (tmp_path / "more" / "tex" / "red.png").write_bytes(png)
+    with pytest.raises(ValueError, match="several files match"):
+        L.Scene.from_file(str(tmp_path / "scene.obj"), mtllib=str(tmp_path / "scene.mtl"))
+    (tmp_path / "scene.mtl").write_bytes(MTL.replace(b"newmtl red\n", b"newmtl red\nmap_Kd nowhere.png\n"))
+    with pytest.raises(ValueError, match="no file"):
+        L.Scene.from_file(str(tmp_path / "scene.obj"), mtllib=str(tmp_path / "scene.mtl"))
