@@ -1109,7 +1109,7 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
 // the order n = p * G + g on pass set / stream n % K (K >= G).  Unit (g, p) waits for unit (g, p - 1)'s
 // camera before its own, and for its ring before its bounce RR_DEPTH, before any bounce that may
 // run the tail kernel (n_shadow == 1: it takes paths through Russian roulette) and before its film.
-// Set reuse (unit n + K) is ordered by its stream.  The host runs every in-flight unit's bounce
+// Set reuse (unit n + K, started once unit n has issued its ring) is ordered by its stream.  The host runs every in-flight unit's bounce
 // loop (count snapshots `ahead` launches back, as the sequential loop), blocks only on the oldest
 // unit, which never waits for a unit the host has not finished issuing, and enqueues every wait
 // after the record it waits for.  Every per-path operation and every film / ring sum of a task is
@@ -1251,10 +1251,17 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         if (g_timing) resolve_timers(c);
         return LUMO_OK;
     };
+    // unit n reuses the set of unit n - K: it starts once that unit has issued its ring (units of
+    // different groups finish out of order, so a free slot in `act` does not mean a free set)
+    auto set_free = [&](int set) {
+        for (const PS& ps : act)
+            if (ps.set == set) return false;
+        return true;
+    };
     lumo_status e = LUMO_OK;
     while (next < units || !act.empty()) {
         bool progress = false;
-        if ((int)act.size() < K && next < units) {
+        if ((int)act.size() < K && next < units && set_free((int)(next % K))) {
             if ((e = start())) return e;
             progress = true;
         }
