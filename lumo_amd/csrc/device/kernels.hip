@@ -852,6 +852,7 @@ int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per 
 int g_heads = 0;                   // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
 int g_split_pipe = 4;              // split schedule: passes in flight (render_split_pipelined; 1 = sequential)
 int g_split_groups = 2;            // split schedule: independent task groups (render_split_pipelined)
+int g_fused_split = 0;             // fused bounces through render_split_pipelined instead of render_pipelined
 int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
 // allow_top: the kernel has a TOP-staged variant (k_closest_q, k_shadow_q); it is used when the
 // whole scene does not fit in LDS but its top levels were packed at upload (DScene::top).
@@ -1503,7 +1504,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     // that point see empty queues and exit at once.
     const int ahead = c.bounce_ahead;
     const bool fused_now = ns == 1 && (g_fused < 0 ? (g_lds && c.sc.hot_bytes > 0) : g_fused != 0);
-    const bool pipe = !bdpt && fused_now && g_pipeline;
+    const bool pipe = !bdpt && fused_now && g_pipeline && !g_fused_split;
     if (pipe) {
         const lumo_status ps = render_pipelined(c, S, T, D, dump_p, N, (int)n_tasks, dim_stride, max_samples, max_P, st);
         if (ps) return ps;
@@ -1897,6 +1898,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_TOP")) g_top = std::atoi(e);
     if (const char* e = std::getenv("LUMO_SPLIT_PIPE")) g_split_pipe = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("LUMO_SPLIT_GROUPS")) g_split_groups = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("LUMO_FUSED_SPLIT")) g_fused_split = std::atoi(e);
     if (const char* e = std::getenv("LUMO_TOP_KB")) c->top_lds_bytes = std::max(0, std::atoi(e)) * 1024;
     if (const char* e = std::getenv("LUMO_FUSED")) g_fused = std::atoi(e);
     if (const char* e = std::getenv("LUMO_QSORT")) g_qsort = std::atoi(e) & 3;
