@@ -117,6 +117,14 @@ struct DScene {
     const DBvh* onodes_lds;
     const DBvh* lnodes_lds;
     int32_t n_onodes_lds, n_lnodes_lds;
+    // kd stack in LDS (TOP kernels): the first kst_n entries of this thread's kd stack live in LDS
+    // at kst_node[k * kst_stride] / kst_ts[k * kst_stride] (this thread's column), deeper ones in
+    // its scratch array.  kst_n == 0: the whole stack in scratch.
+    int32_t kst_n, kst_stride;
+    int32_t* kst_node;
+    double* kst_ts;
+    int32_t kst_cfg;  // entries per thread the TOP kernels keep in LDS (kst_n of their view; 0 in HBM views)
+    uint32_t top_shm;  // dynamic LDS of a TOP block: the TOP set + the kd stack columns
 };
 
 // TOP view: copy the packed top levels into LDS; the rest of the scene stays in HBM / L2.
@@ -132,6 +140,13 @@ __device__ __forceinline__ DScene stage_top_lds(const DScene& sc, char* lds) {
     v.n_lnodes_lds = sc.top_lnodes;
     v.oitems = reinterpret_cast<const int32_t*>(lds + sc.off_top_oitems);
     v.tobjs = reinterpret_cast<const DObj*>(lds + sc.off_top_tobjs);
+    v.kst_n = sc.kst_cfg;
+    if (sc.kst_cfg > 0) {  // this thread's column of the LDS kd stack, after the TOP set
+        char* base = lds + ((sc.top_bytes + 15u) & ~15u);
+        v.kst_stride = (int32_t)blockDim.x;
+        v.kst_ts = reinterpret_cast<double*>(base) + threadIdx.x;
+        v.kst_node = reinterpret_cast<int32_t*>(base + (size_t)8 * sc.kst_cfg * blockDim.x) + threadIdx.x;
+    }
     return v;
 }
 
@@ -540,6 +555,23 @@ __device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_mi
 #else
 #define KD_INLINE
 #endif
+// kd stack entry k: in this thread's LDS column when k < sc.kst_n (TOP kernels), else in scratch
+__device__ __forceinline__ void kst_push(const DScene& sc, int* st_node, double* st_ts, int k, int node, double t) {
+    if (k < sc.kst_n) {
+        sc.kst_node[k * sc.kst_stride] = node;
+        sc.kst_ts[k * sc.kst_stride] = t;
+    } else {
+        st_node[k] = node;
+        st_ts[k] = t;
+    }
+}
+__device__ __forceinline__ int kst_node(const DScene& sc, const int* st_node, int k) {
+    return k < sc.kst_n ? sc.kst_node[k * sc.kst_stride] : st_node[k];
+}
+__device__ __forceinline__ double kst_t(const DScene& sc, const double* st_ts, int k) {
+    return k < sc.kst_n ? sc.kst_ts[k * sc.kst_stride] : st_ts[k];
+}
+
 template <bool GEO, int STK>
 __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const RayX& r, double t_min, double t_max,
                               int* idx_out, Counters& C) {
@@ -579,8 +611,7 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const 
                 curr = second;
             } else {
                 curr = first;
-                st_node[sp] = second;
-                st_ts[sp] = t_split;
+                kst_push(sc, st_node, st_ts, sp, second, t_split);
                 t_end = t_split;
                 sp++;
             }
@@ -605,9 +636,9 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const 
             }
             if (sp == 0) break;
             sp--;
-            curr = st_node[sp];
-            t_start = st_ts[sp];
-            t_end = sp == 0 ? t_end0 : st_ts[sp - 1];
+            curr = kst_node(sc, st_node, sp);
+            t_start = kst_t(sc, st_ts, sp);
+            t_end = sp == 0 ? t_end0 : kst_t(sc, st_ts, sp - 1);
         } else {
             C.kd++;
             const int ax = axis;
@@ -623,8 +654,7 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const 
                 curr = second;
             } else {
                 curr = first;
-                st_node[sp] = second;
-                st_ts[sp] = t_split;
+                kst_push(sc, st_node, st_ts, sp, second, t_split);
                 t_end = t_split;
                 sp++;
             }

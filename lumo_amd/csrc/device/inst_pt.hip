@@ -92,7 +92,7 @@ void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, c
                   int n, int any_hit, double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
                   unsigned long long* tcount, bool top) {
     if (top)
-        k_trace<STK, true><<<grid, TOP_BLOCK, sc.top_bytes, sm>>>(sc, o, d, light, n, any_hit, t_out, kind_out, obj_out,
+        k_trace<STK, true><<<grid, TOP_BLOCK, sc.top_shm, sm>>>(sc, o, d, light, n, any_hit, t_out, kind_out, obj_out,
                                                                   prim_out, tcount);
     else
         k_trace<STK, false><<<grid, BLOCK, 0, sm>>>(sc, o, d, light, n, any_hit, t_out, kind_out, obj_out, prim_out,

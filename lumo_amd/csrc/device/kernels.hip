@@ -645,6 +645,7 @@ struct Ctx {
     // C3 shadow 438 ms per 8-spp frame at one block per CU vs 446 at four, 817 at half the CUs)
     int top_grid_cap = 256;  // set to the device's CU count at creation (LUMO_TOP_GRID)
     int top_lds_bytes = 160 * 1024 - 256;  // TOP set budget (LUMO_TOP_KB)
+    int kd_lds = 8;  // kd stack entries per thread in LDS in TOP kernels when room is left (LUMO_KD_LDS; C2 frame -3 %)
     int tone_map = LUMO_TONEMAP_NONE;  // of the lumo_render_tiles call in progress
     double tone_arg = 0.0;
     // per-bounce queue-count snapshots (pinned) and their completion events
@@ -867,7 +868,7 @@ void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr, bo
     if (top) {
         l.top = true;
         l.grid = std::min(ceil_div(count, TOP_BLOCK), c.top_grid_cap);
-        l.shm = c.sc.top_bytes;
+        l.shm = c.sc.top_shm;
     }
     by_stack_class(c.sc.stack_class, [&](auto K) { f(K, l); });
 }
@@ -1900,6 +1901,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_SPLIT_GROUPS")) g_split_groups = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("LUMO_FUSED_SPLIT")) g_fused_split = std::atoi(e);
     if (const char* e = std::getenv("LUMO_TOP_KB")) c->top_lds_bytes = std::max(0, std::atoi(e)) * 1024;
+    if (const char* e = std::getenv("LUMO_KD_LDS")) c->kd_lds = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("LUMO_FUSED")) g_fused = std::atoi(e);
     if (const char* e = std::getenv("LUMO_QSORT")) g_qsort = std::atoi(e) & 3;
     if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -2258,6 +2260,15 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
             }
             s.top = dp;
             s.top_bytes = (uint32_t)top.size();
+        }
+        // kd stack entries per thread in LDS after the TOP set (TOP_BLOCK threads, 12 B each)
+        s.kst_n = 0;
+        s.kst_cfg = 0;
+        s.top_shm = (s.top_bytes + 15u) & ~15u;
+        if (s.top_bytes > 0 && c->kd_lds > 0) {
+            const size_t room = (size_t)(160 * 1024) - s.top_shm;
+            s.kst_cfg = (int32_t)std::min<size_t>((size_t)c->kd_lds, room / (12 * (size_t)TOP_BLOCK));
+            s.top_shm += (uint32_t)(12 * (size_t)TOP_BLOCK * s.kst_cfg);
         }
     }
     int n = d->num_lights, lg = 0;
