@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define LUMO_ABI_VERSION 6
+#define LUMO_ABI_VERSION 7
 
 typedef int32_t lumo_status;
 enum {
@@ -400,6 +400,12 @@ void lumo_set_lds_staging(int on);
  * Every mode gives bit-identical results.
  * Also LUMO_FUSED / LUMO_TAIL / LUMO_PIPELINE in the environment. */
 void lumo_set_bounce_mode(int fused, uint32_t tail_below, int pipeline);
+/* Perf switch (bidirectional path tracer): once fewer than 4 * below subpaths of a walk are alive
+ * the host launches a walk-tail kernel ahead of each bounce; when fewer than `below` are alive (the
+ * exact count, read on the device) it runs every remaining light / camera subpath to its end in
+ * that launch and the bounce kernels skip (below = 0: never; default 65536).  Bit-identical.
+ * Also LUMO_BDPT_TAIL in the environment. */
+void lumo_set_bdpt_tail(uint32_t below);
 
 #ifdef __cplusplus
 }

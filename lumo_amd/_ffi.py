@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 6  # include/lumo_amd.h LUMO_ABI_VERSION
+ABI_VERSION = 7  # include/lumo_amd.h LUMO_ABI_VERSION
 LIB_PATH = os.environ.get("LUMO_AMD_LIB") or os.path.join(_HERE, "liblumo_amd.so")
 
 c_double_p = C.POINTER(C.c_double)
@@ -193,6 +193,7 @@ DEVICE_API = [
     ("lumo_set_timing", None, [C.c_int]),
     ("lumo_set_lds_staging", None, [C.c_int]),
     ("lumo_set_bounce_mode", None, [C.c_int, C.c_uint32, C.c_int]),
+    ("lumo_set_bdpt_tail", None, [C.c_uint32]),
     ("lumo_debug_stream", C.c_int32, [C.c_void_p, C.c_size_t]),
     ("lumo_scene_info", C.c_int32, [C.c_void_p, C.POINTER(SceneInfo)]),
     ("lumo_debug_set_integrator", C.c_int32, [C.c_void_p, C.c_int]),

@@ -4,12 +4,11 @@
 // A BDPT sample (bd_path_trace.rs:23-74) runs as a wavefront: the light subpaths of all slots
 // bounce through k_closest + k_bdpt_step, then the camera subpaths; k_bdpt_conn then evaluates
 // every (s, t) strategy of every sample as its own work item (visibility, MIS weight,
-// contribution) and k_bdpt_fold adds the contributions in lumo's order.  Subpath vertices live in HBM,
-// structure-of-arrays by vertex index (lanes of a wave walk the same depth together, so vertex
-// reads and writes coalesce).  Light-tracing connections (t = 1) produce splats, kept per slot in
-// generation order and turned into film taps by k_bdpt_taps.  Everything follows the oracle's
-// restatement (oracle/src/oracle.cpp, "BDPT") operation for operation, so results are
-// bit-identical to it.
+// contribution) and k_bdpt_fold adds the contributions in lumo's order.  Subpath vertices live in
+// HBM by vertex index and slot, each vertex's fields contiguous (VStore).  Light-tracing
+// connections (t = 1) produce splats, kept per slot in generation order and turned into film taps
+// by k_bdpt_taps.  Everything follows the oracle's restatement (oracle/src/oracle.cpp, "BDPT")
+// operation for operation, so results are bit-identical to it.
 //
 // Reference: bd_path_trace.rs:23-290, bd_path_trace/{path_gen.rs:4-157, mis.rs:4-239,
 // vertex.rs:1-162, measure.rs}, camera.rs:170-388, object.rs:99-126.
@@ -37,13 +36,25 @@ struct BVtx {
     bool del = false;  // stored flag only (walk vertices); v_is_delta recomputes it
 };
 
-// Vertex storage of one subpath kind: field f of vertex v of slot s at ((f * V + v) * N + s).
+// Vertex storage of one subpath kind.  LUMO_VSTORE_AOS (default): the fields of vertex v of slot s
+// are contiguous, at ((v * N + s) * VD_N + f): a walk's wave writes vertex v of consecutive slots
+// (one contiguous range), and a connection item, which reads whole vertices of its own slot, pulls
+// 184 contiguous bytes per vertex instead of one cache line per field.  Otherwise field-major,
+// ((f * V + v) * N + s).
+#ifndef LUMO_VSTORE_AOS
+#define LUMO_VSTORE_AOS 1
+#endif
 struct VStore {
     double* d;
     int32_t* i;
     int V, N;
+#if LUMO_VSTORE_AOS
+    __device__ __forceinline__ double& D(int f, int v, int s) const { return d[((size_t)v * N + s) * VD_N + f]; }
+    __device__ __forceinline__ int32_t& I(int f, int v, int s) const { return i[((size_t)v * N + s) * VI_N + f]; }
+#else
     __device__ __forceinline__ double& D(int f, int v, int s) const { return d[((size_t)f * V + v) * N + s]; }
     __device__ __forceinline__ int32_t& I(int f, int v, int s) const { return i[((size_t)f * V + v) * N + s]; }
+#endif
     __device__ void store(int v, int s, const BVtx& x) const {
         const V3* vs[5] = {&x.p, &x.err, &x.ns, &x.ng, &x.wo};
         for (int k = 0; k < 5; ++k) {
@@ -844,8 +855,10 @@ __device__ void bdpt_step_one(const DScene& sc, const Paths& S, const Tasks& T, 
 }
 template <int STK, int FX>
 __global__ __launch_bounds__(BLOCK, LUMO_BDPT_STEP_WAVES) void k_bdpt_step(DScene sc, Paths S, Tasks T, Bdpt B, BItems I,
-                                                                       int mode, const int32_t* queue, int32_t* next_queue) {
+                                                                       int mode, const int32_t* queue, int32_t* next_queue,
+                                                                       uint32_t tail_below) {
     const uint32_t count = S.counts[CNT_CUR];
+    if (count < tail_below) return;  // k_bdpt_tail took this bounce
     Counters C{0, 0, 0};
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
         const uint32_t q = base + threadIdx.x;
@@ -858,6 +871,66 @@ __global__ __launch_bounds__(BLOCK, LUMO_BDPT_STEP_WAVES) void k_bdpt_step(DScen
         block_append(alive, slot, next_queue, S.counts + CNT_NEXT);
     }
     flush_counters(C, S.tcount);
+}
+
+// Walk tail: launched ahead of k_closest + k_bdpt_step once few subpaths are alive; when fewer
+// than tail_below are (the exact count, read here), each lane runs its subpath to its end, one
+// (closest hit, step) pair after the other, exactly as the two kernels would bounce by bounce
+// (the same per-slot reads and writes), and takes the next queued subpath when it ends (one
+// fetch atomic per wave and round).  The two kernels, given the same threshold, skip the bounce;
+// the next queue stays empty, so the host's bounce loop ends.  Bit-identical: a walk does not
+// depend on other walks.  The closest queries after each subpath's first are added to TC_TAILQ.
+template <int STK, bool LDS, int FX>
+__global__ __launch_bounds__(BLOCK, LUMO_BDPT_STEP_WAVES) void k_bdpt_tail(DScene sc0, Paths S, Tasks T, Bdpt B,
+                                                                       BItems I, int mode, const int32_t* queue,
+                                                                       uint32_t tail_below) {
+    extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+    const uint32_t count = S.counts[CNT_CUR];
+    if (count >= tail_below) return;  // the bounce kernels take this bounce
+    if (count <= blockIdx.x * blockDim.x) return;  // before staging: whole block idle
+    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    Counters C{0, 0, 0};
+    uint32_t tailq = 0;
+    int slot = -1;
+    bool have = false, more = true, first = true;
+    for (;;) {
+        if (more) {
+            const uint64_t need = __ballot(!have);
+            if (need) {
+                const int lead = __ffsll((unsigned long long)need) - 1;
+                const uint32_t n_need = (uint32_t)__popcll(need);
+                uint32_t b = 0;
+                if (lane_id() == lead) b = atomicAdd(S.counts + CNT_FETCH_T, n_need);
+                b = __shfl(b, lead, 64);
+                if (b + n_need >= count) more = false;
+                if (!have) {
+                    const uint32_t q = b + mbcnt64(need);
+                    if (q < count) {
+                        slot = queue[q];
+                        have = true;
+                        first = true;
+                    }
+                }
+            }
+        }
+        if (__ballot(have) == 0) break;
+        if (have) {
+            const RayX r = rayx(Ray{ldv3(S.ro, slot), ldv3(S.rd, slot)});  // k_closest
+            const HitRef h = scene_hit<STK, FX>(sc, r, C);
+            S.hit_t[slot] = h.t;
+            S.hit_kind[slot] = h.kind;
+            S.hit_obj[slot] = h.obj;
+            S.hit_tri[slot] = h.tri;
+            S.queries[slot] += 1;
+            if (!first) tailq++;
+            first = false;
+            bool alive = false;
+            bdpt_step_one<STK, FX>(sc, S, T, B, I, mode, slot, alive, C);
+            have = alive;
+        }
+    }
+    flush_counters(C, S.tcount);
+    flush_resolved(tailq, S.tcount + TC_TAILQ);
 }
 
 // The same two walks in one thread (path_gen.rs as written), from the slot's saved start state

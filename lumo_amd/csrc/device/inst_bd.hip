@@ -11,10 +11,11 @@ namespace dev {
 
 template <int STK>
 void launch_bdpt_step(int grid, hipStream_t sm, int fx, const DScene& sc, const Paths& S, const Tasks& T,
-                      const Bdpt& B, const BItems& I, int mode, const int32_t* queue, int32_t* next_queue) {
-    if (fx == 2) k_bdpt_step<STK, 2><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue);
-    else if (fx) k_bdpt_step<STK, 1><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue);
-    else k_bdpt_step<STK, 0><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue);
+                      const Bdpt& B, const BItems& I, int mode, const int32_t* queue, int32_t* next_queue,
+                      uint32_t tail_below) {
+    if (fx == 2) k_bdpt_step<STK, 2><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue, tail_below);
+    else if (fx) k_bdpt_step<STK, 1><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue, tail_below);
+    else k_bdpt_step<STK, 0><<<grid, BLOCK, 0, sm>>>(sc, S, T, B, I, mode, queue, next_queue, tail_below);
 }
 
 #define LUMO_TRAV_LAUNCH(KERNEL, ...)                                                        \
@@ -29,6 +30,12 @@ void launch_bdpt_step(int grid, hipStream_t sm, int fx, const DScene& sc, const 
             else KERNEL<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(__VA_ARGS__);        \
         }                                                                                    \
     } while (0)
+
+template <int STK>
+void launch_bdpt_tail(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const Bdpt& B,
+                      const BItems& I, int mode, const int32_t* queue, uint32_t tail_below) {
+    LUMO_TRAV_LAUNCH(k_bdpt_tail, sc, S, T, B, I, mode, queue, tail_below);
+}
 
 template <int STK>
 void launch_bdpt_redo(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const DCam& cam,
@@ -49,7 +56,9 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
 }
 
 template void launch_bdpt_step<LUMO_STK>(int, hipStream_t, int, const DScene&, const Paths&, const Tasks&,
-                                         const Bdpt&, const BItems&, int, const int32_t*, int32_t*);
+                                         const Bdpt&, const BItems&, int, const int32_t*, int32_t*, uint32_t);
+template void launch_bdpt_tail<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Tasks&, const Bdpt&,
+                                         const BItems&, int, const int32_t*, uint32_t);
 template void launch_bdpt_redo<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Tasks&, const DCam&,
                                          const Bdpt&, const Bdpt&, const BItems&);
 template void launch_bdpt_trace_a<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const DCam&, const Bdpt&,

@@ -11,13 +11,13 @@ namespace lumo {
 namespace dev {
 
 template <int STK>
-void launch_closest(const TravLaunch& l, const DScene& sc, const Paths& S, const int32_t* queue) {
+void launch_closest(const TravLaunch& l, const DScene& sc, const Paths& S, const int32_t* queue, uint32_t tail_below) {
     if (l.lds) {
-        if (l.fx) k_closest<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, queue);
-        else k_closest<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, queue);
+        if (l.fx) k_closest<STK, true, true><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, queue, tail_below);
+        else k_closest<STK, true, false><<<l.grid, BLOCK, l.shm, l.sm>>>(sc, S, queue, tail_below);
     } else {
-        if (l.fx) k_closest<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, queue);
-        else k_closest<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, queue);
+        if (l.fx) k_closest<STK, false, true><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, queue, tail_below);
+        else k_closest<STK, false, false><<<l.grid, BLOCK, 0, l.sm>>>(sc, S, queue, tail_below);
     }
 }
 
@@ -99,7 +99,7 @@ void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, c
                                                     tcount);
 }
 
-template void launch_closest<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const int32_t*);
+template void launch_closest<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const int32_t*, uint32_t);
 template void launch_closest_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const QState&, uint32_t);
 template void launch_shadow_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const QState&);
 template void launch_bounce_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Tasks&, const QState&,

@@ -287,15 +287,13 @@ __device__ __forceinline__ void count_checks(int cat, unsigned long long* dst) {
     }
 }
 
+// (the sample's luminance and cost for the adaptive-RR ring are k_ring's, from the same values)
 __device__ __forceinline__ V3 finish_one(const DScene& sc, const Paths& S, const DCam& cam, int s, uint32_t pass,
                                          const Dump& dump, int dump_p, int tone_map, double tone_arg) {
     double L[NS];
     for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * s + i];
     const DColor c = ldc(S.rad, s);
-    const double lum = luminance(sc, c, L);
     const V3 rgb = sample_rgb(sc, cam, c, L, tone_map, tone_arg);
-    S.p_lum[s] = lum;
-    S.p_cost[s] = S.depth[s];
     if (dump.rad) {
         const size_t o = (size_t)pass * dump_p + S.pix[s];
         for (int i = 0; i < NS; ++i) {
@@ -456,7 +454,8 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S, Tasks
 // `zero_counts` (when set): the pass's queue counters, zeroed by block 0 for the next pass that
 // uses them (every kernel of the pass that reads them precedes the ring on its stream), so a pass
 // starts without a fill of its own.
-__global__ __launch_bounds__(64) void k_ring(Paths S, Tasks T, int n_tasks, int update, uint32_t* zero_counts, int t0) {
+__global__ __launch_bounds__(64) void k_ring(DScene sc, Paths S, Tasks T, int n_tasks, int update, uint32_t* zero_counts,
+                                             int t0) {
     const int ti = t0 + (int)blockIdx.x;  // tasks [t0, n_tasks)
     if (ti >= n_tasks) return;
     const int lane = threadIdx.x;
@@ -479,12 +478,13 @@ __global__ __launch_bounds__(64) void k_ring(Paths S, Tasks T, int n_tasks, int 
         unsigned long long rays = 0, q = 0;
         for (int j = lane; j < P; j += 64) {
             const int sl = f0 + j;
-            rays += S.p_cost[sl];
+            const uint32_t cost = S.depth[sl];  // sample.cost
+            rays += cost;
             q += S.queries[sl];
             if (j + n >= P) {
                 const int r = (int)((ptr + (uint32_t)j) % (uint32_t)n);
-                lum[r] = S.p_lum[sl];
-                cst[r] = S.p_cost[sl];
+                lum[r] = luminance(sc, ldc(S.rad, sl), S.lam + 4 * (size_t)sl);  // sample.color.luminance(&lambda)
+                cst[r] = cost;
             }
         }
         for (int off = 32; off > 0; off >>= 1) {
@@ -629,10 +629,11 @@ struct DevBuf {
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;  // pipelined passes: each pass's tail, film and ring
+    hipStream_t stream2 = nullptr;  // pipelined passes: each pass's tail and ring
     hipStream_t stream3 = nullptr;  // pipelined passes (2-3 head streams): further head streams
     hipStream_t stream4 = nullptr;
-    hipEvent_t pass_ev[4] = {}, tail_ev[4] = {}, cam_ev[4] = {};
+    hipStream_t stream5 = nullptr;  // pipelined passes: each pass's film, off the ring's chain
+    hipEvent_t pass_ev[4] = {}, tail_ev[4] = {}, cam_ev[4] = {}, film_ev[4] = {}, done_ev[4] = {};
     bool has_scene = false, has_camera = false;
     DScene sc{};
     DCam cam{};
@@ -704,7 +705,7 @@ int ceil_div(uint64_t a, uint64_t b) { return (int)((a + b - 1) / b); }
 enum WorkId {
     W_RO, W_RD, W_GATH, W_RAD, W_LAM, W_RASTER, W_RNG, W_DEPTH, W_FLAGS, W_QUERIES, W_TASK, W_PIX, W_PSEED, W_MJRNG,
     W_MJSTATE, W_PERM, W_HIT_T, W_HIT_KIND, W_HIT_OBJ, W_HIT_TRI, W_SH_O, W_SH_D, W_SH_F, W_SH_PSCT, W_SH_COS,
-    W_SH_OUT, W_SH_LIGHT, W_SH_FLAGS, W_G_SH, W_PDF_L, W_P_RGB, W_P_LUM, W_P_COST, W_P_VALID, W_FILM, W_Q0, W_Q1,
+    W_SH_OUT, W_SH_LIGHT, W_SH_FLAGS, W_G_SH, W_PDF_L, W_P_RGB, W_P_VALID, W_FILM, W_Q0, W_Q1,
     W_SQ, W_RQ, W_COUNTS, W_TCOUNT, W_TASKS, W_FIRST, W_RING_COST, W_RING_LUM, W_RING_PTR, W_DELTA, W_NUM_RAYS,
     W_TQUERIES, W_DUMP_RAD, W_DUMP_LAM, W_DUMP_RASTER, W_DUMP_DEPTH, W_DUMP_DELTA,
     W_BD_LD, W_BD_LI, W_BD_CD, W_BD_CI, W_BD_SP, W_BD_SPN, W_BD_OVF, W_BD_CNT, W_BD_OFF, W_BD_RANGES, W_BD_TAPS,
@@ -849,6 +850,10 @@ int g_fused = -1;  // n_shadow == 1: k_bounce_q instead of closest / shade / sha
 uint32_t g_tail_below = 1u << 18;  // n_shadow == 1: k_bounce_q tail mode below this many live paths
 int g_pipeline = 3;                // fused passes overlapped (render_pipelined): 0 off, else the number of head streams (1-3)
 int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from a counter
+int g_tail_refill = 0;             // tail kernel: lanes refill one path at a time (else 64 per wave)
+int g_pipe_groups = 1;             // pipelined fused passes: independent task groups (1 or 2)
+uint32_t g_bdpt_tail = 1u << 16;    // BDPT walks: k_bdpt_tail below this many live subpaths (0: never)
+int g_film_mode = 2;               // pipelined fused passes: film 0 before the ring, 1 after it (both on the tail stream), 2 own stream
 int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
 int g_heads = 0;                   // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
 int g_split_pipe = 4;              // split schedule: passes in flight (render_split_pipelined; 1 = sequential)
@@ -925,12 +930,20 @@ size_t split_set_bytes(const Paths& S, int N, int ns) {
 // per-slot outputs; every per-path operation and every film / ring sum is the same as in the
 // sequential loop, so the result is bit-identical.
 lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump_p, int N, int n_tasks, int dim_stride,
-                             uint64_t max_samples, uint64_t max_P, lumo_status& st) {
-    // NA head streams (1 to 3, g_pipeline): with more than one, the first bounces of consecutive
-    // passes also run concurrently (filling the GPU when a rank holds few slots); NSETS = NA + 1
-    // sets of queues, counters and per-slot outputs, so a set is reused only after the pass
-    // NSETS back has finished its film.
-    const int NA = std::min(std::max(g_pipeline, 1), 3), NSETS = NA + 1;
+                             uint64_t max_samples, uint64_t max_P, const std::vector<int32_t>& first, int G,
+                             lumo_status& st) {
+    // G independent task groups (G = 1: the whole frame): the tasks are cut into G groups of
+    // consecutive tasks whose pass chains are independent (a task's delta needs only its own
+    // previous pass, task.rs:28-53; the sampler state is per slot), units (group g, pass p) are
+    // issued in the order n = p * G + g, and each group hands its units' tails to its own stream,
+    // so one group's latency-bound tail kernel, film and ring overlap the other's.  NA head
+    // streams (G = 1: 1 to 3, g_pipeline; G = 2: 2) run the units' cameras and first bounces; with
+    // more than one, consecutive units' first bounces also run concurrently (filling the GPU when
+    // a rank holds few slots).  NSETS = 4 sets of queues, counters and per-slot outputs (G = 1 with
+    // NA head streams: NA + 1), so a set is reused only after the unit NSETS back has issued its ring.
+    G = std::max(1, std::min(G, std::min(2, n_tasks)));
+    if (D.delta || D.rad) G = 1;  // debug dumps follow one pass chain
+    const int NA = G == 1 ? std::min(std::max(g_pipeline, 1), 3) : 2, NSETS = G == 1 ? NA + 1 : 4;
     // On an error return, work already queued on the other streams may still use the buffers the
     // next call re-initialises on stream 0: drain every stream before reporting the error.
     struct JoinOnError {
@@ -938,18 +951,30 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         bool ok = false;
         ~JoinOnError() {
             if (ok) return;
-            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream})
+            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream5, c.stream})
                 if (s) (void)hipStreamSynchronize(s);
         }
     } join{c};
+    // groups of consecutive tasks, about N / G slots each
+    std::vector<int> t_lo(G), t_hi(G);
+    for (int g = 0, t = 0; g < G; ++g) {
+        t_lo[g] = t;
+        const int64_t target = (int64_t)N * (g + 1) / G;
+        while (t < n_tasks && (g == G - 1 || first[t + 1] <= target || t == t_lo[g])) ++t;
+        t = std::max(std::min(t, n_tasks - (G - 1 - g)), t_lo[g] + 1);
+        t_hi[g] = t;
+    }
     Paths P3[4] = {S, S, S, S};
     for (int k = 1; k < NSETS; ++k) alloc_pass_set(c, P3[k], k, N, st);
     if (st) return st;
-    hipStream_t As[3] = {c.stream, c.stream3, c.stream4}, B = c.stream2;
+    hipStream_t As[3] = {c.stream, c.stream3, c.stream4};
+    hipStream_t Bs[2] = {c.stream2, c.stream4}, F = c.stream5;
+    if (G == 2) As[1] = c.stream3;
     // every event starts "done" after the setup enqueued on stream 0 (tasks, memsets, the initial
-    // ring): pass p waits for pass p - NSETS's film before reusing its set, for pass p - 1's camera
-    // (the sampler state is per slot) and, before bounce RR_DEPTH, for pass p - 1's ring
-    // each set's counters start zeroed; from then on every pass's ring zeroes its set's counters
+    // ring): unit n waits for unit n - NSETS's ring before reusing its set, for its group's
+    // previous camera (the sampler state is per slot) and, before bounce RR_DEPTH, for its
+    // group's previous ring.  Every wait is enqueued after the record it waits for (NSETS > G).
+    // each set's counters start zeroed; from then on every unit's ring zeroes its set's counters
     {
         ZeroList z;
         for (int k = 1; k < NSETS; ++k) z.add(P3[k].counts, sizeof(uint32_t) * CNT_N);
@@ -958,22 +983,28 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
     for (int k = 0; k < 4; ++k) {
         HIPCHK(hipEventRecord(c.pass_ev[k], As[0]));
         HIPCHK(hipEventRecord(c.cam_ev[k], As[0]));
+        HIPCHK(hipEventRecord(c.film_ev[k], As[0]));
     }
-    const int gN = ceil_div(N, BLOCK);
-    // bounces 0..heads-1 on the head stream: through the RR bounce when a pass holds many paths;
-    // with few (a rank's share of a multi-GPU run) the RR bounce goes to the tail kernel too, so
-    // the head stream never waits for the previous pass's ring (362^2: 509 -> 434 ms per frame)
-    const int heads = g_heads > 0 ? g_heads : (N >= (1 << 21) ? RR_DEPTH + 1 : RR_DEPTH);
-    for (uint64_t pass = 0; pass < max_samples; ++pass) {
-        const int set = (int)(pass % NSETS), prev = (int)((pass + NSETS - 1) % NSETS);
-        hipStream_t A = As[pass % NA];
+    const uint64_t units = max_samples * (uint64_t)G;
+    for (uint64_t n = 0; n < units; ++n) {
+        const int g = (int)(n % G);
+        const uint64_t pass = n / G;
+        const int set = (int)(n % NSETS), prev = (int)((n + NSETS - G) % NSETS);  // prev: unit n - G
+        const int t0 = t_lo[g], t1 = t_hi[g], s0 = first[t0], s1 = first[t1], Nu = s1 - s0;
+        hipStream_t A = As[n % NA], B = Bs[g];
         Paths& P = P3[set];
+        // bounces 0..heads-1 on the head stream: through the RR bounce when a unit holds many
+        // paths; with few (a rank's share of a multi-GPU run) the RR bounce goes to the tail kernel
+        // too, so the head stream never waits for the previous pass's ring (362^2: 509 -> 434 ms)
+        const int heads = g_heads > 0 ? g_heads : (Nu >= (1 << 21) ? RR_DEPTH + 1 : RR_DEPTH);
+        const int gN = ceil_div(Nu, BLOCK);
         // ---- head stream: camera + the first bounces
-        HIPCHK(hipStreamWaitEvent(A, c.pass_ev[set], 0));  // pass - NSETS done with this set (its ring zeroed the counters)
-        if (NA > 1) HIPCHK(hipStreamWaitEvent(A, c.cam_ev[prev], 0));  // pass - 1's camera (sampler state)
+        HIPCHK(hipStreamWaitEvent(A, c.pass_ev[set], 0));  // unit n - NSETS done with this set (its ring zeroed the counters)
+        HIPCHK(hipStreamWaitEvent(A, c.film_ev[set], 0));  // ... and its film
+        if (NA > 1 || G > 1) HIPCHK(hipStreamWaitEvent(A, c.cam_ev[prev], 0));  // the group's previous camera
         {
             StageTimer tm(c, g_timing, ST_CAMERA, A);
-            k_camera<true><<<gN, BLOCK, 0, A>>>(T, P, c.cam, N, dim_stride, (uint32_t)pass, 0);
+            k_camera<true><<<gN, BLOCK, 0, A>>>(T, P, c.cam, s1, dim_stride, (uint32_t)pass, s0);
         }
         HIPCHK(hipEventRecord(c.cam_ev[set], A));
         for (int b = 0; b < heads; ++b) {
@@ -981,7 +1012,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
             k_bounce_begin<<<1, 64, 0, A>>>(P.counts, P.tcount + TC_HEADQ);
             StageTimer tm(c, g_timing, ST_CLOSEST, A);
             launch_trav(
-                c, (uint64_t)N,
+                c, (uint64_t)Nu,
                 [&](auto K, const TravLaunch& l) {
                     launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[b & 1], P.qs[(b + 1) & 1], 0u, false,
                                                         g_dyn, g_bounce_threads);
@@ -990,42 +1021,63 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.tail_ev[set], A));
-        // ---- stream B: the rest of the pass, film, ring
+        // ---- the group's stream: the rest of the pass, film, ring
         HIPCHK(hipStreamWaitEvent(B, c.tail_ev[set], 0));
+        if (G > 1) HIPCHK(hipStreamWaitEvent(B, c.pass_ev[prev], 0));  // the group's previous ring (the tail takes paths through RR)
         if (D.delta) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, B));
         k_bounce_begin<<<1, 64, 0, B>>>(P.counts, P.tcount + TC_HEADQ);
         {
             StageTimer tm(c, g_timing, ST_RESOLVE, B);
             launch_trav(
-                c, (uint64_t)N,
+                c, (uint64_t)Nu,
                 [&](auto K, const TravLaunch& l) {
                     launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[heads & 1], P.qs[(heads + 1) & 1],
-                                                        0xffffffffu, true, 0, BLOCK);
+                                                        0xffffffffu, true, g_tail_refill, BLOCK);
                 },
                 B);
         }
-        if (max_P <= BLOCK) {
-            StageTimer tm(c, g_timing, ST_FILM, B);
-            k_finish_film<<<n_tasks, BLOCK, 0, B>>>(c.sc, P, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
-                                                    c.tone_arg, 0);
-        } else {
-            {
-                StageTimer tm(c, g_timing, ST_FINISH, B);
-                k_finish<<<gN, BLOCK, 0, B>>>(c.sc, P, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg, 0);
+        auto film = [&](hipStream_t fs) -> lumo_status {
+            if (max_P <= BLOCK) {
+                StageTimer tm(c, g_timing, ST_FILM, fs);
+                k_finish_film<<<t1 - t0, BLOCK, 0, fs>>>(c.sc, P, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
+                                                         c.tone_arg, t0);
+            } else {
+                {
+                    StageTimer tm(c, g_timing, ST_FINISH, fs);
+                    k_finish<<<gN, BLOCK, 0, fs>>>(c.sc, P, c.cam, s1, (uint32_t)pass, D, dump_p, c.tone_map,
+                                                   c.tone_arg, s0);
+                }
+                StageTimer tm(c, g_timing, ST_FILM, fs);
+                k_film<<<gN, BLOCK, 0, fs>>>(P, T, c.cam, s1, s0);
             }
-            StageTimer tm(c, g_timing, ST_FILM, B);
-            k_film<<<gN, BLOCK, 0, B>>>(P, T, c.cam, N, 0);
-        }
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(c.film_ev[set], fs));
+            return LUMO_OK;
+        };
+        // the ring computes the samples' luminance itself, so it need not follow the film:
+        // g_film_mode 0: film then ring on B; 1: ring then film on B; 2: the film on its own
+        // stream F (in pass order), off the chain that Russian roulette of the next pass waits on
+        lumo_status fe = LUMO_OK;
+        if (g_film_mode == 0 && (fe = film(B))) return fe;
+        HIPCHK(hipEventRecord(c.done_ev[set], B));
         {
             StageTimer tm(c, g_timing, ST_RING, B);
-            k_ring<<<n_tasks, 64, 0, B>>>(P, T, n_tasks, 1, P.counts, 0);
+            k_ring<<<t1 - t0, 64, 0, B>>>(c.sc, P, T, t1, 1, P.counts, t0);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.pass_ev[set], B));
+        if (g_film_mode == 1 && (fe = film(B))) return fe;
+        if (g_film_mode == 2) {
+            HIPCHK(hipStreamWaitEvent(F, c.done_ev[set], 0));
+            if ((fe = film(F))) return fe;
+        }
         if (g_timing) resolve_timers(c);
     }
-    // the results are copied on stream 0: after the last pass's ring
-    HIPCHK(hipStreamWaitEvent(As[0], c.pass_ev[(max_samples - 1) % NSETS], 0));
+    // the results are copied on stream 0: after every set's last unit
+    for (int k = 0; k < NSETS; ++k) {
+        HIPCHK(hipStreamWaitEvent(As[0], c.pass_ev[k], 0));
+        HIPCHK(hipStreamWaitEvent(As[0], c.film_ev[k], 0));
+    }
     join.ok = true;
     return LUMO_OK;
 }
@@ -1045,7 +1097,7 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
     if (skip > 0) {
         StageTimer tm(c, g_timing, ST_RESOLVE, sm);
         launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
-            launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true, 0, BLOCK);
+            launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true, g_tail_refill, BLOCK);
         }, sm);
     }
     if (fused_now) {  // one fused kernel per bounce (pt.h k_bounce_q)
@@ -1124,7 +1176,7 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         bool ok = false;
         ~JoinOnError() {
             if (ok) return;
-            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream})
+            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream5, c.stream})
                 if (s) (void)hipStreamSynchronize(s);
         }
     } join{c};
@@ -1151,7 +1203,10 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         for (int k = 1; k < K; ++k) z.add(P[k].counts, sizeof(uint32_t) * CNT_N);
         if (z.n) k_zero_list<<<1, BLOCK, 0, Ss[0]>>>(z);
     }
-    for (int k = 0; k < 4; ++k) HIPCHK(hipEventRecord(c.pass_ev[k], Ss[0]));
+    for (int k = 0; k < 4; ++k) {
+        HIPCHK(hipEventRecord(c.pass_ev[k], Ss[0]));
+        HIPCHK(hipEventRecord(c.film_ev[k], Ss[0]));
+    }
     const int SEG = Ctx::SNAP_RING / 4;  // snapshot slots per set
     const int ahead = std::max(1, std::min(c.bounce_ahead, SEG - 1));
     struct PS {
@@ -1224,12 +1279,22 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         }
         return LUMO_OK;
     };
-    auto finish = [&](PS& ps) -> lumo_status {  // film + ring of the group's tasks
+    auto finish = [&](PS& ps) -> lumo_status {  // ring + film of the group's tasks
         hipStream_t sm = Ss[ps.set];
         Paths& Q = P[ps.set];
         const lumo_status w = wait_prev(ps);
         if (w) return w;
         const int t0 = t_lo[ps.g], t1 = t_hi[ps.g], s0 = first[t0], s1 = first[t1];
+        // the ring (task.rs:28-69, from the pass's final radiance) first: the group's next pass
+        // waits only for it; the film follows on this stream, after the group's previous film
+        // (the film accumulates in pass order)
+        {
+            StageTimer tm(c, g_timing, ST_RING, sm);
+            k_ring<<<t1 - t0, 64, 0, sm>>>(c.sc, Q, T, t1, 1, Q.counts, t0);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c.pass_ev[ps.set], sm));
+        if (ps.pass > 0) HIPCHK(hipStreamWaitEvent(sm, c.film_ev[(ps.unit - G) % K], 0));
         if (max_P <= BLOCK) {
             StageTimer tm(c, g_timing, ST_FILM, sm);
             k_finish_film<<<t1 - t0, BLOCK, 0, sm>>>(c.sc, Q, T, c.cam, (uint32_t)ps.pass, Dump{}, 0, c.tone_map,
@@ -1243,12 +1308,8 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
             StageTimer tm(c, g_timing, ST_FILM, sm);
             k_film<<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(Q, T, c.cam, s1, s0);
         }
-        {
-            StageTimer tm(c, g_timing, ST_RING, sm);
-            k_ring<<<t1 - t0, 64, 0, sm>>>(Q, T, t1, 1, Q.counts, t0);
-        }
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(c.pass_ev[ps.set], sm));
+        HIPCHK(hipEventRecord(c.film_ev[ps.set], sm));
         finished[ps.g] = ps.pass + 1;
         if (g_timing) resolve_timers(c);
         return LUMO_OK;
@@ -1293,7 +1354,10 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         }
     }
     // the results are copied on stream 0: after every set's last unit
-    for (int k = 1; k < K; ++k) HIPCHK(hipStreamWaitEvent(Ss[0], c.pass_ev[k], 0));
+    for (int k = 1; k < K; ++k) {
+        HIPCHK(hipStreamWaitEvent(Ss[0], c.pass_ev[k], 0));
+        HIPCHK(hipStreamWaitEvent(Ss[0], c.film_ev[k], 0));
+    }
     join.ok = true;
     return LUMO_OK;
 }
@@ -1380,8 +1444,6 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         S.sq.hr = ns > 1 ? wbuf<uint64_t>(c, W_SQ_HR, 2 * S.sq.hcap, st) : nullptr;
     }
     S.p_rgb = wbuf<double>(c, W_P_RGB, 3 * (size_t)N, st);
-    S.p_lum = wbuf<double>(c, W_P_LUM, N, st);
-    S.p_cost = wbuf<uint32_t>(c, W_P_COST, N, st);
     S.p_valid = wbuf<uint32_t>(c, W_P_VALID, N, st);
     S.film = wbuf<double>(c, W_FILM, 4 * (size_t)N, st);
     S.counts = wbuf<uint32_t>(c, W_COUNTS, CNT_N, st);
@@ -1493,7 +1555,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     const int gT = ceil_div(n_tasks, BLOCK), gN = ceil_div(N, BLOCK);
     k_init_seeds<<<gT, BLOCK, 0, sm>>>(T, S, (int)n_tasks);
     k_init_mj<<<gN, BLOCK, 0, sm>>>(T, S, N, dim_stride);
-    k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 0, nullptr, 0);
+    k_ring<<<(int)n_tasks, 64, 0, sm>>>(c.sc, S, T, (int)n_tasks, 0, nullptr, 0);
     HIPCHK(hipGetLastError());
 
     uint64_t bounces = 0, closest_q = 0, shadow_q = 0;
@@ -1507,7 +1569,8 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     const bool fused_now = ns == 1 && (g_fused < 0 ? (g_lds && c.sc.hot_bytes > 0) : g_fused != 0);
     const bool pipe = !bdpt && fused_now && g_pipeline && !g_fused_split;
     if (pipe) {
-        const lumo_status ps = render_pipelined(c, S, T, D, dump_p, N, (int)n_tasks, dim_stride, max_samples, max_P, st);
+        const lumo_status ps = render_pipelined(c, S, T, D, dump_p, N, (int)n_tasks, dim_stride, max_samples, max_P, first,
+                                                g_pipe_groups, st);
         if (ps) return ps;
         if (st) return st;
     }
@@ -1594,15 +1657,28 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             // BDPT (bdpt.h): light subpaths, then camera subpaths, bounce by bounce through k_closest
             // + k_bdpt_step; re-runs of samples that did not fit; connection items; fold.  Stage
             // slots: walks = CLOSEST + SHADE, items = SHADOW, re-runs + fold = RESOLVE.
+            // once few subpaths are alive, k_bdpt_tail is launched ahead of each bounce and, below
+            // g_bdpt_tail paths (the exact count, on the device), runs every remaining walk to its
+            // end in that launch; the bounce kernels then skip (as the path tracer's tail kernel)
             auto walk_step = [&](int mode) {
                 return [&, mode](uint32_t ub, int, int32_t* qa, int32_t* qb) {
+                    const uint32_t skip = (uint64_t)ub < 4ull * g_bdpt_tail ? g_bdpt_tail : 0u;
+                    if (skip > 0) {
+                        StageTimer tm(c, g_timing, ST_RESOLVE);
+                        launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
+                            launch_bdpt_tail<decltype(K)::value>(l, c.sc, S, T, B, BI, mode, qa, skip);
+                        });
+                    }
                     {
                         StageTimer tm(c, g_timing, ST_CLOSEST);
-                        launch_trav(c, ub, [&](auto K, const TravLaunch& l) { launch_closest<decltype(K)::value>(l, c.sc, S, qa); });
+                        launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
+                            launch_closest<decltype(K)::value>(l, c.sc, S, qa, skip);
+                        });
                     }
                     StageTimer tm(c, g_timing, ST_SHADE);
                     by_stack_class(c.sc.stack_class, [&](auto K) {
-                        launch_bdpt_step<decltype(K)::value>(ceil_div(ub, BLOCK), sm, c.sc.full, c.sc, S, T, B, BI, mode, qa, qb);
+                        launch_bdpt_step<decltype(K)::value>(ceil_div(ub, BLOCK), sm, c.sc.full, c.sc, S, T, B, BI, mode, qa, qb,
+                                                             skip);
                     });
                 };
             };
@@ -1703,7 +1779,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         }
         {
             StageTimer tm(c, g_timing, ST_RING);
-            k_ring<<<(int)n_tasks, 64, 0, sm>>>(S, T, (int)n_tasks, 1, S.counts, 0);
+            k_ring<<<(int)n_tasks, 64, 0, sm>>>(c.sc, S, T, (int)n_tasks, 1, S.counts, 0);
         }
         HIPCHK(hipGetLastError());
         if (bdpt && dfilm) {
@@ -1871,9 +1947,16 @@ lumo_status lumo_create(int device, void** ctx_out) {
         delete c;
         return LUMO_ERR_HIP;
     }
-    if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+    // LUMO_PRIO=1: the tail / film / ring stream (the chain Russian roulette waits on) at the
+    // device's highest stream priority, so its workgroups are placed ahead of the head streams'
+    int lo_prio = 0, hi_prio = 0;
+    const char* pe = std::getenv("LUMO_PRIO");
+    const bool prio = pe && pe[0] == '1' && hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
+    if ((prio ? hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, hi_prio)
+              : hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking)) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream5, hipStreamNonBlocking) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
         delete c;
         return LUMO_ERR_HIP;
@@ -1882,6 +1965,8 @@ lumo_status lumo_create(int device, void** ctx_out) {
         (void)hipEventCreateWithFlags(&c->pass_ev[i], hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&c->tail_ev[i], hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&c->cam_ev[i], hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&c->film_ev[i], hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&c->done_ev[i], hipEventDisableTiming);
     }
     for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventCreate(&c->ev[i]);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventCreateWithFlags(&c->snap_ev[i], hipEventDisableTiming);
@@ -1907,6 +1992,10 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("LUMO_PIPELINE")) g_pipeline = std::atoi(e);
     if (const char* e = std::getenv("LUMO_DYN")) g_dyn = std::atoi(e);
+    if (const char* e = std::getenv("LUMO_TAIL_REFILL")) g_tail_refill = std::atoi(e);
+    if (const char* e = std::getenv("LUMO_FILM_MODE")) g_film_mode = std::atoi(e);
+    if (const char* e = std::getenv("LUMO_BDPT_TAIL")) g_bdpt_tail = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("LUMO_PIPE_GROUPS")) g_pipe_groups = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("LUMO_HEADS")) g_heads = std::min(std::max(std::atoi(e), 0), 64);
     if (const char* e = std::getenv("LUMO_BOUNCE_THREADS")) {
         const int t = std::atoi(e);
@@ -1926,6 +2015,7 @@ void lumo_destroy(void* ctx) {
     (void)hipStreamSynchronize(c->stream2);
     (void)hipStreamSynchronize(c->stream3);
     (void)hipStreamSynchronize(c->stream4);
+    (void)hipStreamSynchronize(c->stream5);
     free_scene(*c);
     for (DevBuf& b : c->work)
         if (b.p) (void)hipFree(b.p);
@@ -1936,8 +2026,11 @@ void lumo_destroy(void* ctx) {
         (void)hipEventDestroy(c->pass_ev[i]);
         (void)hipEventDestroy(c->tail_ev[i]);
         (void)hipEventDestroy(c->cam_ev[i]);
+        (void)hipEventDestroy(c->film_ev[i]);
+        (void)hipEventDestroy(c->done_ev[i]);
     }
     (void)hipStreamDestroy(c->stream4);
+    (void)hipStreamDestroy(c->stream5);
     (void)hipStreamDestroy(c->stream3);
     (void)hipStreamDestroy(c->stream2);
     (void)hipStreamDestroy(c->stream);
@@ -2518,6 +2611,8 @@ lumo_status lumo_debug_stream(void* ctx, size_t n) {
 
 void lumo_set_timing(int on) { g_timing = on != 0; }
 void lumo_set_lds_staging(int on) { g_lds = on != 0; }
+void lumo_set_bdpt_tail(uint32_t below) { g_bdpt_tail = below; }
+
 void lumo_set_bounce_mode(int fused, uint32_t tail_below, int pipeline) {
     g_fused = fused < 0 ? -1 : (fused != 0 ? 1 : 0);
     g_tail_below = tail_below;

@@ -25,7 +25,7 @@ struct TravLaunch {
 };
 
 template <int STK>
-void launch_closest(const TravLaunch& l, const DScene& sc, const Paths& S, const int32_t* queue);
+void launch_closest(const TravLaunch& l, const DScene& sc, const Paths& S, const int32_t* queue, uint32_t tail_below);
 template <int STK>
 void launch_closest_q(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& cur, uint32_t skip_below);
 template <int STK>
@@ -40,7 +40,11 @@ void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, c
 
 template <int STK>
 void launch_bdpt_step(int grid, hipStream_t sm, int fx, const DScene& sc, const Paths& S, const Tasks& T,
-                      const Bdpt& B, const BItems& I, int mode, const int32_t* queue, int32_t* next_queue);
+                      const Bdpt& B, const BItems& I, int mode, const int32_t* queue, int32_t* next_queue,
+                      uint32_t tail_below);
+template <int STK>
+void launch_bdpt_tail(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const Bdpt& B,
+                      const BItems& I, int mode, const int32_t* queue, uint32_t tail_below);
 template <int STK>
 void launch_bdpt_redo(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const DCam& cam,
                       const Bdpt& B, const Bdpt& R, const BItems& I);
@@ -52,7 +56,8 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
                      const BItems& I, int n, const uint32_t* totals);
 
 #define LUMO_EXTERN_STK(K)                                                                                        \
-    extern template void launch_closest<K>(const TravLaunch&, const DScene&, const Paths&, const int32_t*);        \
+    extern template void launch_closest<K>(const TravLaunch&, const DScene&, const Paths&, const int32_t*,        \
+                                           uint32_t);                                                             \
     extern template void launch_closest_q<K>(const TravLaunch&, const DScene&, const Paths&, const QState&,       \
                                              uint32_t);                                                           \
     extern template void launch_shadow_q<K>(const TravLaunch&, const DScene&, const Paths&, const QState&);        \
@@ -62,7 +67,10 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
                                          const int32_t*, int, int, double*, int32_t*, int32_t*, int32_t*,         \
                                          unsigned long long*, bool);                                              \
     extern template void launch_bdpt_step<K>(int, hipStream_t, int, const DScene&, const Paths&, const Tasks&,   \
-                                             const Bdpt&, const BItems&, int, const int32_t*, int32_t*);          \
+                                             const Bdpt&, const BItems&, int, const int32_t*, int32_t*,           \
+                                             uint32_t);                                                           \
+    extern template void launch_bdpt_tail<K>(const TravLaunch&, const DScene&, const Paths&, const Tasks&,        \
+                                             const Bdpt&, const BItems&, int, const int32_t*, uint32_t);          \
     extern template void launch_bdpt_redo<K>(const TravLaunch&, const DScene&, const Paths&, const Tasks&,        \
                                              const DCam&, const Bdpt&, const Bdpt&, const BItems&);               \
     extern template void launch_bdpt_trace_a<K>(const TravLaunch&, const DScene&, const Paths&, const DCam&,      \

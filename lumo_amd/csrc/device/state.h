@@ -142,8 +142,8 @@ struct Paths {
     double* hit_t;
     int32_t *hit_kind, *hit_obj, *hit_tri;
     // per-pass outputs
-    double *p_rgb, *p_lum;
-    uint32_t *p_cost, *p_valid;
+    double* p_rgb;
+    uint32_t* p_valid;
     double* film;
     int32_t *q0, *q1;  // BDPT walk queues (slot ids)
     uint32_t* counts;

@@ -49,14 +49,22 @@ def test_bdpt_paths(dev, name, tile):
         np.testing.assert_array_equal(g[k], o[k], err_msg=k)
 
 
+# walk tail: 0 = every bounce through k_closest + k_bdpt_step; 300 = the walk-tail kernel takes over
+# once fewer than 300 subpaths are alive (a mix); 65536 (default) = from the first bounce here
+@pytest.mark.parametrize("tail", [0, 300, 65536])
 @pytest.mark.parametrize("name,res,spp", [("cornell", (32, 32), 6), ("caustics", (40, 24), 4), ("zoo", (32, 16), 4)])
-def test_bdpt_tiles_and_splats(dev, name, res, spp):
+def test_bdpt_tiles_and_splats(dev, name, res, spp, tail):
     sc, cam = _scene(name, res)
     sc.build()
     dev.upload(sc, cam)
     tasks = L.make_tasks(res[0], res[1], spp, 0x5EED)
     sp = []
-    bufs, rr = dev.render_tasks(tasks, integrator=BDPT, splats_out=sp)
+    lib = _ffi.load()
+    lib.lumo_set_bdpt_tail(tail)
+    try:
+        bufs, rr = dev.render_tasks(tasks, integrator=BDPT, splats_out=sp)
+    finally:
+        lib.lumo_set_bdpt_tail(65536)
     osp = []
     obufs, orr, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8, integrator=BDPT, splats_out=osp)
     assert sum(len(s) for s in osp) > 0

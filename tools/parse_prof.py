@@ -52,6 +52,16 @@ for r in rows("trace/**/*kernel_trace.csv"):
     res[k]["launches"] += 1
     res[k]["total_ns"] += b - a
     ivs[k].append((a, b))
+    # resources of the code object (the kernel trace carries them per dispatch): registers,
+    # scratch bytes per lane, LDS per workgroup; the register-limited waves per SIMD follow
+    # (512 VGPRs per SIMD lane, arch + accumulation registers in granules of 8)
+    if "VGPR_Count" in r:
+        vg = int(r["VGPR_Count"]) + int(r.get("Accum_VGPR_Count") or 0)
+        wg = int(r.get("Workgroup_Size_X") or r.get("Workgroup_Size") or 0)
+        res[k]["resources"] = {"vgpr": vg, "sgpr": int(r.get("SGPR_Count") or 0),
+                               "scratch_bytes_per_lane": int(r.get("Scratch_Size") or 0),
+                               "lds_bytes_per_workgroup": int(r.get("LDS_Block_Size") or 0), "workgroup": wg,
+                               "waves_per_simd_by_vgpr": min(8, 512 // max(8, (vg + 7) // 8 * 8))}
 for k, v in res.items():
     v["avg_us"] = v["total_ns"] / max(v["launches"], 1) / 1e3
     v["busy_ms"] = union_ns(ivs[k]) / 1e6  # overlapping launches (several streams) counted once
