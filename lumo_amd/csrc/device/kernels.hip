@@ -629,11 +629,10 @@ struct DevBuf {
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;  // pipelined passes: each pass's tail and ring
+    hipStream_t stream2 = nullptr;  // pipelined passes: each pass's tail, film and ring
     hipStream_t stream3 = nullptr;  // pipelined passes (2-3 head streams): further head streams
     hipStream_t stream4 = nullptr;
-    hipStream_t stream5 = nullptr;  // pipelined passes: each pass's film, off the ring's chain
-    hipEvent_t pass_ev[4] = {}, tail_ev[4] = {}, cam_ev[4] = {}, film_ev[4] = {}, done_ev[4] = {};
+    hipEvent_t pass_ev[4] = {}, tail_ev[4] = {}, cam_ev[4] = {}, film_ev[4] = {};
     bool has_scene = false, has_camera = false;
     DScene sc{};
     DCam cam{};
@@ -850,10 +849,9 @@ int g_fused = -1;  // n_shadow == 1: k_bounce_q instead of closest / shade / sha
 uint32_t g_tail_below = 1u << 18;  // n_shadow == 1: k_bounce_q tail mode below this many live paths
 int g_pipeline = 3;                // fused passes overlapped (render_pipelined): 0 off, else the number of head streams (1-3)
 int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from a counter
-int g_tail_refill = 0;             // tail kernel: lanes refill one path at a time (else 64 per wave)
 int g_pipe_groups = 1;             // pipelined fused passes: independent task groups (1 or 2)
 uint32_t g_bdpt_tail = 1u << 16;    // BDPT walks: k_bdpt_tail below this many live subpaths (0: never)
-int g_film_mode = 2;               // pipelined fused passes: film 0 before the ring, 1 after it (both on the tail stream), 2 own stream
+int g_film_mode = 0;               // pipelined fused passes: the film 0 before the ring, 1 after it (tail stream)
 int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
 int g_heads = 0;                   // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
 int g_split_pipe = 4;              // split schedule: passes in flight (render_split_pipelined; 1 = sequential)
@@ -951,7 +949,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         bool ok = false;
         ~JoinOnError() {
             if (ok) return;
-            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream5, c.stream})
+            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream})
                 if (s) (void)hipStreamSynchronize(s);
         }
     } join{c};
@@ -968,7 +966,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
     for (int k = 1; k < NSETS; ++k) alloc_pass_set(c, P3[k], k, N, st);
     if (st) return st;
     hipStream_t As[3] = {c.stream, c.stream3, c.stream4};
-    hipStream_t Bs[2] = {c.stream2, c.stream4}, F = c.stream5;
+    hipStream_t Bs[2] = {c.stream2, c.stream4};
     if (G == 2) As[1] = c.stream3;
     // every event starts "done" after the setup enqueued on stream 0 (tasks, memsets, the initial
     // ring): unit n waits for unit n - NSETS's ring before reusing its set, for its group's
@@ -1032,7 +1030,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
                 c, (uint64_t)Nu,
                 [&](auto K, const TravLaunch& l) {
                     launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[heads & 1], P.qs[(heads + 1) & 1],
-                                                        0xffffffffu, true, g_tail_refill, BLOCK);
+                                                        0xffffffffu, true, 0, BLOCK);
                 },
                 B);
         }
@@ -1055,11 +1053,11 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
             return LUMO_OK;
         };
         // the ring computes the samples' luminance itself, so it need not follow the film:
-        // g_film_mode 0: film then ring on B; 1: ring then film on B; 2: the film on its own
-        // stream F (in pass order), off the chain that Russian roulette of the next pass waits on
+        // g_film_mode 0 (default): film then ring; 1: ring then film.  A film on a stream of its
+        // own, off the chain the next pass's Russian roulette waits on, measured slower (C1 1/8
+        // share 438 -> 488 ms per frame): the head streams, not that chain, bound the frame
         lumo_status fe = LUMO_OK;
         if (g_film_mode == 0 && (fe = film(B))) return fe;
-        HIPCHK(hipEventRecord(c.done_ev[set], B));
         {
             StageTimer tm(c, g_timing, ST_RING, B);
             k_ring<<<t1 - t0, 64, 0, B>>>(c.sc, P, T, t1, 1, P.counts, t0);
@@ -1067,10 +1065,6 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.pass_ev[set], B));
         if (g_film_mode == 1 && (fe = film(B))) return fe;
-        if (g_film_mode == 2) {
-            HIPCHK(hipStreamWaitEvent(F, c.done_ev[set], 0));
-            if ((fe = film(F))) return fe;
-        }
         if (g_timing) resolve_timers(c);
     }
     // the results are copied on stream 0: after every set's last unit
@@ -1097,7 +1091,7 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
     if (skip > 0) {
         StageTimer tm(c, g_timing, ST_RESOLVE, sm);
         launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
-            launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true, g_tail_refill, BLOCK);
+            launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true, 0, BLOCK);
         }, sm);
     }
     if (fused_now) {  // one fused kernel per bounce (pt.h k_bounce_q)
@@ -1176,7 +1170,7 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         bool ok = false;
         ~JoinOnError() {
             if (ok) return;
-            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream5, c.stream})
+            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream})
                 if (s) (void)hipStreamSynchronize(s);
         }
     } join{c};
@@ -1947,16 +1941,9 @@ lumo_status lumo_create(int device, void** ctx_out) {
         delete c;
         return LUMO_ERR_HIP;
     }
-    // LUMO_PRIO=1: the tail / film / ring stream (the chain Russian roulette waits on) at the
-    // device's highest stream priority, so its workgroups are placed ahead of the head streams'
-    int lo_prio = 0, hi_prio = 0;
-    const char* pe = std::getenv("LUMO_PRIO");
-    const bool prio = pe && pe[0] == '1' && hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
-    if ((prio ? hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, hi_prio)
-              : hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking)) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream5, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
         delete c;
         return LUMO_ERR_HIP;
@@ -1966,7 +1953,6 @@ lumo_status lumo_create(int device, void** ctx_out) {
         (void)hipEventCreateWithFlags(&c->tail_ev[i], hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&c->cam_ev[i], hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&c->film_ev[i], hipEventDisableTiming);
-        (void)hipEventCreateWithFlags(&c->done_ev[i], hipEventDisableTiming);
     }
     for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventCreate(&c->ev[i]);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventCreateWithFlags(&c->snap_ev[i], hipEventDisableTiming);
@@ -1992,7 +1978,6 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("LUMO_PIPELINE")) g_pipeline = std::atoi(e);
     if (const char* e = std::getenv("LUMO_DYN")) g_dyn = std::atoi(e);
-    if (const char* e = std::getenv("LUMO_TAIL_REFILL")) g_tail_refill = std::atoi(e);
     if (const char* e = std::getenv("LUMO_FILM_MODE")) g_film_mode = std::atoi(e);
     if (const char* e = std::getenv("LUMO_BDPT_TAIL")) g_bdpt_tail = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("LUMO_PIPE_GROUPS")) g_pipe_groups = std::max(1, std::atoi(e));
@@ -2015,7 +2000,6 @@ void lumo_destroy(void* ctx) {
     (void)hipStreamSynchronize(c->stream2);
     (void)hipStreamSynchronize(c->stream3);
     (void)hipStreamSynchronize(c->stream4);
-    (void)hipStreamSynchronize(c->stream5);
     free_scene(*c);
     for (DevBuf& b : c->work)
         if (b.p) (void)hipFree(b.p);
@@ -2027,10 +2011,8 @@ void lumo_destroy(void* ctx) {
         (void)hipEventDestroy(c->tail_ev[i]);
         (void)hipEventDestroy(c->cam_ev[i]);
         (void)hipEventDestroy(c->film_ev[i]);
-        (void)hipEventDestroy(c->done_ev[i]);
     }
     (void)hipStreamDestroy(c->stream4);
-    (void)hipStreamDestroy(c->stream5);
     (void)hipStreamDestroy(c->stream3);
     (void)hipStreamDestroy(c->stream2);
     (void)hipStreamDestroy(c->stream);

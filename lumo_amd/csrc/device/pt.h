@@ -666,50 +666,12 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
     Counters Cc{0, 0, 0, 0}, Cs{0, 0, 0, 0};
     if constexpr (TAIL) {
         uint32_t tailq = 0;
-        if (dyn) {
-            // per-lane refill: a lane whose path ended takes the next queued path at once (one
-            // atomic per wave and round for the lanes that need one), so a wave no longer idles
-            // until its longest path ends.  Each path's bounces are the same; only which lane and
-            // when change (bit-identical).
-            PathReg P{};
-            bool have = false, more = true;
-            for (;;) {
-                if (more) {
-                    const uint64_t need = __ballot(!have);
-                    if (need) {
-                        const int lead = __ffsll((unsigned long long)need) - 1;
-                        const uint32_t n_need = (uint32_t)__popcll(need);
-                        uint32_t b = 0;
-                        if (lane_id() == lead) b = atomicAdd(S.counts + CNT_FETCH_T, n_need);
-                        b = __shfl(b, lead, 64);
-                        if (b + n_need >= count) more = false;
-                        if (!have) {
-                            const uint32_t q = b + mbcnt64(need);
-                            if (q < count) {
-                                P = load_path(cur, q);
-                                have = true;
-                            }
-                        }
-                    }
-                }
-                if (__ballot(have) == 0) break;
-                if (have) {
-                    if (bounce_path<STK, FX>(sc, T.delta, P, Cc, Cs)) {
-                        tailq++;
-                    } else {
-                        store_final(S, P);
-                        have = false;
-                    }
-                }
-            }
-        } else {
         for (uint32_t w0 = wave_fetch(S.counts + CNT_FETCH_T); w0 < count; w0 = wave_fetch(S.counts + CNT_FETCH_T)) {
             const uint32_t q = w0 + lane_id();
             if (q >= count) continue;
             PathReg P = load_path(cur, q);
             while (bounce_path<STK, FX>(sc, T.delta, P, Cc, Cs)) tailq++;
             store_final(S, P);
-        }
         }
         flush_resolved(tailq, S.tcount + TC_TAILQ);
     } else {

@@ -17,10 +17,10 @@ def rows(pattern):
 def short(name):
     if "k_bounce_q" in name:  # k_bounce_q<STK, LDS, FX, TAIL>: the fused bounce and the tail kernel
         return "k_bounce_tail" if name.split("(")[0].rstrip().endswith("true>") else "k_bounce_q"
-    for k in ("k_camera", "k_closest", "k_shade", "k_shadow_queue", "k_shadow", "k_resolve", "k_finish_film", "k_finish", "k_film",
-              "k_ring", "k_init_mj", "k_init_seeds", "k_trace", "k_bdpt_redo", "k_bdpt_taps", "k_bdpt_trace_a",
-              "k_bdpt_vis", "k_bdpt_eval_a", "k_bdpt_paths", "k_bdpt_step", "k_bdpt_fold", "k_bdpt", "k_nee_gen", "k_nee_fold",
-              "k_calib_read8", "k_calib_write8",
+    for k in ("k_camera", "k_closest", "k_shade", "k_shadow_queue", "k_shadow", "k_resolve", "k_finish_film",
+              "k_finish", "k_film", "k_ring", "k_init_mj", "k_init_seeds", "k_trace", "k_bdpt_redo", "k_bdpt_taps",
+              "k_bdpt_trace_a", "k_bdpt_vis", "k_bdpt_eval_a", "k_bdpt_paths", "k_bdpt_step", "k_bdpt_tail",
+              "k_bdpt_fold", "k_bdpt", "k_nee_gen", "k_nee_fold", "k_calib_read8", "k_calib_write8",
               "k_bounce_begin", "k_task_tap_ranges"):
         if k in name:
             return k
