@@ -555,9 +555,12 @@ __device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_mi
 #else
 #define KD_INLINE
 #endif
-// kd stack entry k: in this thread's LDS column when k < sc.kst_n (TOP kernels), else in scratch
+// kd stack entry k: in this thread's LDS column when k < sc.kst_n (KL: TOP kernels), else in
+// scratch.  KL is a template flag so the kernels without a TOP view (the LDS-staged fused bounce,
+// HBM views) carry no LDS-stack code at all.
+template <bool KL>
 __device__ __forceinline__ void kst_push(const DScene& sc, int* st_node, double* st_ts, int k, int node, double t) {
-    if (k < sc.kst_n) {
+    if (KL && k < sc.kst_n) {
         sc.kst_node[k * sc.kst_stride] = node;
         sc.kst_ts[k * sc.kst_stride] = t;
     } else {
@@ -565,14 +568,16 @@ __device__ __forceinline__ void kst_push(const DScene& sc, int* st_node, double*
         st_ts[k] = t;
     }
 }
+template <bool KL>
 __device__ __forceinline__ int kst_node(const DScene& sc, const int* st_node, int k) {
-    return k < sc.kst_n ? sc.kst_node[k * sc.kst_stride] : st_node[k];
+    return (KL && k < sc.kst_n) ? sc.kst_node[k * sc.kst_stride] : st_node[k];
 }
+template <bool KL>
 __device__ __forceinline__ double kst_t(const DScene& sc, const double* st_ts, int k) {
-    return k < sc.kst_n ? sc.kst_ts[k * sc.kst_stride] : st_ts[k];
+    return (KL && k < sc.kst_n) ? sc.kst_ts[k * sc.kst_stride] : st_ts[k];
 }
 
-template <bool GEO, int STK>
+template <bool GEO, int STK, bool KL = false>
 __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const RayX& r, double t_min, double t_max,
                               int* idx_out, Counters& C) {
     const double origin[3] = {r.o.x, r.o.y, r.o.z};
@@ -611,7 +616,7 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const 
                 curr = second;
             } else {
                 curr = first;
-                kst_push(sc, st_node, st_ts, sp, second, t_split);
+                kst_push<KL>(sc, st_node, st_ts, sp, second, t_split);
                 t_end = t_split;
                 sp++;
             }
@@ -636,9 +641,9 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const 
             }
             if (sp == 0) break;
             sp--;
-            curr = kst_node(sc, st_node, sp);
-            t_start = kst_t(sc, st_ts, sp);
-            t_end = sp == 0 ? t_end0 : kst_t(sc, st_ts, sp - 1);
+            curr = kst_node<KL>(sc, st_node, sp);
+            t_start = kst_t<KL>(sc, st_ts, sp);
+            t_end = sp == 0 ? t_end0 : kst_t<KL>(sc, st_ts, sp - 1);
         } else {
             C.kd++;
             const int ax = axis;
@@ -654,7 +659,7 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const 
                 curr = second;
             } else {
                 curr = first;
-                kst_push(sc, st_node, st_ts, sp, second, t_split);
+                kst_push<KL>(sc, st_node, st_ts, sp, second, t_split);
                 t_end = t_split;
                 sp++;
             }
@@ -786,27 +791,28 @@ constexpr int PRIM_SPHERE = -2;
 // Object::hit_t of the shape (kdtree.rs:178-180, rectangle.rs:87-89, triangle.rs:195-197)
 // FX: full feature set (instances, spheres, triangle objects, microfacet materials); scenes made
 // only of kd meshes / rectangles with Lambertian + Light materials run the FX = false kernels.
-template <int STK, int FX>
+template <int STK, int FX, bool KL = false>
 __device__ __forceinline__ double shape_hit_t(const DScene& sc, const DObj& ob, const RayX& r, double t_min,
                                               double t_max, Counters& C) {
     if constexpr (FX) {
         if (ob.type() == LUMO_OBJ_TRIANGLE) return tri_hit_t(sc, ob.tri_base, r, t_min, t_max, C);
         if (ob.type() == LUMO_OBJ_SPHERE) return sphere_hit_t(ob, r, t_min, t_max);
     }
-    return kd_traverse<false, STK>(sc, ob, r, t_min, t_max, nullptr, C);
+    return kd_traverse<false, STK, KL>(sc, ob, r, t_min, t_max, nullptr, C);
 }
-template <int STK, int FX>
+template <int STK, int FX, bool KL = false>
 __device__ __forceinline__ double object_hit_t(const DScene& sc, const DObj& ob, const RayX& r, double t_min,
                                                double t_max, Counters& C) {
     if constexpr (FX) {
-        if (ob.xform() >= 0) return shape_hit_t<STK, FX>(sc, ob, ray_local(sc.xforms[ob.xform()], r), t_min, t_max, C);
+        if (ob.xform() >= 0)
+            return shape_hit_t<STK, FX, KL>(sc, ob, ray_local(sc.xforms[ob.xform()], r), t_min, t_max, C);
     }
-    return shape_hit_t<STK, FX>(sc, ob, r, t_min, t_max, C);
+    return shape_hit_t<STK, FX, KL>(sc, ob, r, t_min, t_max, C);
 }
 
 // Object::hit: kd GEO traversal, then the winner's GEO test (acceptance + t only; the record is
 // rebuilt by object_record).  Returns the global triangle index, PRIM_SPHERE, or -1 (miss).
-template <int STK, int FX>
+template <int STK, int FX, bool KL = false>
 __device__ __forceinline__ int shape_hit_tri(const DScene& sc, const DObj& ob, const RayX& r, double t_min,
                                              double t_max, Counters& C, DHit& out) {
     if constexpr (FX) {
@@ -817,19 +823,20 @@ __device__ __forceinline__ int shape_hit_tri(const DScene& sc, const DObj& ob, c
         if (ob.type() == LUMO_OBJ_SPHERE) return sphere_hit<false>(ob, r, t_min, t_max, out) ? PRIM_SPHERE : -1;
     }
     int idx = -1;
-    kd_traverse<true, STK>(sc, ob, r, t_min, t_max, &idx, C);
+    kd_traverse<true, STK, KL>(sc, ob, r, t_min, t_max, &idx, C);
     if (idx < 0) return -1;
     C.tri++;
     if (!tri_hit_geo<false>(sc, ob.tri_base + idx, r, t_min, t_max, out)) return -1;
     return ob.tri_base + idx;
 }
-template <int STK, int FX>
+template <int STK, int FX, bool KL = false>
 __device__ __forceinline__ int object_hit_tri(const DScene& sc, const DObj& ob, const RayX& r, double t_min,
                                               double t_max, Counters& C, DHit& out) {
     if constexpr (FX) {
-        if (ob.xform() >= 0) return shape_hit_tri<STK, FX>(sc, ob, ray_local(sc.xforms[ob.xform()], r), t_min, t_max, C, out);
+        if (ob.xform() >= 0)
+            return shape_hit_tri<STK, FX, KL>(sc, ob, ray_local(sc.xforms[ob.xform()], r), t_min, t_max, C, out);
     }
-    return shape_hit_tri<STK, FX>(sc, ob, r, t_min, t_max, C, out);
+    return shape_hit_tri<STK, FX, KL>(sc, ob, r, t_min, t_max, C, out);
 }
 
 // Full hit record of triangle `tri` of object `ob` for world ray r (the GEO test is
@@ -904,7 +911,7 @@ __device__ int bvh_traverse(const DScene& sc, const DBvh* nodes, int n_nodes, co
 #endif
             for (int k = 0; k < count; ++k) {
                 const int i = items[node.first + k];
-                const double t = object_hit_t<STK, FX>(sc, objs[i], r, t_min, tt, C);
+                const double t = object_hit_t<STK, FX, TOP>(sc, objs[i], r, t_min, tt, C);
                 if (GEO) {
                     if (t < tt) {
                         tt = t;
@@ -947,7 +954,7 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     int oi = bvh_traverse<true, STK, FX, TOP>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, r, 0.0, t_max, C, nullptr,
                                               sc.onodes_lds, sc.n_onodes_lds);
     if (oi >= 0) {
-        const int tri = object_hit_tri<STK, FX>(sc, sc.tobjs[oi], r, 0.0, t_max, C, g);
+        const int tri = object_hit_tri<STK, FX, TOP>(sc, sc.tobjs[oi], r, 0.0, t_max, C, g);
         if (tri != -1) {
             h = HitRef{g.t, 1, oi, tri};
             t_max = g.t;
@@ -956,7 +963,7 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     const int li = bvh_traverse<true, STK, FX, TOP>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, r, 0.0, t_max, C,
                                                     nullptr, sc.lnodes_lds, sc.n_lnodes_lds);
     if (li >= 0) {
-        const int tri = object_hit_tri<STK, FX>(sc, sc.tlights[li], r, 0.0, t_max, C, g);
+        const int tri = object_hit_tri<STK, FX, TOP>(sc, sc.tlights[li], r, 0.0, t_max, C, g);
         if (tri != -1) h = HitRef{g.t, 2, li, tri};
     }
     return h;
@@ -972,7 +979,7 @@ __device__ __forceinline__ void hit_record(const DScene& sc, const HitRef& hr, c
 // Scene::hit_light (scene.rs:165-189): returns true and the light hit if visible.
 template <int STK, int FX, bool TOP = false>
 __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit& lh, Counters& C) {
-    const int tri = object_hit_tri<STK, FX>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
+    const int tri = object_hit_tri<STK, FX, TOP>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
     if (tri == -1) return false;
     const double t_max = lh.t - EPSILON;
     if (bvh_hit_t<STK, FX, TOP>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, r, 0.0, t_max, C, sc.onodes_lds,
@@ -991,7 +998,7 @@ __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit
 template <int STK, int FX, bool TOP = false>
 __device__ int scene_hit_light_tri(const DScene& sc, const RayX& r, int light, Counters& C) {
     DHit lh;
-    const int tri = object_hit_tri<STK, FX>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
+    const int tri = object_hit_tri<STK, FX, TOP>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
     if (tri == -1) return -1;
     const double t_max = lh.t - EPSILON;
     if (bvh_hit_t<STK, FX, TOP>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, r, 0.0, t_max, C, sc.onodes_lds,

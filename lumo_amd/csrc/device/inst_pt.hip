@@ -67,7 +67,7 @@ void launch_bounce_q(const TravLaunch& l, const DScene& sc, const Paths& S, cons
     // B record after the staged scene; the tail kernel keeps BLOCK threads and needs no record LDS
     const int nt = tail_only ? BLOCK : threads;
     const int grid = l.grid * (BLOCK / nt);
-    const size_t rec = tail_only ? 0 : (size_t)12 * sizeof(double) * nt;
+    const size_t rec = tail_only ? 0 : (size_t)PARK_DOUBLES * sizeof(double) * nt;
     const size_t scene = l.lds ? (l.shm + 15) / 16 * 16 : 0;
     auto go = [&](auto TL) {
         constexpr bool TAIL = decltype(TL)::value;

@@ -530,6 +530,44 @@ __device__ __forceinline__ DColor shadow_record_r(const DScene& sc, const NeeRec
     return out;
 }
 
+// shadow_record_r with the record's bsdf_f and shading cosine read from LDS only after the
+// traversal (`fc`: f[0..3] at fc[0], fc[nt], fc[2nt], fc[3nt], the cosine at fc[cos_at * nt]), so
+// they hold no registers during the walk.  Same operations in the same order.
+template <int STK, int FX>
+__device__ __forceinline__ DColor shadow_record_lds(const DScene& sc, const Ray& ray, double pdf, const double* fc,
+                                                    int cos_at, uint32_t nt, int li, bool li_mode, const double* L,
+                                                    Counters& C) {
+#if LUMO_SKIP_DEAD
+    if (pdf == 0.0) {  // integrator.rs:146: p_sct == 0 contributes 0 whatever the visibility
+        C.resolved++;
+        return cfill(0.0);
+    }
+#endif
+    const RayX ri = rayx(ray);
+    DHit hi;
+    DColor out = cfill(0.0);
+    if (scene_hit_light<STK, FX>(sc, ri, li, hi, C)) {
+        const lumo_object& Lo = sc.lights[li];
+        const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
+        const double p_sct = pdf;
+        if (!(p_lig == 0.0 || p_sct == 0.0)) {
+            const double denom = p_lig * p_lig + p_sct * p_sct;
+            const double weight = li_mode ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
+            const double p_denom = li_mode ? p_lig : p_sct;
+            const lumo_material hm = sc.mats[hi.material];
+            const DColor f{{fc[0], fc[nt], fc[2 * nt], fc[3 * nt]}};
+            out = f * cfill(1.0) * emit<FX>(sc, hm, L, hi.backface, hi.uv) * fc[cos_at * nt] * weight / p_denom;
+        }
+    }
+    return out;
+}
+
+#ifndef LUMO_PARK_NEE
+#define LUMO_PARK_NEE 1
+#endif
+// doubles per thread in k_bounce_q's LDS: the B record (12), the L record's f and cosine and g_nee (9)
+constexpr int PARK_DOUBLES = LUMO_PARK_NEE ? 12 + 9 : 12;
+
 // A path between bounces, in registers (one QState entry).
 struct PathReg {
     Ray ro;
@@ -725,6 +763,12 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                             const V2 rs = xs_vec2(P.rng);
                             RL = nee_record<FX>(sc, m, ho, wo, light_sample_towards<FX>(sc, sc.lights[li], ho.p, rs),
                                                 P.L);
+                            if (LUMO_PARK_NEE) {  // the L record's f / cosine and g_nee wait in LDS
+                                double* rl = rb_lds + 12 * nt + threadIdx.x;
+                                for (int k = 0; k < 4; ++k) rl[k * nt] = RL.f.s[k];
+                                rl[4 * nt] = RL.cosv;
+                                for (int k = 0; k < 4; ++k) rl[(5 + k) * nt] = g_nee.s[k];
+                            }
                             const double ru = xs_float(P.rng);
                             const V2 rsq2 = xs_vec2(P.rng);
                             V3 wb;
@@ -781,6 +825,20 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
             }
             // phase 3: the pair's visibility + MIS (k_shadow_q, NS1)
             if (resolve) {
+#if LUMO_PARK_NEE
+                const double* rl = rb_lds + 12 * nt + threadIdx.x;
+                const DColor a = shadow_record_lds<STK, FX>(sc, RL.ray, RL.pdf, rl, 4, nt, li, true, P.L, Cs);
+                DColor b = cfill(0.0);
+                if (ok) {
+                    const double* v = rb_lds + threadIdx.x;
+                    const Ray rbr{V3{v[0], v[nt], v[2 * nt]}, V3{v[3 * nt], v[4 * nt], v[5 * nt]}};
+                    b = shadow_record_lds<STK, FX>(sc, rbr, v[10 * nt], v + 6 * nt, 5, nt, li, false, P.L, Cs);
+                }
+                const double pdf_l = sc.alias_pdf[li];  // pdf_light, re-read
+                const DColor g_n{{rl[5 * nt], rl[6 * nt], rl[7 * nt], rl[8 * nt]}};
+                const DColor single = (cfill(0.0) + a + b) / pdf_l;
+                const DColor X = (cfill(0.0) + g_n * single) / 1.0;
+#else
                 const DColor a = shadow_record_r<STK, FX>(sc, RL, li, true, P.L, Cs);
                 DColor b = cfill(0.0);
                 if (ok) {
@@ -794,6 +852,7 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                 }
                 const DColor single = (cfill(0.0) + a + b) / pdf_light;
                 const DColor X = (cfill(0.0) + g_nee * single) / 1.0;
+#endif
                 if (alive)
                     qc(nxt, QD_P, np, X);
                 else  // the radiance stored above, re-read by the thread that wrote it
