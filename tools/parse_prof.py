@@ -54,9 +54,11 @@ for r in rows("trace/**/*kernel_trace.csv"):
     ivs[k].append((a, b))
     # resources of the code object (the kernel trace carries them per dispatch): registers,
     # scratch bytes per lane, LDS per workgroup; the register-limited waves per SIMD follow
-    # (512 VGPRs per SIMD lane, arch + accumulation registers in granules of 8)
+    # (512 VGPRs per SIMD lane, arch + accumulation registers in granules of 8).  On gfx950 the
+    # trace's VGPR_Count is half the allocation the compiler reports (NumVgprs: 168 for the C1 fused
+    # kernel, traced as 84; 256 for the tail kernel, traced as 128), so it is doubled here.
     if "VGPR_Count" in r:
-        vg = int(r["VGPR_Count"]) + int(r.get("Accum_VGPR_Count") or 0)
+        vg = 2 * int(r["VGPR_Count"]) + int(r.get("Accum_VGPR_Count") or 0)
         wg = int(r.get("Workgroup_Size_X") or r.get("Workgroup_Size") or 0)
         res[k]["resources"] = {"vgpr": vg, "sgpr": int(r.get("SGPR_Count") or 0),
                                "scratch_bytes_per_lane": int(r.get("Scratch_Size") or 0),
