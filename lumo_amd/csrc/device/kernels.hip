@@ -851,7 +851,6 @@ int g_pipeline = 3;                // fused passes overlapped (render_pipelined)
 int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from a counter
 int g_pipe_groups = 1;             // pipelined fused passes: independent task groups (1 or 2)
 uint32_t g_bdpt_tail = 1u << 16;    // BDPT walks: k_bdpt_tail below this many live subpaths (0: never)
-int g_film_mode = 0;               // pipelined fused passes: the film 0 before the ring, 1 after it (tail stream)
 int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
 int g_heads = 0;                   // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
 int g_split_pipe = 4;              // split schedule: passes in flight (render_split_pipelined; 1 = sequential)
@@ -1052,19 +1051,17 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
             HIPCHK(hipEventRecord(c.film_ev[set], fs));
             return LUMO_OK;
         };
-        // the ring computes the samples' luminance itself, so it need not follow the film:
-        // g_film_mode 0 (default): film then ring; 1: ring then film.  A film on a stream of its
-        // own, off the chain the next pass's Russian roulette waits on, measured slower (C1 1/8
-        // share 438 -> 488 ms per frame): the head streams, not that chain, bound the frame
-        lumo_status fe = LUMO_OK;
-        if (g_film_mode == 0 && (fe = film(B))) return fe;
+        // film, then the ring (which computes the samples' luminance itself).  A film on a stream
+        // of its own, off the chain the next pass's Russian roulette waits on, measured slower (C1
+        // 1/8 share 438 -> 488 ms per frame), ring-then-film the same: the head streams, not that
+        // chain, bound the frame
+        if (const lumo_status fe = film(B)) return fe;
         {
             StageTimer tm(c, g_timing, ST_RING, B);
             k_ring<<<t1 - t0, 64, 0, B>>>(c.sc, P, T, t1, 1, P.counts, t0);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.pass_ev[set], B));
-        if (g_film_mode == 1 && (fe = film(B))) return fe;
         if (g_timing) resolve_timers(c);
     }
     // the results are copied on stream 0: after every set's last unit
@@ -1978,7 +1975,6 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("LUMO_PIPELINE")) g_pipeline = std::atoi(e);
     if (const char* e = std::getenv("LUMO_DYN")) g_dyn = std::atoi(e);
-    if (const char* e = std::getenv("LUMO_FILM_MODE")) g_film_mode = std::atoi(e);
     if (const char* e = std::getenv("LUMO_BDPT_TAIL")) g_bdpt_tail = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("LUMO_PIPE_GROUPS")) g_pipe_groups = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("LUMO_HEADS")) g_heads = std::min(std::max(std::atoi(e), 0), 64);
