@@ -677,6 +677,8 @@ lumo_status dev_alloc(DevBuf& b, size_t bytes) {
     b.bytes = 0;
     if (hipMalloc(&b.p, bytes) != hipSuccess) return LUMO_ERR_OOM;
     b.bytes = bytes;
+    static const bool poison = std::getenv("LUMO_POISON") != nullptr;  // debug: new buffers all ones (NaN)
+    if (poison) (void)hipMemset(b.p, 0xFF, bytes);
     return LUMO_OK;
 }
 
@@ -1198,6 +1200,11 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         HIPCHK(hipEventRecord(c.pass_ev[k], Ss[0]));
         HIPCHK(hipEventRecord(c.film_ev[k], Ss[0]));
     }
+    // The render's setup (task and pixel tables, seeds, sampler permutations, the initial ring) and
+    // the sets' counter zeroing ran on stream 0: every other stream waits for them before its first
+    // unit (a pass-0 unit waits for nothing else).  Without this wait a unit on another stream
+    // could start on stale counters and tables: found by poisoning fresh buffers (LUMO_POISON).
+    for (int k = 1; k < K; ++k) HIPCHK(hipStreamWaitEvent(Ss[k], c.pass_ev[0], 0));
     const int SEG = Ctx::SNAP_RING / 4;  // snapshot slots per set
     const int ahead = std::max(1, std::min(c.bounce_ahead, SEG - 1));
     struct PS {
