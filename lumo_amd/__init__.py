@@ -869,28 +869,43 @@ class Renderer:
         self._device = int(d)
         return self
 
-    def render(self, rank=0, world_size=1):
-        """Render all (batch, tile) tasks; with world_size > 1 this rank renders the tiles
-        with tile_index % world_size == rank and returns its partial film."""
+    def render(self, rank=0, world_size=1, schedule="static", chunk=None, store=None):
+        """Render all (batch, tile) tasks and return this rank's (partial) film.
+
+        With world_size > 1, `schedule="static"` renders the tiles with
+        tile_index % world_size == rank; `schedule="dynamic"` claims
+        chunks of `chunk` tiles from a `dist.TileQueue` in the process group's store until none
+        are left (lumo's shared task receiver, pool.rs:26, 41-54), for scenes whose tiles cost
+        unequal time.  Either way the reduced film is the single-process film."""
         import time
+        if schedule not in ("static", "dynamic"):
+            raise ValueError(f"unknown schedule {schedule!r}")
         if self._seed is None:
             self._seed = time.time_ns() & 0xFFFFFFFFFFFFFFFF or 1
         w, h = self.camera.resolution
         tasks = make_tasks(w, h, self._samples, self._seed)
-        from .dist import shard_tasks
-        mine = shard_tasks(tasks, w, h, rank, world_size)
+        from .dist import TileQueue, shard_tasks, tasks_of_tiles
+        if schedule == "static" or world_size == 1:
+            chunks = iter([shard_tasks(tasks, w, h, rank, world_size)])
+        else:
+            queue = TileQueue(w, h, world_size, chunk=chunk, store=store)
+            chunks = (tasks_of_tiles(tasks, w, h, tiles) for tiles in queue)
         dev = Device(self._device)
         dev.upload(self.scene, self.camera)
         film = Film(w, h, getattr(self.camera, "color_space", 1), samples=self._samples)
-        if self._integrator == Integrator.BDPathTrace:
-            # light-tracing splats are summed on the device straight into the film's splat buffer
-            bufs, res = dev.render_tasks(mine, tone_map=self._tone_map, integrator=self._integrator,
-                                         splat_film=film.splats, sampler=self._sampler)
-        else:
-            bufs, res = dev.render_tasks(mine, tone_map=self._tone_map, sampler=self._sampler)
-        for t, b in zip(mine, bufs):
-            film.add_tile(t, b)
-        self.num_rays = sum(r.num_rays for r in res)
-        self.num_camera_rays = sum(r.num_camera_rays for r in res)
+        self.num_rays = self.num_camera_rays = 0
+        self.tasks_rendered = 0
+        for mine in chunks:
+            if self._integrator == Integrator.BDPathTrace:
+                # light-tracing splats are summed on the device straight into the film's splat buffer
+                bufs, res = dev.render_tasks(mine, tone_map=self._tone_map, integrator=self._integrator,
+                                             splat_film=film.splats, sampler=self._sampler)
+            else:
+                bufs, res = dev.render_tasks(mine, tone_map=self._tone_map, sampler=self._sampler)
+            for t, b in zip(mine, bufs):
+                film.add_tile(t, b)
+            self.num_rays += sum(r.num_rays for r in res)
+            self.num_camera_rays += sum(r.num_camera_rays for r in res)
+            self.tasks_rendered += len(mine)
         dev.close()
         return film

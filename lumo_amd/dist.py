@@ -5,6 +5,10 @@ FilmTile into the Film (film.rs:155-171).  Across GPUs the same split holds: eve
 tiles with tile_index % world_size == rank for every batch (so a rank's batches of one tile stay
 on one GPU), renders them with no communication, and the partial films are summed once at the
 end.  The sum is the only collective and it is off the hot path.
+
+For skewed scenes `TileQueue` hands tiles out dynamically instead (lumo's shared task receiver,
+pool.rs:26); the measured `tile % 8` shares of the benchmark scenes are balanced to 1.02 max/mean
+(DESIGN.md §6), so the static split stays the default.
 """
 import numpy as np
 
@@ -21,6 +25,62 @@ def shard_tasks(tasks, width, height, rank, world_size):
         raise ValueError(f"rank {rank} outside world of {world_size}")
     tpb = tiles_per_batch(width, height)
     return [t for i, t in enumerate(tasks) if (i % tpb) % world_size == rank]
+
+
+def tasks_of_tiles(tasks, width, height, tiles):
+    """The tasks (every batch, publish order) of the given tile indices."""
+    tpb = tiles_per_batch(width, height)
+    keep = set(int(t) for t in tiles)
+    return [t for i, t in enumerate(tasks) if (i % tpb) in keep]
+
+
+_queue_generation = 0
+
+
+class TileQueue:
+    """Dynamic, skew-tolerant tile distribution across ranks.
+
+    lumo's workers pop RenderTasks from one shared `Mutex<Receiver>` (pool.rs:26, 41-54; published
+    by renderer.rs:179-204), so a slow tile never holds up the others.  Across GPUs the shared
+    receiver is a counter in the process group's key-value store: `claim()` takes the next chunk
+    of `chunk` tiles with one atomic `add` (no collective, nothing on the data path) and returns
+    its tile indices, or [] once every tile has been handed out.  Every tile goes to exactly one
+    rank; since each task carries its own seed (renderer.rs:196-203) the film does not depend on
+    which rank renders which tile.
+
+    All ranks must construct their queues in the same order (one per render): the store key is
+    numbered by a per-process generation counter.  `chunk` defaults to an eighth of one rank's
+    static share, so a rank that falls behind gives up at most 1/8 of a share."""
+
+    def __init__(self, width, height, world_size, chunk=None, store=None):
+        global _queue_generation
+        if store is None:
+            import torch.distributed as dist
+            store = dist.distributed_c10d._get_default_store()
+        self.n_tiles = tiles_per_batch(width, height)
+        if chunk is None:
+            chunk = max(1, self.n_tiles // (8 * max(1, world_size)))
+        if chunk < 1:
+            raise ValueError(f"chunk {chunk} < 1")
+        self.chunk = int(chunk)
+        self.store = store
+        _queue_generation += 1
+        self.key = f"lumo_amd/tile_queue/{_queue_generation}"
+
+    def claim(self):
+        # store.add returns the counter after the increment: this claim owns [end - chunk, end)
+        end = int(self.store.add(self.key, self.chunk))
+        lo = end - self.chunk
+        if lo >= self.n_tiles:
+            return []
+        return list(range(lo, min(end, self.n_tiles)))
+
+    def __iter__(self):
+        while True:
+            tiles = self.claim()
+            if not tiles:
+                return
+            yield tiles
 
 
 def reduce_film(film, group=None, dst=None):

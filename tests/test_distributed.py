@@ -121,3 +121,108 @@ def test_gpu_renderer_sharded_equals_single(integrator, tmp_path):
     for r in range(2):
         np.testing.assert_array_equal(np.load(tmp_path / f"film{r}.npy"), single.pixels)
         np.testing.assert_allclose(np.load(tmp_path / f"splats{r}.npy"), single.splats, rtol=0, atol=1e-12)
+
+
+def test_tile_queue_hands_out_every_tile_once():
+    """TileQueue over one store: interleaved claims from two queues (two ranks) cover every tile
+    exactly once, in chunks, and a later queue (the next render) starts from tile 0 again."""
+    import torch.distributed as dist
+    from lumo_amd.dist import TileQueue, tiles_per_batch
+    store = dist.HashStore()
+    n = tiles_per_batch(W, H)
+    qs = [TileQueue(W, H, 2, chunk=2, store=store) for _ in range(2)]
+    qs[1].key = qs[0].key  # the ranks' queues of one render share a key
+    got = []
+    while True:
+        a, b = qs[0].claim(), qs[1].claim()
+        got += a + b
+        if not a and not b:
+            break
+        assert len(a) <= 2 and len(b) <= 2
+    assert sorted(got) == list(range(n))
+    nxt = TileQueue(W, H, 2, chunk=5, store=store)
+    assert nxt.claim() == list(range(5))
+    assert TileQueue(W, H, 2, store=store).chunk == max(1, n // 16)
+    with pytest.raises(ValueError):
+        TileQueue(W, H, 2, chunk=0, store=store)
+
+
+def _dyn_worker(rank, ws, port, out_dir, integrator):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    import lumo_amd as L
+    from lumo_amd.dist import TileQueue, reduce_film, tasks_of_tiles
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+    tasks = L.make_tasks(W, H, SPP, SEED)
+    film = L.Film(W, H, samples=SPP)
+    rays = n_tasks = 0
+    for tiles in TileQueue(W, H, ws, chunk=1):
+        mine = tasks_of_tiles(tasks, W, H, tiles)
+        part, r = _render(mine, integrator)
+        film.pixels += part.pixels
+        film.splats += part.splats
+        rays += r
+        n_tasks += len(mine)
+    total = reduce_film(film)
+    np.save(os.path.join(out_dir, f"film{rank}.npy"), total.pixels)
+    np.save(os.path.join(out_dir, f"splats{rank}.npy"), total.splats)
+    np.save(os.path.join(out_dir, f"rays{rank}.npy"), np.array([rays, n_tasks]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("integrator", [0, 1], ids=["pathtrace", "bdpt"])
+def test_dynamic_queue_render_equals_single(integrator, tmp_path):
+    """Tiles claimed one at a time from the shared TileQueue by two gloo ranks, rendered through
+    the oracle and summed with reduce_film: the single-process film (pixels exact)."""
+    import lumo_amd as L
+    ws = 2
+    _spawn(_dyn_worker, ws, str(tmp_path), integrator)
+    tasks = L.make_tasks(W, H, SPP, SEED)
+    film, rays = _render(list(tasks), integrator)
+    parts = [np.load(tmp_path / f"rays{r}.npy") for r in range(ws)]
+    assert sum(int(p[1]) for p in parts) == len(tasks)
+    assert sum(int(p[0]) for p in parts) == rays
+    for r in range(ws):
+        np.testing.assert_array_equal(np.load(tmp_path / f"film{r}.npy"), film.pixels)
+        np.testing.assert_allclose(np.load(tmp_path / f"splats{r}.npy"), film.splats, rtol=0, atol=1e-12)
+
+
+def _gpu_dyn_worker(rank, ws, port, out_dir, integrator):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    import lumo_amd as L
+    from lumo_amd.dist import reduce_film
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+    sc, cam = _scene(integrator)
+    r = L.Renderer(sc, cam).samples(SPP).seed(SEED).integrator(
+        L.Integrator.BDPathTrace if integrator else L.Integrator.PathTrace)
+    total = reduce_film(r.render(rank, ws, schedule="dynamic", chunk=3))
+    np.save(os.path.join(out_dir, f"film{rank}.npy"), total.pixels)
+    np.save(os.path.join(out_dir, f"splats{rank}.npy"), total.splats)
+    np.save(os.path.join(out_dir, f"tasks{rank}.npy"), np.array([r.tasks_rendered]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("integrator", [0, 1], ids=["pathtrace", "bdpt"])
+def test_gpu_renderer_dynamic_equals_single(integrator, tmp_path):
+    """Renderer.render(rank, 2, schedule="dynamic") on both ranks + reduce_film ==
+    Renderer.render() in one process."""
+    import lumo_amd as L
+    _spawn(_gpu_dyn_worker, 2, str(tmp_path), integrator)
+    sc, cam = _scene(integrator)
+    single = L.Renderer(sc, cam).samples(SPP).seed(SEED).integrator(
+        L.Integrator.BDPathTrace if integrator else L.Integrator.PathTrace).render()
+    assert sum(int(np.load(tmp_path / f"tasks{r}.npy")[0]) for r in range(2)) == len(L.make_tasks(W, H, SPP, SEED))
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"film{r}.npy"), single.pixels)
+        np.testing.assert_allclose(np.load(tmp_path / f"splats{r}.npy"), single.splats, rtol=0, atol=1e-12)
+
+
+def test_render_rejects_unknown_schedule():
+    import lumo_amd as L
+    r = L.Renderer(L.Scene.cornell_box(), L.Camera.cornell_box((W, H))).samples(1).seed(1)
+    with pytest.raises(ValueError):
+        r.render(0, 2, schedule="round-robin")
