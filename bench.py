@@ -81,6 +81,10 @@ def main():
     ap.add_argument("--share", default=None,
                     help="R/N: render only rank R's share of an N-rank run (tile %% N == R) in this single "
                          "process, to time one rank's load of a multi-GPU run on one GPU")
+    ap.add_argument("--schedule", default="static", choices=["static", "dynamic"],
+                    help="multi-GPU tile distribution: tile %% N (static) or chunks claimed from a shared "
+                         "queue in the process group's store (dynamic, lumo_amd.dist.TileQueue)")
+    ap.add_argument("--chunk", type=int, default=None, help="tiles per claim of the dynamic schedule")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -123,7 +127,7 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
     return the JSON record (rank 0 fields complete)."""
     import lumo_amd as L
     from lumo_amd import _ffi
-    from lumo_amd.dist import shard_tasks, tiles_per_batch
+    from lumo_amd.dist import TileQueue, shard_tasks, tasks_of_tiles, tiles_per_batch
 
     scene, cam, (W, H), spp, wl = build_config(config, res, spp)
     bdpt = wl.get("integrator") == L.Integrator.BDPathTrace
@@ -169,7 +173,15 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
     barrier()
     t0 = time.perf_counter()
     q = cams = rays = 0
+    dynamic = getattr(args, "schedule", "static") == "dynamic" and ws > 1 and not share
     for _ in range(steps):
+        if dynamic:
+            # every rank builds one queue per timed frame, in the same order (TileQueue keys)
+            for tl in TileQueue(W, H, ws, chunk=args.chunk):
+                part = tasks_of_tiles(tasks, W, H, tl)
+                a, b, c = step((_ffi.TileTask * len(part))(*part))
+                q, cams, rays = q + a, cams + b, rays + c
+            continue
         a, b, c = step(mine_arr)
         q, cams, rays = q + a, cams + b, rays + c
     barrier()  # lumo_render_tiles returns only after its stream has drained
@@ -222,7 +234,7 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
                 "integrator": wl.get("integrator_name", "PathTrace (NEE + MIS + RR)"),
                 "seed": SEED,
                 "rng_mode": "wavefront (per-path Xorshiftr128+ streams; DESIGN.md §RNG)",
-                "parallelism": f"tiles sharded tile%{ws}",
+                "parallelism": (f"tiles from a shared queue, {ws} ranks" if dynamic else f"tiles sharded tile%{ws}"),
             },
             "msamples_per_s": round(cams / elapsed / 1e6, 3),
             "lumo_total_rays_per_s_M": round(rays / elapsed / 1e6, 3),
