@@ -142,7 +142,7 @@ def test_tile_queue_hands_out_every_tile_once():
     assert sorted(got) == list(range(n))
     nxt = TileQueue(W, H, 2, chunk=5, store=store)
     assert nxt.claim() == list(range(5))
-    assert TileQueue(W, H, 2, store=store).chunk == max(1, n // 16)
+    assert TileQueue(W, H, 2, store=store).chunk == max(1, n // 4)
     with pytest.raises(ValueError):
         TileQueue(W, H, 2, chunk=0, store=store)
 
