@@ -168,7 +168,7 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
 
     for _ in range(warmup):
         step(warm_arr)
-    lib.lumo_set_timing(1)
+    dev.set_option("timing", 1)
     lib.lumo_stats_reset(dev.ctx)
     barrier()
     t0 = time.perf_counter()
@@ -186,7 +186,7 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
         q, cams, rays = q + a, cams + b, rays + c
     barrier()  # lumo_render_tiles returns only after its stream has drained
     elapsed = time.perf_counter() - t0
-    lib.lumo_set_timing(0)
+    dev.set_option("timing", 0)
     st = dev.stats()
     # busy time (union of launch intervals) of every stage and of the roofline units
     busy = {name: dev.busy_ms(stages) for name, stages in UNIT_STAGES.items()}

@@ -4,8 +4,10 @@
  * Every entry point names the reference interface it replaces (paths relative to the
  * lumo source tree).  Plain C: fixed-width integers, doubles, pointers and sizes only.
  * All calls return lumo_status (0 = OK); no exceptions cross the ABI.  A context is
- * bound to one GPU and is thread-compatible (one host thread per context; contexts on
- * different GPUs may be driven concurrently).
+ * bound to one GPU and owns all of its state (device buffers, streams, options, timers):
+ * contexts share nothing mutable, so different contexts, on the same GPU or on different
+ * ones, may be driven concurrently from different host threads; one context is used by one
+ * thread at a time.
  */
 #ifndef LUMO_AMD_H
 #define LUMO_AMD_H
@@ -17,7 +19,7 @@
 extern "C" {
 #endif
 
-#define LUMO_ABI_VERSION 7
+#define LUMO_ABI_VERSION 8
 
 typedef int32_t lumo_status;
 enum {
@@ -294,7 +296,7 @@ typedef struct {
     int32_t* prim;   /* triangle index (global)                                        */
 } lumo_hit_soa;
 
-/* Per-stage device time (HIP events; only with LUMO_TIMING=1 in the environment), launch
+/* Per-stage device time (HIP events; only with LUMO_OPT_TIMING on), launch
  * counts, query counts and traversal counters (AABB slab tests, kd split-node visits,
  * triangle tests) of the closest-hit [0] and shadow / connection [1] kernels, summed over
  * renders.  BDPT: CLOSEST + SHADE are the subpath walks, RESOLVE the re-runs + fold, BD_* the
@@ -356,8 +358,71 @@ lumo_status lumo_stats_reset(void* ctx);
  * length of the union of their launches' intervals.  kernel_ms sums launch durations, which counts
  * twice the time that launches on concurrent streams overlap (pipelined passes); this does not. */
 lumo_status lumo_stats_busy_ms(void* ctx, uint32_t stage_mask, double* ms);
-/* Enable per-launch HIP-event timing of every stage (also LUMO_TIMING=1). */
-void lumo_set_timing(int on);
+/* ---------------------------------------------------------------------------------
+ * Per-context execution options.  Every option changes only how the work is scheduled on the
+ * device, never a result: all values give bit-identical films, counters and traces.  Options are
+ * state of the context, so contexts (on one GPU or on several) driven from different host
+ * threads do not interfere (lumo's executors share nothing but the task receiver, pool.rs:17-38).
+ * A context starts from the defaults below, overridden by the environment variable named beside
+ * each (read once, in lumo_create).  Options marked "upload" take effect at the next
+ * lumo_scene_upload.  lumo_set_option returns LUMO_ERR_INVALID for an unknown option or a value
+ * out of range.
+ * ------------------------------------------------------------------------------- */
+enum {
+    LUMO_OPT_TIMING = 0,       /* per-launch HIP-event timing of every stage: 0 / 1 (LUMO_TIMING, 0)   */
+    LUMO_OPT_LDS_STAGING,      /* stage a scene of <= 48 KiB whole in LDS: 0 / 1 (LUMO_LDS, 1)          */
+    LUMO_OPT_TOP_STAGING,      /* TOP staging of larger scenes: 0 / 1 (LUMO_TOP, 1)                    */
+    LUMO_OPT_FUSED,            /* n_shadow = 1: -1 fused bounce when LDS-staged, 0 three kernels,
+                                  1 fused (LUMO_FUSED, -1)                                          */
+    LUMO_OPT_TAIL_BELOW,       /* n_shadow = 1: tail kernel below this many live paths, 0 never
+                                  (LUMO_TAIL, 262144)                                               */
+    LUMO_OPT_PIPELINE,         /* passes overlapped: 0 off, fused bounces 1-3 head streams, split
+                                  schedule on when > 0 (LUMO_PIPELINE, 3)                            */
+    LUMO_OPT_HEADS,            /* fused pipeline: bounces per pass on its head stream, 0 auto
+                                  (LUMO_HEADS, 0)                                                   */
+    LUMO_OPT_MERGE_PASSES,     /* fused pipeline: consecutive passes whose cameras and head bounces
+                                  run as one queue, 0 auto, 1-8 (LUMO_MERGE, 0)                      */
+    LUMO_OPT_DYN_FETCH,        /* fused bounce: blocks fetch paths from a counter: 0 / 1 (LUMO_DYN, 1)*/
+    LUMO_OPT_BOUNCE_THREADS,   /* fused bounce: threads per block 64 / 128 / 256
+                                  (LUMO_BOUNCE_THREADS, 256)                                        */
+    LUMO_OPT_SPLIT_PIPE,       /* split schedule: units in flight 1-4 (LUMO_SPLIT_PIPE, 4)           */
+    LUMO_OPT_SPLIT_GROUPS,     /* split schedule: independent task groups 1-4 (LUMO_SPLIT_GROUPS, 2) */
+    LUMO_OPT_BDPT_TAIL,        /* BDPT: walk-tail kernel below this many live subpaths, 0 never
+                                  (LUMO_BDPT_TAIL, 65536)                                           */
+    LUMO_OPT_BOUNCE_AHEAD,     /* bounces enqueued ahead of the host's count snapshots 1-63
+                                  (LUMO_BOUNCE_AHEAD, 3)                                            */
+    LUMO_OPT_LDS_GRID,         /* persistent grid cap of LDS-staged kernels (LUMO_LDS_GRID, 2048)    */
+    LUMO_OPT_TOP_GRID,         /* grid cap of TOP kernels (LUMO_TOP_GRID, the device's CU count)     */
+    LUMO_OPT_TOP_KB,           /* upload: TOP set budget in KiB, <= the CU's LDS (LUMO_TOP_KB)       */
+    LUMO_OPT_KD_LDS,           /* upload: kd stack entries per thread in LDS in TOP kernels
+                                  (LUMO_KD_LDS, 8)                                                  */
+    LUMO_OPT_STACK_CLASS,      /* upload: kd stack class override, 0 auto; never below the scene's
+                                  need (LUMO_STACK_CLASS, 0)                                        */
+    LUMO_OPT_FULL_KERNELS,     /* upload: general feature kernels even for lean scenes: 0 / 1
+                                  (LUMO_FULL_KERNELS, 0)                                            */
+    LUMO_OPT_POISON,           /* debug: fill every newly allocated device buffer with 0xFF bytes,
+                                  so a read of a buffer before its first write shows (LUMO_POISON, 0)*/
+    LUMO_OPT_COUNT
+};
+lumo_status lumo_set_option(void* ctx, int32_t option, int64_t value);
+lumo_status lumo_get_option(void* ctx, int32_t option, int64_t* value);
+
+/* The schedule the last lumo_render_tiles call used (after its last max_paths chunk): which
+ * pass loop ran and with how many streams, units, groups and merged passes.  Lets callers and
+ * tests check that a requested schedule was not cut back (free HBM bounds the split schedule's
+ * units in flight). */
+enum { LUMO_SCHED_SEQUENTIAL = 0, LUMO_SCHED_FUSED_PIPELINE = 1, LUMO_SCHED_SPLIT_PIPELINE = 2 };
+typedef struct {
+    int32_t schedule;        /* LUMO_SCHED_*                                               */
+    int32_t head_streams;    /* fused pipeline: head streams                               */
+    int32_t head_bounces;    /* fused pipeline: bounces per pass on the head stream        */
+    int32_t merged_passes;   /* fused pipeline: passes per head unit                       */
+    int32_t units_in_flight; /* split pipeline: (group, pass) units in flight              */
+    int32_t task_groups;     /* split pipeline: independent task groups                    */
+    int32_t fused;           /* 1: fused bounce kernel, 0: three kernels per bounce         */
+    int32_t pad0;
+} lumo_schedule_info;
+lumo_status lumo_last_schedule(void* ctx, lumo_schedule_info* info);
 
 /* Test hook: render one task in the wavefront order and dump every path. */
 lumo_status lumo_debug_paths(void* ctx, const lumo_tile_task* task, lumo_path_dump* dump);
@@ -384,28 +449,6 @@ lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info);
  * (kernels k_calib_read8 / k_calib_write8), to calibrate rocprofv3 FETCH_SIZE / WRITE_SIZE for
  * the access width of the path kernels. */
 lumo_status lumo_debug_stream(void* ctx, size_t n);
-/* Perf switch: stage the packed scene in LDS inside the traversal kernels (default on; also
- * LUMO_LDS=0 in the environment). */
-void lumo_set_lds_staging(int on);
-/* Perf switch (path tracer, one light sample per bounce).  fused = 0: each bounce is three
- * kernels (closest hit / shading / visibility); fused = 1: one kernel (closest hit + shading +
- * the NEE pair traced from registers); fused = -1 (default): fused when the scene is staged in
- * LDS (small scenes), else three kernels.  Bounces are preceded by a tail kernel that takes the
- * bounce instead when fewer than tail_below paths are alive and runs each of them to its end in
- * that launch (tail_below = 0: never; default 262144).  pipeline (with fused bounces): 1 each
- * pass runs its first bounces on a head stream and hands the rest (tail kernel, film, ring) to a
- * second stream while the next pass starts; 2 or 3 (default 3) rotate that many head streams so
- * consecutive passes' first bounces also overlap; 0 off (also for the split schedule, which
- * otherwise keeps up to LUMO_SPLIT_PIPE = 4 passes in flight on four streams when HBM allows).
- * Every mode gives bit-identical results.
- * Also LUMO_FUSED / LUMO_TAIL / LUMO_PIPELINE in the environment. */
-void lumo_set_bounce_mode(int fused, uint32_t tail_below, int pipeline);
-/* Perf switch (bidirectional path tracer): once fewer than 4 * below subpaths of a walk are alive
- * the host launches a walk-tail kernel ahead of each bounce; when fewer than `below` are alive (the
- * exact count, read on the device) it runs every remaining light / camera subpath to its end in
- * that launch and the bounce kernels skip (below = 0: never; default 65536).  Bit-identical.
- * Also LUMO_BDPT_TAIL in the environment. */
-void lumo_set_bdpt_tail(uint32_t below);
 
 #ifdef __cplusplus
 }

@@ -694,7 +694,7 @@ class Film:
 class Device:
     """One lumo_amd context bound to one GPU (lumo_create)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, **options):
         L = lib()
         ctx = C.c_void_p()
         st = L.lumo_create(device, C.byref(ctx))
@@ -702,6 +702,8 @@ class Device:
             raise RuntimeError(f"lumo_create(device={device}) failed: {L.lumo_status_str(st).decode()}")
         self.ctx = ctx
         self.scene = None
+        for k, v in options.items():  # execution options (LUMO_OPT_*), e.g. Device(0, split_pipe=1)
+            self.set_option(k, v)
 
     def upload(self, scene, camera=None):
         L = lib()
@@ -813,6 +815,23 @@ class Device:
         check(lib().lumo_stats_busy_ms(self.ctx, mask, C.byref(ms)), "stats_busy_ms")
         return ms.value
 
+    def set_option(self, name, value):
+        """lumo_set_option: one of _ffi.OPTIONS (LUMO_OPT_*); scheduling only, results unchanged."""
+        check(lib().lumo_set_option(self.ctx, _ffi.OPT[name], int(value)), f"set_option({name}={value})")
+        return self
+
+    def option(self, name):
+        v = C.c_int64(0)
+        check(lib().lumo_get_option(self.ctx, _ffi.OPT[name], C.byref(v)), f"get_option({name})")
+        return v.value
+
+    def last_schedule(self):
+        """lumo_last_schedule: the pass loop, streams, units, groups and merged passes of the last
+        render_tasks call."""
+        s = _ffi.ScheduleInfo()
+        check(lib().lumo_last_schedule(self.ctx, C.byref(s)), "last_schedule")
+        return s
+
     def close(self):
         if getattr(self, "ctx", None):
             lib().lumo_destroy(self.ctx)
@@ -881,7 +900,13 @@ class Renderer:
         if schedule not in ("static", "dynamic"):
             raise ValueError(f"unknown schedule {schedule!r}")
         if self._seed is None:
-            self._seed = time.time_ns() & 0xFFFFFFFFFFFFFFFF or 1
+            seed = [time.time_ns() & 0xFFFFFFFFFFFFFFFF or 1]
+            if world_size > 1:  # every rank must render its tiles with the same task seeds
+                import torch.distributed as dist
+                if not dist.is_initialized():
+                    raise ValueError("Renderer.render(rank, world_size > 1): set .seed() or initialise torch.distributed")
+                dist.broadcast_object_list(seed, src=0)  # rank 0's seed
+            self._seed = seed[0]
         w, h = self.camera.resolution
         tasks = make_tasks(w, h, self._samples, self._seed)
         from .dist import TileQueue, shard_tasks, tasks_of_tiles

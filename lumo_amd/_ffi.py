@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 7  # include/lumo_amd.h LUMO_ABI_VERSION
+ABI_VERSION = 8  # include/lumo_amd.h LUMO_ABI_VERSION
 LIB_PATH = os.environ.get("LUMO_AMD_LIB") or os.path.join(_HERE, "liblumo_amd.so")
 
 c_double_p = C.POINTER(C.c_double)
@@ -161,6 +161,20 @@ class Stats(C.Structure):
                 ("shadow_resolved", C.c_uint64)]
 
 
+class ScheduleInfo(C.Structure):
+    _fields_ = [("schedule", C.c_int32), ("head_streams", C.c_int32), ("head_bounces", C.c_int32),
+                ("merged_passes", C.c_int32), ("units_in_flight", C.c_int32), ("task_groups", C.c_int32),
+                ("fused", C.c_int32), ("pad0", C.c_int32)]
+
+
+SCHED_SEQUENTIAL, SCHED_FUSED_PIPELINE, SCHED_SPLIT_PIPELINE = range(3)
+# LUMO_OPT_* (include/lumo_amd.h), by the name Device.set_option takes
+OPTIONS = ["timing", "lds_staging", "top_staging", "fused", "tail_below", "pipeline", "heads", "merge_passes",
+           "dyn_fetch", "bounce_threads", "split_pipe", "split_groups", "bdpt_tail", "bounce_ahead", "lds_grid",
+           "top_grid", "top_kb", "kd_lds", "stack_class", "full_kernels", "poison"]
+OPT = {name: i for i, name in enumerate(OPTIONS)}
+
+
 class CameraParams(C.Structure):
     _fields_ = [("origin", C.c_double * 3), ("towards", C.c_double * 3), ("up", C.c_double * 3),
                 ("zoom", C.c_double), ("lens_radius", C.c_double), ("focal_length", C.c_double),
@@ -190,10 +204,9 @@ DEVICE_API = [
     ("lumo_stats_get", C.c_int32, [C.c_void_p, C.POINTER(Stats)]),
     ("lumo_stats_reset", C.c_int32, [C.c_void_p]),
     ("lumo_stats_busy_ms", C.c_int32, [C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]),
-    ("lumo_set_timing", None, [C.c_int]),
-    ("lumo_set_lds_staging", None, [C.c_int]),
-    ("lumo_set_bounce_mode", None, [C.c_int, C.c_uint32, C.c_int]),
-    ("lumo_set_bdpt_tail", None, [C.c_uint32]),
+    ("lumo_set_option", C.c_int32, [C.c_void_p, C.c_int32, C.c_int64]),
+    ("lumo_get_option", C.c_int32, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]),
+    ("lumo_last_schedule", C.c_int32, [C.c_void_p, C.POINTER(ScheduleInfo)]),
     ("lumo_debug_stream", C.c_int32, [C.c_void_p, C.c_size_t]),
     ("lumo_scene_info", C.c_int32, [C.c_void_p, C.POINTER(SceneInfo)]),
     ("lumo_debug_set_integrator", C.c_int32, [C.c_void_p, C.c_int]),

@@ -122,88 +122,96 @@ __device__ __forceinline__ uint64_t wf_path_seed(uint64_t pixel_seed, uint64_t k
     return splitmix64(pixel_seed ^ splitmix64(k + 1));
 }
 
-// ------------------------------------------------------------------ camera (pass `pass`)
+// ------------------------------------------------------------------ camera (passes pass0 .. pass0 + npass - 1)
 // QUEUE (path tracer): the camera paths enter the queue-order state qs[0]; otherwise (BDPT) the
 // ray, throughput, wavelengths and RNG stay per slot and the slot ids are queued in q0.
+// npass > 1 (merged passes of the fused pipeline, render_pipelined): each thread generates its
+// slot's samples of npass consecutive passes in pass order (the sampler state is per slot), and
+// the path of pass pass0 + m carries the virtual slot s + m * vstride, where that pass's per-slot
+// outputs (raster, validity, final radiance, ...) live.
 template <bool QUEUE>
-__global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, int n, int dim_stride, uint32_t pass,
-                                                  int s0) {
+__global__ __launch_bounds__(BLOCK) void k_camera(Tasks T, Paths S, DCam cam, int n, int dim_stride, uint32_t pass0,
+                                                  int s0, int npass, int vstride) {
     const int s = s0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);  // slots [s0, n)
-    bool active = false;
-    Ray ray{V3{0, 0, 0}, V3{0, 0, 0}};
-    double L[NS] = {0.0, 0.0, 0.0, 0.0};
-    Xorshift r{0, 0};
-    int task = 0;
-    if (s < n) {
-        task = S.task[s];
-        const lumo_tile_task& t = T.t[task];
-        active = pass < t.samples;
-        S.p_valid[s] = active ? 1u : 0u;
-        if (active) {
-            Xorshift mr{S.mj_rng[2 * s], S.mj_rng[2 * s + 1]};
-            const uint64_t st = S.mj_state[s];
-            const uint16_t* px = S.perm + (size_t)s * 2 * dim_stride;
-            const V2 rs = sampler_next(T.sampler, t, px, px + dim_stride, st, mr, S.pseed[s]);
-            S.mj_state[s] = st + 1;
-            S.mj_rng[2 * s] = mr.hi;
-            S.mj_rng[2 * s + 1] = mr.lo;
-            const int j = S.pix[s];
-            const uint64_t W = t.px_max[0] - t.px_min[0];
-            const V2 xy = V2{(double)(t.px_min[0] + (uint64_t)j % W), (double)(t.px_min[1] + (uint64_t)j / W)};
-            const V2 raster = xy + rs;
-            // Integrator::integrate: lens sample (2 draws), then wavelengths (1 draw)
-            r = xs_new(wf_path_seed(S.pseed[s], pass));
-            const V2 lens = xs_vec2(r);
-            const V3 screen = xf_pt_inv(cam.sctr, V3{raster.x, raster.y, 0.0});
-            // Camera::generate_ray (camera.rs:257-268): Perspective aims from the origin through the
-            // normalised camera-space point; Orthographic starts at the point, along +z
-            const V3 cpt = xf_pt_inv(cam.cts, screen);
-            const V3 wl0 = cam.orthographic ? V3{0.0, 0.0, 1.0} : normalize(cpt);
-            V3 xo_local = cam.orthographic ? cpt : V3{0, 0, 0}, wi_local = wl0;
-            if (cam.lens_radius != 0.0) {  // camera.rs:221-243
-                const V2 lxy = cam.lens_radius * square_to_disk(lens);
-                const V3 lz = V3{lxy.x, lxy.y, 0.0};
-                const V3 focus = (cam.focal_length / wl0.z) * wl0;
-                xo_local = xo_local + lz;
-                wi_local = focus - lz;
-            }
-            ray = ray_new(xf_pt_inv(cam.wtc, xo_local), xf_dir_inv(cam.wtc, wi_local));
-            wl_sample(xs_float(r), L);
-            S.raster[2 * s] = raster.x;
-            S.raster[2 * s + 1] = raster.y;
-            if (!QUEUE) {
-                stv3(S.ro, s, ray.o);
-                stv3(S.rd, s, ray.d);
-                stc(S.gath, s, cfill(1.0));
-                stc(S.rad, s, cfill(0.0));
-                for (int i = 0; i < NS; ++i) S.lam[4 * s + i] = L[i];
-                S.rng[2 * s] = r.hi;
-                S.rng[2 * s + 1] = r.lo;
-                S.depth[s] = 0;
-                S.flags[s] = 1u;  // last_specular
-                S.queries[s] = 0;
+    for (int m = 0; m < npass; ++m) {
+        const uint32_t pass = pass0 + (uint32_t)m;
+        const int v = s + m * vstride;  // virtual slot of this pass
+        bool active = false;
+        Ray ray{V3{0, 0, 0}, V3{0, 0, 0}};
+        double L[NS] = {0.0, 0.0, 0.0, 0.0};
+        Xorshift r{0, 0};
+        int task = 0;
+        if (s < n) {
+            task = S.task[s];
+            const lumo_tile_task& t = T.t[task];
+            active = pass < t.samples;
+            S.p_valid[v] = active ? 1u : 0u;
+            if (active) {
+                Xorshift mr{S.mj_rng[2 * s], S.mj_rng[2 * s + 1]};
+                const uint64_t st = S.mj_state[s];
+                const uint16_t* px = S.perm + (size_t)s * 2 * dim_stride;
+                const V2 rs = sampler_next(T.sampler, t, px, px + dim_stride, st, mr, S.pseed[s]);
+                S.mj_state[s] = st + 1;
+                S.mj_rng[2 * s] = mr.hi;
+                S.mj_rng[2 * s + 1] = mr.lo;
+                const int j = S.pix[s];
+                const uint64_t W = t.px_max[0] - t.px_min[0];
+                const V2 xy = V2{(double)(t.px_min[0] + (uint64_t)j % W), (double)(t.px_min[1] + (uint64_t)j / W)};
+                const V2 raster = xy + rs;
+                // Integrator::integrate: lens sample (2 draws), then wavelengths (1 draw)
+                r = xs_new(wf_path_seed(S.pseed[s], pass));
+                const V2 lens = xs_vec2(r);
+                const V3 screen = xf_pt_inv(cam.sctr, V3{raster.x, raster.y, 0.0});
+                // Camera::generate_ray (camera.rs:257-268): Perspective aims from the origin through the
+                // normalised camera-space point; Orthographic starts at the point, along +z
+                const V3 cpt = xf_pt_inv(cam.cts, screen);
+                const V3 wl0 = cam.orthographic ? V3{0.0, 0.0, 1.0} : normalize(cpt);
+                V3 xo_local = cam.orthographic ? cpt : V3{0, 0, 0}, wi_local = wl0;
+                if (cam.lens_radius != 0.0) {  // camera.rs:221-243
+                    const V2 lxy = cam.lens_radius * square_to_disk(lens);
+                    const V3 lz = V3{lxy.x, lxy.y, 0.0};
+                    const V3 focus = (cam.focal_length / wl0.z) * wl0;
+                    xo_local = xo_local + lz;
+                    wi_local = focus - lz;
+                }
+                ray = ray_new(xf_pt_inv(cam.wtc, xo_local), xf_dir_inv(cam.wtc, wi_local));
+                wl_sample(xs_float(r), L);
+                S.raster[2 * v] = raster.x;
+                S.raster[2 * v + 1] = raster.y;
+                if (!QUEUE) {
+                    stv3(S.ro, s, ray.o);
+                    stv3(S.rd, s, ray.d);
+                    stc(S.gath, s, cfill(1.0));
+                    stc(S.rad, s, cfill(0.0));
+                    for (int i = 0; i < NS; ++i) S.lam[4 * s + i] = L[i];
+                    S.rng[2 * s] = r.hi;
+                    S.rng[2 * s + 1] = r.lo;
+                    S.depth[s] = 0;
+                    S.flags[s] = 1u;  // last_specular
+                    S.queries[s] = 0;
+                }
             }
         }
-    }
-    if (QUEUE) {
-        const uint32_t q = block_slot(active, S.counts + CNT_NEXT);
-        if (active) {
-            const QState& Q = S.qs[0];
-            qv3(Q, QD_O, q, ray.o);
-            qv3(Q, QD_D, q, ray.d);
-            qc(Q, QD_G, q, cfill(1.0));
-            qc(Q, QD_R, q, cfill(0.0));
-            for (int i = 0; i < NS; ++i) Q.D(QD_L + i, q) = L[i];
-            Q.R(0, q) = r.hi;
-            Q.R(1, q) = r.lo;
-            Q.I(QI_SLOT, q) = s;
-            Q.I(QI_TASK, q) = task;
-            Q.I(QI_DEPTH, q) = 0;
-            Q.I(QI_FLAGS, q) = QF_SPECULAR;  // last_specular starts true (path_trace.rs:14)
-            Q.I(QI_QUERIES, q) = 0;
+        if (QUEUE) {
+            const uint32_t q = block_slot(active, S.counts + CNT_NEXT);
+            if (active) {
+                const QState& Q = S.qs[0];
+                qv3(Q, QD_O, q, ray.o);
+                qv3(Q, QD_D, q, ray.d);
+                qc(Q, QD_G, q, cfill(1.0));
+                qc(Q, QD_R, q, cfill(0.0));
+                for (int i = 0; i < NS; ++i) Q.D(QD_L + i, q) = L[i];
+                Q.R(0, q) = r.hi;
+                Q.R(1, q) = r.lo;
+                Q.I(QI_SLOT, q) = v;
+                Q.I(QI_TASK, q) = task;
+                Q.I(QI_DEPTH, q) = 0;
+                Q.I(QI_FLAGS, q) = QF_SPECULAR;  // last_specular starts true (path_trace.rs:14)
+                Q.I(QI_QUERIES, q) = 0;
+            }
+        } else {
+            block_append(active, s, S.q0, S.counts + CNT_NEXT);
         }
-    } else {
-        block_append(active, s, S.q0, S.counts + CNT_NEXT);
     }
 }
 
@@ -227,7 +235,12 @@ struct ZeroList {
     uint32_t* p[MAX];
     uint64_t words[MAX];
     int n = 0;
+    bool overflow = false;  // more than MAX buffers added: the caller fails instead of launching
     void add(void* ptr, size_t bytes) {
+        if (n == MAX) {
+            overflow = true;
+            return;
+        }
         p[n] = static_cast<uint32_t*>(ptr);
         words[n] = bytes / 4;
         ++n;
@@ -237,6 +250,11 @@ __global__ __launch_bounds__(BLOCK) void k_zero_list(ZeroList z) {
     const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
     for (int k = 0; k < z.n; ++k)
         for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < z.words[k]; i += stride) z.p[k][i] = 0u;
+}
+
+// The tail kernel's fetch counter zeroed between the passes of a merged unit (render_pipelined).
+__global__ void k_zero_fetch(uint32_t* counts) {
+    if (threadIdx.x == 0) counts[CNT_FETCH_T] = 0u;
 }
 
 // Queue counters (and optionally one more word) zeroed in-stream: a kernel instead of a fill.
@@ -626,8 +644,71 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+// Per-launch HIP event pairs, resolved at the synchronisation points the host loop already
+// has (queue-count readbacks), so timing adds no extra stalls.
+struct Timing {
+    std::vector<hipEvent_t> free_ev;
+    struct Pending {
+        int stage;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    hipEvent_t get() {
+        if (free_ev.empty()) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            return e;
+        }
+        hipEvent_t e = free_ev.back();
+        free_ev.pop_back();
+        return e;
+    }
+    ~Timing() {
+        for (hipEvent_t e : free_ev) (void)hipEventDestroy(e);
+        for (const Pending& p : pending) {
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+    }
+};
+
+// Merged passes of the fused pipeline (render_pipelined): at most MAX_MERGE passes per unit, by
+// default as many as bring a unit to about kMergeTarget paths (a full 1024^2 frame: 1).
+constexpr int MAX_MERGE = 8;
+constexpr uint64_t kMergeTarget = (uint64_t)1 << 21;
+
+// Execution options of a context (lumo_set_option; include/lumo_amd.h LUMO_OPT_*).  None of them
+// changes a result.  Defaults here, then the environment at lumo_create.
+struct Opts {
+    int timing = 0;
+    int lds = 1;                       // whole scene in LDS when it fits (48 KiB)
+    int top = 1;                       // TOP staging of larger scenes
+    int fused = -1;                    // n_shadow == 1: k_bounce_q instead of closest / shade / shadow (-1: when LDS-staged)
+    uint32_t tail_below = 1u << 18;    // n_shadow == 1: k_bounce_q tail mode below this many live paths
+    int pipeline = 3;                  // fused passes overlapped (render_pipelined): 0 off, else head streams (1-3)
+    int heads = 0;                     // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
+    int merge = 0;                     // pipelined passes: passes merged into one head unit (0: auto)
+    int dyn = 1;                       // k_bounce_q: blocks fetch their paths from a counter
+    int bounce_threads = BLOCK;        // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
+    int split_pipe = 4;                // split schedule: units in flight (render_split_pipelined; 1 = sequential)
+    int split_groups = 2;              // split schedule: independent task groups
+    uint32_t bdpt_tail = 1u << 16;     // BDPT walks: k_bdpt_tail below this many live subpaths (0: never)
+    int bounce_ahead = 3;              // bounces enqueued ahead of the host's count snapshots
+    int lds_grid = 2048;               // persistent grid cap of the LDS-staged kernels
+    int top_grid = 256;                // TOP kernels: blocks (one per CU; C3 shadow 438 ms per 8-spp frame vs 446 at
+                                       // four per CU, 817 at half the CUs); set to the CU count at creation
+    int top_kb = 160;                  // TOP set budget (KiB), at most the CU's LDS
+    int kd_lds = 8;                    // kd stack entries per thread in LDS in TOP kernels when room is left (C2 -3 %)
+    int stack_class = 0;               // kd stack class override (0: the scene's need)
+    int full_kernels = 0;              // general feature kernels for lean scenes too
+    int poison = 0;                    // new device buffers filled with 0xFF (reads before writes show as NaN / -1)
+};
+
 struct Ctx {
     int device = 0;
+    size_t lds_cu = 160 * 1024;     // LDS per CU (hipDeviceProp_t::maxSharedMemoryPerMultiProcessor)
+    size_t lds_block = 160 * 1024;  // LDS one block may allocate (sharedMemPerBlock)
+    Opts o;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // pipelined passes: each pass's tail, film and ring
     hipStream_t stream3 = nullptr;  // pipelined passes (2-3 head streams): further head streams
@@ -639,20 +720,14 @@ struct Ctx {
     std::vector<DevBuf> scene_bufs;
     std::vector<DevBuf> work;  // grown on demand
     lumo_stats stats{};
-    hipEvent_t ev[2 * ST_COUNT];
-    int lds_grid_cap = 2048;
-    // TOP-staged traversal kernels: blocks of TOP_BLOCK threads, one per CU (each holds a CU's LDS;
-    // C3 shadow 438 ms per 8-spp frame at one block per CU vs 446 at four, 817 at half the CUs)
-    int top_grid_cap = 256;  // set to the device's CU count at creation (LUMO_TOP_GRID)
-    int top_lds_bytes = 160 * 1024 - 256;  // TOP set budget (LUMO_TOP_KB)
-    int kd_lds = 8;  // kd stack entries per thread in LDS in TOP kernels when room is left (LUMO_KD_LDS; C2 frame -3 %)
+    lumo_schedule_info sched{};  // of the last render
+    Timing tm;
     int tone_map = LUMO_TONEMAP_NONE;  // of the lumo_render_tiles call in progress
     double tone_arg = 0.0;
     // per-bounce queue-count snapshots (pinned) and their completion events
     static constexpr int SNAP_RING = 64;
     uint32_t* snap = nullptr;
     hipEvent_t snap_ev[SNAP_RING];
-    int bounce_ahead = 3;
     // integrator of the call in progress (BDPT: vertex storage per subpath, optional splat film)
     int integrator = LUMO_INTEGRATOR_PATH_TRACE;
     int max_vertices = 64;
@@ -669,7 +744,7 @@ struct Ctx {
     std::vector<std::pair<float, float>> intervals[LUMO_STAGE_COUNT];
 };
 
-lumo_status dev_alloc(DevBuf& b, size_t bytes) {
+lumo_status dev_alloc(const Ctx& c, DevBuf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.bytes >= bytes) return LUMO_OK;
     if (b.p) (void)hipFree(b.p);
@@ -677,8 +752,7 @@ lumo_status dev_alloc(DevBuf& b, size_t bytes) {
     b.bytes = 0;
     if (hipMalloc(&b.p, bytes) != hipSuccess) return LUMO_ERR_OOM;
     b.bytes = bytes;
-    static const bool poison = std::getenv("LUMO_POISON") != nullptr;  // debug: new buffers all ones (NaN)
-    if (poison) (void)hipMemset(b.p, 0xFF, bytes);
+    if (c.o.poison) (void)hipMemset(b.p, 0xFF, bytes);  // debug: new buffers all ones (NaN, -1)
     return LUMO_OK;
 }
 
@@ -686,7 +760,7 @@ template <typename T>
 lumo_status upload(Ctx& c, const T* host, size_t count, const T** dptr) {
     c.scene_bufs.emplace_back();
     DevBuf& b = c.scene_bufs.back();
-    const lumo_status st = dev_alloc(b, sizeof(T) * count);
+    const lumo_status st = dev_alloc(c, b, sizeof(T) * count);
     if (st) return st;
     if (count && host) HIPCHK(hipMemcpy(b.p, host, sizeof(T) * count, hipMemcpyHostToDevice));
     *dptr = static_cast<const T*>(b.p);
@@ -725,35 +799,9 @@ enum WorkId {
 template <typename T>
 T* wbuf(Ctx& c, int id, size_t count, lumo_status& st) {
     if (c.work.size() < W_COUNT) c.work.resize(W_COUNT);
-    const lumo_status s = dev_alloc(c.work[id], sizeof(T) * count);
+    const lumo_status s = dev_alloc(c, c.work[id], sizeof(T) * count);
     if (s) st = s;
     return static_cast<T*>(c.work[id].p);
-}
-
-// Per-launch HIP event pairs, resolved at the synchronisation points the host loop already
-// has (queue-count readbacks), so timing adds no extra stalls.
-struct Timing {
-    std::vector<hipEvent_t> free_ev;
-    struct Pending {
-        Ctx* c;
-        int stage;
-        hipEvent_t a, b;
-    };
-    std::vector<Pending> pending;
-    hipEvent_t get() {
-        if (free_ev.empty()) {
-            hipEvent_t e;
-            (void)hipEventCreate(&e);
-            return e;
-        }
-        hipEvent_t e = free_ev.back();
-        free_ev.pop_back();
-        return e;
-    }
-};
-Timing& timing() {
-    static Timing t;
-    return t;
 }
 
 struct StageTimer {
@@ -765,8 +813,8 @@ struct StageTimer {
     StageTimer(Ctx& cc, bool enable, int st, hipStream_t stream = nullptr)
         : c(cc), on(enable), stage(st), sm(stream ? stream : cc.stream) {
         if (on) {
-            a = timing().get();
-            b = timing().get();
+            a = c.tm.get();
+            b = c.tm.get();
             if (!c.ref_recorded) {
                 if (!c.ref_ev) (void)hipEventCreate(&c.ref_ev);
                 (void)hipEventRecord(c.ref_ev, sm);
@@ -779,7 +827,7 @@ struct StageTimer {
     ~StageTimer() {
         if (on) {
             (void)hipEventRecord(b, sm);
-            timing().pending.push_back({&c, stage, a, b});
+            c.tm.pending.push_back({stage, a, b});
         }
     }
 };
@@ -787,10 +835,10 @@ struct StageTimer {
 // Adds the elapsed time of every completed timer pair; pairs still in flight stay pending (the
 // end of lumo_render_tiles synchronises, so all are resolved by its last call).
 void resolve_timers(Ctx& c) {
-    Timing& t = timing();
+    Timing& t = c.tm;
     std::vector<Timing::Pending> still;
     for (auto& p : t.pending) {
-        if (p.c != &c || hipEventQuery(p.b) != hipSuccess) {
+        if (hipEventQuery(p.b) != hipSuccess) {
             still.push_back(p);
             continue;
         }
@@ -827,8 +875,6 @@ double busy_ms(const Ctx& c, uint32_t mask) {
     return total;
 }
 
-bool g_timing = false;
-
 // Stack-class dispatch (launch.h STACK_CLASSES).
 template <typename F>
 void by_stack_class(int cls, F&& f) {
@@ -845,33 +891,18 @@ void by_stack_class(int cls, F&& f) {
 
 // Traversal launch: stack class x LDS staging.  With LDS staging the grid is capped (persistent
 // grid-stride loop) so each workgroup copies the packed scene once per launch.
-bool g_lds = true;
-int g_buckets = NB;  // LUMO_BUCKETS=0: NEE records not grouped by origin object
-int g_fused = -1;  // n_shadow == 1: k_bounce_q instead of closest / shade / shadow (-1: when the scene is LDS-staged)
-uint32_t g_tail_below = 1u << 18;  // n_shadow == 1: k_bounce_q tail mode below this many live paths
-int g_pipeline = 3;                // fused passes overlapped (render_pipelined): 0 off, else the number of head streams (1-3)
-int g_dyn = 1;                     // k_bounce_q: blocks fetch their paths from a counter
-int g_pipe_groups = 1;             // pipelined fused passes: independent task groups (1 or 2)
-uint32_t g_bdpt_tail = 1u << 16;    // BDPT walks: k_bdpt_tail below this many live subpaths (0: never)
-int g_bounce_threads = BLOCK;      // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
-int g_heads = 0;                   // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
-int g_split_pipe = 4;              // split schedule: passes in flight (render_split_pipelined; 1 = sequential)
-int g_split_groups = 2;            // split schedule: independent task groups (render_split_pipelined)
-int g_fused_split = 0;             // fused bounces through render_split_pipelined instead of render_pipelined
-int g_qsort = 0;                   // k_shade_q: next ray queue grouped per block (0 off, 1 object, 2 octant, 3 both)
 // allow_top: the kernel has a TOP-staged variant (k_closest_q, k_shadow_q); it is used when the
 // whole scene does not fit in LDS but its top levels were packed at upload (DScene::top).
-int g_top = 1;  // LUMO_TOP=0: no TOP staging
 template <typename F>
 void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr, bool allow_top = false) {
-    const bool lds = g_lds && c.sc.hot_bytes > 0;
-    const bool top = !lds && allow_top && g_top && c.sc.top_bytes > 0;
+    const bool lds = c.o.lds && c.sc.hot_bytes > 0;
+    const bool top = !lds && allow_top && c.o.top && c.sc.top_bytes > 0;
     const int grid_full = ceil_div(count, BLOCK);
-    TravLaunch l{lds ? std::min(grid_full, c.lds_grid_cap) : grid_full, lds ? (size_t)c.sc.hot_bytes : 0, lds,
+    TravLaunch l{lds ? std::min(grid_full, c.o.lds_grid) : grid_full, lds ? (size_t)c.sc.hot_bytes : 0, lds,
                  c.sc.full, stream ? stream : c.stream};
     if (top) {
         l.top = true;
-        l.grid = std::min(ceil_div(count, TOP_BLOCK), c.top_grid_cap);
+        l.grid = std::min(ceil_div(count, TOP_BLOCK), c.o.top_grid);
         l.shm = c.sc.top_shm;
     }
     by_stack_class(c.sc.stack_class, [&](auto K) { f(K, l); });
@@ -919,30 +950,41 @@ size_t split_set_bytes(const Paths& S, int N, int ns) {
            S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4 + (ns > 1 ? 16 : 0));
 }
 
+// Per-slot outputs of pass m of a merged unit (render_pipelined): virtual slots [m N, (m + 1) N).
+Paths pass_view(const Paths& P, int m, int N) {
+    Paths V = P;
+    const size_t o = (size_t)m * (size_t)N;
+    V.rad = P.rad + 4 * o;
+    V.lam = P.lam + 4 * o;
+    V.raster = P.raster + 2 * o;
+    V.depth = P.depth + o;
+    V.queries = P.queries + o;
+    V.p_valid = P.p_valid + o;
+    return V;
+}
+
 // Pipelined passes (n_shadow == 1, fused bounces).  Russian roulette reads the pass's adaptive
 // delta only from depth RR_DEPTH on (path_trace.rs:60-69), and that delta needs the previous
-// pass's film + ring.  So on stream A each pass runs its camera and its first RR_DEPTH + 1 bounces
-// as fused launches (waiting for the previous pass's ring only before bounce RR_DEPTH), then hands
-// its queue to stream B, which runs the tail kernel (every remaining path to its end), the film and
-// the ring; meanwhile A starts the next pass.  The latency-bound tail, film and ring of pass p thus
-// overlap the heavy first bounces of pass p + 1.  Each pass parity has its own queues, counters and
-// per-slot outputs; every per-path operation and every film / ring sum is the same as in the
-// sequential loop, so the result is bit-identical.
+// pass's film + ring.  So on a head stream each unit runs its camera and its first bounces as
+// fused launches, then hands its queue to stream B, which runs the tail kernel (every remaining
+// path to its end), the film and the ring; meanwhile the next unit starts.  The latency-bound
+// tail, film and ring of one unit thus overlap the heavy first bounces of the next.
+//
+// A unit is M consecutive passes (merged passes; M = 1 on a full frame).  Its camera kernel
+// generates every slot's samples of those passes in pass order and its head bounces run all of
+// their paths as one queue (M times the paths per launch: a rank's share of a multi-GPU frame
+// holds a few hundred thousand slots per pass, too few to keep the GPU busy).  With M > 1 the
+// head bounces stop before RR_DEPTH, so they read no delta; stream B then runs the unit's tails
+// pass by pass (the tail kernel takes only that pass's virtual slots), each followed by the
+// pass's film and ring, so every pass's Russian roulette sees the delta of the ring before it.
+//
+// NA head streams (1 to 3) rotate over the units, so consecutive units' first bounces also run
+// concurrently; NA + 1 sets of queues, counters and per-slot outputs, a set reused only after
+// the unit NA + 1 back has issued its ring.  Every per-path operation and every film / ring sum
+// is the one the sequential loop performs, in the same order: bit-identical.
 lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump_p, int N, int n_tasks, int dim_stride,
-                             uint64_t max_samples, uint64_t max_P, const std::vector<int32_t>& first, int G,
-                             lumo_status& st) {
-    // G independent task groups (G = 1: the whole frame): the tasks are cut into G groups of
-    // consecutive tasks whose pass chains are independent (a task's delta needs only its own
-    // previous pass, task.rs:28-53; the sampler state is per slot), units (group g, pass p) are
-    // issued in the order n = p * G + g, and each group hands its units' tails to its own stream,
-    // so one group's latency-bound tail kernel, film and ring overlap the other's.  NA head
-    // streams (G = 1: 1 to 3, g_pipeline; G = 2: 2) run the units' cameras and first bounces; with
-    // more than one, consecutive units' first bounces also run concurrently (filling the GPU when
-    // a rank holds few slots).  NSETS = 4 sets of queues, counters and per-slot outputs (G = 1 with
-    // NA head streams: NA + 1), so a set is reused only after the unit NSETS back has issued its ring.
-    G = std::max(1, std::min(G, std::min(2, n_tasks)));
-    if (D.delta || D.rad) G = 1;  // debug dumps follow one pass chain
-    const int NA = G == 1 ? std::min(std::max(g_pipeline, 1), 3) : 2, NSETS = G == 1 ? NA + 1 : 4;
+                             uint64_t max_samples, uint64_t max_P, int M, lumo_status& st) {
+    const int NA = std::min(std::max(c.o.pipeline, 1), 3), NSETS = NA + 1;
     // On an error return, work already queued on the other streams may still use the buffers the
     // next call re-initialises on stream 0: drain every stream before reporting the error.
     struct JoinOnError {
@@ -954,123 +996,113 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
                 if (s) (void)hipStreamSynchronize(s);
         }
     } join{c};
-    // groups of consecutive tasks, about N / G slots each
-    std::vector<int> t_lo(G), t_hi(G);
-    for (int g = 0, t = 0; g < G; ++g) {
-        t_lo[g] = t;
-        const int64_t target = (int64_t)N * (g + 1) / G;
-        while (t < n_tasks && (g == G - 1 || first[t + 1] <= target || t == t_lo[g])) ++t;
-        t = std::max(std::min(t, n_tasks - (G - 1 - g)), t_lo[g] + 1);
-        t_hi[g] = t;
-    }
     Paths P3[4] = {S, S, S, S};
-    for (int k = 1; k < NSETS; ++k) alloc_pass_set(c, P3[k], k, N, st);
+    for (int k = 1; k < NSETS; ++k) alloc_pass_set(c, P3[k], k, N * M, st);  // M passes' outputs and paths
     if (st) return st;
     hipStream_t As[3] = {c.stream, c.stream3, c.stream4};
-    hipStream_t Bs[2] = {c.stream2, c.stream4};
-    if (G == 2) As[1] = c.stream3;
-    // every event starts "done" after the setup enqueued on stream 0 (tasks, memsets, the initial
-    // ring): unit n waits for unit n - NSETS's ring before reusing its set, for its group's
-    // previous camera (the sampler state is per slot) and, before bounce RR_DEPTH, for its
-    // group's previous ring.  Every wait is enqueued after the record it waits for (NSETS > G).
-    // each set's counters start zeroed; from then on every unit's ring zeroes its set's counters
+    hipStream_t B = c.stream2;
+    // each set's counters start zeroed; from then on every unit's last ring zeroes its set's counters
     {
         ZeroList z;
         for (int k = 1; k < NSETS; ++k) z.add(P3[k].counts, sizeof(uint32_t) * CNT_N);
         k_zero_list<<<1, BLOCK, 0, As[0]>>>(z);
     }
+    // every event starts "done" after the setup enqueued on stream 0 (tasks, zeroing, the initial
+    // ring): unit u waits for unit u - NSETS's ring and film before reusing its set, for unit u - 1's
+    // camera (the sampler state is per slot) and, before a bounce RR_DEPTH, for unit u - 1's ring
     for (int k = 0; k < 4; ++k) {
         HIPCHK(hipEventRecord(c.pass_ev[k], As[0]));
         HIPCHK(hipEventRecord(c.cam_ev[k], As[0]));
         HIPCHK(hipEventRecord(c.film_ev[k], As[0]));
     }
-    const uint64_t units = max_samples * (uint64_t)G;
-    for (uint64_t n = 0; n < units; ++n) {
-        const int g = (int)(n % G);
-        const uint64_t pass = n / G;
-        const int set = (int)(n % NSETS), prev = (int)((n + NSETS - G) % NSETS);  // prev: unit n - G
-        const int t0 = t_lo[g], t1 = t_hi[g], s0 = first[t0], s1 = first[t1], Nu = s1 - s0;
-        hipStream_t A = As[n % NA], B = Bs[g];
+    HIPCHK(hipStreamWaitEvent(B, c.pass_ev[0], 0));
+    // bounces on the head stream: through the RR bounce when a pass holds many paths; with fewer
+    // (a rank's share of a multi-GPU run) the RR bounce goes to the tail kernel too, so the head
+    // stream never waits for the previous pass's ring (362^2: 509 -> 434 ms).  Merged units
+    // (M > 1) always stop before it.
+    int heads = c.o.heads > 0 ? c.o.heads : (N >= (1 << 21) ? RR_DEPTH + 1 : RR_DEPTH);
+    if (M > 1) heads = std::min(heads, RR_DEPTH);
+    c.sched.head_streams = NA;
+    c.sched.head_bounces = heads;
+    c.sched.merged_passes = M;
+    const int gN = ceil_div(N, BLOCK);
+    const uint64_t units = (max_samples + (uint64_t)M - 1) / (uint64_t)M;
+    for (uint64_t u = 0; u < units; ++u) {
+        const uint64_t p0 = u * (uint64_t)M;
+        const int mu = (int)std::min<uint64_t>((uint64_t)M, max_samples - p0);  // passes of this unit
+        const int set = (int)(u % NSETS), prev = (int)((u + NSETS - 1) % NSETS);
+        hipStream_t A = As[u % NA];
         Paths& P = P3[set];
-        // bounces 0..heads-1 on the head stream: through the RR bounce when a unit holds many
-        // paths; with few (a rank's share of a multi-GPU run) the RR bounce goes to the tail kernel
-        // too, so the head stream never waits for the previous pass's ring (362^2: 509 -> 434 ms)
-        const int heads = g_heads > 0 ? g_heads : (Nu >= (1 << 21) ? RR_DEPTH + 1 : RR_DEPTH);
-        const int gN = ceil_div(Nu, BLOCK);
-        // ---- head stream: camera + the first bounces
-        HIPCHK(hipStreamWaitEvent(A, c.pass_ev[set], 0));  // unit n - NSETS done with this set (its ring zeroed the counters)
+        // ---- head stream: camera + the first bounces of the unit's passes
+        HIPCHK(hipStreamWaitEvent(A, c.pass_ev[set], 0));  // unit u - NSETS done with this set (its ring zeroed the counters)
         HIPCHK(hipStreamWaitEvent(A, c.film_ev[set], 0));  // ... and its film
-        if (NA > 1 || G > 1) HIPCHK(hipStreamWaitEvent(A, c.cam_ev[prev], 0));  // the group's previous camera
+        if (NA > 1) HIPCHK(hipStreamWaitEvent(A, c.cam_ev[prev], 0));  // the previous unit's camera
         {
-            StageTimer tm(c, g_timing, ST_CAMERA, A);
-            k_camera<true><<<gN, BLOCK, 0, A>>>(T, P, c.cam, s1, dim_stride, (uint32_t)pass, s0);
+            StageTimer tm(c, c.o.timing, ST_CAMERA, A);
+            k_camera<true><<<gN, BLOCK, 0, A>>>(T, P, c.cam, N, dim_stride, (uint32_t)p0, 0, mu, N);
         }
         HIPCHK(hipEventRecord(c.cam_ev[set], A));
         for (int b = 0; b < heads; ++b) {
-            if (b == RR_DEPTH) HIPCHK(hipStreamWaitEvent(A, c.pass_ev[prev], 0));  // this pass's delta
+            if (b == RR_DEPTH) HIPCHK(hipStreamWaitEvent(A, c.pass_ev[prev], 0));  // this pass's delta (M == 1)
             k_bounce_begin<<<1, 64, 0, A>>>(P.counts, P.tcount + TC_HEADQ);
-            StageTimer tm(c, g_timing, ST_CLOSEST, A);
+            StageTimer tm(c, c.o.timing, ST_CLOSEST, A);
             launch_trav(
-                c, (uint64_t)Nu,
+                c, (uint64_t)N * mu,
                 [&](auto K, const TravLaunch& l) {
                     launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[b & 1], P.qs[(b + 1) & 1], 0u, false,
-                                                        g_dyn, g_bounce_threads);
+                                                        c.o.dyn, c.o.bounce_threads);
                 },
                 A);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.tail_ev[set], A));
-        // ---- the group's stream: the rest of the pass, film, ring
+        // ---- stream B: per pass, the rest of its paths, its film and its ring
         HIPCHK(hipStreamWaitEvent(B, c.tail_ev[set], 0));
-        if (G > 1) HIPCHK(hipStreamWaitEvent(B, c.pass_ev[prev], 0));  // the group's previous ring (the tail takes paths through RR)
-        if (D.delta) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, B));
         k_bounce_begin<<<1, 64, 0, B>>>(P.counts, P.tcount + TC_HEADQ);
-        {
-            StageTimer tm(c, g_timing, ST_RESOLVE, B);
-            launch_trav(
-                c, (uint64_t)Nu,
-                [&](auto K, const TravLaunch& l) {
-                    launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[heads & 1], P.qs[(heads + 1) & 1],
-                                                        0xffffffffu, true, 0, BLOCK);
-                },
-                B);
-        }
-        auto film = [&](hipStream_t fs) -> lumo_status {
+        for (int m = 0; m < mu; ++m) {
+            const uint64_t pass = p0 + (uint64_t)m;
+            Paths V = pass_view(P, m, N);
+            if (D.delta) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, B));
+            if (m > 0) k_zero_fetch<<<1, 64, 0, B>>>(P.counts);
+            {
+                StageTimer tm(c, c.o.timing, ST_RESOLVE, B);
+                launch_trav(
+                    c, (uint64_t)N * mu,
+                    [&](auto K, const TravLaunch& l) {
+                        // P, not the view: the paths carry virtual slots
+                        launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[heads & 1], P.qs[(heads + 1) & 1],
+                                                            0xffffffffu, true, 0, BLOCK, m * N, (m + 1) * N);
+                    },
+                    B);
+            }
+            // film, then the ring (which computes the samples' luminance itself).  A film on a
+            // stream of its own, off the chain the next pass's Russian roulette waits on, measured
+            // slower (C1 1/8 share 438 -> 488 ms per frame), ring-then-film the same
             if (max_P <= BLOCK) {
-                StageTimer tm(c, g_timing, ST_FILM, fs);
-                k_finish_film<<<t1 - t0, BLOCK, 0, fs>>>(c.sc, P, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
-                                                         c.tone_arg, t0);
+                StageTimer tm(c, c.o.timing, ST_FILM, B);
+                k_finish_film<<<n_tasks, BLOCK, 0, B>>>(c.sc, V, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
+                                                        c.tone_arg, 0);
             } else {
                 {
-                    StageTimer tm(c, g_timing, ST_FINISH, fs);
-                    k_finish<<<gN, BLOCK, 0, fs>>>(c.sc, P, c.cam, s1, (uint32_t)pass, D, dump_p, c.tone_map,
-                                                   c.tone_arg, s0);
+                    StageTimer tm(c, c.o.timing, ST_FINISH, B);
+                    k_finish<<<gN, BLOCK, 0, B>>>(c.sc, V, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg,
+                                                  0);
                 }
-                StageTimer tm(c, g_timing, ST_FILM, fs);
-                k_film<<<gN, BLOCK, 0, fs>>>(P, T, c.cam, s1, s0);
+                StageTimer tm(c, c.o.timing, ST_FILM, B);
+                k_film<<<gN, BLOCK, 0, B>>>(V, T, c.cam, N, 0);
+            }
+            {
+                StageTimer tm(c, c.o.timing, ST_RING, B);
+                k_ring<<<n_tasks, 64, 0, B>>>(c.sc, V, T, n_tasks, 1, m == mu - 1 ? P.counts : nullptr, 0);
             }
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(c.film_ev[set], fs));
-            return LUMO_OK;
-        };
-        // film, then the ring (which computes the samples' luminance itself).  A film on a stream
-        // of its own, off the chain the next pass's Russian roulette waits on, measured slower (C1
-        // 1/8 share 438 -> 488 ms per frame), ring-then-film the same: the head streams, not that
-        // chain, bound the frame
-        if (const lumo_status fe = film(B)) return fe;
-        {
-            StageTimer tm(c, g_timing, ST_RING, B);
-            k_ring<<<t1 - t0, 64, 0, B>>>(c.sc, P, T, t1, 1, P.counts, t0);
         }
-        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c.film_ev[set], B));
         HIPCHK(hipEventRecord(c.pass_ev[set], B));
-        if (g_timing) resolve_timers(c);
+        if (c.o.timing) resolve_timers(c);
     }
     // the results are copied on stream 0: after every set's last unit
-    for (int k = 0; k < NSETS; ++k) {
-        HIPCHK(hipStreamWaitEvent(As[0], c.pass_ev[k], 0));
-        HIPCHK(hipStreamWaitEvent(As[0], c.film_ev[k], 0));
-    }
+    for (int k = 0; k < NSETS; ++k) HIPCHK(hipStreamWaitEvent(As[0], c.pass_ev[k], 0));
     join.ok = true;
     return LUMO_OK;
 }
@@ -1082,62 +1114,62 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
 void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, const QState& nxt, uint32_t ub,
                         hipStream_t sm, bool fused_now) {
     const int ns = c.sc.n_shadow;
-    // n_shadow == 1: the tail kernel takes the bounce when fewer than g_tail_below paths
+    // n_shadow == 1: the tail kernel takes the bounce when fewer than c.o.tail_below paths
     // are alive (decided on the device from the exact count); the bounce kernels skip it
     // (launched only once the last count the host has seen is below 4x the threshold:
     // before that the bounce kernels get threshold 0 and take every path)
-    const uint32_t skip = (ns == 1 && (uint64_t)ub < 4ull * g_tail_below) ? g_tail_below : 0u;
+    const uint32_t skip = (ns == 1 && (uint64_t)ub < 4ull * c.o.tail_below) ? c.o.tail_below : 0u;
     if (skip > 0) {
-        StageTimer tm(c, g_timing, ST_RESOLVE, sm);
+        StageTimer tm(c, c.o.timing, ST_RESOLVE, sm);
         launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
             launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, true, 0, BLOCK);
         }, sm);
     }
     if (fused_now) {  // one fused kernel per bounce (pt.h k_bounce_q)
-        StageTimer tm(c, g_timing, ST_CLOSEST, sm);
+        StageTimer tm(c, c.o.timing, ST_CLOSEST, sm);
         launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
-            launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, false, g_dyn, g_bounce_threads);
+            launch_bounce_q<decltype(K)::value>(l, c.sc, S, T, cur, nxt, skip, false, c.o.dyn, c.o.bounce_threads);
         }, sm);
         return;
     }
     {
-        StageTimer tm(c, g_timing, ST_CLOSEST, sm);
+        StageTimer tm(c, c.o.timing, ST_CLOSEST, sm);
         launch_trav(
             c, ub, [&](auto K, const TravLaunch& l) { launch_closest_q<decltype(K)::value>(l, c.sc, S, cur, skip); },
             sm, true);
     }
     {
-        StageTimer tm(c, g_timing, ST_SHADE, sm);
+        StageTimer tm(c, c.o.timing, ST_SHADE, sm);
         const int g = ceil_div(ub, BLOCK);
         if (ns > 1) {  // NEE pairs by k_nee_gen, one thread per pair
             const int gp = std::min(ceil_div((uint64_t)ub * (uint32_t)ns, BLOCK), 1 << 16);
             if (c.sc.full == 2) {
-                k_shade_q<2, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+                k_shade_q<2, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, skip);
                 k_nee_gen<2><<<gp, BLOCK, 0, sm>>>(c.sc, S);
             } else if (c.sc.full) {
-                k_shade_q<1, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+                k_shade_q<1, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, skip);
                 k_nee_gen<1><<<gp, BLOCK, 0, sm>>>(c.sc, S);
             } else {
-                k_shade_q<0, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+                k_shade_q<0, true><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, skip);
                 k_nee_gen<0><<<gp, BLOCK, 0, sm>>>(c.sc, S);
             }
         } else if (c.sc.full == 2) {
-            k_shade_q<2, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+            k_shade_q<2, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, skip);
         } else if (c.sc.full) {
-            k_shade_q<1, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+            k_shade_q<1, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, skip);
         } else {
-            k_shade_q<0, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, g_buckets, skip, g_qsort);
+            k_shade_q<0, false><<<g, BLOCK, 0, sm>>>(c.sc, S, T, cur, nxt, skip);
         }
     }
     {
-        StageTimer tm(c, g_timing, ST_SHADOW, sm);
+        StageTimer tm(c, c.o.timing, ST_SHADOW, sm);
         launch_trav(
             c, (uint64_t)ub * (uint32_t)ns,
             [&](auto K, const TravLaunch& l) { launch_shadow_q<decltype(K)::value>(l, c.sc, S, nxt); }, sm,
             true);
     }
     if (ns > 1) {
-        StageTimer tm(c, g_timing, ST_RESOLVE, sm);
+        StageTimer tm(c, c.o.timing, ST_RESOLVE, sm);
         k_nee_fold<<<std::min(ceil_div(ub, BLOCK), 1 << 14), BLOCK, 0, sm>>>(S, nxt, ns);
     }
 }
@@ -1206,7 +1238,7 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
     // could start on stale counters and tables: found by poisoning fresh buffers (LUMO_POISON).
     for (int k = 1; k < K; ++k) HIPCHK(hipStreamWaitEvent(Ss[k], c.pass_ev[0], 0));
     const int SEG = Ctx::SNAP_RING / 4;  // snapshot slots per set
-    const int ahead = std::max(1, std::min(c.bounce_ahead, SEG - 1));
+    const int ahead = std::max(1, std::min(c.o.bounce_ahead, SEG - 1));
     struct PS {
         uint64_t unit, pass;
         int g, set, issued, consumed;
@@ -1224,9 +1256,9 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         const int s0 = first[t_lo[g]], s1 = first[t_hi[g]];
         if (pass > 0) HIPCHK(hipStreamWaitEvent(sm, c.cam_ev[(next - G) % K], 0));  // sampler state per slot
         {
-            StageTimer tm(c, g_timing, ST_CAMERA, sm);
+            StageTimer tm(c, c.o.timing, ST_CAMERA, sm);
             k_camera<true><<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(T, P[set], c.cam, s1, dim_stride, (uint32_t)pass,
-                                                                        s0);
+                                                                        s0, 1, 0);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.cam_ev[set], sm));
@@ -1243,7 +1275,7 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
     // the tail kernel (n_shadow == 1, launched once few paths are alive) runs paths to their end,
     // through Russian roulette, in whatever bounce it is launched: such a bounce needs the delta too
     auto tail_possible = [&](const PS& ps) {
-        return ns == 1 && g_tail_below > 0 && (uint64_t)ps.ub < 4ull * g_tail_below;
+        return ns == 1 && c.o.tail_below > 0 && (uint64_t)ps.ub < 4ull * c.o.tail_below;
     };
     auto issue = [&](PS& ps) -> lumo_status {
         hipStream_t sm = Ss[ps.set];
@@ -1287,29 +1319,29 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         // waits only for it; the film follows on this stream, after the group's previous film
         // (the film accumulates in pass order)
         {
-            StageTimer tm(c, g_timing, ST_RING, sm);
+            StageTimer tm(c, c.o.timing, ST_RING, sm);
             k_ring<<<t1 - t0, 64, 0, sm>>>(c.sc, Q, T, t1, 1, Q.counts, t0);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.pass_ev[ps.set], sm));
         if (ps.pass > 0) HIPCHK(hipStreamWaitEvent(sm, c.film_ev[(ps.unit - G) % K], 0));
         if (max_P <= BLOCK) {
-            StageTimer tm(c, g_timing, ST_FILM, sm);
+            StageTimer tm(c, c.o.timing, ST_FILM, sm);
             k_finish_film<<<t1 - t0, BLOCK, 0, sm>>>(c.sc, Q, T, c.cam, (uint32_t)ps.pass, Dump{}, 0, c.tone_map,
                                                      c.tone_arg, t0);
         } else {
             {
-                StageTimer tm(c, g_timing, ST_FINISH, sm);
+                StageTimer tm(c, c.o.timing, ST_FINISH, sm);
                 k_finish<<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(c.sc, Q, c.cam, s1, (uint32_t)ps.pass, Dump{}, 0,
                                                                      c.tone_map, c.tone_arg, s0);
             }
-            StageTimer tm(c, g_timing, ST_FILM, sm);
+            StageTimer tm(c, c.o.timing, ST_FILM, sm);
             k_film<<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(Q, T, c.cam, s1, s0);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.film_ev[ps.set], sm));
         finished[ps.g] = ps.pass + 1;
-        if (g_timing) resolve_timers(c);
+        if (c.o.timing) resolve_timers(c);
         return LUMO_OK;
     };
     // unit n reuses the set of unit n - K: it starts once that unit has issued its ring (units of
@@ -1393,13 +1425,34 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
 
     lumo_status st = LUMO_OK;
     const bool bdpt = c.integrator == LUMO_INTEGRATOR_BDPT;
+    // schedule: fused bounces (n_shadow == 1, the scene and the fused kernel's parked NEE records
+    // fit the LDS of a block) in the pipelined pass loop, which merges M passes per unit when a
+    // pass holds few paths (kMergeTarget); else the split schedule (below)
+    const bool fused_fits = (size_t)(c.sc.hot_bytes + 15u) / 16u * 16u +
+                                (size_t)PARK_DOUBLES * sizeof(double) * (size_t)c.o.bounce_threads <= c.lds_block;
+    const bool fused_now =
+        ns == 1 && (c.o.fused < 0 ? (c.o.lds && c.sc.hot_bytes > 0 && fused_fits) : c.o.fused != 0);
+    const bool pipe = !bdpt && fused_now && c.o.pipeline;
+    int M = 1;
+    if (pipe) {
+        M = c.o.merge > 0 ? c.o.merge : (int)std::min<uint64_t>(MAX_MERGE, (kMergeTarget + N - 1) / (uint64_t)N);
+        M = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)M, max_samples));
+        if ((uint64_t)N * (uint64_t)M > ((uint64_t)1 << 30)) M = 1;
+    }
+    const size_t NV = (size_t)N * (size_t)M;  // virtual slots: M passes' per-slot outputs
+    c.sched = lumo_schedule_info{};
+    c.sched.schedule = pipe ? LUMO_SCHED_FUSED_PIPELINE : LUMO_SCHED_SEQUENTIAL;
+    c.sched.fused = fused_now ? 1 : 0;
+    c.sched.merged_passes = 1;
+    c.sched.units_in_flight = 1;
+    c.sched.task_groups = 1;
     Paths S{};
     // per slot: camera sampler, raster, final values; BDPT also its walk state
-    S.rad = wbuf<double>(c, W_RAD, 4 * (size_t)N, st);
-    S.lam = wbuf<double>(c, W_LAM, 4 * (size_t)N, st);
-    S.raster = wbuf<double>(c, W_RASTER, 2 * (size_t)N, st);
-    S.depth = wbuf<uint32_t>(c, W_DEPTH, N, st);
-    S.queries = wbuf<uint32_t>(c, W_QUERIES, N, st);
+    S.rad = wbuf<double>(c, W_RAD, 4 * NV, st);
+    S.lam = wbuf<double>(c, W_LAM, 4 * NV, st);
+    S.raster = wbuf<double>(c, W_RASTER, 2 * NV, st);
+    S.depth = wbuf<uint32_t>(c, W_DEPTH, NV, st);
+    S.queries = wbuf<uint32_t>(c, W_QUERIES, NV, st);
     S.task = wbuf<int32_t>(c, W_TASK, N, st);
     S.pix = wbuf<int32_t>(c, W_PIX, N, st);
     S.pseed = wbuf<uint64_t>(c, W_PSEED, N, st);
@@ -1422,18 +1475,17 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         // path tracer: queue-order state (ping-pong), hits, NEE records (state.h)
         const size_t cap = (size_t)N;
         for (int k = 0; k < 2; ++k) {
-            S.qs[k].cap = cap;
-            S.qs[k].d = wbuf<double>(c, k ? W_QS1_D : W_QS0_D, QD_N * cap, st);
-            S.qs[k].r = wbuf<uint64_t>(c, k ? W_QS1_R : W_QS0_R, 2 * cap, st);
-            S.qs[k].i = wbuf<int32_t>(c, k ? W_QS1_I : W_QS0_I, QI_N * cap, st);
+            S.qs[k].cap = NV;
+            S.qs[k].d = wbuf<double>(c, k ? W_QS1_D : W_QS0_D, QD_N * NV, st);
+            S.qs[k].r = wbuf<uint64_t>(c, k ? W_QS1_R : W_QS0_R, 2 * NV, st);
+            S.qs[k].i = wbuf<int32_t>(c, k ? W_QS1_I : W_QS0_I, QI_N * NV, st);
         }
         S.hq.cap = cap;
         S.hq.t = wbuf<double>(c, W_HQ_T, cap, st);
         S.hq.i = wbuf<int32_t>(c, W_HQ_I, 3 * cap, st);
         // bucket segments of `cap` paths each (MI355X has the HBM for the worst case)
-        const int nb = g_buckets > 1 ? NB : 1;
         S.sq.seg = (uint32_t)cap;
-        S.sq.hcap = cap * nb;
+        S.sq.hcap = cap * NB;
         S.sq.cap = S.sq.hcap * (size_t)ns;
         S.sq.d = wbuf<double>(c, W_SQ_D, SD_N * S.sq.cap, st);
         S.sq.i = wbuf<int32_t>(c, W_SQ_I, SI_N * S.sq.cap, st);
@@ -1442,7 +1494,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         S.sq.hr = ns > 1 ? wbuf<uint64_t>(c, W_SQ_HR, 2 * S.sq.hcap, st) : nullptr;
     }
     S.p_rgb = wbuf<double>(c, W_P_RGB, 3 * (size_t)N, st);
-    S.p_valid = wbuf<uint32_t>(c, W_P_VALID, N, st);
+    S.p_valid = wbuf<uint32_t>(c, W_P_VALID, NV, st);
     S.film = wbuf<double>(c, W_FILM, 4 * (size_t)N, st);
     S.counts = wbuf<uint32_t>(c, W_COUNTS, CNT_N, st);
     S.tcount = wbuf<unsigned long long>(c, W_TCOUNT, TC_ALL + TC_STATS, st);
@@ -1547,6 +1599,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             z.add(B.overflow, sizeof(uint32_t));
             if (dfilm) z.add(dfilm, sizeof(double) * film_n);
         }
+        if (z.overflow) return LUMO_ERR_INVALID;
         k_zero_list<<<std::min(ceil_div((uint64_t)4 * N, BLOCK), 2048), BLOCK, 0, sm>>>(z);
     }
 
@@ -1563,33 +1616,30 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     // as an upper bound (counts never grow within a pass); the kernels read the exact counts from
     // device memory.  A pass ends once a snapshot shows no path alive; the bounces enqueued past
     // that point see empty queues and exit at once.
-    const int ahead = c.bounce_ahead;
-    const bool fused_now = ns == 1 && (g_fused < 0 ? (g_lds && c.sc.hot_bytes > 0) : g_fused != 0);
-    const bool pipe = !bdpt && fused_now && g_pipeline && !g_fused_split;
+    const int ahead = c.o.bounce_ahead;
     if (pipe) {
-        const lumo_status ps = render_pipelined(c, S, T, D, dump_p, N, (int)n_tasks, dim_stride, max_samples, max_P, first,
-                                                g_pipe_groups, st);
+        const lumo_status ps = render_pipelined(c, S, T, D, dump_p, N, (int)n_tasks, dim_stride, max_samples, max_P, M, st);
         if (ps) return ps;
         if (st) return st;
     }
-    // split schedule: passes in flight, as many as g_split_pipe and the free HBM allow
+    // split schedule: passes in flight, as many as c.o.split_pipe and the free HBM allow
     int K = 1;
-    const uint64_t units = max_samples * (uint64_t)std::max(1, std::min(g_split_groups, (int)n_tasks));
-    if (!bdpt && !pipe && !dump_host && g_pipeline && g_split_pipe > 1 && units > 1) {
+    const uint64_t units = max_samples * (uint64_t)std::max(1, std::min(c.o.split_groups, (int)n_tasks));
+    if (!bdpt && !pipe && !dump_host && c.o.pipeline && c.o.split_pipe > 1 && units > 1) {
         size_t free_b = 0, total_b = 0;
         const size_t per_set = split_set_bytes(S, N, ns);
         const size_t margin = (size_t)8 << 30;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-            K = std::min(std::min(g_split_pipe, 4), (int)std::min<uint64_t>(units, 4));
+            K = std::min(std::min(c.o.split_pipe, 4), (int)std::min<uint64_t>(units, 4));
             while (K > 1 && (size_t)(K - 1) * per_set + margin > free_b + c.split_sets_bytes) K--;
         }
     }
-    if (std::getenv("LUMO_DEBUG_SCHED"))
-        std::fprintf(stderr, "lumo: N=%d passes=%llu ns=%d fused=%d pipe=%d split K=%d g_pipeline=%d tail=%u\n", N,
-                     (unsigned long long)max_samples, ns, (int)fused_now, (int)pipe, K, g_pipeline, g_tail_below);
     if (K > 1) {
+        c.sched.schedule = LUMO_SCHED_SPLIT_PIPELINE;
+        c.sched.units_in_flight = K;
+        c.sched.task_groups = std::max(1, std::min(c.o.split_groups, std::min(K, (int)n_tasks)));
         const lumo_status ps = render_split_pipelined(c, S, T, N, (int)n_tasks, dim_stride, max_samples, max_P,
-                                                      fused_now, K, g_split_groups, first, bounces, st);
+                                                      fused_now, K, c.o.split_groups, first, bounces, st);
         if (ps) return ps;
         if (st) return st;
         c.split_sets_bytes = std::max(c.split_sets_bytes, (size_t)(K - 1) * split_set_bytes(S, N, ns));
@@ -1598,11 +1648,11 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         if (dump_host) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, sm));
         // S.counts: zeroed at setup, then by the ring at the end of every pass
         {
-            StageTimer tm(c, g_timing, ST_CAMERA);
+            StageTimer tm(c, c.o.timing, ST_CAMERA);
             if (bdpt)
-                k_camera<false><<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass, 0);
+                k_camera<false><<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass, 0, 1, 0);
             else
-                k_camera<true><<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass, 0);
+                k_camera<true><<<gN, BLOCK, 0, sm>>>(T, S, c.cam, N, dim_stride, (uint32_t)pass, 0, 1, 0);
         }
         HIPCHK(hipGetLastError());
         // Bounce loop over the alive queue (filled by the producer just launched): `step` launches
@@ -1656,24 +1706,24 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             // + k_bdpt_step; re-runs of samples that did not fit; connection items; fold.  Stage
             // slots: walks = CLOSEST + SHADE, items = SHADOW, re-runs + fold = RESOLVE.
             // once few subpaths are alive, k_bdpt_tail is launched ahead of each bounce and, below
-            // g_bdpt_tail paths (the exact count, on the device), runs every remaining walk to its
+            // c.o.bdpt_tail paths (the exact count, on the device), runs every remaining walk to its
             // end in that launch; the bounce kernels then skip (as the path tracer's tail kernel)
             auto walk_step = [&](int mode) {
                 return [&, mode](uint32_t ub, int, int32_t* qa, int32_t* qb) {
-                    const uint32_t skip = (uint64_t)ub < 4ull * g_bdpt_tail ? g_bdpt_tail : 0u;
+                    const uint32_t skip = (uint64_t)ub < 4ull * c.o.bdpt_tail ? c.o.bdpt_tail : 0u;
                     if (skip > 0) {
-                        StageTimer tm(c, g_timing, ST_RESOLVE);
+                        StageTimer tm(c, c.o.timing, ST_RESOLVE);
                         launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
                             launch_bdpt_tail<decltype(K)::value>(l, c.sc, S, T, B, BI, mode, qa, skip);
                         });
                     }
                     {
-                        StageTimer tm(c, g_timing, ST_CLOSEST);
+                        StageTimer tm(c, c.o.timing, ST_CLOSEST);
                         launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
                             launch_closest<decltype(K)::value>(l, c.sc, S, qa, skip);
                         });
                     }
-                    StageTimer tm(c, g_timing, ST_SHADE);
+                    StageTimer tm(c, c.o.timing, ST_SHADE);
                     by_stack_class(c.sc.stack_class, [&](auto K) {
                         launch_bdpt_step<decltype(K)::value>(ceil_div(ub, BLOCK), sm, c.sc.full, c.sc, S, T, B, BI, mode, qa, qb,
                                                              skip);
@@ -1694,7 +1744,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             bst = bounce_loop(walk_step(TR_RADIANCE));
             if (bst) return bst;
             {
-                StageTimer tm(c, g_timing, ST_RESOLVE);
+                StageTimer tm(c, c.o.timing, ST_RESOLVE);
                 launch_trav(c, (uint64_t)B.redo_cap, [&](auto K, const TravLaunch& l) {
                     launch_bdpt_redo<decltype(K)::value>(l, c.sc, S, T, c.cam, B, BR, BI);
                 });
@@ -1723,12 +1773,12 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             if (st) return st;
             if (totals[0] > 0) {
                 {
-                    StageTimer tm(c, g_timing, ST_BD_TRACE_A);
+                    StageTimer tm(c, c.o.timing, ST_BD_TRACE_A);
                     launch_trav(c, (uint64_t)totals[0], [&](auto K, const TravLaunch& l) {
                         launch_bdpt_trace_a<decltype(K)::value>(l, c.sc, S, c.cam, B, BR, BI, N, items_total);
                     });
                 }
-                StageTimer tm(c, g_timing, ST_BD_EVAL_A);
+                StageTimer tm(c, c.o.timing, ST_BD_EVAL_A);
                 const int grid = std::min(ceil_div(totals[0], BLOCK), 1 << 16);
                 if (c.sc.full == 2)
                     k_bdpt_eval_a<2><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
@@ -1739,12 +1789,12 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             }
             if (totals[1] > 0) {
                 {
-                    StageTimer tm(c, g_timing, ST_BD_VIS);
+                    StageTimer tm(c, c.o.timing, ST_BD_VIS);
                     launch_trav(c, (uint64_t)totals[1], [&](auto K, const TravLaunch& l) {
                         launch_bdpt_vis<decltype(K)::value>(l, c.sc, S, B, BR, BI, N, items_total);
                     });
                 }
-                StageTimer tm(c, g_timing, ST_BD_PATHS);
+                StageTimer tm(c, c.o.timing, ST_BD_PATHS);
                 const int grid = std::min(ceil_div(totals[1], BLOCK), 1 << 16);
                 if (c.sc.full == 2)
                     k_bdpt_paths<2><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
@@ -1754,29 +1804,29 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                     k_bdpt_paths<0><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
             }
             {
-                StageTimer tm(c, g_timing, ST_RESOLVE);
+                StageTimer tm(c, c.o.timing, ST_RESOLVE);
                 k_bdpt_fold<<<gN, BLOCK, 0, sm>>>(S, B, BR, BI, N);
             }
             HIPCHK(hipGetLastError());
         }
-        if (g_timing && bdpt) HIPCHK(hipStreamSynchronize(sm));  // BDPT passes have no bounce snapshots
-        if (g_timing) resolve_timers(c);
+        if (c.o.timing && bdpt) HIPCHK(hipStreamSynchronize(sm));  // BDPT passes have no bounce snapshots
+        if (c.o.timing) resolve_timers(c);
         if (max_P <= BLOCK) {  // one block per tile (lumo's 16x16 tiles)
-            StageTimer tm(c, g_timing, ST_FILM);
+            StageTimer tm(c, c.o.timing, ST_FILM);
             k_finish_film<<<(int)n_tasks, BLOCK, 0, sm>>>(c.sc, S, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
                                                           c.tone_arg, 0);
         } else {
             {
-                StageTimer tm(c, g_timing, ST_FINISH);
+                StageTimer tm(c, c.o.timing, ST_FINISH);
                 k_finish<<<gN, BLOCK, 0, sm>>>(c.sc, S, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg, 0);
             }
             {
-                StageTimer tm(c, g_timing, ST_FILM);
+                StageTimer tm(c, c.o.timing, ST_FILM);
                 k_film<<<gN, BLOCK, 0, sm>>>(S, T, c.cam, N, 0);
             }
         }
         {
-            StageTimer tm(c, g_timing, ST_RING);
+            StageTimer tm(c, c.o.timing, ST_RING);
             k_ring<<<(int)n_tasks, 64, 0, sm>>>(c.sc, S, T, (int)n_tasks, 1, S.counts, 0);
         }
         HIPCHK(hipGetLastError());
@@ -1843,7 +1893,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         HIPCHK(hipMemcpyAsync(dump_host->delta, D.delta, sizeof(double) * dump_samples, hipMemcpyDeviceToHost, sm));
     }
     HIPCHK(hipStreamSynchronize(sm));
-    if (g_timing) resolve_timers(c);
+    if (c.o.timing) resolve_timers(c);
     bool splat_oom = false;
     if (bdpt) {
         uint32_t ovf = 0;
@@ -1901,6 +1951,99 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     return splat_oom ? LUMO_ERR_OOM : LUMO_OK;
 }
 
+// ------------------------------------------------------------------ options (LUMO_OPT_*)
+const char* const kOptEnv[LUMO_OPT_COUNT] = {
+    "LUMO_TIMING", "LUMO_LDS", "LUMO_TOP", "LUMO_FUSED", "LUMO_TAIL", "LUMO_PIPELINE", "LUMO_HEADS", "LUMO_MERGE",
+    "LUMO_DYN", "LUMO_BOUNCE_THREADS", "LUMO_SPLIT_PIPE", "LUMO_SPLIT_GROUPS", "LUMO_BDPT_TAIL", "LUMO_BOUNCE_AHEAD",
+    "LUMO_LDS_GRID", "LUMO_TOP_GRID", "LUMO_TOP_KB", "LUMO_KD_LDS", "LUMO_STACK_CLASS", "LUMO_FULL_KERNELS",
+    "LUMO_POISON"};
+
+void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
+    lo = 0;
+    hi = 1;
+    switch (k) {
+        case LUMO_OPT_FUSED: lo = -1; break;
+        case LUMO_OPT_TAIL_BELOW: case LUMO_OPT_BDPT_TAIL: hi = (int64_t)1 << 31; break;
+        case LUMO_OPT_PIPELINE: hi = 3; break;
+        case LUMO_OPT_HEADS: hi = 64; break;
+        case LUMO_OPT_MERGE_PASSES: hi = MAX_MERGE; break;
+        case LUMO_OPT_BOUNCE_THREADS: lo = 64; hi = BLOCK; break;
+        case LUMO_OPT_SPLIT_PIPE: case LUMO_OPT_SPLIT_GROUPS: lo = 1; hi = 4; break;
+        case LUMO_OPT_BOUNCE_AHEAD: lo = 1; hi = Ctx::SNAP_RING / 4 - 1; break;
+        case LUMO_OPT_LDS_GRID: case LUMO_OPT_TOP_GRID: lo = 1; hi = 1 << 20; break;
+        case LUMO_OPT_TOP_KB: hi = (int64_t)(c.lds_cu / 1024); break;
+        case LUMO_OPT_KD_LDS: hi = 64; break;
+        case LUMO_OPT_STACK_CLASS: hi = 64; break;
+        default: break;
+    }
+}
+
+lumo_status set_opt(Ctx& c, int k, int64_t v) {
+    if (k < 0 || k >= LUMO_OPT_COUNT) return LUMO_ERR_INVALID;
+    int64_t lo, hi;
+    opt_range(c, k, lo, hi);
+    if (v < lo || v > hi) return LUMO_ERR_INVALID;
+    if (k == LUMO_OPT_BOUNCE_THREADS && v != 64 && v != 128 && v != BLOCK) return LUMO_ERR_INVALID;
+    if (k == LUMO_OPT_STACK_CLASS && v != 0 &&
+        std::find(std::begin(STACK_CLASSES), std::end(STACK_CLASSES), (int)v) == std::end(STACK_CLASSES))
+        return LUMO_ERR_INVALID;
+    Opts& o = c.o;
+    const int iv = (int)v;
+    switch (k) {
+        case LUMO_OPT_TIMING: o.timing = iv; break;
+        case LUMO_OPT_LDS_STAGING: o.lds = iv; break;
+        case LUMO_OPT_TOP_STAGING: o.top = iv; break;
+        case LUMO_OPT_FUSED: o.fused = iv; break;
+        case LUMO_OPT_TAIL_BELOW: o.tail_below = (uint32_t)v; break;
+        case LUMO_OPT_PIPELINE: o.pipeline = iv; break;
+        case LUMO_OPT_HEADS: o.heads = iv; break;
+        case LUMO_OPT_MERGE_PASSES: o.merge = iv; break;
+        case LUMO_OPT_DYN_FETCH: o.dyn = iv; break;
+        case LUMO_OPT_BOUNCE_THREADS: o.bounce_threads = iv; break;
+        case LUMO_OPT_SPLIT_PIPE: o.split_pipe = iv; break;
+        case LUMO_OPT_SPLIT_GROUPS: o.split_groups = iv; break;
+        case LUMO_OPT_BDPT_TAIL: o.bdpt_tail = (uint32_t)v; break;
+        case LUMO_OPT_BOUNCE_AHEAD: o.bounce_ahead = iv; break;
+        case LUMO_OPT_LDS_GRID: o.lds_grid = iv; break;
+        case LUMO_OPT_TOP_GRID: o.top_grid = iv; break;
+        case LUMO_OPT_TOP_KB: o.top_kb = iv; break;
+        case LUMO_OPT_KD_LDS: o.kd_lds = iv; break;
+        case LUMO_OPT_STACK_CLASS: o.stack_class = iv; break;
+        case LUMO_OPT_FULL_KERNELS: o.full_kernels = iv; break;
+        case LUMO_OPT_POISON: o.poison = iv; break;
+        default: return LUMO_ERR_INVALID;
+    }
+    return LUMO_OK;
+}
+
+int64_t get_opt(const Ctx& c, int k) {
+    const Opts& o = c.o;
+    switch (k) {
+        case LUMO_OPT_TIMING: return o.timing;
+        case LUMO_OPT_LDS_STAGING: return o.lds;
+        case LUMO_OPT_TOP_STAGING: return o.top;
+        case LUMO_OPT_FUSED: return o.fused;
+        case LUMO_OPT_TAIL_BELOW: return o.tail_below;
+        case LUMO_OPT_PIPELINE: return o.pipeline;
+        case LUMO_OPT_HEADS: return o.heads;
+        case LUMO_OPT_MERGE_PASSES: return o.merge;
+        case LUMO_OPT_DYN_FETCH: return o.dyn;
+        case LUMO_OPT_BOUNCE_THREADS: return o.bounce_threads;
+        case LUMO_OPT_SPLIT_PIPE: return o.split_pipe;
+        case LUMO_OPT_SPLIT_GROUPS: return o.split_groups;
+        case LUMO_OPT_BDPT_TAIL: return o.bdpt_tail;
+        case LUMO_OPT_BOUNCE_AHEAD: return o.bounce_ahead;
+        case LUMO_OPT_LDS_GRID: return o.lds_grid;
+        case LUMO_OPT_TOP_GRID: return o.top_grid;
+        case LUMO_OPT_TOP_KB: return o.top_kb;
+        case LUMO_OPT_KD_LDS: return o.kd_lds;
+        case LUMO_OPT_STACK_CLASS: return o.stack_class;
+        case LUMO_OPT_FULL_KERNELS: return o.full_kernels;
+        case LUMO_OPT_POISON: return o.poison;
+        default: return 0;
+    }
+}
+
 }  // namespace
 
 // ================================================================== C ABI
@@ -1940,7 +2083,10 @@ lumo_status lumo_create(int device, void** ctx_out) {
     Ctx* c = new (std::nothrow) Ctx();
     if (!c) return LUMO_ERR_OOM;
     c->device = device;
-    c->top_grid_cap = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    c->o.top_grid = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (prop.maxSharedMemoryPerMultiProcessor > 0) c->lds_cu = prop.maxSharedMemoryPerMultiProcessor;
+    if (prop.sharedMemPerBlock > 0) c->lds_block = std::min(c->lds_cu, (size_t)prop.sharedMemPerBlock);
+    c->o.top_kb = (int)(c->lds_cu / 1024);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return LUMO_ERR_HIP;
@@ -1958,39 +2104,21 @@ lumo_status lumo_create(int device, void** ctx_out) {
         (void)hipEventCreateWithFlags(&c->cam_ev[i], hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&c->film_ev[i], hipEventDisableTiming);
     }
-    for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventCreate(&c->ev[i]);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventCreateWithFlags(&c->snap_ev[i], hipEventDisableTiming);
     if (hipHostMalloc(reinterpret_cast<void**>(&c->snap), sizeof(uint32_t) * CNT_N * Ctx::SNAP_RING) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
         delete c;
         return LUMO_ERR_OOM;
     }
-    if (const char* e = std::getenv("LUMO_BOUNCE_AHEAD"))
-        c->bounce_ahead = std::min(Ctx::SNAP_RING - 1, std::max(1, std::atoi(e)));
-    if (const char* e = std::getenv("LUMO_LDS")) g_lds = e[0] != '0';
-    if (const char* e = std::getenv("LUMO_BUCKETS")) g_buckets = e[0] == '0' ? 1 : NB;
-    if (const char* e = std::getenv("LUMO_LDS_GRID")) c->lds_grid_cap = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("LUMO_TOP_GRID")) c->top_grid_cap = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("LUMO_TOP")) g_top = std::atoi(e);
-    if (const char* e = std::getenv("LUMO_SPLIT_PIPE")) g_split_pipe = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("LUMO_SPLIT_GROUPS")) g_split_groups = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("LUMO_FUSED_SPLIT")) g_fused_split = std::atoi(e);
-    if (const char* e = std::getenv("LUMO_TOP_KB")) c->top_lds_bytes = std::max(0, std::atoi(e)) * 1024;
-    if (const char* e = std::getenv("LUMO_KD_LDS")) c->kd_lds = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("LUMO_FUSED")) g_fused = std::atoi(e);
-    if (const char* e = std::getenv("LUMO_QSORT")) g_qsort = std::atoi(e) & 3;
-    if (const char* e = std::getenv("LUMO_TAIL")) g_tail_below = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("LUMO_PIPELINE")) g_pipeline = std::atoi(e);
-    if (const char* e = std::getenv("LUMO_DYN")) g_dyn = std::atoi(e);
-    if (const char* e = std::getenv("LUMO_BDPT_TAIL")) g_bdpt_tail = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("LUMO_PIPE_GROUPS")) g_pipe_groups = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("LUMO_HEADS")) g_heads = std::min(std::max(std::atoi(e), 0), 64);
-    if (const char* e = std::getenv("LUMO_BOUNCE_THREADS")) {
-        const int t = std::atoi(e);
-        g_bounce_threads = (t == 64 || t == 128) ? t : BLOCK;
+    // the environment's overrides of the defaults (out-of-range values are clamped)
+    for (int k = 0; k < LUMO_OPT_COUNT; ++k) {
+        const char* e = std::getenv(kOptEnv[k]);
+        if (!e || !*e) continue;
+        int64_t lo = 0, hi = 0;
+        opt_range(*c, k, lo, hi);
+        const int64_t v = std::min(hi, std::max(lo, (int64_t)std::strtoll(e, nullptr, 10)));
+        if (set_opt(*c, k, v) != LUMO_OK && k == LUMO_OPT_BOUNCE_THREADS) (void)set_opt(*c, k, BLOCK);
     }
-    const char* tm = std::getenv("LUMO_TIMING");
-    g_timing = tm && tm[0] == '1';
     *ctx_out = c;
     return LUMO_OK;
 }
@@ -2006,7 +2134,6 @@ void lumo_destroy(void* ctx) {
     free_scene(*c);
     for (DevBuf& b : c->work)
         if (b.p) (void)hipFree(b.p);
-    for (int i = 0; i < 2 * ST_COUNT; ++i) (void)hipEventDestroy(c->ev[i]);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventDestroy(c->snap_ev[i]);
     if (c->snap) (void)hipHostFree(c->snap);
     for (int i = 0; i < 4; ++i) {
@@ -2310,7 +2437,8 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         s.top_onodes = s.top_lnodes = 0;
         s.onodes_lds = s.lnodes_lds = nullptr;
         s.n_onodes_lds = s.n_lnodes_lds = 0;
-        const size_t budget = (size_t)c->top_lds_bytes;
+        const size_t cap = std::min((size_t)c->o.top_kb * 1024, c->lds_cu);
+        const size_t budget = cap > 256 ? cap - 256 : 0;  // 256 B: the kernels' static LDS
         const size_t objs_b = ((sizeof(int32_t) * d->num_object_items + 15) & ~(size_t)15) + sizeof(DObj) * tobjs.size();
         if (s.hot_bytes == 0 && budget >= 4096 && objs_b + 64 * sizeof(DBvh) <= budget) {
             std::vector<char> top;
@@ -2343,9 +2471,9 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         s.kst_n = 0;
         s.kst_cfg = 0;
         s.top_shm = (s.top_bytes + 15u) & ~15u;
-        if (s.top_bytes > 0 && c->kd_lds > 0) {
-            const size_t room = (size_t)(160 * 1024) - s.top_shm;
-            s.kst_cfg = (int32_t)std::min<size_t>((size_t)c->kd_lds, room / (12 * (size_t)TOP_BLOCK));
+        if (s.top_bytes > 0 && c->o.kd_lds > 0) {
+            const size_t room = c->lds_block > s.top_shm + 256 ? c->lds_block - s.top_shm - 256 : 0;
+            s.kst_cfg = (int32_t)std::min<size_t>((size_t)c->o.kd_lds, room / (12 * (size_t)TOP_BLOCK));
             s.top_shm += (uint32_t)(12 * (size_t)TOP_BLOCK * s.kst_cfg);
         }
     }
@@ -2394,11 +2522,7 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
             s.stack_class = cls;
             break;
         }
-    if (const char* e = std::getenv("LUMO_STACK_CLASS")) {  // A/B override (never below the needs)
-        const int f = std::atoi(e);
-        for (int cls : STACK_CLASSES)
-            if (cls == f && fits(cls)) s.stack_class = f;
-    }
+    if (c->o.stack_class > 0 && fits(c->o.stack_class)) s.stack_class = c->o.stack_class;  // A/B override
     // feature class: the lean kernels cover kd meshes / rectangles with Lambertian + Light only
     bool full = d->num_transforms > 0;
     for (int i = 0; i < d->num_materials; ++i)
@@ -2412,7 +2536,7 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         const lumo_material& m = d->materials[i];
         textured = textured || m.albedo_tex >= 0 || m.ks_tex >= 0 || m.tf_tex >= 0 || m.normal_map >= 0;
     }
-    if (const char* e = std::getenv("LUMO_FULL_KERNELS")) full = full || std::atoi(e) != 0;  // A/B switch
+    full = full || c->o.full_kernels != 0;  // A/B switch
     s.full = textured ? 2 : (full ? 1 : 0);
     c->has_scene = true;
     return LUMO_OK;
@@ -2535,8 +2659,8 @@ lumo_status lumo_trace(void* ctx, const lumo_ray_soa* rays, size_t n, lumo_hit_s
     HIPCHK(hipMemcpyAsync(d, rays->dir, sizeof(double) * 3 * n, hipMemcpyHostToDevice, sm));
     if (any_hit) HIPCHK(hipMemcpyAsync(light, rays->light, sizeof(int32_t) * n, hipMemcpyHostToDevice, sm));
     HIPCHK(hipMemsetAsync(tc, 0, sizeof(unsigned long long) * (TC_ALL + TC_STATS), sm));
-    const bool top = g_top && c->sc.top_bytes > 0 && !(g_lds && c->sc.hot_bytes > 0);
-    const int grid = top ? std::min(ceil_div(n, TOP_BLOCK), c->top_grid_cap) : ceil_div(n, BLOCK);
+    const bool top = c->o.top && c->sc.top_bytes > 0 && !(c->o.lds && c->sc.hot_bytes > 0);
+    const int grid = top ? std::min(ceil_div(n, TOP_BLOCK), c->o.top_grid) : ceil_div(n, BLOCK);
     by_stack_class(c->sc.stack_class, [&](auto K) {
         launch_trace<decltype(K)::value>(grid, sm, c->sc, o, d, light, (int)n, any_hit, t, kind, obj, prim, tc, top);
     });
@@ -2561,10 +2685,10 @@ lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info) {
     if (!c || !info) return LUMO_ERR_INVALID;
     if (!c->has_scene) return LUMO_ERR_NO_SCENE;
     info->stack_class = c->sc.stack_class;
-    info->lds_bytes = g_lds ? (int32_t)c->sc.hot_bytes : 0;
+    info->lds_bytes = c->o.lds ? (int32_t)c->sc.hot_bytes : 0;
     info->full_kernels = c->sc.full;
     info->n_shadow = c->sc.n_shadow;
-    const bool top = g_top && c->sc.top_bytes > 0 && !(g_lds && c->sc.hot_bytes > 0);
+    const bool top = c->o.top && c->sc.top_bytes > 0 && !(c->o.lds && c->sc.hot_bytes > 0);
     info->top_bytes = top ? (int32_t)c->sc.top_bytes : 0;
     info->top_object_nodes = c->sc.top_onodes;
     info->top_light_nodes = c->sc.top_lnodes;
@@ -2594,14 +2718,24 @@ lumo_status lumo_debug_stream(void* ctx, size_t n) {
     return LUMO_OK;
 }
 
-void lumo_set_timing(int on) { g_timing = on != 0; }
-void lumo_set_lds_staging(int on) { g_lds = on != 0; }
-void lumo_set_bdpt_tail(uint32_t below) { g_bdpt_tail = below; }
+lumo_status lumo_set_option(void* ctx, int32_t option, int64_t value) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return LUMO_ERR_INVALID;
+    return set_opt(*c, option, value);
+}
 
-void lumo_set_bounce_mode(int fused, uint32_t tail_below, int pipeline) {
-    g_fused = fused < 0 ? -1 : (fused != 0 ? 1 : 0);
-    g_tail_below = tail_below;
-    g_pipeline = pipeline;
+lumo_status lumo_get_option(void* ctx, int32_t option, int64_t* value) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !value || option < 0 || option >= LUMO_OPT_COUNT) return LUMO_ERR_INVALID;
+    *value = get_opt(*c, option);
+    return LUMO_OK;
+}
+
+lumo_status lumo_last_schedule(void* ctx, lumo_schedule_info* info) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !info) return LUMO_ERR_INVALID;
+    *info = c->sched;
+    return LUMO_OK;
 }
 
 lumo_status lumo_stats_reset(void* ctx) {

@@ -131,7 +131,7 @@ constexpr int NEE_DRAWS = 6;  // RNG draws per pair in nee_pair
 // generates the pairs, one thread each; this kernel steps its RNG past their draws.
 template <int FX, bool SPLIT>
 __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE_WAVES) void k_shade_q(DScene sc, Paths S, Tasks T, QState cur, QState nxt,
-                                                                      int buckets, uint32_t skip_below, int qsort) {
+                                                                      uint32_t skip_below) {
     const uint32_t count = S.counts[CNT_CUR];
     if (count < skip_below) return;  // k_bounce_q<TAIL> ran this bounce's paths to their end
     const int ns = sc.n_shadow;
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
                 } else {
                     resolve = !mat_is_delta<FX>(sc, m, L);
                     origin = kind == 2 ? sc.n_objs + hr.obj : hr.obj;  // objects, then lights
-                    if (resolve && buckets > 1) key = origin % NB;    // bucket of the shadow rays
+                    if (resolve) key = origin % NB;                   // bucket of the shadow rays
                 }
             }
         }
@@ -232,16 +232,7 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
                 alive = cont;
             }
         }
-        // next ray queue: grouped within the block by origin object and / or direction octant
-        // (qsort 1 / 2 / 3; 0: lane order), see block_slot_sorted
-        uint32_t np;
-        if (qsort) {
-            const int oct = (rn.d.x < 0.0 ? 1 : 0) | (rn.d.y < 0.0 ? 2 : 0) | (rn.d.z < 0.0 ? 4 : 0);
-            const int ck = qsort == 1 ? (origin & 63) : (qsort == 2 ? oct : ((origin & 7) << 3 | oct));
-            np = block_slot_sorted<64>(alive, ck, S.counts + CNT_NEXT);
-        } else {
-            np = block_slot(alive, S.counts + CNT_NEXT);
-        }
+        const uint32_t np = block_slot(alive, S.counts + CNT_NEXT);  // next ray queue, lane order
         if (alive) {
             qv3(nxt, QD_O, np, rn.o);
             qv3(nxt, QD_D, np, rn.d);
@@ -692,10 +683,13 @@ __device__ __forceinline__ void store_final(const Paths& S, const PathReg& P) { 
 // continuation, compacted into `nxt` at once (with the NEE term pending, as k_shade_q); then the
 // pair's two traversals from registers, the term delivered into the continuation's entry or the
 // final radiance (as k_shadow_q).  Neither hits nor records go through HBM.
+// TAIL takes only the paths whose (virtual) slot is in [vlo, vhi): the pipeline's merged passes
+// run their tails pass by pass (each needs its previous pass's ring for Russian roulette).
 template <int STK, bool LDS, int FX, bool TAIL>
 __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_q(DScene sc0, Paths S, Tasks T,
                                                                                   QState cur, QState nxt,
-                                                                                  uint32_t tail_below, int dyn) {
+                                                                                  uint32_t tail_below, int dyn,
+                                                                                  int32_t vlo, int32_t vhi) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
     if ((count < tail_below) != TAIL) return;      // the other kernel takes this bounce
@@ -707,6 +701,8 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
         for (uint32_t w0 = wave_fetch(S.counts + CNT_FETCH_T); w0 < count; w0 = wave_fetch(S.counts + CNT_FETCH_T)) {
             const uint32_t q = w0 + lane_id();
             if (q >= count) continue;
+            const int32_t vs = cur.I(QI_SLOT, q);
+            if (vs < vlo || vs >= vhi) continue;  // another pass of a merged unit
             PathReg P = load_path(cur, q);
             while (bounce_path<STK, FX>(sc, T.delta, P, Cc, Cs)) tailq++;
             store_final(S, P);

@@ -58,8 +58,8 @@ static_assert(ST_COUNT == LUMO_STAGE_COUNT, "stage slots match lumo_stats");
 enum { CNT_NEXT = 0, CNT_FETCH_B, CNT_FETCH_C, CNT_FETCH_T, CNT_CUR, CNT_BUCKET0, CNT_N = CNT_BUCKET0 + 8 };
 // k_shade_q files each path's NEE records into one of NB buckets by the shadow rays' origin
 // object (objects, then lights, mod NB), each bucket a contiguous segment of the record queue, so
-// that a wave's visibility queries start on the same surface and walk the same BVH / kd nodes
-// (LUMO_BUCKETS=0: one bucket).  k_shadow_q walks the buckets in order.
+// that a wave's visibility queries start on the same surface and walk the same BVH / kd nodes.
+// k_shadow_q walks the buckets in order.
 constexpr int NB = 8;
 enum { TC_AABB = 0, TC_KD, TC_TRI, TC_N };  // traversal counters per stage class (closest / shadow)
 constexpr int TC_RESOLVED = 2 * TC_N;  // + shadow records answered without traversal; W_TCOUNT has TC_ALL
@@ -237,35 +237,6 @@ __device__ __forceinline__ uint32_t block_slot_bucket(bool pred, int key, uint32
     }
     __syncthreads();
     const uint32_t pos = pred ? base_s[key] + cnt[key][w] + rank : 0u;
-    __syncthreads();
-    return pos;
-}
-
-// block_slot with the block's entries grouped by key (0 <= key < NK) inside its segment of the
-// queue: an LDS histogram gives each entry its rank within its key, the keys' offsets are
-// scanned, and one atomic per workgroup reserves the segment.  Which path lands in which lane of
-// the consuming kernel does not change any path's result, only how alike the paths of a wave
-// are (rays leaving the same surface in the same octant walk similar BVH / kd nodes).  The
-// order within a key is that of the LDS atomics.  Every thread of the block must call it.
-template <int NK>
-__device__ __forceinline__ uint32_t block_slot_sorted(bool pred, int key, uint32_t* counter) {
-    __shared__ uint32_t hist[NK];
-    __shared__ uint32_t base_s;
-    for (int k = threadIdx.x; k < NK; k += blockDim.x) hist[k] = 0u;
-    __syncthreads();
-    const uint32_t rank = pred ? atomicAdd(&hist[key], 1u) : 0u;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int k = 0; k < NK; ++k) {
-            const uint32_t c = hist[k];
-            hist[k] = t;
-            t += c;
-        }
-        base_s = t ? atomicAdd(counter, t) : 0u;
-    }
-    __syncthreads();
-    const uint32_t pos = pred ? base_s + hist[key] + rank : 0u;
     __syncthreads();
     return pos;
 }

@@ -34,7 +34,7 @@ def tasks_of_tiles(tasks, width, height, tiles):
     return [t for i, t in enumerate(tasks) if (i % tpb) in keep]
 
 
-_queue_generation = 0
+_GENERATION_KEY = "lumo_amd/tile_queue/generation"
 
 
 class TileQueue:
@@ -48,15 +48,22 @@ class TileQueue:
     rank; since each task carries its own seed (renderer.rs:196-203) the film does not depend on
     which rank renders which tile.
 
-    All ranks must construct their queues in the same order (one per render): the store key is
-    numbered by a per-process generation counter.  `chunk` defaults to half of one rank's
-    static share: every claim is one more render call with fewer paths in flight and its own
-    pipeline fill and drain (C1 1024² @ 64 spp, two ranks on one GPU: static 221 ms per frame;
-    chunks of 1/2, 1/4, 1/8 share 266, 348, 435 ms; profiles/r03/dist), so claims stay few and
-    large."""
+    The ranks' queues of one render share a store key, agreed on collectively: rank 0 draws a
+    fresh generation number from the store and broadcasts it (one small collective per render,
+    off the data path), so a rank that built more or fewer queues before (a preview render, a
+    retry) cannot pair up with another render's queue.  When the iteration over a queue ends,
+    every rank adds the tiles it took to a per-key total and, after a barrier, checks that
+    the total is the frame's tile count (`verify`), so a lost or doubled tile raises instead of
+    silently changing the reduced film.  `key=` (with a bare store, no process group) skips both,
+    for single-process use.
 
-    def __init__(self, width, height, world_size, chunk=None, store=None):
-        global _queue_generation
+    `chunk` defaults to half of one rank's static share: every claim is one more render call with
+    fewer paths in flight and its own pipeline fill and drain (C1 1024² @ 64 spp, two ranks on one
+    GPU: static 221 ms per frame; chunks of 1/2, 1/4, 1/8 share 266, 348, 435 ms; profiles/r03/dist),
+    so claims stay few and large."""
+
+    def __init__(self, width, height, world_size, chunk=None, store=None, key=None, group=None):
+        self.collective = key is None
         if store is None:
             import torch.distributed as dist
             store = dist.distributed_c10d._get_default_store()
@@ -67,8 +74,15 @@ class TileQueue:
             raise ValueError(f"chunk {chunk} < 1")
         self.chunk = int(chunk)
         self.store = store
-        _queue_generation += 1
-        self.key = f"lumo_amd/tile_queue/{_queue_generation}"
+        self.group = group
+        self.claimed = 0
+        if key is None:
+            import torch.distributed as dist
+            gen = [int(store.add(_GENERATION_KEY, 1)) if dist.get_rank(group) == 0 else 0]
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast_object_list(gen, src=src, group=group)
+            key = f"lumo_amd/tile_queue/{gen[0]}"
+        self.key = key
 
     def claim(self):
         # store.add returns the counter after the increment: this claim owns [end - chunk, end)
@@ -78,12 +92,26 @@ class TileQueue:
             return []
         return list(range(lo, min(end, self.n_tiles)))
 
+    def verify(self):
+        """Collective, after this rank's last chunk: the chunks the ranks iterated over cover the
+        frame (claims are disjoint by construction; this catches tiles claimed but not taken
+        through the iteration, or a rank on another frame size)."""
+        import torch.distributed as dist
+        self.store.add(self.key + "/done", self.claimed)
+        dist.barrier(group=self.group)
+        total = int(self.store.add(self.key + "/done", 0))
+        if total != self.n_tiles:
+            raise RuntimeError(f"tile queue {self.key}: {total} tiles handed out, the frame has {self.n_tiles}")
+
     def __iter__(self):
         while True:
             tiles = self.claim()
             if not tiles:
-                return
+                break
+            self.claimed += len(tiles)
             yield tiles
+        if self.collective:
+            self.verify()
 
 
 def reduce_film(film, group=None, dst=None):

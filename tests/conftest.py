@@ -5,6 +5,11 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# Every device context of the session fills each buffer it allocates with 0xFF bytes
+# (LUMO_OPT_POISON, read at lumo_create): a kernel that reads a buffer before the render has
+# written it then sees NaN / -1 instead of zeros an earlier test left, so a missing
+# initialisation or cross-stream wait fails deterministically, not depending on test order.
+os.environ.setdefault("LUMO_POISON", "1")
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 

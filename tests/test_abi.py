@@ -32,7 +32,7 @@ def test_ffi_table_covers_header():
 
 def test_abi_version_and_status_strings():
     lib = L.lib()
-    assert lib.lumo_abi_version() == 7
+    assert lib.lumo_abi_version() == 8 == _ffi.ABI_VERSION
     assert lib.lumo_status_str(0) == b"ok"
     assert lib.lumo_status_str(6) == b"unsupported"
 
@@ -51,3 +51,18 @@ def test_null_arguments_rejected():
     lib = L.lib()
     assert lib.lumo_scene_upload(None, None) == 1
     assert lib.lumo_render_tiles(None, None, 0, None, None) == 1
+    assert lib.lumo_set_option(None, 0, 1) == 1
+    assert lib.lumo_get_option(None, 0, None) == 1
+    assert lib.lumo_last_schedule(None, None) == 1
+
+
+def test_option_table_matches_header():
+    """_ffi.OPTIONS lists LUMO_OPT_* in the header's order, and every option has its environment
+    variable in the library's table (names only; values need a context, i.e. a GPU)."""
+    txt = open(os.path.join(ROOT, "include", "lumo_amd.h")).read()
+    body = txt[txt.index("LUMO_OPT_TIMING = 0"):txt.index("LUMO_OPT_COUNT")]
+    names = re.findall(r"\bLUMO_OPT_([A-Z_]+)\b", re.sub(r"/\*.*?\*/", "", body, flags=re.S))
+    assert [n.lower() for n in names] == _ffi.OPTIONS
+    so = open(_ffi.LIB_PATH, "rb").read()
+    for env in re.findall(r"\((LUMO_[A-Z_]+), ", body):
+        assert env.encode() in so, env

@@ -130,8 +130,7 @@ def test_tile_queue_hands_out_every_tile_once():
     from lumo_amd.dist import TileQueue, tiles_per_batch
     store = dist.HashStore()
     n = tiles_per_batch(W, H)
-    qs = [TileQueue(W, H, 2, chunk=2, store=store) for _ in range(2)]
-    qs[1].key = qs[0].key  # the ranks' queues of one render share a key
+    qs = [TileQueue(W, H, 2, chunk=2, store=store, key="render1") for _ in range(2)]  # one render's two ranks
     got = []
     while True:
         a, b = qs[0].claim(), qs[1].claim()
@@ -140,11 +139,11 @@ def test_tile_queue_hands_out_every_tile_once():
             break
         assert len(a) <= 2 and len(b) <= 2
     assert sorted(got) == list(range(n))
-    nxt = TileQueue(W, H, 2, chunk=5, store=store)
+    nxt = TileQueue(W, H, 2, chunk=5, store=store, key="render2")
     assert nxt.claim() == list(range(5))
-    assert TileQueue(W, H, 2, store=store).chunk == max(1, n // 4)
+    assert TileQueue(W, H, 2, store=store, key="render3").chunk == max(1, n // 4)
     with pytest.raises(ValueError):
-        TileQueue(W, H, 2, chunk=0, store=store)
+        TileQueue(W, H, 2, chunk=0, store=store, key="render4")
 
 
 def _dyn_worker(rank, ws, port, out_dir, integrator):
@@ -153,6 +152,9 @@ def _dyn_worker(rank, ws, port, out_dir, integrator):
     import lumo_amd as L
     from lumo_amd.dist import TileQueue, reduce_film, tasks_of_tiles
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+    if rank == 1:  # a rank-local queue first (a preview render): must not shift the shared render's key
+        store = dist.distributed_c10d._get_default_store()
+        TileQueue(W, H, 1, chunk=4, store=store, key="lumo_amd/preview").claim()
     tasks = L.make_tasks(W, H, SPP, SEED)
     film = L.Film(W, H, samples=SPP)
     rays = n_tasks = 0
@@ -226,3 +228,30 @@ def test_render_rejects_unknown_schedule():
     r = L.Renderer(L.Scene.cornell_box(), L.Camera.cornell_box((W, H))).samples(1).seed(1)
     with pytest.raises(ValueError):
         r.render(0, 2, schedule="round-robin")
+
+
+def _verify_worker(rank, ws, port, out_dir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    from lumo_amd.dist import TileQueue
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+    q = TileQueue(W, H, ws, chunk=2)
+    ok = 0
+    if rank == 0:
+        q.claim()  # a chunk handed out but never taken through the iteration: its tiles are lost
+    try:
+        for _ in q:
+            pass
+    except RuntimeError:
+        ok = 1
+    np.save(os.path.join(out_dir, f"raised{rank}.npy"), np.array([ok]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tile_queue_detects_lost_tiles(tmp_path):
+    """A chunk claimed by rank 0 but never rendered (not taken through the iteration): the ranks'
+    per-key total of tiles taken falls short of the frame's, and both ranks raise instead of
+    reducing a film with missing tiles."""
+    _spawn(_verify_worker, 2, str(tmp_path))
+    assert [int(np.load(tmp_path / f"raised{r}.npy")[0]) for r in range(2)] == [1, 1]

@@ -11,7 +11,7 @@ import pytest
 import lumo_amd as L
 import oracle_ffi as O
 from lumo_amd import _ffi, scenes
-from parity import gpu_paths
+from parity import gpu_paths, oracle_threads
 from scenes import default_camera, material_zoo
 
 pytestmark = pytest.mark.gpu
@@ -59,12 +59,11 @@ def test_bdpt_tiles_and_splats(dev, name, res, spp, tail):
     dev.upload(sc, cam)
     tasks = L.make_tasks(res[0], res[1], spp, 0x5EED)
     sp = []
-    lib = _ffi.load()
-    lib.lumo_set_bdpt_tail(tail)
+    dev.set_option("bdpt_tail", tail)
     try:
         bufs, rr = dev.render_tasks(tasks, integrator=BDPT, splats_out=sp)
     finally:
-        lib.lumo_set_bdpt_tail(65536)
+        dev.set_option("bdpt_tail", 65536)
     osp = []
     obufs, orr, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8, integrator=BDPT, splats_out=osp)
     assert sum(len(s) for s in osp) > 0
@@ -134,3 +133,30 @@ def test_bdpt_redo_list_overflow_fails_loudly(dev):
         dev.render_tasks(tasks, integrator=BDPT, splat_film=film, max_vertices=2)
     bufs, _ = dev.render_tasks(tasks, integrator=BDPT, splat_film=film)
     assert all(np.isfinite(b).all() for b in bufs)
+
+
+def test_c4_full_frame_tiles_match_oracle(dev):
+    """C4's configuration at its full resolution (caustics.rs: 1024x1024, BDPT) with the default
+    walk-tail threshold, 2 passes: all 4 096 tiles rendered as one wavefront (1 M samples per
+    pass, every connection item list at full size); every 64th tile's pixels, counts and
+    light-tracing splat list (lumo's order) equal the oracle's."""
+    W = H = 1024
+    sc, cam = _scene("caustics", (W, H))
+    sc.build()
+    dev.upload(sc, cam)
+    assert dev.option("bdpt_tail") == 65536
+    tasks = L.make_tasks(W, H, 2, 0xC4)
+    sp = []
+    bufs, rr = dev.render_tasks(tasks, integrator=BDPT, splats_out=sp)
+    sub = list(range(0, len(tasks), 64))
+    osp = []
+    obufs, orr, _ = O.render_tasks(sc.desc(), cam.desc, [tasks[i] for i in sub], O.WAVEFRONT, oracle_threads(),
+                                   integrator=BDPT, splats_out=osp)
+    assert sum(len(s) for s in osp) > 0
+    for i, ob, o, os_ in zip(sub, obufs, orr, osp):
+        np.testing.assert_array_equal(bufs[i], ob)
+        r = rr[i]
+        assert (r.num_rays, r.num_queries, r.num_camera_rays) == (o.num_rays, o.num_queries, o.num_camera_rays)
+        assert len(sp[i]) == len(os_)
+        np.testing.assert_array_equal(sp[i]["rgb"], os_["rgb"])
+        np.testing.assert_array_equal(sp[i]["x"], os_["x"])

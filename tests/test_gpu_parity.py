@@ -201,9 +201,7 @@ def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
     tiles and the closest / shadow query counts all equal the oracle's.  (Traversal counters are
     not compared here: the device answers p_sct == 0 records without traversal, the oracle
     traces them; lumo_trace's counter parity is in test_gpu_trace / test_gpu_scale.)"""
-    from lumo_amd import _ffi
-    lib = _ffi.load()
-    lib.lumo_set_bounce_mode(fused, tail, pipe)
+    dev.set_option("fused", fused).set_option("tail_below", tail).set_option("pipeline", pipe)
     try:
         cam = L.Camera.cornell_box((48, 40))
         dev.upload(cornell, cam)
@@ -219,7 +217,7 @@ def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
         assert after.closest_queries - before.closest_queries == cnt.closest_queries
         assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
     finally:
-        lib.lumo_set_bounce_mode(-1, 1 << 18, 3)
+        dev.set_option("fused", -1).set_option("tail_below", 1 << 18).set_option("pipeline", 3)
 
 
 @pytest.mark.parametrize("heads", [4, 5, 6, 8])
@@ -227,22 +225,18 @@ def test_head_bounce_counts_match_oracle(cornell, heads):
     """Pipelined passes handing over to the tail kernel after 4, 5, 6 or 8 head bounces (the choice
     between the RR bounce on the head stream or in the tail kernel is a size heuristic; every
     count must give the oracle's tiles)."""
-    import os
-    os.environ["LUMO_HEADS"] = str(heads)  # read when a device context is created
-    try:
-        d = L.Device(0)
-        cam = L.Camera.cornell_box((48, 40))
-        d.upload(cornell, cam)
-        tasks = L.make_tasks(48, 40, 24, SEED)
-        bufs, res = d.render_tasks(tasks)
-        d.close()
-        obufs, ores, _ = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
-        for b, ob, r, orr in zip(bufs, obufs, res, ores):
-            np.testing.assert_array_equal(b, ob)
-            assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
-    finally:
-        os.environ["LUMO_HEADS"] = "0"
-        L.Device(0).close()  # back to the automatic count
+    d = L.Device(0, heads=heads, merge_passes=1)
+    cam = L.Camera.cornell_box((48, 40))
+    d.upload(cornell, cam)
+    tasks = L.make_tasks(48, 40, 24, SEED)
+    bufs, res = d.render_tasks(tasks)
+    sch = d.last_schedule()
+    d.close()
+    assert (sch.schedule, sch.head_bounces, sch.merged_passes) == (1, heads, 1)
+    obufs, ores, _ = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
 
 
 HEADLINE = (1536, 1536, 8)  # 2.36 M slots per pass >= 2^21: the automatic head count is 6, as at 1024^2
@@ -256,10 +250,7 @@ def test_headline_schedule_matches_oracle(cornell):
     query counts, and the frame's closest / shadow query totals equal the oracle's (wavefront
     order).  Then the same frame without pipelining (pipeline 0: passes in sequence, one stream)
     must give the same bits: the cross-stream machinery adds nothing to any per-path result."""
-    from lumo_amd import _ffi
     W, H, spp = HEADLINE
-    lib = _ffi.load()
-    lib.lumo_set_bounce_mode(-1, 1 << 18, 3)
     d = L.Device(0)
     try:
         cam = L.Camera.cornell_box((W, H))
@@ -270,10 +261,12 @@ def test_headline_schedule_matches_oracle(cornell):
         bufs, res = d.render_tasks(tasks, max_paths=1 << 23)
         after = d.stats()
         assert after.launches[1] - before.launches[1] == 6 * spp  # 6 fused head bounces per pass
-        lib.lumo_set_bounce_mode(-1, 1 << 18, 0)
+        sch = d.last_schedule()
+        assert (sch.schedule, sch.head_streams, sch.head_bounces, sch.merged_passes) == (1, 3, 6, 1)
+        d.set_option("pipeline", 0)
         seq, seq_res = d.render_tasks(tasks, max_paths=1 << 23)
+        assert d.last_schedule().schedule == 0
     finally:
-        lib.lumo_set_bounce_mode(-1, 1 << 18, 3)
         d.close()
     for b, s, r, sr in zip(bufs, seq, res, seq_res):
         np.testing.assert_array_equal(b, s)
@@ -348,7 +341,7 @@ def test_busy_time_is_a_union(dev, cornell):
     cam = L.Camera.cornell_box((256, 256))
     dev.upload(cornell, cam)
     tasks = L.make_tasks(256, 256, 32, SEED)
-    lib.lumo_set_timing(1)
+    dev.set_option("timing", 1)
     try:
         lib.lumo_stats_reset(dev.ctx)
         t0 = time.perf_counter()
@@ -358,7 +351,7 @@ def test_busy_time_is_a_union(dev, cornell):
         unit = dev.busy_ms([1, 4])
         allst = dev.busy_ms(range(len(_ffi.STAGES)))
     finally:
-        lib.lumo_set_timing(0)
+        dev.set_option("timing", 0)
     assert 0 < unit <= st.kernel_ms[1] + st.kernel_ms[4] + 1e-3
     assert max(dev.busy_ms([1]), dev.busy_ms([4])) <= unit + 1e-6
     assert unit <= allst <= wall_ms
@@ -414,3 +407,130 @@ def test_orthographic_bdpt_refused(dev):
     dev.upload(dof_scene(), ortho_camera((16, 16)))
     with pytest.raises(Exception):
         dev.render_tasks(L.make_tasks(16, 16, 1, SEED), integrator=L.Integrator.BDPathTrace, splats_out=[])
+
+
+@pytest.mark.parametrize("merge,heads", [(1, 0), (2, 0), (3, 0), (8, 0), (0, 0), (4, 4), (3, 6)])
+def test_merged_passes_match_oracle(cornell, merge, heads):
+    """Merged passes of the fused pipeline (render_pipelined): M consecutive passes' cameras and
+    head bounces run as one queue with virtual slots, their tails / films / rings pass by pass.
+    24 passes with M = 1, 2, 3 (a ragged last unit), 8, automatic (0: the largest, 8, for this
+    tiny frame) and with 4 or 6 head bounces (6 is cut to RR_DEPTH when M > 1): every path (per-pass
+    delta included), tile, ray and query count equals the oracle's (task.rs:28-69 order)."""
+    d = L.Device(0, merge_passes=merge, heads=heads)
+    try:
+        cam = L.Camera.cornell_box((48, 40))
+        d.upload(cornell, cam)
+        tasks = L.make_tasks(48, 40, 24, SEED)
+        _cmp_paths(gpu_paths(d, tasks[4]), O.trace_paths(cornell.desc(), cam.desc, tasks[4]))
+        before = d.stats()
+        bufs, res = d.render_tasks(tasks)
+        after = d.stats()
+        sch = d.last_schedule()
+    finally:
+        d.close()
+    m = merge if merge else 8
+    want_heads = heads if heads else 5  # automatic: 5 for passes of < 2^21 slots
+    assert (sch.schedule, sch.merged_passes, sch.head_bounces) == (1, m, min(want_heads, 5) if m > 1 else want_heads)
+    obufs, ores, cnt = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+    assert after.closest_queries - before.closest_queries == cnt.closest_queries
+    assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
+
+
+def test_share_schedule_matches_sequential_and_oracle(cornell):
+    """One rank's 1/8 share of the C1 frame (the tiles with index % 8 == 0 of 1024^2, 131 k slots
+    per pass, bench.py --share) with the merged-pass schedule the device picks for it (8 passes per
+    unit, 3 head streams): every tile, ray and query count equals the same share rendered with
+    sequential passes on one stream, and every 8th tile of the share equals the oracle's."""
+    from lumo_amd.dist import shard_tasks
+    W = H = 1024
+    spp = 24
+    cam = L.Camera.cornell_box((W, H))
+    tasks = shard_tasks(L.make_tasks(W, H, spp, SEED), W, H, 0, 8)
+    d = L.Device(0)
+    try:
+        d.upload(cornell, cam)
+        bufs, res = d.render_tasks(tasks)
+        sch = d.last_schedule()
+        d.set_option("pipeline", 0)
+        seq, seq_res = d.render_tasks(tasks)
+        assert d.last_schedule().schedule == 0
+    finally:
+        d.close()
+    assert (sch.schedule, sch.head_streams, sch.merged_passes) == (1, 3, 8)
+    for b, s, r, sr in zip(bufs, seq, res, seq_res):
+        np.testing.assert_array_equal(b, s)
+        assert (r.num_rays, r.num_queries) == (sr.num_rays, sr.num_queries)
+    sub = list(range(0, len(tasks), 8))
+    obufs, ores, _ = O.render_tasks(cornell.desc(), cam.desc, [tasks[i] for i in sub], O.WAVEFRONT, oracle_threads())
+    for i, ob, orr in zip(sub, obufs, ores):
+        np.testing.assert_array_equal(bufs[i], ob)
+        assert (res[i].num_rays, res[i].num_queries) == (orr.num_rays, orr.num_queries)
+
+
+def test_two_contexts_two_threads(cornell):
+    """lumo's executors share nothing but the task receiver (pool.rs:17-38): two contexts on
+    device 0, each driven from its own host thread with its own execution options (one pipelined
+    with timing on, one with sequential passes), render disjoint tile sets concurrently, three
+    times each; every tile equals one context's render of the whole frame, and each context keeps
+    its own options and schedule (INTEGRATION.md's one-context-per-thread layout)."""
+    import threading
+    W = H = 256
+    cam = L.Camera.cornell_box((W, H))
+    tasks = list(L.make_tasks(W, H, 16, SEED))
+    halves = [tasks[0::2], tasks[1::2]]
+    ref = L.Device(0)
+    ref.upload(cornell, cam)
+    rbufs, rres = ref.render_tasks(tasks)
+    ref.close()
+    devs = [L.Device(0, timing=1), L.Device(0, pipeline=0, merge_passes=2)]
+    for d in devs:
+        d.upload(cornell, cam)
+    out, errs = [None, None], []
+
+    def run(k):
+        try:
+            for _ in range(3):
+                out[k] = devs[k].render_tasks(halves[k])
+        except Exception as e:  # noqa: BLE001 (re-raised below)
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    try:
+        assert not errs, errs
+        assert devs[0].option("timing") == 1 and devs[1].option("timing") == 0
+        assert devs[0].last_schedule().schedule == 1 and devs[1].last_schedule().schedule == 0
+        assert devs[0].stats().kernel_ms[1] > 0 and devs[1].stats().kernel_ms[1] == 0  # timing only in context 0
+    finally:
+        for d in devs:
+            d.close()
+    for k in range(2):
+        bufs, res = out[k]
+        for i, (b, r) in enumerate(zip(bufs, res)):
+            np.testing.assert_array_equal(b, rbufs[2 * i + k])
+            assert (r.num_rays, r.num_queries) == (rres[2 * i + k].num_rays, rres[2 * i + k].num_queries)
+
+
+def test_option_api(dev):
+    """lumo_set_option / lumo_get_option: per-context values, range checks (LUMO_ERR_INVALID)."""
+    d2 = L.Device(0)
+    try:
+        dev.set_option("split_pipe", 2)
+        assert dev.option("split_pipe") == 2 and d2.option("split_pipe") == 4
+        for name, bad in (("bounce_threads", 96), ("split_pipe", 0), ("stack_class", 12), ("fused", 2),
+                          ("merge_passes", 9), ("timing", 2)):
+            with pytest.raises(RuntimeError, match="INVALID"):
+                dev.set_option(name, bad)
+        assert dev.option("poison") == 1  # the test session's LUMO_POISON (conftest)
+        from lumo_amd import _ffi
+        v = __import__("ctypes").c_int64()
+        assert _ffi.load().lumo_get_option(dev.ctx, len(_ffi.OPTIONS), __import__("ctypes").byref(v)) == 1
+    finally:
+        dev.set_option("split_pipe", 4)
+        d2.close()

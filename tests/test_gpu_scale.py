@@ -8,7 +8,7 @@
   inputs); per-path parity of two 16x16 tiles at each bench camera (k_closest / k_shade /
   k_shadow of that stack class, kdtree.rs:101-169 + bvh.rs:315-362 semantics).
 * Cornell and the small dragon over every stack class >= the scene's need x LDS staging on/off
-  x lean/full feature kernels (LUMO_STACK_CLASS, lumo_set_lds_staging, LUMO_FULL_KERNELS):
+  x lean/full feature kernels (options stack_class, lds_staging, full_kernels):
   per-path parity and tile parity for each instantiation, with lumo_scene_info confirming the
   variant that ran.
 """
@@ -21,7 +21,7 @@ import lumo_amd as L
 import oracle_ffi as O
 from lumo_amd import _ffi, scenes
 from lumo_amd.procedural import torus_knot_tube
-from parity import gpu_paths
+from parity import gpu_paths, oracle_threads
 
 pytestmark = pytest.mark.gpu
 SEED = 0x5EED1234
@@ -150,15 +150,9 @@ def test_paths_full_scale_bench_camera(dev, which, request):
 
 # ---------------------------------------------------------------------------- kernel variants
 @pytest.fixture
-def variant_env():
-    saved = {k: os.environ.get(k) for k in ("LUMO_STACK_CLASS", "LUMO_FULL_KERNELS")}
+def variant_env(dev):
     yield
-    for k, v in saved.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
-    _ffi.load().lumo_set_lds_staging(1)
+    dev.set_option("stack_class", 0).set_option("full_kernels", 0).set_option("lds_staging", 1)
 
 
 def _variant_scene(name):
@@ -175,9 +169,7 @@ def _variant_scene(name):
 def test_kernel_variants(dev, variant_env, name, cls, lds, full):
     sc, cam, tasks = _variant_scene(name)
     sc.build()
-    os.environ["LUMO_STACK_CLASS"] = str(cls)
-    os.environ["LUMO_FULL_KERNELS"] = str(full)
-    _ffi.load().lumo_set_lds_staging(lds)
+    dev.set_option("stack_class", cls).set_option("full_kernels", full).set_option("lds_staging", lds)
     dev.upload(sc, cam)
     info = dev.scene_info()
     if info.stack_class != cls:
@@ -203,8 +195,7 @@ def test_kernel_variants(dev, variant_env, name, cls, lds, full):
 def test_bounce_modes_small_dragon(dev, fused, tail, pipe):
     """The fused bounce kernel and the tail kernel on an instanced glass mesh (feature class 1,
     no LDS staging, deep kd stack): paths and tiles equal the oracle's."""
-    lib = _ffi.load()
-    lib.lumo_set_bounce_mode(fused, tail, pipe)
+    dev.set_option("fused", fused).set_option("tail_below", tail).set_option("pipeline", pipe)
     try:
         sc, cam, tasks = _variant_scene("small_dragon")
         sc.build()
@@ -220,7 +211,7 @@ def test_bounce_modes_small_dragon(dev, fused, tail, pipe):
             np.testing.assert_array_equal(b, ob)
             assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
     finally:
-        lib.lumo_set_bounce_mode(-1, 1 << 18, 3)
+        dev.set_option("fused", -1).set_option("tail_below", 1 << 18).set_option("pipeline", 3)
 
 
 # ---------------------------------------------------------------------------- TOP staging
@@ -248,44 +239,35 @@ def test_top_staging_budgets(mid_bistro, budget_kb, top):
     HBM otherwise: with the staged prefix cutting the objects BVH (8 KiB), the lights BVH
     (20 KiB), neither (default) or TOP off, lumo_trace (t / kind / object and the traversal
     counters) and rendered tiles equal the oracle's."""
-    env = {"LUMO_TOP": str(top)}
+    opts = {"top_staging": top}
     if budget_kb is not None:
-        env["LUMO_TOP_KB"] = str(budget_kb)
-    saved = {k: os.environ.get(k) for k in ("LUMO_TOP", "LUMO_TOP_KB")}
-    os.environ.update(env)
-    try:
-        d = L.Device(0)  # the budget is read when a context is created
-        sc = mid_bistro
-        d.upload(sc)
-        info = d.scene_info()
-        desc = sc.desc()
-        if top == 0:
-            assert info.top_bytes == 0
-        elif budget_kb == 8:
-            assert 0 < info.top_object_nodes < desc.num_object_nodes and info.top_light_nodes == 0
-        elif budget_kb == 20:
-            assert info.top_object_nodes == desc.num_object_nodes and 0 < info.top_light_nodes < desc.num_light_nodes
-        else:
-            assert info.top_object_nodes == desc.num_object_nodes and info.top_light_nodes == desc.num_light_nodes
-        o, dd = _closest_rays(desc, (-16.0, 5.0, -1.0), 1 << 17, 21)
-        _trace_cmp(d, sc, o, dd)
-        o, dd, li = _visibility_rays(desc, 1 << 17, 22)
-        _trace_cmp(d, sc, o, dd, lights=li)
-        cam = scenes.bistro_camera((96, 64))
-        d.upload(sc, cam)
-        tasks = L.make_tasks(96, 64, 4, SEED)[8:14]
-        bufs, res = d.render_tasks(tasks)
-        obufs, ores, _ = O.render_tasks(desc, cam.desc, tasks, O.WAVEFRONT, 8)
-        for b, ob, r, orr in zip(bufs, obufs, res, ores):
-            np.testing.assert_array_equal(b, ob)
-            assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
-        d.close()
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        opts["top_kb"] = budget_kb
+    d = L.Device(0, **opts)  # the budget applies at the scene upload
+    sc = mid_bistro
+    d.upload(sc)
+    info = d.scene_info()
+    desc = sc.desc()
+    if top == 0:
+        assert info.top_bytes == 0
+    elif budget_kb == 8:
+        assert 0 < info.top_object_nodes < desc.num_object_nodes and info.top_light_nodes == 0
+    elif budget_kb == 20:
+        assert info.top_object_nodes == desc.num_object_nodes and 0 < info.top_light_nodes < desc.num_light_nodes
+    else:
+        assert info.top_object_nodes == desc.num_object_nodes and info.top_light_nodes == desc.num_light_nodes
+    o, dd = _closest_rays(desc, (-16.0, 5.0, -1.0), 1 << 17, 21)
+    _trace_cmp(d, sc, o, dd)
+    o, dd, li = _visibility_rays(desc, 1 << 17, 22)
+    _trace_cmp(d, sc, o, dd, lights=li)
+    cam = scenes.bistro_camera((96, 64))
+    d.upload(sc, cam)
+    tasks = L.make_tasks(96, 64, 4, SEED)[8:14]
+    bufs, res = d.render_tasks(tasks)
+    obufs, ores, _ = O.render_tasks(desc, cam.desc, tasks, O.WAVEFRONT, 8)
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+    d.close()
 
 
 @pytest.mark.parametrize("k,groups", [(1, 1), (2, 1), (3, 1), (4, 1), (2, 2), (4, 2), (3, 3), (4, 4)])
@@ -295,28 +277,61 @@ def test_split_pipeline_passes_in_flight(mid_bistro, k, groups):
     independent groups; a 9-pass render's tiles, ray and query counts equal the oracle's (a unit
     waits for its group's previous pass's camera, and its ring before bounce RR_DEPTH and before
     its film; set reuse is ordered by stream)."""
-    saved = {v: os.environ.get(v) for v in ("LUMO_SPLIT_PIPE", "LUMO_SPLIT_GROUPS")}
-    os.environ["LUMO_SPLIT_PIPE"] = str(k)
-    os.environ["LUMO_SPLIT_GROUPS"] = str(groups)
-    try:
-        d = L.Device(0)
-        cam = scenes.bistro_camera((64, 48))
-        d.upload(mid_bistro, cam)
-        assert d.scene_info().n_shadow > 1
-        tasks = L.make_tasks(64, 48, 9, SEED)
-        before = d.stats()
-        bufs, res = d.render_tasks(tasks)
-        after = d.stats()
-        d.close()
-    finally:
-        for v, x in saved.items():
-            if x is None:
-                os.environ.pop(v, None)
-            else:
-                os.environ[v] = x
+    d = L.Device(0, split_pipe=k, split_groups=groups)
+    cam = scenes.bistro_camera((64, 48))
+    d.upload(mid_bistro, cam)
+    assert d.scene_info().n_shadow > 1
+    tasks = L.make_tasks(64, 48, 9, SEED)
+    before = d.stats()
+    bufs, res = d.render_tasks(tasks)
+    after = d.stats()
+    sch = d.last_schedule()
+    d.close()
+    # the requested schedule ran (free HBM did not cut the units in flight back)
+    if k == 1:
+        assert sch.schedule == 0
+    else:
+        assert (sch.schedule, sch.units_in_flight, sch.task_groups) == (2, k, min(groups, k))
     obufs, ores, cnt = O.render_tasks(mid_bistro.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
     for b, ob, r, orr in zip(bufs, obufs, res, ores):
         np.testing.assert_array_equal(b, ob)
         assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
     assert after.closest_queries - before.closest_queries == cnt.closest_queries
     assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
+
+
+def test_c3_bench_schedule_full_frame(c3):
+    """C3 as the bench renders it: the full 1920x1080 Bistro stand-in frame (8 160 tiles, 2.07 M
+    slots per pass, n_shadow = 11, the full TOP set) through render_split_pipelined with the
+    default 4 units in flight in 2 task groups, at 2 spp.  Every tile, ray and query count equals
+    the same frame with sequential passes (split_pipe 1), and every 64th tile equals the oracle's
+    (task.rs:25-82 pass order, renderer.rs:179-204 tasks).  Buffers are poisoned (conftest), so a
+    unit that read another stream's stale counters or tables would show."""
+    W, H, spp = 1920, 1080, 2
+    cam = scenes.bistro_camera((W, H))
+    tasks = L.make_tasks(W, H, spp, SEED)
+    d = L.Device(0)
+    try:
+        d.upload(c3, cam)
+        info = d.scene_info()
+        assert info.n_shadow == 11 and info.top_bytes > 0 and info.top_object_nodes == c3.desc().num_object_nodes
+        before = d.stats()
+        bufs, res = d.render_tasks(tasks, max_paths=1 << 23)
+        after = d.stats()
+        sch = d.last_schedule()
+        assert (sch.schedule, sch.units_in_flight, sch.task_groups, sch.fused) == (2, 4, 2, 0)
+        d.set_option("split_pipe", 1)
+        seq, seq_res = d.render_tasks(tasks, max_paths=1 << 23)
+        assert d.last_schedule().schedule == 0
+    finally:
+        d.close()
+    for b, s, r, sr in zip(bufs, seq, res, seq_res):
+        np.testing.assert_array_equal(b, s)
+        assert (r.num_rays, r.num_queries) == (sr.num_rays, sr.num_queries)
+    sub = list(range(0, len(tasks), 64))
+    obufs, ores, _ = O.render_tasks(c3.desc(), cam.desc, [tasks[i] for i in sub], O.WAVEFRONT, oracle_threads())
+    bad = [i for i, ob in zip(sub, obufs) if not np.array_equal(bufs[i], ob)]
+    assert not bad, f"{len(bad)} of {len(sub)} sampled tiles differ, first {bad[:8]}"
+    for i, orr in zip(sub, ores):
+        assert (res[i].num_rays, res[i].num_queries) == (orr.num_rays, orr.num_queries)
+    assert after.closest_queries > before.closest_queries
