@@ -402,6 +402,9 @@ enum {
                                   (LUMO_FULL_KERNELS, 0)                                            */
     LUMO_OPT_POISON,           /* debug: fill every newly allocated device buffer with 0xFF bytes,
                                   so a read of a buffer before its first write shows (LUMO_POISON, 0)*/
+    LUMO_OPT_TAIL_PRIORITY,    /* fused pipeline: the stream of the passes' tails, films and rings (the
+                                  chain each pass's Russian roulette waits on) at high priority: 0 / 1
+                                  (LUMO_TAIL_PRIORITY, 0)                                           */
     LUMO_OPT_COUNT
 };
 lumo_status lumo_set_option(void* ctx, int32_t option, int64_t value);

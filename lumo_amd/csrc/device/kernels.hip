@@ -37,6 +37,19 @@ using namespace lumo::dev;
 
 namespace {
 
+// Per-slot outputs of pass m of a merged unit (render_pipelined): virtual slots [m N, (m + 1) N).
+__host__ __device__ inline Paths pass_view(const Paths& P, int m, int N) {
+    Paths V = P;
+    const size_t o = (size_t)m * (size_t)N;
+    V.rad = P.rad + 4 * o;
+    V.lam = P.lam + 4 * o;
+    V.raster = P.raster + 2 * o;
+    V.depth = P.depth + o;
+    V.queries = P.queries + o;
+    V.p_valid = P.p_valid + o;
+    return V;
+}
+
 // ------------------------------------------------------------------ init
 // Pixel sampler seeds: the tile stream's first P outputs.
 __global__ void k_init_seeds(Tasks T, Paths S, int n_tasks) {
@@ -355,13 +368,12 @@ __device__ __forceinline__ double gauss(double x, double sigma) {
 // raster order, the samples whose (tile-clipped) 3x3 footprint contains it.  Sources farther
 // than 2 px cannot.  `src` reads a source sample by its pixel index within the tile.
 template <class Src>
-__device__ __forceinline__ void film_gather(const Paths& S, const lumo_tile_task& t, const DCam& cam, int s, int j,
-                                            const Src& src, const FilmTerms* terms = nullptr) {
+__device__ __forceinline__ void film_gather_acc(double* acc, const lumo_tile_task& t, const DCam& cam, int j,
+                                                const Src& src, const FilmTerms* terms = nullptr) {
     const int W = (int)(t.px_max[0] - t.px_min[0]), H = (int)(t.px_max[1] - t.px_min[1]);
     const int dx = j % W, dy = j / W;
     const uint64_t gx = t.px_min[0] + dx, gy = t.px_min[1] + dy;
     const uint64_t r = (uint64_t)ceil(cam.fr - 0.5);
-    double acc[4] = {S.film[4 * s], S.film[4 * s + 1], S.film[4 * s + 2], S.film[4 * s + 3]};
     const double gr = gauss(cam.fr, cam.fsig);
     for (int sy = dy - 2; sy <= dy + 1; ++sy) {
         if (sy < 0 || sy >= H) continue;
@@ -391,6 +403,12 @@ __device__ __forceinline__ void film_gather(const Paths& S, const lumo_tile_task
             }
         }
     }
+}
+template <class Src>
+__device__ __forceinline__ void film_gather(const Paths& S, const lumo_tile_task& t, const DCam& cam, int s, int j,
+                                            const Src& src, const FilmTerms* terms = nullptr) {
+    double acc[4] = {S.film[4 * s], S.film[4 * s + 1], S.film[4 * s + 2], S.film[4 * s + 3]};
+    film_gather_acc(acc, t, cam, j, src, terms);
     for (int i = 0; i < 4; ++i) S.film[4 * s + i] = acc[i];
 }
 
@@ -423,9 +441,13 @@ struct LdsSrc {  // sources staged in LDS by k_finish_film
 
 // k_finish + k_film for tasks of at most BLOCK pixels (lumo's 16x16 tiles): one block per task,
 // the tile's sample RGB and raster positions staged in LDS instead of a round trip through HBM.
-// Same arithmetic as the two kernels, so the film is bit-identical.
-__global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S, Tasks T, DCam cam, uint32_t pass, Dump dump,
-                                                        int dump_p, int tone_map, double tone_arg, int t0) {
+// npass consecutive passes (a merged unit of render_pipelined; pass m's per-slot outputs at
+// virtual slots + m * vstride) in pass order, the tile's film accumulators held in registers
+// across them.  Same arithmetic and additions in the same order as one k_finish + k_film per
+// pass, so the film is bit-identical.
+__global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S0, Tasks T, DCam cam, uint32_t pass0,
+                                                        Dump dump, int dump_p, int tone_map, double tone_arg, int t0,
+                                                        int npass, int vstride) {
     __shared__ double l_rgb[3 * BLOCK];
     __shared__ double l_ras[2 * BLOCK];
     __shared__ uint32_t l_ok[BLOCK];
@@ -437,32 +459,41 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S, Tasks
     const int s = first + j;
     const int r = (int)ceil(cam.fr - 0.5);
     const bool pre = r <= FILM_R;  // uniform
-    if (j < P) {
-        const bool ok = S.p_valid[s] != 0;
-        l_ok[j] = ok ? 1u : 0u;
-        if (ok) {
-            const V3 rgb = finish_one(sc, S, cam, s, pass, dump, dump_p, tone_map, tone_arg);
-            l_rgb[3 * j] = rgb.x;
-            l_rgb[3 * j + 1] = rgb.y;
-            l_rgb[3 * j + 2] = rgb.z;
-            const double rx = S.raster[2 * s], ry = S.raster[2 * s + 1];
-            l_ras[2 * j] = rx;
-            l_ras[2 * j + 1] = ry;
-            if (pre) {  // this sample's column / row terms, as film_gather computes them
-                const double gr = gauss(cam.fr, cam.fsig);
-                const int64_t px = rx > 0.0 ? (int64_t)floor(rx) : 0, py = ry > 0.0 ? (int64_t)floor(ry) : 0;
-                for (int i = 0; i <= 2 * r; ++i) {
-                    const double gx = (double)(px - r + i), gy = (double)(py - r + i);
-                    l_wx[i * BLOCK + j] = rmax(gauss(rx - (0.5 + gx), cam.fsig) - gr, 0.0);
-                    l_wy[i * BLOCK + j] = rmax(gauss(ry - (0.5 + gy), cam.fsig) - gr, 0.0);
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (j < P)
+        for (int i = 0; i < 4; ++i) acc[i] = S0.film[4 * s + i];
+    for (int m = 0; m < npass; ++m) {
+        const Paths S = pass_view(S0, m, vstride);
+        if (j < P) {
+            const bool ok = S.p_valid[s] != 0;
+            l_ok[j] = ok ? 1u : 0u;
+            if (ok) {
+                const V3 rgb = finish_one(sc, S, cam, s, pass0 + (uint32_t)m, dump, dump_p, tone_map, tone_arg);
+                l_rgb[3 * j] = rgb.x;
+                l_rgb[3 * j + 1] = rgb.y;
+                l_rgb[3 * j + 2] = rgb.z;
+                const double rx = S.raster[2 * s], ry = S.raster[2 * s + 1];
+                l_ras[2 * j] = rx;
+                l_ras[2 * j + 1] = ry;
+                if (pre) {  // this sample's column / row terms, as film_gather computes them
+                    const double gr = gauss(cam.fr, cam.fsig);
+                    const int64_t px = rx > 0.0 ? (int64_t)floor(rx) : 0, py = ry > 0.0 ? (int64_t)floor(ry) : 0;
+                    for (int i = 0; i <= 2 * r; ++i) {
+                        const double gx = (double)(px - r + i), gy = (double)(py - r + i);
+                        l_wx[i * BLOCK + j] = rmax(gauss(rx - (0.5 + gx), cam.fsig) - gr, 0.0);
+                        l_wy[i * BLOCK + j] = rmax(gauss(ry - (0.5 + gy), cam.fsig) - gr, 0.0);
+                    }
                 }
             }
         }
+        __syncthreads();
+        count_checks(j < P && l_ok[j] ? sample_check(ldc(S.rad, s)) : 0, S.checks);
+        const FilmTerms terms{l_wx, l_wy, r};
+        if (j < P) film_gather_acc(acc, T.t[ti], cam, j, LdsSrc{l_rgb, l_ras, l_ok}, pre ? &terms : nullptr);
+        __syncthreads();  // the next pass overwrites the staged samples
     }
-    __syncthreads();
-    count_checks(j < P && l_ok[j] ? sample_check(ldc(S.rad, s)) : 0, S.checks);
-    const FilmTerms terms{l_wx, l_wy, r};
-    if (j < P) film_gather(S, T.t[ti], cam, s, j, LdsSrc{l_rgb, l_ras, l_ok}, pre ? &terms : nullptr);
+    if (j < P)
+        for (int i = 0; i < 4; ++i) S0.film[4 * s + i] = acc[i];
 }
 
 // task.rs:42-53 + 64-69: ring update in pixel order, then delta for the next pass.
@@ -702,6 +733,7 @@ struct Opts {
     int stack_class = 0;               // kd stack class override (0: the scene's need)
     int full_kernels = 0;              // general feature kernels for lean scenes too
     int poison = 0;                    // new device buffers filled with 0xFF (reads before writes show as NaN / -1)
+    int tail_priority = 0;             // the pipelined passes' tail / film / ring stream at high priority
 };
 
 struct Ctx {
@@ -752,7 +784,12 @@ lumo_status dev_alloc(const Ctx& c, DevBuf& b, size_t bytes) {
     b.bytes = 0;
     if (hipMalloc(&b.p, bytes) != hipSuccess) return LUMO_ERR_OOM;
     b.bytes = bytes;
-    if (c.o.poison) (void)hipMemset(b.p, 0xFF, bytes);  // debug: new buffers all ones (NaN, -1)
+    if (c.o.poison) {  // debug: new buffers all ones (NaN, -1)
+        // hipMemset runs on the null stream, which the context's non-blocking streams do not wait
+        // for: finish it here, or it could land after the render's own initialisation
+        (void)hipMemset(b.p, 0xFF, bytes);
+        (void)hipStreamSynchronize(nullptr);
+    }
     return LUMO_OK;
 }
 
@@ -950,18 +987,6 @@ size_t split_set_bytes(const Paths& S, int N, int ns) {
            S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4 + (ns > 1 ? 16 : 0));
 }
 
-// Per-slot outputs of pass m of a merged unit (render_pipelined): virtual slots [m N, (m + 1) N).
-Paths pass_view(const Paths& P, int m, int N) {
-    Paths V = P;
-    const size_t o = (size_t)m * (size_t)N;
-    V.rad = P.rad + 4 * o;
-    V.lam = P.lam + 4 * o;
-    V.raster = P.raster + 2 * o;
-    V.depth = P.depth + o;
-    V.queries = P.queries + o;
-    V.p_valid = P.p_valid + o;
-    return V;
-}
 
 // Pipelined passes (n_shadow == 1, fused bounces).  Russian roulette reads the pass's adaptive
 // delta only from depth RR_DEPTH on (path_trace.rs:60-69), and that delta needs the previous
@@ -1001,6 +1026,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
     if (st) return st;
     hipStream_t As[3] = {c.stream, c.stream3, c.stream4};
     hipStream_t B = c.stream2;
+    hipStream_t F = NA <= 2 ? c.stream4 : B;  // the films (four streams: the device's hardware queues)
     // each set's counters start zeroed; from then on every unit's last ring zeroes its set's counters
     {
         ZeroList z;
@@ -1075,14 +1101,14 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
                     },
                     B);
             }
-            // film, then the ring (which computes the samples' luminance itself).  A film on a
-            // stream of its own, off the chain the next pass's Russian roulette waits on, measured
-            // slower (C1 1/8 share 438 -> 488 ms per frame), ring-then-film the same
-            if (max_P <= BLOCK) {
-                StageTimer tm(c, c.o.timing, ST_FILM, B);
-                k_finish_film<<<n_tasks, BLOCK, 0, B>>>(c.sc, V, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
-                                                        c.tone_arg, 0);
-            } else {
+            // the ring (which computes the samples' luminance itself): the next pass's Russian
+            // roulette waits for it; the film is off that chain
+            {
+                StageTimer tm(c, c.o.timing, ST_RING, B);
+                k_ring<<<n_tasks, 64, 0, B>>>(c.sc, V, T, n_tasks, 1, m == mu - 1 ? P.counts : nullptr, 0);
+            }
+            HIPCHK(hipGetLastError());
+            if (max_P > BLOCK) {  // tiles larger than a block: per pass, on B
                 {
                     StageTimer tm(c, c.o.timing, ST_FINISH, B);
                     k_finish<<<gN, BLOCK, 0, B>>>(c.sc, V, c.cam, N, (uint32_t)pass, D, dump_p, c.tone_map, c.tone_arg,
@@ -1091,18 +1117,25 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
                 StageTimer tm(c, c.o.timing, ST_FILM, B);
                 k_film<<<gN, BLOCK, 0, B>>>(V, T, c.cam, N, 0);
             }
-            {
-                StageTimer tm(c, c.o.timing, ST_RING, B);
-                k_ring<<<n_tasks, 64, 0, B>>>(c.sc, V, T, n_tasks, 1, m == mu - 1 ? P.counts : nullptr, 0);
-            }
+        }
+        HIPCHK(hipEventRecord(c.pass_ev[set], B));
+        // the film of the unit's passes, one launch in pass order (after the previous unit's film on
+        // the same stream), on a stream of its own when one is free
+        if (max_P <= BLOCK) {
+            if (F != B) HIPCHK(hipStreamWaitEvent(F, c.pass_ev[set], 0));
+            StageTimer tm(c, c.o.timing, ST_FILM, F);
+            k_finish_film<<<n_tasks, BLOCK, 0, F>>>(c.sc, P, T, c.cam, (uint32_t)p0, D, dump_p, c.tone_map, c.tone_arg,
+                                                    0, mu, N);
             HIPCHK(hipGetLastError());
         }
-        HIPCHK(hipEventRecord(c.film_ev[set], B));
-        HIPCHK(hipEventRecord(c.pass_ev[set], B));
+        HIPCHK(hipEventRecord(c.film_ev[set], max_P <= BLOCK ? F : B));
         if (c.o.timing) resolve_timers(c);
     }
-    // the results are copied on stream 0: after every set's last unit
-    for (int k = 0; k < NSETS; ++k) HIPCHK(hipStreamWaitEvent(As[0], c.pass_ev[k], 0));
+    // the results are copied on stream 0: after every set's last unit and film
+    for (int k = 0; k < NSETS; ++k) {
+        HIPCHK(hipStreamWaitEvent(As[0], c.pass_ev[k], 0));
+        HIPCHK(hipStreamWaitEvent(As[0], c.film_ev[k], 0));
+    }
     join.ok = true;
     return LUMO_OK;
 }
@@ -1328,7 +1361,7 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         if (max_P <= BLOCK) {
             StageTimer tm(c, c.o.timing, ST_FILM, sm);
             k_finish_film<<<t1 - t0, BLOCK, 0, sm>>>(c.sc, Q, T, c.cam, (uint32_t)ps.pass, Dump{}, 0, c.tone_map,
-                                                     c.tone_arg, t0);
+                                                     c.tone_arg, t0, 1, 0);
         } else {
             {
                 StageTimer tm(c, c.o.timing, ST_FINISH, sm);
@@ -1814,7 +1847,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         if (max_P <= BLOCK) {  // one block per tile (lumo's 16x16 tiles)
             StageTimer tm(c, c.o.timing, ST_FILM);
             k_finish_film<<<(int)n_tasks, BLOCK, 0, sm>>>(c.sc, S, T, c.cam, (uint32_t)pass, D, dump_p, c.tone_map,
-                                                          c.tone_arg, 0);
+                                                          c.tone_arg, 0, 1, 0);
         } else {
             {
                 StageTimer tm(c, c.o.timing, ST_FINISH);
@@ -1939,11 +1972,11 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         c.stats.tri_tests[k] += tc[k * TC_N + TC_TRI];
     }
     c.stats.shadow_resolved += tc[TC_RESOLVED];
-#if LUMO_SHADOW_STATS
+#if LUMO_SHADOW_STATS || LUMO_PHASE_CLOCKS
     {
         unsigned long long ss[TC_STATS];
         HIPCHK(hipMemcpy(ss, S.tcount + TC_ALL, sizeof(ss), hipMemcpyDeviceToHost));
-        fprintf(stderr, "LUMO_SHADOW_STATS");
+        fprintf(stderr, LUMO_SHADOW_STATS ? "LUMO_SHADOW_STATS" : "LUMO_PHASE_CLOCKS");
         for (int k = 0; k < TC_STATS; ++k) fprintf(stderr, " %llu", ss[k]);
         fprintf(stderr, "\n");
     }
@@ -1956,7 +1989,7 @@ const char* const kOptEnv[LUMO_OPT_COUNT] = {
     "LUMO_TIMING", "LUMO_LDS", "LUMO_TOP", "LUMO_FUSED", "LUMO_TAIL", "LUMO_PIPELINE", "LUMO_HEADS", "LUMO_MERGE",
     "LUMO_DYN", "LUMO_BOUNCE_THREADS", "LUMO_SPLIT_PIPE", "LUMO_SPLIT_GROUPS", "LUMO_BDPT_TAIL", "LUMO_BOUNCE_AHEAD",
     "LUMO_LDS_GRID", "LUMO_TOP_GRID", "LUMO_TOP_KB", "LUMO_KD_LDS", "LUMO_STACK_CLASS", "LUMO_FULL_KERNELS",
-    "LUMO_POISON"};
+    "LUMO_POISON", "LUMO_TAIL_PRIORITY"};
 
 void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
     lo = 0;
@@ -1976,6 +2009,25 @@ void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
         case LUMO_OPT_STACK_CLASS: hi = 64; break;
         default: break;
     }
+}
+
+// The pipelined passes' tail stream (stream2), (re)created at normal or the device's highest
+// priority: the workgroups of its kernels are then dispatched ahead of the head streams' as CUs
+// free up.
+lumo_status make_tail_stream(Ctx& c, int high) {
+    (void)hipSetDevice(c.device);
+    if (c.stream2) {
+        (void)hipStreamSynchronize(c.stream2);
+        (void)hipStreamDestroy(c.stream2);
+        c.stream2 = nullptr;
+    }
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = least = 0;
+    if (hipStreamCreateWithPriority(&c.stream2, hipStreamNonBlocking, high ? greatest : least) != hipSuccess) {
+        last_hip_error() = hipErrorInvalidValue;
+        return LUMO_ERR_HIP;
+    }
+    return LUMO_OK;
 }
 
 lumo_status set_opt(Ctx& c, int k, int64_t v) {
@@ -2011,6 +2063,13 @@ lumo_status set_opt(Ctx& c, int k, int64_t v) {
         case LUMO_OPT_STACK_CLASS: o.stack_class = iv; break;
         case LUMO_OPT_FULL_KERNELS: o.full_kernels = iv; break;
         case LUMO_OPT_POISON: o.poison = iv; break;
+        case LUMO_OPT_TAIL_PRIORITY:
+            if (iv != o.tail_priority) {
+                const lumo_status e = make_tail_stream(c, iv);
+                if (e) return e;
+            }
+            o.tail_priority = iv;
+            break;
         default: return LUMO_ERR_INVALID;
     }
     return LUMO_OK;
@@ -2040,6 +2099,7 @@ int64_t get_opt(const Ctx& c, int k) {
         case LUMO_OPT_STACK_CLASS: return o.stack_class;
         case LUMO_OPT_FULL_KERNELS: return o.full_kernels;
         case LUMO_OPT_POISON: return o.poison;
+        case LUMO_OPT_TAIL_PRIORITY: return o.tail_priority;
         default: return 0;
     }
 }
@@ -2091,7 +2151,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
         delete c;
         return LUMO_ERR_HIP;
     }
-    if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+    if (make_tail_stream(*c, c->o.tail_priority) != LUMO_OK ||
         hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);

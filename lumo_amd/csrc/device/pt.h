@@ -718,6 +718,12 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
         double* rb_lds = reinterpret_cast<double*>(lds_scene + (LDS ? (sc0.hot_bytes + 15u) / 16u * 16u : 0u));
         const uint32_t nt = blockDim.x;
         uint32_t base = blockIdx.x * blockDim.x;
+#if LUMO_PHASE_CLOCKS
+        uint64_t ph[5] = {0, 0, 0, 0, 0}, tc0 = clock64(), tc1 = 0;
+#define LUMO_PHASE(k) (tc1 = clock64(), ph[k] += tc1 - tc0, tc0 = tc1)
+#else
+#define LUMO_PHASE(k) ((void)0)
+#endif
         if (dyn) {
             if (threadIdx.x == 0) next_base = atomicAdd(S.counts + CNT_FETCH_B, (uint32_t)blockDim.x);
             __syncthreads();
@@ -726,9 +732,11 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
         while (base < count) {
             const uint32_t q = base + threadIdx.x;
             const bool live = q < count;
+            LUMO_PHASE(3);
             // phase 1: Scene::hit (k_closest_q)
             HitRef hr{DINF, 0, -1, -1};
             if (live) hr = scene_hit<STK, FX>(sc, rayx(Ray{qv3(cur, QD_O, q), qv3(cur, QD_D, q)}), Cc);
+            LUMO_PHASE(0);
             // phase 2: the bounce of k_shade_q (NS1) with the pair's records kept in registers
             PathReg P{};
             bool resolve = false, alive = false, ok = false;
@@ -799,6 +807,7 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                     }
                 }
             }
+            LUMO_PHASE(1);
             const uint32_t np = block_slot(alive, S.counts + CNT_NEXT);
             if (alive) {
                 qv3(nxt, QD_O, np, rn.o);
@@ -819,6 +828,7 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                 S.queries[P.slot] = P.queries;
                 stc(S.rad, P.slot, P.rad);
             }
+            LUMO_PHASE(4);
             // phase 3: the pair's visibility + MIS (k_shadow_q, NS1)
             if (resolve) {
 #if LUMO_PARK_NEE
@@ -854,6 +864,7 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                 else  // the radiance stored above, re-read by the thread that wrote it
                     stc(S.rad, P.slot, ldc(S.rad, P.slot) + X);
             }
+            LUMO_PHASE(2);
             if (dyn) {
                 __syncthreads();  // every thread has read next_base
                 if (threadIdx.x == 0) next_base = atomicAdd(S.counts + CNT_FETCH_B, (uint32_t)blockDim.x);
@@ -863,7 +874,14 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                 base += gridDim.x * blockDim.x;
             }
         }
+#if LUMO_PHASE_CLOCKS
+        // per wave (lane 0): cycles in the closest hit, shading, fetch, visibility and compaction
+        // phases (wave-uniform spans: every lane passes the same marks)
+        if (lane_id() == 0)
+            for (int k = 0; k < 5; ++k) atomicAdd(S.tcount + TC_ALL + k, (unsigned long long)ph[k]);
+#endif
     }
+#undef LUMO_PHASE
     flush_counters(Cc, S.tcount);
     flush_counters(Cs, S.tcount + TC_N);
     if (LUMO_SKIP_DEAD) flush_resolved(Cs.resolved, S.tcount + TC_RESOLVED);

@@ -69,7 +69,11 @@ constexpr int TC_ALL = 2 * TC_N + 3;
 #ifndef LUMO_SHADOW_STATS
 #define LUMO_SHADOW_STATS 0
 #endif
-constexpr int TC_STATS = LUMO_SHADOW_STATS ? 218 : 0;  // diagnostics build: k_shadow_q cost classes
+#ifndef LUMO_PHASE_CLOCKS  // diagnostics build: wave cycles per phase of the fused bounce kernel
+#define LUMO_PHASE_CLOCKS 0
+#endif
+// diagnostics builds: k_shadow_q cost classes, or k_bounce_q phase clocks
+constexpr int TC_STATS = LUMO_SHADOW_STATS ? 218 : (LUMO_PHASE_CLOCKS ? 8 : 0);
 
 struct DCam {
     Xform wtc, sctr, cts;
