@@ -238,6 +238,7 @@ __global__ void k_bounce_begin(uint32_t* counts, unsigned long long* headq) {
         counts[CNT_FETCH_C] = 0;
         counts[CNT_FETCH_T] = 0;
         for (int b = 0; b < NB; ++b) counts[CNT_BUCKET0 + b] = 0;
+        counts[CNT_SHQ] = 0;
     }
 }
 
@@ -829,8 +830,9 @@ enum WorkId {
     W_QS2_R, W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I, W_RAD3, W_LAM3, W_RASTER3, W_DEPTH3, W_QUERIES3, W_P_VALID3,
     W_COUNTS3, W_QS4_D, W_QS4_R, W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I, W_RAD4, W_LAM4, W_RASTER4, W_DEPTH4,
     W_QUERIES4, W_P_VALID4, W_COUNTS4, W_QS6_D, W_QS6_R, W_QS6_I, W_QS7_D, W_QS7_R, W_QS7_I,
-    W_SPLIT_SET1,  // render_split_pipelined sets 1..3: hits + NEE records, 7 buffers each
-    W_COUNT = W_SPLIT_SET1 + 3 * 7
+    W_SQ_QL,
+    W_SPLIT_SET1,  // render_split_pipelined sets 1..3: hits + NEE records, 8 buffers each
+    W_COUNT = W_SPLIT_SET1 + 3 * 8
 };
 
 template <typename T>
@@ -971,7 +973,7 @@ void alloc_pass_set(Ctx& c, Paths& Q, int k, int N, lumo_status& st) {
 }
 // ... and, for the split schedule, the set's closest hits and NEE records (the sizes of set 0's)
 void alloc_split_set(Ctx& c, Paths& Q, const Paths& S, int k, int ns, lumo_status& st) {
-    const int w = W_SPLIT_SET1 + 7 * (k - 1);
+    const int w = W_SPLIT_SET1 + 8 * (k - 1);
     Q.hq.t = wbuf<double>(c, w + 0, S.hq.cap, st);
     Q.hq.i = wbuf<int32_t>(c, w + 1, 3 * S.hq.cap, st);
     Q.sq.d = wbuf<double>(c, w + 2, SD_N * S.sq.cap, st);
@@ -979,12 +981,13 @@ void alloc_split_set(Ctx& c, Paths& Q, const Paths& S, int k, int ns, lumo_statu
     Q.sq.hd = wbuf<double>(c, w + 4, (ns > 1 ? SH_N : SH_N1) * S.sq.hcap, st);
     Q.sq.hi = wbuf<int32_t>(c, w + 5, SHI_N * S.sq.hcap, st);
     Q.sq.hr = ns > 1 ? wbuf<uint64_t>(c, w + 6, 2 * S.sq.hcap, st) : nullptr;
+    Q.sq.ql = ns > 1 ? wbuf<int32_t>(c, w + 7, 2 * S.sq.cap, st) : nullptr;
 }
 // Device bytes of one extra pass set of the split schedule.
 size_t split_set_bytes(const Paths& S, int N, int ns) {
     return (size_t)N * (4 + 4 + 2) * 8 + (size_t)N * 3 * 4 + 2 * (size_t)N * (QD_N * 8 + 16 + QI_N * 4) +
            S.hq.cap * (8 + 12) + S.sq.cap * (SD_N * 8 + SI_N * 4) +
-           S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4 + (ns > 1 ? 16 : 0));
+           S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4 + (ns > 1 ? 16 : 0)) + (ns > 1 ? S.sq.cap * 8 : 0);
 }
 
 
@@ -1196,8 +1199,9 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
     }
     {
         StageTimer tm(c, c.o.timing, ST_SHADOW, sm);
+        // n_shadow > 1: one thread per visibility query (the records that need a walk, k_nee_gen)
         launch_trav(
-            c, (uint64_t)ub * (uint32_t)ns,
+            c, (uint64_t)ub * (uint32_t)ns * (ns > 1 ? 2u : 1u),
             [&](auto K, const TravLaunch& l) { launch_shadow_q<decltype(K)::value>(l, c.sc, S, nxt); }, sm,
             true);
     }
@@ -1525,6 +1529,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         S.sq.hd = wbuf<double>(c, W_SQ_HD, (ns > 1 ? SH_N : SH_N1) * S.sq.hcap, st);
         S.sq.hi = wbuf<int32_t>(c, W_SQ_HI, SHI_N * S.sq.hcap, st);
         S.sq.hr = ns > 1 ? wbuf<uint64_t>(c, W_SQ_HR, 2 * S.sq.hcap, st) : nullptr;
+        S.sq.ql = ns > 1 ? wbuf<int32_t>(c, W_SQ_QL, 2 * S.sq.cap, st) : nullptr;
     }
     S.p_rgb = wbuf<double>(c, W_P_RGB, 3 * (size_t)N, st);
     S.p_valid = wbuf<uint32_t>(c, W_P_VALID, NV, st);

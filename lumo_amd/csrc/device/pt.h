@@ -312,23 +312,42 @@ __device__ __forceinline__ void deliver_nee(const Paths& S, const ShadowQ& Q, co
     }
 }
 
-// Thread per pair r = p * n_shadow + i (path p, light sample i): single_i = (light-sampled +
-// BSDF-sampled) / pdf_light (integrator.rs:87-137).  NS1 (n_shadow = 1): the thread also folds
-// the path's NEE term; otherwise it stores single_i over the pair's (consumed) L-record bsdf_f
-// planes and k_nee_fold adds the path's singles in i order.  No block barrier: a wave that
-// finishes its traversals early moves on to its next pairs.
+// NS1 (n_shadow = 1): thread per pair r (path p = r): single = (light-sampled + BSDF-sampled) /
+// pdf_light (integrator.rs:87-137), folded into the path's NEE term at once.  Otherwise thread per
+// visibility query: the records that need a walk (k_nee_gen's list: records whose BSDF pdf is 0
+// contribute 0 whatever the visibility, integrator.rs:146, and invalid B records none), each
+// query's MIS term stored over its (consumed) record's bsdf_f planes; k_nee_fold forms single_i =
+// (0 + L + B) / pdf_light and adds the path's singles in i order.  The L and B records of a pair and
+// the pairs of a path run on different lanes, and no lane idles on a record without a walk.  No
+// block barrier: a wave that finishes its traversals early moves on to its next queries.
 template <int STK, int LDS, int FX, bool NS1>
 __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) void k_shadow_q(DScene sc0, Paths S,
                                                                                               QState nxt) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const int ns = NS1 ? 1 : sc0.n_shadow;
-    uint32_t count = 0;  // pairs over all buckets
-    for (int b = 0; b < NB; ++b) count += S.counts[CNT_BUCKET0 + b];
-    count *= (uint32_t)ns;
+    uint32_t count = 0;  // NS1: pairs over all buckets; else the queries
+    if (NS1) {
+        for (int b = 0; b < NB; ++b) count += S.counts[CNT_BUCKET0 + b];
+    } else {
+        count = S.counts[CNT_SHQ];
+    }
     if (count <= blockIdx.x * blockDim.x) return;
     const DScene sc = LDS == 1 ? stage_scene_lds(sc0, lds_scene) : (LDS == 2 ? stage_top_lds(sc0, lds_scene) : sc0);
     const ShadowQ Q = S.sq;
     Counters C{0, 0, 0};
+    if constexpr (!NS1) {
+        // static stride (one fetch atomic per wave on one counter cost more than the balance gained)
+        for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
+            const int32_t qv = Q.ql[j];
+            const size_t r = (size_t)(qv >> 1);
+            const int which = qv & 1;  // 0: light-sampled record, 1: BSDF-sampled
+            const int b = which ? SD_BO : SD_LO;
+            const DColor x = shadow_record_q<STK, FX, LDS == 2>(sc, Q, b, r, which == 0, (uint32_t)(r / (size_t)ns), C);
+            for (int k = 0; k < NS; ++k) Q.D(b + 6 + k, r) = x.s[k];
+        }
+        flush_counters(C, S.tcount + TC_N);
+        return;
+    }
     // static stride: with 11 pairs per path, one fetch atomic per wave (~350 k per C3 bounce on one
     // counter) cost more than the balance gained (C3 shadow 560 -> 639 ms per 8-spp frame)
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
@@ -381,12 +400,8 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) vo
         const DColor b = Q.I(SI_BVALID, r) ? shadow_record_q<STK, FX, LDS == 2>(sc, Q, SD_BO, r, false, p, C) : cfill(0.0);
 #endif
         const DColor single = (cfill(0.0) + a + b) / Q.D(SD_PDFL, r);
-        if (NS1) {
-            const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};
-            deliver_nee(S, Q, nxt, p, (cfill(0.0) + g * single) / 1.0);
-        } else {
-            for (int k = 0; k < NS; ++k) Q.D(SD_LF + k, r) = single.s[k];
-        }
+        const DColor g{{Q.HD(SH_G, p), Q.HD(SH_G + 1, p), Q.HD(SH_G + 2, p), Q.HD(SH_G + 3, p)}};
+        deliver_nee(S, Q, nxt, p, (cfill(0.0) + g * single) / 1.0);
     }
     flush_counters(C, S.tcount + TC_N);
     if (LUMO_SKIP_DEAD) flush_resolved(C.resolved, S.tcount + TC_RESOLVED);
@@ -395,6 +410,9 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) vo
 // n_shadow > 1: the NEE pairs of this bounce, one thread per pair (path p, light sample i), from the
 // header k_shade_q wrote; the path's RNG is stepped past the draws of pairs 0..i-1 (6 each), so
 // every pair draws exactly what the path's loop over i would have drawn.
+// The pair's records that need a walk go to the bounce's visibility query list (k_shadow_q): the
+// L record unless its BSDF pdf is 0, the B record when it exists and its pdf is not 0 (those
+// contribute 0 whatever the visibility, integrator.rs:146: k_nee_fold adds 0 for them).
 template <int FX>
 __global__ __launch_bounds__(BLOCK, LUMO_NEE_WAVES) void k_nee_gen(DScene sc, Paths S) {
     const int ns = sc.n_shadow;
@@ -404,11 +422,17 @@ __global__ __launch_bounds__(BLOCK, LUMO_NEE_WAVES) void k_nee_gen(DScene sc, Pa
         count += bc[b];
     }
     const ShadowQ sq = S.sq;
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
+    uint32_t dead = 0;
+    // whole blocks per round: the query-list append needs every thread of the block
+    for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < count; j0 += gridDim.x * blockDim.x) {
+        const uint32_t j = j0 + threadIdx.x;
+        size_t r = 0;
+        bool live_l = false, live_b = false;
+        if (j < count) {
         uint32_t lj = j;
         int bk = 0;
         while (lj >= bc[bk]) lj -= bc[bk++];
-        const size_t r = (size_t)bk * sq.seg * ns + lj;
+        r = (size_t)bk * sq.seg * ns + lj;
         const uint32_t p = (uint32_t)(r / (size_t)ns);
         const int i = (int)(r - (size_t)p * ns);
         DHit ho;
@@ -426,8 +450,17 @@ __global__ __launch_bounds__(BLOCK, LUMO_NEE_WAVES) void k_nee_gen(DScene sc, Pa
         Xorshift rng{sq.HR(0, p), sq.HR(1, p)};
         for (int k = 0; k < NEE_DRAWS * i; ++k) xs_step(rng);
         const lumo_material m = sc.mats[ho.material];
-        nee_pair<FX>(sc, sq, r, ho, m, wo, L, rng);
+        const bool ok = nee_pair<FX>(sc, sq, r, ho, m, wo, L, rng);
+        live_l = !LUMO_SKIP_DEAD || sq.D(SD_LPS, r) != 0.0;
+        live_b = ok && (!LUMO_SKIP_DEAD || sq.D(SD_BPS, r) != 0.0);
+        dead += (live_l ? 0u : 1u) + (ok && !live_b ? 1u : 0u);
+        }
+        const int n = (live_l ? 1 : 0) + (live_b ? 1 : 0);
+        const uint32_t pos = block_slot2(n, S.counts + CNT_SHQ);
+        if (live_l) sq.ql[pos] = (int32_t)(2 * r);
+        if (live_b) sq.ql[pos + (live_l ? 1u : 0u)] = (int32_t)(2 * r + 1);
     }
+    if (LUMO_SKIP_DEAD) flush_resolved(dead, S.tcount + TC_RESOLVED);
 }
 
 #ifdef LUMO_MAIN_TU
@@ -451,9 +484,18 @@ __global__ __launch_bounds__(BLOCK) void k_nee_fold(Paths S, QState nxt, int ns)
         int32_t nb = 0;
         for (int i = 0; i < ns; ++i) {
             const size_t r = (size_t)p * ns + i;
-            const DColor single{{Q.D(SD_LF, r), Q.D(SD_LF + 1, r), Q.D(SD_LF + 2, r), Q.D(SD_LF + 3, r)}};
+            // the records' MIS terms (k_shadow_q wrote them over their bsdf_f planes), 0 for those
+            // without a walk; single_i = (0 + L + B) / pdf_light (integrator.rs:87-137)
+            const bool bv = Q.I(SI_BVALID, r) != 0;
+            const bool live_l = !LUMO_SKIP_DEAD || Q.D(SD_LPS, r) != 0.0;
+            const bool live_b = bv && (!LUMO_SKIP_DEAD || Q.D(SD_BPS, r) != 0.0);
+            const DColor a = live_l ? DColor{{Q.D(SD_LF, r), Q.D(SD_LF + 1, r), Q.D(SD_LF + 2, r), Q.D(SD_LF + 3, r)}}
+                                    : cfill(0.0);
+            const DColor b = live_b ? DColor{{Q.D(SD_BF, r), Q.D(SD_BF + 1, r), Q.D(SD_BF + 2, r), Q.D(SD_BF + 3, r)}}
+                                    : cfill(0.0);
+            const DColor single = (cfill(0.0) + a + b) / Q.D(SD_PDFL, r);
             acc = acc + g * single;
-            nb += Q.I(SI_BVALID, r);
+            nb += bv ? 1 : 0;
         }
         deliver_nee(S, Q, nxt, p, acc / (double)ns);
         const int next = Q.HI(SHI_NEXT, p);
@@ -712,7 +754,7 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
         // Whole blocks of the queue; block_slot needs every thread of the block each round.  With
         // `dyn`, a persistent block takes its next 256 paths from a counter (CNT_FETCH_B, zeroed by
         // k_bounce_begin) instead of a fixed grid stride, so CUs whose paths ran long take fewer.
-        __shared__ uint32_t next_base;
+        __shared__ uint32_t first_base;
         // the B record waits here (not in VGPRs) for phase 3: 12 planes of blockDim.x doubles in the
         // dynamic LDS after the staged scene
         double* rb_lds = reinterpret_cast<double*>(lds_scene + (LDS ? (sc0.hot_bytes + 15u) / 16u * 16u : 0u));
@@ -725,9 +767,9 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
 #define LUMO_PHASE(k) ((void)0)
 #endif
         if (dyn) {
-            if (threadIdx.x == 0) next_base = atomicAdd(S.counts + CNT_FETCH_B, (uint32_t)blockDim.x);
+            if (threadIdx.x == 0) first_base = atomicAdd(S.counts + CNT_FETCH_B, (uint32_t)blockDim.x);
             __syncthreads();
-            base = next_base;
+            base = first_base;
         }
         while (base < count) {
             const uint32_t q = base + threadIdx.x;
@@ -808,7 +850,12 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                 }
             }
             LUMO_PHASE(1);
-            const uint32_t np = block_slot(alive, S.counts + CNT_NEXT);
+            // the next queue's positions; with `dyn` the block's next 256 paths are claimed in the
+            // same step (no barrier of its own: the waves go on to their next closest hits without
+            // waiting for the block's slowest visibility phase)
+            uint32_t next_base = 0;
+            const uint32_t np = dyn ? block_slot_fetch(alive, S.counts + CNT_NEXT, S.counts + CNT_FETCH_B, &next_base)
+                                    : block_slot(alive, S.counts + CNT_NEXT);
             if (alive) {
                 qv3(nxt, QD_O, np, rn.o);
                 qv3(nxt, QD_D, np, rn.d);
@@ -865,14 +912,7 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                     stc(S.rad, P.slot, ldc(S.rad, P.slot) + X);
             }
             LUMO_PHASE(2);
-            if (dyn) {
-                __syncthreads();  // every thread has read next_base
-                if (threadIdx.x == 0) next_base = atomicAdd(S.counts + CNT_FETCH_B, (uint32_t)blockDim.x);
-                __syncthreads();
-                base = next_base;
-            } else {
-                base += gridDim.x * blockDim.x;
-            }
+            base = dyn ? next_base : base + gridDim.x * blockDim.x;
         }
 #if LUMO_PHASE_CLOCKS
         // per wave (lane 0): cycles in the closest hit, shading, fetch, visibility and compaction

@@ -55,7 +55,8 @@ static_assert(ST_COUNT == LUMO_STAGE_COUNT, "stage slots match lumo_stats");
 // waits for a count before launching the next stage.
 // CNT_FETCH_*: work counters from which the kernels' waves / blocks take their next paths
 // (dynamic load balance; k_bounce_begin zeroes them every bounce).
-enum { CNT_NEXT = 0, CNT_FETCH_B, CNT_FETCH_C, CNT_FETCH_T, CNT_CUR, CNT_BUCKET0, CNT_N = CNT_BUCKET0 + 8 };
+// CNT_SHQ: visibility queries of the bounce (n_shadow > 1: the NEE records that need a walk).
+enum { CNT_NEXT = 0, CNT_FETCH_B, CNT_FETCH_C, CNT_FETCH_T, CNT_CUR, CNT_BUCKET0, CNT_SHQ = CNT_BUCKET0 + 8, CNT_N };
 // k_shade_q files each path's NEE records into one of NB buckets by the shadow rays' origin
 // object (objects, then lights, mod NB), each bucket a contiguous segment of the record queue, so
 // that a wave's visibility queries start on the same surface and walk the same BVH / kd nodes.
@@ -124,6 +125,7 @@ struct ShadowQ {
     double* hd;    // SH_* planes, hcap paths
     int32_t* hi;   // SHI_* planes
     uint64_t* hr;  // path RNG at the start of its NEE draws (hi, lo), n_shadow > 1
+    int32_t* ql;   // n_shadow > 1: the bounce's visibility queries, 2 * pair + (0: L record, 1: B record)
     size_t hcap;
     uint32_t seg;  // paths per bucket segment
     __device__ __forceinline__ double& D(int k, size_t r) const { return d[(size_t)k * cap + r]; }
@@ -193,6 +195,56 @@ __device__ __forceinline__ uint32_t block_slot(bool pred, uint32_t* counter) {
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t prefix = mbcnt64(mask);
     if (lane == 0) wtot[w] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+            const uint32_t cnt = wtot[i];
+            wtot[i] = t;
+            t += cnt;
+        }
+        base_s = t ? atomicAdd(counter, t) : 0u;
+    }
+    __syncthreads();
+    const uint32_t pos = base_s + wtot[w] + prefix;
+    __syncthreads();
+    return pos;
+}
+// block_slot that also takes the block's next batch of work: thread 0 adds blockDim.x to `fetch` in
+// the same serial section (no extra barrier) and every thread gets the batch base in *next.
+__device__ __forceinline__ uint32_t block_slot_fetch(bool pred, uint32_t* counter, uint32_t* fetch, uint32_t* next) {
+    __shared__ uint32_t wtot[BLOCK / 64];
+    __shared__ uint32_t base_s, next_s;
+    const uint64_t mask = __ballot(pred);
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t prefix = mbcnt64(mask);
+    if (lane == 0) wtot[w] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+            const uint32_t cnt = wtot[i];
+            wtot[i] = t;
+            t += cnt;
+        }
+        base_s = t ? atomicAdd(counter, t) : 0u;
+        next_s = atomicAdd(fetch, (uint32_t)blockDim.x);
+    }
+    __syncthreads();
+    const uint32_t pos = base_s + wtot[w] + prefix;
+    *next = next_s;
+    __syncthreads();
+    return pos;
+}
+// block_slot for up to two entries per thread (n = 0, 1 or 2): this thread's first position, its
+// entries at pos and pos + 1, in lane order.  Every thread of the block must call it.
+__device__ __forceinline__ uint32_t block_slot2(int n, uint32_t* counter) {
+    __shared__ uint32_t wtot[BLOCK / 64];
+    __shared__ uint32_t base_s;
+    const uint64_t m1 = __ballot(n >= 1), m2 = __ballot(n >= 2);
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t prefix = mbcnt64(m1) + mbcnt64(m2);
+    if (lane == 0) wtot[w] = (uint32_t)(__popcll(m1) + __popcll(m2));
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t t = 0;

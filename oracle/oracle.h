@@ -67,6 +67,9 @@ int oracle_trace_paths(const lumo_scene_desc* scene, const lumo_camera_desc* cam
 int oracle_debug_trace(const lumo_scene_desc* scene, const lumo_camera_desc* camera,
                        const lumo_tile_task* task, int pass, int pixel, double* out, int* n_out);
 
+/* Diagnostics: each ray's traversal counters (AABB, kd nodes, triangles) in cost3[3 i ..]. */
+int oracle_trace_costs(const lumo_scene_desc* scene, const lumo_ray_soa* rays, size_t n, int any_hit,
+                       uint32_t* cost3);
 /* Scene::hit (any_hit = 0) or Scene::hit_light (any_hit != 0) for a batch of rays. */
 int oracle_trace(const lumo_scene_desc* scene, const lumo_ray_soa* rays, size_t n,
                  lumo_hit_soa* hits, int any_hit, oracle_counters* counters);

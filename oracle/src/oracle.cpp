@@ -2322,6 +2322,30 @@ extern "C" int oracle_trace(const lumo_scene_desc* scene, const lumo_ray_soa* ra
     return LUMO_OK;
 }
 
+// Diagnostics (tools/): oracle_trace with each ray's traversal counters (AABB tests, kd nodes,
+// triangle tests) in cost3[3 * i .. 3 * i + 2], for lane-divergence studies of query orderings.
+extern "C" int oracle_trace_costs(const lumo_scene_desc* scene, const lumo_ray_soa* rays, size_t n, int any_hit,
+                                  uint32_t* cost3) {
+    if (!scene || !rays || !cost3) return LUMO_ERR_INVALID;
+    const Scene sc{scene};
+    for (size_t i = 0; i < n; ++i) {
+        Counters C;
+        const Ray r{V3{rays->origin[3 * i], rays->origin[3 * i + 1], rays->origin[3 * i + 2]},
+                    V3{rays->dir[3 * i], rays->dir[3 * i + 1], rays->dir[3 * i + 2]}};
+        Hit h;
+        if (!any_hit) {
+            int kind = 0, which = -1;
+            scene_hit(sc, r, &h, &kind, &which, C);
+        } else {
+            scene_hit_light(sc, r, rays->light[i], &h, C);
+        }
+        cost3[3 * i] = (uint32_t)C.aabb;
+        cost3[3 * i + 1] = (uint32_t)C.kd;
+        cost3[3 * i + 2] = (uint32_t)C.tri;
+    }
+    return LUMO_OK;
+}
+
 extern "C" int oracle_debug_trace(const lumo_scene_desc* scene, const lumo_camera_desc* camera,
                                   const lumo_tile_task* task, int pass, int pixel, double* out, int* n_out) {
     if (!scene || !camera || !task || !valid_task(*task)) return LUMO_ERR_INVALID;
