@@ -43,6 +43,7 @@ B_CLOSEST_IO = 48 + 20  # ray in + hit out
 B_RECORD, B_FOLD = 104, 104  # shadow record in; per path: gathered + pdf_light + radiance read/write
 B_CONN_IO = 104  # BDPT connection query: the two vertices' position / error / normal in, result out
 LUMO_DEFAULT_THREADS = 4  # renderer.rs:21
+CPU_REPEATS = 3  # CPU baseline: median of this many runs per thread count
 # f64 VALU peak in lane-operations per second (an FMA counts once): 256 CUs x 4 SIMDs x 16 f64
 # lanes per cycle x 2.4 GHz = 78.6 TFLOP/s / 2 (MI355X FP64 vector rate).  The VALU bound prices
 # every VALU lane-operation at this rate (integer / f32 ops issue at twice it, so the fraction is
@@ -77,7 +78,7 @@ def main():
     ap.add_argument("--max-paths", type=int, default=1 << 23, help="paths in flight per wavefront")
     ap.add_argument("--max-vertices", type=int, default=0, help="BDPT vertex storage per subpath (0 = 128)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU work per baseline run")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="target CPU work per baseline run (x3 repeats)")
     ap.add_argument("--share", default=None,
                     help="R/N: render only rank R's share of an N-rank run (tile %% N == R) in this single "
                          "process, to time one rank's load of a multi-GPU run on one GPU")
@@ -450,19 +451,25 @@ def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl):
         stride = max(1, int(round(base_stride * 16 / threads * 8.0 / args.cpu_seconds))) | 1  # odd: all columns
         sample = [t for i, t in enumerate(tasks)
                   if (i % tiles) % stride == 0 and (batches is None or i // tiles < batches)]
-        t0 = time.perf_counter()
-        bufs, res, cnt = O.render_tasks(scene.desc(), cam.desc, sample, O.LUMO_ORDER, threads,
-                                        integrator=integrator, splats_out=[] if integrator else None)
-        dt = time.perf_counter() - t0
+        times = []
+        for _ in range(CPU_REPEATS):  # the host is shared: the median of repeated runs, with their spread
+            t0 = time.perf_counter()
+            bufs, res, cnt = O.render_tasks(scene.desc(), cam.desc, sample, O.LUMO_ORDER, threads,
+                                            integrator=integrator, splats_out=[] if integrator else None)
+            times.append(time.perf_counter() - t0)
+        dt = sorted(times)[len(times) // 2]
         q = sum(r.num_queries for r in res)
         paths = sum(r.num_camera_rays for r in res)
         runs.append({"threads": threads, "value": round(q / dt / 1e6, 4), "msamples_per_s": round(paths / dt / 1e6, 4),
-                     "seconds": round(dt, 2),
+                     "seconds": round(dt, 2), "repeats": len(times),
+                     "value_min": round(q / max(times) / 1e6, 4), "value_max": round(q / min(times) / 1e6, 4),
                      "sample": f"{len(sample)} tasks = every {stride}th 16x16 tile of "
                                f"{'each' if batches is None else f'the first {batches}'} 256-spp batch(es) of "
                                f"the {W}x{H} @ {spp} spp frame ({paths} paths), lumo tile-serial RNG order"})
     best = runs[0]
     return {"value": best["value"], "unit": "Mrays/s", "cores": best["threads"], "kind": "port",
+            "statistic": f"median of {CPU_REPEATS} runs", "value_min": best["value_min"],
+            "value_max": best["value_max"],
             "msamples_per_s": best["msamples_per_s"], "seconds": best["seconds"], "sample": best["sample"],
             "cpu_model": info["model"], "host": info, "runs": runs}
 

@@ -405,6 +405,8 @@ enum {
     LUMO_OPT_TAIL_PRIORITY,    /* fused pipeline: the stream of the passes' tails, films and rings (the
                                   chain each pass's Russian roulette waits on) at high priority: 0 / 1
                                   (LUMO_TAIL_PRIORITY, 0)                                           */
+    LUMO_OPT_TOP_KD,           /* upload: the TOP set's spare LDS holds the top treelets of the
+                                  largest kd tree: 0 / 1 (LUMO_TOP_KD, 1)                           */
     LUMO_OPT_COUNT
 };
 lumo_status lumo_set_option(void* ctx, int32_t option, int64_t value);
@@ -445,7 +447,8 @@ lumo_status lumo_debug_trace(void* ctx, const lumo_tile_task* task, int pass, in
  * the objects / lights BVH, the object items and the objects' traversal records. */
 typedef struct {
     int32_t stack_class, lds_bytes, full_kernels, n_shadow;
-    int32_t top_bytes, top_object_nodes, top_light_nodes, pad0;
+    int32_t top_bytes, top_object_nodes, top_light_nodes;
+    int32_t top_kd_nodes; /* kd nodes of the largest kd tree (its top treelets) in the TOP set */
 } lumo_scene_info_t;
 lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info);
 /* Diagnostics: one coalesced 8-B-per-lane read stream and one write stream over n doubles

@@ -145,7 +145,7 @@ class HitSoA(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("stack_class", C.c_int32), ("lds_bytes", C.c_int32), ("full_kernels", C.c_int32),
                 ("n_shadow", C.c_int32), ("top_bytes", C.c_int32), ("top_object_nodes", C.c_int32),
-                ("top_light_nodes", C.c_int32), ("pad0", C.c_int32)]
+                ("top_light_nodes", C.c_int32), ("top_kd_nodes", C.c_int32)]
 
 
 STAGE_COUNT = 12  # LUMO_STAGE_COUNT
@@ -171,7 +171,7 @@ SCHED_SEQUENTIAL, SCHED_FUSED_PIPELINE, SCHED_SPLIT_PIPELINE = range(3)
 # LUMO_OPT_* (include/lumo_amd.h), by the name Device.set_option takes
 OPTIONS = ["timing", "lds_staging", "top_staging", "fused", "tail_below", "pipeline", "heads", "merge_passes",
            "dyn_fetch", "bounce_threads", "split_pipe", "split_groups", "bdpt_tail", "bounce_ahead", "lds_grid",
-           "top_grid", "top_kb", "kd_lds", "stack_class", "full_kernels", "poison", "tail_priority"]
+           "top_grid", "top_kb", "kd_lds", "stack_class", "full_kernels", "poison", "tail_priority", "top_kd"]
 OPT = {name: i for i, name in enumerate(OPTIONS)}
 
 

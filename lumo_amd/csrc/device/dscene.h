@@ -125,6 +125,11 @@ struct DScene {
     double* kst_ts;
     int32_t kst_cfg;  // entries per thread the TOP kernels keep in LDS (kst_n of their view; 0 in HBM views)
     uint32_t top_shm;  // dynamic LDS of a TOP block: the TOP set + the kd stack columns
+    // kd nodes in the TOP set: kdp[top_kd_lo .. top_kd_lo + top_kd_n), the first treelets (the top
+    // levels) of the largest kd tree, at off_top_kd; in a TOP view read from kd_lds
+    uint32_t off_top_kd;
+    int32_t top_kd_lo, top_kd_n;
+    const DKd* kd_lds;
 };
 
 // TOP view: copy the packed top levels into LDS; the rest of the scene stays in HBM / L2.
@@ -140,6 +145,7 @@ __device__ __forceinline__ DScene stage_top_lds(const DScene& sc, char* lds) {
     v.n_lnodes_lds = sc.top_lnodes;
     v.oitems = reinterpret_cast<const int32_t*>(lds + sc.off_top_oitems);
     v.tobjs = reinterpret_cast<const DObj*>(lds + sc.off_top_tobjs);
+    v.kd_lds = reinterpret_cast<const DKd*>(lds + sc.off_top_kd);
     v.kst_n = sc.kst_cfg;
     if (sc.kst_cfg > 0) {  // this thread's column of the LDS kd stack, after the TOP set
         char* base = lds + ((sc.top_bytes + 15u) & ~15u);
@@ -577,6 +583,16 @@ __device__ __forceinline__ double kst_t(const DScene& sc, const double* st_ts, i
     return (KL && k < sc.kst_n) ? sc.kst_ts[k * sc.kst_stride] : st_ts[k];
 }
 
+// kd node i: from the TOP set in LDS when KL (TOP kernels) and i is in its staged range.
+template <bool KL>
+__device__ __forceinline__ DKd kd_at(const DScene& sc, int i) {
+    if (KL) {
+        const uint32_t k = (uint32_t)(i - sc.top_kd_lo);
+        if (k < (uint32_t)sc.top_kd_n) return sc.kd_lds[k];
+    }
+    return sc.kdp[i];
+}
+
 template <bool GEO, int STK, bool KL = false>
 __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const RayX& r, double t_min, double t_max,
                               int* idx_out, Counters& C) {
@@ -595,7 +611,7 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const 
     const double t_end0 = t_end;
     for (;;) {
         if (t_hit < t_start) break;
-        DKd node = sc.kdp[curr];
+        DKd node = kd_at<KL>(sc, curr);
 #if LUMO_WHILE_WHILE
         // while-while (Aila & Laine 2009): descend interior nodes until this lane is at a leaf
         // before any lane tests triangles, so the leaves of a wave's lanes are processed together.
@@ -620,7 +636,7 @@ __device__ KD_INLINE double kd_traverse(const DScene& sc, const DObj& ob, const 
                 t_end = t_split;
                 sp++;
             }
-            node = sc.kdp[curr];
+            node = kd_at<KL>(sc, curr);
         }
 #endif
         const int axis = node.meta & 3;

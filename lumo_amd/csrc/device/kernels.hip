@@ -735,6 +735,7 @@ struct Opts {
     int full_kernels = 0;              // general feature kernels for lean scenes too
     int poison = 0;                    // new device buffers filled with 0xFF (reads before writes show as NaN / -1)
     int tail_priority = 0;             // the pipelined passes' tail / film / ring stream at high priority
+    int top_kd = 1;                    // the TOP set's spare LDS holds the top treelets of the largest kd tree
 };
 
 struct Ctx {
@@ -1994,7 +1995,7 @@ const char* const kOptEnv[LUMO_OPT_COUNT] = {
     "LUMO_TIMING", "LUMO_LDS", "LUMO_TOP", "LUMO_FUSED", "LUMO_TAIL", "LUMO_PIPELINE", "LUMO_HEADS", "LUMO_MERGE",
     "LUMO_DYN", "LUMO_BOUNCE_THREADS", "LUMO_SPLIT_PIPE", "LUMO_SPLIT_GROUPS", "LUMO_BDPT_TAIL", "LUMO_BOUNCE_AHEAD",
     "LUMO_LDS_GRID", "LUMO_TOP_GRID", "LUMO_TOP_KB", "LUMO_KD_LDS", "LUMO_STACK_CLASS", "LUMO_FULL_KERNELS",
-    "LUMO_POISON", "LUMO_TAIL_PRIORITY"};
+    "LUMO_POISON", "LUMO_TAIL_PRIORITY", "LUMO_TOP_KD"};
 
 void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
     lo = 0;
@@ -2068,6 +2069,7 @@ lumo_status set_opt(Ctx& c, int k, int64_t v) {
         case LUMO_OPT_STACK_CLASS: o.stack_class = iv; break;
         case LUMO_OPT_FULL_KERNELS: o.full_kernels = iv; break;
         case LUMO_OPT_POISON: o.poison = iv; break;
+        case LUMO_OPT_TOP_KD: o.top_kd = iv; break;
         case LUMO_OPT_TAIL_PRIORITY:
             if (iv != o.tail_priority) {
                 const lumo_status e = make_tail_stream(c, iv);
@@ -2105,6 +2107,7 @@ int64_t get_opt(const Ctx& c, int k) {
         case LUMO_OPT_FULL_KERNELS: return o.full_kernels;
         case LUMO_OPT_POISON: return o.poison;
         case LUMO_OPT_TAIL_PRIORITY: return o.tail_priority;
+        case LUMO_OPT_TOP_KD: return o.top_kd;
         default: return 0;
     }
 }
@@ -2352,12 +2355,19 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     // packed without alignment.  Children are stored as explicit indices (DKd::left).
     std::vector<int32_t> kd_new(d->num_kd_nodes, -1);
     std::vector<DKd> kdp;
+    std::vector<std::pair<size_t, size_t>> kd_trees;  // [first, end) of each tree's treelets in kdp
     {
         std::vector<int32_t> order;  // old indices in new order (-1: padding)
         auto kid = [&](int i, int which) { return which == 0 ? i + 1 : d->kd_nodes[i].right; };
         auto valid = [&](int i) { return i >= 0 && i < d->num_kd_nodes; };
         auto place_tree = [&](int root) {
             if (!valid(root) || kd_new[root] >= 0) return;
+            struct Extent {
+                std::vector<std::pair<size_t, size_t>>& v;
+                std::vector<int32_t>& o;
+                size_t lo;
+                ~Extent() { v.emplace_back(lo, o.size()); }
+            } extent{kd_trees, order, order.size()};
             int size = 0;  // nodes of the tree (bounded walk)
             {
                 std::vector<int32_t> st{root};
@@ -2523,6 +2533,27 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
             s.off_top_lnodes = put(lbvh.data(), sizeof(DBvh) * nl);
             s.top_onodes = (int32_t)no;
             s.top_lnodes = (int32_t)nl;
+            // kd stack entries per thread in LDS after the TOP set (TOP_BLOCK threads, 12 B each)
+            const size_t aligned = (top.size() + 15) & ~(size_t)15;
+            size_t room = c->lds_block > aligned + 256 ? c->lds_block - aligned - 256 : 0;
+            s.kst_cfg = c->o.kd_lds > 0 ? (int32_t)std::min<size_t>((size_t)c->o.kd_lds, room / (12 * (size_t)TOP_BLOCK)) : 0;
+            room -= 12 * (size_t)TOP_BLOCK * s.kst_cfg;
+            // then, in what is left, the first treelets of the largest kd tree (its top levels: the
+            // trees are laid out breadth-first by 128-B treelet, so they are a prefix of its range)
+            s.top_kd_lo = s.top_kd_n = 0;
+            s.off_top_kd = 0;
+            size_t big = 0, big_lo = 0;
+            for (const auto& tr : kd_trees)
+                if (tr.second - tr.first > big) {
+                    big = tr.second - tr.first;
+                    big_lo = tr.first;
+                }
+            if (c->o.top_kd && big > 8 && room >= 16 * 64 + 16) {
+                const size_t nk = std::min(big, (room - 16) / sizeof(DKd));
+                s.off_top_kd = put(kdp.data() + big_lo, sizeof(DKd) * nk);
+                s.top_kd_lo = (int32_t)big_lo;
+                s.top_kd_n = (int32_t)nk;
+            }
             const char* dp = nullptr;
             chk(upload(*c, top.data(), top.size(), &dp));
             if (st) {
@@ -2531,16 +2562,13 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
             }
             s.top = dp;
             s.top_bytes = (uint32_t)top.size();
+        } else {
+            s.kst_cfg = 0;
+            s.top_kd_lo = s.top_kd_n = 0;
+            s.off_top_kd = 0;
         }
-        // kd stack entries per thread in LDS after the TOP set (TOP_BLOCK threads, 12 B each)
         s.kst_n = 0;
-        s.kst_cfg = 0;
-        s.top_shm = (s.top_bytes + 15u) & ~15u;
-        if (s.top_bytes > 0 && c->o.kd_lds > 0) {
-            const size_t room = c->lds_block > s.top_shm + 256 ? c->lds_block - s.top_shm - 256 : 0;
-            s.kst_cfg = (int32_t)std::min<size_t>((size_t)c->o.kd_lds, room / (12 * (size_t)TOP_BLOCK));
-            s.top_shm += (uint32_t)(12 * (size_t)TOP_BLOCK * s.kst_cfg);
-        }
+        s.top_shm = ((s.top_bytes + 15u) & ~15u) + (uint32_t)(12 * (size_t)TOP_BLOCK * s.kst_cfg);
     }
     int n = d->num_lights, lg = 0;
     while (n > 1) {
@@ -2757,6 +2785,7 @@ lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info) {
     info->top_bytes = top ? (int32_t)c->sc.top_bytes : 0;
     info->top_object_nodes = c->sc.top_onodes;
     info->top_light_nodes = c->sc.top_lnodes;
+    info->top_kd_nodes = top ? c->sc.top_kd_n : 0;
     return LUMO_OK;
 }
 

@@ -116,6 +116,8 @@ def test_trace_closest_full_scale(dev, which, request):
     g = _trace_cmp(dev, sc, o, d)
     info = dev.scene_info()
     assert info.stack_class == (48 if which == "c2" else 24)
+    if which == "c2":  # the dragon's top kd treelets are walked from LDS (C3's TOP set is full)
+        assert info.top_kd_nodes > 1000
     assert np.mean(g[1] > 0) > 0.3
 
 
@@ -335,3 +337,34 @@ def test_c3_bench_schedule_full_frame(c3):
     for i, orr in zip(sub, ores):
         assert (res[i].num_rays, res[i].num_queries) == (orr.num_rays, orr.num_queries)
     assert after.closest_queries > before.closest_queries
+
+
+@pytest.mark.parametrize("top_kd,kd_lds", [(1, 8), (1, 4), (1, 0), (0, 8)])
+def test_kd_treelets_in_lds(top_kd, kd_lds):
+    """The TOP set's spare LDS holds the first treelets (top levels) of the largest kd tree
+    (kdtree.rs:101-169 walked from LDS below the staged range, from HBM above it): on the small
+    dragon (an instanced 7 200-triangle mesh, feature class 1) with 8 / 4 / 0 kd stack entries in
+    LDS (more or less room for nodes) and with the staging off, lumo_trace (t / kind / object and
+    traversal counters) and rendered tiles equal the oracle's."""
+    sc = scenes.dragon(torus_knot_tube(300, 12)).build()
+    d = L.Device(0, top_kd=top_kd, kd_lds=kd_lds)
+    try:
+        d.upload(sc)
+        info = d.scene_info()
+        assert info.lds_bytes == 0 and info.top_bytes > 0
+        assert (info.top_kd_nodes > 0) == (top_kd == 1)
+        desc = sc.desc()
+        o, dd = _closest_rays(desc, (0.0, 0.0, 0.0), 1 << 16, 31)
+        _trace_cmp(d, sc, o, dd)
+        o, dd, li = _visibility_rays(desc, 1 << 16, 32)
+        _trace_cmp(d, sc, o, dd, lights=li)
+        cam = scenes.default_camera((64, 48))
+        d.upload(sc, cam)
+        tasks = L.make_tasks(64, 48, 4, SEED)[:8]
+        bufs, res = d.render_tasks(tasks)
+    finally:
+        d.close()
+    obufs, ores, _ = O.render_tasks(desc, cam.desc, tasks, O.WAVEFRONT, 8)
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
