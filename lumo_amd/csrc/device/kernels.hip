@@ -554,16 +554,18 @@ __global__ __launch_bounds__(64) void k_ring(DScene sc, Paths S, Tasks T, int n_
     }
     __syncthreads();
     if (lane == 0) {
+        // task.rs:57-63: the three sums are independent chains, each in lumo's slot order, so one
+        // loop carries them side by side (the adds of one chain are exactly task.rs's)
         double f = 0.0, f2 = 0.0;
-        for (int i = 0; i < n; ++i) f = f + lum[i];
-        for (int i = 0; i < n; ++i) f2 = f2 + lum[i] * lum[i];
-        const double var = f2 - f * f / (double)n;
-        double delta = 1e-5;
-        if (!(var <= 0.0)) {
-            uint64_t cost = 0;
-            for (int i = 0; i < n; ++i) cost += cst[i];
-            delta = sqrt(var / (double)cost);
+        uint64_t cost = 0;
+        for (int i = 0; i < n; ++i) {
+            const double l = lum[i];
+            f = f + l;
+            f2 = f2 + l * l;
+            cost += cst[i];
         }
+        const double var = f2 - f * f / (double)n;
+        const double delta = !(var <= 0.0) ? sqrt(var / (double)cost) : 1e-5;
         T.delta[ti] = delta;
     }
 }

@@ -97,6 +97,15 @@ __device__ __forceinline__ void put_record(const ShadowQ& Q, int b, size_t r, co
 // One (light sample, BSDF sample) pair of NEE records (integrator.rs:87-137) at pair index r:
 // the light pick, its direction, bsdf_f / pdf / cosine, then the BSDF-sampled direction (6 RNG
 // draws).  Returns whether the BSDF sample exists (SI_BVALID).
+// A record's bsdf_f is read only when its pdf is not 0 (integrator.rs:146: mis_sample returns 0
+// first), so it is evaluated only then (LUMO_SKIP_DEAD): bsdf_f and bsdf_pdf draw nothing.
+template <int FX>
+__device__ __forceinline__ DColor record_f(const DScene& sc, const lumo_material& m, const DHit& ho, V3 wo, V3 w,
+                                           const double* L, double pdf) {
+    if (LUMO_SKIP_DEAD && pdf == 0.0) return cfill(0.0);
+    return bsdf_f<FX>(sc, m, ho, wo, w, L);
+}
+
 template <int FX>
 __device__ __forceinline__ bool nee_pair(const DScene& sc, const ShadowQ& sq, size_t r, const DHit& ho,
                                          const lumo_material& m, V3 wo, double* L, Xorshift& rng) {
@@ -107,17 +116,18 @@ __device__ __forceinline__ bool nee_pair(const DScene& sc, const ShadowQ& sq, si
     {
         const V2 rs = xs_vec2(rng);
         const V3 w = light_sample_towards<FX>(sc, Lo, ho.p, rs);
-        put_record(sq, SD_LO, r, spawn(ho, w), bsdf_f<FX>(sc, m, ho, wo, w, L), bsdf_pdf<FX>(sc, m, ho, wo, w, L),
-                   shading_cosine(m, w, ho.ns));
+        const double pdf = bsdf_pdf<FX>(sc, m, ho, wo, w, L);
+        put_record(sq, SD_LO, r, spawn(ho, w), record_f<FX>(sc, m, ho, wo, w, L, pdf), pdf, shading_cosine(m, w, ho.ns));
     }
     const double ru = xs_float(rng);
     const V2 rsq = xs_vec2(rng);
     V3 w;
     const bool ok = bsdf_sample<FX>(sc, m, ho, wo, L, ru, rsq, w);
     sq.I(SI_BVALID, r) = ok ? 1 : 0;
-    if (ok)
-        put_record(sq, SD_BO, r, spawn(ho, w), bsdf_f<FX>(sc, m, ho, wo, w, L), bsdf_pdf<FX>(sc, m, ho, wo, w, L),
-                   shading_cosine(m, w, ho.ns));
+    if (ok) {
+        const double pdf = bsdf_pdf<FX>(sc, m, ho, wo, w, L);
+        put_record(sq, SD_BO, r, spawn(ho, w), record_f<FX>(sc, m, ho, wo, w, L, pdf), pdf, shading_cosine(m, w, ho.ns));
+    }
     return ok;
 }
 constexpr int NEE_DRAWS = 6;  // RNG draws per pair in nee_pair
@@ -530,8 +540,8 @@ struct NeeRec {
 template <int FX>
 __device__ __forceinline__ NeeRec nee_record(const DScene& sc, const lumo_material& m, const DHit& ho, V3 wo, V3 w,
                                              const double* L) {
-    return NeeRec{spawn(ho, w), bsdf_f<FX>(sc, m, ho, wo, w, L), bsdf_pdf<FX>(sc, m, ho, wo, w, L),
-                  shading_cosine(m, w, ho.ns)};
+    const double pdf = bsdf_pdf<FX>(sc, m, ho, wo, w, L);
+    return NeeRec{spawn(ho, w), record_f<FX>(sc, m, ho, wo, w, L, pdf), pdf, shading_cosine(m, w, ho.ns)};
 }
 
 // shadow_record_q on a record held in registers (Scene::hit_light + mis_sample,
@@ -762,6 +772,7 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
         uint32_t base = blockIdx.x * blockDim.x;
 #if LUMO_PHASE_CLOCKS
         uint64_t ph[5] = {0, 0, 0, 0, 0}, tc0 = clock64(), tc1 = 0;
+        uint64_t lanes[4] = {0, 0, 0, 0};  // wave rounds; live lanes; lanes with an L record; with a B record
 #define LUMO_PHASE(k) (tc1 = clock64(), ph[k] += tc1 - tc0, tc0 = tc1)
 #else
 #define LUMO_PHASE(k) ((void)0)
@@ -876,6 +887,12 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
                 stc(S.rad, P.slot, P.rad);
             }
             LUMO_PHASE(4);
+#if LUMO_PHASE_CLOCKS
+            lanes[0] += 1;
+            lanes[1] += (uint64_t)__popcll(__ballot(live));
+            lanes[2] += (uint64_t)__popcll(__ballot(resolve));
+            lanes[3] += (uint64_t)__popcll(__ballot(resolve && ok));
+#endif
             // phase 3: the pair's visibility + MIS (k_shadow_q, NS1)
             if (resolve) {
 #if LUMO_PARK_NEE
@@ -917,8 +934,10 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
 #if LUMO_PHASE_CLOCKS
         // per wave (lane 0): cycles in the closest hit, shading, fetch, visibility and compaction
         // phases (wave-uniform spans: every lane passes the same marks)
-        if (lane_id() == 0)
+        if (lane_id() == 0) {
             for (int k = 0; k < 5; ++k) atomicAdd(S.tcount + TC_ALL + k, (unsigned long long)ph[k]);
+            for (int k = 0; k < 4; ++k) atomicAdd(S.tcount + TC_ALL + 5 + k, (unsigned long long)lanes[k]);
+        }
 #endif
     }
 #undef LUMO_PHASE

@@ -74,7 +74,7 @@ constexpr int TC_ALL = 2 * TC_N + 3;
 #define LUMO_PHASE_CLOCKS 0
 #endif
 // diagnostics builds: k_shadow_q cost classes, or k_bounce_q phase clocks
-constexpr int TC_STATS = LUMO_SHADOW_STATS ? 218 : (LUMO_PHASE_CLOCKS ? 8 : 0);
+constexpr int TC_STATS = LUMO_SHADOW_STATS ? 218 : (LUMO_PHASE_CLOCKS ? 12 : 0);
 
 struct DCam {
     Xform wtc, sctr, cts;
