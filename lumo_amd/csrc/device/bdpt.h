@@ -44,10 +44,21 @@ struct BVtx {
 #ifndef LUMO_VSTORE_AOS
 #define LUMO_VSTORE_AOS 1
 #endif
+// MIS plane (m, mf): each vertex's pdf_fwd, pdf_bck and flags again, slot-major ((s * V + v)), so
+// the MIS weight of a connection item (mis.rs:103-239), which walks these three fields along both
+// subpaths of its sample, reads them from a few contiguous lines its neighbouring items (the same
+// sample's other (s, t)) share, instead of one 184-B vertex record per vertex.
 struct VStore {
     double* d;
     int32_t* i;
     int V, N;
+    double* m;    // 2 per vertex: pdf_fwd, pdf_bck
+    int32_t* mf;  // VF_* flags
+    __device__ __forceinline__ size_t mi(int v, int s) const { return (size_t)s * V + v; }
+    __device__ __forceinline__ void set_bck(int v, int s, double bck) const {
+        D(20, v, s) = bck;
+        m[2 * mi(v, s) + 1] = bck;
+    }
 #if LUMO_VSTORE_AOS
     __device__ __forceinline__ double& D(int f, int v, int s) const { return d[((size_t)v * N + s) * VD_N + f]; }
     __device__ __forceinline__ int32_t& I(int f, int v, int s) const { return i[((size_t)v * N + s) * VI_N + f]; }
@@ -69,7 +80,11 @@ struct VStore {
         D(22, v, s) = x.uv.y;
         I(0, v, s) = x.mat;
         I(1, v, s) = x.light;
-        I(2, v, s) = (x.blank ? VF_BLANK : 0) | (x.backface ? VF_BACKFACE : 0) | (x.del ? VF_DELTA : 0);
+        const int32_t fl = (x.blank ? VF_BLANK : 0) | (x.backface ? VF_BACKFACE : 0) | (x.del ? VF_DELTA : 0);
+        I(2, v, s) = fl;
+        m[2 * mi(v, s)] = x.pdf_fwd;
+        m[2 * mi(v, s) + 1] = x.pdf_bck;
+        mf[mi(v, s)] = fl;
     }
     __device__ BVtx load(int v, int s) const {
         BVtx x;
@@ -367,7 +382,7 @@ __device__ int bdpt_walk(const DScene& sc, const VStore& st, int slot, Ray ro, X
         const double corr = mode == TR_RADIANCE ? 1.0 : v_shading_correction(sc, curr, wi2);
         const DColor bsdf = bsdf_f<FX>(sc, m, ho, wo, wi2, L, mode == TR_IMPORTANCE);
         gathered = gathered * (bsdf * v_shading_cosine(sc, curr, wi2, curr.ns) * corr / pdf_fwd);
-        st.D(20, depth - 1, slot) = v_pdf_prev<FX>(sc, curr, prev, wi2, L);  // verts[prev].pdf_bck
+        st.set_bck(depth - 1, slot, v_pdf_prev<FX>(sc, curr, prev, wi2, L));  // verts[prev].pdf_bck
         if (depth >= BDPT_RR_DEPTH) {
             const double lum = luminance(sc, gathered, L);
             const double rr_prob = rmin(lum / delta, 1.0);
@@ -405,9 +420,10 @@ __device__ MisE mis_plain(const DScene& sc, const PView& pv, int i, const double
         return light_side ? MisE{v.pdf_bck, v.pdf_fwd, v_is_delta<FX>(sc, v, L)}
                           : MisE{v.pdf_fwd, v.pdf_bck, v_is_delta<FX>(sc, v, L)};
     }
-    const VStore& st = *pv.st;
-    const double fwd = st.D(19, i, pv.slot), bck = st.D(20, i, pv.slot);
-    const bool del = (st.I(2, i, pv.slot) & VF_DELTA) != 0;  // == v_is_delta (blank vertices never set it)
+    const VStore& st = *pv.st;  // the MIS plane
+    const size_t k = st.mi(i, pv.slot);
+    const double fwd = st.m[2 * k], bck = st.m[2 * k + 1];
+    const bool del = (st.mf[k] & VF_DELTA) != 0;  // == v_is_delta (blank vertices never set it)
     return light_side ? MisE{bck, fwd, del} : MisE{fwd, bck, del};
 }
 
@@ -815,7 +831,7 @@ __device__ void bdpt_step_one(const DScene& sc, const Paths& S, const Tasks& T, 
                 const double corr = mode == TR_RADIANCE ? 1.0 : v_shading_correction(sc, curr, wi2);
                 const DColor bsdf = bsdf_f<FX>(sc, m, ho, wo, wi2, L, mode == TR_IMPORTANCE);
                 gathered = gathered * (bsdf * v_shading_cosine(sc, curr, wi2, curr.ns) * corr / pdf_fwd);
-                st.D(20, depth - 1, slot) = v_pdf_prev<FX>(sc, curr, prev, wi2, L);  // verts[prev].pdf_bck
+                st.set_bck(depth - 1, slot, v_pdf_prev<FX>(sc, curr, prev, wi2, L));  // verts[prev].pdf_bck
                 bool cont = true;
                 if (depth >= BDPT_RR_DEPTH) {
                     const double lum = luminance(sc, gathered, L);

@@ -833,7 +833,7 @@ enum WorkId {
     W_QS2_R, W_QS2_I, W_QS3_D, W_QS3_R, W_QS3_I, W_RAD3, W_LAM3, W_RASTER3, W_DEPTH3, W_QUERIES3, W_P_VALID3,
     W_COUNTS3, W_QS4_D, W_QS4_R, W_QS4_I, W_QS5_D, W_QS5_R, W_QS5_I, W_RAD4, W_LAM4, W_RASTER4, W_DEPTH4,
     W_QUERIES4, W_P_VALID4, W_COUNTS4, W_QS6_D, W_QS6_R, W_QS6_I, W_QS7_D, W_QS7_R, W_QS7_I,
-    W_SQ_QL,
+    W_SQ_QL, W_BD_LM, W_BD_LMF, W_BD_CM, W_BD_CMF, W_BDR_LM, W_BDR_LMF, W_BDR_CM, W_BDR_CMF,
     W_SPLIT_SET1,  // render_split_pipelined sets 1..3: hits + NEE records, 8 buffers each
     W_COUNT = W_SPLIT_SET1 + 3 * 8
 };
@@ -1572,8 +1572,10 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     size_t film_n = 0;
     if (bdpt) {
         const int V = c.max_vertices;
-        B.lp = VStore{wbuf<double>(c, W_BD_LD, (size_t)VD_N * V * N, st), wbuf<int32_t>(c, W_BD_LI, (size_t)VI_N * V * N, st), V, N};
-        B.cp = VStore{wbuf<double>(c, W_BD_CD, (size_t)VD_N * V * N, st), wbuf<int32_t>(c, W_BD_CI, (size_t)VI_N * V * N, st), V, N};
+        B.lp = VStore{wbuf<double>(c, W_BD_LD, (size_t)VD_N * V * N, st), wbuf<int32_t>(c, W_BD_LI, (size_t)VI_N * V * N, st), V, N,
+                      wbuf<double>(c, W_BD_LM, (size_t)2 * V * N, st), wbuf<int32_t>(c, W_BD_LMF, (size_t)V * N, st)};
+        B.cp = VStore{wbuf<double>(c, W_BD_CD, (size_t)VD_N * V * N, st), wbuf<int32_t>(c, W_BD_CI, (size_t)VI_N * V * N, st), V, N,
+                      wbuf<double>(c, W_BD_CM, (size_t)2 * V * N, st), wbuf<int32_t>(c, W_BD_CMF, (size_t)V * N, st)};
         B.sp = SplatStore{wbuf<double>(c, W_BD_SP, (size_t)10 * V * N, st), wbuf<int32_t>(c, W_BD_SPN, N, st), V, N};
         B.overflow = wbuf<uint32_t>(c, W_BD_OVF, 2, st);
         B.redo_count = B.overflow + 1;
@@ -1597,8 +1599,10 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         BI.lam0 = wbuf<double>(c, W_BD_LAM0, 4 * (size_t)N, st);
         items_total = wbuf<uint32_t>(c, W_BD_ITOTAL, 2, st);
         BR = B;
-        BR.lp = VStore{wbuf<double>(c, W_BDR_LD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_LI, (size_t)VI_N * VR * NR, st), VR, NR};
-        BR.cp = VStore{wbuf<double>(c, W_BDR_CD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_CI, (size_t)VI_N * VR * NR, st), VR, NR};
+        BR.lp = VStore{wbuf<double>(c, W_BDR_LD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_LI, (size_t)VI_N * VR * NR, st), VR, NR,
+                       wbuf<double>(c, W_BDR_LM, (size_t)2 * VR * NR, st), wbuf<int32_t>(c, W_BDR_LMF, (size_t)VR * NR, st)};
+        BR.cp = VStore{wbuf<double>(c, W_BDR_CD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_CI, (size_t)VI_N * VR * NR, st), VR, NR,
+                       wbuf<double>(c, W_BDR_CM, (size_t)2 * VR * NR, st), wbuf<int32_t>(c, W_BDR_CMF, (size_t)VR * NR, st)};
         BR.sp = SplatStore{wbuf<double>(c, W_BDR_SP, (size_t)10 * VR * NR, st), wbuf<int32_t>(c, W_BDR_SPN, NR, st), VR, NR};
         BR.draws = wbuf<double>(c, W_BDR_DRAWS, (size_t)5 * VR * NR, st);
         BR.ok = wbuf<int32_t>(c, W_BDR_OK, (size_t)VR * NR, st);
