@@ -407,6 +407,10 @@ enum {
                                   (LUMO_TAIL_PRIORITY, 0)                                           */
     LUMO_OPT_TOP_KD,           /* upload: the TOP set's spare LDS holds the top treelets of the
                                   largest kd tree: 0 / 1 (LUMO_TOP_KD, 1)                           */
+    LUMO_OPT_TAIL_BOUNCES,     /* fused pipeline, one pass per unit: fused bounces the tail stream runs
+                                  before the tail kernel, 0-16 (LUMO_TAIL_BOUNCES, 0)               */
+    LUMO_OPT_FILM_FIRST,       /* fused pipeline, film on the tail stream: the unit's film before its
+                                  last ring: 0 / 1 (LUMO_FILM_FIRST, 0)                             */
     LUMO_OPT_COUNT
 };
 lumo_status lumo_set_option(void* ctx, int32_t option, int64_t value);

@@ -738,6 +738,8 @@ struct Opts {
     int poison = 0;                    // new device buffers filled with 0xFF (reads before writes show as NaN / -1)
     int tail_priority = 0;             // the pipelined passes' tail / film / ring stream at high priority
     int top_kd = 1;                    // the TOP set's spare LDS holds the top treelets of the largest kd tree
+    int tail_bounces = 0;              // fused pipeline, M == 1: fused bounces on the tail stream before the tail kernel
+    int film_first = 0;                // fused pipeline, film on the tail stream: the film before the unit's last ring
 };
 
 struct Ctx {
@@ -1090,6 +1092,22 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         HIPCHK(hipEventRecord(c.tail_ev[set], A));
         // ---- stream B: per pass, the rest of its paths, its film and its ring
         HIPCHK(hipStreamWaitEvent(B, c.tail_ev[set], 0));
+        // M == 1: B first runs tail_bounces more fused bounces over the whole queue (the bulk of the
+        // paths left after the head bounces, at full throughput, past Russian roulette: B runs them
+        // after the previous pass's ring), then the tail kernel takes the rest
+        const int bb = mu == 1 ? c.o.tail_bounces : 0;
+        for (int b = heads; b < heads + bb; ++b) {
+            k_bounce_begin<<<1, 64, 0, B>>>(P.counts, P.tcount + TC_HEADQ);
+            StageTimer tm(c, c.o.timing, ST_CLOSEST, B);
+            launch_trav(
+                c, (uint64_t)N,
+                [&](auto K, const TravLaunch& l) {
+                    launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[b & 1], P.qs[(b + 1) & 1], 0u, false,
+                                                        c.o.dyn, c.o.bounce_threads);
+                },
+                B);
+        }
+        const int qt = heads + bb;  // the tail kernel's queue
         k_bounce_begin<<<1, 64, 0, B>>>(P.counts, P.tcount + TC_HEADQ);
         for (int m = 0; m < mu; ++m) {
             const uint64_t pass = p0 + (uint64_t)m;
@@ -1102,13 +1120,20 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
                     c, (uint64_t)N * mu,
                     [&](auto K, const TravLaunch& l) {
                         // P, not the view: the paths carry virtual slots
-                        launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[heads & 1], P.qs[(heads + 1) & 1],
+                        launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[qt & 1], P.qs[(qt + 1) & 1],
                                                             0xffffffffu, true, 0, BLOCK, m * N, (m + 1) * N);
                     },
                     B);
             }
             // the ring (which computes the samples' luminance itself): the next pass's Russian
-            // roulette waits for it; the film is off that chain
+            // roulette waits for it; the film is off that chain (film_first: the unit's film before
+            // its last ring when they share stream B)
+            const bool film_here = max_P <= BLOCK && F == B && c.o.film_first && m == mu - 1;
+            if (film_here) {
+                StageTimer tm(c, c.o.timing, ST_FILM, B);
+                k_finish_film<<<n_tasks, BLOCK, 0, B>>>(c.sc, P, T, c.cam, (uint32_t)p0, D, dump_p, c.tone_map,
+                                                        c.tone_arg, 0, mu, N);
+            }
             {
                 StageTimer tm(c, c.o.timing, ST_RING, B);
                 k_ring<<<n_tasks, 64, 0, B>>>(c.sc, V, T, n_tasks, 1, m == mu - 1 ? P.counts : nullptr, 0);
@@ -1127,7 +1152,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         HIPCHK(hipEventRecord(c.pass_ev[set], B));
         // the film of the unit's passes, one launch in pass order (after the previous unit's film on
         // the same stream), on a stream of its own when one is free
-        if (max_P <= BLOCK) {
+        if (max_P <= BLOCK && !(F == B && c.o.film_first)) {
             if (F != B) HIPCHK(hipStreamWaitEvent(F, c.pass_ev[set], 0));
             StageTimer tm(c, c.o.timing, ST_FILM, F);
             k_finish_film<<<n_tasks, BLOCK, 0, F>>>(c.sc, P, T, c.cam, (uint32_t)p0, D, dump_p, c.tone_map, c.tone_arg,
@@ -2001,7 +2026,7 @@ const char* const kOptEnv[LUMO_OPT_COUNT] = {
     "LUMO_TIMING", "LUMO_LDS", "LUMO_TOP", "LUMO_FUSED", "LUMO_TAIL", "LUMO_PIPELINE", "LUMO_HEADS", "LUMO_MERGE",
     "LUMO_DYN", "LUMO_BOUNCE_THREADS", "LUMO_SPLIT_PIPE", "LUMO_SPLIT_GROUPS", "LUMO_BDPT_TAIL", "LUMO_BOUNCE_AHEAD",
     "LUMO_LDS_GRID", "LUMO_TOP_GRID", "LUMO_TOP_KB", "LUMO_KD_LDS", "LUMO_STACK_CLASS", "LUMO_FULL_KERNELS",
-    "LUMO_POISON", "LUMO_TAIL_PRIORITY", "LUMO_TOP_KD"};
+    "LUMO_POISON", "LUMO_TAIL_PRIORITY", "LUMO_TOP_KD", "LUMO_TAIL_BOUNCES", "LUMO_FILM_FIRST"};
 
 void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
     lo = 0;
@@ -2018,6 +2043,7 @@ void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
         case LUMO_OPT_LDS_GRID: case LUMO_OPT_TOP_GRID: lo = 1; hi = 1 << 20; break;
         case LUMO_OPT_TOP_KB: hi = (int64_t)(c.lds_cu / 1024); break;
         case LUMO_OPT_KD_LDS: hi = 64; break;
+        case LUMO_OPT_TAIL_BOUNCES: hi = 16; break;
         case LUMO_OPT_STACK_CLASS: hi = 64; break;
         default: break;
     }
@@ -2076,6 +2102,8 @@ lumo_status set_opt(Ctx& c, int k, int64_t v) {
         case LUMO_OPT_FULL_KERNELS: o.full_kernels = iv; break;
         case LUMO_OPT_POISON: o.poison = iv; break;
         case LUMO_OPT_TOP_KD: o.top_kd = iv; break;
+        case LUMO_OPT_TAIL_BOUNCES: o.tail_bounces = iv; break;
+        case LUMO_OPT_FILM_FIRST: o.film_first = iv; break;
         case LUMO_OPT_TAIL_PRIORITY:
             if (iv != o.tail_priority) {
                 const lumo_status e = make_tail_stream(c, iv);
@@ -2114,6 +2142,8 @@ int64_t get_opt(const Ctx& c, int k) {
         case LUMO_OPT_POISON: return o.poison;
         case LUMO_OPT_TAIL_PRIORITY: return o.tail_priority;
         case LUMO_OPT_TOP_KD: return o.top_kd;
+        case LUMO_OPT_TAIL_BOUNCES: return o.tail_bounces;
+        case LUMO_OPT_FILM_FIRST: return o.film_first;
         default: return 0;
     }
 }
