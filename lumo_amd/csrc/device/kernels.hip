@@ -266,9 +266,47 @@ __global__ __launch_bounds__(BLOCK) void k_zero_list(ZeroList z) {
         for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < z.words[k]; i += stride) z.p[k][i] = 0u;
 }
 
-// The tail kernel's fetch counter zeroed between the passes of a merged unit (render_pipelined).
-__global__ void k_zero_fetch(uint32_t* counts) {
-    if (threadIdx.x == 0) counts[CNT_FETCH_T] = 0u;
+// The queue of a merged unit after its head bounces, split by pass (render_pipelined): the entry of
+// a path of pass m (virtual slot in [m N, (m + 1) N)) goes to segment m of `dst` (entries m N + k),
+// counted in CNT_NEXT of counts + (1 + m) CNT_N (zeroed by the caller; k_bounce_begin then starts
+// the pass's bounce as usual).  Entries keep every
+// plane; each pass's tail kernel then runs on full waves of its own paths.  Positions within a
+// segment follow the block-aggregated atomics, a lane assignment only.
+__global__ __launch_bounds__(BLOCK) void k_split_passes(QState src, QState dst, uint32_t* counts, int N, int M) {
+    __shared__ uint32_t hist[MAX_MERGE], seg_base[MAX_MERGE];
+    const uint32_t count = counts[CNT_NEXT];  // the last head bounce's continuing paths
+    for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < count; b0 += gridDim.x * blockDim.x) {
+        if (threadIdx.x < MAX_MERGE) hist[threadIdx.x] = 0u;
+        __syncthreads();
+        const uint32_t q = b0 + threadIdx.x;
+        int m = -1;
+        uint32_t rank = 0;
+        if (q < count) {
+            m = src.I(QI_SLOT, q) / N;
+            rank = atomicAdd(&hist[m], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < M && hist[threadIdx.x])
+            seg_base[threadIdx.x] = atomicAdd(counts + (1 + threadIdx.x) * CNT_N + CNT_NEXT, hist[threadIdx.x]);
+        __syncthreads();
+        if (m >= 0) {
+            const size_t d = (size_t)m * N + seg_base[m] + rank;
+            for (int k = 0; k < QD_N; ++k) dst.D(k, d) = src.D(k, q);
+            for (int k = 0; k < 2; ++k) dst.R(k, d) = src.R(k, q);
+            for (int k = 0; k < QI_N; ++k) dst.I(k, d) = src.I(k, q);
+        }
+        __syncthreads();
+    }
+}
+
+// Segment m (entries m N ..) of a queue as a queue of its own.
+QState segment(const QState& Q, int m, int N) {
+    QState V = Q;
+    const size_t o = (size_t)m * (size_t)N;
+    V.d += o;
+    V.r += o;
+    V.i += o;
+    return V;
 }
 
 // Queue counters (and optionally one more word) zeroed in-stream: a kernel instead of a fill.
@@ -706,9 +744,8 @@ struct Timing {
     }
 };
 
-// Merged passes of the fused pipeline (render_pipelined): at most MAX_MERGE passes per unit, by
-// default as many as bring a unit to about kMergeTarget paths (a full 1024^2 frame: 1).
-constexpr int MAX_MERGE = 8;
+// Merged passes of the fused pipeline (render_pipelined): at most MAX_MERGE (state.h) passes per
+// unit, by default as many as bring a unit to about kMergeTarget paths (a full 1024^2 frame: 1).
 constexpr uint64_t kMergeTarget = (uint64_t)1 << 21;
 
 // Execution options of a context (lumo_set_option; include/lumo_amd.h LUMO_OPT_*).  None of them
@@ -968,7 +1005,7 @@ void alloc_pass_set(Ctx& c, Paths& Q, int k, int N, lumo_status& st) {
     Q.depth = wbuf<uint32_t>(c, w[3], N, st);
     Q.queries = wbuf<uint32_t>(c, w[4], N, st);
     Q.p_valid = wbuf<uint32_t>(c, w[5], N, st);
-    Q.counts = wbuf<uint32_t>(c, w[6], CNT_N, st);
+    Q.counts = wbuf<uint32_t>(c, w[6], (size_t)CNT_N * (1 + MAX_MERGE), st);  // + the merged passes' queues
     for (int h = 0; h < 2; ++h) {
         Q.qs[h].cap = (size_t)N;
         Q.qs[h].d = wbuf<double>(c, w[7 + 3 * h], QD_N * (size_t)N, st);
@@ -1092,36 +1129,45 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         HIPCHK(hipEventRecord(c.tail_ev[set], A));
         // ---- stream B: per pass, the rest of its paths, its film and its ring
         HIPCHK(hipStreamWaitEvent(B, c.tail_ev[set], 0));
-        // M == 1: B first runs tail_bounces more fused bounces over the whole queue (the bulk of the
-        // paths left after the head bounces, at full throughput, past Russian roulette: B runs them
-        // after the previous pass's ring), then the tail kernel takes the rest
-        const int bb = mu == 1 ? c.o.tail_bounces : 0;
-        for (int b = heads; b < heads + bb; ++b) {
-            k_bounce_begin<<<1, 64, 0, B>>>(P.counts, P.tcount + TC_HEADQ);
-            StageTimer tm(c, c.o.timing, ST_CLOSEST, B);
-            launch_trav(
-                c, (uint64_t)N,
-                [&](auto K, const TravLaunch& l) {
-                    launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[b & 1], P.qs[(b + 1) & 1], 0u, false,
-                                                        c.o.dyn, c.o.bounce_threads);
-                },
-                B);
+        // the unit's queue split by pass (M > 1) into segments of the other ping-pong queue, each
+        // with counters of its own; then per pass: tail_bounces more fused bounces over its paths
+        // (past Russian roulette, after the previous pass's ring on this stream), the tail kernel
+        // for the rest, the ring
+        const QState& Qh = P.qs[heads & 1];
+        const QState& Qs = P.qs[(heads + 1) & 1];
+        if (mu > 1) {
+            ZeroList z;
+            z.add(P.counts + CNT_N, sizeof(uint32_t) * CNT_N * (size_t)mu);
+            k_zero_list<<<1, BLOCK, 0, B>>>(z);
+            k_split_passes<<<std::min(ceil_div((uint64_t)N * mu, BLOCK), 4096), BLOCK, 0, B>>>(Qh, Qs, P.counts, N, mu);
         }
-        const int qt = heads + bb;  // the tail kernel's queue
-        k_bounce_begin<<<1, 64, 0, B>>>(P.counts, P.tcount + TC_HEADQ);
+        const int bb = c.o.tail_bounces;
         for (int m = 0; m < mu; ++m) {
             const uint64_t pass = p0 + (uint64_t)m;
             Paths V = pass_view(P, m, N);
+            Paths Pm = P;  // this pass's paths: its own counters, its queue segment (virtual slots)
+            Pm.counts = mu > 1 ? P.counts + (size_t)(1 + m) * CNT_N : P.counts;
+            const QState q0 = mu > 1 ? segment(Qs, m, N) : Qh, q1 = mu > 1 ? segment(Qh, m, N) : Qs;
             if (D.delta) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, B));
-            if (m > 0) k_zero_fetch<<<1, 64, 0, B>>>(P.counts);
+            for (int b = 0; b < bb; ++b) {
+                k_bounce_begin<<<1, 64, 0, B>>>(Pm.counts, P.tcount + TC_HEADQ);
+                StageTimer tm(c, c.o.timing, ST_CLOSEST, B);
+                launch_trav(
+                    c, (uint64_t)N,
+                    [&](auto K, const TravLaunch& l) {
+                        launch_bounce_q<decltype(K)::value>(l, c.sc, Pm, T, (b & 1) ? q1 : q0, (b & 1) ? q0 : q1, 0u,
+                                                            false, c.o.dyn, c.o.bounce_threads);
+                    },
+                    B);
+            }
+            k_bounce_begin<<<1, 64, 0, B>>>(Pm.counts, P.tcount + TC_HEADQ);
             {
                 StageTimer tm(c, c.o.timing, ST_RESOLVE, B);
                 launch_trav(
-                    c, (uint64_t)N * mu,
+                    c, (uint64_t)N,
                     [&](auto K, const TravLaunch& l) {
-                        // P, not the view: the paths carry virtual slots
-                        launch_bounce_q<decltype(K)::value>(l, c.sc, P, T, P.qs[qt & 1], P.qs[(qt + 1) & 1],
-                                                            0xffffffffu, true, 0, BLOCK, m * N, (m + 1) * N);
+                        launch_bounce_q<decltype(K)::value>(l, c.sc, Pm, T, (bb & 1) ? q1 : q0, (bb & 1) ? q0 : q1,
+                                                            0xffffffffu, true, 0, BLOCK);
                     },
                     B);
             }
@@ -1562,7 +1608,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     S.p_rgb = wbuf<double>(c, W_P_RGB, 3 * (size_t)N, st);
     S.p_valid = wbuf<uint32_t>(c, W_P_VALID, NV, st);
     S.film = wbuf<double>(c, W_FILM, 4 * (size_t)N, st);
-    S.counts = wbuf<uint32_t>(c, W_COUNTS, CNT_N, st);
+    S.counts = wbuf<uint32_t>(c, W_COUNTS, (size_t)CNT_N * (1 + MAX_MERGE), st);  // + the merged passes' queues
     S.tcount = wbuf<unsigned long long>(c, W_TCOUNT, TC_ALL + TC_STATS, st);
     S.checks = wbuf<unsigned long long>(c, W_CHECKS, 3, st);
     Tasks T{};

@@ -43,6 +43,7 @@ constexpr int TOP_BLOCK = 1024;
 #define LUMO_BDPT_STEP_WAVES 2
 #endif
 constexpr uint64_t SAMPLES_INCREMENT = 256;
+constexpr int MAX_MERGE = 8;  // passes per unit of the fused pipeline (render_pipelined)
 constexpr int RR_DEPTH = 5;
 
 // ST_RESOLVE: path tracer k_nee_fold (n_shadow > 1); BDPT re-runs + fold.
