@@ -212,7 +212,8 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
                 for (int k = 0; k < NEE_DRAWS * ns; ++k) xs_step(rng);
                 n_sh = (uint32_t)ns;  // the L records; k_nee_fold adds the valid B records
             } else {
-                for (int i = 0; i < ns; ++i) n_sh += 1u + (nee_pair<FX>(sc, sq, (size_t)sp * ns + i, ho, m, wo, L, rng) ? 1u : 0u);
+                for (int i = 0; i < ns; ++i)
+                    n_sh += 1u + (nee_pair<FX>(sc, sq, (size_t)i * sq.hcap + sp, ho, m, wo, L, rng) ? 1u : 0u);
             }
             for (int k = 0; k < NS; ++k) {
                 sq.HD(SH_G + k, sp) = gathered.s[k];
@@ -352,7 +353,7 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) vo
             const size_t r = (size_t)(qv >> 1);
             const int which = qv & 1;  // 0: light-sampled record, 1: BSDF-sampled
             const int b = which ? SD_BO : SD_LO;
-            const DColor x = shadow_record_q<STK, FX, LDS == 2>(sc, Q, b, r, which == 0, (uint32_t)(r / (size_t)ns), C);
+            const DColor x = shadow_record_q<STK, FX, LDS == 2>(sc, Q, b, r, which == 0, (uint32_t)(r % Q.hcap), C);
             for (int k = 0; k < NS; ++k) Q.D(b + 6 + k, r) = x.s[k];
         }
         flush_counters(C, S.tcount + TC_N);
@@ -369,8 +370,8 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) vo
             lj -= c;
             bk++;
         }
-        const size_t r = (size_t)bk * Q.seg * ns + lj;  // pair index
-        const uint32_t p = (uint32_t)(NS1 ? r : r / (size_t)ns);
+        const size_t r = (size_t)bk * Q.seg + lj;  // pair index (n_shadow = 1: the path's)
+        const uint32_t p = (uint32_t)r;
 #if LUMO_SHADOW_STATS
         // diagnostics build: per-record traversal cost (AABB + kd + triangle steps) by class
         // (record L/B x environment light x light missed / occluded / visible), cost histogram
@@ -426,11 +427,12 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) vo
 template <int FX>
 __global__ __launch_bounds__(BLOCK, LUMO_NEE_WAVES) void k_nee_gen(DScene sc, Paths S) {
     const int ns = sc.n_shadow;
-    uint32_t bc[NB], count = 0;  // pairs per bucket
+    uint32_t pc[NB], paths = 0;  // paths per bucket
     for (int b = 0; b < NB; ++b) {
-        bc[b] = S.counts[CNT_BUCKET0 + b] * (uint32_t)ns;
-        count += bc[b];
+        pc[b] = S.counts[CNT_BUCKET0 + b];
+        paths += pc[b];
     }
+    const uint32_t count = paths * (uint32_t)ns;
     const ShadowQ sq = S.sq;
     uint32_t dead = 0;
     // whole blocks per round: the query-list append needs every thread of the block
@@ -439,12 +441,15 @@ __global__ __launch_bounds__(BLOCK, LUMO_NEE_WAVES) void k_nee_gen(DScene sc, Pa
         size_t r = 0;
         bool live_l = false, live_b = false;
         if (j < count) {
-        uint32_t lj = j;
+        // light sample i of the bucket-ordered path k: pairs are stored light-sample-major
+        // (r = i * hcap + p), so a wave's lanes take consecutive paths with the same i (coalesced
+        // header reads and record writes, the same RNG skip on every lane)
+        const int i = (int)(j / paths);
+        uint32_t lj = j - (uint32_t)i * paths;
         int bk = 0;
-        while (lj >= bc[bk]) lj -= bc[bk++];
-        r = (size_t)bk * sq.seg * ns + lj;
-        const uint32_t p = (uint32_t)(r / (size_t)ns);
-        const int i = (int)(r - (size_t)p * ns);
+        while (lj >= pc[bk]) lj -= pc[bk++];
+        const uint32_t p = bk * sq.seg + lj;
+        r = (size_t)i * sq.hcap + p;
         DHit ho;
         ho.t = 0.0;
         ho.p = V3{sq.HD(SH_P, p), sq.HD(SH_P + 1, p), sq.HD(SH_P + 2, p)};
@@ -493,7 +498,7 @@ __global__ __launch_bounds__(BLOCK) void k_nee_fold(Paths S, QState nxt, int ns)
         DColor acc = cfill(0.0);
         int32_t nb = 0;
         for (int i = 0; i < ns; ++i) {
-            const size_t r = (size_t)p * ns + i;
+            const size_t r = (size_t)i * Q.hcap + p;
             // the records' MIS terms (k_shadow_q wrote them over their bsdf_f planes), 0 for those
             // without a walk; single_i = (0 + L + B) / pdf_light (integrator.rs:87-137)
             const bool bv = Q.I(SI_BVALID, r) != 0;

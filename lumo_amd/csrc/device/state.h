@@ -109,7 +109,7 @@ struct HitQ {
 };
 // NEE records in queue order: per path with shadow rays a header (gathered, wavelengths, radiance
 // of a path that ends this bounce, slot, next-queue position or -1), and per light sample i the
-// pair of records (light-sampled L, BSDF-sampled B) at pair index P * n_shadow + i.  Path P of
+// pair of records (light-sampled L, BSDF-sampled B) at pair index i * hcap + P (light-sample-major).  Path P of
 // bucket b is at P = b * seg + (its position in the bucket); hcap = NB * seg.
 enum { SD_LO = 0, SD_LD = 3, SD_LF = 6, SD_LPS = 10, SD_LCOS = 11, SD_BO = 12, SD_BD = 15, SD_BF = 18,
        SD_BPS = 22, SD_BCOS = 23, SD_PDFL = 24, SD_N = 25 };
