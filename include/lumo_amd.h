@@ -407,8 +407,9 @@ enum {
                                   (LUMO_TAIL_PRIORITY, 0)                                           */
     LUMO_OPT_TOP_KD,           /* upload: the TOP set's spare LDS holds the top treelets of the
                                   largest kd tree: 0 / 1 (LUMO_TOP_KD, 1)                           */
-    LUMO_OPT_TAIL_BOUNCES,     /* fused pipeline, one pass per unit: fused bounces the tail stream runs
-                                  before the tail kernel, 0-16 (LUMO_TAIL_BOUNCES, 0)               */
+    LUMO_OPT_TAIL_BOUNCES,     /* fused pipeline: fused bounces per pass the tail stream runs before the
+                                  tail kernel, -1 auto (2 for one-pass units, 0 for merged ones), 0-16
+                                  (LUMO_TAIL_BOUNCES, -1)                                           */
     LUMO_OPT_FILM_FIRST,       /* fused pipeline, film on the tail stream: the unit's film before its
                                   last ring: 0 / 1 (LUMO_FILM_FIRST, 0)                             */
     LUMO_OPT_COUNT

@@ -775,7 +775,7 @@ struct Opts {
     int poison = 0;                    // new device buffers filled with 0xFF (reads before writes show as NaN / -1)
     int tail_priority = 0;             // the pipelined passes' tail / film / ring stream at high priority
     int top_kd = 1;                    // the TOP set's spare LDS holds the top treelets of the largest kd tree
-    int tail_bounces = 0;              // fused pipeline, M == 1: fused bounces on the tail stream before the tail kernel
+    int tail_bounces = -1;             // fused pipeline: fused bounces per pass on the tail stream before the tail kernel (-1 auto)
     int film_first = 0;                // fused pipeline, film on the tail stream: the film before the unit's last ring
 };
 
@@ -1141,7 +1141,10 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
             k_zero_list<<<1, BLOCK, 0, B>>>(z);
             k_split_passes<<<std::min(ceil_div((uint64_t)N * mu, BLOCK), 4096), BLOCK, 0, B>>>(Qh, Qs, P.counts, N, mu);
         }
-        const int bb = c.o.tail_bounces;
+        // automatic: 2 for one-pass units (a full frame: its chain of tails and rings has room, and
+        // the bulk of the paths left after the head bounces runs at full throughput; C1 2 467 ->
+        // 2 380 ms), none for merged units (a rank's share: the tail stream is the critical chain)
+        const int bb = c.o.tail_bounces >= 0 ? c.o.tail_bounces : (mu == 1 ? 2 : 0);
         for (int m = 0; m < mu; ++m) {
             const uint64_t pass = p0 + (uint64_t)m;
             Paths V = pass_view(P, m, N);
@@ -2089,7 +2092,7 @@ void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
         case LUMO_OPT_LDS_GRID: case LUMO_OPT_TOP_GRID: lo = 1; hi = 1 << 20; break;
         case LUMO_OPT_TOP_KB: hi = (int64_t)(c.lds_cu / 1024); break;
         case LUMO_OPT_KD_LDS: hi = 64; break;
-        case LUMO_OPT_TAIL_BOUNCES: hi = 16; break;
+        case LUMO_OPT_TAIL_BOUNCES: lo = -1; hi = 16; break;
         case LUMO_OPT_STACK_CLASS: hi = 64; break;
         default: break;
     }
