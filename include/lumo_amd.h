@@ -430,7 +430,7 @@ typedef struct {
     int32_t units_in_flight; /* split pipeline: (group, pass) units in flight              */
     int32_t task_groups;     /* split pipeline: independent task groups                    */
     int32_t fused;           /* 1: fused bounce kernel, 0: three kernels per bounce         */
-    int32_t pad0;
+    int32_t tail_bounces;    /* fused pipeline: fused bounces per pass on the tail stream   */
 } lumo_schedule_info;
 lumo_status lumo_last_schedule(void* ctx, lumo_schedule_info* info);
 

@@ -164,7 +164,7 @@ class Stats(C.Structure):
 class ScheduleInfo(C.Structure):
     _fields_ = [("schedule", C.c_int32), ("head_streams", C.c_int32), ("head_bounces", C.c_int32),
                 ("merged_passes", C.c_int32), ("units_in_flight", C.c_int32), ("task_groups", C.c_int32),
-                ("fused", C.c_int32), ("pad0", C.c_int32)]
+                ("fused", C.c_int32), ("tail_bounces", C.c_int32)]
 
 
 SCHED_SEQUENTIAL, SCHED_FUSED_PIPELINE, SCHED_SPLIT_PIPELINE = range(3)

@@ -1096,6 +1096,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
     c.sched.head_streams = NA;
     c.sched.head_bounces = heads;
     c.sched.merged_passes = M;
+    c.sched.tail_bounces = c.o.tail_bounces >= 0 ? c.o.tail_bounces : (M == 1 ? 2 : 0);
     const int gN = ceil_div(N, BLOCK);
     const uint64_t units = (max_samples + (uint64_t)M - 1) / (uint64_t)M;
     for (uint64_t u = 0; u < units; ++u) {
@@ -1144,7 +1145,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
         // automatic: 2 for one-pass units (a full frame: its chain of tails and rings has room, and
         // the bulk of the paths left after the head bounces runs at full throughput; C1 2 467 ->
         // 2 380 ms), none for merged units (a rank's share: the tail stream is the critical chain)
-        const int bb = c.o.tail_bounces >= 0 ? c.o.tail_bounces : (mu == 1 ? 2 : 0);
+        const int bb = c.sched.tail_bounces;
         for (int m = 0; m < mu; ++m) {
             const uint64_t pass = p0 + (uint64_t)m;
             Paths V = pass_view(P, m, N);

@@ -260,9 +260,10 @@ def test_headline_schedule_matches_oracle(cornell):
         before = d.stats()
         bufs, res = d.render_tasks(tasks, max_paths=1 << 23)
         after = d.stats()
-        assert after.launches[1] - before.launches[1] == 6 * spp  # 6 fused head bounces per pass
+        # 6 fused head bounces and 2 more on the tail stream per pass, then the tail kernel
+        assert after.launches[1] - before.launches[1] == (6 + 2) * spp
         sch = d.last_schedule()
-        assert (sch.schedule, sch.head_streams, sch.head_bounces, sch.merged_passes) == (1, 3, 6, 1)
+        assert (sch.schedule, sch.head_streams, sch.head_bounces, sch.merged_passes, sch.tail_bounces) == (1, 3, 6, 1, 2)
         d.set_option("pipeline", 0)
         seq, seq_res = d.render_tasks(tasks, max_paths=1 << 23)
         assert d.last_schedule().schedule == 0
