@@ -238,7 +238,7 @@ __global__ void k_bounce_begin(uint32_t* counts, unsigned long long* headq) {
         counts[CNT_FETCH_C] = 0;
         counts[CNT_FETCH_T] = 0;
         for (int b = 0; b < NB; ++b) counts[CNT_BUCKET0 + b] = 0;
-        counts[CNT_SHQ] = 0;
+        for (int k = 0; k < SHQ_CLASSES; ++k) counts[CNT_SHQ + k] = 0;
     }
 }
 
@@ -1023,13 +1023,13 @@ void alloc_split_set(Ctx& c, Paths& Q, const Paths& S, int k, int ns, lumo_statu
     Q.sq.hd = wbuf<double>(c, w + 4, (ns > 1 ? SH_N : SH_N1) * S.sq.hcap, st);
     Q.sq.hi = wbuf<int32_t>(c, w + 5, SHI_N * S.sq.hcap, st);
     Q.sq.hr = ns > 1 ? wbuf<uint64_t>(c, w + 6, 2 * S.sq.hcap, st) : nullptr;
-    Q.sq.ql = ns > 1 ? wbuf<int32_t>(c, w + 7, 2 * S.sq.cap, st) : nullptr;
+    Q.sq.ql = ns > 1 ? wbuf<int32_t>(c, w + 7, SHQ_CLASSES * S.sq.cap, st) : nullptr;
 }
 // Device bytes of one extra pass set of the split schedule.
 size_t split_set_bytes(const Paths& S, int N, int ns) {
     return (size_t)N * (4 + 4 + 2) * 8 + (size_t)N * 3 * 4 + 2 * (size_t)N * (QD_N * 8 + 16 + QI_N * 4) +
            S.hq.cap * (8 + 12) + S.sq.cap * (SD_N * 8 + SI_N * 4) +
-           S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4 + (ns > 1 ? 16 : 0)) + (ns > 1 ? S.sq.cap * 8 : 0);
+           S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4 + (ns > 1 ? 16 : 0)) + (ns > 1 ? S.sq.cap * 4 * SHQ_CLASSES : 0);
 }
 
 
@@ -1607,7 +1607,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         S.sq.hd = wbuf<double>(c, W_SQ_HD, (ns > 1 ? SH_N : SH_N1) * S.sq.hcap, st);
         S.sq.hi = wbuf<int32_t>(c, W_SQ_HI, SHI_N * S.sq.hcap, st);
         S.sq.hr = ns > 1 ? wbuf<uint64_t>(c, W_SQ_HR, 2 * S.sq.hcap, st) : nullptr;
-        S.sq.ql = ns > 1 ? wbuf<int32_t>(c, W_SQ_QL, 2 * S.sq.cap, st) : nullptr;
+        S.sq.ql = ns > 1 ? wbuf<int32_t>(c, W_SQ_QL, SHQ_CLASSES * S.sq.cap, st) : nullptr;
     }
     S.p_rgb = wbuf<double>(c, W_P_RGB, 3 * (size_t)N, st);
     S.p_valid = wbuf<uint32_t>(c, W_P_VALID, NV, st);

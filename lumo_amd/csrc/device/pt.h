@@ -340,7 +340,7 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) vo
     if (NS1) {
         for (int b = 0; b < NB; ++b) count += S.counts[CNT_BUCKET0 + b];
     } else {
-        count = S.counts[CNT_SHQ];
+        for (int k = 0; k < SHQ_CLASSES; ++k) count += S.counts[CNT_SHQ + k];
     }
     if (count <= blockIdx.x * blockDim.x) return;
     const DScene sc = LDS == 1 ? stage_scene_lds(sc0, lds_scene) : (LDS == 2 ? stage_top_lds(sc0, lds_scene) : sc0);
@@ -349,7 +349,10 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) vo
     if constexpr (!NS1) {
         // static stride (one fetch atomic per wave on one counter cost more than the balance gained)
         for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
-            const int32_t qv = Q.ql[j];
+            uint32_t k = j;
+            int cl = 0;
+            for (uint32_t c; k >= (c = S.counts[CNT_SHQ + cl]); ++cl) k -= c;  // class list of query j
+            const int32_t qv = Q.ql[(size_t)cl * Q.cap + k];
             const size_t r = (size_t)(qv >> 1);
             const int which = qv & 1;  // 0: light-sampled record, 1: BSDF-sampled
             const int b = which ? SD_BO : SD_LO;
@@ -440,6 +443,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_NEE_WAVES) void k_nee_gen(DScene sc, Pa
         const uint32_t j = j0 + threadIdx.x;
         size_t r = 0;
         bool live_l = false, live_b = false;
+        int env = 0;  // the pair's light is the environment
         if (j < count) {
         // light sample i of the bucket-ordered path k: pairs are stored light-sample-major
         // (r = i * hcap + p), so a wave's lanes take consecutive paths with the same i (coalesced
@@ -469,11 +473,19 @@ __global__ __launch_bounds__(BLOCK, LUMO_NEE_WAVES) void k_nee_gen(DScene sc, Pa
         live_l = !LUMO_SKIP_DEAD || sq.D(SD_LPS, r) != 0.0;
         live_b = ok && (!LUMO_SKIP_DEAD || sq.D(SD_BPS, r) != 0.0);
         dead += (live_l ? 0u : 1u) + (ok && !live_b ? 1u : 0u);
+        if (LUMO_SHQ_CLASSES) env = sc.lights[sq.I(SI_LIGHT, r)].type == LUMO_OBJ_SPHERE ? 1 : 0;
         }
-        const int n = (live_l ? 1 : 0) + (live_b ? 1 : 0);
-        const uint32_t pos = block_slot2(n, S.counts + CNT_SHQ);
-        if (live_l) sq.ql[pos] = (int32_t)(2 * r);
-        if (live_b) sq.ql[pos + (live_l ? 1u : 0u)] = (int32_t)(2 * r + 1);
+        if (LUMO_SHQ_CLASSES) {  // lists (L, other), (L, env), (B, other), (B, env)
+            const uint32_t pl = block_slot_bucket(live_l, env, S.counts + CNT_SHQ);
+            const uint32_t pb = block_slot_bucket(live_b, 2 + env, S.counts + CNT_SHQ);
+            if (live_l) sq.ql[(size_t)env * sq.cap + pl] = (int32_t)(2 * r);
+            if (live_b) sq.ql[(size_t)(2 + env) * sq.cap + pb] = (int32_t)(2 * r + 1);
+        } else {
+            const int n = (live_l ? 1 : 0) + (live_b ? 1 : 0);
+            const uint32_t pos = block_slot2(n, S.counts + CNT_SHQ);
+            if (live_l) sq.ql[pos] = (int32_t)(2 * r);
+            if (live_b) sq.ql[pos + (live_l ? 1u : 0u)] = (int32_t)(2 * r + 1);
+        }
     }
     if (LUMO_SKIP_DEAD) flush_resolved(dead, S.tcount + TC_RESOLVED);
 }

@@ -57,7 +57,14 @@ static_assert(ST_COUNT == LUMO_STAGE_COUNT, "stage slots match lumo_stats");
 // CNT_FETCH_*: work counters from which the kernels' waves / blocks take their next paths
 // (dynamic load balance; k_bounce_begin zeroes them every bounce).
 // CNT_SHQ: visibility queries of the bounce (n_shadow > 1: the NEE records that need a walk).
-enum { CNT_NEXT = 0, CNT_FETCH_B, CNT_FETCH_C, CNT_FETCH_T, CNT_CUR, CNT_BUCKET0, CNT_SHQ = CNT_BUCKET0 + 8, CNT_N };
+// The visibility queries go to SHQ_CLASSES lists by (record, light): L / B record x environment /
+// other light (LUMO_SHQ_CLASSES; 0: one list), so a wave's walks are of one kind.
+#ifndef LUMO_SHQ_CLASSES
+#define LUMO_SHQ_CLASSES 1
+#endif
+constexpr int SHQ_CLASSES = 4;
+enum { CNT_NEXT = 0, CNT_FETCH_B, CNT_FETCH_C, CNT_FETCH_T, CNT_CUR, CNT_BUCKET0, CNT_SHQ = CNT_BUCKET0 + 8,
+       CNT_N = CNT_SHQ + SHQ_CLASSES };
 // k_shade_q files each path's NEE records into one of NB buckets by the shadow rays' origin
 // object (objects, then lights, mod NB), each bucket a contiguous segment of the record queue, so
 // that a wave's visibility queries start on the same surface and walk the same BVH / kd nodes.
