@@ -209,7 +209,9 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
 
     out = None
     if rank == 0:
-        roof = roofline(st, n_shadow_rays(scene), bdpt=bdpt, workload=config, elapsed=elapsed, busy=busy)
+        # a rank's share launches fewer paths per pass: its own PMC entry when one was profiled
+        wkey = f"{config}_share" if share and pmc_traffic(f"{config}_share", "source") else config
+        roof = roofline(st, n_shadow_rays(scene), bdpt=bdpt, workload=wkey, elapsed=elapsed, busy=busy)
         cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl) if (args.cpu_baseline and ws == 1) else None
         out = {
             "metric": "Mrays/s",
@@ -395,7 +397,8 @@ def n_shadow_rays(scene):
 
 
 def pmc_traffic(workload, kernel):
-    """HBM bytes per launch of `kernel` for `workload` from the committed rocprofv3 PMC summary."""
+    """HBM bytes per launch of `kernel` for `workload` from the committed rocprofv3 PMC summary
+    (kernel "source": the entry's provenance string, i.e. whether the workload was profiled)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU call that checks and measures the tree: the GPU test suite, the C1 line (3 frames), one C3
 # frame, C2 at 4 spp, C4 at 8 spp, the fused kernel's phase clocks (diagnostics build, if built), one C1 1/8-share frame set
-# and its kernel-trace occupancy.  Every step has its own time limit; the chain stops at the first
+# and its kernel-trace occupancy; with MEASURE_DEFAULT=1 also the default bench line (C1 + C3 + CPU baselines).  Every step has its own time limit; the chain stops at the first
 # failure.  Usage (on the GPU box, repo root): bash tools/measure.sh <tag>
 set -o pipefail
 TAG=${1:-measure}
@@ -11,6 +11,7 @@ R=$(pwd)
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 &&
 tail -2 $OUT/pytest.log &&
 timeout -k 10 200 python3 bench.py --steps 3 --warmup 1 --bistro-frames 0 --cpu-baseline 0 > $OUT/c1.json 2> $OUT/c1.err &&
+{ [ -z "$MEASURE_DEFAULT" ] || timeout -k 10 600 python3 bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err; } &&
 timeout -k 10 200 python3 bench.py --config c3 --steps 1 --warmup 0 --cpu-baseline 0 > $OUT/c3.json 2> $OUT/c3.err &&
 timeout -k 10 200 python3 bench.py --config c2 --spp 4 --steps 2 --warmup 1 --cpu-baseline 0 > $OUT/c2.json 2> $OUT/c2.err &&
 timeout -k 10 200 python3 bench.py --config c4 --spp 8 --steps 1 --warmup 1 --cpu-baseline 0 > $OUT/c4.json 2> $OUT/c4.err &&
@@ -22,6 +23,7 @@ SWEEP_TAG=$TAG timeout -k 10 300 bash tools/share_sweep.sh base &&
    -o run -- python3 $R/bench.py --share 0/8 --steps 1 --warmup 1 --bistro-frames 0 --cpu-baseline 0 \
    > $R/$OUT/share_trace.json 2> $R/$OUT/share_trace.err) &&
 python3 tools/stream_busy.py $OUT/share_trace/run_kernel_trace.csv > $OUT/share_busy.json &&
+rm -rf $OUT/share_trace &&
 python3 - $OUT <<'PY'
 import json, sys
 o = sys.argv[1]
