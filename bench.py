@@ -450,10 +450,14 @@ def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl):
     runs = []
     # stride for 16 threads at ~8 s (measured per config), scaled to the thread count
     base_stride = wl.get("cpu_tile_stride", 32)
+    space = [i for i in range(len(tasks)) if batches is None or i // tiles < batches]
     for threads in sorted({info["usable"], LUMO_DEFAULT_THREADS}, reverse=True):
-        stride = max(1, int(round(base_stride * 16 / threads * 8.0 / args.cpu_seconds))) | 1  # odd: all columns
-        sample = [t for i, t in enumerate(tasks)
-                  if (i % tiles) % stride == 0 and (batches is None or i // tiles < batches)]
+        stride = max(1, int(round(base_stride * 16 / threads * 8.0 / args.cpu_seconds))) | 1
+        # a whole number of tasks per thread (at least one each: a thread without a tile would
+        # understate the host), evenly spaced over the frame's tiles
+        n = max(threads, -(-(-(-len(space) // stride)) // threads) * threads)
+        n = min(n, len(space))
+        sample = [tasks[space[(k * len(space)) // n]] for k in range(n)]
         times = []
         for _ in range(CPU_REPEATS):  # the host is shared: the median of repeated runs, with their spread
             t0 = time.perf_counter()
@@ -466,8 +470,8 @@ def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl):
         runs.append({"threads": threads, "value": round(q / dt / 1e6, 4), "msamples_per_s": round(paths / dt / 1e6, 4),
                      "seconds": round(dt, 2), "repeats": len(times),
                      "value_min": round(q / max(times) / 1e6, 4), "value_max": round(q / min(times) / 1e6, 4),
-                     "sample": f"{len(sample)} tasks = every {stride}th 16x16 tile of "
-                               f"{'each' if batches is None else f'the first {batches}'} 256-spp batch(es) of "
+                     "sample": f"{len(sample)} 16x16 tiles evenly spaced over "
+                               f"{'all' if batches is None else f'the first {batches}'} 256-spp batch(es) of "
                                f"the {W}x{H} @ {spp} spp frame ({paths} paths), lumo tile-serial RNG order"})
     best = runs[0]
     return {"value": best["value"], "unit": "Mrays/s", "cores": best["threads"], "kind": "port",
