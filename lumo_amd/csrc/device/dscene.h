@@ -320,11 +320,40 @@ __device__ __forceinline__ double luminance(const DScene& sc, const DColor& c, c
     const DColor pdf = wl_pdf(L);
     return cmean(dense_sample(sc.dense + 95 * 1, L) * c / pdf) / Y_INTEGRAL;
 }
+// dense_one of three consecutive 95-entry tables (the CIE x, y, z curves) at one wavelength: the
+// bin and weights computed once, each value exactly dense_one's.
+__device__ __forceinline__ void dense_three(const double* v, double lambda, double* out) {
+    const double STEP = (830.0 - 360.0) / (95.0 - 1.0);
+    const double fb = ceil((lambda - 360.0) / STEP);
+    int b1 = fb > 0.0 ? (int)fmin(fb, 1e9) : 0;
+    const double l1 = 360.0 + STEP * (double)b1;
+    if (lambda == 0.0) {
+        out[0] = out[1] = out[2] = 0.0;
+        return;
+    }
+    if (b1 > 94) b1 = 94;
+    if (lambda == l1) {
+        for (int k = 0; k < 3; ++k) out[k] = v[95 * k + b1];
+        return;
+    }
+    const int b0 = b1 == 0 ? 0 : b1 - 1;
+    const double l0 = l1 - STEP;
+    const double x1 = (lambda - l0) / STEP;
+    const double x0 = 1.0 - x1;
+    for (int k = 0; k < 3; ++k) out[k] = v[95 * k + b0] * x0 + v[95 * k + b1] * x1;
+}
 __device__ __forceinline__ V3 color_xyz(const DScene& sc, const DColor& c, const double* L) {
     const DColor pdf = wl_pdf(L);
-    return V3{cmean(dense_sample(sc.dense, L) * c / pdf), cmean(dense_sample(sc.dense + 95, L) * c / pdf),
-              cmean(dense_sample(sc.dense + 190, L) * c / pdf)} /
-           Y_INTEGRAL;
+    DColor cx, cy, cz;  // dense_sample of the x, y, z curves
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        double o[3];
+        dense_three(sc.dense, L[i], o);
+        cx.s[i] = o[0];
+        cy.s[i] = o[1];
+        cz.s[i] = o[2];
+    }
+    return V3{cmean(cx * c / pdf), cmean(cy * c / pdf), cmean(cz * c / pdf)} / Y_INTEGRAL;
 }
 
 // ---------------------------------------------------------------- textures (texture.rs, image.rs, perlin.rs)

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -467,6 +468,35 @@ __global__ __launch_bounds__(BLOCK) void k_film(Paths S, Tasks T, DCam cam, int 
     film_gather(S, T.t[ti], cam, s, S.pix[s], HbmSrc{S, T.first[ti]});
 }
 
+// film_gather_acc with the source terms staged (r <= FILM_R): source k's footprint origin
+// (ox, oy) = (px - r, py - r) relative to the tile, precomputed once per source (INT_MIN/4 for an
+// invalid sample), so destination (dx, dy) takes source k iff 0 <= dx - ox <= 2r and
+// 0 <= dy - oy <= 2r: the tile-clipped [px - r, px + r] test of film_gather_acc for destinations
+// inside the tile.  Same sources in the same order, same weights and additions.
+__device__ __forceinline__ void film_gather_staged(double* acc, const lumo_tile_task& t, int j, const double* rgb,
+                                                   const int* l_ox, const int* l_oy, const FilmTerms& terms) {
+    const int W = (int)(t.px_max[0] - t.px_min[0]), H = (int)(t.px_max[1] - t.px_min[1]);
+    const int dx = j % W, dy = j / W;
+    const unsigned r2 = 2u * (unsigned)terms.r;
+    for (int sy = dy - 2; sy <= dy + 1; ++sy) {
+        if (sy < 0 || sy >= H) continue;
+        for (int sx = dx - 2; sx <= dx + 1; ++sx) {
+            if (sx < 0 || sx >= W) continue;
+            const int k = sy * W + sx;
+            const unsigned ix = (unsigned)(dx - l_ox[k]), iy = (unsigned)(dy - l_oy[k]);
+            if (ix > r2 || iy > r2) continue;
+            const double w = terms.wx[(int)ix * BLOCK + k] * terms.wy[(int)iy * BLOCK + k];
+            if (w != 0.0) {
+                const V3 c = V3{rgb[3 * k], rgb[3 * k + 1], rgb[3 * k + 2]} * w;
+                acc[0] += c.x;
+                acc[1] += c.y;
+                acc[2] += c.z;
+                acc[3] += w;
+            }
+        }
+    }
+}
+
 struct LdsSrc {  // sources staged in LDS by k_finish_film
     const double* rgb_;
     const double* ras;
@@ -491,6 +521,7 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S0, Task
     __shared__ double l_ras[2 * BLOCK];
     __shared__ uint32_t l_ok[BLOCK];
     __shared__ double l_wx[(2 * FILM_R + 1) * BLOCK], l_wy[(2 * FILM_R + 1) * BLOCK];
+    __shared__ int l_ox[BLOCK], l_oy[BLOCK];  // staged terms: each source's footprint origin in the tile
     const int ti = t0 + (int)blockIdx.x;  // tasks [t0, t0 + gridDim.x)
     const int first = T.first[ti];
     const int P = T.first[ti + 1] - first;
@@ -506,6 +537,7 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S0, Task
         if (j < P) {
             const bool ok = S.p_valid[s] != 0;
             l_ok[j] = ok ? 1u : 0u;
+            l_ox[j] = l_oy[j] = INT_MIN / 4;
             if (ok) {
                 const V3 rgb = finish_one(sc, S, cam, s, pass0 + (uint32_t)m, dump, dump_p, tone_map, tone_arg);
                 l_rgb[3 * j] = rgb.x;
@@ -517,6 +549,8 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S0, Task
                 if (pre) {  // this sample's column / row terms, as film_gather computes them
                     const double gr = gauss(cam.fr, cam.fsig);
                     const int64_t px = rx > 0.0 ? (int64_t)floor(rx) : 0, py = ry > 0.0 ? (int64_t)floor(ry) : 0;
+                    l_ox[j] = (int)(px - r - (int64_t)T.t[ti].px_min[0]);
+                    l_oy[j] = (int)(py - r - (int64_t)T.t[ti].px_min[1]);
                     for (int i = 0; i <= 2 * r; ++i) {
                         const double gx = (double)(px - r + i), gy = (double)(py - r + i);
                         l_wx[i * BLOCK + j] = rmax(gauss(rx - (0.5 + gx), cam.fsig) - gr, 0.0);
@@ -528,7 +562,12 @@ __global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S0, Task
         __syncthreads();
         count_checks(j < P && l_ok[j] ? sample_check(ldc(S.rad, s)) : 0, S.checks);
         const FilmTerms terms{l_wx, l_wy, r};
-        if (j < P) film_gather_acc(acc, T.t[ti], cam, j, LdsSrc{l_rgb, l_ras, l_ok}, pre ? &terms : nullptr);
+        if (j < P) {
+            if (pre)
+                film_gather_staged(acc, T.t[ti], j, l_rgb, l_ox, l_oy, terms);
+            else
+                film_gather_acc(acc, T.t[ti], cam, j, LdsSrc{l_rgb, l_ras, l_ok});
+        }
         __syncthreads();  // the next pass overwrites the staged samples
     }
     if (j < P)
