@@ -412,6 +412,9 @@ enum {
                                   (LUMO_TAIL_BOUNCES, -1)                                           */
     LUMO_OPT_FILM_FIRST,       /* fused pipeline, film on the tail stream: the unit's film before its
                                   last ring: 0 / 1 (LUMO_FILM_FIRST, 0)                             */
+    LUMO_OPT_BDPT_TOP,         /* BDPT connection visibility (k_bdpt_vis) of scenes too large to stage
+                                  whole reads the TOP set and kd stack columns from LDS: 0 / 1
+                                  (LUMO_BDPT_TOP, 1)                                                */
     LUMO_OPT_COUNT
 };
 lumo_status lumo_set_option(void* ctx, int32_t option, int64_t value);

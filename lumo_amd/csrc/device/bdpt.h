@@ -531,15 +531,17 @@ __device__ double mis_weight(const DScene& sc, const DCam& cam, const double* L,
 }
 
 // bd_path_trace.rs:279-290: visible() tests with Scene::hit_t (any-hit first, objects then lights)
-template <int STK, int FX>
+template <int STK, int FX, bool TOP = false>
 __device__ bool bdpt_visible(const DScene& sc, const BVtx& a, const BVtx& b, Counters& C) {
     const V3 xo = a.p, xi = b.p;
     const Ray ri = spawn(vtx_hit(a), xi - xo);
     if (dot(ri.d, a.ng) < EPSILON) return false;
     const RayX rx = rayx(ri);
     double t = DINF;
-    t = rmin(t, bvh_hit_t<STK, FX>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, rx, 0.0, t, C));
-    t = rmin(t, bvh_hit_t<STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, rx, 0.0, t, C));
+    t = rmin(t, bvh_hit_t<STK, FX, TOP>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, rx, 0.0, t, C, sc.onodes_lds,
+                                        sc.n_onodes_lds));
+    t = rmin(t, bvh_hit_t<STK, FX, TOP>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, rx, 0.0, t, C, sc.lnodes_lds,
+                                        sc.n_lnodes_lds));
     return fabs(sqrt(rmax(distance_squared(xo, xi), 0.0)) - t) < EPSILON;
 }
 
@@ -896,15 +898,14 @@ __global__ __launch_bounds__(BLOCK, LUMO_BDPT_STEP_WAVES) void k_bdpt_step(DScen
 // fetch atomic per wave and round).  The two kernels, given the same threshold, skip the bounce;
 // the next queue stays empty, so the host's bounce loop ends.  Bit-identical: a walk does not
 // depend on other walks.  The closest queries after each subpath's first are added to TC_TAILQ.
-template <int STK, bool LDS, int FX>
-__global__ __launch_bounds__(BLOCK, LUMO_BDPT_STEP_WAVES) void k_bdpt_tail(DScene sc0, Paths S, Tasks T, Bdpt B,
-                                                                       BItems I, int mode, const int32_t* queue,
-                                                                       uint32_t tail_below) {
+template <int STK, int LDS, int FX>
+__global__ __launch_bounds__(BLOCK, LUMO_BDPT_STEP_WAVES) void k_bdpt_tail(
+    DScene sc0, Paths S, Tasks T, Bdpt B, BItems I, int mode, const int32_t* queue, uint32_t tail_below) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
     if (count >= tail_below) return;  // the bounce kernels take this bounce
     if (count <= blockIdx.x * blockDim.x) return;  // before staging: whole block idle
-    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    const DScene sc = LDS == 1 ? stage_scene_lds(sc0, lds_scene) : (LDS == 2 ? stage_top_lds(sc0, lds_scene) : sc0);
     Counters C{0, 0, 0};
     uint32_t tailq = 0;
     int slot = -1;
@@ -932,7 +933,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_BDPT_STEP_WAVES) void k_bdpt_tail(DScen
         if (__ballot(have) == 0) break;
         if (have) {
             const RayX r = rayx(Ray{ldv3(S.ro, slot), ldv3(S.rd, slot)});  // k_closest
-            const HitRef h = scene_hit<STK, FX>(sc, r, C);
+            const HitRef h = scene_hit<STK, FX, LDS == 2>(sc, r, C);
             S.hit_t[slot] = h.t;
             S.hit_kind[slot] = h.kind;
             S.hit_obj[slot] = h.obj;
@@ -1034,13 +1035,13 @@ __device__ __forceinline__ ItemSel item_store(const Bdpt& B, const Bdpt& R, int 
 // (a) items, traversal part: the camera ray of each t = 1 connection and the light ray of each
 // s = 1 connection, traced whenever the ray exists (before lumo's BSDF-pdf guards, which
 // k_bdpt_eval_a evaluates; a ray the guards reject is never read and not counted as a query).
-template <int STK, bool LDS, int FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_trace_a(DScene sc0, Paths S, DCam cam, Bdpt B, Bdpt R,
-                                                                           BItems I, int n, const uint32_t* totals) {
+template <int STK, int LDS, int FX>
+__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_trace_a(
+    DScene sc0, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n, const uint32_t* totals) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t total = totals[0];
     if (total <= blockIdx.x * blockDim.x) return;
-    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    const DScene sc = LDS == 1 ? stage_scene_lds(sc0, lds_scene) : (LDS == 2 ? stage_top_lds(sc0, lds_scene) : sc0);
     Counters C{0, 0, 0};
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
         const int slot = item_slot(I.off_a, n, q);
@@ -1056,7 +1057,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_trace_a(DScen
                 const V3 xi{X.lp.D(0, s - 1, si), X.lp.D(1, s - 1, si), X.lp.D(2, s - 1, si)};
                 Ray ri;
                 if (cam_sample_towards(cam, xi, V2{X.Dr(0, s - 2, si), X.Dr(1, s - 2, si)}, &ri))
-                    hr = scene_hit<STK, FX>(sc, rayx(ri), C);
+                    hr = scene_hit<STK, FX, LDS == 2>(sc, rayx(ri), C);
             }
         } else if (j > (uint32_t)(Sl - 1)) {
             const int t = (int)j - Sl + 2;
@@ -1064,7 +1065,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_trace_a(DScen
             if (!(cl.del || cl.light >= 0)) {
                 const int li = sample_light(sc, X.Dr(2, t - 2, si));
                 const V3 wi = light_sample_towards<FX>(sc, sc.lights[li], cl.p, V2{X.Dr(3, t - 2, si), X.Dr(4, t - 2, si)});
-                hr.tri = scene_hit_light_tri<STK, FX>(sc, rayx(spawn(vtx_hit(cl), wi)), li, C);
+                hr.tri = scene_hit_light_tri<STK, FX, LDS == 2>(sc, rayx(spawn(vtx_hit(cl), wi)), li, C);
             }
         }
         I.a_t[q] = hr.t;
@@ -1131,13 +1132,13 @@ __device__ __forceinline__ void item_b_st(const BItems& I, int slot, uint32_t q,
 }
 
 // bdpt_visible of every (b) item whose guard reaches it (bd_path_trace.rs:279-290)
-template <int STK, bool LDS, int FX>
-__global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_vis(DScene sc0, Paths S, Bdpt B, Bdpt R, BItems I,
-                                                                       int n, const uint32_t* totals) {
+template <int STK, int LDS, int FX>
+__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_vis(
+    DScene sc0, Paths S, Bdpt B, Bdpt R, BItems I, int n, const uint32_t* totals) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t total = totals[1];
     if (total <= blockIdx.x * blockDim.x) return;
-    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    const DScene sc = LDS == 1 ? stage_scene_lds(sc0, lds_scene) : (LDS == 2 ? stage_top_lds(sc0, lds_scene) : sc0);
     Counters C{0, 0, 0};
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
         const int slot = item_slot(I.off_b, n, q);
@@ -1157,7 +1158,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_vis(DScene sc
             a.mat = 0;
             a.backface = false;
             b.p = V3{cv.D(0, t - 1, e.si), cv.D(1, t - 1, e.si), cv.D(2, t - 1, e.si)};
-            vis = bdpt_visible<STK, FX>(sc, a, b, C);
+            vis = bdpt_visible<STK, FX, LDS == 2>(sc, a, b, C);
         }
         I.vis[q] = vis ? 1 : 0;
     }

@@ -31,6 +31,21 @@ void launch_bdpt_step(int grid, hipStream_t sm, int fx, const DScene& sc, const 
         }                                                                                    \
     } while (0)
 
+// ... and, for kernels with a TOP variant (LDS mode 2: scenes too large to stage whole, fx 0 / 1),
+// `TB` threads per block with the TOP set (and the kd stack columns) in `l.shm` bytes of LDS.
+// Only the (b)-item visibility has one: TOP variants of the walk (k_closest), the walk tail and
+// the (a)-item traces were slower on C4 (the tail 150 -> 239 ms per 8-spp frame, (a) traces
+// 177 -> 191 ms), while the visibility went 200 -> 85 ms.
+#define LUMO_TRAV_LAUNCH_TOP(KERNEL, TB, ...)                                                 \
+    do {                                                                                     \
+        if (l.top && l.fx != 2) {                                                            \
+            if (l.fx) KERNEL<STK, 2, 1><<<l.grid, TB, l.shm, l.sm>>>(__VA_ARGS__);           \
+            else KERNEL<STK, 2, 0><<<l.grid, TB, l.shm, l.sm>>>(__VA_ARGS__);               \
+        } else {                                                                             \
+            LUMO_TRAV_LAUNCH(KERNEL, __VA_ARGS__);                                           \
+        }                                                                                    \
+    } while (0)
+
 template <int STK>
 void launch_bdpt_tail(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const Bdpt& B,
                       const BItems& I, int mode, const int32_t* queue, uint32_t tail_below) {
@@ -52,7 +67,7 @@ void launch_bdpt_trace_a(const TravLaunch& l, const DScene& sc, const Paths& S, 
 template <int STK>
 void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, const Bdpt& B, const Bdpt& R,
                      const BItems& I, int n, const uint32_t* totals) {
-    LUMO_TRAV_LAUNCH(k_bdpt_vis, sc, S, B, R, I, n, totals);
+    LUMO_TRAV_LAUNCH_TOP(k_bdpt_vis, TOP_BLOCK, sc, S, B, R, I, n, totals);
 }
 
 template void launch_bdpt_step<LUMO_STK>(int, hipStream_t, int, const DScene&, const Paths&, const Tasks&,

@@ -815,6 +815,7 @@ struct Opts {
     int tail_priority = 0;             // the pipelined passes' tail / film / ring stream at high priority
     int top_kd = 1;                    // the TOP set's spare LDS holds the top treelets of the largest kd tree
     int tail_bounces = -1;             // fused pipeline: fused bounces per pass on the tail stream before the tail kernel (-1 auto)
+    int bdpt_top = 1;                  // BDPT connection visibility of large scenes with TOP staging
     int film_first = 0;                // fused pipeline, film on the tail stream: the film before the unit's last ring
 };
 
@@ -1011,8 +1012,8 @@ void by_stack_class(int cls, F&& f) {
 
 // Traversal launch: stack class x LDS staging.  With LDS staging the grid is capped (persistent
 // grid-stride loop) so each workgroup copies the packed scene once per launch.
-// allow_top: the kernel has a TOP-staged variant (k_closest_q, k_shadow_q); it is used when the
-// whole scene does not fit in LDS but its top levels were packed at upload (DScene::top).
+// allow_top: the kernel has a TOP-staged variant (k_closest_q, k_shadow_q, k_bdpt_vis); it is used
+// when the whole scene does not fit in LDS but its top levels were packed at upload (DScene::top).
 template <typename F>
 void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr, bool allow_top = false) {
     const bool lds = c.o.lds && c.sc.hot_bytes > 0;
@@ -1949,9 +1950,12 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             if (totals[1] > 0) {
                 {
                     StageTimer tm(c, c.o.timing, ST_BD_VIS);
-                    launch_trav(c, (uint64_t)totals[1], [&](auto K, const TravLaunch& l) {
-                        launch_bdpt_vis<decltype(K)::value>(l, c.sc, S, B, BR, BI, N, items_total);
-                    });
+                    launch_trav(
+                        c, (uint64_t)totals[1],
+                        [&](auto K, const TravLaunch& l) {
+                            launch_bdpt_vis<decltype(K)::value>(l, c.sc, S, B, BR, BI, N, items_total);
+                        },
+                        nullptr, c.o.bdpt_top != 0);
                 }
                 StageTimer tm(c, c.o.timing, ST_BD_PATHS);
                 const int grid = std::min(ceil_div(totals[1], BLOCK), 1 << 16);
@@ -2115,7 +2119,8 @@ const char* const kOptEnv[LUMO_OPT_COUNT] = {
     "LUMO_TIMING", "LUMO_LDS", "LUMO_TOP", "LUMO_FUSED", "LUMO_TAIL", "LUMO_PIPELINE", "LUMO_HEADS", "LUMO_MERGE",
     "LUMO_DYN", "LUMO_BOUNCE_THREADS", "LUMO_SPLIT_PIPE", "LUMO_SPLIT_GROUPS", "LUMO_BDPT_TAIL", "LUMO_BOUNCE_AHEAD",
     "LUMO_LDS_GRID", "LUMO_TOP_GRID", "LUMO_TOP_KB", "LUMO_KD_LDS", "LUMO_STACK_CLASS", "LUMO_FULL_KERNELS",
-    "LUMO_POISON", "LUMO_TAIL_PRIORITY", "LUMO_TOP_KD", "LUMO_TAIL_BOUNCES", "LUMO_FILM_FIRST"};
+    "LUMO_POISON", "LUMO_TAIL_PRIORITY", "LUMO_TOP_KD", "LUMO_TAIL_BOUNCES", "LUMO_FILM_FIRST",
+    "LUMO_BDPT_TOP"};
 
 void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
     lo = 0;
@@ -2193,6 +2198,7 @@ lumo_status set_opt(Ctx& c, int k, int64_t v) {
         case LUMO_OPT_TOP_KD: o.top_kd = iv; break;
         case LUMO_OPT_TAIL_BOUNCES: o.tail_bounces = iv; break;
         case LUMO_OPT_FILM_FIRST: o.film_first = iv; break;
+        case LUMO_OPT_BDPT_TOP: o.bdpt_top = iv; break;
         case LUMO_OPT_TAIL_PRIORITY:
             if (iv != o.tail_priority) {
                 const lumo_status e = make_tail_stream(c, iv);
@@ -2233,6 +2239,7 @@ int64_t get_opt(const Ctx& c, int k) {
         case LUMO_OPT_TOP_KD: return o.top_kd;
         case LUMO_OPT_TAIL_BOUNCES: return o.tail_bounces;
         case LUMO_OPT_FILM_FIRST: return o.film_first;
+        case LUMO_OPT_BDPT_TOP: return o.bdpt_top;
         default: return 0;
     }
 }

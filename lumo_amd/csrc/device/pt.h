@@ -9,19 +9,21 @@ namespace lumo {
 namespace dev {
 
 // ------------------------------------------------------------------ closest hit
-template <int STK, bool LDS, int FX>
-__global__ __launch_bounds__(BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc0, Paths S, const int32_t* queue,
-                                                                              uint32_t tail_below) {
+// LDS: 0 scene in HBM, 1 whole scene staged, 2 TOP staging (TOP_BLOCK threads per block).
+template <int STK, int LDS, int FX>
+__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc0, Paths S,
+                                                                                             const int32_t* queue,
+                                                                                             uint32_t tail_below) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
     if (count < tail_below) return;  // k_bdpt_tail took this bounce
     if (count <= blockIdx.x * blockDim.x) return;  // before staging: whole block idle
-    const DScene sc = LDS ? stage_scene_lds(sc0, lds_scene) : sc0;
+    const DScene sc = LDS == 1 ? stage_scene_lds(sc0, lds_scene) : (LDS == 2 ? stage_top_lds(sc0, lds_scene) : sc0);
     Counters C{0, 0, 0};
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < count; q += gridDim.x * blockDim.x) {
         const int s = queue[q];
         const RayX r = rayx(Ray{ldv3(S.ro, s), ldv3(S.rd, s)});
-        const HitRef h = scene_hit<STK, FX>(sc, r, C);
+        const HitRef h = scene_hit<STK, FX, LDS == 2>(sc, r, C);
         S.hit_t[s] = h.t;
         S.hit_kind[s] = h.kind;
         S.hit_obj[s] = h.obj;

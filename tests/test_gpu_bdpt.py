@@ -76,6 +76,33 @@ def test_bdpt_tiles_and_splats(dev, name, res, spp, tail):
         np.testing.assert_array_equal(s["rgb"], os_["rgb"])
 
 
+@pytest.mark.parametrize("top", [0, 1])
+def test_bdpt_top_visibility_matches_oracle(dev, top):
+    """The caustics scene does not fit in LDS whole (two ~1k-triangle kd meshes), so its TOP set
+    (BVH, object records, the largest kd tree's top treelets) is packed at upload and the (b)-item
+    visibility kernel reads it and its kd stack from LDS (option bdpt_top, default 1); with or
+    without it every tile, count and splat equals the oracle's."""
+    sc, cam = _scene("caustics", (48, 32))
+    sc.build()
+    dev.upload(sc, cam)
+    info = dev.scene_info()
+    assert info.lds_bytes == 0 and info.top_bytes > 0 and info.top_kd_nodes > 0
+    tasks = L.make_tasks(48, 32, 4, 0x70B)
+    sp = []
+    dev.set_option("bdpt_top", top)
+    try:
+        bufs, rr = dev.render_tasks(tasks, integrator=BDPT, splats_out=sp)
+    finally:
+        dev.set_option("bdpt_top", 1)
+    osp = []
+    obufs, orr, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8, integrator=BDPT, splats_out=osp)
+    assert sum(len(s) for s in osp) > 0
+    for b, ob, r, o, s, os_ in zip(bufs, obufs, rr, orr, sp, osp):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries, r.num_camera_rays) == (o.num_rays, o.num_queries, o.num_camera_rays)
+        np.testing.assert_array_equal(s["rgb"], os_["rgb"])
+
+
 def test_bdpt_long_subpaths_are_rerun(dev):
     """max_vertices = 3 sends almost every sample through the redo kernel (storage for lumo's
     1024-bounce maximum); the results must not change."""
