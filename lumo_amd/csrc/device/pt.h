@@ -153,7 +153,7 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
         const uint32_t q = base + threadIdx.x;
         const bool live = q < count;
-        int slot = 0, task = 0, key = 0, origin = 0;
+        int slot = 0, task = 0, key = 0;
         uint32_t depth = 0, flags = 0, queries = 0;
         double L[NS] = {0.0, 0.0, 0.0, 0.0};
         DColor gathered = cfill(0.0), radiance = cfill(0.0);
@@ -188,12 +188,14 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
                     if (flags & QF_SPECULAR) radiance = radiance + gathered * emit<FX>(sc, m, L, ho.backface, ho.uv);
                 } else {
                     resolve = !mat_is_delta<FX>(sc, m, L);
-                    origin = kind == 2 ? sc.n_objs + hr.obj : hr.obj;  // objects, then lights
-                    if (resolve) key = origin % NB;                   // bucket of the shadow rays
+                    // the NEE pairs' bucket: the material kind, so k_nee_gen's waves (and their
+                    // visibility queries) run one BSDF's code (C3 8-spp frame 593 -> 554 ms; by
+                    // origin object, round 2: no gain)
+                    if (resolve) key = m.kind % NB;
                 }
             }
         }
-        // NEE records (integrator.rs:87-137), filed into the bucket of the origin object
+        // NEE records (integrator.rs:87-137), filed into the bucket of the material kind
         const uint32_t sp = key * sq.seg + block_slot_bucket(resolve, key, S.counts + CNT_BUCKET0);
         if (resolve) {
             uint32_t n_sh = 0;
