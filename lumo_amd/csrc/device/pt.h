@@ -134,6 +134,55 @@ __device__ __forceinline__ bool nee_pair(const DScene& sc, const ShadowQ& sq, si
 }
 constexpr int NEE_DRAWS = 6;  // RNG draws per pair in nee_pair
 
+// Material of a closest hit without its record: the triangle's (a sphere's, the object's), or the
+// instance's override (object_record / instance_fix_hit).
+__device__ __forceinline__ int hit_material(const DScene& sc, int kind, int obj, int tri) {
+    const lumo_object& ob = kind == 1 ? sc.objs[obj] : sc.lights[obj];
+    int mat = ob.type == LUMO_OBJ_SPHERE ? ob.material : sc.tris[tri].material;
+    if (ob.xform >= 0 && ob.material_override >= 0) mat = ob.material_override;
+    return mat;
+}
+// This thread's queue entry for one block round of k_shade_q: the round's entries [base, base +
+// blockDim.x) ordered by their hit's material kind (stable within a kind); count if none is left.
+// Every thread of the block must call it.
+__device__ __forceinline__ uint32_t block_by_material(const DScene& sc, const HitQ& hq, uint32_t base, uint32_t count) {
+    constexpr int NK = 8, NW = BLOCK / 64;
+    __shared__ uint32_t cnt[NK][NW];
+    __shared__ uint32_t order[BLOCK];
+    const uint32_t q0 = base + threadIdx.x;
+    const bool live = q0 < count;
+    int k = 0;
+    if (live) {
+        const int kind = hq.i[q0];
+        if (kind != 0) k = 1 + sc.mats[hit_material(sc, kind, hq.i[hq.cap + q0], hq.i[2 * hq.cap + q0])].kind % (NK - 1);
+    }
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t rank = 0;
+#pragma unroll
+    for (int b = 0; b < NK; ++b) {
+        const uint64_t m = __ballot(live && k == b);
+        if (live && k == b) rank = mbcnt64(m);
+        if (lane == 0) cnt[b][w] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive scan over (kind, wave)
+        uint32_t t = 0;
+        for (int b = 0; b < NK; ++b)
+            for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+                const uint32_t c = cnt[b][i];
+                cnt[b][i] = t;
+                t += c;
+            }
+    }
+    __syncthreads();
+    const uint32_t rem = count > base ? count - base : 0u, n = rem < blockDim.x ? rem : blockDim.x;
+    if (live) order[cnt[k][w] + rank] = q0;
+    __syncthreads();
+    const uint32_t q = threadIdx.x < n ? order[threadIdx.x] : count;
+    __syncthreads();  // the next round rewrites order / cnt
+    return q;
+}
+
 // The bounce of every queued path (path_trace.rs:18-77): the pending NEE term of the previous
 // bounce, the hit record, emission, BSDF sample, the NEE records of integrator.rs:87-137
 // (n_shadow x [light pick, light direction, BSDF sample]), the continuation and Russian
@@ -151,7 +200,10 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
     const ShadowQ sq = S.sq;
     // grid-stride over whole blocks: the block collectives need every thread of the block each round
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
-        const uint32_t q = base + threadIdx.x;
+        // the block's paths taken in order of their hit's material kind (misses first), so a
+        // wave shades with one BSDF's code; which thread takes which path changes nothing else
+        // (C2 4-spp frame 343 -> 336 ms, C3 within noise)
+        const uint32_t q = block_by_material(sc, hq, base, count);
         const bool live = q < count;
         int slot = 0, task = 0, key = 0;
         uint32_t depth = 0, flags = 0, queries = 0;
