@@ -529,19 +529,14 @@ __global__ __launch_bounds__(BLOCK, LUMO_NEE_WAVES) void k_nee_gen(DScene sc, Pa
         live_l = !LUMO_SKIP_DEAD || sq.D(SD_LPS, r) != 0.0;
         live_b = ok && (!LUMO_SKIP_DEAD || sq.D(SD_BPS, r) != 0.0);
         dead += (live_l ? 0u : 1u) + (ok && !live_b ? 1u : 0u);
-        if (LUMO_SHQ_CLASSES) env = sc.lights[sq.I(SI_LIGHT, r)].type == LUMO_OBJ_SPHERE ? 1 : 0;
+        env = sc.lights[sq.I(SI_LIGHT, r)].type == LUMO_OBJ_SPHERE ? 1 : 0;
         }
-        if (LUMO_SHQ_CLASSES) {  // lists (L, other), (L, env), (B, other), (B, env)
-            const uint32_t pl = block_slot_bucket(live_l, env, S.counts + CNT_SHQ);
-            const uint32_t pb = block_slot_bucket(live_b, 2 + env, S.counts + CNT_SHQ);
-            if (live_l) sq.ql[(size_t)env * sq.cap + pl] = (int32_t)(2 * r);
-            if (live_b) sq.ql[(size_t)(2 + env) * sq.cap + pb] = (int32_t)(2 * r + 1);
-        } else {
-            const int n = (live_l ? 1 : 0) + (live_b ? 1 : 0);
-            const uint32_t pos = block_slot2(n, S.counts + CNT_SHQ);
-            if (live_l) sq.ql[pos] = (int32_t)(2 * r);
-            if (live_b) sq.ql[pos + (live_l ? 1u : 0u)] = (int32_t)(2 * r + 1);
-        }
+        // lists (L, other), (L, environment), (B, other), (B, environment)
+        const int kl = env, kb = 2 + env;
+        const uint32_t pl = block_slot_bucket(live_l, kl, S.counts + CNT_SHQ);
+        const uint32_t pb = block_slot_bucket(live_b, kb, S.counts + CNT_SHQ);
+        if (live_l) sq.ql[(size_t)kl * sq.cap + pl] = (int32_t)(2 * r);
+        if (live_b) sq.ql[(size_t)kb * sq.cap + pb] = (int32_t)(2 * r + 1);
     }
     if (LUMO_SKIP_DEAD) flush_resolved(dead, S.tcount + TC_RESOLVED);
 }

@@ -57,11 +57,9 @@ static_assert(ST_COUNT == LUMO_STAGE_COUNT, "stage slots match lumo_stats");
 // CNT_FETCH_*: work counters from which the kernels' waves / blocks take their next paths
 // (dynamic load balance; k_bounce_begin zeroes them every bounce).
 // CNT_SHQ: visibility queries of the bounce (n_shadow > 1: the NEE records that need a walk).
-// The visibility queries go to SHQ_CLASSES lists by (record, light): L / B record x environment /
-// other light (LUMO_SHQ_CLASSES; 0: one list), so a wave's walks are of one kind.
-#ifndef LUMO_SHQ_CLASSES
-#define LUMO_SHQ_CLASSES 1
-#endif
+// The visibility queries go to SHQ_CLASSES lists by (record, light): light- / BSDF-sampled record x
+// environment / other light, so a wave's walks are of one kind (splitting the other lights further
+// by light-index range: no gain).
 constexpr int SHQ_CLASSES = 4;
 enum { CNT_NEXT = 0, CNT_FETCH_B, CNT_FETCH_C, CNT_FETCH_T, CNT_CUR, CNT_BUCKET0, CNT_SHQ = CNT_BUCKET0 + 8,
        CNT_N = CNT_SHQ + SHQ_CLASSES };
@@ -241,30 +239,6 @@ __device__ __forceinline__ uint32_t block_slot_fetch(bool pred, uint32_t* counte
     __syncthreads();
     const uint32_t pos = base_s + wtot[w] + prefix;
     *next = next_s;
-    __syncthreads();
-    return pos;
-}
-// block_slot for up to two entries per thread (n = 0, 1 or 2): this thread's first position, its
-// entries at pos and pos + 1, in lane order.  Every thread of the block must call it.
-__device__ __forceinline__ uint32_t block_slot2(int n, uint32_t* counter) {
-    __shared__ uint32_t wtot[BLOCK / 64];
-    __shared__ uint32_t base_s;
-    const uint64_t m1 = __ballot(n >= 1), m2 = __ballot(n >= 2);
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-    const uint32_t prefix = mbcnt64(m1) + mbcnt64(m2);
-    if (lane == 0) wtot[w] = (uint32_t)(__popcll(m1) + __popcll(m2));
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
-            const uint32_t cnt = wtot[i];
-            wtot[i] = t;
-            t += cnt;
-        }
-        base_s = t ? atomicAdd(counter, t) : 0u;
-    }
-    __syncthreads();
-    const uint32_t pos = base_s + wtot[w] + prefix;
     __syncthreads();
     return pos;
 }
