@@ -375,7 +375,7 @@ enum {
     LUMO_OPT_FUSED,            /* n_shadow = 1: -1 fused bounce when LDS-staged, 0 three kernels,
                                   1 fused (LUMO_FUSED, -1)                                          */
     LUMO_OPT_TAIL_BELOW,       /* n_shadow = 1: tail kernel below this many live paths, 0 never
-                                  (LUMO_TAIL, 262144)                                               */
+                                  (LUMO_TAIL, 65536)                                               */
     LUMO_OPT_PIPELINE,         /* passes overlapped: 0 off, fused bounces 1-3 head streams, split
                                   schedule on when > 0 (LUMO_PIPELINE, 3)                            */
     LUMO_OPT_HEADS,            /* fused pipeline: bounces per pass on its head stream, 0 auto

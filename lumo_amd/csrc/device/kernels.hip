@@ -794,7 +794,8 @@ struct Opts {
     int lds = 1;                       // whole scene in LDS when it fits (48 KiB)
     int top = 1;                       // TOP staging of larger scenes
     int fused = -1;                    // n_shadow == 1: k_bounce_q instead of closest / shade / shadow (-1: when LDS-staged)
-    uint32_t tail_below = 1u << 18;    // n_shadow == 1: k_bounce_q tail mode below this many live paths
+    uint32_t tail_below = 1u << 16;    // n_shadow == 1: k_bounce_q tail mode below this many live paths
+                                       // (split passes; C2 4-spp frame 332 ms at 2^18, 312-319 ms at 2^16)
     int pipeline = 3;                  // fused passes overlapped (render_pipelined): 0 off, else head streams (1-3)
     int heads = 0;                     // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
     int merge = 0;                     // pipelined passes: passes merged into one head unit (0: auto)

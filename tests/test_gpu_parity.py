@@ -217,7 +217,7 @@ def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
         assert after.closest_queries - before.closest_queries == cnt.closest_queries
         assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
     finally:
-        dev.set_option("fused", -1).set_option("tail_below", 1 << 18).set_option("pipeline", 3)
+        dev.set_option("fused", -1).set_option("tail_below", 1 << 16).set_option("pipeline", 3)
 
 
 @pytest.mark.parametrize("heads", [4, 5, 6, 8])

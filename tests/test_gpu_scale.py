@@ -213,7 +213,7 @@ def test_bounce_modes_small_dragon(dev, fused, tail, pipe):
             np.testing.assert_array_equal(b, ob)
             assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
     finally:
-        dev.set_option("fused", -1).set_option("tail_below", 1 << 18).set_option("pipeline", 3)
+        dev.set_option("fused", -1).set_option("tail_below", 1 << 16).set_option("pipeline", 3)
 
 
 # ---------------------------------------------------------------------------- TOP staging
