@@ -9,6 +9,11 @@ Default run (the driver's `python bench.py --gpus N --steps K --warmup W`):
   * C3 = BASELINE configs[3]: the Bistro stand-in, PathTrace, 1920x1080 @ 256 spp, one timed
     frame after a 1-spp warmup frame (`--bistro-frames`, 0 disables).  Reported under "c3" with
     its own ms_per_step, roofline and CPU baseline.
+  * C2 = BASELINE configs[2]: the dragon stand-in, PathTrace, 1920x1080 @ 256 spp, one timed frame
+    after a 1-spp warmup frame (`--dragon-frames`, 0 disables), under "c2".
+  * C4 = BASELINE configs[4] (caustics.rs, BDPT, 1024x1024 @ 4096 spp, quoted on 8 GPUs): one
+    rank's share of the 8-GPU run (the tiles with tile % 8 == 0, `--c4-share`, "" disables), timed
+    on this GPU after a 1-spp warmup, under "c4_share" with "share": "0/8".
 With N ranks (one per GPU, launched by torch.distributed.run) the tasks are sharded by tile index
 (tile % N == rank, all batches of a tile on one rank), the scene is replicated, and no collective
 touches the data path; only the timing barriers and the final max/sum of scalars use the group.
@@ -54,6 +59,11 @@ UNIT_STAGES = {"k_bounce_q+k_bounce_tail": [1, 4], "k_closest": [1], "k_shadow":
                "k_bdpt_trace_a+k_bdpt_vis": [8, 10], "frame": list(range(12))}
 
 
+def progress(msg):
+    """A progress line on stderr (long default runs: the C4 share and the CPU baselines)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -75,6 +85,11 @@ def main():
     ap.add_argument("--bistro-frames", type=int, default=1,
                     help="with --config c1: also time this many C3 Bistro frames at 1920x1080@256 (0: skip)")
     ap.add_argument("--bistro-spp", type=int, default=256)
+    ap.add_argument("--dragon-frames", type=int, default=1,
+                    help="with --config c1: also time this many C2 dragon frames at 1920x1080@256 (0: skip)")
+    ap.add_argument("--c4-share", default="0/8",
+                    help="with --config c1: also time this rank share R/N of the C4 caustics BDPT frame "
+                         "(1024^2@4096) on this GPU (empty: skip)")
     ap.add_argument("--max-paths", type=int, default=1 << 23, help="paths in flight per wavefront")
     ap.add_argument("--max-vertices", type=int, default=0, help="BDPT vertex storage per subpath (0 = 128)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on the host (rank 0, N=1)")
@@ -105,36 +120,43 @@ def main():
         pg = dist
 
     main_res = run(args.config, args, ws, rank, local, pg, steps=args.steps, warmup=args.warmup,
-                   res=args.res, spp=args.spp)
-    c3 = None
+                   res=args.res, spp=args.spp, share=args.share)
+    extra = {}
     if args.config == "c1" and args.bistro_frames > 0:
-        c3 = run("c3", args, ws, rank, local, pg, steps=args.bistro_frames, warmup=1, spp=args.bistro_spp,
-                 warm_spp=1)
+        extra["c3"] = run("c3", args, ws, rank, local, pg, steps=args.bistro_frames, warmup=1, spp=args.bistro_spp,
+                          warm_spp=1)
+    if args.config == "c1" and args.dragon_frames > 0:
+        extra["c2"] = run("c2", args, ws, rank, local, pg, steps=args.dragon_frames, warmup=1, warm_spp=1)
+    if args.config == "c1" and args.c4_share and ws == 1:
+        # one rank's load of the 8-GPU C4 run (BASELINE configs[4] is quoted on 8 GPUs), on this GPU
+        extra["c4_share"] = run("c4", args, ws, rank, local, pg, steps=1, warmup=1, warm_spp=1, share=args.c4_share)
     if rank == 0:
         out = main_res
-        if c3 is not None:
-            out["c3"] = {k: c3[k] for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype",
-                                            "data", "config", "msamples_per_s", "lumo_total_rays_per_s_M",
-                                            "queries_per_step", "shadow_resolved_per_step",
-                                            "mrays_traversed_per_s", "mrays_lumo_equivalent_per_s", "scene_build_s", "sample_checks", "roofline",
-                                            "cpu_baseline")}
+        keys = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype", "data", "config",
+                "msamples_per_s", "lumo_total_rays_per_s_M", "queries_per_step", "shadow_resolved_per_step",
+                "mrays_traversed_per_s", "mrays_lumo_equivalent_per_s", "scene_build_s", "sample_checks", "roofline",
+                "cpu_baseline", "warmup_spp", "share")
+        for name, rec in extra.items():
+            out[name] = {k: rec[k] for k in keys if k in rec}
         print(json.dumps(out))
     if pg is not None:
         pg.destroy_process_group()
 
 
-def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, warm_spp=None):
+def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, warm_spp=None, share=None):
     """Render `steps` timed frames of `config` (after `warmup` frames, at `warm_spp` if given) and
-    return the JSON record (rank 0 fields complete)."""
+    return the JSON record (rank 0 fields complete).  `share` "R/N": only the tiles with
+    tile % N == R (one rank's load of an N-rank run), in this process."""
     import lumo_amd as L
     from lumo_amd import _ffi
     from lumo_amd.dist import TileQueue, shard_tasks, tasks_of_tiles, tiles_per_batch
 
+    progress(f"{config}: building the scene")
     scene, cam, (W, H), spp, wl = build_config(config, res, spp)
+    progress(f"{config}: {W}x{H} @ {spp} spp{' share ' + share if share else ''}, scene built in {wl['scene_build_s']} s")
     bdpt = wl.get("integrator") == L.Integrator.BDPathTrace
     tasks = L.make_tasks(W, H, spp, SEED)
     tiles = tiles_per_batch(W, H)
-    share = getattr(args, "share", None) if config == args.config else None
     if share:
         sr, sn = (int(x) for x in share.split("/"))
         mine = shard_tasks(tasks, W, H, sr, sn)
@@ -143,7 +165,8 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
     mine_arr = (_ffi.TileTask * len(mine))(*mine)
     warm_arr = mine_arr
     if warm_spp is not None:
-        wt = shard_tasks(L.make_tasks(W, H, warm_spp, SEED), W, H, rank, ws)
+        wr, wn = (int(x) for x in share.split("/")) if share else (rank, ws)
+        wt = shard_tasks(L.make_tasks(W, H, warm_spp, SEED), W, H, wr, wn)
         warm_arr = (_ffi.TileTask * len(wt))(*wt)
 
     splat_film = np.zeros((H, W, 3)) if bdpt else None
@@ -169,6 +192,7 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
 
     for _ in range(warmup):
         step(warm_arr)
+    progress(f"{config}: warmup done, timing {steps} step(s)")
     dev.set_option("timing", 1)
     lib.lumo_stats_reset(dev.ctx)
     barrier()
@@ -187,6 +211,7 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
         q, cams, rays = q + a, cams + b, rays + c
     barrier()  # lumo_render_tiles returns only after its stream has drained
     elapsed = time.perf_counter() - t0
+    progress(f"{config}: {elapsed / steps * 1e3:.1f} ms per step")
     dev.set_option("timing", 0)
     st = dev.stats()
     # busy time (union of launch intervals) of every stage and of the roofline units
@@ -212,7 +237,8 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
         # a rank's share launches fewer paths per pass: its own PMC entry when one was profiled
         wkey = f"{config}_share" if share and pmc_traffic(f"{config}_share", "source") else config
         roof = roofline(st, n_shadow_rays(scene), bdpt=bdpt, workload=wkey, elapsed=elapsed, busy=busy)
-        cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl) if (args.cpu_baseline and ws == 1) else None
+        cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl, repeats=wl.get("cpu_repeats", CPU_REPEATS)) \
+            if (args.cpu_baseline and ws == 1) else None
         out = {
             "metric": "Mrays/s",
             # traversed queries only: the shadow records answered without a traversal (their BSDF
@@ -432,7 +458,7 @@ def host_cpus():
             "cgroup_quota_cpus": quota, "model": model}
 
 
-def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl):
+def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl, repeats=CPU_REPEATS):
     """The oracle (f64 restatement of lumo's CPU path, lumo's own tile-serial RNG order) on this
     host, BASELINE.md §5: once with every usable core and once with lumo's default 4 threads
     (renderer.rs:21).  Each run renders every k-th tile of the frame's batches at the frame's spp,
@@ -459,7 +485,8 @@ def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl):
         n = min(n, len(space))
         sample = [tasks[space[(k * len(space)) // n]] for k in range(n)]
         times = []
-        for _ in range(CPU_REPEATS):  # the host is shared: the median of repeated runs, with their spread
+        progress(f"cpu baseline: {len(sample)} tiles at {threads} threads x {repeats}")
+        for _ in range(repeats):  # the host is shared: the median of repeated runs, with their spread
             t0 = time.perf_counter()
             bufs, res, cnt = O.render_tasks(scene.desc(), cam.desc, sample, O.LUMO_ORDER, threads,
                                             integrator=integrator, splats_out=[] if integrator else None)
@@ -475,7 +502,7 @@ def cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl):
                                f"the {W}x{H} @ {spp} spp frame ({paths} paths), lumo tile-serial RNG order"})
     best = runs[0]
     return {"value": best["value"], "unit": "Mrays/s", "cores": best["threads"], "kind": "port",
-            "statistic": f"median of {CPU_REPEATS} runs", "value_min": best["value_min"],
+            "statistic": f"median of {repeats} runs", "value_min": best["value_min"],
             "value_max": best["value_max"],
             "msamples_per_s": best["msamples_per_s"], "seconds": best["seconds"], "sample": best["sample"],
             "cpu_model": info["model"], "host": info, "runs": runs}

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define LUMO_ABI_VERSION 8
+#define LUMO_ABI_VERSION 9
 
 typedef int32_t lumo_status;
 enum {
@@ -316,6 +316,9 @@ typedef struct {
      * visibility: the record's BSDF pdf is 0, so mis_sample returns 0 before using the hit
      * (integrator.rs:146); the device answers them without traversing the scene. */
     uint64_t shadow_resolved;
+    /* closest queries (included in closest_queries) run by the path tracer's tail kernel past
+     * the first bounce it takes: > 0 when the device switched a pass to the tail kernel (ABI 9) */
+    uint64_t tail_queries;
 } lumo_stats;
 
 /* Per-path dump of one task (test hook for per-path parity): arrays sized samples x pixels
@@ -380,8 +383,9 @@ enum {
                                   schedule on when > 0 (LUMO_PIPELINE, 3)                            */
     LUMO_OPT_HEADS,            /* fused pipeline: bounces per pass on its head stream, 0 auto
                                   (LUMO_HEADS, 0)                                                   */
-    LUMO_OPT_MERGE_PASSES,     /* fused pipeline: consecutive passes whose cameras and head bounces
-                                  run as one queue, 0 auto, 1-8 (LUMO_MERGE, 0)                      */
+    LUMO_OPT_MERGE_PASSES,     /* fused and split pipelines: consecutive passes whose cameras and
+                                  head bounces (those before Russian roulette) run as one queue,
+                                  0 auto, 1-8 (LUMO_MERGE, 0)                                        */
     LUMO_OPT_DYN_FETCH,        /* fused bounce: blocks fetch paths from a counter: 0 / 1 (LUMO_DYN, 1)*/
     LUMO_OPT_BOUNCE_THREADS,   /* fused bounce: threads per block 64 / 128 / 256
                                   (LUMO_BOUNCE_THREADS, 256)                                        */
@@ -429,7 +433,7 @@ typedef struct {
     int32_t schedule;        /* LUMO_SCHED_*                                               */
     int32_t head_streams;    /* fused pipeline: head streams                               */
     int32_t head_bounces;    /* fused pipeline: bounces per pass on the head stream        */
-    int32_t merged_passes;   /* fused pipeline: passes per head unit                       */
+    int32_t merged_passes;   /* fused / split pipeline: passes per head unit               */
     int32_t units_in_flight; /* split pipeline: (group, pass) units in flight              */
     int32_t task_groups;     /* split pipeline: independent task groups                    */
     int32_t fused;           /* 1: fused bounce kernel, 0: three kernels per bounce         */
@@ -457,6 +461,8 @@ typedef struct {
     int32_t stack_class, lds_bytes, full_kernels, n_shadow;
     int32_t top_bytes, top_object_nodes, top_light_nodes;
     int32_t top_kd_nodes; /* kd nodes of the largest kd tree (its top treelets) in the TOP set */
+    int32_t top_shm;      /* LDS per TOP block: the TOP set + the kd stack columns, within
+                             LUMO_OPT_TOP_KB (ABI 9)                                          */
 } lumo_scene_info_t;
 lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info);
 /* Diagnostics: one coalesced 8-B-per-lane read stream and one write stream over n doubles

@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 8  # include/lumo_amd.h LUMO_ABI_VERSION
+ABI_VERSION = 9  # include/lumo_amd.h LUMO_ABI_VERSION
 LIB_PATH = os.environ.get("LUMO_AMD_LIB") or os.path.join(_HERE, "liblumo_amd.so")
 
 c_double_p = C.POINTER(C.c_double)
@@ -145,7 +145,7 @@ class HitSoA(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("stack_class", C.c_int32), ("lds_bytes", C.c_int32), ("full_kernels", C.c_int32),
                 ("n_shadow", C.c_int32), ("top_bytes", C.c_int32), ("top_object_nodes", C.c_int32),
-                ("top_light_nodes", C.c_int32), ("top_kd_nodes", C.c_int32)]
+                ("top_light_nodes", C.c_int32), ("top_kd_nodes", C.c_int32), ("top_shm", C.c_int32)]
 
 
 STAGE_COUNT = 12  # LUMO_STAGE_COUNT
@@ -158,7 +158,7 @@ class Stats(C.Structure):
                 ("closest_queries", C.c_uint64), ("shadow_queries", C.c_uint64), ("bounces", C.c_uint64),
                 ("aabb_tests", C.c_uint64 * 2), ("kd_nodes", C.c_uint64 * 2), ("tri_tests", C.c_uint64 * 2),
                 ("samples_nan", C.c_uint64), ("samples_neg", C.c_uint64), ("samples_large", C.c_uint64),
-                ("shadow_resolved", C.c_uint64)]
+                ("shadow_resolved", C.c_uint64), ("tail_queries", C.c_uint64)]
 
 
 class ScheduleInfo(C.Structure):

@@ -33,6 +33,8 @@ void launch_bdpt_step(int grid, hipStream_t sm, int fx, const DScene& sc, const 
 
 // ... and, for kernels with a TOP variant (LDS mode 2: scenes too large to stage whole, fx 0 / 1),
 // `TB` threads per block with the TOP set (and the kd stack columns) in `l.shm` bytes of LDS.
+// The caller asks for TOP (launch_trav's allow_top) only for fx 0 / 1: l.grid is then sized for
+// TB-thread blocks, too small a grid for the fallback's BLOCK threads.
 // Only the (b)-item visibility has one: TOP variants of the walk (k_closest), the walk tail and
 // the (a)-item traces were slower on C4 (the tail 150 -> 239 ms per 8-spp frame, (a) traces
 // 177 -> 191 ms), while the visibility went 200 -> 85 ms.

@@ -62,8 +62,7 @@ void launch_shadow_q(const TravLaunch& l, const DScene& sc, const Paths& S, cons
 
 template <int STK>
 void launch_bounce_q(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const QState& cur,
-                     const QState& nxt, uint32_t tail_below, bool tail_only, int dyn, int threads, int32_t vlo,
-                     int32_t vhi) {
+                     const QState& nxt, uint32_t tail_below, bool tail_only, int dyn, int threads) {
     // fused bounce: `threads` per block (64 / 128 / 256), 12 doubles of LDS per thread for the
     // B record after the staged scene; the tail kernel keeps BLOCK threads and needs no record LDS
     const int nt = tail_only ? BLOCK : threads;
@@ -73,15 +72,15 @@ void launch_bounce_q(const TravLaunch& l, const DScene& sc, const Paths& S, cons
     auto go = [&](auto TL) {
         constexpr bool TAIL = decltype(TL)::value;
         if (l.fx == 2) {  // textured scenes: no LDS staging variant (as k_shadow_q)
-            k_bounce_q<STK, false, 2, TAIL><<<grid, nt, rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn, vlo, vhi);
+            k_bounce_q<STK, false, 2, TAIL><<<grid, nt, rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn);
         } else if (l.lds) {
             if (l.fx)
-                k_bounce_q<STK, true, 1, TAIL><<<grid, nt, scene + rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn, vlo, vhi);
+                k_bounce_q<STK, true, 1, TAIL><<<grid, nt, scene + rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn);
             else
-                k_bounce_q<STK, true, 0, TAIL><<<grid, nt, scene + rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn, vlo, vhi);
+                k_bounce_q<STK, true, 0, TAIL><<<grid, nt, scene + rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn);
         } else {
-            if (l.fx) k_bounce_q<STK, false, 1, TAIL><<<grid, nt, rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn, vlo, vhi);
-            else k_bounce_q<STK, false, 0, TAIL><<<grid, nt, rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn, vlo, vhi);
+            if (l.fx) k_bounce_q<STK, false, 1, TAIL><<<grid, nt, rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn);
+            else k_bounce_q<STK, false, 0, TAIL><<<grid, nt, rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn);
         }
     };
     if (tail_only)
@@ -106,7 +105,7 @@ template void launch_closest<LUMO_STK>(const TravLaunch&, const DScene&, const P
 template void launch_closest_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const QState&, uint32_t);
 template void launch_shadow_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const QState&);
 template void launch_bounce_q<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Tasks&, const QState&,
-                                        const QState&, uint32_t, bool, int, int, int32_t, int32_t);
+                                        const QState&, uint32_t, bool, int, int);
 template void launch_trace<LUMO_STK>(int, hipStream_t, const DScene&, const double*, const double*, const int32_t*,
                                      int, int, double*, int32_t*, int32_t*, int32_t*, unsigned long long*, bool);
 

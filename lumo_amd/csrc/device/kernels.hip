@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <strings.h>
 #include <deque>
 #include <new>
 #include <type_traits>
@@ -1063,14 +1064,14 @@ void alloc_split_set(Ctx& c, Paths& Q, const Paths& S, int k, int ns, lumo_statu
     Q.sq.i = wbuf<int32_t>(c, w + 3, SI_N * S.sq.cap, st);
     Q.sq.hd = wbuf<double>(c, w + 4, (ns > 1 ? SH_N : SH_N1) * S.sq.hcap, st);
     Q.sq.hi = wbuf<int32_t>(c, w + 5, SHI_N * S.sq.hcap, st);
-    Q.sq.hr = ns > 1 ? wbuf<uint64_t>(c, w + 6, 2 * S.sq.hcap, st) : nullptr;
+    Q.sq.hr = ns > 1 ? wbuf<uint64_t>(c, w + 6, 2 * S.sq.cap, st) : nullptr;
     Q.sq.ql = ns > 1 ? wbuf<int32_t>(c, w + 7, SHQ_CLASSES * S.sq.cap, st) : nullptr;
 }
 // Device bytes of one extra pass set of the split schedule.
 size_t split_set_bytes(const Paths& S, int N, int ns) {
     return (size_t)N * (4 + 4 + 2) * 8 + (size_t)N * 3 * 4 + 2 * (size_t)N * (QD_N * 8 + 16 + QI_N * 4) +
            S.hq.cap * (8 + 12) + S.sq.cap * (SD_N * 8 + SI_N * 4) +
-           S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4 + (ns > 1 ? 16 : 0)) + (ns > 1 ? S.sq.cap * 4 * SHQ_CLASSES : 0);
+           S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4) + (ns > 1 ? S.sq.cap * (4 * SHQ_CLASSES + 16) : 0);
 }
 
 
@@ -1265,15 +1266,18 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
 // One path-tracing bounce of the split (not fused-LDS) schedule on stream `sm`: the tail kernel when
 // few paths are alive (n_shadow == 1), then the fused bounce (fused_now) or closest hit -> shading
 // (+ NEE pair generation when n_shadow > 1) -> visibility (+ the NEE fold).  `ub` is an upper bound
-// on the live count (grids); the kernels read the exact count from S.counts.
+// on the live count (grids); the kernels read the exact count from S.counts.  allow_tail = false:
+// the bounce must not run paths through Russian roulette (a merged head, which reads no delta).
 void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, const QState& nxt, uint32_t ub,
-                        hipStream_t sm, bool fused_now) {
+                        hipStream_t sm, bool fused_now, bool allow_tail = true) {
     const int ns = c.sc.n_shadow;
-    // n_shadow == 1: the tail kernel takes the bounce when fewer than c.o.tail_below paths
-    // are alive (decided on the device from the exact count); the bounce kernels skip it
+    // n_shadow == 1: the tail kernel takes the bounce when fewer than c.o.tail_below paths are alive
+    // (decided on the device from the exact count); the bounce kernels skip it.  (A tail kernel for
+    // n_shadow > 1, each thread tracing its path's 2 x n_shadow visibility rays per bounce in turn,
+    // made C3's 1/8 share 720 -> 1 300-2 460 ms at thresholds 2^12-2^16: rejected, round 5)
     // (launched only once the last count the host has seen is below 4x the threshold:
     // before that the bounce kernels get threshold 0 and take every path)
-    const uint32_t skip = (ns == 1 && (uint64_t)ub < 4ull * c.o.tail_below) ? c.o.tail_below : 0u;
+    const uint32_t skip = (allow_tail && ns == 1 && (uint64_t)ub < 4ull * c.o.tail_below) ? c.o.tail_below : 0u;
     if (skip > 0) {
         StageTimer tm(c, c.o.timing, ST_RESOLVE, sm);
         launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
@@ -1334,23 +1338,34 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
 // large for the fused LDS kernel, n_shadow > 1).  A pass whose queue has shrunk to a few thousand
 // paths runs latency-bound launches (one long walk sets a kernel's duration: C3 at one rank's 1/8
 // share spent ~0.4 ms per closest / visibility launch for every bounce past the fifth), so several
-// passes run at once on their own streams and pass sets (queues, counters, hits, NEE records,
+// units run at once on their own streams and pass sets (queues, counters, hits, NEE records,
 // per-slot outputs).
 //
 // Russian roulette reads a task's adaptive delta from depth RR_DEPTH on (path_trace.rs:60-69) and
 // the delta of pass p needs the film and ring of pass p - 1 *of the same task* (task.rs:28-53); the
 // sampler state is per slot.  So the tasks are cut into G groups of consecutive tasks (about equal
-// slots) whose pass chains are independent, and the units of work are (group g, pass p), issued in
-// the order n = p * G + g on pass set / stream n % K (K >= G).  Unit (g, p) waits for unit (g, p - 1)'s
-// camera before its own, and for its ring before its bounce RR_DEPTH, before any bounce that may
-// run the tail kernel (n_shadow == 1: it takes paths through Russian roulette) and before its film.
-// Set reuse (unit n + K, started once unit n has issued its ring) is ordered by its stream.  The host runs every in-flight unit's bounce
-// loop (count snapshots `ahead` launches back, as the sequential loop), blocks only on the oldest
-// unit, which never waits for a unit the host has not finished issuing, and enqueues every wait
-// after the record it waits for.  Every per-path operation and every film / ring sum of a task is
-// the sequential loop's, in the same order: bit-identical.
+// slots) whose pass chains are independent, and the units of work are (group g, passes p0 ..
+// p0 + mu - 1), issued in the order n = u * G + g on pass set / stream n % K (K >= G).
+//
+// Merged passes (M > 1: a pass holds few paths, e.g. one rank's share of a multi-GPU frame): the
+// unit's camera generates the samples of its mu passes in pass order into one queue (pass m's
+// per-slot outputs at virtual slots s + m N), and its first RR_DEPTH bounces (the head, which reads
+// no delta) run them as one queue, mu times the paths per launch.  k_split_passes then cuts the
+// queue into one segment per pass, each with its own counters, and the passes run their remaining
+// bounces one after the other, each followed by its ring: every pass's Russian roulette sees the
+// delta of the ring before it.  One film launch takes the unit's passes in pass order.
+//
+// Unit (g, u) waits for unit (g, u - 1)'s camera before its own, and for its last ring before the
+// first bounce that reads the delta: bounce RR_DEPTH of a one-pass unit (or any bounce that may run
+// the tail kernel: n_shadow == 1, it takes paths through Russian roulette), the first per-pass
+// bounce of a merged unit; and for its film before its own film.  Set reuse (unit n + K, started
+// once unit n has issued its last ring) is ordered by its stream.  The host runs every in-flight
+// unit's bounce loop (count snapshots `ahead` launches back, as the sequential loop), blocks only on
+// the oldest unit, which never waits for a unit the host has not finished issuing, and enqueues
+// every wait after the record it waits for.  Every per-path operation and every film / ring sum of
+// a task is the sequential loop's, in the same order: bit-identical.
 lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int n_tasks, int dim_stride,
-                                   uint64_t max_samples, uint64_t max_P, bool fused_now, int K, int G,
+                                   uint64_t max_samples, uint64_t max_P, bool fused_now, int K, int G, int M,
                                    const std::vector<int32_t>& first, uint64_t& bounces, lumo_status& st) {
     struct JoinOnError {
         Ctx& c;
@@ -1374,7 +1389,7 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
     }
     Paths P[4] = {S, S, S, S};
     for (int k = 1; k < K; ++k) {
-        alloc_pass_set(c, P[k], k, N, st);
+        alloc_pass_set(c, P[k], k, N * M, st);  // M passes' outputs and paths
         alloc_split_set(c, P[k], S, k, ns, st);
     }
     if (st) return st;
@@ -1395,35 +1410,43 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
     for (int k = 1; k < K; ++k) HIPCHK(hipStreamWaitEvent(Ss[k], c.pass_ev[0], 0));
     const int SEG = Ctx::SNAP_RING / 4;  // snapshot slots per set
     const int ahead = std::max(1, std::min(c.o.bounce_ahead, SEG - 1));
+    // A unit's bounce loops: seg -1 the merged head (mu > 1), then seg m = its pass m (a one-pass unit
+    // starts at seg 0 with its head included).  Snapshots are numbered over the whole unit; those of an
+    // earlier segment are consumed for the statistics only.
     struct PS {
-        uint64_t unit, pass;
-        int g, set, issued, consumed;
+        uint64_t unit, pass0;
+        int g, set, mu, seg;
+        int issued, consumed, seg_first, seg_issued, head_issued;
         uint32_t ub;
         bool done, waited;
     };
     std::deque<PS> act;
-    std::vector<uint64_t> finished(G, 0);  // passes of each group whose ring has been issued
-    const uint64_t units = max_samples * (uint64_t)G;
+    std::vector<uint64_t> finished(G, 0);  // passes of each group whose last ring has been issued
+    const uint64_t per_group = (max_samples + (uint64_t)M - 1) / (uint64_t)M;
+    const uint64_t units = per_group * (uint64_t)G;
     uint64_t next = 0;
+    auto group_slots = [&](int g) { return (uint32_t)(first[t_hi[g]] - first[t_lo[g]]); };
     auto start = [&]() -> lumo_status {
         const int set = (int)(next % K), g = (int)(next % G);
-        const uint64_t pass = next / G;
+        const uint64_t pass0 = (next / G) * (uint64_t)M;
+        const int mu = (int)std::min<uint64_t>((uint64_t)M, max_samples - pass0);
         hipStream_t sm = Ss[set];
         const int s0 = first[t_lo[g]], s1 = first[t_hi[g]];
-        if (pass > 0) HIPCHK(hipStreamWaitEvent(sm, c.cam_ev[(next - G) % K], 0));  // sampler state per slot
+        if (pass0 > 0) HIPCHK(hipStreamWaitEvent(sm, c.cam_ev[(next - G) % K], 0));  // sampler state per slot
         {
             StageTimer tm(c, c.o.timing, ST_CAMERA, sm);
-            k_camera<true><<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(T, P[set], c.cam, s1, dim_stride, (uint32_t)pass,
-                                                                        s0, 1, 0);
+            k_camera<true><<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(T, P[set], c.cam, s1, dim_stride, (uint32_t)pass0,
+                                                                        s0, mu, N);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.cam_ev[set], sm));
-        act.push_back(PS{next, pass, g, set, 0, 0, (uint32_t)(s1 - s0), false, pass == 0});
+        act.push_back(PS{next, pass0, g, set, mu, mu > 1 ? -1 : 0, 0, 0, 0, 0, 0, group_slots(g) * (uint32_t)mu, false,
+                         pass0 == 0});
         next++;
         return LUMO_OK;
     };
-    auto ready = [&](const PS& ps) { return ps.waited || finished[ps.g] >= ps.pass; };
-    auto wait_prev = [&](PS& ps) -> lumo_status {  // unit (g, p - 1)'s ring, already issued
+    auto ready = [&](const PS& ps) { return ps.waited || finished[ps.g] >= ps.pass0; };
+    auto wait_prev = [&](PS& ps) -> lumo_status {  // unit (g, u - 1)'s last ring, already issued
         if (!ps.waited) HIPCHK(hipStreamWaitEvent(Ss[ps.set], c.pass_ev[(ps.unit - G) % K], 0));
         ps.waited = true;
         return LUMO_OK;
@@ -1433,24 +1456,45 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
     auto tail_possible = [&](const PS& ps) {
         return ns == 1 && c.o.tail_below > 0 && (uint64_t)ps.ub < 4ull * c.o.tail_below;
     };
+    // the queues and counters of the unit's current segment
+    auto seg_paths = [&](const PS& ps) {
+        Paths Q = P[ps.set];
+        if (ps.seg >= 0 && ps.mu > 1) Q.counts = P[ps.set].counts + (size_t)(1 + ps.seg) * CNT_N;
+        return Q;
+    };
+    auto seg_queue = [&](const PS& ps, int parity) {
+        const Paths& Q = P[ps.set];
+        if (ps.seg < 0 || ps.mu == 1) return Q.qs[parity];
+        // pass m's paths: segment m of the queue k_split_passes wrote (the other parity than the head's last)
+        return segment(Q.qs[(ps.head_issued + 1 + parity) & 1], ps.seg, N);
+    };
+    // bounce of the current segment: a merged head never reads the delta (no tail kernel); every
+    // per-pass bounce of a merged unit does (depth >= RR_DEPTH)
+    auto needs_delta = [&](const PS& ps) {
+        if (ps.seg < 0) return false;
+        return ps.mu > 1 || ps.seg_issued >= RR_DEPTH || tail_possible(ps);
+    };
     auto issue = [&](PS& ps) -> lumo_status {
         hipStream_t sm = Ss[ps.set];
-        Paths& Q = P[ps.set];
-        if (ps.issued >= RR_DEPTH || tail_possible(ps)) {
+        if (needs_delta(ps)) {
             const lumo_status w = wait_prev(ps);
             if (w) return w;
         }
+        Paths Q = seg_paths(ps);
         k_bounce_begin<<<1, 64, 0, sm>>>(Q.counts, Q.tcount + TC_HEADQ);
-        issue_split_bounce(c, Q, T, Q.qs[ps.issued & 1], Q.qs[(ps.issued + 1) & 1], ps.ub, sm, fused_now);
+        issue_split_bounce(c, Q, T, seg_queue(ps, ps.seg_issued & 1), seg_queue(ps, (ps.seg_issued + 1) & 1), ps.ub, sm,
+                           fused_now, ps.seg >= 0);
         HIPCHK(hipGetLastError());
         const int slot = ps.set * SEG + ps.issued % SEG;
         HIPCHK(hipMemcpyAsync(c.snap + CNT_N * slot, Q.counts, sizeof(uint32_t) * CNT_N, hipMemcpyDeviceToHost, sm));
         HIPCHK(hipEventRecord(c.snap_ev[slot], sm));
         ps.issued++;
+        ps.seg_issued++;
+        if (ps.seg < 0) ps.head_issued++;
         return LUMO_OK;
     };
     auto poll = [&](PS& ps, bool block) -> lumo_status {
-        while (ps.consumed < ps.issued && !ps.done) {
+        while (ps.consumed < ps.issued && !(ps.done && ps.consumed >= ps.seg_first)) {
             const int slot = ps.set * SEG + ps.consumed % SEG;
             if (hipEventQuery(c.snap_ev[slot]) != hipSuccess) {
                 if (!block) break;
@@ -1459,49 +1503,82 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
             }
             const uint32_t* k = c.snap + CNT_N * slot;
             bounces += k[CNT_CUR] > 0 ? 1 : 0;
-            ps.ub = k[CNT_NEXT];
-            ps.done = ps.ub == 0;
+            if (ps.consumed >= ps.seg_first) {
+                ps.ub = k[CNT_NEXT];
+                ps.done = ps.ub == 0;
+            }
             ps.consumed++;
         }
         return LUMO_OK;
     };
-    auto finish = [&](PS& ps) -> lumo_status {  // ring + film of the group's tasks
+    // the merged head is over (RR_DEPTH bounces, or no path left): its queue split by pass
+    auto split = [&](PS& ps) -> lumo_status {
         hipStream_t sm = Ss[ps.set];
-        Paths& Q = P[ps.set];
+        const Paths& Q = P[ps.set];
+        ZeroList z;
+        z.add(Q.counts + CNT_N, sizeof(uint32_t) * CNT_N * (size_t)ps.mu);
+        k_zero_list<<<1, BLOCK, 0, sm>>>(z);
+        const uint64_t n_head = (uint64_t)group_slots(ps.g) * (uint64_t)ps.mu;
+        k_split_passes<<<std::min(ceil_div(n_head, BLOCK), 4096), BLOCK, 0, sm>>>(
+            Q.qs[ps.head_issued & 1], Q.qs[(ps.head_issued + 1) & 1], Q.counts, N, ps.mu);
+        HIPCHK(hipGetLastError());
+        ps.seg = 0;
+        ps.seg_first = ps.issued;
+        ps.seg_issued = 0;
+        ps.ub = group_slots(ps.g);
+        ps.done = false;
+        return LUMO_OK;
+    };
+    // the ring of the segment's pass (task.rs:28-69, from the pass's final radiance); after the
+    // unit's last pass its film (after the group's previous film: the film accumulates in pass order)
+    auto finish = [&](PS& ps) -> lumo_status {
+        hipStream_t sm = Ss[ps.set];
+        const Paths& Q = P[ps.set];
+        const int t0 = t_lo[ps.g], t1 = t_hi[ps.g], s0 = first[t0], s1 = first[t1];
         const lumo_status w = wait_prev(ps);
         if (w) return w;
-        const int t0 = t_lo[ps.g], t1 = t_hi[ps.g], s0 = first[t0], s1 = first[t1];
-        // the ring (task.rs:28-69, from the pass's final radiance) first: the group's next pass
-        // waits only for it; the film follows on this stream, after the group's previous film
-        // (the film accumulates in pass order)
+        const int m = ps.seg;
+        const bool last = m == ps.mu - 1;
         {
             StageTimer tm(c, c.o.timing, ST_RING, sm);
-            k_ring<<<t1 - t0, 64, 0, sm>>>(c.sc, Q, T, t1, 1, Q.counts, t0);
+            k_ring<<<t1 - t0, 64, 0, sm>>>(c.sc, pass_view(Q, m, N), T, t1, 1, last ? Q.counts : nullptr, t0);
         }
         HIPCHK(hipGetLastError());
+        if (!last) {  // the unit's next pass: its bounces follow this ring on the stream
+            ps.seg = m + 1;
+            ps.seg_first = ps.issued;
+            ps.seg_issued = 0;
+            ps.ub = group_slots(ps.g);
+            ps.done = false;
+            return LUMO_OK;
+        }
         HIPCHK(hipEventRecord(c.pass_ev[ps.set], sm));
-        if (ps.pass > 0) HIPCHK(hipStreamWaitEvent(sm, c.film_ev[(ps.unit - G) % K], 0));
+        if (ps.pass0 > 0) HIPCHK(hipStreamWaitEvent(sm, c.film_ev[(ps.unit - G) % K], 0));
         if (max_P <= BLOCK) {
             StageTimer tm(c, c.o.timing, ST_FILM, sm);
-            k_finish_film<<<t1 - t0, BLOCK, 0, sm>>>(c.sc, Q, T, c.cam, (uint32_t)ps.pass, Dump{}, 0, c.tone_map,
-                                                     c.tone_arg, t0, 1, 0);
+            k_finish_film<<<t1 - t0, BLOCK, 0, sm>>>(c.sc, Q, T, c.cam, (uint32_t)ps.pass0, Dump{}, 0, c.tone_map,
+                                                     c.tone_arg, t0, ps.mu, N);
         } else {
-            {
-                StageTimer tm(c, c.o.timing, ST_FINISH, sm);
-                k_finish<<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(c.sc, Q, c.cam, s1, (uint32_t)ps.pass, Dump{}, 0,
-                                                                     c.tone_map, c.tone_arg, s0);
+            for (int k = 0; k < ps.mu; ++k) {
+                const Paths V = pass_view(Q, k, N);
+                {
+                    StageTimer tm(c, c.o.timing, ST_FINISH, sm);
+                    k_finish<<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(c.sc, V, c.cam, s1, (uint32_t)(ps.pass0 + k),
+                                                                         Dump{}, 0, c.tone_map, c.tone_arg, s0);
+                }
+                StageTimer tm(c, c.o.timing, ST_FILM, sm);
+                k_film<<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(V, T, c.cam, s1, s0);
             }
-            StageTimer tm(c, c.o.timing, ST_FILM, sm);
-            k_film<<<ceil_div(s1 - s0, BLOCK), BLOCK, 0, sm>>>(Q, T, c.cam, s1, s0);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c.film_ev[ps.set], sm));
-        finished[ps.g] = ps.pass + 1;
+        finished[ps.g] = ps.pass0 + (uint64_t)ps.mu;
+        ps.seg = ps.mu;  // unit complete
         if (c.o.timing) resolve_timers(c);
         return LUMO_OK;
     };
-    // unit n reuses the set of unit n - K: it starts once that unit has issued its ring (units of
-    // different groups finish out of order, so a free slot in `act` does not mean a free set)
+    // unit n reuses the set of unit n - K: it starts once that unit has issued its last ring (units
+    // of different groups finish out of order, so a free slot in `act` does not mean a free set)
     auto set_free = [&](int set) {
         for (const PS& ps : act)
             if (ps.set == set) return false;
@@ -1517,18 +1594,29 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
         for (size_t i = 0; i < act.size(); ++i) {
             PS& ps = act[i];
             if ((e = poll(ps, false))) return e;
-            if (ps.done) {
-                if (ready(ps)) {  // the group's previous pass has issued its ring
-                    if ((e = finish(ps))) return e;
-                    act.erase(act.begin() + (std::ptrdiff_t)i);
+            if (ps.seg < 0) {  // merged head: RR_DEPTH bounces, then the split
+                if (ps.done || ps.seg_issued == RR_DEPTH) {
+                    if ((e = split(ps))) return e;
                     progress = true;
-                    break;
+                } else if (ps.issued - ps.consumed < ahead) {
+                    if ((e = issue(ps))) return e;
+                    progress = true;
                 }
                 continue;
             }
-            // a unit stops before bounce RR_DEPTH (or a tail-kernel bounce) until the group's
-            // previous pass has issued its ring
-            const bool may = (ps.issued < RR_DEPTH && !tail_possible(ps)) || ready(ps);
+            if (ps.done) {
+                if (ready(ps)) {  // the group's previous unit has issued its last ring
+                    if ((e = finish(ps))) return e;
+                    progress = true;
+                    if (ps.seg == ps.mu) {
+                        act.erase(act.begin() + (std::ptrdiff_t)i);
+                        break;
+                    }
+                }
+                continue;
+            }
+            // a bounce that reads the delta waits until the group's previous unit has issued its ring
+            const bool may = !needs_delta(ps) || ready(ps);
             if (may && ps.issued - ps.consumed < ahead) {
                 if ((e = issue(ps))) return e;
                 progress = true;
@@ -1589,9 +1677,17 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     const bool fused_now =
         ns == 1 && (c.o.fused < 0 ? (c.o.lds && c.sc.hot_bytes > 0 && fused_fits) : c.o.fused != 0);
     const bool pipe = !bdpt && fused_now && c.o.pipeline;
+    // the split schedule's pipeline (render_split_pipelined), when the free HBM allows (below)
+    const uint64_t split_units = max_samples * (uint64_t)std::max(1, std::min(c.o.split_groups, (int)n_tasks));
+    const bool split_try = !bdpt && !pipe && !dump_host && c.o.pipeline && c.o.split_pipe > 1 && split_units > 1;
     int M = 1;
-    if (pipe) {
-        M = c.o.merge > 0 ? c.o.merge : (int)std::min<uint64_t>(MAX_MERGE, (kMergeTarget + N - 1) / (uint64_t)N);
+    if (pipe || split_try) {  // merged passes: units of about kMergeTarget paths
+        M = (int)std::min<uint64_t>(MAX_MERGE, (kMergeTarget + N - 1) / (uint64_t)N);
+        // the split schedule merges passes only on request: at C3's 1/8 share merged units made the
+        // frame slower (M = 2 / 4 / 8: 723 -> 761 / 807 / 812 ms; the unit's large head launches
+        // hold the CUs while the latency-bound per-pass bounces of the group's chain wait; round 5)
+        if (split_try) M = 1;
+        if (c.o.merge > 0) M = c.o.merge;
         M = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)M, max_samples));
         if ((uint64_t)N * (uint64_t)M > ((uint64_t)1 << 30)) M = 1;
     }
@@ -1628,8 +1724,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         S.q0 = wbuf<int32_t>(c, W_Q0, N, st);
         S.q1 = wbuf<int32_t>(c, W_Q1, N, st);
     } else {
-        // path tracer: queue-order state (ping-pong), hits, NEE records (state.h)
-        const size_t cap = (size_t)N;
+        // path tracer: queue-order state (ping-pong), hits, NEE records (state.h); a merged unit of the
+        // split schedule runs its head bounces on the M passes' paths at once
+        const size_t cap = split_try ? NV : (size_t)N;
         for (int k = 0; k < 2; ++k) {
             S.qs[k].cap = NV;
             S.qs[k].d = wbuf<double>(c, k ? W_QS1_D : W_QS0_D, QD_N * NV, st);
@@ -1647,7 +1744,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         S.sq.i = wbuf<int32_t>(c, W_SQ_I, SI_N * S.sq.cap, st);
         S.sq.hd = wbuf<double>(c, W_SQ_HD, (ns > 1 ? SH_N : SH_N1) * S.sq.hcap, st);
         S.sq.hi = wbuf<int32_t>(c, W_SQ_HI, SHI_N * S.sq.hcap, st);
-        S.sq.hr = ns > 1 ? wbuf<uint64_t>(c, W_SQ_HR, 2 * S.sq.hcap, st) : nullptr;
+        S.sq.hr = ns > 1 ? wbuf<uint64_t>(c, W_SQ_HR, 2 * S.sq.cap, st) : nullptr;
         S.sq.ql = ns > 1 ? wbuf<int32_t>(c, W_SQ_QL, SHQ_CLASSES * S.sq.cap, st) : nullptr;
     }
     S.p_rgb = wbuf<double>(c, W_P_RGB, 3 * (size_t)N, st);
@@ -1783,13 +1880,14 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         if (ps) return ps;
         if (st) return st;
     }
-    // split schedule: passes in flight, as many as c.o.split_pipe and the free HBM allow
+    // split schedule: units in flight, as many as c.o.split_pipe and the free HBM allow
     int K = 1;
-    const uint64_t units = max_samples * (uint64_t)std::max(1, std::min(c.o.split_groups, (int)n_tasks));
-    if (!bdpt && !pipe && !dump_host && c.o.pipeline && c.o.split_pipe > 1 && units > 1) {
+    if (split_try) {
         size_t free_b = 0, total_b = 0;
-        const size_t per_set = split_set_bytes(S, N, ns);
+        const size_t per_set = split_set_bytes(S, (int)NV, ns);
         const size_t margin = (size_t)8 << 30;
+        const uint64_t units = (max_samples + (uint64_t)M - 1) / (uint64_t)M *
+                               (uint64_t)std::max(1, std::min(c.o.split_groups, (int)n_tasks));
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
             K = std::min(std::min(c.o.split_pipe, 4), (int)std::min<uint64_t>(units, 4));
             while (K > 1 && (size_t)(K - 1) * per_set + margin > free_b + c.split_sets_bytes) K--;
@@ -1799,11 +1897,12 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         c.sched.schedule = LUMO_SCHED_SPLIT_PIPELINE;
         c.sched.units_in_flight = K;
         c.sched.task_groups = std::max(1, std::min(c.o.split_groups, std::min(K, (int)n_tasks)));
+        c.sched.merged_passes = M;
         const lumo_status ps = render_split_pipelined(c, S, T, N, (int)n_tasks, dim_stride, max_samples, max_P,
-                                                      fused_now, K, c.o.split_groups, first, bounces, st);
+                                                      fused_now, K, c.o.split_groups, M, first, bounces, st);
         if (ps) return ps;
         if (st) return st;
-        c.split_sets_bytes = std::max(c.split_sets_bytes, (size_t)(K - 1) * split_set_bytes(S, N, ns));
+        c.split_sets_bytes = std::max(c.split_sets_bytes, (size_t)(K - 1) * split_set_bytes(S, (int)NV, ns));
     }
     for (uint64_t pass = 0; pass < ((pipe || K > 1) ? 0 : max_samples); ++pass) {
         if (dump_host) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, sm));
@@ -1956,7 +2055,8 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                         [&](auto K, const TravLaunch& l) {
                             launch_bdpt_vis<decltype(K)::value>(l, c.sc, S, B, BR, BI, N, items_total);
                         },
-                        nullptr, c.o.bdpt_top != 0);
+                        // textured scenes (fx 2) have no TOP variant: their full-grid launch
+                        nullptr, c.o.bdpt_top != 0 && c.sc.full != 2);
                 }
                 StageTimer tm(c, c.o.timing, ST_BD_PATHS);
                 const int grid = std::min(ceil_div(totals[1], BLOCK), 1 << 16);
@@ -2103,6 +2203,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         c.stats.tri_tests[k] += tc[k * TC_N + TC_TRI];
     }
     c.stats.shadow_resolved += tc[TC_RESOLVED];
+    c.stats.tail_queries += tc[TC_TAILQ];
 #if LUMO_SHADOW_STATS || LUMO_PHASE_CLOCKS
     {
         unsigned long long ss[TC_STATS];
@@ -2311,14 +2412,36 @@ lumo_status lumo_create(int device, void** ctx_out) {
         delete c;
         return LUMO_ERR_OOM;
     }
-    // the environment's overrides of the defaults (out-of-range values are clamped)
+    // the environment's overrides of the defaults: integers; the 0 / 1 switches also take
+    // on / off, true / false, yes / no.  A value that does not parse is ignored and an
+    // out-of-range one clamped, each with a one-line warning on stderr
     for (int k = 0; k < LUMO_OPT_COUNT; ++k) {
         const char* e = std::getenv(kOptEnv[k]);
         if (!e || !*e) continue;
         int64_t lo = 0, hi = 0;
         opt_range(*c, k, lo, hi);
-        const int64_t v = std::min(hi, std::max(lo, (int64_t)std::strtoll(e, nullptr, 10)));
-        if (set_opt(*c, k, v) != LUMO_OK && k == LUMO_OPT_BOUNCE_THREADS) (void)set_opt(*c, k, BLOCK);
+        char* end = nullptr;
+        int64_t v = (int64_t)std::strtoll(e, &end, 10);
+        if (end == e || *end != '\0') {
+            auto is = [&](const char* w) { return strcasecmp(e, w) == 0; };
+            const bool sw = lo == 0 && hi == 1;
+            if (sw && (is("on") || is("true") || is("yes"))) {
+                v = 1;
+            } else if (sw && (is("off") || is("false") || is("no"))) {
+                v = 0;
+            } else {
+                fprintf(stderr, "lumo_amd: %s=%s is not a number; ignored\n", kOptEnv[k], e);
+                continue;
+            }
+        }
+        if (v < lo || v > hi) {
+            const int64_t cl = std::min(hi, std::max(lo, v));
+            fprintf(stderr, "lumo_amd: %s=%s outside [%lld, %lld]; using %lld\n", kOptEnv[k], e, (long long)lo,
+                    (long long)hi, (long long)cl);
+            v = cl;
+        }
+        if (set_opt(*c, k, v) != LUMO_OK)
+            fprintf(stderr, "lumo_amd: %s=%s not accepted; default kept\n", kOptEnv[k], e);
     }
     *ctx_out = c;
     return LUMO_OK;
@@ -2666,9 +2789,11 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
             s.off_top_lnodes = put(lbvh.data(), sizeof(DBvh) * nl);
             s.top_onodes = (int32_t)no;
             s.top_lnodes = (int32_t)nl;
-            // kd stack entries per thread in LDS after the TOP set (TOP_BLOCK threads, 12 B each)
+            // kd stack entries per thread in LDS after the TOP set (TOP_BLOCK threads, 12 B each),
+            // within the same budget (LUMO_OPT_TOP_KB caps the TOP kernels' whole LDS use)
             const size_t aligned = (top.size() + 15) & ~(size_t)15;
-            size_t room = c->lds_block > aligned + 256 ? c->lds_block - aligned - 256 : 0;
+            const size_t lim = std::min(cap, c->lds_block);
+            size_t room = lim > aligned + 256 ? lim - aligned - 256 : 0;
             s.kst_cfg = c->o.kd_lds > 0 ? (int32_t)std::min<size_t>((size_t)c->o.kd_lds, room / (12 * (size_t)TOP_BLOCK)) : 0;
             room -= 12 * (size_t)TOP_BLOCK * s.kst_cfg;
             // then, in what is left, the first treelets of the largest kd tree (its top levels: the
@@ -2919,6 +3044,7 @@ lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info) {
     info->top_object_nodes = c->sc.top_onodes;
     info->top_light_nodes = c->sc.top_lnodes;
     info->top_kd_nodes = top ? c->sc.top_kd_n : 0;
+    info->top_shm = top ? (int32_t)c->sc.top_shm : 0;
     return LUMO_OK;
 }
 

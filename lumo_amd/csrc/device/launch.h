@@ -32,8 +32,7 @@ template <int STK>
 void launch_shadow_q(const TravLaunch& l, const DScene& sc, const Paths& S, const QState& nxt);
 template <int STK>
 void launch_bounce_q(const TravLaunch& l, const DScene& sc, const Paths& S, const Tasks& T, const QState& cur,
-                     const QState& nxt, uint32_t tail_below, bool tail_only, int dyn, int threads,
-                     int32_t vlo = 0, int32_t vhi = 0x7fffffff);
+                     const QState& nxt, uint32_t tail_below, bool tail_only, int dyn, int threads);
 template <int STK>
 void launch_trace(int grid, hipStream_t sm, const DScene& sc, const double* o, const double* d, const int32_t* light,
                   int n, int any_hit, double* t_out, int32_t* kind_out, int32_t* obj_out, int32_t* prim_out,
@@ -63,8 +62,7 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
                                              uint32_t);                                                           \
     extern template void launch_shadow_q<K>(const TravLaunch&, const DScene&, const Paths&, const QState&);        \
     extern template void launch_bounce_q<K>(const TravLaunch&, const DScene&, const Paths&, const Tasks&,        \
-                                            const QState&, const QState&, uint32_t, bool, int, int, int32_t,      \
-                                            int32_t);                                                             \
+                                            const QState&, const QState&, uint32_t, bool, int, int);             \
     extern template void launch_trace<K>(int, hipStream_t, const DScene&, const double*, const double*,          \
                                          const int32_t*, int, int, double*, int32_t*, int32_t*, int32_t*,         \
                                          unsigned long long*, bool);                                              \

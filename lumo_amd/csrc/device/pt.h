@@ -263,9 +263,15 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
                 sq.HD(SH_UV + 1, sp) = ho.uv.y;
                 sq.HI(SHI_MAT, sp) = ho.material;
                 sq.HI(SHI_BACK, sp) = ho.backface ? 1 : 0;
-                sq.HR(0, sp) = rng.hi;
-                sq.HR(1, sp) = rng.lo;
-                for (int k = 0; k < NEE_DRAWS * ns; ++k) xs_step(rng);
+                // each pair's starting RNG state (pair i starts 6 i draws in), so k_nee_gen reads
+                // one state per pair instead of stepping past the draws of the pairs before it
+                // (O(n_shadow^2) steps per path: C3 ~330 instead of 66)
+                for (int i = 0; i < ns; ++i) {
+                    const size_t r = (size_t)i * sq.hcap + sp;
+                    sq.HR(0, r) = rng.hi;
+                    sq.HR(1, r) = rng.lo;
+                    for (int k = 0; k < NEE_DRAWS; ++k) xs_step(rng);
+                }
                 n_sh = (uint32_t)ns;  // the L records; k_nee_fold adds the valid B records
             } else {
                 for (int i = 0; i < ns; ++i)
@@ -478,8 +484,9 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) vo
 }
 
 // n_shadow > 1: the NEE pairs of this bounce, one thread per pair (path p, light sample i), from the
-// header k_shade_q wrote; the path's RNG is stepped past the draws of pairs 0..i-1 (6 each), so
-// every pair draws exactly what the path's loop over i would have drawn.
+// header k_shade_q wrote; the pair's RNG state is the path's after the draws of pairs 0..i-1 (6
+// each, stored per pair by k_shade_q), so every pair draws exactly what the path's loop over i
+// would have drawn.
 // The pair's records that need a walk go to the bounce's visibility query list (k_shadow_q): the
 // L record unless its BSDF pdf is 0, the B record when it exists and its pdf is not 0 (those
 // contribute 0 whatever the visibility, integrator.rs:146: k_nee_fold adds 0 for them).
@@ -522,8 +529,7 @@ __global__ __launch_bounds__(BLOCK, LUMO_NEE_WAVES) void k_nee_gen(DScene sc, Pa
         const V3 wo{sq.HD(SH_WO, p), sq.HD(SH_WO + 1, p), sq.HD(SH_WO + 2, p)};
         double L[NS];
         for (int k = 0; k < NS; ++k) L[k] = sq.HD(SH_L + k, p);
-        Xorshift rng{sq.HR(0, p), sq.HR(1, p)};
-        for (int k = 0; k < NEE_DRAWS * i; ++k) xs_step(rng);
+        Xorshift rng{sq.HR(0, r), sq.HR(1, r)};  // k_shade_q stepped it past pairs 0..i-1
         const lumo_material m = sc.mats[ho.material];
         const bool ok = nee_pair<FX>(sc, sq, r, ho, m, wo, L, rng);
         live_l = !LUMO_SKIP_DEAD || sq.D(SD_LPS, r) != 0.0;
@@ -803,13 +809,12 @@ __device__ __forceinline__ void store_final(const Paths& S, const PathReg& P) { 
 // continuation, compacted into `nxt` at once (with the NEE term pending, as k_shade_q); then the
 // pair's two traversals from registers, the term delivered into the continuation's entry or the
 // final radiance (as k_shadow_q).  Neither hits nor records go through HBM.
-// TAIL takes only the paths whose (virtual) slot is in [vlo, vhi): the pipeline's merged passes
-// run their tails pass by pass (each needs its previous pass's ring for Russian roulette).
+// The pipeline's merged passes run their tails pass by pass (each needs its previous pass's ring
+// for Russian roulette): k_split_passes first cuts the unit's queue into one segment per pass.
 template <int STK, bool LDS, int FX, bool TAIL>
 __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_q(DScene sc0, Paths S, Tasks T,
                                                                                   QState cur, QState nxt,
-                                                                                  uint32_t tail_below, int dyn,
-                                                                                  int32_t vlo, int32_t vhi) {
+                                                                                  uint32_t tail_below, int dyn) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
     if ((count < tail_below) != TAIL) return;      // the other kernel takes this bounce
@@ -821,8 +826,6 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
         for (uint32_t w0 = wave_fetch(S.counts + CNT_FETCH_T); w0 < count; w0 = wave_fetch(S.counts + CNT_FETCH_T)) {
             const uint32_t q = w0 + lane_id();
             if (q >= count) continue;
-            const int32_t vs = cur.I(QI_SLOT, q);
-            if (vs < vlo || vs >= vhi) continue;  // another pass of a merged unit
             PathReg P = load_path(cur, q);
             while (bounce_path<STK, FX>(sc, T.delta, P, Cc, Cs)) tailq++;
             store_final(S, P);

@@ -130,7 +130,7 @@ struct ShadowQ {
     size_t cap;
     double* hd;    // SH_* planes, hcap paths
     int32_t* hi;   // SHI_* planes
-    uint64_t* hr;  // path RNG at the start of its NEE draws (hi, lo), n_shadow > 1
+    uint64_t* hr;  // n_shadow > 1: per pair r, the path's RNG at the start of the pair's draws (hi, lo)
     int32_t* ql;   // n_shadow > 1: the bounce's visibility queries, 2 * pair + (0: L record, 1: B record)
     size_t hcap;
     uint32_t seg;  // paths per bucket segment
@@ -138,7 +138,7 @@ struct ShadowQ {
     __device__ __forceinline__ int32_t& I(int k, size_t r) const { return i[(size_t)k * cap + r]; }
     __device__ __forceinline__ double& HD(int k, size_t p) const { return hd[(size_t)k * hcap + p]; }
     __device__ __forceinline__ int32_t& HI(int k, size_t p) const { return hi[(size_t)k * hcap + p]; }
-    __device__ __forceinline__ uint64_t& HR(int k, size_t p) const { return hr[(size_t)k * hcap + p]; }
+    __device__ __forceinline__ uint64_t& HR(int k, size_t r) const { return hr[(size_t)k * cap + r]; }
 };
 
 // Per-slot state.  The path tracer keeps only the camera sampler state, the raster position and

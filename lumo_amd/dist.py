@@ -54,16 +54,21 @@ class TileQueue:
     retry) cannot pair up with another render's queue.  When the iteration over a queue ends,
     every rank adds the tiles it took to a per-key total and, after a barrier, checks that
     the total is the frame's tile count (`verify`), so a lost or doubled tile raises instead of
-    silently changing the reduced film.  `key=` (with a bare store, no process group) skips both,
-    for single-process use.
+    silently changing the reduced film.  `key=` skips both and needs no process group (a bare
+    store, single-process use); without `key=` the queue needs an initialised torch.distributed
+    process group even when `store=` is given.  The coverage check waits on the store with a
+    deadline (`timeout` seconds) rather than in a barrier, so a rank that failed mid-render turns
+    into an error on the others instead of a hang until the backend's timeout.
 
     `chunk` defaults to half of one rank's static share: every claim is one more render call with
     fewer paths in flight and its own pipeline fill and drain (C1 1024² @ 64 spp, two ranks on one
     GPU: static 221 ms per frame; chunks of 1/2, 1/4, 1/8 share 266, 348, 435 ms; profiles/r03/dist),
     so claims stay few and large."""
 
-    def __init__(self, width, height, world_size, chunk=None, store=None, key=None, group=None):
+    def __init__(self, width, height, world_size, chunk=None, store=None, key=None, group=None,
+                 timeout=300.0):
         self.collective = key is None
+        self.timeout = float(timeout)
         if store is None:
             import torch.distributed as dist
             store = dist.distributed_c10d._get_default_store()
@@ -96,9 +101,18 @@ class TileQueue:
         """Collective, after this rank's last chunk: the chunks the ranks iterated over cover the
         frame (claims are disjoint by construction; this catches tiles claimed but not taken
         through the iteration, or a rank on another frame size)."""
+        import time
         import torch.distributed as dist
         self.store.add(self.key + "/done", self.claimed)
-        dist.barrier(group=self.group)
+        self.store.add(self.key + "/ranks", 1)
+        ws = dist.get_world_size(self.group)
+        deadline = time.monotonic() + self.timeout
+        while int(self.store.add(self.key + "/ranks", 0)) < ws:
+            if time.monotonic() > deadline:
+                arrived = int(self.store.add(self.key + "/ranks", 0))
+                raise RuntimeError(f"tile queue {self.key}: only {arrived} of {ws} ranks finished their "
+                                   f"tiles within {self.timeout:.0f} s (a rank failed mid-render?)")
+            time.sleep(0.005)
         total = int(self.store.add(self.key + "/done", 0))
         if total != self.n_tiles:
             raise RuntimeError(f"tile queue {self.key}: {total} tiles handed out, the frame has {self.n_tiles}")

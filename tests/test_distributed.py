@@ -239,6 +239,9 @@ def _verify_worker(rank, ws, port, out_dir):
     ok = 0
     if rank == 0:
         q.claim()  # a chunk handed out but never taken through the iteration: its tiles are lost
+    # the lost chunk must be claimed before either rank iterates, or rank 1 may drain the queue
+    # first and rank 0's claim comes back empty (nothing lost, nothing to detect)
+    dist.barrier()
     try:
         for _ in q:
             pass
@@ -255,3 +258,35 @@ def test_tile_queue_detects_lost_tiles(tmp_path):
     reducing a film with missing tiles."""
     _spawn(_verify_worker, 2, str(tmp_path))
     assert [int(np.load(tmp_path / f"raised{r}.npy")[0]) for r in range(2)] == [1, 1]
+
+
+def _failed_rank_worker(rank, ws, port, out_dir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+    import time
+    import torch.distributed as dist
+    from lumo_amd.dist import TileQueue
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=ws)
+    q = TileQueue(W, H, ws, chunk=2, timeout=2.0)
+    msg = ""
+    t0 = time.monotonic()
+    if rank == 0:
+        try:
+            for _ in q:
+                pass
+        except RuntimeError as e:
+            msg = str(e)
+    # rank 1 "fails mid-render": it never iterates to the end of the queue, so never reaches verify
+    np.save(os.path.join(out_dir, f"failed{rank}.npy"), np.array([len(msg) > 0, time.monotonic() - t0]))
+    with open(os.path.join(out_dir, f"msg{rank}.txt"), "w") as f:
+        f.write(msg)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tile_queue_failed_rank_raises_not_hangs(tmp_path):
+    """A rank that never finishes its tiles: the others' coverage check gives up at the queue's
+    deadline with an error naming the missing ranks, instead of blocking in a barrier."""
+    _spawn(_failed_rank_worker, 2, str(tmp_path))
+    r0 = np.load(tmp_path / "failed0.npy")
+    assert bool(r0[0]) and r0[1] < 30
+    assert "1 of 2 ranks" in (tmp_path / "msg0.txt").read_text()

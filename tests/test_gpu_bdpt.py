@@ -187,3 +187,29 @@ def test_c4_full_frame_tiles_match_oracle(dev):
         assert len(sp[i]) == len(os_)
         np.testing.assert_array_equal(sp[i]["rgb"], os_["rgb"])
         np.testing.assert_array_equal(sp[i]["x"], os_["x"])
+
+
+def test_bdpt_textured_large_scene(dev):
+    """A textured scene too large to stage whole (the caustics scene plus a marble / Mandelbrot
+    checkerboard cube: feature class 2, which has no TOP variant of the (b)-item visibility): the
+    visibility runs on its full-grid fallback, and every tile, count and splat equals the oracle's."""
+    from scenes import cube_obj
+    sc = scenes.caustics()
+    marble = L.Texture.marble(99, L.Spectrum.from_rgb(0.8, 0.75, 0.7))
+    sc.add_obj(cube_obj((0.0, -0.6, -1.7), 0.35, rot_y=0.3),
+               L.Material.diffuse(L.Texture.checkerboard(marble, L.Texture.mandelbrot(), 5.0)))
+    cam = scenes.caustics_camera((48, 32))
+    sc.build()
+    dev.upload(sc, cam)
+    info = dev.scene_info()
+    assert info.lds_bytes == 0 and info.top_bytes > 0 and info.full_kernels == 2
+    tasks = L.make_tasks(48, 32, 4, 0x7E7)
+    sp = []
+    bufs, rr = dev.render_tasks(tasks, integrator=BDPT, splats_out=sp)
+    osp = []
+    obufs, orr, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8, integrator=BDPT, splats_out=osp)
+    assert sum(len(s) for s in osp) > 0
+    for b, ob, r, o, s, os_ in zip(bufs, obufs, rr, orr, sp, osp):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries, r.num_camera_rays) == (o.num_rays, o.num_queries, o.num_camera_rays)
+        np.testing.assert_array_equal(s["rgb"], os_["rgb"])

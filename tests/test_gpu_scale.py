@@ -279,7 +279,7 @@ def test_split_pipeline_passes_in_flight(mid_bistro, k, groups):
     independent groups; a 9-pass render's tiles, ray and query counts equal the oracle's (a unit
     waits for its group's previous pass's camera, and its ring before bounce RR_DEPTH and before
     its film; set reuse is ordered by stream)."""
-    d = L.Device(0, split_pipe=k, split_groups=groups)
+    d = L.Device(0, split_pipe=k, split_groups=groups, merge_passes=1)  # one-pass units (merged: below)
     cam = scenes.bistro_camera((64, 48))
     d.upload(mid_bistro, cam)
     assert d.scene_info().n_shadow > 1
@@ -300,6 +300,77 @@ def test_split_pipeline_passes_in_flight(mid_bistro, k, groups):
         assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
     assert after.closest_queries - before.closest_queries == cnt.closest_queries
     assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
+
+
+@pytest.mark.parametrize("scene,merge,k,groups", [("bistro", 8, 4, 2), ("bistro", 2, 4, 2), ("bistro", 3, 3, 1),
+                                                   ("bistro", 8, 4, 4), ("dragon", 8, 4, 2), ("dragon", 4, 2, 2)])
+def test_split_merged_passes(mid_bistro, scene, merge, k, groups):
+    """Merged passes in render_split_pipelined: a unit's camera generates the samples of M passes
+    into one queue, its first RR_DEPTH bounces run them at once (they read no delta,
+    path_trace.rs:60-69), k_split_passes cuts the queue by pass, and each pass runs its remaining
+    bounces (the tail kernel included, n_shadow = 1) after the ring before it.  Opt-in (option
+    merge_passes; measured slower at C3's share).  9 passes (a ragged last unit),
+    M = 2 / 3 / 4 / 8: tiles, ray and query counts equal sequential passes and the oracle's."""
+    if scene == "bistro":
+        sc, cam = mid_bistro, scenes.bistro_camera((64, 48))
+    else:
+        sc = scenes.dragon(torus_knot_tube(300, 12)).build()
+        cam = scenes.default_camera((64, 48))
+    d = L.Device(0, split_pipe=k, split_groups=groups, merge_passes=merge, tail_below=300)
+    try:
+        d.upload(sc, cam)
+        tasks = L.make_tasks(64, 48, 9, SEED)
+        before = d.stats()
+        bufs, res = d.render_tasks(tasks)
+        after = d.stats()
+        sch = d.last_schedule()
+        assert (sch.schedule, sch.units_in_flight, sch.task_groups) == (2, k, min(groups, k))
+        assert sch.merged_passes == merge
+        if scene == "dragon":
+            assert after.tail_queries > before.tail_queries
+        d.set_option("split_pipe", 1)
+        seq, seq_res = d.render_tasks(tasks)
+        assert d.last_schedule().schedule == 0
+    finally:
+        d.close()
+    obufs, ores, cnt = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+    for b, sb, ob, r, sr, orr in zip(bufs, seq, obufs, res, seq_res, ores):
+        np.testing.assert_array_equal(b, ob)
+        np.testing.assert_array_equal(sb, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+        assert (sr.num_rays, sr.num_queries) == (orr.num_rays, orr.num_queries)
+    assert after.closest_queries - before.closest_queries == cnt.closest_queries
+    assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
+
+
+def test_c3_share_merged_passes(c3):
+    """One rank's share of the 8-GPU C3 run (the tiles with tile % 8 == 0 of 1920x1080, 261 k slots
+    per pass) at 16 spp with merged passes (merge_passes 8): 4 units of 8 passes in flight in 2 task
+    groups.  Every tile, ray and query count equals sequential passes; every 8th tile the oracle's."""
+    from lumo_amd.dist import shard_tasks
+    W, H, spp = 1920, 1080, 16
+    cam = scenes.bistro_camera((W, H))
+    tasks = shard_tasks(L.make_tasks(W, H, spp, SEED), W, H, 0, 8)
+    d = L.Device(0, merge_passes=8)
+    try:
+        d.upload(c3, cam)
+        bufs, res = d.render_tasks(tasks, max_paths=1 << 23)
+        sch = d.last_schedule()
+        assert (sch.schedule, sch.units_in_flight, sch.task_groups, sch.merged_passes) == (2, 4, 2, 8)
+        d.set_option("split_pipe", 1)
+        seq, seq_res = d.render_tasks(tasks, max_paths=1 << 23)
+        assert d.last_schedule().schedule == 0
+    finally:
+        d.close()
+    for b, s, r, sr in zip(bufs, seq, res, seq_res):
+        np.testing.assert_array_equal(b, s)
+        assert (r.num_rays, r.num_queries) == (sr.num_rays, sr.num_queries)
+    sub = list(range(0, len(tasks), 8))
+    obufs, ores, _ = O.render_tasks(c3.desc(), cam.desc, [tasks[i] for i in sub], O.WAVEFRONT, oracle_threads())
+    bad = [i for i, ob in zip(sub, obufs) if not np.array_equal(bufs[i], ob)]
+    assert not bad, f"{len(bad)} of {len(sub)} sampled tiles differ, first {bad[:8]}"
+    for i, orr in zip(sub, ores):
+        assert (res[i].num_rays, res[i].num_queries) == (orr.num_rays, orr.num_queries)
 
 
 def test_c3_bench_schedule_full_frame(c3):
@@ -337,6 +408,70 @@ def test_c3_bench_schedule_full_frame(c3):
     for i, orr in zip(sub, ores):
         assert (res[i].num_rays, res[i].num_queries) == (orr.num_rays, orr.num_queries)
     assert after.closest_queries > before.closest_queries
+
+
+def test_c2_bench_schedule_full_frame(c2):
+    """C2 as the bench renders it: the full 1920x1080 dragon stand-in frame (8 160 tiles, 2.07 M
+    slots per pass, n_shadow = 1, kd stack class 48, not LDS-staged: three-kernel bounces) through
+    render_split_pipelined with 4 units in flight in 2 task groups at 2 spp, the tail kernel taking
+    over on the device once a pass holds fewer than 2^16 live paths (asserted: tail queries > 0).
+    Every tile, ray and query count equals the same frame with sequential passes, and every 64th
+    tile equals the oracle's (task.rs:25-82 pass order, renderer.rs:179-204 tasks)."""
+    W, H, spp = 1920, 1080, 2
+    cam = scenes.default_camera((W, H))
+    tasks = L.make_tasks(W, H, spp, SEED)
+    d = L.Device(0)
+    try:
+        d.upload(c2, cam)
+        info = d.scene_info()
+        assert info.n_shadow == 1 and info.stack_class == 48 and info.lds_bytes == 0 and info.top_kd_nodes > 0
+        assert d.option("tail_below") == 1 << 16
+        before = d.stats()
+        bufs, res = d.render_tasks(tasks, max_paths=1 << 23)
+        after = d.stats()
+        sch = d.last_schedule()
+        assert (sch.schedule, sch.units_in_flight, sch.task_groups, sch.fused) == (2, 4, 2, 0)
+        assert after.tail_queries > before.tail_queries  # the mid-pass hand-over to the tail kernel ran
+        d.set_option("split_pipe", 1)
+        b2 = d.stats()
+        seq, seq_res = d.render_tasks(tasks, max_paths=1 << 23)
+        a2 = d.stats()
+        assert d.last_schedule().schedule == 0
+        # the same closest queries in all (where the tail kernel takes over differs: a task group's
+        # unit holds half the frame's paths, so it drops below 2^16 live paths bounces earlier)
+        assert a2.closest_queries - b2.closest_queries == after.closest_queries - before.closest_queries
+    finally:
+        d.close()
+    for b, s, r, sr in zip(bufs, seq, res, seq_res):
+        np.testing.assert_array_equal(b, s)
+        assert (r.num_rays, r.num_queries) == (sr.num_rays, sr.num_queries)
+    sub = list(range(0, len(tasks), 64))
+    obufs, ores, _ = O.render_tasks(c2.desc(), cam.desc, [tasks[i] for i in sub], O.WAVEFRONT, oracle_threads())
+    bad = [i for i, ob in zip(sub, obufs) if not np.array_equal(bufs[i], ob)]
+    assert not bad, f"{len(bad)} of {len(sub)} sampled tiles differ, first {bad[:8]}"
+    for i, orr in zip(sub, ores):
+        assert (res[i].num_rays, res[i].num_queries) == (orr.num_rays, orr.num_queries)
+
+
+@pytest.mark.parametrize("top_kb", [24, 64, 160])
+def test_top_budget_caps_lds(top_kb):
+    """LUMO_OPT_TOP_KB caps the TOP kernels' whole LDS use: the TOP set, the kd stack columns and
+    the kd treelets together (top_shm) stay within the budget, and the tiles equal the oracle's."""
+    sc = scenes.dragon(torus_knot_tube(300, 12)).build()
+    d = L.Device(0, top_kb=top_kb)
+    try:
+        cam = scenes.default_camera((64, 48))
+        d.upload(sc, cam)
+        info = d.scene_info()
+        assert 0 < info.top_shm <= top_kb * 1024
+        tasks = L.make_tasks(64, 48, 4, SEED)[:6]
+        bufs, res = d.render_tasks(tasks)
+    finally:
+        d.close()
+    obufs, ores, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
 
 
 @pytest.mark.parametrize("top_kd,kd_lds", [(1, 8), (1, 4), (1, 0), (0, 8)])
