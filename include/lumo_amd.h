@@ -419,6 +419,11 @@ enum {
     LUMO_OPT_BDPT_TOP,         /* BDPT connection visibility (k_bdpt_vis) of scenes too large to stage
                                   whole reads the TOP set and kd stack columns from LDS: 0 / 1
                                   (LUMO_BDPT_TOP, 1)                                                */
+    LUMO_OPT_BDPT_GROUPS,      /* BDPT: task groups rendered as concurrent chains of passes on their own
+                                  streams, 1-4 (LUMO_BDPT_GROUPS, 2; ABI 9)                          */
+    LUMO_OPT_RAY_SORT,         /* three-kernel bounces: the closest-hit rays of a bounce sorted by
+                                  direction octant and origin cell (radix sort) before their walks:
+                                  0 / 1 (LUMO_RAY_SORT, 0; ABI 9)                                    */
     LUMO_OPT_COUNT
 };
 lumo_status lumo_set_option(void* ctx, int32_t option, int64_t value);
@@ -428,14 +433,15 @@ lumo_status lumo_get_option(void* ctx, int32_t option, int64_t* value);
  * pass loop ran and with how many streams, units, groups and merged passes.  Lets callers and
  * tests check that a requested schedule was not cut back (free HBM bounds the split schedule's
  * units in flight). */
-enum { LUMO_SCHED_SEQUENTIAL = 0, LUMO_SCHED_FUSED_PIPELINE = 1, LUMO_SCHED_SPLIT_PIPELINE = 2 };
+enum { LUMO_SCHED_SEQUENTIAL = 0, LUMO_SCHED_FUSED_PIPELINE = 1, LUMO_SCHED_SPLIT_PIPELINE = 2,
+       LUMO_SCHED_BDPT_GROUPS = 3 /* ABI 9 */ };
 typedef struct {
     int32_t schedule;        /* LUMO_SCHED_*                                               */
     int32_t head_streams;    /* fused pipeline: head streams                               */
     int32_t head_bounces;    /* fused pipeline: bounces per pass on the head stream        */
     int32_t merged_passes;   /* fused / split pipeline: passes per head unit               */
-    int32_t units_in_flight; /* split pipeline: (group, pass) units in flight              */
-    int32_t task_groups;     /* split pipeline: independent task groups                    */
+    int32_t units_in_flight; /* split pipeline: (group, pass) units in flight; BDPT groups  */
+    int32_t task_groups;     /* split pipeline / BDPT groups: independent task groups      */
     int32_t fused;           /* 1: fused bounce kernel, 0: three kernels per bounce         */
     int32_t tail_bounces;    /* fused pipeline: fused bounces per pass on the tail stream   */
 } lumo_schedule_info;

@@ -172,7 +172,7 @@ SCHED_SEQUENTIAL, SCHED_FUSED_PIPELINE, SCHED_SPLIT_PIPELINE = range(3)
 OPTIONS = ["timing", "lds_staging", "top_staging", "fused", "tail_below", "pipeline", "heads", "merge_passes",
            "dyn_fetch", "bounce_threads", "split_pipe", "split_groups", "bdpt_tail", "bounce_ahead", "lds_grid",
            "top_grid", "top_kb", "kd_lds", "stack_class", "full_kernels", "poison", "tail_priority", "top_kd",
-           "tail_bounces", "film_first", "bdpt_top"]
+           "tail_bounces", "film_first", "bdpt_top", "bdpt_groups", "ray_sort"]
 OPT = {name: i for i, name in enumerate(OPTIONS)}
 
 

@@ -44,6 +44,14 @@ struct BVtx {
 #ifndef LUMO_VSTORE_AOS
 #define LUMO_VSTORE_AOS 1
 #endif
+// Slot-major records (round 5, default): ((s * V + v) * VD_N + f), so a sample's vertices are
+// contiguous and the connection items of one sample, which read vertices all along both of its
+// subpaths, share the lines they fetch (vertex-major, a 184-B record straddled lines shared with the
+// neighbouring slots' records: the connection unit's traffic was 2.0x its bytes).  C4 8-spp frame
+// 1 026 -> 1 005 ms, 1/8 share 60.0 -> 58.9 s.
+#ifndef LUMO_VSTORE_SLOT
+#define LUMO_VSTORE_SLOT 1
+#endif
 // MIS plane (m, mf): each vertex's pdf_fwd, pdf_bck and flags again, slot-major ((s * V + v)), so
 // the MIS weight of a connection item (mis.rs:103-239), which walks these three fields along both
 // subpaths of its sample, reads them from a few contiguous lines its neighbouring items (the same
@@ -59,7 +67,10 @@ struct VStore {
         D(20, v, s) = bck;
         m[2 * mi(v, s) + 1] = bck;
     }
-#if LUMO_VSTORE_AOS
+#if LUMO_VSTORE_SLOT
+    __device__ __forceinline__ double& D(int f, int v, int s) const { return d[((size_t)s * V + v) * VD_N + f]; }
+    __device__ __forceinline__ int32_t& I(int f, int v, int s) const { return i[((size_t)s * V + v) * VI_N + f]; }
+#elif LUMO_VSTORE_AOS
     __device__ __forceinline__ double& D(int f, int v, int s) const { return d[((size_t)v * N + s) * VD_N + f]; }
     __device__ __forceinline__ int32_t& I(int f, int v, int s) const { return i[((size_t)v * N + s) * VI_N + f]; }
 #else

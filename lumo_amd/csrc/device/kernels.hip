@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -242,6 +243,35 @@ __global__ void k_bounce_begin(uint32_t* counts, unsigned long long* headq) {
         for (int b = 0; b < NB; ++b) counts[CNT_BUCKET0 + b] = 0;
         for (int k = 0; k < SHQ_CLASSES; ++k) counts[CNT_SHQ + k] = 0;
     }
+}
+
+// Ray sorting (LUMO_OPT_RAY_SORT): a 30-bit key per queued ray, the direction octant above a Morton
+// code of the origin (9 bits per axis over the objects BVH's world box); rays past the live count
+// get the largest key, so a stable sort leaves them behind the live ones.  The sort changes which
+// lane walks which ray, nothing else (k_closest_q writes each hit at its ray's own position).
+__device__ __forceinline__ uint32_t spread3(uint32_t x) {  // 9 bits -> every third bit
+    x &= 0x1ffu;
+    x = (x | (x << 16)) & 0x030000ffu;
+    x = (x | (x << 8)) & 0x0300f00fu;
+    x = (x | (x << 4)) & 0x030c30c3u;
+    x = (x | (x << 2)) & 0x09249249u;
+    return x;
+}
+__global__ __launch_bounds__(BLOCK) void k_sort_keys(QState cur, const uint32_t* counts, uint32_t n, V3 lo, V3 scale,
+                                                      uint32_t* keys, uint32_t* vals) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    uint32_t key = 0xffffffffu;
+    if (q < counts[CNT_CUR]) {
+        const V3 o = qv3(cur, QD_O, q), d = qv3(cur, QD_D, q);
+        auto cell = [](double x) { return (uint32_t)(x < 0.0 ? 0.0 : (x > 511.0 ? 511.0 : x)); };
+        const uint32_t m = spread3(cell((o.x - lo.x) * scale.x)) | (spread3(cell((o.y - lo.y) * scale.y)) << 1) |
+                           (spread3(cell((o.z - lo.z) * scale.z)) << 2);
+        const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
+        key = (oct << 27) | m;
+    }
+    keys[q] = key;
+    vals[q] = q;
 }
 
 // Setup zeroing of a render's accumulators and counters in one launch instead of a fill per
@@ -716,11 +746,12 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_taps(DScene sc, Paths S, Bdpt B,
     if (MODE == 0) cnt[slot] = k;
 }
 // first tap of each task in this pass (exclusive scan gathered at the tasks' first slots)
+// (tasks t0 .. t0 + n_tasks - 1 whose slots start at s0: cnt / off are that range's, from its first slot)
 __global__ void k_task_tap_ranges(Tasks T, const uint32_t* cnt, const uint32_t* off, int n_tasks, int n,
-                                  uint64_t* ranges) {
+                                  uint64_t* ranges, int t0 = 0, int s0 = 0) {
     const int ti = blockIdx.x * blockDim.x + threadIdx.x;
     if (ti > n_tasks) return;
-    ranges[ti] = ti < n_tasks ? (uint64_t)off[T.first[ti]] : (uint64_t)off[n - 1] + cnt[n - 1];
+    ranges[ti] = ti < n_tasks ? (uint64_t)off[T.first[t0 + ti] - s0] : (uint64_t)off[n - 1] + cnt[n - 1];
 }
 
 // ------------------------------------------------------------------ PMC calibration (lumo_debug_stream)
@@ -819,6 +850,8 @@ struct Opts {
     int tail_bounces = -1;             // fused pipeline: fused bounces per pass on the tail stream before the tail kernel (-1 auto)
     int bdpt_top = 1;                  // BDPT connection visibility of large scenes with TOP staging
     int film_first = 0;                // fused pipeline, film on the tail stream: the film before the unit's last ring
+    int bdpt_groups = 2;               // BDPT: task groups rendered as concurrent pass chains (render_bdpt_groups)
+    int ray_sort = 0;                  // split bounces: closest-hit rays sorted by origin cell and octant
 };
 
 struct Ctx {
@@ -859,6 +892,11 @@ struct Ctx {
     hipEvent_t ref_ev = nullptr;
     bool ref_recorded = false;
     std::vector<std::pair<float, float>> intervals[LUMO_STAGE_COUNT];
+    // BDPT task groups (render_bdpt_groups): per-group work buffers, pinned item totals, events
+    std::vector<DevBuf> gwork;
+    uint32_t* bd_totals_h = nullptr;
+    hipEvent_t bd_ev[4] = {};
+    V3 sort_lo{0.0, 0.0, 0.0}, sort_scale{0.0, 0.0, 0.0};  // ray sorting: the scene's world box -> 512 cells per axis
 };
 
 lumo_status dev_alloc(const Ctx& c, DevBuf& b, size_t bytes) {
@@ -916,7 +954,8 @@ enum WorkId {
     W_QUERIES4, W_P_VALID4, W_COUNTS4, W_QS6_D, W_QS6_R, W_QS6_I, W_QS7_D, W_QS7_R, W_QS7_I,
     W_SQ_QL, W_BD_LM, W_BD_LMF, W_BD_CM, W_BD_CMF, W_BDR_LM, W_BDR_LMF, W_BDR_CM, W_BDR_CMF,
     W_SPLIT_SET1,  // render_split_pipelined sets 1..3: hits + NEE records, 8 buffers each
-    W_COUNT = W_SPLIT_SET1 + 3 * 8
+    W_SORT_SET0 = W_SPLIT_SET1 + 3 * 8,  // ray sorting of pass set k: keys x 2, values x 2, temp
+    W_COUNT = W_SORT_SET0 + 4 * 5
 };
 
 template <typename T>
@@ -1055,6 +1094,26 @@ void alloc_pass_set(Ctx& c, Paths& Q, int k, int N, lumo_status& st) {
         Q.qs[h].i = wbuf<int32_t>(c, w[9 + 3 * h], QI_N * (size_t)N, st);
     }
 }
+// Ray sorting buffers of pass set k (none when the option is off)
+void alloc_sort(Ctx& c, HitQ& hq, int k, lumo_status& st) {
+    hq.perm = nullptr;
+    hq.sk[0] = hq.sk[1] = hq.sv[0] = hq.sv[1] = nullptr;
+    hq.tmp = nullptr;
+    hq.tmp_bytes = 0;
+    if (!c.o.ray_sort) return;
+    const int w = W_SORT_SET0 + 5 * k;
+    for (int b = 0; b < 2; ++b) {
+        hq.sk[b] = wbuf<uint32_t>(c, w + b, hq.cap, st);
+        hq.sv[b] = wbuf<uint32_t>(c, w + 2 + b, hq.cap, st);
+    }
+    hipcub::DoubleBuffer<uint32_t> kb(hq.sk[0], hq.sk[1]), vb(hq.sv[0], hq.sv[1]);
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, hq.tmp_bytes, kb, vb, (int)hq.cap, 0, 30) != hipSuccess) {
+        st = LUMO_ERR_HIP;
+        return;
+    }
+    hq.tmp = wbuf<char>(c, w + 4, hq.tmp_bytes, st);
+}
+
 // ... and, for the split schedule, the set's closest hits and NEE records (the sizes of set 0's)
 void alloc_split_set(Ctx& c, Paths& Q, const Paths& S, int k, int ns, lumo_status& st) {
     const int w = W_SPLIT_SET1 + 8 * (k - 1);
@@ -1066,6 +1125,7 @@ void alloc_split_set(Ctx& c, Paths& Q, const Paths& S, int k, int ns, lumo_statu
     Q.sq.hi = wbuf<int32_t>(c, w + 5, SHI_N * S.sq.hcap, st);
     Q.sq.hr = ns > 1 ? wbuf<uint64_t>(c, w + 6, 2 * S.sq.cap, st) : nullptr;
     Q.sq.ql = ns > 1 ? wbuf<int32_t>(c, w + 7, SHQ_CLASSES * S.sq.cap, st) : nullptr;
+    alloc_sort(c, Q.hq, k, st);
 }
 // Device bytes of one extra pass set of the split schedule.
 size_t split_set_bytes(const Paths& S, int N, int ns) {
@@ -1268,6 +1328,7 @@ lumo_status render_pipelined(Ctx& c, Paths& S, const Tasks& T, Dump& D, int dump
 // (+ NEE pair generation when n_shadow > 1) -> visibility (+ the NEE fold).  `ub` is an upper bound
 // on the live count (grids); the kernels read the exact count from S.counts.  allow_tail = false:
 // the bounce must not run paths through Russian roulette (a merged head, which reads no delta).
+constexpr uint32_t kSortMin = 1u << 15;  // ray sorting only for bounces with at least this many rays
 void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, const QState& nxt, uint32_t ub,
                         hipStream_t sm, bool fused_now, bool allow_tail = true) {
     const int ns = c.sc.n_shadow;
@@ -1291,10 +1352,20 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
         }, sm);
         return;
     }
+    Paths Sc = S;  // the closest-hit launch's view: with the queue's sort order when rays are sorted
+    if (c.o.ray_sort && S.hq.tmp && ub >= kSortMin && (uint64_t)ub <= S.hq.cap) {
+        StageTimer tm(c, c.o.timing, ST_CLOSEST, sm);
+        k_sort_keys<<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(cur, S.counts, ub, c.sort_lo, c.sort_scale, S.hq.sk[0],
+                                                           S.hq.sv[0]);
+        hipcub::DoubleBuffer<uint32_t> kb(S.hq.sk[0], S.hq.sk[1]), vb(S.hq.sv[0], S.hq.sv[1]);
+        size_t tb = S.hq.tmp_bytes;
+        if (hipcub::DeviceRadixSort::SortPairs(S.hq.tmp, tb, kb, vb, (int)ub, 0, 30, sm) == hipSuccess)
+            Sc.hq.perm = vb.Current();
+    }
     {
         StageTimer tm(c, c.o.timing, ST_CLOSEST, sm);
         launch_trav(
-            c, ub, [&](auto K, const TravLaunch& l) { launch_closest_q<decltype(K)::value>(l, c.sc, S, cur, skip); },
+            c, ub, [&](auto K, const TravLaunch& l) { launch_closest_q<decltype(K)::value>(l, c.sc, Sc, cur, skip); },
             sm, true);
     }
     {
@@ -1636,6 +1707,416 @@ lumo_status render_split_pipelined(Ctx& c, Paths& S, const Tasks& T, int N, int 
     return LUMO_OK;
 }
 
+// BDPT in task groups (render_impl, bidirectional integrator): the tasks are cut into G groups of
+// consecutive tasks, each rendered as its own chain of passes on its own stream, with its own view
+// of the per-slot buffers (offset to its first slot), its own walk queues, counters, redo list and
+// store, connection item lists and scan storage.  lumo's adaptive Russian roulette reads a task's
+// delta in the walks (path_gen.rs:133-145) and the delta of pass p needs that task's ring of pass
+// p - 1 (task.rs:28-53): within a group the passes follow one another on the group's stream, as in
+// the sequential loop; groups share nothing but the scene, the task table and the splat film
+// (atomics: its sum order is unspecified anyway), so their chains overlap freely: one group's
+// latency-bound walk tails and connection traces run beside the other's item kernels.  The host
+// drives every group's pass as a state machine (walk bounces issued `ahead` of their count
+// snapshots; the item totals read back through pinned memory when their event completes), so it
+// waits for nothing a group needs.  Every per-sample operation, every item and every film / ring
+// sum of a task is the sequential loop's, in the same order: bit-identical.  (Per-task splat lists,
+// the test / library path, are read back with a blocking wait per pass.)
+enum BdPhase { BD_LIGHT = 0, BD_CAMERA, BD_TOTALS, BD_DONE };
+struct BdGroup {
+    int t0, t1, s0, n;
+    hipStream_t sm;
+    Paths S;
+    Bdpt B, R;
+    BItems I;
+    uint32_t* totals;  // device: (a), (b) item totals of the pass
+    uint64_t pass = 0;
+    int phase = BD_LIGHT;
+    int issued = 0, consumed = 0, seg_first = 0, walk = 0;  // snapshots; bounces of the current walk
+    uint32_t ub = 0;
+    bool done = false;
+};
+
+// Per-group work buffers (k: BdBuf), grown on demand like the render's own.
+enum BdBuf { BG_TERM_A, BG_TERM_B, BG_VIS, BG_AT, BG_AKIND, BG_AOBJ, BG_ATRI, BG_SCAN, BG_RANGES, BG_TAPS,
+             BG_RLD, BG_RLI, BG_RCD, BG_RCI, BG_RSP, BG_RSPN, BG_RDRAWS, BG_ROK, BG_RLM, BG_RLMF, BG_RCM, BG_RCMF,
+             BG_REDO, BG_COUNT };
+template <typename T>
+T* gbuf(Ctx& c, int g, int k, size_t count, lumo_status& st) {
+    if (c.gwork.size() < (size_t)4 * BG_COUNT) c.gwork.resize((size_t)4 * BG_COUNT);
+    const lumo_status s = dev_alloc(c, c.gwork[(size_t)g * BG_COUNT + k], sizeof(T) * count);
+    if (s) st = s;
+    return static_cast<T*>(c.gwork[(size_t)g * BG_COUNT + k].p);
+}
+
+// A store of `n` slots carved out of one of `total` slots at slot s0 (every plane is (fields x V) x
+// slots with the slot index innermost of the (v, slot) pair, so a group's range is contiguous).
+VStore vstore_part(const VStore& v, int s0, int n) {
+    const size_t o = (size_t)v.V * (size_t)s0;
+    return VStore{v.d + o * VD_N, v.i + o * VI_N, v.V, n, v.m + 2 * o, v.mf + o};
+}
+
+lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, const BItems& BI, int N, int n_tasks,
+                               int dim_stride, uint64_t max_samples, uint64_t max_P, int G,
+                               const std::vector<int32_t>& first, uint32_t* items_total, bool splat_lists, double* dfilm, uint32_t* tap_cnt,
+                               uint32_t* tap_off, lumo_tile_result* out, std::vector<uint64_t>& n_splats,
+                               uint64_t& bounces, lumo_status& st) {
+    struct JoinOnError {
+        Ctx& c;
+        bool ok = false;
+        ~JoinOnError() {
+            if (ok) return;
+            for (hipStream_t s : {c.stream2, c.stream3, c.stream4, c.stream})
+                if (s) (void)hipStreamSynchronize(s);
+        }
+    } join{c};
+    G = std::max(1, std::min(std::min(G, 4), n_tasks));
+    hipStream_t Ss[4] = {c.stream, c.stream2, c.stream3, c.stream4};
+    std::vector<BdGroup> gr(G);
+    const int V = B.lp.V, VR = BDPT_MAX_DEPTH + 1;
+    for (int g = 0, t = 0; g < G; ++g) {  // groups of consecutive tasks, about N / G slots each
+        BdGroup& q = gr[g];
+        q.t0 = t;
+        const int64_t target = (int64_t)N * (g + 1) / G;
+        while (t < n_tasks && (g == G - 1 || first[t + 1] <= target || t == q.t0)) ++t;
+        t = std::max(std::min(t, n_tasks - (G - 1 - g)), q.t0 + 1);
+        q.t1 = t;
+        q.s0 = first[q.t0];
+        q.n = first[q.t1] - q.s0;
+        q.sm = Ss[g];
+        const size_t o = (size_t)q.s0;
+        Paths& P = q.S;
+        P = S;
+        P.ro = S.ro + 3 * o;
+        P.rd = S.rd + 3 * o;
+        P.gath = S.gath + 4 * o;
+        P.rad = S.rad + 4 * o;
+        P.lam = S.lam + 4 * o;
+        P.raster = S.raster + 2 * o;
+        P.rng = S.rng + 2 * o;
+        P.depth = S.depth + o;
+        P.flags = S.flags + o;
+        P.queries = S.queries + o;
+        P.task = S.task + o;
+        P.pix = S.pix + o;
+        P.pseed = S.pseed + o;
+        P.mj_rng = S.mj_rng + 2 * o;
+        P.mj_state = S.mj_state + o;
+        P.perm = S.perm + 2 * (size_t)dim_stride * o;
+        P.hit_t = S.hit_t + o;
+        P.hit_kind = S.hit_kind + o;
+        P.hit_obj = S.hit_obj + o;
+        P.hit_tri = S.hit_tri + o;
+        P.p_rgb = S.p_rgb + 3 * o;
+        P.p_valid = S.p_valid + o;
+        P.film = S.film + 4 * o;
+        P.q0 = S.q0 + o;
+        P.q1 = S.q1 + o;
+        P.counts = S.counts + (size_t)g * CNT_N;  // zeroed at setup, then by the group's rings
+        Bdpt& X = q.B;
+        X = B;
+        X.lp = vstore_part(B.lp, q.s0, q.n);
+        X.cp = vstore_part(B.cp, q.s0, q.n);
+        X.sp = SplatStore{B.sp.d + (size_t)10 * V * o, B.sp.n + o, V, q.n};
+        X.draws = B.draws + (size_t)5 * V * o;
+        X.ok = B.ok + (size_t)V * o;
+        X.overflow = B.overflow + 2 * g;  // per group: overflow flag, redo count
+        X.redo_count = X.overflow + 1;
+        X.redo_cap = (uint32_t)std::min(q.n, 4096);
+        X.redo_list = gbuf<int32_t>(c, g, BG_REDO, X.redo_cap, st);
+        X.redo_index = B.redo_index + o;
+        const int NR = (int)X.redo_cap;
+        Bdpt& RR = q.R;  // storage for lumo's deepest subpaths of the group's re-runs
+        RR = X;
+        RR.lp = VStore{gbuf<double>(c, g, BG_RLD, (size_t)VD_N * VR * NR, st), gbuf<int32_t>(c, g, BG_RLI, (size_t)VI_N * VR * NR, st),
+                       VR, NR, gbuf<double>(c, g, BG_RLM, (size_t)2 * VR * NR, st), gbuf<int32_t>(c, g, BG_RLMF, (size_t)VR * NR, st)};
+        RR.cp = VStore{gbuf<double>(c, g, BG_RCD, (size_t)VD_N * VR * NR, st), gbuf<int32_t>(c, g, BG_RCI, (size_t)VI_N * VR * NR, st),
+                       VR, NR, gbuf<double>(c, g, BG_RCM, (size_t)2 * VR * NR, st), gbuf<int32_t>(c, g, BG_RCMF, (size_t)VR * NR, st)};
+        RR.sp = SplatStore{gbuf<double>(c, g, BG_RSP, (size_t)10 * VR * NR, st), gbuf<int32_t>(c, g, BG_RSPN, NR, st), VR, NR};
+        RR.draws = gbuf<double>(c, g, BG_RDRAWS, (size_t)5 * VR * NR, st);
+        RR.ok = gbuf<int32_t>(c, g, BG_ROK, (size_t)VR * NR, st);
+        BItems& I = q.I;
+        I = BI;
+        I.nl = BI.nl + o;
+        I.nc = BI.nc + o;
+        I.n_a = BI.n_a + o;
+        I.off_a = BI.off_a + o;
+        I.n_b = BI.n_b + o;
+        I.off_b = BI.off_b + o;
+        I.pdf = BI.pdf + o;
+        I.wdepth = BI.wdepth + o;
+        I.cam_o = BI.cam_o + 3 * o;
+        I.cam_d = BI.cam_d + 3 * o;
+        I.rng0 = BI.rng0 + 2 * o;
+        I.lam0 = BI.lam0 + 4 * o;
+        q.totals = items_total + 2 * g;
+    }
+    if (st) return st;
+    // every group stream waits for the render's setup on stream 0 (tables, seeds, zeroing, ring)
+    HIPCHK(hipEventRecord(c.pass_ev[0], Ss[0]));
+    for (int g = 1; g < G; ++g) HIPCHK(hipStreamWaitEvent(Ss[g], c.pass_ev[0], 0));
+    const int SEG = Ctx::SNAP_RING / 4;
+    const int ahead = std::max(1, std::min(c.o.bounce_ahead, SEG - 1));
+    const int fx = c.sc.full;
+    auto start_walk = [&](BdGroup& q, int phase) {
+        q.phase = phase;
+        q.walk = 0;
+        q.seg_first = q.issued;
+        q.ub = (uint32_t)q.n;
+        q.done = false;
+    };
+    auto start_pass = [&](BdGroup& q) -> lumo_status {
+        {
+            StageTimer tm(c, c.o.timing, ST_CAMERA, q.sm);
+            k_camera<false><<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(T, q.S, c.cam, q.n, dim_stride, (uint32_t)q.pass, 0,
+                                                                       1, 0);
+        }
+        k_zero_counts<<<1, 64, 0, q.sm>>>(q.S.counts, q.B.redo_count);  // drop k_camera's queue; no re-runs yet
+        const int g = ceil_div(q.n, BLOCK);
+        if (fx == 2)
+            k_bdpt_light_init<2><<<g, BLOCK, 0, q.sm>>>(c.sc, q.S, q.B, q.I, q.n);
+        else if (fx)
+            k_bdpt_light_init<1><<<g, BLOCK, 0, q.sm>>>(c.sc, q.S, q.B, q.I, q.n);
+        else
+            k_bdpt_light_init<0><<<g, BLOCK, 0, q.sm>>>(c.sc, q.S, q.B, q.I, q.n);
+        HIPCHK(hipGetLastError());
+        start_walk(q, BD_LIGHT);
+        return LUMO_OK;
+    };
+    // one walk bounce (k_bdpt_tail ahead of it once few subpaths are alive, then k_closest +
+    // k_bdpt_step), its count snapshot recorded on the group's stream
+    auto issue_walk = [&](BdGroup& q, int gi) -> lumo_status {
+        const int mode = q.phase == BD_LIGHT ? TR_IMPORTANCE : TR_RADIANCE;
+        int32_t* qa = (q.walk & 1) ? q.S.q1 : q.S.q0;
+        int32_t* qb = (q.walk & 1) ? q.S.q0 : q.S.q1;
+        const uint32_t ub = q.ub;
+        k_bounce_begin<<<1, 64, 0, q.sm>>>(q.S.counts, q.S.tcount + TC_HEADQ);
+        const uint32_t skip = (uint64_t)ub < 4ull * c.o.bdpt_tail ? c.o.bdpt_tail : 0u;
+        if (skip > 0) {
+            StageTimer tm(c, c.o.timing, ST_RESOLVE, q.sm);
+            launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {
+                launch_bdpt_tail<decltype(K)::value>(l, c.sc, q.S, T, q.B, q.I, mode, qa, skip);
+            }, q.sm);
+        }
+        {
+            StageTimer tm(c, c.o.timing, ST_CLOSEST, q.sm);
+            launch_trav(c, ub, [&](auto K, const TravLaunch& l) {
+                launch_closest<decltype(K)::value>(l, c.sc, q.S, qa, skip);
+            }, q.sm);
+        }
+        {
+            StageTimer tm(c, c.o.timing, ST_SHADE, q.sm);
+            by_stack_class(c.sc.stack_class, [&](auto K) {
+                launch_bdpt_step<decltype(K)::value>(ceil_div(ub, BLOCK), q.sm, fx, c.sc, q.S, T, q.B, q.I, mode, qa, qb,
+                                                     skip);
+            });
+        }
+        HIPCHK(hipGetLastError());
+        const int slot = gi * SEG + q.issued % SEG;
+        HIPCHK(hipMemcpyAsync(c.snap + CNT_N * slot, q.S.counts, sizeof(uint32_t) * CNT_N, hipMemcpyDeviceToHost, q.sm));
+        HIPCHK(hipEventRecord(c.snap_ev[slot], q.sm));
+        q.issued++;
+        q.walk++;
+        return LUMO_OK;
+    };
+    auto poll = [&](BdGroup& q, int gi) -> lumo_status {
+        while (q.consumed < q.issued && !(q.done && q.consumed >= q.seg_first)) {
+            const int slot = gi * SEG + q.consumed % SEG;
+            if (hipEventQuery(c.snap_ev[slot]) != hipSuccess) break;
+            const uint32_t* k = c.snap + CNT_N * slot;
+            bounces += k[CNT_CUR] > 0 ? 1 : 0;
+            if (q.consumed >= q.seg_first) {
+                q.ub = k[CNT_NEXT];
+                q.done = q.ub == 0;
+            }
+            q.consumed++;
+        }
+        return LUMO_OK;
+    };
+    // both walks done: re-runs, the item lists' scans and totals (read back through pinned memory)
+    auto after_walks = [&](BdGroup& q, int gi) -> lumo_status {
+        {
+            StageTimer tm(c, c.o.timing, ST_RESOLVE, q.sm);
+            launch_trav(c, (uint64_t)q.B.redo_cap, [&](auto K, const TravLaunch& l) {
+                launch_bdpt_redo<decltype(K)::value>(l, c.sc, q.S, T, c.cam, q.B, q.R, q.I);
+            }, q.sm);
+        }
+        for (int k = 0; k < 2; ++k) {
+            uint32_t* cnt = k == 0 ? q.I.n_a : q.I.n_b;
+            uint32_t* off = k == 0 ? q.I.off_a : q.I.off_b;
+            size_t tmp_bytes = 0;
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, q.n, q.sm));
+            void* tmp = gbuf<char>(c, gi, BG_SCAN, tmp_bytes, st);
+            if (st) return st;
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, q.n, q.sm));
+        }
+        k_bdpt_total<<<1, 64, 0, q.sm>>>(q.I, q.n, q.totals);
+        HIPCHK(hipMemcpyAsync(c.bd_totals_h + 2 * gi, q.totals, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, q.sm));
+        HIPCHK(hipEventRecord(c.bd_ev[gi], q.sm));
+        q.phase = BD_TOTALS;
+        return LUMO_OK;
+    };
+    // the totals are known: connection items, fold, film, ring, splat taps; then the next pass
+    auto items = [&](BdGroup& q, int gi) -> lumo_status {
+        const uint32_t tot[2] = {c.bd_totals_h[2 * gi], c.bd_totals_h[2 * gi + 1]};
+        auto cap = [](uint32_t x) { return (size_t)std::max<uint64_t>(1, (uint64_t)x + x / 4); };  // grown with headroom
+        const size_t ca = cap(tot[0]), cb = cap(tot[1]);
+        const size_t need[BG_SCAN] = {4 * ca * 8, 4 * cb * 8, cb, ca * 8, ca * 4, ca * 4, ca * 4};
+        for (int k = 0; k < BG_SCAN; ++k)  // a buffer that grows is freed: nothing of this group may be using it
+            if (c.gwork.size() > (size_t)gi * BG_COUNT + k && c.gwork[(size_t)gi * BG_COUNT + k].bytes < need[k]) {
+                HIPCHK(hipStreamSynchronize(q.sm));
+                break;
+            }
+        q.I.term_a = gbuf<double>(c, gi, BG_TERM_A, 4 * ca, st);
+        q.I.term_b = gbuf<double>(c, gi, BG_TERM_B, 4 * cb, st);
+        q.I.vis = gbuf<uint8_t>(c, gi, BG_VIS, cb, st);
+        q.I.a_t = gbuf<double>(c, gi, BG_AT, ca, st);
+        q.I.a_kind = gbuf<int32_t>(c, gi, BG_AKIND, ca, st);
+        q.I.a_obj = gbuf<int32_t>(c, gi, BG_AOBJ, ca, st);
+        q.I.a_tri = gbuf<int32_t>(c, gi, BG_ATRI, ca, st);
+        if (st) return st;
+        if (tot[0] > 0) {
+            {
+                StageTimer tm(c, c.o.timing, ST_BD_TRACE_A, q.sm);
+                launch_trav(c, (uint64_t)tot[0], [&](auto K, const TravLaunch& l) {
+                    launch_bdpt_trace_a<decltype(K)::value>(l, c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
+                }, q.sm);
+            }
+            StageTimer tm(c, c.o.timing, ST_BD_EVAL_A, q.sm);
+            const int grid = std::min(ceil_div(tot[0], BLOCK), 1 << 16);
+            if (fx == 2)
+                k_bdpt_eval_a<2><<<grid, BLOCK, 0, q.sm>>>(c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
+            else if (fx)
+                k_bdpt_eval_a<1><<<grid, BLOCK, 0, q.sm>>>(c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
+            else
+                k_bdpt_eval_a<0><<<grid, BLOCK, 0, q.sm>>>(c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
+        }
+        if (tot[1] > 0) {
+            {
+                StageTimer tm(c, c.o.timing, ST_BD_VIS, q.sm);
+                // textured scenes (fx 2) have no TOP variant: their full-grid launch
+                launch_trav(c, (uint64_t)tot[1], [&](auto K, const TravLaunch& l) {
+                    launch_bdpt_vis<decltype(K)::value>(l, c.sc, q.S, q.B, q.R, q.I, q.n, q.totals);
+                }, q.sm, c.o.bdpt_top != 0 && fx != 2);
+            }
+            StageTimer tm(c, c.o.timing, ST_BD_PATHS, q.sm);
+            const int grid = std::min(ceil_div(tot[1], BLOCK), 1 << 16);
+            if (fx == 2)
+                k_bdpt_paths<2><<<grid, BLOCK, 0, q.sm>>>(c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
+            else if (fx)
+                k_bdpt_paths<1><<<grid, BLOCK, 0, q.sm>>>(c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
+            else
+                k_bdpt_paths<0><<<grid, BLOCK, 0, q.sm>>>(c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
+        }
+        {
+            StageTimer tm(c, c.o.timing, ST_RESOLVE, q.sm);
+            k_bdpt_fold<<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(q.S, q.B, q.R, q.I, q.n);
+        }
+        HIPCHK(hipGetLastError());
+        const int s1 = q.s0 + q.n;
+        if (max_P <= BLOCK) {  // film and ring from the render's whole per-slot view, this group's tasks
+            StageTimer tm(c, c.o.timing, ST_FILM, q.sm);
+            k_finish_film<<<q.t1 - q.t0, BLOCK, 0, q.sm>>>(c.sc, S, T, c.cam, (uint32_t)q.pass, Dump{}, 0, c.tone_map,
+                                                            c.tone_arg, q.t0, 1, 0);
+        } else {
+            {
+                StageTimer tm(c, c.o.timing, ST_FINISH, q.sm);
+                k_finish<<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(c.sc, S, c.cam, s1, (uint32_t)q.pass, Dump{}, 0,
+                                                                  c.tone_map, c.tone_arg, q.s0);
+            }
+            StageTimer tm(c, c.o.timing, ST_FILM, q.sm);
+            k_film<<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(S, T, c.cam, s1, q.s0);
+        }
+        {
+            StageTimer tm(c, c.o.timing, ST_RING, q.sm);
+            k_ring<<<q.t1 - q.t0, 64, 0, q.sm>>>(c.sc, S, T, q.t1, 1, q.S.counts, q.t0);
+        }
+        HIPCHK(hipGetLastError());
+        if (dfilm) {
+            k_bdpt_taps<2><<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(c.sc, q.S, q.B, q.R, c.cam, q.n, c.tone_map,
+                                                                      c.tone_arg, nullptr, nullptr, nullptr, dfilm);
+            HIPCHK(hipGetLastError());
+        } else if (splat_lists) {  // this pass's taps in lumo's order, appended per task (blocking)
+            uint32_t* cnt = tap_cnt + q.s0;
+            uint32_t* off = tap_off + q.s0;
+            k_bdpt_taps<0><<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(c.sc, q.S, q.B, q.R, c.cam, q.n, c.tone_map,
+                                                                      c.tone_arg, cnt, nullptr, nullptr, nullptr);
+            size_t tmp_bytes = 0;
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, q.n, q.sm));
+            void* tmp = gbuf<char>(c, gi, BG_SCAN, tmp_bytes, st);
+            if (st) return st;
+            HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, q.n, q.sm));
+            const int ntg = q.t1 - q.t0;
+            uint64_t* ranges = gbuf<uint64_t>(c, gi, BG_RANGES, (size_t)ntg + 1, st);
+            if (st) return st;
+            k_task_tap_ranges<<<ceil_div(ntg + 1, BLOCK), BLOCK, 0, q.sm>>>(T, cnt, off, ntg, q.n, ranges, q.t0, q.s0);
+            std::vector<uint64_t> ranges_h((size_t)ntg + 1);
+            HIPCHK(hipMemcpyAsync(ranges_h.data(), ranges, sizeof(uint64_t) * (ntg + 1), hipMemcpyDeviceToHost, q.sm));
+            HIPCHK(hipStreamSynchronize(q.sm));
+            const uint64_t total = ranges_h[ntg];
+            if (total > 0) {
+                if (c.gwork[(size_t)gi * BG_COUNT + BG_TAPS].bytes < sizeof(lumo_splat) * total)
+                    HIPCHK(hipStreamSynchronize(q.sm));
+                lumo_splat* dtaps = gbuf<lumo_splat>(c, gi, BG_TAPS, total, st);
+                if (st) return st;
+                k_bdpt_taps<1><<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(c.sc, q.S, q.B, q.R, c.cam, q.n, c.tone_map,
+                                                                          c.tone_arg, nullptr, off, dtaps, nullptr);
+                HIPCHK(hipGetLastError());
+                std::vector<lumo_splat> taps_h(total);
+                HIPCHK(hipMemcpyAsync(taps_h.data(), dtaps, sizeof(lumo_splat) * total, hipMemcpyDeviceToHost, q.sm));
+                HIPCHK(hipStreamSynchronize(q.sm));
+                for (int i = 0; i < ntg; ++i) {
+                    const int ti = q.t0 + i;
+                    for (uint64_t k = ranges_h[i]; k < ranges_h[i + 1]; ++k) {
+                        if (n_splats[ti] < out[ti].splat_cap) out[ti].splats[n_splats[ti]] = taps_h[k];
+                        n_splats[ti]++;
+                    }
+                }
+            }
+        }
+        if (c.o.timing) resolve_timers(c);
+        q.pass++;
+        if (q.pass < max_samples) return start_pass(q);
+        q.phase = BD_DONE;
+        return LUMO_OK;
+    };
+    lumo_status e = LUMO_OK;
+    for (int g = 0; g < G; ++g)
+        if ((e = start_pass(gr[g]))) return e;
+    for (;;) {
+        bool all_done = true;
+        for (int g = 0; g < G; ++g) {
+            BdGroup& q = gr[g];
+            if (q.phase == BD_DONE) continue;
+            all_done = false;
+            if (q.phase == BD_TOTALS) {
+                if (hipEventQuery(c.bd_ev[g]) == hipSuccess && (e = items(q, g))) return e;
+                continue;
+            }
+            if ((e = poll(q, g))) return e;
+            if (q.done) {  // the walk has ended
+                if (q.phase == BD_LIGHT) {
+                    k_zero_counts<<<1, 64, 0, q.sm>>>(q.S.counts, nullptr);
+                    k_bdpt_cam_init<<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(q.S, q.B, q.I, c.cam, q.n);
+                    HIPCHK(hipGetLastError());
+                    start_walk(q, BD_CAMERA);
+                } else if ((e = after_walks(q, g))) {
+                    return e;
+                }
+            } else if (q.issued - q.consumed < ahead) {
+                if ((e = issue_walk(q, g))) return e;
+            }
+        }
+        if (all_done) break;
+    }
+    // the results are copied on stream 0: after every group's last pass
+    for (int g = 1; g < G; ++g) {
+        HIPCHK(hipEventRecord(c.pass_ev[g], Ss[g]));
+        HIPCHK(hipStreamWaitEvent(Ss[0], c.pass_ev[g], 0));
+    }
+    join.ok = true;
+    return LUMO_OK;
+}
+
 lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lumo_tile_result* out, Dump* dump_host,
                         uint64_t dump_samples) {
     if (!c.has_scene) return LUMO_ERR_NO_SCENE;
@@ -1736,6 +2217,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         S.hq.cap = cap;
         S.hq.t = wbuf<double>(c, W_HQ_T, cap, st);
         S.hq.i = wbuf<int32_t>(c, W_HQ_I, 3 * cap, st);
+        alloc_sort(c, S.hq, 0, st);
         // bucket segments of `cap` paths each (MI355X has the HBM for the worst case)
         S.sq.seg = (uint32_t)cap;
         S.sq.hcap = cap * NB;
@@ -1790,7 +2272,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         B.cp = VStore{wbuf<double>(c, W_BD_CD, (size_t)VD_N * V * N, st), wbuf<int32_t>(c, W_BD_CI, (size_t)VI_N * V * N, st), V, N,
                       wbuf<double>(c, W_BD_CM, (size_t)2 * V * N, st), wbuf<int32_t>(c, W_BD_CMF, (size_t)V * N, st)};
         B.sp = SplatStore{wbuf<double>(c, W_BD_SP, (size_t)10 * V * N, st), wbuf<int32_t>(c, W_BD_SPN, N, st), V, N};
-        B.overflow = wbuf<uint32_t>(c, W_BD_OVF, 2, st);
+        B.overflow = wbuf<uint32_t>(c, W_BD_OVF, 8, st);  // (overflow, redo count) per task group
         B.redo_count = B.overflow + 1;
         B.redo_cap = (uint32_t)std::min(N, 4096);
         B.redo_list = wbuf<int32_t>(c, W_BD_REDO_LIST, B.redo_cap, st);
@@ -1810,7 +2292,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         BI.cam_d = wbuf<double>(c, W_BD_CAMD, 3 * (size_t)N, st);
         BI.rng0 = wbuf<uint64_t>(c, W_BD_RNG0, 2 * (size_t)N, st);
         BI.lam0 = wbuf<double>(c, W_BD_LAM0, 4 * (size_t)N, st);
-        items_total = wbuf<uint32_t>(c, W_BD_ITOTAL, 2, st);
+        items_total = wbuf<uint32_t>(c, W_BD_ITOTAL, 8, st);  // (a), (b) per task group
         BR = B;
         BR.lp = VStore{wbuf<double>(c, W_BDR_LD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_LI, (size_t)VI_N * VR * NR, st), VR, NR,
                        wbuf<double>(c, W_BDR_LM, (size_t)2 * VR * NR, st), wbuf<int32_t>(c, W_BDR_LMF, (size_t)VR * NR, st)};
@@ -1852,9 +2334,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         z.add(S.film, sizeof(double) * 4 * N);
         z.add(S.tcount, sizeof(unsigned long long) * (TC_ALL + TC_STATS));
         z.add(S.checks, sizeof(unsigned long long) * 3);
-        z.add(S.counts, sizeof(uint32_t) * CNT_N);
+        z.add(S.counts, sizeof(uint32_t) * CNT_N * 4);  // + the BDPT task groups' counters
         if (bdpt) {
-            z.add(B.overflow, sizeof(uint32_t));
+            z.add(B.overflow, sizeof(uint32_t) * 8);
             if (dfilm) z.add(dfilm, sizeof(double) * film_n);
         }
         if (z.overflow) return LUMO_ERR_INVALID;
@@ -1904,7 +2386,20 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         if (st) return st;
         c.split_sets_bytes = std::max(c.split_sets_bytes, (size_t)(K - 1) * split_set_bytes(S, (int)NV, ns));
     }
-    for (uint64_t pass = 0; pass < ((pipe || K > 1) ? 0 : max_samples); ++pass) {
+    // BDPT: task groups as concurrent pass chains (render_bdpt_groups)
+    const int bd_groups = std::min(std::min(c.o.bdpt_groups, 4), (int)n_tasks);
+    const bool bd_grouped = bdpt && !dump_host && bd_groups > 1;
+    if (bd_grouped) {
+        c.sched.schedule = LUMO_SCHED_BDPT_GROUPS;
+        c.sched.task_groups = bd_groups;
+        c.sched.units_in_flight = bd_groups;
+        const lumo_status ps = render_bdpt_groups(c, S, T, B, BI, N, (int)n_tasks, dim_stride, max_samples, max_P,
+                                                  bd_groups, first, items_total, splat_lists, dfilm, tap_cnt, tap_off,
+                                                  out, n_splats, bounces, st);
+        if (ps) return ps;
+        if (st) return st;
+    }
+    for (uint64_t pass = 0; pass < ((pipe || K > 1 || bd_grouped) ? 0 : max_samples); ++pass) {
         if (dump_host) HIPCHK(hipMemcpyAsync(D.delta + pass, T.delta, sizeof(double), hipMemcpyDeviceToDevice, sm));
         // S.counts: zeroed at setup, then by the ring at the end of every pass
         {
@@ -2160,9 +2655,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
     if (c.o.timing) resolve_timers(c);
     bool splat_oom = false;
     if (bdpt) {
-        uint32_t ovf = 0;
-        HIPCHK(hipMemcpy(&ovf, B.overflow, sizeof(uint32_t), hipMemcpyDeviceToHost));
-        if (ovf) return LUMO_ERR_UNSUPPORTED;  // more long subpaths in one pass than the redo list holds
+        uint32_t ovf[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (overflow, redo count) per task group
+        HIPCHK(hipMemcpy(ovf, B.overflow, sizeof(ovf), hipMemcpyDeviceToHost));
+        if (ovf[0] | ovf[2] | ovf[4] | ovf[6]) return LUMO_ERR_UNSUPPORTED;  // more long subpaths in one pass than a redo list holds
         if (dfilm) {
             std::vector<double> f(film_n);
             HIPCHK(hipMemcpy(f.data(), dfilm, sizeof(double) * film_n, hipMemcpyDeviceToHost));
@@ -2222,7 +2717,7 @@ const char* const kOptEnv[LUMO_OPT_COUNT] = {
     "LUMO_DYN", "LUMO_BOUNCE_THREADS", "LUMO_SPLIT_PIPE", "LUMO_SPLIT_GROUPS", "LUMO_BDPT_TAIL", "LUMO_BOUNCE_AHEAD",
     "LUMO_LDS_GRID", "LUMO_TOP_GRID", "LUMO_TOP_KB", "LUMO_KD_LDS", "LUMO_STACK_CLASS", "LUMO_FULL_KERNELS",
     "LUMO_POISON", "LUMO_TAIL_PRIORITY", "LUMO_TOP_KD", "LUMO_TAIL_BOUNCES", "LUMO_FILM_FIRST",
-    "LUMO_BDPT_TOP"};
+    "LUMO_BDPT_TOP", "LUMO_BDPT_GROUPS", "LUMO_RAY_SORT"};
 
 void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
     lo = 0;
@@ -2241,6 +2736,7 @@ void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
         case LUMO_OPT_KD_LDS: hi = 64; break;
         case LUMO_OPT_TAIL_BOUNCES: lo = -1; hi = 16; break;
         case LUMO_OPT_STACK_CLASS: hi = 64; break;
+        case LUMO_OPT_BDPT_GROUPS: lo = 1; hi = 4; break;
         default: break;
     }
 }
@@ -2301,6 +2797,8 @@ lumo_status set_opt(Ctx& c, int k, int64_t v) {
         case LUMO_OPT_TAIL_BOUNCES: o.tail_bounces = iv; break;
         case LUMO_OPT_FILM_FIRST: o.film_first = iv; break;
         case LUMO_OPT_BDPT_TOP: o.bdpt_top = iv; break;
+        case LUMO_OPT_BDPT_GROUPS: o.bdpt_groups = iv; break;
+        case LUMO_OPT_RAY_SORT: o.ray_sort = iv; break;
         case LUMO_OPT_TAIL_PRIORITY:
             if (iv != o.tail_priority) {
                 const lumo_status e = make_tail_stream(c, iv);
@@ -2342,6 +2840,8 @@ int64_t get_opt(const Ctx& c, int k) {
         case LUMO_OPT_TAIL_BOUNCES: return o.tail_bounces;
         case LUMO_OPT_FILM_FIRST: return o.film_first;
         case LUMO_OPT_BDPT_TOP: return o.bdpt_top;
+        case LUMO_OPT_BDPT_GROUPS: return o.bdpt_groups;
+        case LUMO_OPT_RAY_SORT: return o.ray_sort;
         default: return 0;
     }
 }
@@ -2407,6 +2907,12 @@ lumo_status lumo_create(int device, void** ctx_out) {
         (void)hipEventCreateWithFlags(&c->film_ev[i], hipEventDisableTiming);
     }
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventCreateWithFlags(&c->snap_ev[i], hipEventDisableTiming);
+    for (int i = 0; i < 4; ++i) (void)hipEventCreateWithFlags(&c->bd_ev[i], hipEventDisableTiming);
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->bd_totals_h), sizeof(uint32_t) * 8) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return LUMO_ERR_OOM;
+    }
     if (hipHostMalloc(reinterpret_cast<void**>(&c->snap), sizeof(uint32_t) * CNT_N * Ctx::SNAP_RING) != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
         delete c;
@@ -2458,8 +2964,12 @@ void lumo_destroy(void* ctx) {
     free_scene(*c);
     for (DevBuf& b : c->work)
         if (b.p) (void)hipFree(b.p);
+    for (DevBuf& b : c->gwork)
+        if (b.p) (void)hipFree(b.p);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventDestroy(c->snap_ev[i]);
     if (c->snap) (void)hipHostFree(c->snap);
+    if (c->bd_totals_h) (void)hipHostFree(c->bd_totals_h);
+    for (int i = 0; i < 4; ++i) (void)hipEventDestroy(c->bd_ev[i]);
     for (int i = 0; i < 4; ++i) {
         (void)hipEventDestroy(c->pass_ev[i]);
         (void)hipEventDestroy(c->tail_ev[i]);
@@ -2521,6 +3031,17 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         if (x && !st) st = x;
     };
     chk(upload(*c, d->vertices, (size_t)3 * d->num_vertices, &s.vertices));
+    if (d->num_object_nodes > 0 && d->object_nodes) {  // ray sorting's cells: the objects BVH's world box
+        const lumo_bvh_node& r = d->object_nodes[0];
+        double lo[3], sc3[3];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = r.bmin[a];
+            const double ext = r.bmax[a] - r.bmin[a];
+            sc3[a] = ext > 0.0 && std::isfinite(ext) ? 512.0 / ext : 0.0;
+        }
+        c->sort_lo = V3{lo[0], lo[1], lo[2]};
+        c->sort_scale = V3{sc3[0], sc3[1], sc3[2]};
+    }
     chk(upload(*c, d->normals, (size_t)3 * d->num_normals, &s.normals));
     chk(upload(*c, d->uvs, (size_t)2 * d->num_uvs, &s.uvs));
     chk(upload(*c, d->triangles, (size_t)d->num_triangles, &s.tris));

@@ -69,8 +69,9 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_CLOSEST_WAVES) v
     const HitQ hq = S.hq;
     Counters C{0, 0, 0};
     for (uint32_t w0 = wave_fetch(S.counts + CNT_FETCH_C); w0 < count; w0 = wave_fetch(S.counts + CNT_FETCH_C)) {
-        const uint32_t q = w0 + lane_id();
-        if (q >= count) continue;
+        const uint32_t q0 = w0 + lane_id();
+        if (q0 >= count) continue;
+        const uint32_t q = hq.perm ? hq.perm[q0] : q0;  // sorted rays: neighbouring lanes walk alike
         const RayX r = rayx(Ray{qv3(cur, QD_O, q), qv3(cur, QD_D, q)});
         const HitRef h = scene_hit<STK, FX, LDS == 2>(sc, r, C);
         hq.t[q] = h.t;

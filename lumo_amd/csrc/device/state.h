@@ -106,11 +106,17 @@ struct QState {
     __device__ __forceinline__ uint64_t& R(int k, size_t q) const { return r[(size_t)k * cap + q]; }
     __device__ __forceinline__ int32_t& I(int k, size_t q) const { return i[(size_t)k * cap + q]; }
 };
-// Closest hits of the current ray queue, same order.
+// Closest hits of the current ray queue, same order.  `perm` (ray sorting, LUMO_OPT_RAY_SORT): the
+// queue positions in the order k_closest_q takes them (sorted by origin cell and direction octant);
+// the hits still land at the rays' own positions.  sk / sv: the sort's key / value double buffers.
 struct HitQ {
     double* t;
     int32_t* i;  // kind, object, triangle planes
     size_t cap;
+    const uint32_t* perm;
+    uint32_t *sk[2], *sv[2];
+    void* tmp;  // the sort's temporary storage (tmp_bytes)
+    size_t tmp_bytes;
 };
 // NEE records in queue order: per path with shadow rays a header (gathered, wavelengths, radiance
 // of a path that ends this bounce, slot, next-queue position or -1), and per light sample i the

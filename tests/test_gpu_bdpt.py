@@ -150,12 +150,13 @@ def test_renderer_bdpt_image(dev):
 
 
 def test_bdpt_redo_list_overflow_fails_loudly(dev):
-    """More long samples in one pass than the redo list holds (4096): the call fails with
-    LUMO_ERR_UNSUPPORTED instead of truncating subpaths, and the context stays usable."""
-    sc, cam = _scene("cornell", (128, 64))
+    """More long samples in one pass than a redo list holds (4096 per task group, 8 192 slots per
+    group here): the call fails with LUMO_ERR_UNSUPPORTED instead of truncating subpaths, and the
+    context stays usable."""
+    sc, cam = _scene("cornell", (256, 64))
     dev.upload(sc, cam)
-    tasks = L.make_tasks(128, 64, 1, 5)
-    film = np.zeros((64, 128, 3))
+    tasks = L.make_tasks(256, 64, 1, 5)
+    film = np.zeros((64, 256, 3))
     with pytest.raises(RuntimeError, match="UNSUPPORTED"):
         dev.render_tasks(tasks, integrator=BDPT, splat_film=film, max_vertices=2)
     bufs, _ = dev.render_tasks(tasks, integrator=BDPT, splat_film=film)
@@ -213,3 +214,44 @@ def test_bdpt_textured_large_scene(dev):
         np.testing.assert_array_equal(b, ob)
         assert (r.num_rays, r.num_queries, r.num_camera_rays) == (o.num_rays, o.num_queries, o.num_camera_rays)
         np.testing.assert_array_equal(s["rgb"], os_["rgb"])
+
+
+@pytest.mark.parametrize("groups", [1, 2, 3, 4])
+@pytest.mark.parametrize("film", [0, 1], ids=["lists", "splat_film"])
+def test_bdpt_task_groups(groups, film):
+    """render_bdpt_groups: the tasks cut into 1-4 groups, each a chain of passes on its own stream
+    with its own views, walk queues, counters, redo list and item lists (a group's pass p + 1 reads
+    the delta of its ring of pass p, path_gen.rs:133-145 / task.rs:28-53).  caustics.rs (mirror +
+    glass, delta vertices, re-runs with max_vertices 6), 5 passes: every tile, count and splat (lists:
+    lumo's order per task; film: summed on the device) equals the oracle's."""
+    sc, cam = _scene("caustics", (48, 32))
+    sc.build()
+    d = L.Device(0, bdpt_groups=groups)
+    try:
+        d.upload(sc, cam)
+        tasks = L.make_tasks(48, 32, 5, 0x6B0)
+        sp = []
+        if film:
+            dfilm = np.zeros((32, 48, 3))
+            bufs, rr = d.render_tasks(tasks, integrator=BDPT, splat_film=dfilm, max_vertices=6)
+        else:
+            bufs, rr = d.render_tasks(tasks, integrator=BDPT, splats_out=sp, max_vertices=6)
+        sch = d.last_schedule()
+        assert (sch.schedule, sch.task_groups) == ((3, groups) if groups > 1 else (0, 1))
+    finally:
+        d.close()
+    osp = []
+    obufs, orr, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8, integrator=BDPT, splats_out=osp)
+    for b, ob, r, o in zip(bufs, obufs, rr, orr):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries, r.num_camera_rays) == (o.num_rays, o.num_queries, o.num_camera_rays)
+    if film:
+        seq = L.Film(48, 32, samples=5)
+        for t, ob, s in zip(tasks, obufs, osp):
+            seq.add_tile(t, ob, s)
+        np.testing.assert_allclose(dfilm, seq.splats, rtol=1e-12, atol=1e-300)
+    else:
+        for s, os_ in zip(sp, osp):
+            assert len(s) == len(os_)
+            np.testing.assert_array_equal(s["rgb"], os_["rgb"])
+            np.testing.assert_array_equal(s["x"], os_["x"])

@@ -373,6 +373,37 @@ def test_c3_share_merged_passes(c3):
         assert (res[i].num_rays, res[i].num_queries) == (orr.num_rays, orr.num_queries)
 
 
+@pytest.mark.parametrize("scene", ["dragon", "bistro"])
+def test_ray_sort_matches_oracle(mid_bistro, scene):
+    """Ray sorting (option ray_sort): each bounce's closest-hit rays are radix-sorted by direction
+    octant and origin cell and walked in that order; the hits land at the rays' own queue positions,
+    so tiles, ray and query counts and the traversal counters equal the oracle's (kdtree.rs:101-169,
+    bvh.rs:315-362: the walks themselves are unchanged)."""
+    if scene == "bistro":
+        sc, cam = mid_bistro, scenes.bistro_camera((256, 192))
+    else:
+        sc = scenes.dragon(torus_knot_tube(300, 12)).build()
+        cam = scenes.default_camera((256, 192))
+    d = L.Device(0, ray_sort=1)
+    try:
+        d.upload(sc, cam)
+        tasks = L.make_tasks(256, 192, 2, SEED)  # 49 k slots per pass: bounces above the sort minimum
+        before = d.stats()
+        bufs, res = d.render_tasks(tasks)
+        after = d.stats()
+    finally:
+        d.close()
+    obufs, ores, cnt = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, oracle_threads())
+    for b, ob, r, orr in zip(bufs, obufs, res, ores):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+    assert after.closest_queries - before.closest_queries == cnt.closest_queries
+    assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
+    got = [sum(after.aabb_tests) - sum(before.aabb_tests), sum(after.kd_nodes) - sum(before.kd_nodes),
+           sum(after.tri_tests) - sum(before.tri_tests)]
+    assert got == [cnt.aabb_tests, cnt.kd_nodes, cnt.tri_tests]
+
+
 def test_c3_bench_schedule_full_frame(c3):
     """C3 as the bench renders it: the full 1920x1080 Bistro stand-in frame (8 160 tiles, 2.07 M
     slots per pass, n_shadow = 11, the full TOP set) through render_split_pipelined with the
