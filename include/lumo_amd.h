@@ -421,9 +421,9 @@ enum {
                                   (LUMO_BDPT_TOP, 1)                                                */
     LUMO_OPT_BDPT_GROUPS,      /* BDPT: task groups rendered as concurrent chains of passes on their own
                                   streams, 1-4 (LUMO_BDPT_GROUPS, 2; ABI 9)                          */
-    LUMO_OPT_RAY_SORT,         /* three-kernel bounces: the closest-hit rays of a bounce sorted by
-                                  direction octant and origin cell (radix sort) before their walks:
-                                  0 / 1 (LUMO_RAY_SORT, 0; ABI 9)                                    */
+    LUMO_OPT_RAY_SORT,         /* three-kernel bounces: the closest-hit rays of a bounce radix-sorted
+                                  before their walks: 0 off, 1 direction octant major, 2 origin cell
+                                  major, -1 auto (1 for kd stack class >= 32) (LUMO_RAY_SORT, -1; ABI 9)*/
     LUMO_OPT_COUNT
 };
 lumo_status lumo_set_option(void* ctx, int32_t option, int64_t value);

@@ -482,13 +482,15 @@ __device__ double pdf_connection(const DScene& sc, const BVtx& curr, const BVtx&
     return sa_to_area(pdf_sa, xo, xi, wi, ngi);
 }
 
+// `ls1_in` / `ct1_in`: the vertices s - 1 / t - 1 when the caller holds them already (connect_paths:
+// the connection's own two vertices), so they are not read again.
 template <int FX>
 __device__ double mis_weight(const DScene& sc, const DCam& cam, const double* L, const PView& lp, int s, const PView& cp,
-                             int t) {
+                             int t, const BVtx* ls1_in = nullptr, const BVtx* ct1_in = nullptr) {
     if (s + t == 2) return 1.0;
-    const BVtx ct1 = cp.get(t - 1);
+    const BVtx ct1 = ct1_in ? *ct1_in : cp.get(t - 1);
     BVtx ls1;
-    if (s > 0) ls1 = lp.get(s - 1);
+    if (s > 0) ls1 = ls1_in ? *ls1_in : lp.get(s - 1);
     // special entries at indices s-2, s-1, s, s+1 (mis.rs:40-120)
     MisE e_s2{1.0, 1.0, false}, e_s1{1.0, 1.0, false}, e_t1{1.0, 1.0, false}, e_t2{1.0, 1.0, false};
     if (s > 1) {
@@ -654,7 +656,7 @@ __device__ DColor connect_paths(const DScene& sc, const DCam& cam, const double*
     const DColor radiance = ll.gath * lb * v_shading_cosine(sc, ll, -wi, ll.ns) * cl.gath * cb *
                             v_shading_cosine(sc, cl, wi, cl.ns) * cfill(1.0) / distance_squared(xc, xl);
     if (radiance.s[0] == 0.0 && radiance.s[1] == 0.0 && radiance.s[2] == 0.0 && radiance.s[3] == 0.0) return cfill(0.0);
-    return radiance * mis_weight<FX>(sc, cam, L, lp, s, cp, t);
+    return radiance * mis_weight<FX>(sc, cam, L, lp, s, cp, t, &ll, &cl);
 }
 
 // ---- per-slot state of the wavefront walks and the connection items
@@ -671,6 +673,10 @@ struct BItems {
     double *cam_o, *cam_d;  // the camera ray, kept while the light subpath walks
     uint64_t* rng0;       // the slot's RNG at the start of the sample (2 per slot), for re-runs
     double* lam0;         // its wavelengths at the start of the sample (4 per slot)
+    // the (a) items that trace, by kind (k_bdpt_alists): camera rays of t = 1 connections at
+    // [0, alist_cap), light rays of s = 1 connections at [alist_cap, 2 alist_cap)
+    int32_t* alist;
+    size_t alist_cap;
 };
 __device__ __forceinline__ uint32_t bdpt_n_a(int S, int T) { return (uint32_t)(S + T - 1); }
 __device__ __forceinline__ uint32_t bdpt_n_b(int S, int T) { return (uint32_t)(S - 1) * (uint32_t)(T - 1); }
@@ -1043,18 +1049,70 @@ __device__ __forceinline__ ItemSel item_store(const Bdpt& B, const Bdpt& R, int 
     return ri >= 0 ? ItemSel{slot, ri, &R} : ItemSel{slot, slot, &B};
 }
 
+// The (a) items that trace, listed by kind so that a wave of k_bdpt_trace_a walks rays of one kind
+// (camera rays of t = 1 connections: Scene::hit; light rays of s = 1 connections: hit_light),
+// instead of running both walks in turn: per slot, the items whose vertex is neither delta nor
+// (camera side) on a light, exactly the ones k_bdpt_trace_a traces.  totals[2 + kind] counts them
+// (zeroed by k_bdpt_total); one append atomic per wave and list.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
+    uint32_t x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane_id() >= off) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+#ifdef LUMO_MAIN_TU
+__global__ __launch_bounds__(BLOCK) void k_bdpt_alists(Bdpt B, Bdpt R, BItems I, int n, uint32_t* totals) {
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = slot < n && I.n_a[slot] > 0;
+    ItemSel e{0, 0, &B};
+    int Sl = 0, Tc = 0;
+    uint32_t nc = 0, nl = 0;
+    if (live) {
+        e = item_store(B, R, slot);
+        Sl = I.nl[slot];
+        Tc = I.nc[slot];
+        for (int s = 2; s <= Sl; ++s) nc += (e.X->lp.I(2, s - 1, e.si) & VF_DELTA) ? 0u : 1u;
+        for (int t = 2; t <= Tc; ++t)
+            nl += ((e.X->cp.I(2, t - 1, e.si) & VF_DELTA) || e.X->cp.I(1, t - 1, e.si) >= 0) ? 0u : 1u;
+    }
+    uint32_t tc, tl;
+    const uint32_t pc = wave_excl_scan(nc, tc), pl = wave_excl_scan(nl, tl);
+    uint32_t bc = 0, bl = 0;
+    if (lane_id() == 0) {
+        if (tc) bc = atomicAdd(totals + 2, tc);
+        if (tl) bl = atomicAdd(totals + 3, tl);
+    }
+    bc = __shfl(bc, 0, 64);
+    bl = __shfl(bl, 0, 64);
+    if (!live) return;
+    const uint32_t q0 = I.off_a[slot];
+    uint32_t kc = bc + pc, kl = bl + pl;
+    for (int s = 2; s <= Sl; ++s)
+        if (!(e.X->lp.I(2, s - 1, e.si) & VF_DELTA)) I.alist[kc++] = (int32_t)(q0 + (uint32_t)(s - 2));
+    for (int t = 2; t <= Tc; ++t)
+        if (!((e.X->cp.I(2, t - 1, e.si) & VF_DELTA) || e.X->cp.I(1, t - 1, e.si) >= 0))
+            I.alist[I.alist_cap + kl++] = (int32_t)(q0 + (uint32_t)(Sl + t - 2));
+}
+#endif  // LUMO_MAIN_TU
+
 // (a) items, traversal part: the camera ray of each t = 1 connection and the light ray of each
 // s = 1 connection, traced whenever the ray exists (before lumo's BSDF-pdf guards, which
 // k_bdpt_eval_a evaluates; a ray the guards reject is never read and not counted as a query).
+// One launch per kind, over that kind's list (k_bdpt_alists).
 template <int STK, int LDS, int FX>
-__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_trace_a(
-    DScene sc0, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n, const uint32_t* totals) {
+__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_BDTRACE_WAVES) void k_bdpt_trace_a(
+    DScene sc0, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n, const uint32_t* totals, int kind) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
-    const uint32_t total = totals[0];
+    const uint32_t total = totals[2 + kind];
     if (total <= blockIdx.x * blockDim.x) return;
     const DScene sc = LDS == 1 ? stage_scene_lds(sc0, lds_scene) : (LDS == 2 ? stage_top_lds(sc0, lds_scene) : sc0);
+    const int32_t* list = I.alist + (size_t)kind * I.alist_cap;
     Counters C{0, 0, 0};
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x) {
+        const uint32_t q = (uint32_t)list[k];
         const int slot = item_slot(I.off_a, n, q);
         const ItemSel e = item_store(B, R, slot);
         const Bdpt& X = *e.X;
@@ -1144,7 +1202,7 @@ __device__ __forceinline__ void item_b_st(const BItems& I, int slot, uint32_t q,
 
 // bdpt_visible of every (b) item whose guard reaches it (bd_path_trace.rs:279-290)
 template <int STK, int LDS, int FX>
-__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_SHADOW_WAVES) void k_bdpt_vis(
+__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_BDTRACE_WAVES) void k_bdpt_vis(
     DScene sc0, Paths S, Bdpt B, Bdpt R, BItems I, int n, const uint32_t* totals) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t total = totals[1];
@@ -1234,11 +1292,13 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_fold(Paths S, Bdpt B, Bdpt R, BI
 #endif  // LUMO_MAIN_TU
 
 #ifdef LUMO_MAIN_TU
-// item totals of the pass: (a), (b)
+// item totals of the pass: (a), (b); the (a) trace lists' counters zeroed
 __global__ void k_bdpt_total(BItems I, int n, uint32_t* totals) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         totals[0] = I.off_a[n - 1] + I.n_a[n - 1];
         totals[1] = I.off_b[n - 1] + I.n_b[n - 1];
+        totals[2] = 0u;
+        totals[3] = 0u;
     }
 }
 #endif  // LUMO_MAIN_TU

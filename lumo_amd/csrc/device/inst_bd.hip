@@ -62,8 +62,8 @@ void launch_bdpt_redo(const TravLaunch& l, const DScene& sc, const Paths& S, con
 
 template <int STK>
 void launch_bdpt_trace_a(const TravLaunch& l, const DScene& sc, const Paths& S, const DCam& cam, const Bdpt& B,
-                         const Bdpt& R, const BItems& I, int n, const uint32_t* totals) {
-    LUMO_TRAV_LAUNCH(k_bdpt_trace_a, sc, S, cam, B, R, I, n, totals);
+                         const Bdpt& R, const BItems& I, int n, const uint32_t* totals, int kind) {
+    LUMO_TRAV_LAUNCH(k_bdpt_trace_a, sc, S, cam, B, R, I, n, totals, kind);
 }
 
 template <int STK>
@@ -79,7 +79,7 @@ template void launch_bdpt_tail<LUMO_STK>(const TravLaunch&, const DScene&, const
 template void launch_bdpt_redo<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Tasks&, const DCam&,
                                          const Bdpt&, const Bdpt&, const BItems&);
 template void launch_bdpt_trace_a<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const DCam&, const Bdpt&,
-                                            const Bdpt&, const BItems&, int, const uint32_t*);
+                                            const Bdpt&, const BItems&, int, const uint32_t*, int);
 template void launch_bdpt_vis<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Bdpt&, const Bdpt&,
                                         const BItems&, int, const uint32_t*);
 

@@ -258,7 +258,7 @@ __device__ __forceinline__ uint32_t spread3(uint32_t x) {  // 9 bits -> every th
     return x;
 }
 __global__ __launch_bounds__(BLOCK) void k_sort_keys(QState cur, const uint32_t* counts, uint32_t n, V3 lo, V3 scale,
-                                                      uint32_t* keys, uint32_t* vals) {
+                                                      uint32_t* keys, uint32_t* vals, int mode) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
     uint32_t key = 0xffffffffu;
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(BLOCK) void k_sort_keys(QState cur, const uint32_t*
         const uint32_t m = spread3(cell((o.x - lo.x) * scale.x)) | (spread3(cell((o.y - lo.y) * scale.y)) << 1) |
                            (spread3(cell((o.z - lo.z) * scale.z)) << 2);
         const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
-        key = (oct << 27) | m;
+        key = mode == 2 ? (m << 3) | oct : (oct << 27) | m;  // 2: origin cell major
     }
     keys[q] = key;
     vals[q] = q;
@@ -851,7 +851,9 @@ struct Opts {
     int bdpt_top = 1;                  // BDPT connection visibility of large scenes with TOP staging
     int film_first = 0;                // fused pipeline, film on the tail stream: the film before the unit's last ring
     int bdpt_groups = 2;               // BDPT: task groups rendered as concurrent pass chains (render_bdpt_groups)
-    int ray_sort = 0;                  // split bounces: closest-hit rays sorted by origin cell and octant
+    int ray_sort = -1;                 // split bounces: closest-hit rays sorted (1 octant major, 2 origin major;
+                                       // -1 auto: 1 for deep kd trees, stack class >= 32: C2 4-spp frame
+                                       // 309 / 312 -> 302 ms; C3, class 24: 556 -> 563 ms, so off there)
 };
 
 struct Ctx {
@@ -955,7 +957,8 @@ enum WorkId {
     W_SQ_QL, W_BD_LM, W_BD_LMF, W_BD_CM, W_BD_CMF, W_BDR_LM, W_BDR_LMF, W_BDR_CM, W_BDR_CMF,
     W_SPLIT_SET1,  // render_split_pipelined sets 1..3: hits + NEE records, 8 buffers each
     W_SORT_SET0 = W_SPLIT_SET1 + 3 * 8,  // ray sorting of pass set k: keys x 2, values x 2, temp
-    W_COUNT = W_SORT_SET0 + 4 * 5
+    W_BD_ALIST = W_SORT_SET0 + 4 * 5,    // BDPT (a)-item trace lists
+    W_COUNT
 };
 
 template <typename T>
@@ -1095,12 +1098,13 @@ void alloc_pass_set(Ctx& c, Paths& Q, int k, int N, lumo_status& st) {
     }
 }
 // Ray sorting buffers of pass set k (none when the option is off)
+int ray_sort_mode(const Ctx& c) { return c.o.ray_sort >= 0 ? c.o.ray_sort : (c.sc.stack_class >= 32 ? 1 : 0); }
 void alloc_sort(Ctx& c, HitQ& hq, int k, lumo_status& st) {
     hq.perm = nullptr;
     hq.sk[0] = hq.sk[1] = hq.sv[0] = hq.sv[1] = nullptr;
     hq.tmp = nullptr;
     hq.tmp_bytes = 0;
-    if (!c.o.ray_sort) return;
+    if (!ray_sort_mode(c)) return;
     const int w = W_SORT_SET0 + 5 * k;
     for (int b = 0; b < 2; ++b) {
         hq.sk[b] = wbuf<uint32_t>(c, w + b, hq.cap, st);
@@ -1353,10 +1357,11 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
         return;
     }
     Paths Sc = S;  // the closest-hit launch's view: with the queue's sort order when rays are sorted
-    if (c.o.ray_sort && S.hq.tmp && ub >= kSortMin && (uint64_t)ub <= S.hq.cap) {
+    const int sort_mode = ray_sort_mode(c);
+    if (sort_mode && S.hq.tmp && ub >= kSortMin && (uint64_t)ub <= S.hq.cap) {
         StageTimer tm(c, c.o.timing, ST_CLOSEST, sm);
         k_sort_keys<<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(cur, S.counts, ub, c.sort_lo, c.sort_scale, S.hq.sk[0],
-                                                           S.hq.sv[0]);
+                                                           S.hq.sv[0], sort_mode);
         hipcub::DoubleBuffer<uint32_t> kb(S.hq.sk[0], S.hq.sk[1]), vb(S.hq.sv[0], S.hq.sv[1]);
         size_t tb = S.hq.tmp_bytes;
         if (hipcub::DeviceRadixSort::SortPairs(S.hq.tmp, tb, kb, vb, (int)ub, 0, 30, sm) == hipSuccess)
@@ -1737,7 +1742,7 @@ struct BdGroup {
 };
 
 // Per-group work buffers (k: BdBuf), grown on demand like the render's own.
-enum BdBuf { BG_TERM_A, BG_TERM_B, BG_VIS, BG_AT, BG_AKIND, BG_AOBJ, BG_ATRI, BG_SCAN, BG_RANGES, BG_TAPS,
+enum BdBuf { BG_TERM_A, BG_TERM_B, BG_VIS, BG_AT, BG_AKIND, BG_AOBJ, BG_ATRI, BG_ALIST, BG_SCAN, BG_RANGES, BG_TAPS,
              BG_RLD, BG_RLI, BG_RCD, BG_RCI, BG_RSP, BG_RSPN, BG_RDRAWS, BG_ROK, BG_RLM, BG_RLMF, BG_RCM, BG_RCMF,
              BG_REDO, BG_COUNT };
 template <typename T>
@@ -1848,7 +1853,7 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
         I.cam_d = BI.cam_d + 3 * o;
         I.rng0 = BI.rng0 + 2 * o;
         I.lam0 = BI.lam0 + 4 * o;
-        q.totals = items_total + 2 * g;
+        q.totals = items_total + 4 * g;
     }
     if (st) return st;
     // every group stream waits for the render's setup on stream 0 (tables, seeds, zeroing, ring)
@@ -1950,7 +1955,7 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
             HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, q.n, q.sm));
         }
         k_bdpt_total<<<1, 64, 0, q.sm>>>(q.I, q.n, q.totals);
-        HIPCHK(hipMemcpyAsync(c.bd_totals_h + 2 * gi, q.totals, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, q.sm));
+        HIPCHK(hipMemcpyAsync(c.bd_totals_h + 2 * gi, q.totals, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, q.sm));  // (a), (b)
         HIPCHK(hipEventRecord(c.bd_ev[gi], q.sm));
         q.phase = BD_TOTALS;
         return LUMO_OK;
@@ -1960,7 +1965,7 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
         const uint32_t tot[2] = {c.bd_totals_h[2 * gi], c.bd_totals_h[2 * gi + 1]};
         auto cap = [](uint32_t x) { return (size_t)std::max<uint64_t>(1, (uint64_t)x + x / 4); };  // grown with headroom
         const size_t ca = cap(tot[0]), cb = cap(tot[1]);
-        const size_t need[BG_SCAN] = {4 * ca * 8, 4 * cb * 8, cb, ca * 8, ca * 4, ca * 4, ca * 4};
+        const size_t need[BG_SCAN] = {4 * ca * 8, 4 * cb * 8, cb, ca * 8, ca * 4, ca * 4, ca * 4, 2 * ca * 4};
         for (int k = 0; k < BG_SCAN; ++k)  // a buffer that grows is freed: nothing of this group may be using it
             if (c.gwork.size() > (size_t)gi * BG_COUNT + k && c.gwork[(size_t)gi * BG_COUNT + k].bytes < need[k]) {
                 HIPCHK(hipStreamSynchronize(q.sm));
@@ -1973,13 +1978,17 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
         q.I.a_kind = gbuf<int32_t>(c, gi, BG_AKIND, ca, st);
         q.I.a_obj = gbuf<int32_t>(c, gi, BG_AOBJ, ca, st);
         q.I.a_tri = gbuf<int32_t>(c, gi, BG_ATRI, ca, st);
+        q.I.alist = gbuf<int32_t>(c, gi, BG_ALIST, 2 * ca, st);
+        q.I.alist_cap = ca;
         if (st) return st;
         if (tot[0] > 0) {
             {
                 StageTimer tm(c, c.o.timing, ST_BD_TRACE_A, q.sm);
-                launch_trav(c, (uint64_t)tot[0], [&](auto K, const TravLaunch& l) {
-                    launch_bdpt_trace_a<decltype(K)::value>(l, c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
-                }, q.sm);
+                k_bdpt_alists<<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(q.B, q.R, q.I, q.n, q.totals);
+                for (int kind = 0; kind < 2; ++kind)
+                    launch_trav(c, (uint64_t)tot[0], [&](auto K, const TravLaunch& l) {
+                        launch_bdpt_trace_a<decltype(K)::value>(l, c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals, kind);
+                    }, q.sm);
             }
             StageTimer tm(c, c.o.timing, ST_BD_EVAL_A, q.sm);
             const int grid = std::min(ceil_div(tot[0], BLOCK), 1 << 16);
@@ -2292,7 +2301,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         BI.cam_d = wbuf<double>(c, W_BD_CAMD, 3 * (size_t)N, st);
         BI.rng0 = wbuf<uint64_t>(c, W_BD_RNG0, 2 * (size_t)N, st);
         BI.lam0 = wbuf<double>(c, W_BD_LAM0, 4 * (size_t)N, st);
-        items_total = wbuf<uint32_t>(c, W_BD_ITOTAL, 8, st);  // (a), (b) per task group
+        items_total = wbuf<uint32_t>(c, W_BD_ITOTAL, 16, st);  // (a), (b) and the (a) trace lists' counts per task group
         BR = B;
         BR.lp = VStore{wbuf<double>(c, W_BDR_LD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_LI, (size_t)VI_N * VR * NR, st), VR, NR,
                        wbuf<double>(c, W_BDR_LM, (size_t)2 * VR * NR, st), wbuf<int32_t>(c, W_BDR_LMF, (size_t)VR * NR, st)};
@@ -2525,13 +2534,17 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             BI.a_kind = wbuf<int32_t>(c, W_BD_AKIND, std::max(totals[0], 1u), st);
             BI.a_obj = wbuf<int32_t>(c, W_BD_AOBJ, std::max(totals[0], 1u), st);
             BI.a_tri = wbuf<int32_t>(c, W_BD_ATRI, std::max(totals[0], 1u), st);
+            BI.alist = wbuf<int32_t>(c, W_BD_ALIST, 2 * (size_t)std::max(totals[0], 1u), st);
+            BI.alist_cap = std::max(totals[0], 1u);
             if (st) return st;
             if (totals[0] > 0) {
                 {
                     StageTimer tm(c, c.o.timing, ST_BD_TRACE_A);
-                    launch_trav(c, (uint64_t)totals[0], [&](auto K, const TravLaunch& l) {
-                        launch_bdpt_trace_a<decltype(K)::value>(l, c.sc, S, c.cam, B, BR, BI, N, items_total);
-                    });
+                    k_bdpt_alists<<<gN, BLOCK, 0, sm>>>(B, BR, BI, N, items_total);
+                    for (int kind = 0; kind < 2; ++kind)
+                        launch_trav(c, (uint64_t)totals[0], [&](auto K, const TravLaunch& l) {
+                            launch_bdpt_trace_a<decltype(K)::value>(l, c.sc, S, c.cam, B, BR, BI, N, items_total, kind);
+                        });
                 }
                 StageTimer tm(c, c.o.timing, ST_BD_EVAL_A);
                 const int grid = std::min(ceil_div(totals[0], BLOCK), 1 << 16);
@@ -2737,6 +2750,7 @@ void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
         case LUMO_OPT_TAIL_BOUNCES: lo = -1; hi = 16; break;
         case LUMO_OPT_STACK_CLASS: hi = 64; break;
         case LUMO_OPT_BDPT_GROUPS: lo = 1; hi = 4; break;
+        case LUMO_OPT_RAY_SORT: lo = -1; hi = 2; break;
         default: break;
     }
 }

@@ -50,7 +50,7 @@ void launch_bdpt_redo(const TravLaunch& l, const DScene& sc, const Paths& S, con
                       const Bdpt& B, const Bdpt& R, const BItems& I);
 template <int STK>
 void launch_bdpt_trace_a(const TravLaunch& l, const DScene& sc, const Paths& S, const DCam& cam, const Bdpt& B,
-                         const Bdpt& R, const BItems& I, int n, const uint32_t* totals);
+                         const Bdpt& R, const BItems& I, int n, const uint32_t* totals, int kind);
 template <int STK>
 void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, const Bdpt& B, const Bdpt& R,
                      const BItems& I, int n, const uint32_t* totals);
@@ -74,7 +74,8 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
     extern template void launch_bdpt_redo<K>(const TravLaunch&, const DScene&, const Paths&, const Tasks&,        \
                                              const DCam&, const Bdpt&, const Bdpt&, const BItems&);               \
     extern template void launch_bdpt_trace_a<K>(const TravLaunch&, const DScene&, const Paths&, const DCam&,      \
-                                                const Bdpt&, const Bdpt&, const BItems&, int, const uint32_t*);   \
+                                                const Bdpt&, const Bdpt&, const BItems&, int, const uint32_t*,    \
+                                                int);                                                             \
     extern template void launch_bdpt_vis<K>(const TravLaunch&, const DScene&, const Paths&, const Bdpt&,          \
                                             const Bdpt&, const BItems&, int, const uint32_t*);
 #ifndef LUMO_STK

@@ -11,7 +11,7 @@ namespace dev {
 // ------------------------------------------------------------------ closest hit
 // LDS: 0 scene in HBM, 1 whole scene staged, 2 TOP staging (TOP_BLOCK threads per block).
 template <int STK, int LDS, int FX>
-__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_CLOSEST_WAVES) void k_closest(DScene sc0, Paths S,
+__global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_WALK_WAVES) void k_closest(DScene sc0, Paths S,
                                                                                              const int32_t* queue,
                                                                                              uint32_t tail_below) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];

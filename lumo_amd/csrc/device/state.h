@@ -24,6 +24,12 @@ constexpr int TOP_BLOCK = 1024;
 #ifndef LUMO_SHADOW_WAVES
 #define LUMO_SHADOW_WAVES 4
 #endif
+#ifndef LUMO_BDTRACE_WAVES  // BDPT (a)-item traces and (b)-item visibility
+#define LUMO_BDTRACE_WAVES LUMO_SHADOW_WAVES
+#endif
+#ifndef LUMO_WALK_WAVES  // BDPT subpath walks' closest hits (k_closest)
+#define LUMO_WALK_WAVES LUMO_CLOSEST_WAVES
+#endif
 #ifndef LUMO_SHADE_WAVES  // k_shade_q: 2 waves/SIMD measured best (C3 shade 411 -> 337 ms, C1 neutral)
 #define LUMO_SHADE_WAVES 2
 #endif
