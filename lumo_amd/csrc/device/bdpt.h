@@ -665,7 +665,7 @@ struct BItems {
     uint32_t *n_a, *n_b;  // items per slot: (a) t = 1, s = 0, s = 1 strategies; (b) s, t >= 2
     uint32_t *off_a, *off_b;  // exclusive scans
     double *term_a, *term_b;  // 4 per item
-    uint8_t* vis;         // per (b) item: bdpt_visible
+
     double* a_t;          // per (a) item: the traced hit (t = 1: Scene::hit; s = 1: a_tri = light triangle or -1)
     int32_t *a_kind, *a_obj, *a_tri;
     double* pdf;          // running pdf_fwd of the walk
@@ -677,6 +677,11 @@ struct BItems {
     // [0, alist_cap), light rays of s = 1 connections at [alist_cap, 2 alist_cap)
     int32_t* alist;
     size_t alist_cap;
+    // the (b) items past lumo's guard (neither vertex delta, the camera vertex not on a light) at
+    // [0, blist_cap), and of those the visible ones at [blist_cap, 2 blist_cap) (k_bdpt_blists,
+    // k_bdpt_vis); every other (b) item's term is 0
+    int32_t* blist;
+    size_t blist_cap;
 };
 __device__ __forceinline__ uint32_t bdpt_n_a(int S, int T) { return (uint32_t)(S + T - 1); }
 __device__ __forceinline__ uint32_t bdpt_n_b(int S, int T) { return (uint32_t)(S - 1) * (uint32_t)(T - 1); }
@@ -1096,6 +1101,45 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_alists(Bdpt B, Bdpt R, BItems I,
         if (!((e.X->cp.I(2, t - 1, e.si) & VF_DELTA) || e.X->cp.I(1, t - 1, e.si) >= 0))
             I.alist[I.alist_cap + kl++] = (int32_t)(q0 + (uint32_t)(Sl + t - 2));
 }
+
+// The (b) items of each slot that pass the guard of connect_paths before its visibility test
+// (bd_path_trace.rs:279-290: neither vertex delta, the camera vertex not on a light), listed for
+// k_bdpt_vis (counted in totals[4]); every other item's term is 0, written here.
+__global__ __launch_bounds__(BLOCK) void k_bdpt_blists(Bdpt B, Bdpt R, BItems I, int n, uint32_t* totals) {
+    const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = slot < n && I.n_b[slot] > 0;
+    ItemSel e{0, 0, &B};
+    int Sl = 0, Tc = 0;
+    uint32_t nc = 0, cams = 0, lights = 0;
+    if (live) {
+        e = item_store(B, R, slot);
+        Sl = I.nl[slot];
+        Tc = I.nc[slot];
+        for (int s = 2; s <= Sl; ++s) lights += (e.X->lp.I(2, s - 1, e.si) & VF_DELTA) ? 0u : 1u;
+        for (int t = 2; t <= Tc; ++t)
+            cams += ((e.X->cp.I(2, t - 1, e.si) & VF_DELTA) || e.X->cp.I(1, t - 1, e.si) >= 0) ? 0u : 1u;
+        nc = lights * cams;
+    }
+    uint32_t tot;
+    const uint32_t p = wave_excl_scan(nc, tot);
+    uint32_t b = 0;
+    if (lane_id() == 0 && tot) b = atomicAdd(totals + 4, tot);
+    b = __shfl(b, 0, 64);
+    if (!live) return;
+    const uint32_t q0 = I.off_b[slot];
+    uint32_t k = b + p;
+    for (int t = 2; t <= Tc; ++t) {  // item q0 + (t - 2)(S - 1) + (s - 2): t major (item_b_st)
+        const bool ct = !((e.X->cp.I(2, t - 1, e.si) & VF_DELTA) || e.X->cp.I(1, t - 1, e.si) >= 0);
+        for (int s = 2; s <= Sl; ++s) {
+            const uint32_t q = q0 + (uint32_t)(t - 2) * (uint32_t)(Sl - 1) + (uint32_t)(s - 2);
+            if (ct && !(e.X->lp.I(2, s - 1, e.si) & VF_DELTA)) {
+                I.blist[k++] = (int32_t)q;
+            } else {
+                for (int i = 0; i < NS; ++i) I.term_b[4 * (size_t)q + i] = 0.0;
+            }
+        }
+    }
+}
 #endif  // LUMO_MAIN_TU
 
 // (a) items, traversal part: the camera ray of each t = 1 connection and the light ray of each
@@ -1145,24 +1189,57 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_BDTRACE_WAVES) v
     flush_counters(C, S.tcount + TC_N);
 }
 
-// (a) items, evaluation: lumo's connection code with the traces looked up
-template <int FX>
+// (a) items, evaluation: lumo's connection code with the traces looked up.  KIND 0: the t = 1
+// camera connections of k_bdpt_alists's first list, KIND 1: the s = 1 light connections of its
+// second, so a wave runs one connection's code; KIND 2: one thread per slot for the rest, the
+// camera subpath's own emission (s = 0) and the connections whose vertex is delta (or, s = 1, on a
+// light), which produce no splat and a zero term (connect_light_path / connect_camera_path return
+// before any draw is used or query counted).
+template <int FX, int KIND>
 __global__ __launch_bounds__(BLOCK) void k_bdpt_eval_a(DScene sc, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n,
                                                         const uint32_t* totals) {
-    const uint32_t total = totals[0];
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+    if constexpr (KIND == 2) {
+        const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+        if (slot >= n || I.n_a[slot] == 0) return;
+        const ItemSel e = item_store(B, R, slot);
+        const Bdpt& X = *e.X;
+        const int si = e.si;
+        const int Sl = I.nl[slot], Tc = I.nc[slot];
+        const uint32_t q0 = I.off_a[slot];
+        auto zero = [&](uint32_t q) {
+            for (int i = 0; i < NS; ++i) I.term_a[4 * (size_t)q + i] = 0.0;
+        };
+        for (int s = 2; s <= Sl; ++s)
+            if (X.lp.I(2, s - 1, si) & VF_DELTA) {
+                X.Ok(s - 2, si) = 0;
+                zero(q0 + (uint32_t)(s - 2));
+            }
+        double L[NS];
+        for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * slot + i];
+        const PView cp{&X.cp, si, nullptr};
+        const DColor term = add_camera_path<FX>(sc, cam, L, cp, Tc);
+        const uint32_t qe = q0 + (uint32_t)(Sl - 1);
+        for (int i = 0; i < NS; ++i) I.term_a[4 * (size_t)qe + i] = term.s[i];
+        for (int t = 2; t <= Tc; ++t)
+            if ((X.cp.I(2, t - 1, si) & VF_DELTA) || X.cp.I(1, t - 1, si) >= 0) zero(q0 + (uint32_t)(Sl + t - 2));
+        return;
+    }
+    const uint32_t total = totals[2 + KIND];
+    const int32_t* list = I.alist + (size_t)KIND * I.alist_cap;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x) {
+        const uint32_t q = (uint32_t)list[k];
         const int slot = item_slot(I.off_a, n, q);
         const ItemSel e = item_store(B, R, slot);
         const Bdpt& X = *e.X;
         const int si = e.si;
         const uint32_t j = q - I.off_a[slot];
-        const int Sl = I.nl[slot], Tc = I.nc[slot];
+        const int Sl = I.nl[slot];
         double L[NS];
         for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * slot + i];
         const PView lp{&X.lp, si, nullptr}, cp{&X.cp, si, nullptr};
         uint32_t queries = 0;
         DColor term = cfill(0.0);
-        if (j < (uint32_t)(Sl - 1)) {
+        if constexpr (KIND == 0) {
             const int s = (int)j + 2;
             const BVtx ll = X.lp.load(s - 1, si);
             const V2 rs = ll.del ? V2{0.0, 0.0} : V2{X.Dr(0, s - 2, si), X.Dr(1, s - 2, si)};
@@ -1177,8 +1254,6 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_eval_a(DScene sc, Paths S, DCam 
                 X.sp.D(1, s - 2, si) = raster.y;
                 for (int k = 0; k < NS; ++k) X.sp.D(2 + k, s - 2, si) = color.s[k];
             }
-        } else if (j == (uint32_t)(Sl - 1)) {
-            term = add_camera_path<FX>(sc, cam, L, cp, Tc);
         } else {
             const int t = (int)j - Sl + 2;
             const BVtx cl = X.cp.load(t - 1, si);
@@ -1200,16 +1275,19 @@ __device__ __forceinline__ void item_b_st(const BItems& I, int slot, uint32_t q,
     s = 2 + (int)(k % sm1);
 }
 
-// bdpt_visible of every (b) item whose guard reaches it (bd_path_trace.rs:279-290)
+// bdpt_visible of every (b) item whose guard reaches it (bd_path_trace.rs:279-290), over the list
+// of those items (k_bdpt_blists): the visible ones go to the second list (totals[5], one append
+// atomic per wave), an invisible one's term is 0.
 template <int STK, int LDS, int FX>
 __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_BDTRACE_WAVES) void k_bdpt_vis(
-    DScene sc0, Paths S, Bdpt B, Bdpt R, BItems I, int n, const uint32_t* totals) {
+    DScene sc0, Paths S, Bdpt B, Bdpt R, BItems I, int n, uint32_t* totals) {
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
-    const uint32_t total = totals[1];
+    const uint32_t total = totals[4];
     if (total <= blockIdx.x * blockDim.x) return;
     const DScene sc = LDS == 1 ? stage_scene_lds(sc0, lds_scene) : (LDS == 2 ? stage_top_lds(sc0, lds_scene) : sc0);
     Counters C{0, 0, 0};
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x) {
+        const uint32_t q = (uint32_t)I.blist[k];
         const int slot = item_slot(I.off_b, n, q);
         const ItemSel e = item_store(B, R, slot);
         int s, t;
@@ -1229,17 +1307,27 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_BDTRACE_WAVES) v
             b.p = V3{cv.D(0, t - 1, e.si), cv.D(1, t - 1, e.si), cv.D(2, t - 1, e.si)};
             vis = bdpt_visible<STK, FX, LDS == 2>(sc, a, b, C);
         }
-        I.vis[q] = vis ? 1 : 0;
+        const uint64_t m = __ballot(vis);  // the lanes still in the loop
+        if (m) {
+            const int lead = __ffsll((unsigned long long)m) - 1;
+            uint32_t base = 0;
+            if (lane_id() == lead) base = atomicAdd(totals + 5, (uint32_t)__popcll(m));
+            base = __shfl(base, lead, 64);
+            if (vis) I.blist[I.blist_cap + base + mbcnt64(m)] = (int32_t)q;
+        }
+        if (!vis)
+            for (int i = 0; i < NS; ++i) I.term_b[4 * (size_t)q + i] = 0.0;
     }
     flush_counters(C, S.tcount + TC_N);  // counted with the visibility (shadow) class
 }
 
-// MIS weight and contribution of every (b) item (bd_path_trace.rs:148-277), visibility from k_bdpt_vis
+// MIS weight and contribution of every visible (b) item (bd_path_trace.rs:148-277), over k_bdpt_vis's list
 template <int FX>
 __global__ __launch_bounds__(BLOCK) void k_bdpt_paths(DScene sc, Paths S, DCam cam, Bdpt B, Bdpt R, BItems I, int n,
                                                        const uint32_t* totals) {
-    const uint32_t total = totals[1];
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+    const uint32_t total = totals[5];
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x) {
+        const uint32_t q = (uint32_t)I.blist[I.blist_cap + k];
         const int slot = item_slot(I.off_b, n, q);
         const ItemSel e = item_store(B, R, slot);
         int s, t;
@@ -1248,7 +1336,7 @@ __global__ __launch_bounds__(BLOCK) void k_bdpt_paths(DScene sc, Paths S, DCam c
         for (int i = 0; i < NS; ++i) L[i] = S.lam[4 * slot + i];
         const PView lp{&e.X->lp, e.si, nullptr}, cp{&e.X->cp, e.si, nullptr};
         const DColor term = connect_paths<FX>(sc, cam, L, lp, s, cp, t, e.X->lp.load(s - 1, e.si),
-                                              e.X->cp.load(t - 1, e.si), I.vis[q] != 0);
+                                              e.X->cp.load(t - 1, e.si), true);
         for (int i = 0; i < NS; ++i) I.term_b[4 * (size_t)q + i] = term.s[i];
     }
 }
@@ -1297,8 +1385,7 @@ __global__ void k_bdpt_total(BItems I, int n, uint32_t* totals) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         totals[0] = I.off_a[n - 1] + I.n_a[n - 1];
         totals[1] = I.off_b[n - 1] + I.n_b[n - 1];
-        totals[2] = 0u;
-        totals[3] = 0u;
+        for (int k = 2; k < 8; ++k) totals[k] = 0u;
     }
 }
 #endif  // LUMO_MAIN_TU

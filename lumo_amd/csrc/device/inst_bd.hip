@@ -68,7 +68,7 @@ void launch_bdpt_trace_a(const TravLaunch& l, const DScene& sc, const Paths& S, 
 
 template <int STK>
 void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, const Bdpt& B, const Bdpt& R,
-                     const BItems& I, int n, const uint32_t* totals) {
+                     const BItems& I, int n, uint32_t* totals) {
     LUMO_TRAV_LAUNCH_TOP(k_bdpt_vis, TOP_BLOCK, sc, S, B, R, I, n, totals);
 }
 
@@ -81,7 +81,7 @@ template void launch_bdpt_redo<LUMO_STK>(const TravLaunch&, const DScene&, const
 template void launch_bdpt_trace_a<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const DCam&, const Bdpt&,
                                             const Bdpt&, const BItems&, int, const uint32_t*, int);
 template void launch_bdpt_vis<LUMO_STK>(const TravLaunch&, const DScene&, const Paths&, const Bdpt&, const Bdpt&,
-                                        const BItems&, int, const uint32_t*);
+                                        const BItems&, int, uint32_t*);
 
 }  // namespace dev
 }  // namespace lumo

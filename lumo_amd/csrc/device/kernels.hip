@@ -1040,6 +1040,24 @@ double busy_ms(const Ctx& c, uint32_t mask) {
     return total;
 }
 
+// The (a) items' evaluation: the two trace lists (camera, light connections), then per slot the rest.
+template <int FX>
+void launch_eval_a_fx(int grid, int grid_slots, hipStream_t sm, const DScene& sc, const Paths& S, const DCam& cam,
+                      const Bdpt& B, const Bdpt& R, const BItems& I, int n, const uint32_t* totals) {
+    k_bdpt_eval_a<FX, 0><<<grid, BLOCK, 0, sm>>>(sc, S, cam, B, R, I, n, totals);
+    k_bdpt_eval_a<FX, 1><<<grid, BLOCK, 0, sm>>>(sc, S, cam, B, R, I, n, totals);
+    k_bdpt_eval_a<FX, 2><<<grid_slots, BLOCK, 0, sm>>>(sc, S, cam, B, R, I, n, totals);
+}
+void launch_eval_a(int fx, int grid, int grid_slots, hipStream_t sm, const DScene& sc, const Paths& S, const DCam& cam,
+                   const Bdpt& B, const Bdpt& R, const BItems& I, int n, const uint32_t* totals) {
+    if (fx == 2)
+        launch_eval_a_fx<2>(grid, grid_slots, sm, sc, S, cam, B, R, I, n, totals);
+    else if (fx)
+        launch_eval_a_fx<1>(grid, grid_slots, sm, sc, S, cam, B, R, I, n, totals);
+    else
+        launch_eval_a_fx<0>(grid, grid_slots, sm, sc, S, cam, B, R, I, n, totals);
+}
+
 // Stack-class dispatch (launch.h STACK_CLASSES).
 template <typename F>
 void by_stack_class(int cls, F&& f) {
@@ -1742,7 +1760,7 @@ struct BdGroup {
 };
 
 // Per-group work buffers (k: BdBuf), grown on demand like the render's own.
-enum BdBuf { BG_TERM_A, BG_TERM_B, BG_VIS, BG_AT, BG_AKIND, BG_AOBJ, BG_ATRI, BG_ALIST, BG_SCAN, BG_RANGES, BG_TAPS,
+enum BdBuf { BG_TERM_A, BG_TERM_B, BG_BLIST, BG_AT, BG_AKIND, BG_AOBJ, BG_ATRI, BG_ALIST, BG_SCAN, BG_RANGES, BG_TAPS,
              BG_RLD, BG_RLI, BG_RCD, BG_RCI, BG_RSP, BG_RSPN, BG_RDRAWS, BG_ROK, BG_RLM, BG_RLMF, BG_RCM, BG_RCMF,
              BG_REDO, BG_COUNT };
 template <typename T>
@@ -1853,7 +1871,7 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
         I.cam_d = BI.cam_d + 3 * o;
         I.rng0 = BI.rng0 + 2 * o;
         I.lam0 = BI.lam0 + 4 * o;
-        q.totals = items_total + 4 * g;
+        q.totals = items_total + 8 * g;
     }
     if (st) return st;
     // every group stream waits for the render's setup on stream 0 (tables, seeds, zeroing, ring)
@@ -1965,7 +1983,7 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
         const uint32_t tot[2] = {c.bd_totals_h[2 * gi], c.bd_totals_h[2 * gi + 1]};
         auto cap = [](uint32_t x) { return (size_t)std::max<uint64_t>(1, (uint64_t)x + x / 4); };  // grown with headroom
         const size_t ca = cap(tot[0]), cb = cap(tot[1]);
-        const size_t need[BG_SCAN] = {4 * ca * 8, 4 * cb * 8, cb, ca * 8, ca * 4, ca * 4, ca * 4, 2 * ca * 4};
+        const size_t need[BG_SCAN] = {4 * ca * 8, 4 * cb * 8, 2 * cb * 4, ca * 8, ca * 4, ca * 4, ca * 4, 2 * ca * 4};
         for (int k = 0; k < BG_SCAN; ++k)  // a buffer that grows is freed: nothing of this group may be using it
             if (c.gwork.size() > (size_t)gi * BG_COUNT + k && c.gwork[(size_t)gi * BG_COUNT + k].bytes < need[k]) {
                 HIPCHK(hipStreamSynchronize(q.sm));
@@ -1973,7 +1991,8 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
             }
         q.I.term_a = gbuf<double>(c, gi, BG_TERM_A, 4 * ca, st);
         q.I.term_b = gbuf<double>(c, gi, BG_TERM_B, 4 * cb, st);
-        q.I.vis = gbuf<uint8_t>(c, gi, BG_VIS, cb, st);
+        q.I.blist = gbuf<int32_t>(c, gi, BG_BLIST, 2 * cb, st);
+        q.I.blist_cap = cb;
         q.I.a_t = gbuf<double>(c, gi, BG_AT, ca, st);
         q.I.a_kind = gbuf<int32_t>(c, gi, BG_AKIND, ca, st);
         q.I.a_obj = gbuf<int32_t>(c, gi, BG_AOBJ, ca, st);
@@ -1991,17 +2010,13 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
                     }, q.sm);
             }
             StageTimer tm(c, c.o.timing, ST_BD_EVAL_A, q.sm);
-            const int grid = std::min(ceil_div(tot[0], BLOCK), 1 << 16);
-            if (fx == 2)
-                k_bdpt_eval_a<2><<<grid, BLOCK, 0, q.sm>>>(c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
-            else if (fx)
-                k_bdpt_eval_a<1><<<grid, BLOCK, 0, q.sm>>>(c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
-            else
-                k_bdpt_eval_a<0><<<grid, BLOCK, 0, q.sm>>>(c.sc, q.S, c.cam, q.B, q.R, q.I, q.n, q.totals);
+            launch_eval_a(fx, std::min(ceil_div(tot[0], BLOCK), 1 << 16), ceil_div(q.n, BLOCK), q.sm, c.sc, q.S, c.cam,
+                          q.B, q.R, q.I, q.n, q.totals);
         }
         if (tot[1] > 0) {
             {
                 StageTimer tm(c, c.o.timing, ST_BD_VIS, q.sm);
+                k_bdpt_blists<<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(q.B, q.R, q.I, q.n, q.totals);
                 // textured scenes (fx 2) have no TOP variant: their full-grid launch
                 launch_trav(c, (uint64_t)tot[1], [&](auto K, const TravLaunch& l) {
                     launch_bdpt_vis<decltype(K)::value>(l, c.sc, q.S, q.B, q.R, q.I, q.n, q.totals);
@@ -2301,7 +2316,7 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
         BI.cam_d = wbuf<double>(c, W_BD_CAMD, 3 * (size_t)N, st);
         BI.rng0 = wbuf<uint64_t>(c, W_BD_RNG0, 2 * (size_t)N, st);
         BI.lam0 = wbuf<double>(c, W_BD_LAM0, 4 * (size_t)N, st);
-        items_total = wbuf<uint32_t>(c, W_BD_ITOTAL, 16, st);  // (a), (b) and the (a) trace lists' counts per task group
+        items_total = wbuf<uint32_t>(c, W_BD_ITOTAL, 32, st);  // (a), (b) and the item lists' counts per task group
         BR = B;
         BR.lp = VStore{wbuf<double>(c, W_BDR_LD, (size_t)VD_N * VR * NR, st), wbuf<int32_t>(c, W_BDR_LI, (size_t)VI_N * VR * NR, st), VR, NR,
                        wbuf<double>(c, W_BDR_LM, (size_t)2 * VR * NR, st), wbuf<int32_t>(c, W_BDR_LMF, (size_t)VR * NR, st)};
@@ -2529,7 +2544,8 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             HIPCHK(hipStreamSynchronize(sm));
             BI.term_a = wbuf<double>(c, W_BD_TERM, 4 * (size_t)std::max(totals[0], 1u), st);
             BI.term_b = wbuf<double>(c, W_BD_TERMB, 4 * (size_t)std::max(totals[1], 1u), st);
-            BI.vis = wbuf<uint8_t>(c, W_BD_VIS, std::max(totals[1], 1u), st);
+            BI.blist = wbuf<int32_t>(c, W_BD_VIS, 2 * (size_t)std::max(totals[1], 1u), st);
+            BI.blist_cap = std::max(totals[1], 1u);
             BI.a_t = wbuf<double>(c, W_BD_AT, std::max(totals[0], 1u), st);
             BI.a_kind = wbuf<int32_t>(c, W_BD_AKIND, std::max(totals[0], 1u), st);
             BI.a_obj = wbuf<int32_t>(c, W_BD_AOBJ, std::max(totals[0], 1u), st);
@@ -2547,17 +2563,13 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
                         });
                 }
                 StageTimer tm(c, c.o.timing, ST_BD_EVAL_A);
-                const int grid = std::min(ceil_div(totals[0], BLOCK), 1 << 16);
-                if (c.sc.full == 2)
-                    k_bdpt_eval_a<2><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
-                else if (c.sc.full)
-                    k_bdpt_eval_a<1><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
-                else
-                    k_bdpt_eval_a<0><<<grid, BLOCK, 0, sm>>>(c.sc, S, c.cam, B, BR, BI, N, items_total);
+                launch_eval_a(c.sc.full, std::min(ceil_div(totals[0], BLOCK), 1 << 16), gN, sm, c.sc, S, c.cam, B, BR, BI,
+                              N, items_total);
             }
             if (totals[1] > 0) {
                 {
                     StageTimer tm(c, c.o.timing, ST_BD_VIS);
+                    k_bdpt_blists<<<gN, BLOCK, 0, sm>>>(B, BR, BI, N, items_total);
                     launch_trav(
                         c, (uint64_t)totals[1],
                         [&](auto K, const TravLaunch& l) {

@@ -53,7 +53,7 @@ void launch_bdpt_trace_a(const TravLaunch& l, const DScene& sc, const Paths& S, 
                          const Bdpt& R, const BItems& I, int n, const uint32_t* totals, int kind);
 template <int STK>
 void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, const Bdpt& B, const Bdpt& R,
-                     const BItems& I, int n, const uint32_t* totals);
+                     const BItems& I, int n, uint32_t* totals);
 
 #define LUMO_EXTERN_STK(K)                                                                                        \
     extern template void launch_closest<K>(const TravLaunch&, const DScene&, const Paths&, const int32_t*,        \
@@ -77,7 +77,7 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
                                                 const Bdpt&, const Bdpt&, const BItems&, int, const uint32_t*,    \
                                                 int);                                                             \
     extern template void launch_bdpt_vis<K>(const TravLaunch&, const DScene&, const Paths&, const Bdpt&,          \
-                                            const Bdpt&, const BItems&, int, const uint32_t*);
+                                            const Bdpt&, const BItems&, int, uint32_t*);
 #ifndef LUMO_STK
 LUMO_EXTERN_STK(4)
 LUMO_EXTERN_STK(8)
