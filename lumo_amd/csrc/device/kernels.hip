@@ -1374,19 +1374,18 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
         }, sm);
         return;
     }
-    Paths Sc = S;  // the closest-hit launch's view: with the queue's sort order when rays are sorted
-    const int sort_mode = ray_sort_mode(c);
-    if (sort_mode && S.hq.tmp && ub >= kSortMin && (uint64_t)ub <= S.hq.cap) {
+    {   // the closest hits; with ray sorting, the rays' sort order first (timed as one closest-hit launch)
+        Paths Sc = S;
         StageTimer tm(c, c.o.timing, ST_CLOSEST, sm);
-        k_sort_keys<<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(cur, S.counts, ub, c.sort_lo, c.sort_scale, S.hq.sk[0],
-                                                           S.hq.sv[0], sort_mode);
-        hipcub::DoubleBuffer<uint32_t> kb(S.hq.sk[0], S.hq.sk[1]), vb(S.hq.sv[0], S.hq.sv[1]);
-        size_t tb = S.hq.tmp_bytes;
-        if (hipcub::DeviceRadixSort::SortPairs(S.hq.tmp, tb, kb, vb, (int)ub, 0, 30, sm) == hipSuccess)
-            Sc.hq.perm = vb.Current();
-    }
-    {
-        StageTimer tm(c, c.o.timing, ST_CLOSEST, sm);
+        const int sort_mode = ray_sort_mode(c);
+        if (sort_mode && S.hq.tmp && ub >= kSortMin && (uint64_t)ub <= S.hq.cap) {
+            k_sort_keys<<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(cur, S.counts, ub, c.sort_lo, c.sort_scale, S.hq.sk[0],
+                                                               S.hq.sv[0], sort_mode);
+            hipcub::DoubleBuffer<uint32_t> kb(S.hq.sk[0], S.hq.sk[1]), vb(S.hq.sv[0], S.hq.sv[1]);
+            size_t tb = S.hq.tmp_bytes;
+            if (hipcub::DeviceRadixSort::SortPairs(S.hq.tmp, tb, kb, vb, (int)ub, 0, 30, sm) == hipSuccess)
+                Sc.hq.perm = vb.Current();
+        }
         launch_trav(
             c, ub, [&](auto K, const TravLaunch& l) { launch_closest_q<decltype(K)::value>(l, c.sc, Sc, cur, skip); },
             sm, true);

@@ -21,3 +21,7 @@ timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -
 timeout -s KILL 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_FLAT SQ_INSTS_LDS \
   --output-format csv -d $OUT/valu -o run -- python3 $REPO/bench.py $ARGS > $OUT/bench_valu.json 2> $OUT/valu.err
 cd $REPO && python3 tools/parse_prof.py $OUT > $OUT/summary.json
+# keep the summaries (the per-dispatch CSVs of a long run exceed what a gpurun call copies back)
+if [ -z "$KEEP_CSV" ]; then
+  find $OUT -name '*.csv' ! -name 'run_kernel_stats.csv' -delete
+fi
