@@ -545,7 +545,10 @@ struct LdsSrc {  // sources staged in LDS by k_finish_film
 // virtual slots + m * vstride) in pass order, the tile's film accumulators held in registers
 // across them.  Same arithmetic and additions in the same order as one k_finish + k_film per
 // pass, so the film is bit-identical.
-__global__ __launch_bounds__(BLOCK) void k_finish_film(DScene sc, Paths S0, Tasks T, DCam cam, uint32_t pass0,
+#ifndef LUMO_FILM_WAVES  // k_finish_film: 129 VGPRs gave 3 waves / SIMD; 4 fit its LDS (4 x 33 KB per CU)
+#define LUMO_FILM_WAVES 4
+#endif
+__global__ __launch_bounds__(BLOCK, LUMO_FILM_WAVES) void k_finish_film(DScene sc, Paths S0, Tasks T, DCam cam, uint32_t pass0,
                                                         Dump dump, int dump_p, int tone_map, double tone_arg, int t0,
                                                         int npass, int vstride) {
     __shared__ double l_rgb[3 * BLOCK];
