@@ -257,21 +257,31 @@ __device__ __forceinline__ uint32_t spread3(uint32_t x) {  // 9 bits -> every th
     x = (x | (x << 2)) & 0x09249249u;
     return x;
 }
+__device__ __forceinline__ uint32_t ray_key(V3 o, V3 d, V3 lo, V3 scale, int mode) {
+    auto cell = [](double x) { return (uint32_t)(x < 0.0 ? 0.0 : (x > 511.0 ? 511.0 : x)); };
+    const uint32_t m = spread3(cell((o.x - lo.x) * scale.x)) | (spread3(cell((o.y - lo.y) * scale.y)) << 1) |
+                       (spread3(cell((o.z - lo.z) * scale.z)) << 2);
+    const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
+    return mode == 2 ? (m << 3) | oct : (oct << 27) | m;  // 2: origin cell major
+}
 __global__ __launch_bounds__(BLOCK) void k_sort_keys(QState cur, const uint32_t* counts, uint32_t n, V3 lo, V3 scale,
                                                       uint32_t* keys, uint32_t* vals, int mode) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
-    uint32_t key = 0xffffffffu;
-    if (q < counts[CNT_CUR]) {
-        const V3 o = qv3(cur, QD_O, q), d = qv3(cur, QD_D, q);
-        auto cell = [](double x) { return (uint32_t)(x < 0.0 ? 0.0 : (x > 511.0 ? 511.0 : x)); };
-        const uint32_t m = spread3(cell((o.x - lo.x) * scale.x)) | (spread3(cell((o.y - lo.y) * scale.y)) << 1) |
-                           (spread3(cell((o.z - lo.z) * scale.z)) << 2);
-        const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
-        key = mode == 2 ? (m << 3) | oct : (oct << 27) | m;  // 2: origin cell major
-    }
-    keys[q] = key;
+    keys[q] = q < counts[CNT_CUR] ? ray_key(qv3(cur, QD_O, q), qv3(cur, QD_D, q), lo, scale, mode) : 0xffffffffu;
     vals[q] = q;
+}
+// ... of a BDPT walk bounce: the queue holds slot ids, the rays live per slot; the sorted values are
+// the slot ids in walk order (a queue in their own right)
+__global__ __launch_bounds__(BLOCK) void k_sort_keys_slots(const int32_t* queue, const double* ro, const double* rd,
+                                                            const uint32_t* counts, uint32_t n, V3 lo, V3 scale,
+                                                            uint32_t* keys, uint32_t* vals, int mode) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const bool live = q < counts[CNT_CUR];
+    const int s = live ? queue[q] : 0;
+    keys[q] = live ? ray_key(ldv3(ro, s), ldv3(rd, s), lo, scale, mode) : 0xffffffffu;
+    vals[q] = (uint32_t)s;
 }
 
 // Setup zeroing of a render's accumulators and counters in one launch instead of a fill per
@@ -1764,7 +1774,7 @@ struct BdGroup {
 // Per-group work buffers (k: BdBuf), grown on demand like the render's own.
 enum BdBuf { BG_TERM_A, BG_TERM_B, BG_BLIST, BG_AT, BG_AKIND, BG_AOBJ, BG_ATRI, BG_ALIST, BG_SCAN, BG_RANGES, BG_TAPS,
              BG_RLD, BG_RLI, BG_RCD, BG_RCI, BG_RSP, BG_RSPN, BG_RDRAWS, BG_ROK, BG_RLM, BG_RLMF, BG_RCM, BG_RCMF,
-             BG_REDO, BG_COUNT };
+             BG_REDO, BG_SK0, BG_SK1, BG_SV0, BG_SV1, BG_STMP, BG_COUNT };
 template <typename T>
 T* gbuf(Ctx& c, int g, int k, size_t count, lumo_status& st) {
     if (c.gwork.size() < (size_t)4 * BG_COUNT) c.gwork.resize((size_t)4 * BG_COUNT);
@@ -1882,6 +1892,7 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
     const int SEG = Ctx::SNAP_RING / 4;
     const int ahead = std::max(1, std::min(c.o.bounce_ahead, SEG - 1));
     const int fx = c.sc.full;
+    const int walk_sort = c.o.ray_sort > 0 ? c.o.ray_sort : 0;  // walks: on request (LUMO_OPT_RAY_SORT 1 / 2)
     auto start_walk = [&](BdGroup& q, int phase) {
         q.phase = phase;
         q.walk = 0;
@@ -1916,6 +1927,23 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
         const uint32_t ub = q.ub;
         k_bounce_begin<<<1, 64, 0, q.sm>>>(q.S.counts, q.S.tcount + TC_HEADQ);
         const uint32_t skip = (uint64_t)ub < 4ull * c.o.bdpt_tail ? c.o.bdpt_tail : 0u;
+        if (walk_sort && skip == 0 && ub >= kSortMin) {  // the walk's rays sorted (lane order only)
+            StageTimer tm(c, c.o.timing, ST_CLOSEST, q.sm);
+            const size_t nq = (size_t)q.n;
+            uint32_t* sk0 = gbuf<uint32_t>(c, gi, BG_SK0, nq, st);
+            uint32_t* sk1 = gbuf<uint32_t>(c, gi, BG_SK1, nq, st);
+            uint32_t* sv0 = gbuf<uint32_t>(c, gi, BG_SV0, nq, st);
+            uint32_t* sv1 = gbuf<uint32_t>(c, gi, BG_SV1, nq, st);
+            hipcub::DoubleBuffer<uint32_t> kb(sk0, sk1), vb(sv0, sv1);
+            size_t tb = 0;
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kb, vb, (int)nq, 0, 30, q.sm));
+            void* tmp = gbuf<char>(c, gi, BG_STMP, tb, st);
+            if (st) return st;
+            k_sort_keys_slots<<<ceil_div(ub, BLOCK), BLOCK, 0, q.sm>>>(qa, q.S.ro, q.S.rd, q.S.counts, ub, c.sort_lo,
+                                                                         c.sort_scale, sk0, sv0, walk_sort);
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kb, vb, (int)ub, 0, 30, q.sm));
+            qa = reinterpret_cast<int32_t*>(vb.Current());
+        }
         if (skip > 0) {
             StageTimer tm(c, c.o.timing, ST_RESOLVE, q.sm);
             launch_trav(c, std::min(ub, skip), [&](auto K, const TravLaunch& l) {

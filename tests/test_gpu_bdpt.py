@@ -255,3 +255,29 @@ def test_bdpt_task_groups(groups, film):
             assert len(s) == len(os_)
             np.testing.assert_array_equal(s["rgb"], os_["rgb"])
             np.testing.assert_array_equal(s["x"], os_["x"])
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_bdpt_walk_ray_sort(mode):
+    """Ray sorting of the BDPT walks (option ray_sort 1 / 2 in the task-group path): each walk
+    bounce's queue of slot ids is radix-sorted by its rays' direction octant and origin cell before
+    the closest hits and steps, which changes only the lane order; caustics.rs at 384x256 (49 k
+    slots per group, above the sort minimum), 1 pass: tiles, counts and splats equal the oracle's."""
+    sc, cam = _scene("caustics", (384, 256))
+    sc.build()
+    d = L.Device(0, ray_sort=mode)
+    try:
+        d.upload(sc, cam)
+        tasks = L.make_tasks(384, 256, 1, 0x50A7)
+        sp = []
+        bufs, rr = d.render_tasks(tasks, integrator=BDPT, splats_out=sp)
+        assert d.last_schedule().schedule == 3
+    finally:
+        d.close()
+    osp = []
+    obufs, orr, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, oracle_threads(), integrator=BDPT,
+                                   splats_out=osp)
+    for b, ob, r, o, s, os_ in zip(bufs, obufs, rr, orr, sp, osp):
+        np.testing.assert_array_equal(b, ob)
+        assert (r.num_rays, r.num_queries, r.num_camera_rays) == (o.num_rays, o.num_queries, o.num_camera_rays)
+        np.testing.assert_array_equal(s["rgb"], os_["rgb"])
