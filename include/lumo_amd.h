@@ -386,7 +386,7 @@ enum {
     LUMO_OPT_MERGE_PASSES,     /* fused and split pipelines: consecutive passes whose cameras and
                                   head bounces (those before Russian roulette) run as one queue,
                                   0 auto, 1-8 (LUMO_MERGE, 0)                                        */
-    LUMO_OPT_DYN_FETCH,        /* fused bounce: blocks fetch paths from a counter: 0 / 1 (LUMO_DYN, 1)*/
+    LUMO_OPT_DYN_FETCH,        /* fused bounce: blocks fetch paths from a counter: 0 / 1 (LUMO_DYN, 0)*/
     LUMO_OPT_BOUNCE_THREADS,   /* fused bounce: threads per block 64 / 128 / 256
                                   (LUMO_BOUNCE_THREADS, 256)                                        */
     LUMO_OPT_SPLIT_PIPE,       /* split schedule: units in flight 1-4 (LUMO_SPLIT_PIPE, 4)           */
@@ -395,7 +395,7 @@ enum {
                                   (LUMO_BDPT_TAIL, 65536)                                           */
     LUMO_OPT_BOUNCE_AHEAD,     /* bounces enqueued ahead of the host's count snapshots 1-63
                                   (LUMO_BOUNCE_AHEAD, 3)                                            */
-    LUMO_OPT_LDS_GRID,         /* persistent grid cap of LDS-staged kernels (LUMO_LDS_GRID, 2048)    */
+    LUMO_OPT_LDS_GRID,         /* grid cap of LDS-staged kernels (LUMO_LDS_GRID, 1.5 x CUs = 384)    */
     LUMO_OPT_TOP_GRID,         /* grid cap of TOP kernels (LUMO_TOP_GRID, the device's CU count)     */
     LUMO_OPT_TOP_KB,           /* upload: TOP set budget in KiB, <= the CU's LDS (LUMO_TOP_KB)       */
     LUMO_OPT_KD_LDS,           /* upload: kd stack entries per thread in LDS in TOP kernels

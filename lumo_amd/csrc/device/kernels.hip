@@ -844,13 +844,17 @@ struct Opts {
     int pipeline = 3;                  // fused passes overlapped (render_pipelined): 0 off, else head streams (1-3)
     int heads = 0;                     // pipelined passes: fused bounces per pass before the tail kernel (0: auto)
     int merge = 0;                     // pipelined passes: passes merged into one head unit (0: auto)
-    int dyn = 1;                       // k_bounce_q: blocks fetch their paths from a counter
+    int dyn = 0;                       // k_bounce_q: blocks fetch their paths from a counter (1) or take
+                                       // static grid-stride stripes (0; with lds_grid 384: C1 2 150 vs
+                                       // 2 350 ms per frame, 1/8 share 291 vs 367 ms, profiles/r05/ab/r05z*)
     int bounce_threads = BLOCK;        // k_bounce_q (fused, not tail): threads per block (64, 128 or 256)
     int split_pipe = 4;                // split schedule: units in flight (render_split_pipelined; 1 = sequential)
     int split_groups = 2;              // split schedule: independent task groups
     uint32_t bdpt_tail = 1u << 16;     // BDPT walks: k_bdpt_tail below this many live subpaths (0: never)
     int bounce_ahead = 3;              // bounces enqueued ahead of the host's count snapshots
-    int lds_grid = 2048;               // persistent grid cap of the LDS-staged kernels
+    int lds_grid = 384;                // grid cap of the LDS-staged kernels: 1.5 blocks per CU (set from the
+                                       // CU count at creation); the three head streams' launches and the
+                                       // tail stream's share the CUs instead of queueing behind each other
     int top_grid = 256;                // TOP kernels: blocks (one per CU; C3 shadow 438 ms per 8-spp frame vs 446 at
                                        // four per CU, 817 at half the CUs); set to the CU count at creation
     int top_kb = 160;                  // TOP set budget (KiB), at most the CU's LDS
@@ -2942,6 +2946,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
     if (!c) return LUMO_ERR_OOM;
     c->device = device;
     c->o.top_grid = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    c->o.lds_grid = c->o.top_grid * 3 / 2;
     if (prop.maxSharedMemoryPerMultiProcessor > 0) c->lds_cu = prop.maxSharedMemoryPerMultiProcessor;
     if (prop.sharedMemPerBlock > 0) c->lds_block = std::min(c->lds_cu, (size_t)prop.sharedMemPerBlock);
     c->o.top_kb = (int)(c->lds_cu / 1024);

@@ -843,7 +843,7 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
         const uint32_t nt = blockDim.x;
         uint32_t base = blockIdx.x * blockDim.x;
 #if LUMO_PHASE_CLOCKS
-        uint64_t ph[5] = {0, 0, 0, 0, 0}, tc0 = clock64(), tc1 = 0;
+        uint64_t ph[6] = {0, 0, 0, 0, 0, 0}, tc0 = clock64(), tc1 = 0;
         uint64_t lanes[4] = {0, 0, 0, 0};  // wave rounds; live lanes; lanes with an L record; with a B record
 #define LUMO_PHASE(k) (tc1 = clock64(), ph[k] += tc1 - tc0, tc0 = tc1)
 #else
@@ -939,6 +939,7 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
             uint32_t next_base = 0;
             const uint32_t np = dyn ? block_slot_fetch(alive, S.counts + CNT_NEXT, S.counts + CNT_FETCH_B, &next_base)
                                     : block_slot(alive, S.counts + CNT_NEXT);
+            LUMO_PHASE(5);
             if (alive) {
                 qv3(nxt, QD_O, np, rn.o);
                 qv3(nxt, QD_D, np, rn.d);
@@ -1004,11 +1005,13 @@ __global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_
             base = dyn ? next_base : base + gridDim.x * blockDim.x;
         }
 #if LUMO_PHASE_CLOCKS
-        // per wave (lane 0): cycles in the closest hit, shading, fetch, visibility and compaction
-        // phases (wave-uniform spans: every lane passes the same marks)
+        // per wave (lane 0): cycles in the closest hit, shading, visibility, fetch and next-queue
+        // store phases, then the lane counts, then the compaction's (block_slot) cycles
+        // (wave-uniform spans: every lane passes the same marks)
         if (lane_id() == 0) {
             for (int k = 0; k < 5; ++k) atomicAdd(S.tcount + TC_ALL + k, (unsigned long long)ph[k]);
             for (int k = 0; k < 4; ++k) atomicAdd(S.tcount + TC_ALL + 5 + k, (unsigned long long)lanes[k]);
+            atomicAdd(S.tcount + TC_ALL + 9, (unsigned long long)ph[5]);
         }
 #endif
     }

@@ -220,6 +220,28 @@ def test_bounce_modes_match_oracle(dev, cornell, fused, tail, pipe):
         dev.set_option("fused", -1).set_option("tail_below", 1 << 16).set_option("pipeline", 3)
 
 
+@pytest.mark.parametrize("dyn,grid", [(0, 384), (0, 7), (1, 2048), (1, 5)])
+def test_fused_fetch_modes_match_oracle(dev, cornell, dyn, grid):
+    """The fused bounce kernel's two ways of handing paths to blocks: static grid-stride stripes
+    (dyn 0, the default, at the default grid of 1.5 blocks per CU and at a grid of 7 blocks, so
+    every block strides many times) and blocks fetching 256 paths at a time from a counter
+    (dyn 1).  Tiles, ray and query counts equal the oracle's."""
+    d0, g0 = dev.option("dyn_fetch"), dev.option("lds_grid")
+    assert (d0, g0) == (0, 384)
+    dev.set_option("dyn_fetch", dyn).set_option("lds_grid", grid)
+    try:
+        cam = L.Camera.cornell_box((48, 40))
+        dev.upload(cornell, cam)
+        tasks = L.make_tasks(48, 40, 24, SEED)
+        bufs, res = dev.render_tasks(tasks)
+        obufs, ores, _ = O.render_tasks(cornell.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+        for b, ob, r, orr in zip(bufs, obufs, res, ores):
+            np.testing.assert_array_equal(b, ob)
+            assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
+    finally:
+        dev.set_option("dyn_fetch", d0).set_option("lds_grid", g0)
+
+
 @pytest.mark.parametrize("heads", [4, 5, 6, 8])
 def test_head_bounce_counts_match_oracle(cornell, heads):
     """Pipelined passes handing over to the tail kernel after 4, 5, 6 or 8 head bounces (the choice
@@ -246,7 +268,7 @@ def test_headline_schedule_matches_oracle(cornell):
     """The exact schedule behind the C1 bench line, at a size where the device picks it by itself:
     a pass of >= 2^21 slots (6 head bounces, the RR bounce on the head stream), 3 head streams
     rotating 4 sets of queues / counters / per-slot outputs (8 passes: every set is reused),
-    dynamic work fetch, max_paths = 2^23 (bench.py --max-paths).  Every tile's pixels, ray and
+    static grid-stride stripes, max_paths = 2^23 (bench.py --max-paths).  Every tile's pixels, ray and
     query counts, and the frame's closest / shadow query totals equal the oracle's (wavefront
     order).  Then the same frame without pipelining (pipeline 0: passes in sequence, one stream)
     must give the same bits: the cross-stream machinery adds nothing to any per-path result."""
