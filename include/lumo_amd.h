@@ -396,7 +396,7 @@ enum {
     LUMO_OPT_BOUNCE_AHEAD,     /* bounces enqueued ahead of the host's count snapshots 1-63
                                   (LUMO_BOUNCE_AHEAD, 3)                                            */
     LUMO_OPT_LDS_GRID,         /* grid cap of LDS-staged kernels (LUMO_LDS_GRID, 1.5 x CUs = 384)    */
-    LUMO_OPT_TOP_GRID,         /* grid cap of TOP kernels (LUMO_TOP_GRID, the device's CU count)     */
+    LUMO_OPT_TOP_GRID,         /* grid cap of TOP kernels (LUMO_TOP_GRID, half the CU count = 128)   */
     LUMO_OPT_TOP_KB,           /* upload: TOP set budget in KiB, <= the CU's LDS (LUMO_TOP_KB)       */
     LUMO_OPT_KD_LDS,           /* upload: kd stack entries per thread in LDS in TOP kernels
                                   (LUMO_KD_LDS, 8)                                                  */

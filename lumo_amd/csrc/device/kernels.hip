@@ -855,8 +855,10 @@ struct Opts {
     int lds_grid = 384;                // grid cap of the LDS-staged kernels: 1.5 blocks per CU (set from the
                                        // CU count at creation); the three head streams' launches and the
                                        // tail stream's share the CUs instead of queueing behind each other
-    int top_grid = 256;                // TOP kernels: blocks (one per CU; C3 shadow 438 ms per 8-spp frame vs 446 at
-                                       // four per CU, 817 at half the CUs); set to the CU count at creation
+    int top_grid = 128;                // TOP kernels: blocks of 1 024 threads, one per CU on half the CUs (set from
+                                       // the CU count at creation), so the split pipeline's concurrent units
+                                       // share the GPU: C2 4-spp 305 -> 288 ms, C3 64-spp 4 084 -> 4 007 ms, its
+                                       // 1/8 share 723 -> 692 ms against one block on every CU (r05t*)
     int top_kb = 160;                  // TOP set budget (KiB), at most the CU's LDS
     int kd_lds = 8;                    // kd stack entries per thread in LDS in TOP kernels when room is left (C2 -3 %)
     int stack_class = 0;               // kd stack class override (0: the scene's need)
@@ -2945,8 +2947,9 @@ lumo_status lumo_create(int device, void** ctx_out) {
     Ctx* c = new (std::nothrow) Ctx();
     if (!c) return LUMO_ERR_OOM;
     c->device = device;
-    c->o.top_grid = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    c->o.lds_grid = c->o.top_grid * 3 / 2;
+    const int cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    c->o.top_grid = std::max(1, cus / 2);
+    c->o.lds_grid = cus * 3 / 2;
     if (prop.maxSharedMemoryPerMultiProcessor > 0) c->lds_cu = prop.maxSharedMemoryPerMultiProcessor;
     if (prop.sharedMemPerBlock > 0) c->lds_block = std::min(c->lds_cu, (size_t)prop.sharedMemPerBlock);
     c->o.top_kb = (int)(c->lds_cu / 1024);
