@@ -207,6 +207,20 @@ LUMO_HD double lm_cos(double x) {
         default: return lm_ksin(y0, y1);
     }
 }
+// sin and cos of one argument: the reduction and each kernel evaluated once, each result the
+// same operations as lm_sin / lm_cos (|x| <= pi/4 is the reduction's n = 0 with tail 0).
+LUMO_HD void lm_sincos(double x, double& s, double& c) {
+    double y0 = x, y1 = 0.0;
+    int n = 0;
+    if (!(fabs(x) <= 0.7853981633974483)) n = lm_rem_pio2(x, y0, y1);
+    const double ks = lm_ksin(y0, y1), kc = lm_kcos(y0, y1);
+    switch (n & 3) {
+        case 0: s = ks; c = kc; break;
+        case 1: s = kc; c = -ks; break;
+        case 2: s = -ks; c = -kc; break;
+        default: s = -kc; c = ks; break;
+    }
+}
 
 // musl / fdlibm s_atan.c (the Rust `libm` crate that lumo's Complex::arg calls is a musl port)
 LUMO_HD double lm_atan(double x) {

@@ -10,6 +10,9 @@
 #define LUMO_COS lumo::lm_cos
 #define LUMO_SIN lumo::lm_sin
 #endif
+#ifndef LUMO_SINCOS  // (the oracle keeps two separate calls)
+#define LUMO_SINCOS(x, s, c) lumo::lm_sincos(x, s, c)
+#endif
 
 namespace lumo {
 
@@ -74,7 +77,9 @@ LUMO_HD V2 square_to_disk(V2 rand_sq) {
         r = offset.y;
         theta = PI * (0.5 - (offset.x / offset.y) / 4.0);
     }
-    return V2{r * LUMO_COS(theta), r * LUMO_SIN(theta)};
+    double s, c;
+    LUMO_SINCOS(theta, s, c);
+    return V2{r * c, r * s};
 }
 
 // maps.rs:29-36
@@ -89,7 +94,9 @@ LUMO_HD V3 square_to_sphere(V2 rand_sq) {
     const double z = 1.0 - 2.0 * rand_sq.y;
     const double r = sqrt(rmax(1.0 - z * z, 0.0));
     const double phi = 2.0 * PI * rand_sq.x;
-    return V3{r * LUMO_COS(phi), r * LUMO_SIN(phi), z};
+    double s, c;
+    LUMO_SINCOS(phi, s, c);
+    return V3{r * c, r * s, z};
 }
 
 }  // namespace lumo

@@ -3,6 +3,8 @@
 // (lumo_amd/csrc/common/{vec,rng}.h, themselves restatements of math/*.rs and rng.rs);
 // every algorithm below is restated here independently of the HIP kernels.
 #include "../oracle.h"
+// sin and cos as two separate calls (the product's rng.h maps share one reduction, lm_sincos)
+#define LUMO_SINCOS(x, s, c) ((s) = LUMO_SIN(x), (c) = LUMO_COS(x))
 
 #ifdef LUMO_ORACLE_GLIBC  // sensitivity build: platform libm as Rust std would call it
 #include <cmath>
