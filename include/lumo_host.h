@@ -138,7 +138,7 @@ int64_t lumo_make_tasks(int64_t width, int64_t height, uint64_t samples, uint64_
 
 /* Test hook: evaluate the render path's deterministic transcendentals (lmath.h) on the host.
  * which: 0 exp, 1 log1p, 2 cosh, 3 sin, 4 cos, 5 atan, 6 acos. */
-void lumo_lmath(int which, const double* x, double* y, int64_t n);
+void lumo_lmath(int which, const double* x, double* y, int64_t n);  /* 7 / 8: lm_sincos sin / cos */
 
 #ifdef __cplusplus
 }

@@ -386,6 +386,12 @@ void lumo_lmath(int which, const double* x, double* y, int64_t n) {
             case 3: y[i] = lm_sin(x[i]); break;
             case 5: y[i] = lm_atan(x[i]); break;
             case 6: y[i] = lm_acos(x[i]); break;
+            case 7: case 8: {  // lm_sincos: its sin (7) or cos (8)
+                double s, c;
+                lm_sincos(x[i], s, c);
+                y[i] = which == 7 ? s : c;
+                break;
+            }
             default: y[i] = lm_cos(x[i]); break;
         }
     }

@@ -42,3 +42,27 @@ def test_atan2_quadrants():
     y = np.zeros_like(x)
     L.lib().lumo_lmath(5, x.ctypes.data_as(_ffi.c_double_p), y.ctypes.data_as(_ffi.c_double_p), len(x))
     np.testing.assert_allclose(y, np.arctan(x), rtol=2.3e-16, atol=0)
+
+
+def _lm(which, x):
+    y = np.zeros_like(x)
+    L.lib().lumo_lmath(which, x.ctypes.data_as(_ffi.c_double_p), y.ctypes.data_as(_ffi.c_double_p), len(x))
+    return y
+
+
+def test_sincos_same_bits_as_sin_and_cos():
+    """lm_sincos (the disk and sphere maps, rng.h) returns exactly lm_sin's and lm_cos's values: the
+    arguments of square_to_disk (|theta| <= 3 pi / 4 and the pi / 4 boundaries), of
+    square_to_sphere (0 .. 2 pi), multiples of pi / 4 around the reduction's branch points, large
+    and tiny arguments, both signs, and NaN / inf."""
+    rng = np.random.default_rng(7)
+    q = np.pi / 4
+    x = np.concatenate([rng.uniform(-3 * q, 3 * q, 100000), rng.uniform(0.0, 2 * np.pi, 100000),
+                        rng.uniform(-1e5, 1e5, 20000),
+                        np.array([k * q for k in range(-16, 17)]),
+                        np.nextafter(np.array([k * q for k in range(-16, 17)]), np.inf),
+                        np.nextafter(np.array([k * q for k in range(-16, 17)]), -np.inf),
+                        np.array([0.0, -0.0, 1e-300, -1e-300, 1e-9, 3e5, -3e5, np.nan, np.inf, -np.inf])])
+    s, c = _lm(7, x), _lm(8, x)
+    np.testing.assert_array_equal(s.view(np.uint64), _lm(3, x).view(np.uint64))
+    np.testing.assert_array_equal(c.view(np.uint64), _lm(4, x).view(np.uint64))
