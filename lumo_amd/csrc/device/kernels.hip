@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <strings.h>
+#include <unistd.h>  // environ
 #include <deque>
 #include <new>
 #include <type_traits>
@@ -2780,6 +2781,26 @@ const char* const kOptEnv[LUMO_OPT_COUNT] = {
     "LUMO_POISON", "LUMO_TAIL_PRIORITY", "LUMO_TOP_KD", "LUMO_TAIL_BOUNCES", "LUMO_FILM_FIRST",
     "LUMO_BDPT_TOP", "LUMO_BDPT_GROUPS", "LUMO_RAY_SORT"};
 
+// A LUMO_* variable that names no option (e.g. a misspelt LUMO_TAIL_BELOW for LUMO_TAIL) would
+// otherwise be ignored without a trace: warn once per process.  LUMO_AMD_LIB and
+// LUMO_BENCH_BACKEND are read by the Python side.
+void warn_unknown_env() {
+    static bool done = false;
+    if (done) return;
+    done = true;
+    for (char** ev = environ; ev && *ev; ++ev) {
+        const char* kv = *ev;
+        if (std::strncmp(kv, "LUMO_", 5) != 0) continue;
+        const char* eq = std::strchr(kv, '=');
+        const size_t n = eq ? (size_t)(eq - kv) : std::strlen(kv);
+        bool known = false;
+        for (const char* name : kOptEnv) known = known || (std::strlen(name) == n && std::strncmp(name, kv, n) == 0);
+        for (const char* name : {"LUMO_AMD_LIB", "LUMO_BENCH_BACKEND"})
+            known = known || (std::strlen(name) == n && std::strncmp(name, kv, n) == 0);
+        if (!known) fprintf(stderr, "lumo_amd: %.*s names no option; ignored\n", (int)n, kv);
+    }
+}
+
 void opt_range(const Ctx& c, int k, int64_t& lo, int64_t& hi) {
     lo = 0;
     hi = 1;
@@ -3013,6 +3034,7 @@ lumo_status lumo_create(int device, void** ctx_out) {
         if (set_opt(*c, k, v) != LUMO_OK)
             fprintf(stderr, "lumo_amd: %s=%s not accepted; default kept\n", kOptEnv[k], e);
     }
+    warn_unknown_env();
     *ctx_out = c;
     return LUMO_OK;
 }

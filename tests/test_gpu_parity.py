@@ -557,3 +557,23 @@ def test_option_api(dev):
     finally:
         dev.set_option("split_pipe", 4)
         d2.close()
+
+
+@pytest.mark.gpu
+def test_environment_overrides_warn():
+    """Context creation reads the LUMO_* option overrides: a value that does not parse is ignored,
+    an out-of-range one clamped, and a LUMO_* name that is no option (a misspelling such as
+    LUMO_TAIL_BELOW for LUMO_TAIL) is reported, each with one line on stderr."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, LUMO_TAIL="abc", LUMO_MERGE="99", LUMO_TAIL_BELOW="5")
+    code = ("import lumo_amd as L; d = L.Device(0); "
+            "print(d.option('tail_below'), d.option('merge_passes')); d.close()")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == [str(1 << 16), "8"]
+    assert "LUMO_TAIL=abc is not a number; ignored" in r.stderr
+    assert "LUMO_MERGE=99 outside [0, 8]; using 8" in r.stderr
+    assert "LUMO_TAIL_BELOW names no option; ignored" in r.stderr
