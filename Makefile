@@ -18,7 +18,7 @@ HOST_OBJ := $(patsubst lumo_amd/csrc/host/%.cpp,build/host/%.o,$(HOST_SRC))
 # kernels.hip: host orchestration, C ABI and the non-traversal kernels.  The traversal kernels
 # are instantiated once per kd stack class (launch.h STACK_CLASSES) in their own translation
 # units, so they compile in parallel: inst_pt.hip / inst_bd.hip built with -DLUMO_STK=<class>.
-STK_CLASSES := 4 8 16 24 32 48 64
+STK_CLASSES := 0 4 8 16 24 32 48 64
 DEV_OBJ  := $(BUILD)/device/kernels.o $(foreach k,$(STK_CLASSES),$(BUILD)/device/inst_pt_$(k).o $(BUILD)/device/inst_bd_$(k).o)
 DEV_H    := $(wildcard lumo_amd/csrc/device/*.h)
 COMMON_H := $(wildcard lumo_amd/csrc/common/*.h) include/lumo_amd.h include/lumo_host.h

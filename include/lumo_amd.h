@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define LUMO_ABI_VERSION 9
+#define LUMO_ABI_VERSION 10
 
 typedef int32_t lumo_status;
 enum {
@@ -424,6 +424,11 @@ enum {
     LUMO_OPT_RAY_SORT,         /* three-kernel bounces: the closest-hit rays of a bounce radix-sorted
                                   before their walks: 0 off, 1 direction octant major, 2 origin cell
                                   major, -1 auto (1 for kd stack class >= 32) (LUMO_RAY_SORT, -1; ABI 9)*/
+    LUMO_OPT_ACCEL,            /* upload: acceleration structure the walks use.  0 lumo's own (the
+                                  objects / lights BVHs, bvh.rs, and per-mesh kd-trees, kdtree.rs;
+                                  bit-exact with the reference), 1 wide (a 4-wide SAH BVH over all
+                                  primitives, nearest child first; same hit semantics except ties and
+                                  BDPT's visible()) (LUMO_ACCEL, 0; ABI 10)            */
     LUMO_OPT_COUNT
 };
 lumo_status lumo_set_option(void* ctx, int32_t option, int64_t value);
@@ -469,6 +474,11 @@ typedef struct {
     int32_t top_kd_nodes; /* kd nodes of the largest kd tree (its top treelets) in the TOP set */
     int32_t top_shm;      /* LDS per TOP block: the TOP set + the kd stack columns, within
                              LUMO_OPT_TOP_KB (ABI 9)                                          */
+    /* ABI 10: the acceleration structure the uploaded scene is walked with (LUMO_OPT_ACCEL: 0 lumo,
+     * 1 wide; 0 also when wide was asked for and the build refused the scene, e.g. a tree needing
+     * more than 64 walk stack entries) and, for wide, its nodes, leaf triangle records, deepest
+     * walk stack, node levels and the nodes of its TOP set (a breadth-first prefix) */
+    int32_t accel, wide_nodes, wide_tris, wide_stack, wide_depth, top_wide_nodes;
 } lumo_scene_info_t;
 lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info);
 /* Diagnostics: one coalesced 8-B-per-lane read stream and one write stream over n doubles

@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 9  # include/lumo_amd.h LUMO_ABI_VERSION
+ABI_VERSION = 10  # include/lumo_amd.h LUMO_ABI_VERSION
 LIB_PATH = os.environ.get("LUMO_AMD_LIB") or os.path.join(_HERE, "liblumo_amd.so")
 
 c_double_p = C.POINTER(C.c_double)
@@ -145,7 +145,9 @@ class HitSoA(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("stack_class", C.c_int32), ("lds_bytes", C.c_int32), ("full_kernels", C.c_int32),
                 ("n_shadow", C.c_int32), ("top_bytes", C.c_int32), ("top_object_nodes", C.c_int32),
-                ("top_light_nodes", C.c_int32), ("top_kd_nodes", C.c_int32), ("top_shm", C.c_int32)]
+                ("top_light_nodes", C.c_int32), ("top_kd_nodes", C.c_int32), ("top_shm", C.c_int32),
+                ("accel", C.c_int32), ("wide_nodes", C.c_int32), ("wide_tris", C.c_int32), ("wide_stack", C.c_int32),
+                ("wide_depth", C.c_int32), ("top_wide_nodes", C.c_int32)]
 
 
 STAGE_COUNT = 12  # LUMO_STAGE_COUNT
@@ -172,7 +174,7 @@ SCHED_SEQUENTIAL, SCHED_FUSED_PIPELINE, SCHED_SPLIT_PIPELINE = range(3)
 OPTIONS = ["timing", "lds_staging", "top_staging", "fused", "tail_below", "pipeline", "heads", "merge_passes",
            "dyn_fetch", "bounce_threads", "split_pipe", "split_groups", "bdpt_tail", "bounce_ahead", "lds_grid",
            "top_grid", "top_kb", "kd_lds", "stack_class", "full_kernels", "poison", "tail_priority", "top_kd",
-           "tail_bounces", "film_first", "bdpt_top", "bdpt_groups", "ray_sort"]
+           "tail_bounces", "film_first", "bdpt_top", "bdpt_groups", "ray_sort", "accel"]
 OPT = {name: i for i, name in enumerate(OPTIONS)}
 
 

@@ -348,7 +348,10 @@ __device__ __forceinline__ BVtx vtx_of_hit(const DHit& h, DColor gathered, doubl
 template <int STK, int FX>
 __device__ int get_light_at(const DScene& sc, const BVtx& v, Counters& C) {
     const Ray ri = ray_new(ray_origin(vtx_hit(v), true), -v.ng);
-    return bvh_traverse<true, STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, rayx(ri), 0.0, DINF, C);
+    if constexpr (STK == 0)  // wide accel: the lights' closest hit_t (dscene.h wide_walk)
+        return wide_walk<false, FX, false>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, rayx(ri), 0.0, DINF, C).obj;
+    else
+        return bvh_traverse<true, STK, FX>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, rayx(ri), 0.0, DINF, C);
 }
 
 // path_gen.rs:52-157.  Returns the number of vertices stored (root included), or -1 when the
@@ -551,11 +554,21 @@ __device__ bool bdpt_visible(const DScene& sc, const BVtx& a, const BVtx& b, Cou
     if (dot(ri.d, a.ng) < EPSILON) return false;
     const RayX rx = rayx(ri);
     double t = DINF;
+    if constexpr (STK == 0) {
+        // wide accel: Scene::hit_t as the closest hit_t (lumo's any-hit walk returns the first object
+        // its BVH order finds, which has no counterpart in another structure).  Hits
+        // beyond dist + 2 EPSILON fail the test either way, so the walks are capped there.
+        const double dist = sqrt(rmax(distance_squared(xo, xi), 0.0));
+        t = wide_walk<false, FX, TOP>(sc, sc.w_oroot, sc.tobjs, sc.w_oblas, rx, 0.0, dist + 2.0 * EPSILON, C).t;
+        t = rmin(t, wide_walk<false, FX, TOP>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, rx, 0.0, t, C).t);
+        return fabs(dist - t) < EPSILON;
+    } else {
     t = rmin(t, bvh_hit_t<STK, FX, TOP>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, rx, 0.0, t, C, sc.onodes_lds,
                                         sc.n_onodes_lds));
     t = rmin(t, bvh_hit_t<STK, FX, TOP>(sc, sc.lnodes, sc.n_lnodes, sc.litems, sc.tlights, rx, 0.0, t, C, sc.lnodes_lds,
                                         sc.n_lnodes_lds));
     return fabs(sqrt(rmax(distance_squared(xo, xi), 0.0)) - t) < EPSILON;
+    }
 }
 
 // bd_path_trace.rs:77-145 (t = 1): returns true with the splat.  `rs` is the lens sample the

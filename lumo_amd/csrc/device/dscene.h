@@ -12,6 +12,7 @@
 #include "../common/lmath.h"
 #include "../common/rng.h"
 #include "../common/vec.h"
+#include "../common/wbvh.h"
 
 #ifndef LUMO_WHILE_WHILE  // traversal loops as while-while (bvh_traverse, kd_traverse)
 #define LUMO_WHILE_WHILE 1
@@ -130,6 +131,18 @@ struct DScene {
     uint32_t off_top_kd;
     int32_t top_kd_lo, top_kd_n;
     const DKd* kd_lds;
+    // wide accel (accel == 1, wbvh.h): 4-wide nodes, leaf-ordered triangle records
+    // (A, B, C, (tri, obj)), the root refs of the world objects / lights trees, and per object /
+    // light the BLAS root of an instance.  The walks then run with stack class 0 (by_stack_class).
+    int32_t accel, w_oroot, w_lroot, wn_lds;  // wn_lds: nodes below it are read from wnodes_lds (TOP view)
+    const wbvh::Node* wnodes;
+    const double* wtv;
+    const int32_t* w_oblas;
+    const int32_t* w_lblas;
+    const wbvh::Node* wnodes_lds;
+    uint32_t off_wnodes, off_wtv, off_woblas, off_wlblas;  // in `hot` (whole-scene LDS staging)
+    uint32_t off_top_wnodes;
+    int32_t top_wnodes;  // nodes in the TOP set (a breadth-first prefix of wnodes)
 };
 
 // TOP view: copy the packed top levels into LDS; the rest of the scene stays in HBM / L2.
@@ -146,6 +159,8 @@ __device__ __forceinline__ DScene stage_top_lds(const DScene& sc, char* lds) {
     v.oitems = reinterpret_cast<const int32_t*>(lds + sc.off_top_oitems);
     v.tobjs = reinterpret_cast<const DObj*>(lds + sc.off_top_tobjs);
     v.kd_lds = reinterpret_cast<const DKd*>(lds + sc.off_top_kd);
+    v.wnodes_lds = reinterpret_cast<const wbvh::Node*>(lds + sc.off_top_wnodes);
+    v.wn_lds = sc.top_wnodes;
     v.kst_n = sc.kst_cfg;
     if (sc.kst_cfg > 0) {  // this thread's column of the LDS kd stack, after the TOP set
         char* base = lds + ((sc.top_bytes + 15u) & ~15u);
@@ -176,6 +191,12 @@ __device__ __forceinline__ DScene stage_scene_lds(const DScene& sc, char* lds) {
     v.kdp = reinterpret_cast<const DKd*>(lds + sc.off_kdp);
     v.tobjs = reinterpret_cast<const DObj*>(lds + sc.off_tobjs);
     v.tlights = reinterpret_cast<const DObj*>(lds + sc.off_tlights);
+    if (sc.accel) {
+        v.wnodes = reinterpret_cast<const wbvh::Node*>(lds + sc.off_wnodes);
+        v.wtv = reinterpret_cast<const double*>(lds + sc.off_wtv);
+        v.w_oblas = reinterpret_cast<const int32_t*>(lds + sc.off_woblas);
+        v.w_lblas = reinterpret_cast<const int32_t*>(lds + sc.off_wlblas);
+    }
     return v;
 }
 
@@ -489,11 +510,10 @@ __device__ __forceinline__ void slab(const double* bmin, const double* bmax, V3 
     te = min_element(vmax(ro_max, ro_min)) * (1.0 + 2.0 * gamma_n(3));
 }
 
-// triangle.rs:63-187, GEO = false: returns t or INF
-__device__ __forceinline__ double tri_hit_t(const DScene& sc, int ti, const RayX& r, double t_min, double t_max,
-                                            Counters& C) {
+// triangle.rs:63-187, GEO = false: returns t or INF.  tv: the triangle's vertex record (A, B, C).
+__device__ __forceinline__ double tri_hit_t_at(const double* tv, const RayX& r, double t_min, double t_max,
+                                               Counters& C) {
     C.tri++;
-    const double* tv = sc.tv + TV_STRIDE * ti;
     const V3 A = ld3(tv), B = ld3(tv + 3), Cv = ld3(tv + 6);
     const int kz = r.kz;
     const V3 wi = r.wi;
@@ -511,6 +531,10 @@ __device__ __forceinline__ double tri_hit_t(const DScene& sc, int ti, const RayX
     const bool b2 = det > 0.0 && (t_scaled < t_min * det || t_scaled > t_max * det);
     if (b1 || b2) return DINF;
     return t_scaled / det;
+}
+__device__ __forceinline__ double tri_hit_t(const DScene& sc, int ti, const RayX& r, double t_min, double t_max,
+                                            Counters& C) {
+    return tri_hit_t_at(sc.tv + TV_STRIDE * ti, r, t_min, t_max, C);
 }
 
 // triangle.rs:63-187, GEO = true: returns false on miss / self-hit reject.  FULL also builds the
@@ -991,8 +1015,227 @@ struct HitRef {
     double t;
     int kind, obj, tri;
 };
+
+// ---------------------------------------------------------------- wide accel walks (wbvh.h)
+// Stack class 0 selects these walks.  The sampled light's own Object::hit (scene.rs:171) still walks
+// lumo's kd tree of that one light, with a kd stack of WL_STK entries (the upload keeps the wide
+// mode only when every light's kd tree fits it).
+constexpr int WL_STK = wbvh::LIGHT_KD_STACK;
+template <int STK>
+constexpr int kd_stk() {
+    return STK == 0 ? WL_STK : STK;
+}
+
+struct WHit {
+    double t;
+    int32_t tri, obj;  // global triangle (or PRIM_SPHERE) and object / light index; obj -1: none
+};
+
+template <bool TOP>
+__device__ __forceinline__ const wbvh::Node& wnode_at(const DScene& sc, int32_t i) {
+    return (TOP && i < sc.wn_lds) ? sc.wnodes_lds[i] : sc.wnodes[i];
+}
+
+// aabb.rs:33-44 on child i's box (f32 bounds, rounded outward at the build, widened to f64)
+__device__ __forceinline__ void wslab(const wbvh::Node& nd, int i, const RayX& r, double& ts, double& te) {
+    const V3 lo{(double)nd.lo[0][i], (double)nd.lo[1][i], (double)nd.lo[2][i]};
+    const V3 hi{(double)nd.hi[0][i], (double)nd.hi[1][i], (double)nd.hi[2][i]};
+    const V3 ro_min = (lo - r.o) * r.inv;
+    const V3 ro_max = (hi - r.o) * r.inv;
+    ts = max_element(vmin(ro_min, ro_max));
+    te = min_element(vmax(ro_max, ro_min)) * (1.0 + 2.0 * gamma_n(3));
+}
+
+// compare-exchange of the child sort: hits before misses, hits by entry t (a swap only when
+// strictly out of order, so equal entries keep their order)
+__device__ __forceinline__ void wcx(double& ka, int32_t& ra, bool& ha, double& kb, int32_t& rb, bool& hb) {
+    const bool sw = (!ha && hb) || (ha && hb && ka > kb);
+    if (sw) {
+        const double k = ka;
+        ka = kb;
+        kb = k;
+        const int32_t x = ra;
+        ra = rb;
+        rb = x;
+        const bool f = ha;
+        ha = hb;
+        hb = f;
+    }
+}
+
+// Walk of one tree from `root`.  Closest (ANY = false): the smallest hit_t of its primitives (ties:
+// the first found) below t_max, nearest child first, entries beyond the closest hit so far culled
+// when popped.  ANY: the first primitive with hit_t < t_max.  Returns t (t_max when nothing is hit),
+// the triangle (PRIM_SPHERE for a sphere) and the object (`objs` index).  An instance leaf pushes a
+// marker and walks its BLAS with the ray in the instance's space (Ray::transform, ray.rs:24-31: the
+// same t parametrises both), the marker's pop restores the world ray.
+// Counters: aabb = child boxes tested, kd = nodes visited, tri = triangles tested.
+template <bool ANY, int FX, bool TOP>
+__device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, const int32_t* blas, const RayX& rw,
+                          double t_min, double t_max, Counters& C) {
+    WHit h{t_max, -1, -1};
+    if (root == wbvh::NONE) return h;
+    int32_t st_ref[wbvh::STACK];
+    double st_t[wbvh::STACK];
+    int sp = 0;
+    RayX r = rw;
+    int inst = -1;
+    int32_t cur = root;
+    auto pop = [&]() -> bool {
+        for (;;) {
+            if (sp == 0) return false;
+            --sp;
+            const int32_t x = st_ref[sp];
+            if (FX && x == wbvh::MARK) {  // leave the instance
+                r = rw;
+                inst = -1;
+                continue;
+            }
+            if (!ANY && st_t[sp] > h.t) continue;  // its box is entered beyond the closest hit
+            cur = x;
+            return true;
+        }
+    };
+    for (;;) {
+        while (cur >= 0) {  // interior nodes until this lane holds a leaf
+            const wbvh::Node& nd = wnode_at<TOP>(sc, cur);
+            C.kd++;
+            const int n = nd.n;
+            double k0, k1, k2, k3;
+            bool h0, h1, h2, h3;
+            int32_t r0 = nd.ref[0], r1 = nd.ref[1], r2 = nd.ref[2], r3 = nd.ref[3];
+            {
+                double ts, te;
+                C.aabb++;
+                wslab(nd, 0, r, ts, te);
+                k0 = rmax(ts, t_min);
+                h0 = k0 <= rmin(te, h.t);
+                C.aabb++;
+                wslab(nd, 1, r, ts, te);
+                k1 = rmax(ts, t_min);
+                h1 = k1 <= rmin(te, h.t);
+                h2 = h3 = false;
+                k2 = k3 = 0.0;
+                if (n > 2) {
+                    C.aabb++;
+                    wslab(nd, 2, r, ts, te);
+                    k2 = rmax(ts, t_min);
+                    h2 = k2 <= rmin(te, h.t);
+                }
+                if (n > 3) {
+                    C.aabb++;
+                    wslab(nd, 3, r, ts, te);
+                    k3 = rmax(ts, t_min);
+                    h3 = k3 <= rmin(te, h.t);
+                }
+            }
+            wcx(k0, r0, h0, k1, r1, h1);
+            wcx(k2, r2, h2, k3, r3, h3);
+            wcx(k0, r0, h0, k2, r2, h2);
+            wcx(k1, r1, h1, k3, r3, h3);
+            wcx(k1, r1, h1, k2, r2, h2);
+            if (!h0) {
+                if (!pop()) return h;
+                continue;
+            }
+            if (h3) {
+                st_ref[sp] = r3;
+                st_t[sp] = k3;
+                sp++;
+            }
+            if (h2) {
+                st_ref[sp] = r2;
+                st_t[sp] = k2;
+                sp++;
+            }
+            if (h1) {
+                st_ref[sp] = r1;
+                st_t[sp] = k1;
+                sp++;
+            }
+            cur = r0;
+        }
+        // a leaf
+        const int cnt = wbvh::leaf_count(cur), first = wbvh::leaf_first(cur);
+        if (FX && cnt == 0) {  // object leaf: a sphere, or an instance's BLAS
+            const DObj& ob = objs[first];
+            if (ob.type() == LUMO_OBJ_SPHERE) {
+                const RayX rl = ob.xform() >= 0 ? ray_local(sc.xforms[ob.xform()], rw) : rw;
+                const double t = sphere_hit_t(ob, rl, t_min, h.t);
+                if (t < h.t) {
+                    h = WHit{t, PRIM_SPHERE, first};
+                    if (ANY) return h;
+                }
+            } else {
+                st_ref[sp] = wbvh::MARK;
+                st_t[sp] = -DINF;
+                sp++;
+                r = ray_local(sc.xforms[ob.xform()], rw);
+                inst = first;
+                cur = blas[first];
+                continue;
+            }
+        } else {
+            for (int k = 0; k < cnt; ++k) {
+                const double* tv = sc.wtv + wbvh::TV * (size_t)(first + k);
+                const double t = tri_hit_t_at(tv, r, t_min, h.t, C);
+                if (t < h.t) {
+                    const int32_t* ids = reinterpret_cast<const int32_t*>(tv + 9);
+                    h = WHit{t, ids[0], inst >= 0 ? inst : ids[1]};
+                    if (ANY) return h;
+                }
+            }
+        }
+        if (!pop()) return h;
+    }
+}
+
+// The winner's GEO test: lumo's Object::hit re-walks the winning object and accepts or rejects its
+// closest triangle with this test (kdtree.rs:164-168, triangle.rs:63-187; sphere.rs:27-78); the
+// wide walk already knows that triangle, so only the test runs (counted as lumo counts it).
+template <int FX>
+__device__ __forceinline__ bool wide_accept(const DScene& sc, const DObj& ob, int tri, const RayX& r, double t_min,
+                                            double t_max, Counters& C, DHit& out) {
+    if constexpr (FX) {
+        const RayX rl = ob.xform() >= 0 ? ray_local(sc.xforms[ob.xform()], r) : r;
+        if (tri == PRIM_SPHERE) return sphere_hit<false>(ob, rl, t_min, t_max, out);
+        C.tri++;
+        return tri_hit_geo<false>(sc, tri, rl, t_min, t_max, out);
+    } else {
+        C.tri++;
+        return tri_hit_geo<false>(sc, tri, r, t_min, t_max, out);
+    }
+}
+
+// Scene::hit (scene.rs:119-147) on the wide trees: the objects' closest hit, its GEO test, then the
+// lights' closest hit below it and its GEO test.
+template <int FX, bool TOP>
+__device__ HitRef wide_scene_hit(const DScene& sc, const RayX& r, Counters& C) {
+    HitRef h{DINF, 0, -1, -1};
+    double t_max = DINF;
+    DHit g;
+    const WHit o = wide_walk<false, FX, TOP>(sc, sc.w_oroot, sc.tobjs, sc.w_oblas, r, 0.0, DINF, C);
+    if (o.obj >= 0 && wide_accept<FX>(sc, sc.tobjs[o.obj], o.tri, r, 0.0, t_max, C, g)) {
+        h = HitRef{g.t, 1, o.obj, o.tri};
+        t_max = g.t;
+    }
+    const WHit l = wide_walk<false, FX, TOP>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, r, 0.0, t_max, C);
+    if (l.obj >= 0 && wide_accept<FX>(sc, sc.tlights[l.obj], l.tri, r, 0.0, t_max, C, g)) h = HitRef{g.t, 2, l.obj, l.tri};
+    return h;
+}
+
+// Scene::hit_light's occlusion part (scene.rs:171-189) on the wide trees: any object, then any
+// light, hit below t_max.
+template <int FX, bool TOP>
+__device__ __forceinline__ bool wide_occluded(const DScene& sc, const RayX& r, double t_max, Counters& C) {
+    if (wide_walk<true, FX, TOP>(sc, sc.w_oroot, sc.tobjs, sc.w_oblas, r, 0.0, t_max, C).t < t_max) return true;
+    return wide_walk<true, FX, TOP>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, r, 0.0, t_max, C).t < t_max;
+}
 template <int STK, int FX, bool TOP = false>
 __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
+    if constexpr (STK == 0) {
+        return wide_scene_hit<FX, TOP>(sc, r, C);
+    } else {
     HitRef h{DINF, 0, -1, -1};
     double t_max = DINF;
     DHit g;
@@ -1012,6 +1255,7 @@ __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
         if (tri != -1) h = HitRef{g.t, 2, li, tri};
     }
     return h;
+    }
 }
 
 // Rebuild the full hit record of a closest hit (the GEO test is deterministic).
@@ -1024,6 +1268,12 @@ __device__ __forceinline__ void hit_record(const DScene& sc, const HitRef& hr, c
 // Scene::hit_light (scene.rs:165-189): returns true and the light hit if visible.
 template <int STK, int FX, bool TOP = false>
 __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit& lh, Counters& C) {
+    if constexpr (STK == 0) {
+        const int tri = object_hit_tri<kd_stk<STK>(), FX, false>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
+        if (tri == -1 || wide_occluded<FX, TOP>(sc, r, lh.t - EPSILON, C)) return false;
+        object_record<FX>(sc, sc.lights[light], tri, r, lh);
+        return true;
+    } else {
     const int tri = object_hit_tri<STK, FX, TOP>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
     if (tri == -1) return false;
     const double t_max = lh.t - EPSILON;
@@ -1036,6 +1286,7 @@ __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit
     // visible: build the light hit record (same GEO test, now in full)
     object_record<FX>(sc, sc.lights[light], tri, r, lh);
     return true;
+    }
 }
 
 // Scene::hit_light without the record: the light triangle (or PRIM_SPHERE) when visible, else -1;
@@ -1043,6 +1294,11 @@ __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit
 template <int STK, int FX, bool TOP = false>
 __device__ int scene_hit_light_tri(const DScene& sc, const RayX& r, int light, Counters& C) {
     DHit lh;
+    if constexpr (STK == 0) {
+        const int tri = object_hit_tri<kd_stk<STK>(), FX, false>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
+        if (tri == -1 || wide_occluded<FX, TOP>(sc, r, lh.t - EPSILON, C)) return -1;
+        return tri;
+    } else {
     const int tri = object_hit_tri<STK, FX, TOP>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
     if (tri == -1) return -1;
     const double t_max = lh.t - EPSILON;
@@ -1053,6 +1309,7 @@ __device__ int scene_hit_light_tri(const DScene& sc, const RayX& r, int light, C
                                 sc.n_lnodes_lds) < t_max)
         return -1;
     return tri;
+    }
 }
 
 // ---------------------------------------------------------------- materials

@@ -33,6 +33,7 @@
 #include <hipcub/hipcub.hpp>
 
 #define LUMO_MAIN_TU
+#include "../host/wbvh.h"
 #include "launch.h"
 #include "pt.h"
 
@@ -874,6 +875,7 @@ struct Opts {
     int ray_sort = -1;                 // split bounces: closest-hit rays sorted (1 octant major, 2 origin major;
                                        // -1 auto: 1 for deep kd trees, stack class >= 32: C2 4-spp frame
                                        // 309 / 312 -> 302 ms; C3, class 24: 556 -> 563 ms, so off there)
+    int accel = 0;                     // upload: 0 lumo's BVHs + kd-trees, 1 the wide BVH (wbvh.h)
 };
 
 struct Ctx {
@@ -919,6 +921,7 @@ struct Ctx {
     uint32_t* bd_totals_h = nullptr;
     hipEvent_t bd_ev[4] = {};
     V3 sort_lo{0.0, 0.0, 0.0}, sort_scale{0.0, 0.0, 0.0};  // ray sorting: the scene's world box -> 512 cells per axis
+    int w_nodes = 0, w_tris = 0, w_stack = 0, w_depth = 0;     // the uploaded wide BVH (lumo_scene_info)
 };
 
 lumo_status dev_alloc(const Ctx& c, DevBuf& b, size_t bytes) {
@@ -1082,6 +1085,7 @@ void launch_eval_a(int fx, int grid, int grid_slots, hipStream_t sm, const DScen
 template <typename F>
 void by_stack_class(int cls, F&& f) {
     switch (cls) {
+        case 0: f(std::integral_constant<int, 0>{}); break;  // the wide accel's walks (dscene.h wide_walk)
         case 4: f(std::integral_constant<int, 4>{}); break;
         case 8: f(std::integral_constant<int, 8>{}); break;
         case 16: f(std::integral_constant<int, 16>{}); break;
@@ -2779,7 +2783,7 @@ const char* const kOptEnv[LUMO_OPT_COUNT] = {
     "LUMO_DYN", "LUMO_BOUNCE_THREADS", "LUMO_SPLIT_PIPE", "LUMO_SPLIT_GROUPS", "LUMO_BDPT_TAIL", "LUMO_BOUNCE_AHEAD",
     "LUMO_LDS_GRID", "LUMO_TOP_GRID", "LUMO_TOP_KB", "LUMO_KD_LDS", "LUMO_STACK_CLASS", "LUMO_FULL_KERNELS",
     "LUMO_POISON", "LUMO_TAIL_PRIORITY", "LUMO_TOP_KD", "LUMO_TAIL_BOUNCES", "LUMO_FILM_FIRST",
-    "LUMO_BDPT_TOP", "LUMO_BDPT_GROUPS", "LUMO_RAY_SORT"};
+    "LUMO_BDPT_TOP", "LUMO_BDPT_GROUPS", "LUMO_RAY_SORT", "LUMO_ACCEL"};
 
 // A LUMO_* variable that names no option (e.g. a misspelt LUMO_TAIL_BELOW for LUMO_TAIL) would
 // otherwise be ignored without a trace: warn once per process.  LUMO_AMD_LIB and
@@ -2882,6 +2886,7 @@ lumo_status set_opt(Ctx& c, int k, int64_t v) {
         case LUMO_OPT_BDPT_TOP: o.bdpt_top = iv; break;
         case LUMO_OPT_BDPT_GROUPS: o.bdpt_groups = iv; break;
         case LUMO_OPT_RAY_SORT: o.ray_sort = iv; break;
+        case LUMO_OPT_ACCEL: o.accel = iv; break;
         case LUMO_OPT_TAIL_PRIORITY:
             if (iv != o.tail_priority) {
                 const lumo_status e = make_tail_stream(c, iv);
@@ -2925,6 +2930,7 @@ int64_t get_opt(const Ctx& c, int k) {
         case LUMO_OPT_BDPT_TOP: return o.bdpt_top;
         case LUMO_OPT_BDPT_GROUPS: return o.bdpt_groups;
         case LUMO_OPT_RAY_SORT: return o.ray_sort;
+        case LUMO_OPT_ACCEL: return o.accel;
         default: return 0;
     }
 }
@@ -3327,6 +3333,38 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     chk(upload(*c, tlights.data(), tlights.size(), &s.tlights));
     chk(upload(*c, tv.data(), tv.size(), &s.tv));
     chk(upload(*c, kdp.data(), kdp.size(), &s.kdp));
+    // wide accel (LUMO_OPT_ACCEL = 1, wbvh.h): built from the scene description.  The sampled light's
+    // own hit keeps lumo's kd walk with a WL_STK-entry stack, so every light's kd tree must fit it;
+    // a scene the build refuses keeps lumo's structures (lumo_scene_info.accel = 0).
+    wbvh::Accel acc;
+    s.accel = 0;
+    s.w_oroot = s.w_lroot = wbvh::NONE;
+    s.wnodes = s.wnodes_lds = nullptr;
+    s.wtv = nullptr;
+    s.w_oblas = s.w_lblas = nullptr;
+    s.wn_lds = s.top_wnodes = 0;
+    s.off_top_wnodes = 0;
+    s.off_wnodes = s.off_wtv = s.off_woblas = s.off_wlblas = 0;
+    c->w_nodes = c->w_tris = c->w_stack = c->w_depth = 0;
+    if (c->o.accel && !st) {
+        acc = wbvh::build_accel(*d);  // refuses light kd trees deeper than WL_STK
+        if (acc.ok) {
+            s.accel = 1;
+            s.w_oroot = acc.obj_root;
+            s.w_lroot = acc.light_root;
+            chk(upload(*c, acc.nodes.data(), acc.nodes.size(), &s.wnodes));
+            chk(upload(*c, acc.tv.data(), acc.tv.size(), &s.wtv));
+            chk(upload(*c, acc.obj_blas.data(), acc.obj_blas.size(), &s.w_oblas));
+            chk(upload(*c, acc.light_blas.data(), acc.light_blas.size(), &s.w_lblas));
+            c->w_nodes = (int)acc.nodes.size();
+            c->w_tris = (int)(acc.tv.size() / wbvh::TV);
+            c->w_stack = acc.max_stack;
+            c->w_depth = acc.depth;
+        } else {
+            fprintf(stderr, "lumo_amd: the wide accel refused this scene (a light kd tree deeper than %d or a "
+                    "walk stack of %d); walking lumo's structures\n", WL_STK, acc.max_stack);
+        }
+    }
     if (st) {
         free_scene(*c);
         return st;
@@ -3356,6 +3394,12 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         s.off_xforms = put(d->transforms, sizeof(lumo_transform) * d->num_transforms);
         s.off_tobjs = put(tobjs.data(), sizeof(DObj) * tobjs.size());
         s.off_tlights = put(tlights.data(), sizeof(DObj) * tlights.size());
+        if (s.accel) {
+            s.off_wnodes = put(acc.nodes.data(), sizeof(wbvh::Node) * acc.nodes.size());
+            s.off_wtv = put(acc.tv.data(), sizeof(double) * acc.tv.size());
+            s.off_woblas = put(acc.obj_blas.data(), sizeof(int32_t) * acc.obj_blas.size());
+            s.off_wlblas = put(acc.light_blas.data(), sizeof(int32_t) * acc.light_blas.size());
+        }
         s.hot_bytes = 0;
         if (hot.size() <= 48 * 1024) {
             const char* dp = nullptr;
@@ -3378,7 +3422,38 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         const size_t cap = std::min((size_t)c->o.top_kb * 1024, c->lds_cu);
         const size_t budget = cap > 256 ? cap - 256 : 0;  // 256 B: the kernels' static LDS
         const size_t objs_b = ((sizeof(int32_t) * d->num_object_items + 15) & ~(size_t)15) + sizeof(DObj) * tobjs.size();
-        if (s.hot_bytes == 0 && budget >= 4096 && objs_b + 64 * sizeof(DBvh) <= budget) {
+        const size_t wobjs_b = ((sizeof(DObj) * tobjs.size() + 15) & ~(size_t)15);
+        if (s.accel && s.hot_bytes == 0 && budget >= 4096 && wobjs_b + 16 * sizeof(wbvh::Node) <= budget) {
+            // wide accel: the object records (object leaves) and a breadth-first prefix of the nodes
+            // (the top levels of every tree, wbvh_build.h); no kd stack or treelets (the light's own
+            // kd walk reads HBM)
+            std::vector<char> top;
+            auto put = [&](const void* p, size_t bytes) -> uint32_t {
+                const size_t off = (top.size() + 15) & ~(size_t)15;
+                top.resize(off + ((bytes + 15) & ~(size_t)15), 0);
+                if (bytes) std::memcpy(top.data() + off, p, bytes);
+                return (uint32_t)off;
+            };
+            s.off_top_oitems = 0;
+            s.off_top_tobjs = put(tobjs.data(), sizeof(DObj) * tobjs.size());
+            const size_t left = budget - top.size();
+            const size_t nw = std::min(acc.nodes.size(), left / sizeof(wbvh::Node));
+            s.off_top_wnodes = put(acc.nodes.data(), sizeof(wbvh::Node) * nw);
+            s.top_wnodes = (int32_t)nw;
+            s.top_onodes = s.top_lnodes = 0;
+            s.off_top_onodes = s.off_top_lnodes = 0;
+            s.kst_cfg = 0;
+            s.top_kd_lo = s.top_kd_n = 0;
+            s.off_top_kd = 0;
+            const char* dp = nullptr;
+            chk(upload(*c, top.data(), top.size(), &dp));
+            if (st) {
+                free_scene(*c);
+                return st;
+            }
+            s.top = dp;
+            s.top_bytes = (uint32_t)top.size();
+        } else if (!s.accel && s.hot_bytes == 0 && budget >= 4096 && objs_b + 64 * sizeof(DBvh) <= budget) {
             std::vector<char> top;
             auto put = [&](const void* p, size_t bytes) -> uint32_t {
                 const size_t off = (top.size() + 15) & ~(size_t)15;
@@ -3481,6 +3556,7 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
             break;
         }
     if (c->o.stack_class > 0 && fits(c->o.stack_class)) s.stack_class = c->o.stack_class;  // A/B override
+    if (s.accel) s.stack_class = 0;  // the wide walks (by_stack_class)
     // feature class: the lean kernels cover kd meshes / rectangles with Lambertian + Light only
     bool full = d->num_transforms > 0;
     for (int i = 0; i < d->num_materials; ++i)
@@ -3652,6 +3728,12 @@ lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info) {
     info->top_light_nodes = c->sc.top_lnodes;
     info->top_kd_nodes = top ? c->sc.top_kd_n : 0;
     info->top_shm = top ? (int32_t)c->sc.top_shm : 0;
+    info->accel = c->sc.accel;
+    info->wide_nodes = c->w_nodes;
+    info->wide_tris = c->w_tris;
+    info->wide_stack = c->w_stack;
+    info->wide_depth = c->w_depth;
+    info->top_wide_nodes = top ? c->sc.top_wnodes : 0;
     return LUMO_OK;
 }
 

@@ -8,7 +8,8 @@
 namespace lumo {
 namespace dev {
 
-// kd stack classes the kernels are instantiated for (Makefile STK_CLASSES must match).
+// kd stack classes the kernels are instantiated for (Makefile STK_CLASSES must match; it also
+// builds class 0, the wide accel's walks, dscene.h wide_walk).
 constexpr int STACK_CLASSES[] = {4, 8, 16, 24, 32, 48, 64};
 
 // Launch geometry of a traversal kernel: grid, dynamic LDS (staged scene), LDS staging on/off,
@@ -79,6 +80,7 @@ void launch_bdpt_vis(const TravLaunch& l, const DScene& sc, const Paths& S, cons
     extern template void launch_bdpt_vis<K>(const TravLaunch&, const DScene&, const Paths&, const Bdpt&,          \
                                             const Bdpt&, const BItems&, int, uint32_t*);
 #ifndef LUMO_STK
+LUMO_EXTERN_STK(0)
 LUMO_EXTERN_STK(4)
 LUMO_EXTERN_STK(8)
 LUMO_EXTERN_STK(16)

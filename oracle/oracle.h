@@ -52,6 +52,9 @@ int oracle_render_tiles(const lumo_scene_desc* scene, const lumo_camera_desc* ca
 void oracle_set_tone_map(int kind, double arg);
 /* Integrator for subsequent renders: LUMO_INTEGRATOR_PATH_TRACE or LUMO_INTEGRATOR_BDPT. */
 void oracle_set_integrator(int integrator);
+/* Acceleration structure of subsequent calls: 0 lumo's BVHs + kd-trees (default), 1 the wide BVH of
+ * lumo_amd's LUMO_OPT_ACCEL = 1 (same structure as the upload builds, walk restated here). */
+void oracle_set_accel(int accel);
 /* SamplerType of subsequent renders (LUMO_SAMPLER_*, samplers.rs:6-17; default MultiJittered). */
 void oracle_set_sampler(int sampler);
 /* The points SamplerType::new(batch, samples, seed) yields (x, y interleaved, at most cap). */

@@ -32,12 +32,16 @@
 #include <cmath>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <thread>
 #include <vector>
 
 #include "../../lumo_amd/csrc/common/lmath.h"
 #include "../../lumo_amd/csrc/common/rng.h"
 #include "../../lumo_amd/csrc/common/vec.h"
+// The wide accel's structure (LUMO_OPT_ACCEL = 1) is built by the same code the upload runs, so both
+// walk the same nodes; the walk over it is restated below (wide_walk) independently of dscene.h.
+#include "../../lumo_amd/csrc/common/wbvh_build.h"
 
 using namespace lumo;
 
@@ -166,6 +170,7 @@ Color spec_sample(const lumo_spectrum& s, const Lambda& L) {
 // ------------------------------------------------------------------ scene access
 struct Scene {
     const lumo_scene_desc* d;
+    const wbvh::Accel* w = nullptr;  // wide accel mode (oracle_set_accel(1)): the walks run on it
     const double* dense(int idx) const { return d->dense_spectra + 95 * idx; }
     V3 vert(int i) const { return V3{d->vertices[3 * i], d->vertices[3 * i + 1], d->vertices[3 * i + 2]}; }
     int num_shadow_rays() const {  // scene.rs:90-92
@@ -177,6 +182,54 @@ struct Scene {
         return lg > 1 ? lg : 1;
     }
 };
+// Accel mode of subsequent calls (oracle_set_accel): 0 lumo's structures, 1 the wide BVH, built by
+// wbvh_build.h and cached per scene content (a C3-size build takes seconds).
+int g_accel = 0;
+std::mutex g_wide_mu;
+struct WideCache {
+    bool valid = false;
+    uint64_t hash = 0;
+    wbvh::Accel acc;
+} g_wide;
+uint64_t mix_bytes(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, b + i, 8);
+        h = (h ^ w) * 0x100000001b3ull;
+        h ^= h >> 29;
+    }
+    for (; i < n; ++i) h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
+}
+uint64_t desc_hash(const lumo_scene_desc* d) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    const int32_t counts[6] = {d->num_vertices, d->num_triangles, d->num_objects, d->num_lights, d->num_transforms,
+                               d->num_kd_nodes};
+    h = mix_bytes(h, counts, sizeof(counts));
+    h = mix_bytes(h, d->vertices, sizeof(double) * 3 * (size_t)d->num_vertices);
+    h = mix_bytes(h, d->triangles, sizeof(lumo_triangle) * (size_t)d->num_triangles);
+    h = mix_bytes(h, d->objects, sizeof(lumo_object) * (size_t)d->num_objects);
+    h = mix_bytes(h, d->lights, sizeof(lumo_object) * (size_t)d->num_lights);
+    if (d->transforms) h = mix_bytes(h, d->transforms, sizeof(lumo_transform) * (size_t)d->num_transforms);
+    h = mix_bytes(h, d->kd_nodes, sizeof(lumo_kd_node) * (size_t)d->num_kd_nodes);
+    return h;
+}
+Scene make_scene(const lumo_scene_desc* d) {
+    Scene sc{d};
+    if (g_accel) {
+        const uint64_t h = desc_hash(d);
+        std::lock_guard<std::mutex> lk(g_wide_mu);
+        if (!g_wide.valid || g_wide.hash != h) {
+            g_wide.acc = wbvh::build(*d);
+            g_wide.hash = h;
+            g_wide.valid = true;
+        }
+        if (g_wide.acc.ok) sc.w = &g_wide.acc;  // a refused scene walks lumo's structures, as the upload does
+    }
+    return sc;
+}
 double luminance(const Scene& sc, const Color& c, const Lambda& L) {  // color.rs:91-94
     const Color pdf = wl_pdf(L);
     return cmean(dense_sample(sc.dense(1), L) * c / pdf) / Y_INTEGRAL;
@@ -676,8 +729,16 @@ double bvh_hit_t(const Scene& sc, const BvhView& b, const Ray& r, double t_min, 
 }
 
 // scene.rs:119-147. kind: 0 miss, 1 object, 2 light.
-bool scene_hit(const Scene& sc, const Ray& r, Hit* h, int* kind, int* which, Counters& C) {
+bool wide_scene_hit(const Scene& sc, const Ray& r, Hit* h, int* kind, int* which, int* prim, Counters& C);
+bool wide_occluded(const Scene& sc, const Ray& r, double t_max, Counters& C);
+bool scene_hit(const Scene& sc, const Ray& r, Hit* h, int* kind, int* which, Counters& C, int* prim = nullptr) {
     C.closest++;
+    int pr = -1;
+    if (sc.w) {
+        const bool f = wide_scene_hit(sc, r, h, kind, which, &pr, C);
+        if (prim) *prim = pr;
+        return f;
+    }
     double t_max = INF;
     bool found = false;
     *kind = 0;
@@ -705,10 +766,181 @@ bool scene_hit_light(const Scene& sc, const Ray& r, int light, Hit* out, Counter
     Hit lh;
     if (!object_hit(sc, sc.d->lights[light], r, 0.0, INF, &lh, C)) return false;
     const double t_max = lh.t - EPSILON;
+    if (sc.w) {
+        if (wide_occluded(sc, r, t_max, C)) return false;
+        *out = lh;
+        return true;
+    }
     if (bvh_hit_t(sc, objects_of(sc), r, 0.0, t_max, C) < t_max) return false;
     if (bvh_hit_t(sc, lights_of(sc), r, 0.0, t_max, C) < t_max) return false;
     *out = lh;
     return true;
+}
+
+// ------------------------------------------------------------------ wide accel
+// The walk of lumo_amd's wide mode over the shared structure (wbvh.h), restated: nearest child
+// first with entry culling on pop, ANY = first hit below t_max; an instance leaf walks its BLAS with
+// the ray in the instance's space (ray.rs:24-31, unnormalised, so t is shared).  Primitives are
+// tested with lumo's own tests: triangle_hit(GEO = false) (triangle.rs:63-187) and sphere_hit_t.
+// Counters: aabb = child boxes tested, kd = nodes visited, tri = triangles tested.
+constexpr int PRIM_SPHERE_O = -2;
+struct WRes {
+    double t;
+    int tri, obj;
+};
+struct WChild {
+    double k;
+    int32_t ref;
+    bool hit;
+};
+void wide_cx(WChild& a, WChild& b) {  // hits first, hits by entry t; swap only when strictly out of order
+    if ((!a.hit && b.hit) || (a.hit && b.hit && a.k > b.k)) std::swap(a, b);
+}
+WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std::vector<int32_t>& blas,
+               const Ray& rw, double t_min, double t_max, bool any, Counters& C) {
+    const wbvh::Accel& W = *sc.w;
+    WRes h{t_max, -1, -1};
+    if (root == wbvh::NONE) return h;
+    struct Entry {
+        int32_t ref;
+        double t;
+    } st[wbvh::STACK];
+    int sp = 0;
+    Ray r = rw;
+    V3 inv = 1.0 / r.dir;
+    int inst = -1;
+    int32_t cur = root;
+    auto pop = [&]() -> bool {
+        while (sp > 0) {
+            const Entry e = st[--sp];
+            if (e.ref == wbvh::MARK) {
+                r = rw;
+                inv = 1.0 / r.dir;
+                inst = -1;
+                continue;
+            }
+            if (!any && e.t > h.t) continue;
+            cur = e.ref;
+            return true;
+        }
+        return false;
+    };
+    for (;;) {
+        if (!wbvh::is_leaf(cur)) {
+            const wbvh::Node& nd = W.nodes[cur];
+            C.kd++;
+            WChild ch[4];
+            for (int i = 0; i < 4; ++i) ch[i] = WChild{0.0, nd.ref[i], false};
+            for (int i = 0; i < nd.n; ++i) {
+                const double lo[3] = {(double)nd.lo[0][i], (double)nd.lo[1][i], (double)nd.lo[2][i]};
+                const double hi[3] = {(double)nd.hi[0][i], (double)nd.hi[1][i], (double)nd.hi[2][i]};
+                double ts, te;
+                C.aabb++;
+                aabb_intersect(lo, hi, r.origin, inv, ts, te);
+                ch[i].k = rmax(ts, t_min);
+                ch[i].hit = ch[i].k <= rmin(te, h.t);
+            }
+            wide_cx(ch[0], ch[1]);
+            wide_cx(ch[2], ch[3]);
+            wide_cx(ch[0], ch[2]);
+            wide_cx(ch[1], ch[3]);
+            wide_cx(ch[1], ch[2]);
+            if (!ch[0].hit) {
+                if (!pop()) return h;
+                continue;
+            }
+            for (int i = 3; i >= 1; --i)
+                if (ch[i].hit) st[sp++] = Entry{ch[i].ref, ch[i].k};
+            cur = ch[0].ref;
+            continue;
+        }
+        const int cnt = wbvh::leaf_count(cur), first = wbvh::leaf_first(cur);
+        if (cnt == 0) {
+            const lumo_object& ob = objs[first];
+            if (ob.type == LUMO_OBJ_SPHERE) {
+                const Ray rl = ob.xform >= 0 ? ray_to_local(xform_of(sc.d->transforms[ob.xform]), rw, false) : rw;
+                const double t = sphere_hit_t(ob, rl, t_min, h.t);
+                if (t < h.t) {
+                    h = WRes{t, PRIM_SPHERE_O, first};
+                    if (any) return h;
+                }
+            } else {
+                st[sp++] = Entry{wbvh::MARK, -INF};
+                r = ray_to_local(xform_of(sc.d->transforms[ob.xform]), rw, false);
+                inv = 1.0 / r.dir;
+                inst = first;
+                cur = blas[first];
+                continue;
+            }
+        } else {
+            for (int k = 0; k < cnt; ++k) {
+                int32_t ids[2];
+                std::memcpy(ids, &W.tv[(size_t)wbvh::TV * (first + k) + 9], sizeof(ids));
+                Hit dummy;
+                const double t = triangle_hit(sc, ids[0], r, t_min, h.t, false, &dummy, C);
+                if (t < h.t) {
+                    h = WRes{t, ids[0], inst >= 0 ? inst : ids[1]};
+                    if (any) return h;
+                }
+            }
+        }
+        if (!pop()) return h;
+    }
+}
+// Object::hit of a known primitive of object ob: the GEO test lumo's re-walk of the winning object
+// ends with (kdtree.rs:164-168 / triangle.rs / sphere.rs:27-78), then Rectangle uv and the
+// instance's hit transform as object_hit.
+bool object_hit_prim(const Scene& sc, const lumo_object& ob, int prim, const Ray& r, double t_min, double t_max,
+                     Hit* out, Counters& C) {
+    const bool x = ob.xform >= 0;
+    const Xform X = x ? xform_of(sc.d->transforms[ob.xform]) : Xform{};
+    const Ray rl = x ? ray_to_local(X, r, false) : r;
+    if (prim == PRIM_SPHERE_O) {
+        if (!sphere_hit(ob, rl, t_min, t_max, out)) return false;
+    } else {
+        if (triangle_hit(sc, prim, rl, t_min, t_max, true, out, C) == INF) return false;
+        if (ob.type == LUMO_OBJ_RECTANGLE) {
+            const V3 b0{ob.b0[0], ob.b0[1], ob.b0[2]}, b1{ob.b1[0], ob.b1[1], ob.b1[2]};
+            out->uv = wrap_uv(V2{dot(b0, out->p), dot(b1, out->p)});
+        }
+    }
+    if (!x) return true;
+    const M3 N = nrm_of(sc.d->transforms[ob.xform]);
+    out->ns = normalize(m3_mul_vec(N, out->ns));
+    out->ng = normalize(m3_mul_vec(N, out->ng));
+    out->fp_error = propagate_fp_err(X, out->p, out->fp_error);
+    if (ob.material_override >= 0) out->material = ob.material_override;
+    out->p = xf_pt(X, out->p);
+    return true;
+}
+// Scene::hit on the wide trees (scene.rs:119-147): objects' closest, its GEO test, then the lights'
+bool wide_scene_hit(const Scene& sc, const Ray& r, Hit* h, int* kind, int* which, int* prim, Counters& C) {
+    double t_max = INF;
+    bool found = false;
+    *kind = 0;
+    Hit tmp;
+    const WRes o = wide_walk(sc, sc.w->obj_root, sc.d->objects, sc.w->obj_blas, r, 0.0, INF, false, C);
+    if (o.obj >= 0 && object_hit_prim(sc, sc.d->objects[o.obj], o.tri, r, 0.0, t_max, &tmp, C)) {
+        *h = tmp;
+        found = true;
+        *kind = 1;
+        *which = o.obj;
+        *prim = o.tri;
+        t_max = tmp.t;
+    }
+    const WRes l = wide_walk(sc, sc.w->light_root, sc.d->lights, sc.w->light_blas, r, 0.0, t_max, false, C);
+    if (l.obj >= 0 && object_hit_prim(sc, sc.d->lights[l.obj], l.tri, r, 0.0, t_max, &tmp, C)) {
+        *h = tmp;
+        found = true;
+        *kind = 2;
+        *which = l.obj;
+        *prim = l.tri;
+    }
+    return found;
+}
+bool wide_occluded(const Scene& sc, const Ray& r, double t_max, Counters& C) {  // scene.rs:171-189
+    if (wide_walk(sc, sc.w->obj_root, sc.d->objects, sc.w->obj_blas, r, 0.0, t_max, true, C).t < t_max) return true;
+    return wide_walk(sc, sc.w->light_root, sc.d->lights, sc.w->light_blas, r, 0.0, t_max, true, C).t < t_max;
 }
 
 // ------------------------------------------------------------------ materials
@@ -1541,6 +1773,7 @@ enum { TR_RADIANCE = 0, TR_IMPORTANCE = 1 };
 // BVH::get_light_at (bvh.rs:97-102): the closest light (by hit_t) along -ng from just outside h
 int get_light_at(const Scene& sc, const Hit& h, Counters& C) {
     const Ray ri = ray_new(ray_origin(h, true), -h.ng);
+    if (sc.w) return wide_walk(sc, sc.w->light_root, sc.d->lights, sc.w->light_blas, ri, 0.0, INF, false, C).obj;
     const BvhView b = lights_of(sc);
     return bvh_hit_idx(sc, b.nodes, b.n, b.items, b.objs, ri, 0.0, INF, true, C);
 }
@@ -1856,8 +2089,14 @@ bool bdpt_visible(const Scene& sc, const Hit& h1, const Hit& h2, Counters& C) { 
     const V3 xo = h1.p, xi = h2.p;
     const Ray ri = generate_ray(h1, xi - xo);
     if (dot(ri.dir, h1.ng) < EPSILON) return false;
-    // Scene::hit_t (scene.rs:150-162): any-hit-first over objects, then lights
     double t = INF;
+    if (sc.w) {  // wide accel: Scene::hit_t as the closest hit_t, capped at dist + 2 EPSILON
+        const double dist = std::sqrt(rmax(distance_squared(xo, xi), 0.0));
+        t = wide_walk(sc, sc.w->obj_root, sc.d->objects, sc.w->obj_blas, ri, 0.0, dist + 2.0 * EPSILON, false, C).t;
+        t = rmin(t, wide_walk(sc, sc.w->light_root, sc.d->lights, sc.w->light_blas, ri, 0.0, t, false, C).t);
+        return fabs(dist - t) < EPSILON;
+    }
+    // Scene::hit_t (scene.rs:150-162): any-hit-first over objects, then lights
     t = rmin(t, bvh_hit_t(sc, objects_of(sc), ri, 0.0, t, C));
     t = rmin(t, bvh_hit_t(sc, lights_of(sc), ri, 0.0, t, C));
     return fabs(std::sqrt(rmax(distance_squared(xo, xi), 0.0)) - t) < EPSILON;
@@ -2224,7 +2463,7 @@ extern "C" int oracle_render_tiles(const lumo_scene_desc* scene, const lumo_came
     if (!scene || !camera || (!tasks && n) || (!out && n)) return LUMO_ERR_INVALID;
     for (size_t i = 0; i < n; ++i)
         if (!valid_task(tasks[i]) || !out[i].rgb_w) return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     const Cam k = cam_of(camera);
     if (k.orthographic && g_integrator == LUMO_INTEGRATOR_BDPT) return LUMO_ERR_UNSUPPORTED;  // camera.rs:348-351
     if (threads < 1) threads = 1;
@@ -2265,7 +2504,7 @@ extern "C" int oracle_trace_paths(const lumo_scene_desc* scene, const lumo_camer
                                   const lumo_tile_task* task, double* radiance4, double* lambda4, double* raster2,
                                   uint64_t* depth, double* delta_per_pass) {
     if (!scene || !camera || !task || !valid_task(*task)) return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     const Cam k = cam_of(camera);
     if (k.orthographic && g_integrator == LUMO_INTEGRATOR_BDPT) return LUMO_ERR_UNSUPPORTED;
     Counters C;
@@ -2292,19 +2531,19 @@ extern "C" int oracle_trace_paths(const lumo_scene_desc* scene, const lumo_camer
 extern "C" int oracle_trace(const lumo_scene_desc* scene, const lumo_ray_soa* rays, size_t n, lumo_hit_soa* hits,
                             int any_hit, oracle_counters* counters) {
     if (!scene || !rays || !hits) return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     Counters C;
     for (size_t i = 0; i < n; ++i) {
         const Ray r{V3{rays->origin[3 * i], rays->origin[3 * i + 1], rays->origin[3 * i + 2]},
                     V3{rays->dir[3 * i], rays->dir[3 * i + 1], rays->dir[3 * i + 2]}};
         Hit h;
         if (!any_hit) {
-            int kind = 0, which = -1;
-            const bool f = scene_hit(sc, r, &h, &kind, &which, C);
+            int kind = 0, which = -1, prim = -1;
+            const bool f = scene_hit(sc, r, &h, &kind, &which, C, &prim);
             hits->t[i] = f ? h.t : INF;
             hits->kind[i] = f ? kind : 0;
             hits->object[i] = f ? which : -1;
-            hits->prim[i] = -1;
+            hits->prim[i] = f ? prim : -1;  // the wide walk's triangle (lumo's structures: -1, not tracked)
         } else {
             const int light = rays->light[i];
             const bool f = scene_hit_light(sc, r, light, &h, C);
@@ -2329,7 +2568,7 @@ extern "C" int oracle_trace(const lumo_scene_desc* scene, const lumo_ray_soa* ra
 extern "C" int oracle_trace_costs(const lumo_scene_desc* scene, const lumo_ray_soa* rays, size_t n, int any_hit,
                                   uint32_t* cost3) {
     if (!scene || !rays || !cost3) return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     for (size_t i = 0; i < n; ++i) {
         Counters C;
         const Ray r{V3{rays->origin[3 * i], rays->origin[3 * i + 1], rays->origin[3 * i + 2]},
@@ -2351,7 +2590,7 @@ extern "C" int oracle_trace_costs(const lumo_scene_desc* scene, const lumo_ray_s
 extern "C" int oracle_debug_trace(const lumo_scene_desc* scene, const lumo_camera_desc* camera,
                                   const lumo_tile_task* task, int pass, int pixel, double* out, int* n_out) {
     if (!scene || !camera || !task || !valid_task(*task)) return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     const Cam k = cam_of(camera);
     Counters C;
     std::vector<Sample> paths;
@@ -2382,7 +2621,7 @@ extern "C" int oracle_bsdf_sample(const lumo_scene_desc* scene, int material, co
                                   size_t n, uint64_t seed, double* wi3, int* ok) {
     if (!scene || !wo || !lambda4 || !wi3 || !ok || material < 0 || material >= scene->num_materials)
         return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     const Hit h = probe_hit(material);
     Xorshift rng = xs_new(seed);
     const V3 o{wo[0], wo[1], wo[2]};
@@ -2404,7 +2643,7 @@ extern "C" int oracle_bsdf_eval(const lumo_scene_desc* scene, int material, cons
                                 const double* wi3, size_t n, double* pdf, double* f4) {
     if (!scene || !wo || !lambda4 || !wi3 || !pdf || !f4 || material < 0 || material >= scene->num_materials)
         return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     const Hit h = probe_hit(material);
     Lambda L;
     for (int k = 0; k < NS; ++k) L.l[k] = lambda4[k];
@@ -2422,7 +2661,7 @@ extern "C" int oracle_bsdf_eval(const lumo_scene_desc* scene, int material, cons
 extern "C" int oracle_furnace(const lumo_scene_desc* scene, int material, const double* wo, size_t n, uint64_t seed,
                               double* out4) {
     if (!scene || !wo || !out4 || material < 0 || material >= scene->num_materials) return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     const Hit h = probe_hit(material);
     Xorshift rng = xs_new(seed);
     const V3 o{wo[0], wo[1], wo[2]};
@@ -2448,7 +2687,7 @@ extern "C" int oracle_furnace(const lumo_scene_desc* scene, int material, const 
 extern "C" int oracle_light_sample(const lumo_scene_desc* scene, int light, const double* xo, size_t n, uint64_t seed,
                                    double* wi3) {
     if (!scene || !xo || !wi3 || light < 0 || light >= scene->num_lights) return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     Xorshift rng = xs_new(seed);
     const V3 o{xo[0], xo[1], xo[2]};
     for (size_t i = 0; i < n; ++i) {
@@ -2463,7 +2702,7 @@ extern "C" int oracle_light_sample(const lumo_scene_desc* scene, int light, cons
 extern "C" int oracle_light_pdf(const lumo_scene_desc* scene, int light, const double* xo, const double* wi3, size_t n,
                                 double* pdf) {
     if (!scene || !xo || !wi3 || !pdf || light < 0 || light >= scene->num_lights) return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     Counters C;
     const lumo_object& L = scene->lights[light];
     for (size_t i = 0; i < n; ++i) {
@@ -2477,6 +2716,7 @@ extern "C" int oracle_light_pdf(const lumo_scene_desc* scene, int light, const d
 extern "C" void oracle_set_tone_map(int kind, double arg) { g_tone = ToneMap{kind, arg}; }
 
 extern "C" void oracle_set_integrator(int integrator) { g_integrator = integrator; }
+extern "C" void oracle_set_accel(int accel) { g_accel = accel; }
 extern "C" void oracle_set_sampler(int sampler) { g_sampler = sampler; }
 // Probe: the points a pixel sampler (SamplerType::new(batch, samples, seed) of the current
 // g_sampler) yields, x y interleaved; returns how many (at most cap).
@@ -2612,7 +2852,7 @@ done:
 extern "C" int oracle_mis_sums(const lumo_scene_desc* scene, const lumo_camera_desc* camera, size_t n, uint64_t seed,
                                double* sums, int32_t* lengths) {
     if (!scene || !camera || !sums) return LUMO_ERR_INVALID;
-    const Scene sc{scene};
+    const Scene sc = make_scene(scene);
     const Cam cam = cam_of(camera);
     Counters C;
     Xorshift rng = xs_new(seed);

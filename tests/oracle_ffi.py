@@ -39,6 +39,8 @@ def load(path=None):
                                      C.POINTER(_ffi.HitSoA), C.c_int, C.POINTER(Counters)]
         lib.oracle_set_integrator.restype = None
         lib.oracle_set_integrator.argtypes = [C.c_int]
+        lib.oracle_set_accel.restype = None
+        lib.oracle_set_accel.argtypes = [C.c_int]
         lib.oracle_set_sampler.restype = None
         lib.oracle_set_sampler.argtypes = [C.c_int]
         lib.oracle_sampler_points.restype = C.c_int64
@@ -67,11 +69,21 @@ def load(path=None):
 
 
 def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path=None, tone_map=(0, 0.0),
-                 integrator=0, splats_out=None, sampler=0):
+                 integrator=0, splats_out=None, sampler=0, accel=0):
     """Returns (list of rgb_w arrays, results array, counters).  With integrator = 1 (BDPT) the
     per-task light-tracing splats are appended to `splats_out` (a list) as (x, y, rgb) arrays.
-    sampler: lumo_amd.SamplerType (samplers.rs:6-17)."""
+    sampler: lumo_amd.SamplerType (samplers.rs:6-17).  accel: 0 lumo's structures, 1 the wide BVH
+    (LUMO_OPT_ACCEL)."""
     lib = load(path)
+    lib.oracle_set_accel(int(accel))
+    try:
+        return _render_tasks(lib, scene_desc, camera_desc, tasks, mode, threads, tone_map, integrator, splats_out,
+                             sampler)
+    finally:
+        lib.oracle_set_accel(0)
+
+
+def _render_tasks(lib, scene_desc, camera_desc, tasks, mode, threads, tone_map, integrator, splats_out, sampler):
     lib.oracle_set_tone_map(*tone_map)
     lib.oracle_set_integrator(integrator)
     lib.oracle_set_sampler(int(sampler))
@@ -113,10 +125,11 @@ def render_tasks(scene_desc, camera_desc, tasks, mode=WAVEFRONT, threads=1, path
     return bufs, res, cnt
 
 
-def trace_paths(scene_desc, camera_desc, task, path=None, integrator=0, sampler=0):
+def trace_paths(scene_desc, camera_desc, task, path=None, integrator=0, sampler=0, accel=0):
     lib = load(path)
     lib.oracle_set_integrator(integrator)
     lib.oracle_set_sampler(int(sampler))
+    lib.oracle_set_accel(int(accel))
     P = (task.px_max[0] - task.px_min[0]) * (task.px_max[1] - task.px_min[1])
     m = P * task.samples
     rad, lam, ras = np.zeros(4 * m), np.zeros(4 * m), np.zeros(2 * m)
@@ -127,12 +140,15 @@ def trace_paths(scene_desc, camera_desc, task, path=None, integrator=0, sampler=
                                 delta.ctypes.data_as(_ffi.c_double_p))
     lib.oracle_set_integrator(0)
     lib.oracle_set_sampler(0)
+    lib.oracle_set_accel(0)
     assert st == 0, st
     return dict(radiance=rad.reshape(-1, 4), lam=lam.reshape(-1, 4), raster=ras.reshape(-1, 2), depth=depth,
                 delta=delta)
 
 
-def trace(scene_desc, origins, dirs, lights=None):
+def trace(scene_desc, origins, dirs, lights=None, accel=0, with_prim=False):
+    """Scene::hit (lights None) or Scene::hit_light per ray: (t, kind, object, counters), with the
+    triangle (wide accel only; -1 otherwise) before the counters when with_prim."""
     lib = load()
     n = len(origins)
     o = np.ascontiguousarray(origins, dtype=np.float64)
@@ -145,9 +161,15 @@ def trace(scene_desc, origins, dirs, lights=None):
     hits = _ffi.HitSoA(t.ctypes.data_as(_ffi.c_double_p), kind.ctypes.data_as(_ffi.c_int32_p),
                        obj.ctypes.data_as(_ffi.c_int32_p), prim.ctypes.data_as(_ffi.c_int32_p))
     cnt = Counters()
-    st = lib.oracle_trace(C.byref(scene_desc), C.byref(rays), n, C.byref(hits), int(lights is not None),
-                          C.byref(cnt))
+    lib.oracle_set_accel(int(accel))
+    try:
+        st = lib.oracle_trace(C.byref(scene_desc), C.byref(rays), n, C.byref(hits), int(lights is not None),
+                              C.byref(cnt))
+    finally:
+        lib.oracle_set_accel(0)
     assert st == 0
+    if with_prim:
+        return t, kind, obj, prim, cnt
     return t, kind, obj, cnt
 
 

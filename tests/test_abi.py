@@ -32,7 +32,7 @@ def test_ffi_table_covers_header():
 
 def test_abi_version_and_status_strings():
     lib = L.lib()
-    assert lib.lumo_abi_version() == 9 == _ffi.ABI_VERSION
+    assert lib.lumo_abi_version() == 10 == _ffi.ABI_VERSION
     assert lib.lumo_status_str(0) == b"ok"
     assert lib.lumo_status_str(6) == b"unsupported"
 
