@@ -47,6 +47,12 @@ B_AABB, B_KD, B_TRI = 48, 16, 84           # slab test bounds; kd split node; 3 
 B_CLOSEST_IO = 48 + 20  # ray in + hit out
 B_RECORD, B_FOLD = 104, 104  # shadow record in; per path: gathered + pdf_light + radiance read/write
 B_CONN_IO = 104  # BDPT connection query: the two vertices' position / error / normal in, result out
+# wide accel (LUMO_OPT_ACCEL = 1): its counters are child boxes tested (aabb), nodes
+# visited (kd) and triangles tested; a node visit reads its 128-B node (four f32 boxes, refs), a
+# triangle test its 80-B leaf record (three f64 vertices + ids)
+B_WNODE, B_WTRI = 128, 80
+# acceleration structure per workload (--accel auto): the wide BVH where it measured faster
+ACCEL_AUTO = {"c1": 0, "c2": 1, "c3": 1, "c4": 1}
 LUMO_DEFAULT_THREADS = 4  # renderer.rs:21
 CPU_REPEATS = 3  # CPU baseline: median of this many runs per thread count
 # f64 VALU peak in lane-operations per second (an FMA counts once): 256 CUs x 4 SIMDs x 16 f64
@@ -101,6 +107,9 @@ def main():
                     help="multi-GPU tile distribution: tile %% N (static) or chunks claimed from a shared "
                          "queue in the process group's store (dynamic, lumo_amd.dist.TileQueue)")
     ap.add_argument("--chunk", type=int, default=None, help="tiles per claim of the dynamic schedule")
+    ap.add_argument("--accel", default="auto", choices=["auto", "lumo", "wide"],
+                    help="walks over lumo's BVHs + kd-trees (bit-exact with the reference) or the wide BVH "
+                         "(LUMO_OPT_ACCEL, DESIGN.md 4b); auto: per workload, ACCEL_AUTO")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -170,8 +179,10 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
         warm_arr = (_ffi.TileTask * len(wt))(*wt)
 
     splat_film = np.zeros((H, W, 3)) if bdpt else None
-    dev = L.Device(local)
+    accel = ACCEL_AUTO[config] if args.accel == "auto" else int(args.accel == "wide")
+    dev = L.Device(local, accel=accel)
     dev.upload(scene, cam)
+    accel = dev.scene_info().accel  # 0 when the build refused the scene
     lib = _ffi.load()
 
     def step(arr):
@@ -236,7 +247,7 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
     if rank == 0:
         # a rank's share launches fewer paths per pass: its own PMC entry when one was profiled
         wkey = f"{config}_share" if share and pmc_traffic(f"{config}_share", "source") else config
-        roof = roofline(st, n_shadow_rays(scene), bdpt=bdpt, workload=wkey, elapsed=elapsed, busy=busy)
+        roof = roofline(st, n_shadow_rays(scene), bdpt=bdpt, workload=wkey, elapsed=elapsed, busy=busy, accel=accel)
         cpu = cpu_baseline(scene, cam, tasks, tiles, args, W, H, spp, wl, repeats=wl.get("cpu_repeats", CPU_REPEATS)) \
             if (args.cpu_baseline and ws == 1) else None
         out = {
@@ -264,6 +275,8 @@ def run(config, args, ws, rank, local, pg, steps, warmup, res=None, spp=None, wa
                 "seed": SEED,
                 "rng_mode": "wavefront (per-path Xorshiftr128+ streams; DESIGN.md §RNG)",
                 "parallelism": (f"tiles from a shared queue, {ws} ranks" if dynamic else f"tiles sharded tile%{ws}"),
+                "accel": ("wide (4-wide SAH BVH, LUMO_OPT_ACCEL=1; DESIGN.md 4b)" if accel else
+                          "lumo (objects/lights BVH + per-mesh kd-trees, bit-exact with the reference)"),
             },
             "msamples_per_s": round(cams / elapsed / 1e6, 3),
             "lumo_total_rays_per_s_M": round(rays / elapsed / 1e6, 3),
@@ -332,7 +345,7 @@ def build_config(name, res=None, spp_override=None):
     return scene, cam, (W, H), spp, wl
 
 
-def roofline(st, n_shadow, bdpt=False, workload="c1", elapsed=None, busy=None):
+def roofline(st, n_shadow, bdpt=False, workload="c1", elapsed=None, busy=None, accel=0):
     """Dominant-kernel roofline from live HIP-event launch intervals and traversal counters.
 
     Unit = one ray query; bytes = IO + 48 per AABB test + 16 per kd split visit + 84 per triangle
@@ -358,9 +371,13 @@ def roofline(st, n_shadow, bdpt=False, workload="c1", elapsed=None, busy=None):
     # shadow records resolved without traversal (p_sct == 0) read only their pdf
     traversed = st.shadow_queries - st.shadow_resolved
     sq = max(traversed, 1)
-    closest_bytes = (st.closest_queries * B_CLOSEST_IO + st.aabb_tests[0] * B_AABB + st.kd_nodes[0] * B_KD +
-                     st.tri_tests[0] * B_TRI)
-    trav1 = st.aabb_tests[1] * B_AABB + st.kd_nodes[1] * B_KD + st.tri_tests[1] * B_TRI
+    if accel:  # wide walks: 128 B per node visited, 80 B per triangle record (boxes are in the node)
+        closest_bytes = st.closest_queries * B_CLOSEST_IO + st.kd_nodes[0] * B_WNODE + st.tri_tests[0] * B_WTRI
+        trav1 = st.kd_nodes[1] * B_WNODE + st.tri_tests[1] * B_WTRI
+    else:
+        closest_bytes = (st.closest_queries * B_CLOSEST_IO + st.aabb_tests[0] * B_AABB + st.kd_nodes[0] * B_KD +
+                         st.tri_tests[0] * B_TRI)
+        trav1 = st.aabb_tests[1] * B_AABB + st.kd_nodes[1] * B_KD + st.tri_tests[1] * B_TRI
 
     def unit(name, stages, nbytes):
         return (sum(ms[i] for i in stages), sum(launches[i] for i in stages), nbytes, busy.get(name))
@@ -385,10 +402,13 @@ def roofline(st, n_shadow, bdpt=False, workload="c1", elapsed=None, busy=None):
     out = {"bound": "hbm", "kernel": kname, "longest_stage": dom_stage, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "traffic": pmc.get("hbm_bytes_per_launch"), "traffic_raw": pmc.get("hbm_bytes_per_launch_raw"),
            "traffic_source": f"profiles/pmc_traffic.json[{workload}]" if pmc else None, "stages": per_stage}
+    ka, kk = ("boxes", "nodes") if accel else ("aabb", "kd")
     out["per_query"] = {
-        "closest": {"aabb": st.aabb_tests[0] / cq, "kd": st.kd_nodes[0] / cq, "tri": st.tri_tests[0] / cq},
-        ("connection" if bdpt else "shadow"): {"aabb": st.aabb_tests[1] / sq, "kd": st.kd_nodes[1] / sq,
+        "closest": {ka: st.aabb_tests[0] / cq, kk: st.kd_nodes[0] / cq, "tri": st.tri_tests[0] / cq},
+        ("connection" if bdpt else "shadow"): {ka: st.aabb_tests[1] / sq, kk: st.kd_nodes[1] / sq,
                                                "tri": st.tri_tests[1] / sq}}
+    out["byte_model"] = ("query IO + 128 B per wide node visited + 80 B per triangle record" if accel else
+                         "query IO + 48 B per AABB test + 16 B per kd node + 84 B per triangle test")
     if kms > 0 and kl > 0:
         t_busy = (kbusy if kbusy else kms) * 1e-3
         achieved = nbytes / t_busy / 1e9

@@ -24,9 +24,15 @@ namespace wbvh {
 namespace {  // internal linkage: each including file (host/wbvh.cpp, the oracle) has its own copy
 
 
-constexpr int LEAF_MAX = 8;  // triangles per leaf
+#ifndef WBVH_LEAF_MAX  // build parameters (macros only for the offline A/B of tools/wbvh_params.py)
+#define WBVH_LEAF_MAX 8
+#endif
+#ifndef WBVH_C_TRAV
+#define WBVH_C_TRAV 1.0
+#endif
+constexpr int LEAF_MAX = WBVH_LEAF_MAX;  // triangles per leaf
 constexpr int BINS = 32;
-constexpr double C_TRAV = 1.0, C_TRI = 1.0;  // SAH costs of a node visit and a triangle test
+constexpr double C_TRAV = WBVH_C_TRAV, C_TRI = 1.0;  // SAH costs of a node visit and a triangle test
 
 struct Prim {
     double lo[3], hi[3];

@@ -540,9 +540,10 @@ __device__ __forceinline__ double tri_hit_t(const DScene& sc, int ti, const RayX
 // triangle.rs:63-187, GEO = true: returns false on miss / self-hit reject.  FULL also builds the
 // hit record (point, normals, uv, error bounds); !FULL stops after the t <= t_min + delta_t
 // check (callers that only need acceptance and t; the record is rebuilt identically later).
+// tv: the triangle's vertex record; ti: its index in the scene's triangles (FULL only).
 template <bool FULL>
-__device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_min, double t_max, DHit& out) {
-    const double* tv = sc.tv + TV_STRIDE * ti;
+__device__ bool tri_hit_geo_at(const DScene& sc, const double* tv, int ti, const RayX& r, double t_min, double t_max,
+                               DHit& out) {
     const V3 A = ld3(tv), B = ld3(tv + 3), Cv = ld3(tv + 6);
     const int kz = r.kz;
     const V3 wi = r.wi;
@@ -598,6 +599,11 @@ __device__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_mi
     out.ng = ng;
     out.uv = wrap_uv(uv);
     return true;
+}
+template <bool FULL>
+__device__ __forceinline__ bool tri_hit_geo(const DScene& sc, int ti, const RayX& r, double t_min, double t_max,
+                                            DHit& out) {
+    return tri_hit_geo_at<FULL>(sc, sc.tv + TV_STRIDE * ti, ti, r, t_min, t_max, out);
 }
 
 // kdtree.rs:101-169.  GEO: returns the winning local triangle index (or -1);
@@ -1031,41 +1037,116 @@ struct WHit {
     int32_t tri, obj;  // global triangle (or PRIM_SPHERE) and object / light index; obj -1: none
 };
 
+// Node i into registers: eight 16-B loads from the TOP set in LDS (TOP views, i below the staged
+// prefix) or from HBM, each through a pointer of its own address space (ds_read / global_load
+// rather than flat loads that must check the aperture).
+typedef __attribute__((address_space(1))) const uint4 g_uint4;
+typedef __attribute__((address_space(3))) const uint4 l_uint4;
 template <bool TOP>
-__device__ __forceinline__ const wbvh::Node& wnode_at(const DScene& sc, int32_t i) {
-    return (TOP && i < sc.wn_lds) ? sc.wnodes_lds[i] : sc.wnodes[i];
-}
-
-// aabb.rs:33-44 on child i's box (f32 bounds, rounded outward at the build, widened to f64)
-__device__ __forceinline__ void wslab(const wbvh::Node& nd, int i, const RayX& r, double& ts, double& te) {
-    const V3 lo{(double)nd.lo[0][i], (double)nd.lo[1][i], (double)nd.lo[2][i]};
-    const V3 hi{(double)nd.hi[0][i], (double)nd.hi[1][i], (double)nd.hi[2][i]};
-    const V3 ro_min = (lo - r.o) * r.inv;
-    const V3 ro_max = (hi - r.o) * r.inv;
-    ts = max_element(vmin(ro_min, ro_max));
-    te = min_element(vmax(ro_max, ro_min)) * (1.0 + 2.0 * gamma_n(3));
-}
-
-// compare-exchange of the child sort: hits before misses, hits by entry t (a swap only when
-// strictly out of order, so equal entries keep their order)
-__device__ __forceinline__ void wcx(double& ka, int32_t& ra, bool& ha, double& kb, int32_t& rb, bool& hb) {
-    const bool sw = (!ha && hb) || (ha && hb && ka > kb);
-    if (sw) {
-        const double k = ka;
-        ka = kb;
-        kb = k;
-        const int32_t x = ra;
-        ra = rb;
-        rb = x;
-        const bool f = ha;
-        ha = hb;
-        hb = f;
+__device__ __forceinline__ void wnode_load(const DScene& sc, int32_t i, wbvh::Node& nd) {
+    uint4 v[8];
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (TOP) {  // TOP views: the prefix in LDS, the rest in HBM
+        if (i < sc.wn_lds) {
+            extern __shared__ __attribute__((aligned(16))) char lds_scene[];
+            l_uint4* p = (l_uint4*)(lds_scene + sc.off_top_wnodes) + 8 * i;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = p[k];
+        } else {
+            g_uint4* p = (g_uint4*)sc.wnodes + 8 * (size_t)i;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = p[k];
+        }
+    } else
+#endif
+    {  // HBM views and whole-scene LDS views (stage_scene_lds): a generic pointer
+        const uint4* p = reinterpret_cast<const uint4*>(sc.wnodes) + 8 * (size_t)i;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = p[k];
     }
+    __builtin_memcpy(&nd, v, sizeof(nd));
 }
 
-// Walk of one tree from `root`.  Closest (ANY = false): the smallest hit_t of its primitives (ties:
-// the first found) below t_max, nearest child first, entries beyond the closest hit so far culled
-// when popped.  ANY: the first primitive with hit_t < t_max.  Returns t (t_max when nothing is hit),
+// The box test of the wide walks runs in f32 and is conservative: it never rejects a box that the
+// ray's f64 segment [t_min, t_max] enters (the boxes are rounded outward at the build, so no
+// triangle test that would accept a hit is skipped).  Per ray: the origin and 1 / dir rounded to
+// f32, and per axis the t error the origin's rounding causes, e = |o - o32| |1/d| (rounded up).  A
+// slab value T = (p - o32) * inv32 (two roundings, plus those of 1/d and inv32) is within
+// |T| 2^-21 + e of the exact one, so each axis interval is widened by e and the box interval by
+// 2^-21 of its ends.  An axis with |1/d| > 1e30 does not cull (inv32 = 0, e = inf).
+struct RayW {
+    float o[3], inv[3], e[3];
+};
+__device__ __forceinline__ float f32_up(double x) {
+    const float f = (float)x;
+    return (double)f < x ? nextafterf(f, __builtin_huge_valf()) : f;
+}
+__device__ __forceinline__ float f32_down(double x) {
+    const float f = (float)x;
+    return (double)f > x ? nextafterf(f, -__builtin_huge_valf()) : f;
+}
+__device__ __forceinline__ RayW rayw(const RayX& r) {
+    RayW w;
+    const double o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        w.o[a] = (float)o[a];
+        if (fabs(inv[a]) <= 1e30) {
+            w.inv[a] = (float)inv[a];
+            w.e[a] = f32_up(fabs(o[a] - (double)w.o[a]) * fabs(inv[a]) * (1.0 + 0x1p-20));
+        } else {
+            w.inv[a] = 0.0f;
+            w.e[a] = __builtin_huge_valf();
+        }
+    }
+    return w;
+}
+constexpr float WREL = 0x1p-21f;
+#ifndef LUMO_WIDE_ANY_SORT  // any-hit walks: children nearest first (1) or hits in node order (0: C3 8-spp 494 -> 461 ms)
+#define LUMO_WIDE_ANY_SORT 0
+#endif
+// child i of nd: conservative entry k (a lower bound of the box's entry t within [tmin, tmax]) and
+// whether the segment [tmin, tmax] meets the box
+__device__ __forceinline__ bool wslab32(const wbvh::Node& nd, int i, const RayW& w, float tmin, float tmax, float& k) {
+    float ts, te;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float t0 = (nd.lo[a][i] - w.o[a]) * w.inv[a];
+        const float t1 = (nd.hi[a][i] - w.o[a]) * w.inv[a];
+        const float lo = fminf(t0, t1) - w.e[a], hi = fmaxf(t0, t1) + w.e[a];
+        ts = a == 0 ? lo : fmaxf(ts, lo);
+        te = a == 0 ? hi : fminf(te, hi);
+    }
+    ts = ts - fabsf(ts) * WREL;
+    te = te + fabsf(te) * WREL;
+    k = fmaxf(ts, tmin);
+    return k <= fminf(te, tmax);
+}
+
+// compare-exchange of the child sort: hits before misses, hits by entry (a swap only when strictly
+// out of order, so equal entries keep their order)
+template <bool BY_T = true>  // false: hits before misses only
+__device__ __forceinline__ void wcx(float& ka, int32_t& ra, bool& ha, float& kb, int32_t& rb, bool& hb) {
+    const bool sw = hb && (!ha || (BY_T && ka > kb));  // selects, no branch
+    const float k = sw ? kb : ka;
+    kb = sw ? ka : kb;
+    ka = k;
+    const int32_t x = sw ? rb : ra;
+    rb = sw ? ra : rb;
+    ra = x;
+    const bool f = sw ? hb : ha;
+    hb = sw ? ha : hb;
+    ha = f;
+}
+
+// Walk of one tree from `root`.  A primitive counts as hit when lumo's GEO test accepts it: the
+// watertight test with its self-intersection bound (t > t_min + delta_t, triangle.rs:63-187) or
+// the EFloat sphere test (sphere.rs:27-78).  (lumo's traversals compare the GEO = false t and apply
+// the acceptance only to the winning object, where a self-hit at the ray's own origin surface then
+// rejects the whole object; its kd walk rarely meets such hits because its leaf intervals clip
+// them.  Accepting per primitive keeps the walk from stopping at the origin surface)
+// Closest (ANY = false): the smallest accepted t below t_max (ties: the first found), nearest child
+// first, entries beyond the closest hit so far culled when popped.  ANY: the first accepted hit.  Returns t (t_max when nothing is hit),
 // the triangle (PRIM_SPHERE for a sphere) and the object (`objs` index).  An instance leaf pushes a
 // marker and walks its BLAS with the ray in the instance's space (Ray::transform, ray.rs:24-31: the
 // same t parametrises both), the marker's pop restores the world ray.
@@ -1076,83 +1157,87 @@ __device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, cons
     WHit h{t_max, -1, -1};
     if (root == wbvh::NONE) return h;
     int32_t st_ref[wbvh::STACK];
-    double st_t[wbvh::STACK];
+    float st_t[wbvh::STACK];
     int sp = 0;
+    // the top entry of the stack lives in registers (top_ok): the pop after a leaf usually takes the
+    // sibling pushed last, without a scratch round trip; entries below it are in st_ref / st_t
+    bool top_ok = false;
+    int32_t top_ref = 0;
+    float top_t = 0.0f;
+    auto push = [&](int32_t ref, float t) {
+        if (top_ok) {
+            st_ref[sp] = top_ref;
+            st_t[sp] = top_t;
+            sp++;
+        }
+        top_ok = true;
+        top_ref = ref;
+        top_t = t;
+    };
     RayX r = rw;
+    RayW w = rayw(rw);
+    const float tmin32 = f32_down(t_min);
+    float tmax32 = f32_up(t_max);
     int inst = -1;
     int32_t cur = root;
     auto pop = [&]() -> bool {
         for (;;) {
-            if (sp == 0) return false;
-            --sp;
-            const int32_t x = st_ref[sp];
+            int32_t x;
+            float xt;
+            if (top_ok) {
+                top_ok = false;
+                x = top_ref;
+                xt = top_t;
+            } else {
+                if (sp == 0) return false;
+                --sp;
+                x = st_ref[sp];
+                xt = st_t[sp];
+            }
             if (FX && x == wbvh::MARK) {  // leave the instance
                 r = rw;
+                w = rayw(rw);
                 inst = -1;
                 continue;
             }
-            if (!ANY && st_t[sp] > h.t) continue;  // its box is entered beyond the closest hit
+            if (!ANY && (double)xt > h.t) continue;  // its box is entered beyond the closest hit
             cur = x;
             return true;
         }
     };
     for (;;) {
         while (cur >= 0) {  // interior nodes until this lane holds a leaf
-            const wbvh::Node& nd = wnode_at<TOP>(sc, cur);
+            wbvh::Node nd;
+            wnode_load<TOP>(sc, cur, nd);
             C.kd++;
             const int n = nd.n;
-            double k0, k1, k2, k3;
-            bool h0, h1, h2, h3;
+            C.aabb += n;
+            float k0, k1, k2, k3;  // all four slots tested (the unused ones hold finite boxes), then masked
+            bool h0 = wslab32(nd, 0, w, tmin32, tmax32, k0);
+            bool h1 = wslab32(nd, 1, w, tmin32, tmax32, k1);
+            bool h2 = wslab32(nd, 2, w, tmin32, tmax32, k2) && n > 2;
+            bool h3 = wslab32(nd, 3, w, tmin32, tmax32, k3) && n > 3;
             int32_t r0 = nd.ref[0], r1 = nd.ref[1], r2 = nd.ref[2], r3 = nd.ref[3];
-            {
-                double ts, te;
-                C.aabb++;
-                wslab(nd, 0, r, ts, te);
-                k0 = rmax(ts, t_min);
-                h0 = k0 <= rmin(te, h.t);
-                C.aabb++;
-                wslab(nd, 1, r, ts, te);
-                k1 = rmax(ts, t_min);
-                h1 = k1 <= rmin(te, h.t);
-                h2 = h3 = false;
-                k2 = k3 = 0.0;
-                if (n > 2) {
-                    C.aabb++;
-                    wslab(nd, 2, r, ts, te);
-                    k2 = rmax(ts, t_min);
-                    h2 = k2 <= rmin(te, h.t);
-                }
-                if (n > 3) {
-                    C.aabb++;
-                    wslab(nd, 3, r, ts, te);
-                    k3 = rmax(ts, t_min);
-                    h3 = k3 <= rmin(te, h.t);
-                }
+            if (!ANY || LUMO_WIDE_ANY_SORT) {
+                wcx(k0, r0, h0, k1, r1, h1);
+                wcx(k2, r2, h2, k3, r3, h3);
+                wcx(k0, r0, h0, k2, r2, h2);
+                wcx(k1, r1, h1, k3, r3, h3);
+                wcx(k1, r1, h1, k2, r2, h2);
+            } else {  // any hit: no order needed, the hits only moved ahead of the misses
+                wcx<false>(k0, r0, h0, k1, r1, h1);
+                wcx<false>(k2, r2, h2, k3, r3, h3);
+                wcx<false>(k0, r0, h0, k2, r2, h2);
+                wcx<false>(k1, r1, h1, k3, r3, h3);
+                wcx<false>(k1, r1, h1, k2, r2, h2);
             }
-            wcx(k0, r0, h0, k1, r1, h1);
-            wcx(k2, r2, h2, k3, r3, h3);
-            wcx(k0, r0, h0, k2, r2, h2);
-            wcx(k1, r1, h1, k3, r3, h3);
-            wcx(k1, r1, h1, k2, r2, h2);
             if (!h0) {
                 if (!pop()) return h;
                 continue;
             }
-            if (h3) {
-                st_ref[sp] = r3;
-                st_t[sp] = k3;
-                sp++;
-            }
-            if (h2) {
-                st_ref[sp] = r2;
-                st_t[sp] = k2;
-                sp++;
-            }
-            if (h1) {
-                st_ref[sp] = r1;
-                st_t[sp] = k1;
-                sp++;
-            }
+            if (h3) push(r3, k3);
+            if (h2) push(r2, k2);
+            if (h1) push(r1, k1);
             cur = r0;
         }
         // a leaf
@@ -1161,16 +1246,16 @@ __device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, cons
             const DObj& ob = objs[first];
             if (ob.type() == LUMO_OBJ_SPHERE) {
                 const RayX rl = ob.xform() >= 0 ? ray_local(sc.xforms[ob.xform()], rw) : rw;
-                const double t = sphere_hit_t(ob, rl, t_min, h.t);
-                if (t < h.t) {
-                    h = WHit{t, PRIM_SPHERE, first};
+                DHit g;
+                if (sphere_hit<false>(ob, rl, t_min, h.t, g) && g.t < h.t) {
+                    h = WHit{g.t, PRIM_SPHERE, first};
                     if (ANY) return h;
+                    tmax32 = f32_up(h.t);
                 }
             } else {
-                st_ref[sp] = wbvh::MARK;
-                st_t[sp] = -DINF;
-                sp++;
+                push(wbvh::MARK, -__builtin_huge_valf());
                 r = ray_local(sc.xforms[ob.xform()], rw);
+                w = rayw(r);
                 inst = first;
                 cur = blas[first];
                 continue;
@@ -1178,11 +1263,13 @@ __device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, cons
         } else {
             for (int k = 0; k < cnt; ++k) {
                 const double* tv = sc.wtv + wbvh::TV * (size_t)(first + k);
-                const double t = tri_hit_t_at(tv, r, t_min, h.t, C);
-                if (t < h.t) {
+                C.tri++;
+                DHit g;
+                if (tri_hit_geo_at<false>(sc, tv, -1, r, t_min, h.t, g) && g.t < h.t) {
                     const int32_t* ids = reinterpret_cast<const int32_t*>(tv + 9);
-                    h = WHit{t, ids[0], inst >= 0 ? inst : ids[1]};
+                    h = WHit{g.t, ids[0], inst >= 0 ? inst : ids[1]};
                     if (ANY) return h;
+                    tmax32 = f32_up(h.t);
                 }
             }
         }
@@ -1190,37 +1277,15 @@ __device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, cons
     }
 }
 
-// The winner's GEO test: lumo's Object::hit re-walks the winning object and accepts or rejects its
-// closest triangle with this test (kdtree.rs:164-168, triangle.rs:63-187; sphere.rs:27-78); the
-// wide walk already knows that triangle, so only the test runs (counted as lumo counts it).
-template <int FX>
-__device__ __forceinline__ bool wide_accept(const DScene& sc, const DObj& ob, int tri, const RayX& r, double t_min,
-                                            double t_max, Counters& C, DHit& out) {
-    if constexpr (FX) {
-        const RayX rl = ob.xform() >= 0 ? ray_local(sc.xforms[ob.xform()], r) : r;
-        if (tri == PRIM_SPHERE) return sphere_hit<false>(ob, rl, t_min, t_max, out);
-        C.tri++;
-        return tri_hit_geo<false>(sc, tri, rl, t_min, t_max, out);
-    } else {
-        C.tri++;
-        return tri_hit_geo<false>(sc, tri, r, t_min, t_max, out);
-    }
-}
-
-// Scene::hit (scene.rs:119-147) on the wide trees: the objects' closest hit, its GEO test, then the
-// lights' closest hit below it and its GEO test.
+// Scene::hit (scene.rs:119-147) on the wide trees: the objects' closest accepted hit, then the
+// lights' closest accepted hit below it.
 template <int FX, bool TOP>
 __device__ HitRef wide_scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     HitRef h{DINF, 0, -1, -1};
-    double t_max = DINF;
-    DHit g;
     const WHit o = wide_walk<false, FX, TOP>(sc, sc.w_oroot, sc.tobjs, sc.w_oblas, r, 0.0, DINF, C);
-    if (o.obj >= 0 && wide_accept<FX>(sc, sc.tobjs[o.obj], o.tri, r, 0.0, t_max, C, g)) {
-        h = HitRef{g.t, 1, o.obj, o.tri};
-        t_max = g.t;
-    }
-    const WHit l = wide_walk<false, FX, TOP>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, r, 0.0, t_max, C);
-    if (l.obj >= 0 && wide_accept<FX>(sc, sc.tlights[l.obj], l.tri, r, 0.0, t_max, C, g)) h = HitRef{g.t, 2, l.obj, l.tri};
+    if (o.obj >= 0) h = HitRef{o.t, 1, o.obj, o.tri};
+    const WHit l = wide_walk<false, FX, TOP>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, r, 0.0, h.t, C);
+    if (l.obj >= 0) h = HitRef{l.t, 2, l.obj, l.tri};
     return h;
 }
 

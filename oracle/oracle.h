@@ -55,6 +55,12 @@ void oracle_set_integrator(int integrator);
 /* Acceleration structure of subsequent calls: 0 lumo's BVHs + kd-trees (default), 1 the wide BVH of
  * lumo_amd's LUMO_OPT_ACCEL = 1 (same structure as the upload builds, walk restated here). */
 void oracle_set_accel(int accel);
+/* Diagnostics: the wide BVH built for `scene`: info[8] = {ok, nodes, leaf triangle records, walk
+ * stack need, node levels, objects root ref, lights root ref, 0}; non-null buffers (sized from a
+ * first call with nulls) receive the nodes (128 B each), the records (10 doubles each) and the per
+ * object / light BLAS roots. */
+int oracle_wide_export(const lumo_scene_desc* scene, int64_t* info, void* nodes, double* tv, int32_t* obj_blas,
+                       int32_t* light_blas);
 /* SamplerType of subsequent renders (LUMO_SAMPLER_*, samplers.rs:6-17; default MultiJittered). */
 void oracle_set_sampler(int sampler);
 /* The points SamplerType::new(batch, samples, seed) yields (x, y interleaved, at most cap). */

@@ -780,8 +780,9 @@ bool scene_hit_light(const Scene& sc, const Ray& r, int light, Hit* out, Counter
 // ------------------------------------------------------------------ wide accel
 // The walk of lumo_amd's wide mode over the shared structure (wbvh.h), restated: nearest child
 // first with entry culling on pop, ANY = first hit below t_max; an instance leaf walks its BLAS with
-// the ray in the instance's space (ray.rs:24-31, unnormalised, so t is shared).  Primitives are
-// tested with lumo's own tests: triangle_hit(GEO = false) (triangle.rs:63-187) and sphere_hit_t.
+// the ray in the instance's space (ray.rs:24-31, unnormalised, so t is shared).  A primitive is hit
+// when lumo's GEO test accepts it: triangle_hit(GEO = true) (triangle.rs:63-187, with the
+// self-intersection bound) and sphere_hit (sphere.rs:27-78), DESIGN.md §4b.
 // Counters: aabb = child boxes tested, kd = nodes visited, tri = triangles tested.
 constexpr int PRIM_SPHERE_O = -2;
 struct WRes {
@@ -789,12 +790,57 @@ struct WRes {
     int tri, obj;
 };
 struct WChild {
-    double k;
+    float k;
     int32_t ref;
     bool hit;
 };
-void wide_cx(WChild& a, WChild& b) {  // hits first, hits by entry t; swap only when strictly out of order
-    if ((!a.hit && b.hit) || (a.hit && b.hit && a.k > b.k)) std::swap(a, b);
+// The wide walk's conservative f32 box test (lumo_amd dscene.h wslab32): per ray the
+// origin and 1/dir in f32 and per axis e = |o - o32| |1/d| rounded up (an axis with |1/d| > 1e30
+// does not cull); each axis interval widened by e, the box interval by 2^-21 of its ends.
+struct WRay {
+    float o[3], inv[3], e[3];
+};
+float f32_up(double x) {
+    const float f = (float)x;
+    return (double)f < x ? std::nextafter(f, HUGE_VALF) : f;
+}
+float f32_down(double x) {
+    const float f = (float)x;
+    return (double)f > x ? std::nextafter(f, -HUGE_VALF) : f;
+}
+WRay wray_of(const Ray& r) {
+    WRay w;
+    const V3 inv = 1.0 / r.dir;
+    const double o[3] = {r.origin.x, r.origin.y, r.origin.z}, iv[3] = {inv.x, inv.y, inv.z};
+    for (int a = 0; a < 3; ++a) {
+        w.o[a] = (float)o[a];
+        if (std::fabs(iv[a]) <= 1e30) {
+            w.inv[a] = (float)iv[a];
+            w.e[a] = f32_up(std::fabs(o[a] - (double)w.o[a]) * std::fabs(iv[a]) * (1.0 + 0x1p-20));
+        } else {
+            w.inv[a] = 0.0f;
+            w.e[a] = HUGE_VALF;
+        }
+    }
+    return w;
+}
+bool wide_box(const wbvh::Node& nd, int i, const WRay& w, float tmin, float tmax, float* k) {
+    float ts = -HUGE_VALF, te = HUGE_VALF;
+    for (int a = 0; a < 3; ++a) {
+        const float t0 = (nd.lo[a][i] - w.o[a]) * w.inv[a];
+        const float t1 = (nd.hi[a][i] - w.o[a]) * w.inv[a];
+        ts = std::fmax(ts, std::fmin(t0, t1) - w.e[a]);
+        te = std::fmin(te, std::fmax(t0, t1) + w.e[a]);
+    }
+    ts = ts - std::fabs(ts) * 0x1p-21f;
+    te = te + std::fabs(te) * 0x1p-21f;
+    *k = std::fmax(ts, tmin);
+    return *k <= std::fmin(te, tmax);
+}
+// hits first, then (by_t) hits by entry t; a swap only when strictly out of order.  Closest walks
+// sort by entry; any-hit walks only move the hits ahead (their order is irrelevant to the answer).
+void wide_cx(WChild& a, WChild& b, bool by_t) {
+    if (b.hit && (!a.hit || (by_t && a.k > b.k))) std::swap(a, b);
 }
 WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std::vector<int32_t>& blas,
                const Ray& rw, double t_min, double t_max, bool any, Counters& C) {
@@ -803,11 +849,13 @@ WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std
     if (root == wbvh::NONE) return h;
     struct Entry {
         int32_t ref;
-        double t;
+        float t;
     } st[wbvh::STACK];
     int sp = 0;
     Ray r = rw;
-    V3 inv = 1.0 / r.dir;
+    WRay w = wray_of(r);
+    const float tmin32 = f32_down(t_min);
+    float tmax32 = f32_up(t_max);
     int inst = -1;
     int32_t cur = root;
     auto pop = [&]() -> bool {
@@ -815,11 +863,11 @@ WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std
             const Entry e = st[--sp];
             if (e.ref == wbvh::MARK) {
                 r = rw;
-                inv = 1.0 / r.dir;
+                w = wray_of(r);
                 inst = -1;
                 continue;
             }
-            if (!any && e.t > h.t) continue;
+            if (!any && (double)e.t > h.t) continue;
             cur = e.ref;
             return true;
         }
@@ -830,21 +878,16 @@ WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std
             const wbvh::Node& nd = W.nodes[cur];
             C.kd++;
             WChild ch[4];
-            for (int i = 0; i < 4; ++i) ch[i] = WChild{0.0, nd.ref[i], false};
+            for (int i = 0; i < 4; ++i) ch[i] = WChild{0.0f, nd.ref[i], false};
             for (int i = 0; i < nd.n; ++i) {
-                const double lo[3] = {(double)nd.lo[0][i], (double)nd.lo[1][i], (double)nd.lo[2][i]};
-                const double hi[3] = {(double)nd.hi[0][i], (double)nd.hi[1][i], (double)nd.hi[2][i]};
-                double ts, te;
                 C.aabb++;
-                aabb_intersect(lo, hi, r.origin, inv, ts, te);
-                ch[i].k = rmax(ts, t_min);
-                ch[i].hit = ch[i].k <= rmin(te, h.t);
+                ch[i].hit = wide_box(nd, i, w, tmin32, tmax32, &ch[i].k);
             }
-            wide_cx(ch[0], ch[1]);
-            wide_cx(ch[2], ch[3]);
-            wide_cx(ch[0], ch[2]);
-            wide_cx(ch[1], ch[3]);
-            wide_cx(ch[1], ch[2]);
+            wide_cx(ch[0], ch[1], !any);
+            wide_cx(ch[2], ch[3], !any);
+            wide_cx(ch[0], ch[2], !any);
+            wide_cx(ch[1], ch[3], !any);
+            wide_cx(ch[1], ch[2], !any);
             if (!ch[0].hit) {
                 if (!pop()) return h;
                 continue;
@@ -859,15 +902,16 @@ WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std
             const lumo_object& ob = objs[first];
             if (ob.type == LUMO_OBJ_SPHERE) {
                 const Ray rl = ob.xform >= 0 ? ray_to_local(xform_of(sc.d->transforms[ob.xform]), rw, false) : rw;
-                const double t = sphere_hit_t(ob, rl, t_min, h.t);
-                if (t < h.t) {
-                    h = WRes{t, PRIM_SPHERE_O, first};
+                Hit g;
+                if (sphere_hit(ob, rl, t_min, h.t, &g) && g.t < h.t) {
+                    h = WRes{g.t, PRIM_SPHERE_O, first};
                     if (any) return h;
+                    tmax32 = f32_up(h.t);
                 }
             } else {
-                st[sp++] = Entry{wbvh::MARK, -INF};
+                st[sp++] = Entry{wbvh::MARK, -HUGE_VALF};
                 r = ray_to_local(xform_of(sc.d->transforms[ob.xform]), rw, false);
-                inv = 1.0 / r.dir;
+                w = wray_of(r);
                 inst = first;
                 cur = blas[first];
                 continue;
@@ -876,11 +920,12 @@ WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std
             for (int k = 0; k < cnt; ++k) {
                 int32_t ids[2];
                 std::memcpy(ids, &W.tv[(size_t)wbvh::TV * (first + k) + 9], sizeof(ids));
-                Hit dummy;
-                const double t = triangle_hit(sc, ids[0], r, t_min, h.t, false, &dummy, C);
+                Hit g;  // accepted by the GEO test (self-intersection bound included)
+                const double t = triangle_hit(sc, ids[0], r, t_min, h.t, true, &g, C);
                 if (t < h.t) {
                     h = WRes{t, ids[0], inst >= 0 ? inst : ids[1]};
                     if (any) return h;
+                    tmax32 = f32_up(h.t);
                 }
             }
         }
@@ -913,14 +958,15 @@ bool object_hit_prim(const Scene& sc, const lumo_object& ob, int prim, const Ray
     out->p = xf_pt(X, out->p);
     return true;
 }
-// Scene::hit on the wide trees (scene.rs:119-147): objects' closest, its GEO test, then the lights'
+// Scene::hit on the wide trees (scene.rs:119-147): objects' closest accepted hit, then the lights'
 bool wide_scene_hit(const Scene& sc, const Ray& r, Hit* h, int* kind, int* which, int* prim, Counters& C) {
     double t_max = INF;
     bool found = false;
     *kind = 0;
     Hit tmp;
+    Counters rebuild;  // the record of the accepted hit, rebuilt (the device's hit_record; not counted)
     const WRes o = wide_walk(sc, sc.w->obj_root, sc.d->objects, sc.w->obj_blas, r, 0.0, INF, false, C);
-    if (o.obj >= 0 && object_hit_prim(sc, sc.d->objects[o.obj], o.tri, r, 0.0, t_max, &tmp, C)) {
+    if (o.obj >= 0 && object_hit_prim(sc, sc.d->objects[o.obj], o.tri, r, 0.0, t_max, &tmp, rebuild)) {
         *h = tmp;
         found = true;
         *kind = 1;
@@ -929,7 +975,7 @@ bool wide_scene_hit(const Scene& sc, const Ray& r, Hit* h, int* kind, int* which
         t_max = tmp.t;
     }
     const WRes l = wide_walk(sc, sc.w->light_root, sc.d->lights, sc.w->light_blas, r, 0.0, t_max, false, C);
-    if (l.obj >= 0 && object_hit_prim(sc, sc.d->lights[l.obj], l.tri, r, 0.0, t_max, &tmp, C)) {
+    if (l.obj >= 0 && object_hit_prim(sc, sc.d->lights[l.obj], l.tri, r, 0.0, t_max, &tmp, rebuild)) {
         *h = tmp;
         found = true;
         *kind = 2;
@@ -2717,6 +2763,26 @@ extern "C" void oracle_set_tone_map(int kind, double arg) { g_tone = ToneMap{kin
 
 extern "C" void oracle_set_integrator(int integrator) { g_integrator = integrator; }
 extern "C" void oracle_set_accel(int accel) { g_accel = accel; }
+
+// Diagnostics: the wide BVH the upload builds for this scene (wbvh_build.h), for structure tests.
+extern "C" int oracle_wide_export(const lumo_scene_desc* scene, int64_t* info, void* nodes, double* tv,
+                                  int32_t* obj_blas, int32_t* light_blas) {
+    if (!scene || !info) return LUMO_ERR_INVALID;
+    const wbvh::Accel a = wbvh::build(*scene);
+    info[0] = a.ok;
+    info[1] = (int64_t)a.nodes.size();
+    info[2] = (int64_t)(a.tv.size() / wbvh::TV);
+    info[3] = a.max_stack;
+    info[4] = a.depth;
+    info[5] = a.obj_root;
+    info[6] = a.light_root;
+    info[7] = 0;
+    if (nodes) std::memcpy(nodes, a.nodes.data(), a.nodes.size() * sizeof(wbvh::Node));
+    if (tv) std::memcpy(tv, a.tv.data(), a.tv.size() * sizeof(double));
+    if (obj_blas) std::memcpy(obj_blas, a.obj_blas.data(), a.obj_blas.size() * sizeof(int32_t));
+    if (light_blas) std::memcpy(light_blas, a.light_blas.data(), a.light_blas.size() * sizeof(int32_t));
+    return LUMO_OK;
+}
 extern "C" void oracle_set_sampler(int sampler) { g_sampler = sampler; }
 // Probe: the points a pixel sampler (SamplerType::new(batch, samples, seed) of the current
 // g_sampler) yields, x y interleaved; returns how many (at most cap).

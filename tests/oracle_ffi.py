@@ -41,6 +41,9 @@ def load(path=None):
         lib.oracle_set_integrator.argtypes = [C.c_int]
         lib.oracle_set_accel.restype = None
         lib.oracle_set_accel.argtypes = [C.c_int]
+        lib.oracle_wide_export.restype = C.c_int
+        lib.oracle_wide_export.argtypes = [C.POINTER(_ffi.SceneDesc), C.POINTER(C.c_int64), C.c_void_p,
+                                           _ffi.c_double_p, _ffi.c_int32_p, _ffi.c_int32_p]
         lib.oracle_set_sampler.restype = None
         lib.oracle_set_sampler.argtypes = [C.c_int]
         lib.oracle_sampler_points.restype = C.c_int64
@@ -253,3 +256,27 @@ def sampler_points(sampler, batch, samples, seed):
     lib.oracle_set_sampler(0)
     assert n >= 0, n
     return out[:2 * n].reshape(-1, 2)
+
+
+# wide BVH node (lumo_amd/csrc/common/wbvh.h Node, 128 B)
+WNODE = np.dtype([("lo", "<f4", (3, 4)), ("hi", "<f4", (3, 4)), ("ref", "<i4", 4), ("n", "<i4"), ("pad", "<i4", 3)])
+
+
+def wide_export(scene_desc):
+    """The wide BVH the upload builds for the scene: dict with ok, nodes (WNODE array), tv
+    (records x 10 doubles; column 9 holds (tri, obj) int32 pairs), tri / obj ids, the roots and the
+    per object / light BLAS roots, stack need and depth."""
+    lib = load()
+    info = (C.c_int64 * 8)()
+    assert lib.oracle_wide_export(C.byref(scene_desc), info, None, None, None, None) == 0
+    nn, nt = int(info[1]), int(info[2])
+    nodes = np.zeros(max(nn, 1), dtype=WNODE)
+    tv = np.zeros((max(nt, 1), 10))
+    ob = np.zeros(max(scene_desc.num_objects, 1), dtype=np.int32)
+    lb = np.zeros(max(scene_desc.num_lights, 1), dtype=np.int32)
+    assert lib.oracle_wide_export(C.byref(scene_desc), info, nodes.ctypes.data_as(C.c_void_p), _dp(tv),
+                                  ob.ctypes.data_as(_ffi.c_int32_p), lb.ctypes.data_as(_ffi.c_int32_p)) == 0
+    ids = tv[:, 9].copy().view(np.int32).reshape(-1, 2)
+    return dict(ok=bool(info[0]), nodes=nodes[:nn], tv=tv[:nt], tri=ids[:nt, 0], obj=ids[:nt, 1],
+                stack=int(info[3]), depth=int(info[4]), obj_root=int(info[5]), light_root=int(info[6]),
+                obj_blas=ob[:scene_desc.num_objects], light_blas=lb[:scene_desc.num_lights])
