@@ -319,6 +319,8 @@ typedef struct {
     /* closest queries (included in closest_queries) run by the path tracer's tail kernel past
      * the first bounce it takes: > 0 when the device switched a pass to the tail kernel (ABI 9) */
     uint64_t tail_queries;
+    /* bounces whose closest-hit rays were sorted before their walks (LUMO_OPT_RAY_SORT; ABI 10) */
+    uint64_t sorted_bounces;
 } lumo_stats;
 
 /* Per-path dump of one task (test hook for per-path parity): arrays sized samples x pixels
@@ -485,6 +487,9 @@ lumo_status lumo_scene_info(void* ctx, lumo_scene_info_t* info);
  * (kernels k_calib_read8 / k_calib_write8), to calibrate rocprofv3 FETCH_SIZE / WRITE_SIZE for
  * the access width of the path kernels. */
 lumo_status lumo_debug_stream(void* ctx, size_t n);
+/* Diagnostics (ABI 10): the device's exclusive prefix sum (device/scan.h, the BDPT item lists' scan)
+ * of n host uint32 counts into out. */
+lumo_status lumo_debug_scan(void* ctx, const uint32_t* in, uint32_t* out, size_t n);
 
 #ifdef __cplusplus
 }

@@ -888,15 +888,17 @@ class Renderer:
         self._device = int(d)
         return self
 
-    def render(self, rank=0, world_size=1, schedule="static", chunk=None, store=None, key=None):
+    def render(self, rank=0, world_size=1, schedule="static", chunk=None, store=None, key=None, timeout=None):
         """Render all (batch, tile) tasks and return this rank's (partial) film.
 
         With world_size > 1, `schedule="static"` renders the tiles with
         tile_index % world_size == rank; `schedule="dynamic"` claims
         chunks of `chunk` tiles from a `dist.TileQueue` in the process group's store until none
         are left (lumo's shared task receiver, pool.rs:26, 41-54), for scenes whose tiles cost
-        unequal time.  Either way the reduced film is the single-process film.  `store` / `key`
-        go to the TileQueue: with `key` the queue needs no process group (dist.TileQueue)."""
+        unequal time.  Either way the reduced film is the single-process film.  `store` / `key` /
+        `timeout` go to the TileQueue: with `key` the queue needs no process group, and `timeout`
+        bounds the wait for the other ranks after this rank's last chunk (default: the store's
+        timeout; dist.TileQueue)."""
         import time
         if schedule not in ("static", "dynamic"):
             raise ValueError(f"unknown schedule {schedule!r}")
@@ -914,7 +916,7 @@ class Renderer:
         if schedule == "static" or world_size == 1:
             chunks = iter([shard_tasks(tasks, w, h, rank, world_size)])
         else:
-            queue = TileQueue(w, h, world_size, chunk=chunk, store=store, key=key)
+            queue = TileQueue(w, h, world_size, chunk=chunk, store=store, key=key, timeout=timeout)
             chunks = (tasks_of_tiles(tasks, w, h, tiles) for tiles in queue)
         dev = Device(self._device)
         dev.upload(self.scene, self.camera)

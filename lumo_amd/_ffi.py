@@ -15,6 +15,7 @@ c_double_p = C.POINTER(C.c_double)
 c_int32_p = C.POINTER(C.c_int32)
 c_int64_p = C.POINTER(C.c_int64)
 c_uint64_p = C.POINTER(C.c_uint64)
+c_uint32_p = C.POINTER(C.c_uint32)
 
 LUMO_OK = 0
 LUMO_ERR_OOM = 7
@@ -160,7 +161,8 @@ class Stats(C.Structure):
                 ("closest_queries", C.c_uint64), ("shadow_queries", C.c_uint64), ("bounces", C.c_uint64),
                 ("aabb_tests", C.c_uint64 * 2), ("kd_nodes", C.c_uint64 * 2), ("tri_tests", C.c_uint64 * 2),
                 ("samples_nan", C.c_uint64), ("samples_neg", C.c_uint64), ("samples_large", C.c_uint64),
-                ("shadow_resolved", C.c_uint64), ("tail_queries", C.c_uint64)]
+                ("shadow_resolved", C.c_uint64), ("tail_queries", C.c_uint64),
+                ("sorted_bounces", C.c_uint64)]
 
 
 class ScheduleInfo(C.Structure):
@@ -211,6 +213,7 @@ DEVICE_API = [
     ("lumo_get_option", C.c_int32, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64)]),
     ("lumo_last_schedule", C.c_int32, [C.c_void_p, C.POINTER(ScheduleInfo)]),
     ("lumo_debug_stream", C.c_int32, [C.c_void_p, C.c_size_t]),
+    ("lumo_debug_scan", C.c_int32, [C.c_void_p, c_uint32_p, c_uint32_p, C.c_size_t]),
     ("lumo_scene_info", C.c_int32, [C.c_void_p, C.POINTER(SceneInfo)]),
     ("lumo_debug_set_integrator", C.c_int32, [C.c_void_p, C.c_int]),
     ("lumo_debug_set_sampler", C.c_int32, [C.c_void_p, C.c_int]),

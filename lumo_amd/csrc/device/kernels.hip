@@ -30,11 +30,11 @@
 #include <vector>
 
 #include "../../../include/lumo_amd.h"
-#include <hipcub/hipcub.hpp>
 
 #define LUMO_MAIN_TU
 #include "../host/wbvh.h"
 #include "launch.h"
+#include "scan.h"
 #include "pt.h"
 
 using namespace lumo;
@@ -247,43 +247,51 @@ __global__ void k_bounce_begin(uint32_t* counts, unsigned long long* headq) {
     }
 }
 
-// Ray sorting (LUMO_OPT_RAY_SORT): a 30-bit key per queued ray, the direction octant above a Morton
-// code of the origin (9 bits per axis over the objects BVH's world box); rays past the live count
-// get the largest key, so a stable sort leaves them behind the live ones.  The sort changes which
-// lane walks which ray, nothing else (k_closest_q writes each hit at its ray's own position).
-__device__ __forceinline__ uint32_t spread3(uint32_t x) {  // 9 bits -> every third bit
-    x &= 0x1ffu;
-    x = (x | (x << 16)) & 0x030000ffu;
-    x = (x | (x << 8)) & 0x0300f00fu;
-    x = (x | (x << 4)) & 0x030c30c3u;
-    x = (x | (x << 2)) & 0x09249249u;
-    return x;
+// Ray sorting (LUMO_OPT_RAY_SORT): a counting sort of a bounce's live closest-hit rays on a 12-bit
+// key (scan.h rs_key: the direction octant and the origin's cell among 8 per axis of the objects
+// BVH's world box), so that neighbouring lanes walk alike rays.  It changes which lane walks which
+// ray, nothing else (k_closest_q writes each hit at its ray's own position).  Two launches: keys +
+// histogram, then the histogram's scan + scatter into perm (the walk order of queue positions).
+__global__ __launch_bounds__(RS_BLOCK) void k_rsort_keys(QState cur, const uint32_t* counts, uint32_t n, V3 lo,
+                                                         V3 scale, int mode, uint32_t* keys, uint32_t* ws) {
+    const uint32_t q = blockIdx.x * RS_BLOCK + threadIdx.x;
+    const bool live = q < n && q < counts[CNT_CUR];
+    uint32_t key = 0;
+    if (live) {
+        const V3 o = qv3(cur, QD_O, q), d = qv3(cur, QD_D, q);
+        key = rs_key(o.x, o.y, o.z, d.x, d.y, d.z, lo.x, lo.y, lo.z, scale.x, scale.y, scale.z, mode);
+        keys[q] = key;
+    }
+    rs_count_block(key, live, ws);
 }
-__device__ __forceinline__ uint32_t ray_key(V3 o, V3 d, V3 lo, V3 scale, int mode) {
-    auto cell = [](double x) { return (uint32_t)(x < 0.0 ? 0.0 : (x > 511.0 ? 511.0 : x)); };
-    const uint32_t m = spread3(cell((o.x - lo.x) * scale.x)) | (spread3(cell((o.y - lo.y) * scale.y)) << 1) |
-                       (spread3(cell((o.z - lo.z) * scale.z)) << 2);
-    const uint32_t oct = (d.x < 0.0 ? 1u : 0u) | (d.y < 0.0 ? 2u : 0u) | (d.z < 0.0 ? 4u : 0u);
-    return mode == 2 ? (m << 3) | oct : (oct << 27) | m;  // 2: origin cell major
-}
-__global__ __launch_bounds__(BLOCK) void k_sort_keys(QState cur, const uint32_t* counts, uint32_t n, V3 lo, V3 scale,
-                                                      uint32_t* keys, uint32_t* vals, int mode) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n) return;
-    keys[q] = q < counts[CNT_CUR] ? ray_key(qv3(cur, QD_O, q), qv3(cur, QD_D, q), lo, scale, mode) : 0xffffffffu;
-    vals[q] = q;
+__global__ __launch_bounds__(RS_BLOCK) void k_rsort_scatter(const uint32_t* keys, const uint32_t* counts, uint32_t n,
+                                                            uint32_t* ws, uint32_t* perm) {
+    const uint32_t q = blockIdx.x * RS_BLOCK + threadIdx.x;
+    const bool live = q < n && q < counts[CNT_CUR];
+    rs_scatter_block(live ? keys[q] : 0u, live, q, ws, perm);
 }
 // ... of a BDPT walk bounce: the queue holds slot ids, the rays live per slot; the sorted values are
 // the slot ids in walk order (a queue in their own right)
-__global__ __launch_bounds__(BLOCK) void k_sort_keys_slots(const int32_t* queue, const double* ro, const double* rd,
-                                                            const uint32_t* counts, uint32_t n, V3 lo, V3 scale,
-                                                            uint32_t* keys, uint32_t* vals, int mode) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n) return;
-    const bool live = q < counts[CNT_CUR];
-    const int s = live ? queue[q] : 0;
-    keys[q] = live ? ray_key(ldv3(ro, s), ldv3(rd, s), lo, scale, mode) : 0xffffffffu;
-    vals[q] = (uint32_t)s;
+__global__ __launch_bounds__(RS_BLOCK) void k_rsort_keys_slots(const int32_t* queue, const double* ro, const double* rd,
+                                                               const uint32_t* counts, uint32_t n, V3 lo, V3 scale,
+                                                               int mode, uint32_t* keys, uint32_t* ws) {
+    const uint32_t q = blockIdx.x * RS_BLOCK + threadIdx.x;
+    const bool live = q < n && q < counts[CNT_CUR];
+    uint32_t key = 0;
+    if (live) {
+        const int s = queue[q];
+        const V3 o = ldv3(ro, s), d = ldv3(rd, s);
+        key = rs_key(o.x, o.y, o.z, d.x, d.y, d.z, lo.x, lo.y, lo.z, scale.x, scale.y, scale.z, mode);
+        keys[q] = key;
+    }
+    rs_count_block(key, live, ws);
+}
+__global__ __launch_bounds__(RS_BLOCK) void k_rsort_scatter_slots(const int32_t* queue, const uint32_t* keys,
+                                                                  const uint32_t* counts, uint32_t n, uint32_t* ws,
+                                                                  uint32_t* perm) {
+    const uint32_t q = blockIdx.x * RS_BLOCK + threadIdx.x;
+    const bool live = q < n && q < counts[CNT_CUR];
+    rs_scatter_block(live ? keys[q] : 0u, live, live ? (uint32_t)queue[q] : 0u, ws, perm);
 }
 
 // Setup zeroing of a render's accumulators and counters in one launch instead of a fill per
@@ -979,8 +987,8 @@ enum WorkId {
     W_QUERIES4, W_P_VALID4, W_COUNTS4, W_QS6_D, W_QS6_R, W_QS6_I, W_QS7_D, W_QS7_R, W_QS7_I,
     W_SQ_QL, W_BD_LM, W_BD_LMF, W_BD_CM, W_BD_CMF, W_BDR_LM, W_BDR_LMF, W_BDR_CM, W_BDR_CMF,
     W_SPLIT_SET1,  // render_split_pipelined sets 1..3: hits + NEE records, 8 buffers each
-    W_SORT_SET0 = W_SPLIT_SET1 + 3 * 8,  // ray sorting of pass set k: keys x 2, values x 2, temp
-    W_BD_ALIST = W_SORT_SET0 + 4 * 5,    // BDPT (a)-item trace lists
+    W_SORT_SET0 = W_SPLIT_SET1 + 3 * 8,  // ray sorting of pass set k: keys, order, workspace
+    W_BD_ALIST = W_SORT_SET0 + 4 * 3,    // BDPT (a)-item trace lists
     W_COUNT
 };
 
@@ -1141,23 +1149,17 @@ void alloc_pass_set(Ctx& c, Paths& Q, int k, int N, lumo_status& st) {
 }
 // Ray sorting buffers of pass set k (none when the option is off)
 int ray_sort_mode(const Ctx& c) { return c.o.ray_sort >= 0 ? c.o.ray_sort : (c.sc.stack_class >= 32 ? 1 : 0); }
+// keys and walk order (cap each) and the counting sort's workspace (scan.h RS_WORDS), zeroed here
+// and by every sort's last block
 void alloc_sort(Ctx& c, HitQ& hq, int k, lumo_status& st) {
     hq.perm = nullptr;
-    hq.sk[0] = hq.sk[1] = hq.sv[0] = hq.sv[1] = nullptr;
-    hq.tmp = nullptr;
-    hq.tmp_bytes = 0;
+    hq.keys = hq.order = hq.ws = nullptr;
     if (!ray_sort_mode(c)) return;
-    const int w = W_SORT_SET0 + 5 * k;
-    for (int b = 0; b < 2; ++b) {
-        hq.sk[b] = wbuf<uint32_t>(c, w + b, hq.cap, st);
-        hq.sv[b] = wbuf<uint32_t>(c, w + 2 + b, hq.cap, st);
-    }
-    hipcub::DoubleBuffer<uint32_t> kb(hq.sk[0], hq.sk[1]), vb(hq.sv[0], hq.sv[1]);
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, hq.tmp_bytes, kb, vb, (int)hq.cap, 0, 30) != hipSuccess) {
-        st = LUMO_ERR_HIP;
-        return;
-    }
-    hq.tmp = wbuf<char>(c, w + 4, hq.tmp_bytes, st);
+    const int w = W_SORT_SET0 + 3 * k;
+    hq.keys = wbuf<uint32_t>(c, w, hq.cap, st);
+    hq.order = wbuf<uint32_t>(c, w + 1, hq.cap, st);
+    hq.ws = wbuf<uint32_t>(c, w + 2, RS_WORDS, st);
+    if (!st && hipMemset(hq.ws, 0, sizeof(uint32_t) * RS_WORDS) != hipSuccess) st = LUMO_ERR_HIP;
 }
 
 // ... and, for the split schedule, the set's closest hits and NEE records (the sizes of set 0's)
@@ -1177,7 +1179,8 @@ void alloc_split_set(Ctx& c, Paths& Q, const Paths& S, int k, int ns, lumo_statu
 size_t split_set_bytes(const Paths& S, int N, int ns) {
     return (size_t)N * (4 + 4 + 2) * 8 + (size_t)N * 3 * 4 + 2 * (size_t)N * (QD_N * 8 + 16 + QI_N * 4) +
            S.hq.cap * (8 + 12) + S.sq.cap * (SD_N * 8 + SI_N * 4) +
-           S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4) + (ns > 1 ? S.sq.cap * (4 * SHQ_CLASSES + 16) : 0);
+           S.sq.hcap * ((ns > 1 ? SH_N : SH_N1) * 8 + SHI_N * 4) + (ns > 1 ? S.sq.cap * (4 * SHQ_CLASSES + 16) : 0) +
+           (S.hq.keys ? S.hq.cap * 8 + RS_WORDS * 4 : 0);  // the set's ray-sort keys, order and workspace
 }
 
 
@@ -1402,13 +1405,13 @@ void issue_split_bounce(Ctx& c, Paths& S, const Tasks& T, const QState& cur, con
         Paths Sc = S;
         StageTimer tm(c, c.o.timing, ST_CLOSEST, sm);
         const int sort_mode = ray_sort_mode(c);
-        if (sort_mode && S.hq.tmp && ub >= kSortMin && (uint64_t)ub <= S.hq.cap) {
-            k_sort_keys<<<ceil_div(ub, BLOCK), BLOCK, 0, sm>>>(cur, S.counts, ub, c.sort_lo, c.sort_scale, S.hq.sk[0],
-                                                               S.hq.sv[0], sort_mode);
-            hipcub::DoubleBuffer<uint32_t> kb(S.hq.sk[0], S.hq.sk[1]), vb(S.hq.sv[0], S.hq.sv[1]);
-            size_t tb = S.hq.tmp_bytes;
-            if (hipcub::DeviceRadixSort::SortPairs(S.hq.tmp, tb, kb, vb, (int)ub, 0, 30, sm) == hipSuccess)
-                Sc.hq.perm = vb.Current();
+        if (sort_mode && S.hq.keys && ub >= kSortMin && (uint64_t)ub <= S.hq.cap) {
+            const int g = ceil_div(ub, RS_BLOCK);
+            k_rsort_keys<<<g, RS_BLOCK, 0, sm>>>(cur, S.counts, ub, c.sort_lo, c.sort_scale, sort_mode, S.hq.keys,
+                                                 S.hq.ws);
+            k_rsort_scatter<<<g, RS_BLOCK, 0, sm>>>(S.hq.keys, S.counts, ub, S.hq.ws, S.hq.order);
+            Sc.hq.perm = S.hq.order;
+            c.stats.sorted_bounces += 1;
         }
         launch_trav(
             c, ub, [&](auto K, const TravLaunch& l) { launch_closest_q<decltype(K)::value>(l, c.sc, Sc, cur, skip); },
@@ -1780,12 +1783,13 @@ struct BdGroup {
     int issued = 0, consumed = 0, seg_first = 0, walk = 0;  // snapshots; bounces of the current walk
     uint32_t ub = 0;
     bool done = false;
+    bool sort_ws_zeroed = false;  // the walk sort's workspace (zeroed once, then by every sort)
 };
 
 // Per-group work buffers (k: BdBuf), grown on demand like the render's own.
 enum BdBuf { BG_TERM_A, BG_TERM_B, BG_BLIST, BG_AT, BG_AKIND, BG_AOBJ, BG_ATRI, BG_ALIST, BG_SCAN, BG_RANGES, BG_TAPS,
              BG_RLD, BG_RLI, BG_RCD, BG_RCI, BG_RSP, BG_RSPN, BG_RDRAWS, BG_ROK, BG_RLM, BG_RLMF, BG_RCM, BG_RCMF,
-             BG_REDO, BG_SK0, BG_SK1, BG_SV0, BG_SV1, BG_STMP, BG_COUNT };
+             BG_REDO, BG_SK0, BG_SV0, BG_STMP, BG_COUNT };
 template <typename T>
 T* gbuf(Ctx& c, int g, int k, size_t count, lumo_status& st) {
     if (c.gwork.size() < (size_t)4 * BG_COUNT) c.gwork.resize((size_t)4 * BG_COUNT);
@@ -1941,19 +1945,20 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
         if (walk_sort && skip == 0 && ub >= kSortMin) {  // the walk's rays sorted (lane order only)
             StageTimer tm(c, c.o.timing, ST_CLOSEST, q.sm);
             const size_t nq = (size_t)q.n;
-            uint32_t* sk0 = gbuf<uint32_t>(c, gi, BG_SK0, nq, st);
-            uint32_t* sk1 = gbuf<uint32_t>(c, gi, BG_SK1, nq, st);
-            uint32_t* sv0 = gbuf<uint32_t>(c, gi, BG_SV0, nq, st);
-            uint32_t* sv1 = gbuf<uint32_t>(c, gi, BG_SV1, nq, st);
-            hipcub::DoubleBuffer<uint32_t> kb(sk0, sk1), vb(sv0, sv1);
-            size_t tb = 0;
-            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kb, vb, (int)nq, 0, 30, q.sm));
-            void* tmp = gbuf<char>(c, gi, BG_STMP, tb, st);
+            uint32_t* keys = gbuf<uint32_t>(c, gi, BG_SK0, nq, st);
+            uint32_t* order = gbuf<uint32_t>(c, gi, BG_SV0, nq, st);
+            uint32_t* ws = gbuf<uint32_t>(c, gi, BG_STMP, RS_WORDS, st);
             if (st) return st;
-            k_sort_keys_slots<<<ceil_div(ub, BLOCK), BLOCK, 0, q.sm>>>(qa, q.S.ro, q.S.rd, q.S.counts, ub, c.sort_lo,
-                                                                         c.sort_scale, sk0, sv0, walk_sort);
-            HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kb, vb, (int)ub, 0, 30, q.sm));
-            qa = reinterpret_cast<int32_t*>(vb.Current());
+            if (!q.sort_ws_zeroed) {
+                HIPCHK(hipMemsetAsync(ws, 0, sizeof(uint32_t) * RS_WORDS, q.sm));
+                q.sort_ws_zeroed = true;
+            }
+            const int g = ceil_div(ub, RS_BLOCK);
+            k_rsort_keys_slots<<<g, RS_BLOCK, 0, q.sm>>>(qa, q.S.ro, q.S.rd, q.S.counts, ub, c.sort_lo, c.sort_scale,
+                                                         walk_sort, keys, ws);
+            k_rsort_scatter_slots<<<g, RS_BLOCK, 0, q.sm>>>(qa, keys, q.S.counts, ub, ws, order);
+            c.stats.sorted_bounces += 1;
+            qa = reinterpret_cast<int32_t*>(order);
         }
         if (skip > 0) {
             StageTimer tm(c, c.o.timing, ST_RESOLVE, q.sm);
@@ -2007,11 +2012,9 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
         for (int k = 0; k < 2; ++k) {
             uint32_t* cnt = k == 0 ? q.I.n_a : q.I.n_b;
             uint32_t* off = k == 0 ? q.I.off_a : q.I.off_b;
-            size_t tmp_bytes = 0;
-            HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, q.n, q.sm));
-            void* tmp = gbuf<char>(c, gi, BG_SCAN, tmp_bytes, st);
+            uint32_t* sums = gbuf<uint32_t>(c, gi, BG_SCAN, (size_t)scan_blocks(q.n), st);
             if (st) return st;
-            HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, q.n, q.sm));
+            HIPCHK(exclusive_scan(cnt, off, q.n, sums, q.sm));
         }
         k_bdpt_total<<<1, 64, 0, q.sm>>>(q.I, q.n, q.totals);
         HIPCHK(hipMemcpyAsync(c.bd_totals_h + 2 * gi, q.totals, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, q.sm));  // (a), (b)
@@ -2105,11 +2108,9 @@ lumo_status render_bdpt_groups(Ctx& c, Paths& S, const Tasks& T, const Bdpt& B, 
             uint32_t* off = tap_off + q.s0;
             k_bdpt_taps<0><<<ceil_div(q.n, BLOCK), BLOCK, 0, q.sm>>>(c.sc, q.S, q.B, q.R, c.cam, q.n, c.tone_map,
                                                                       c.tone_arg, cnt, nullptr, nullptr, nullptr);
-            size_t tmp_bytes = 0;
-            HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, q.n, q.sm));
-            void* tmp = gbuf<char>(c, gi, BG_SCAN, tmp_bytes, st);
+            uint32_t* sums = gbuf<uint32_t>(c, gi, BG_SCAN, (size_t)scan_blocks(q.n), st);
             if (st) return st;
-            HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, q.n, q.sm));
+            HIPCHK(exclusive_scan(cnt, off, q.n, sums, q.sm));
             const int ntg = q.t1 - q.t0;
             uint64_t* ranges = gbuf<uint64_t>(c, gi, BG_RANGES, (size_t)ntg + 1, st);
             if (st) return st;
@@ -2573,11 +2574,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             for (int k = 0; k < 2; ++k) {
                 uint32_t* cnt = k == 0 ? BI.n_a : BI.n_b;
                 uint32_t* off = k == 0 ? BI.off_a : BI.off_b;
-                size_t tmp_bytes = 0;
-                HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, N, sm));
-                void* tmp = wbuf<char>(c, W_BD_SCAN, tmp_bytes, st);
+                uint32_t* sums = wbuf<uint32_t>(c, W_BD_SCAN, (size_t)scan_blocks(N), st);
                 if (st) return st;
-                HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, N, sm));
+                HIPCHK(exclusive_scan(cnt, off, N, sums, sm));
             }
             k_bdpt_total<<<1, 64, 0, sm>>>(BI, N, items_total);
             uint32_t totals[2] = {0, 0};
@@ -2664,11 +2663,9 @@ lumo_status render_impl(Ctx& c, const lumo_tile_task* tasks, size_t n_tasks, lum
             // order, pixels in order within a task), write, then append per task on the host
             k_bdpt_taps<0><<<gN, BLOCK, 0, sm>>>(c.sc, S, B, BR, c.cam, N, c.tone_map, c.tone_arg, tap_cnt, nullptr, nullptr,
                                                  nullptr);
-            size_t tmp_bytes = 0;
-            HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, tap_cnt, tap_off, N, sm));
-            void* tmp = wbuf<char>(c, W_BD_SCAN, tmp_bytes, st);
+            uint32_t* sums = wbuf<uint32_t>(c, W_BD_SCAN, (size_t)scan_blocks(N), st);
             if (st) return st;
-            HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, tap_cnt, tap_off, N, sm));
+            HIPCHK(exclusive_scan(tap_cnt, tap_off, N, sums, sm));
             k_task_tap_ranges<<<ceil_div(n_tasks + 1, BLOCK), BLOCK, 0, sm>>>(T, tap_cnt, tap_off, (int)n_tasks, N,
                                                                               tap_ranges);
             HIPCHK(hipMemcpyAsync(ranges_h.data(), tap_ranges, sizeof(uint64_t) * (n_tasks + 1), hipMemcpyDeviceToHost, sm));
@@ -3123,13 +3120,15 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
         if (x && !st) st = x;
     };
     chk(upload(*c, d->vertices, (size_t)3 * d->num_vertices, &s.vertices));
+    c->sort_lo = V3{0.0, 0.0, 0.0};  // no world box: every origin in cell 0 (the octant still sorts)
+    c->sort_scale = V3{0.0, 0.0, 0.0};
     if (d->num_object_nodes > 0 && d->object_nodes) {  // ray sorting's cells: the objects BVH's world box
         const lumo_bvh_node& r = d->object_nodes[0];
         double lo[3], sc3[3];
         for (int a = 0; a < 3; ++a) {
             lo[a] = r.bmin[a];
             const double ext = r.bmax[a] - r.bmin[a];
-            sc3[a] = ext > 0.0 && std::isfinite(ext) ? 512.0 / ext : 0.0;
+            sc3[a] = ext > 0.0 && std::isfinite(ext) ? 8.0 / ext : 0.0;  // 8 cells per axis (scan.h rs_key)
         }
         c->sort_lo = V3{lo[0], lo[1], lo[2]};
         c->sort_scale = V3{sc3[0], sc3[1], sc3[2]};
@@ -3755,6 +3754,23 @@ lumo_status lumo_debug_stream(void* ctx, size_t n) {
     k_calib_read8<<<2048, BLOCK, 0, c->stream>>>(buf, n, buf + n);
     k_calib_write8<<<2048, BLOCK, 0, c->stream>>>(buf, n);
     const hipError_t e = hipStreamSynchronize(c->stream);
+    (void)hipFree(buf);
+    HIPCHK(e);
+    return LUMO_OK;
+}
+
+// Diagnostics: the device exclusive scan (scan.h) of n host uint32 counts into out (host).
+lumo_status lumo_debug_scan(void* ctx, const uint32_t* in, uint32_t* out, size_t n) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !in || !out || n == 0 || n > 0xffffffffu) return LUMO_ERR_INVALID;
+    HIPCHK(hipSetDevice(c->device));
+    uint32_t* buf = nullptr;
+    const size_t nb = (size_t)scan_blocks((uint32_t)n);
+    HIPCHK(hipMalloc(&buf, sizeof(uint32_t) * (2 * n + nb)));
+    hipError_t e = hipMemcpyAsync(buf, in, sizeof(uint32_t) * n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = exclusive_scan(buf, buf + n, (uint32_t)n, buf + 2 * n, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, buf + n, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(buf);
     HIPCHK(e);
     return LUMO_OK;

@@ -119,10 +119,8 @@ struct HitQ {
     double* t;
     int32_t* i;  // kind, object, triangle planes
     size_t cap;
-    const uint32_t* perm;
-    uint32_t *sk[2], *sv[2];
-    void* tmp;  // the sort's temporary storage (tmp_bytes)
-    size_t tmp_bytes;
+    const uint32_t* perm;  // walk order of the queue positions (ray sorting), or null
+    uint32_t *keys, *order, *ws;  // ray sorting: keys, the sorted order, the counting sort's workspace
 };
 // NEE records in queue order: per path with shadow rays a header (gathered, wavelengths, radiance
 // of a path that ends this bounce, slot, next-queue position or -1), and per light sample i the

@@ -52,13 +52,15 @@ class TileQueue:
     fresh generation number from the store and broadcasts it (one small collective per render,
     off the data path), so a rank that built more or fewer queues before (a preview render, a
     retry) cannot pair up with another render's queue.  When the iteration over a queue ends,
-    every rank adds the tiles it took to a per-key total and, after a barrier, checks that
-    the total is the frame's tile count (`verify`), so a lost or doubled tile raises instead of
-    silently changing the reduced film.  `key=` skips both and needs no process group (a bare
+    every rank adds the tiles it took to a per-key total and, once every rank has reported (a
+    count in the store, polled), checks that the total is the frame's tile count (`verify`), so a
+    lost or doubled tile raises instead of silently changing the reduced film.  `key=` skips both and needs no process group (a bare
     store, single-process use); without `key=` the queue needs an initialised torch.distributed
     process group even when `store=` is given.  The coverage check waits on the store with a
-    deadline (`timeout` seconds) rather than in a barrier, so a rank that failed mid-render turns
-    into an error on the others instead of a hang until the backend's timeout.
+    deadline rather than in a barrier, so a rank that failed mid-render turns into an error on the
+    others instead of a hang.  The deadline (`timeout` seconds after this rank's last chunk)
+    defaults to the store's own timeout, the process group's (30 min unless configured), because a
+    healthy rank may still be rendering its last chunk long after a fast one finished.
 
     `chunk` defaults to half of one rank's static share: every claim is one more render call with
     fewer paths in flight and its own pipeline fill and drain (C1 1024² @ 64 spp, two ranks on one
@@ -66,12 +68,15 @@ class TileQueue:
     so claims stay few and large."""
 
     def __init__(self, width, height, world_size, chunk=None, store=None, key=None, group=None,
-                 timeout=300.0):
+                 timeout=None):
         self.collective = key is None
-        self.timeout = float(timeout)
         if store is None:
             import torch.distributed as dist
             store = dist.distributed_c10d._get_default_store()
+        if timeout is None:  # the store's timeout (the process group's), else c10d's default 30 min
+            t = getattr(store, "timeout", None)
+            timeout = t.total_seconds() if hasattr(t, "total_seconds") else 1800.0
+        self.timeout = float(timeout)
         self.n_tiles = tiles_per_batch(width, height)
         if chunk is None:
             chunk = max(1, self.n_tiles // (2 * max(1, world_size)))

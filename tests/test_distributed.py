@@ -290,3 +290,17 @@ def test_tile_queue_failed_rank_raises_not_hangs(tmp_path):
     r0 = np.load(tmp_path / "failed0.npy")
     assert bool(r0[0]) and r0[1] < 30
     assert "1 of 2 ranks" in (tmp_path / "msg0.txt").read_text()
+
+
+def test_tile_queue_default_deadline_is_the_store_timeout():
+    """The coverage check's deadline defaults to the store's own timeout (the process group's), not
+    a fixed 300 s that a healthy slow rank could exceed (advisor, round 5)."""
+    from datetime import timedelta
+
+    import torch.distributed as dist
+    from lumo_amd.dist import TileQueue
+    s = dist.HashStore()
+    s.set_timeout(timedelta(seconds=1234))
+    q = TileQueue(64, 64, 2, store=s, key="lumo_amd/test/deadline")
+    assert q.timeout == 1234.0
+    assert TileQueue(64, 64, 2, store=s, key="lumo_amd/test/deadline2", timeout=7).timeout == 7.0

@@ -260,7 +260,7 @@ def test_bdpt_task_groups(groups, film):
 @pytest.mark.parametrize("mode", [1, 2])
 def test_bdpt_walk_ray_sort(mode):
     """Ray sorting of the BDPT walks (option ray_sort 1 / 2 in the task-group path): each walk
-    bounce's queue of slot ids is radix-sorted by its rays' direction octant and origin cell before
+    bounce's queue of slot ids is counting-sorted (scan.h) by its rays' direction octant and origin cell before
     the closest hits and steps, which changes only the lane order; caustics.rs at 384x256 (49 k
     slots per group, above the sort minimum), 1 pass: tiles, counts and splats equal the oracle's."""
     sc, cam = _scene("caustics", (384, 256))
@@ -272,6 +272,7 @@ def test_bdpt_walk_ray_sort(mode):
         sp = []
         bufs, rr = d.render_tasks(tasks, integrator=BDPT, splats_out=sp)
         assert d.last_schedule().schedule == 3
+        assert d.stats().sorted_bounces > 0  # the sorted walk ran
     finally:
         d.close()
     osp = []

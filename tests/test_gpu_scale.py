@@ -375,10 +375,11 @@ def test_c3_share_merged_passes(c3):
 
 @pytest.mark.parametrize("scene", ["dragon", "bistro"])
 def test_ray_sort_matches_oracle(mid_bistro, scene):
-    """Ray sorting (option ray_sort): each bounce's closest-hit rays are radix-sorted by direction
-    octant and origin cell and walked in that order; the hits land at the rays' own queue positions,
-    so tiles, ray and query counts equal the oracle's (kdtree.rs:101-169, bvh.rs:315-362: the walks
-    themselves are unchanged)."""
+    """Ray sorting (option ray_sort): each bounce's closest-hit rays are counting-sorted by direction
+    octant and origin cell (scan.h, 12-bit keys) and walked in that order; the hits land at the rays'
+    own queue positions, so tiles, ray and query counts equal the oracle's (kdtree.rs:101-169,
+    bvh.rs:315-362: the walks themselves are unchanged).  lumo_stats.sorted_bounces shows that the
+    sorted walk ran."""
     if scene == "bistro":
         sc, cam = mid_bistro, scenes.bistro_camera((256, 192))
     else:
@@ -399,6 +400,7 @@ def test_ray_sort_matches_oracle(mid_bistro, scene):
         assert (r.num_rays, r.num_queries) == (orr.num_rays, orr.num_queries)
     assert after.closest_queries - before.closest_queries == cnt.closest_queries
     assert after.shadow_queries - before.shadow_queries == cnt.shadow_queries
+    assert after.sorted_bounces - before.sorted_bounces > 0
 
 
 def test_c3_bench_schedule_full_frame(c3):

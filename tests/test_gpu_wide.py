@@ -195,3 +195,39 @@ def test_default_accel_is_lumo():
         assert d.scene_info().accel == 0 and d.scene_info().stack_class == 4
     finally:
         d.close()
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_wide_ray_sort_matches_oracle(mode):
+    """The counting sort (scan.h) of each bounce's closest-hit rays ahead of the wide walks: only
+    the lane order changes, so the small dragon's tiles and counts equal the oracle's."""
+    sc = scenes.dragon(torus_knot_tube(300, 12)).build()
+    cam = scenes.default_camera((256, 192))
+    d = L.Device(0, accel=1, ray_sort=mode)
+    try:
+        d.upload(sc, cam)
+        tasks = L.make_tasks(256, 192, 2, SEED)
+        bufs, res = d.render_tasks(tasks)
+        assert d.stats().sorted_bounces > 0
+    finally:
+        d.close()
+    obufs, ores, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, oracle_threads(), accel=1)
+    _tiles_cmp(bufs, res, obufs, ores)
+
+
+@pytest.mark.parametrize("n", [1, 2047, 2048, 2049, 5_000_001])
+def test_device_exclusive_scan(n):
+    """The hand-written exclusive scan (scan.h, two launches) that replaced the library scan of the
+    BDPT item lists and splat taps, at sizes around its 2 048-count tile and across ~2 400 tiles."""
+    import ctypes as C
+    rng = np.random.default_rng(n)
+    a = rng.integers(0, 40, size=n).astype(np.uint32)
+    out = np.zeros(n, dtype=np.uint32)
+    d = L.Device(0)
+    try:
+        _ffi.check(_ffi.load().lumo_debug_scan(d.ctx, a.ctypes.data_as(_ffi.c_uint32_p),
+                                                out.ctypes.data_as(_ffi.c_uint32_p), C.c_size_t(n)), "debug_scan")
+    finally:
+        d.close()
+    want = np.concatenate([[0], np.cumsum(a, dtype=np.uint64)[:-1]]).astype(np.uint32)
+    np.testing.assert_array_equal(out, want)

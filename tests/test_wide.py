@@ -170,3 +170,56 @@ def test_wide_matches_lumo_except_kd_misses(name):
     o, dirs, li = _visibility_rays(d, 1 << 15, 22)
     a, b, same = _compare(d, o, dirs, li)
     assert (~same).mean() <= BOUND, (~same).mean()
+
+
+def _image(bufs, tasks, W, H):
+    f = L.Film(W, H)
+    for t, b in zip(tasks, bufs):
+        f.add_tile(t, b)
+    return f.rgb()
+
+
+def _tile_diffs(A, B):
+    """Per 16x16 tile and channel, the mean of A - B.  lumo's film clips every sample's filter to
+    its own tile (tile.rs:74-83), so tiles are independent estimates: their spread gives the
+    standard error of the mean difference."""
+    H, W, _ = A.shape
+    return (A - B).reshape(H // 16, 16, W // 16, 16, 3).mean(axis=(1, 3)).reshape(-1, 3)
+
+
+def test_wide_image_matches_lumo_cornell():
+    """C0 (Cornell 256^2 @ 16) rendered by the oracle on both structures with the same sample
+    streams (wavefront order, 2 seeds), so the images differ only by the paths the two walks send
+    apart.  The light is coplanar with the ceiling (cornell_box.rs:48-60): where a ray's t on the
+    light is an ulp below its t on the ceiling, the wide walk returns the light (scene.rs's rule: a
+    light in front of the object), while lumo's kd walk of the light's flat box clips that hit and
+    returns the ceiling.  Tolerances: the frame's per-channel mean within 3 % (the
+    wide image is ~1.7 % brighter, from the tiles that show the light), the other tiles' mean within
+    0.1 % (measured ~0.005 %, the BSDF-sampled rays that reach the light)."""
+    sc = L.Scene.cornell_box()
+    cam = L.Camera.cornell_box((256, 256))
+    for seed in (1, 2):
+        tasks = L.make_tasks(256, 256, 16, seed)
+        a, _, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+        b, _, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8, accel=1)
+        A, B = _image(a, tasks, 256, 256), _image(b, tasks, 256, 256)
+        light = (np.maximum(A, B).reshape(16, 16, 16, 16, 3).max(axis=(1, 3, 4)) > 10.0).reshape(-1)
+        assert 0 < light.sum() < 40
+        rel = np.abs(B.mean(axis=(0, 1)) - A.mean(axis=(0, 1))) / A.mean(axis=(0, 1))
+        assert np.all(rel < 0.03), rel
+        ta = A.reshape(16, 16, 16, 16, 3).mean(axis=(1, 3)).reshape(-1, 3)[~light].mean(0)
+        tb = B.reshape(16, 16, 16, 16, 3).mean(axis=(1, 3)).reshape(-1, 3)[~light].mean(0)
+        assert np.all(np.abs(tb - ta) / ta < 1e-3), (ta, tb)
+
+
+def test_wide_image_matches_lumo_bistro():
+    """The C3 scene (Bistro stand-in, full size) at 96 x 64 @ 8 spp, paired as above (no coplanar
+    emitters: the lamps sit 0.02 in front of the facades): per-channel means within 0.1 %."""
+    sc = scenes.bistro().build()
+    cam = scenes.bistro_camera((96, 64))
+    tasks = L.make_tasks(96, 64, 8, 3)
+    a, _, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8)
+    b, _, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8, accel=1)
+    A, B = _image(a, tasks, 96, 64), _image(b, tasks, 96, 64)
+    ma, mb = A.mean(axis=(0, 1)), B.mean(axis=(0, 1))
+    assert np.all(np.abs(mb - ma) / ma < 1e-3), (ma, mb)
