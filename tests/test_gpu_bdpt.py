@@ -265,7 +265,7 @@ def test_bdpt_walk_ray_sort(mode):
     slots per group, above the sort minimum), 1 pass: tiles, counts and splats equal the oracle's."""
     sc, cam = _scene("caustics", (384, 256))
     sc.build()
-    d = L.Device(0, ray_sort=mode)
+    d = L.Device(0, ray_sort=mode, bdpt_tail=0)  # no walk tail: every bounce through k_closest (sorted)
     try:
         d.upload(sc, cam)
         tasks = L.make_tasks(384, 256, 1, 0x50A7)

@@ -385,7 +385,9 @@ def test_ray_sort_matches_oracle(mid_bistro, scene):
     else:
         sc = scenes.dragon(torus_knot_tube(300, 12)).build()
         cam = scenes.default_camera((256, 192))
-    d = L.Device(0, ray_sort=1)
+    # no tail kernel (every bounce walks through k_closest_q) and one task group (49 k rays per bounce,
+    # above the sort minimum of 32 k)
+    d = L.Device(0, ray_sort=1, tail_below=0, split_groups=1)
     try:
         d.upload(sc, cam)
         tasks = L.make_tasks(256, 192, 2, SEED)  # 49 k slots per pass: bounces above the sort minimum

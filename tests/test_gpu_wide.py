@@ -203,7 +203,7 @@ def test_wide_ray_sort_matches_oracle(mode):
     the lane order changes, so the small dragon's tiles and counts equal the oracle's."""
     sc = scenes.dragon(torus_knot_tube(300, 12)).build()
     cam = scenes.default_camera((256, 192))
-    d = L.Device(0, accel=1, ray_sort=mode)
+    d = L.Device(0, accel=1, ray_sort=mode, tail_below=0, split_groups=1)
     try:
         d.upload(sc, cam)
         tasks = L.make_tasks(256, 192, 2, SEED)
