@@ -15,6 +15,7 @@ struct Accel {
     std::vector<int32_t> light_blas;    // per light
     int max_stack = 0;                  // deepest walk stack the trees can need
     int depth = 0;                      // deepest node level
+    float max_abs = 0.0f;               // the largest |coordinate| of any child box (the f32 box test's bound)
     bool ok = false;
 };
 

@@ -435,6 +435,9 @@ Accel build(const lumo_scene_desc& d) {
                 acc.depth = std::max(acc.depth, it.level + 1);
             }
         }
+        for (int k = 0; k < nk; ++k)
+            for (int a = 0; a < 3; ++a)
+                acc.max_abs = std::max(acc.max_abs, std::max(std::fabs(nd.lo[a][k]), std::fabs(nd.hi[a][k])));
         acc.nodes[it.node] = nd;
         if (acc.nodes.size() >= (size_t)INT32_MAX / 2) ok = false;
     }

@@ -135,6 +135,7 @@ struct DScene {
     // (A, B, C, (tri, obj)), the root refs of the world objects / lights trees, and per object /
     // light the BLAS root of an instance.  The walks then run with stack class 0 (by_stack_class).
     int32_t accel, w_oroot, w_lroot, wn_lds;  // wn_lds: nodes below it are read from wnodes_lds (TOP view)
+    double w_maxabs;  // the largest |box coordinate| of the wide trees (Accel::max_abs, rayw)
     const wbvh::Node* wnodes;
     const double* wtv;
     const int32_t* w_oblas;
@@ -1068,14 +1069,16 @@ __device__ __forceinline__ void wnode_load(const DScene& sc, int32_t i, wbvh::No
 }
 
 // The box test of the wide walks runs in f32 and is conservative: it never rejects a box that the
-// ray's f64 segment [t_min, t_max] enters (the boxes are rounded outward at the build, so no
-// triangle test that would accept a hit is skipped).  Per ray: the origin and 1 / dir rounded to
-// f32, and per axis the t error the origin's rounding causes, e = |o - o32| |1/d| (rounded up).  A
-// slab value T = (p - o32) * inv32 (two roundings, plus those of 1/d and inv32) is within
-// |T| 2^-21 + e of the exact one, so each axis interval is widened by e and the box interval by
-// 2^-21 of its ends.  An axis with |1/d| > 1e30 does not cull (inv32 = 0, e = inf).
+// ray's f64 segment [t_min, t_max] (t_min >= 0) enters, so no triangle test that would accept a hit
+// is skipped (the boxes are rounded outward at the build).  A slab value is one f32 FMA,
+// T = fma(p, inv32, c) with c = -o / d: inv32 = 1/d rounded to f32 and, per ray and axis, c
+// rounded down (c_lo, for the plane a slab is entered through when 1/d >= 0) or up (c_hi), each
+// moved by E = (M + |o|) |1/d| 2^-23, which bounds the error of inv32's and c's roundings for any
+// plane |p| <= M (wbvh Accel::max_abs, the largest box coordinate of the scene).  The box interval
+// is then widened by 2^-21 of its ends (the FMA's own rounding).  An axis where that bound is not
+// finite in f32 (the ray parallel to it, |1/d| huge) does not cull: inv32 = 0, c = -inf / +inf.
 struct RayW {
-    float o[3], inv[3], e[3];
+    float inv[3], clo[3], chi[3];
 };
 __device__ __forceinline__ float f32_up(double x) {
     const float f = (float)x;
@@ -1085,23 +1088,27 @@ __device__ __forceinline__ float f32_down(double x) {
     const float f = (float)x;
     return (double)f > x ? nextafterf(f, -__builtin_huge_valf()) : f;
 }
-__device__ __forceinline__ RayW rayw(const RayX& r) {
+__device__ __forceinline__ RayW rayw(const RayX& r, double M) {
     RayW w;
     const double o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        w.o[a] = (float)o[a];
-        if (fabs(inv[a]) <= 1e30) {
+        const double e = (M + fabs(o[a])) * fabs(inv[a]);
+        if (e <= 1e36) {
             w.inv[a] = (float)inv[a];
-            w.e[a] = f32_up(fabs(o[a] - (double)w.o[a]) * fabs(inv[a]) * (1.0 + 0x1p-20));
+            const double c = -(o[a] * inv[a]), E = e * 0x1p-23;
+            const float lo = f32_down(c - E), hi = f32_up(c + E);
+            w.clo[a] = inv[a] >= 0.0 ? lo : hi;  // the lo plane's constant: entry side when 1/d >= 0
+            w.chi[a] = inv[a] >= 0.0 ? hi : lo;
         } else {
             w.inv[a] = 0.0f;
-            w.e[a] = __builtin_huge_valf();
+            w.clo[a] = -__builtin_huge_valf();
+            w.chi[a] = __builtin_huge_valf();
         }
     }
     return w;
 }
-constexpr float WREL = 0x1p-21f;
+constexpr float WREL_LO = 1.0f - 0x1p-21f, WREL_HI = 1.0f + 0x1p-21f;
 #ifndef LUMO_WIDE_ANY_SORT  // any-hit walks: children nearest first (1) or hits in node order (0: C3 8-spp 494 -> 461 ms)
 #define LUMO_WIDE_ANY_SORT 0
 #endif
@@ -1111,16 +1118,14 @@ __device__ __forceinline__ bool wslab32(const wbvh::Node& nd, int i, const RayW&
     float ts, te;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const float t0 = (nd.lo[a][i] - w.o[a]) * w.inv[a];
-        const float t1 = (nd.hi[a][i] - w.o[a]) * w.inv[a];
-        const float lo = fminf(t0, t1) - w.e[a], hi = fmaxf(t0, t1) + w.e[a];
+        const float t0 = fmaf(nd.lo[a][i], w.inv[a], w.clo[a]);
+        const float t1 = fmaf(nd.hi[a][i], w.inv[a], w.chi[a]);
+        const float lo = fminf(t0, t1), hi = fmaxf(t0, t1);
         ts = a == 0 ? lo : fmaxf(ts, lo);
         te = a == 0 ? hi : fminf(te, hi);
     }
-    ts = ts - fabsf(ts) * WREL;
-    te = te + fabsf(te) * WREL;
-    k = fmaxf(ts, tmin);
-    return k <= fminf(te, tmax);
+    k = fmaxf(ts * WREL_LO, tmin);  // ts < 0 only matters through tmin >= 0
+    return k <= fminf(te * WREL_HI, tmax);
 }
 
 // compare-exchange of the child sort: hits before misses, hits by entry (a swap only when strictly
@@ -1175,7 +1180,8 @@ __device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, cons
         top_t = t;
     };
     RayX r = rw;
-    RayW w = rayw(rw);
+    const double wM = sc.w_maxabs;
+    RayW w = rayw(rw, wM);
     const float tmin32 = f32_down(t_min);
     float tmax32 = f32_up(t_max);
     int inst = -1;
@@ -1196,7 +1202,7 @@ __device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, cons
             }
             if (FX && x == wbvh::MARK) {  // leave the instance
                 r = rw;
-                w = rayw(rw);
+                w = rayw(rw, wM);
                 inst = -1;
                 continue;
             }
@@ -1255,7 +1261,7 @@ __device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, cons
             } else {
                 push(wbvh::MARK, -__builtin_huge_valf());
                 r = ray_local(sc.xforms[ob.xform()], rw);
-                w = rayw(r);
+                w = rayw(r, wM);
                 inst = first;
                 cur = blas[first];
                 continue;

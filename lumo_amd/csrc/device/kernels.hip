@@ -3342,6 +3342,7 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
     s.wtv = nullptr;
     s.w_oblas = s.w_lblas = nullptr;
     s.wn_lds = s.top_wnodes = 0;
+    s.w_maxabs = 0.0;
     s.off_top_wnodes = 0;
     s.off_wnodes = s.off_wtv = s.off_woblas = s.off_wlblas = 0;
     c->w_nodes = c->w_tris = c->w_stack = c->w_depth = 0;
@@ -3351,6 +3352,7 @@ lumo_status lumo_scene_upload(void* ctx, const lumo_scene_desc* d) {
             s.accel = 1;
             s.w_oroot = acc.obj_root;
             s.w_lroot = acc.light_root;
+            s.w_maxabs = (double)acc.max_abs;
             chk(upload(*c, acc.nodes.data(), acc.nodes.size(), &s.wnodes));
             chk(upload(*c, acc.tv.data(), acc.tv.size(), &s.wtv));
             chk(upload(*c, acc.obj_blas.data(), acc.obj_blas.size(), &s.w_oblas));

@@ -794,11 +794,13 @@ struct WChild {
     int32_t ref;
     bool hit;
 };
-// The wide walk's conservative f32 box test (lumo_amd dscene.h wslab32): per ray the
-// origin and 1/dir in f32 and per axis e = |o - o32| |1/d| rounded up (an axis with |1/d| > 1e30
-// does not cull); each axis interval widened by e, the box interval by 2^-21 of its ends.
+// The wide walk's conservative f32 box test (lumo_amd dscene.h wslab32): a slab value
+// is fma(p, inv32, c) with inv32 = 1/d in f32 and c = -o/d rounded down or up by
+// E = (M + |o|) |1/d| 2^-23 (M: the largest box coordinate), the rounded-down constant on the plane
+// a slab is entered through; the box interval widened by 2^-21 of its ends; an axis whose bound
+// exceeds 1e36 does not cull (inv32 = 0, constants -inf / +inf).
 struct WRay {
-    float o[3], inv[3], e[3];
+    float inv[3], clo[3], chi[3];
 };
 float f32_up(double x) {
     const float f = (float)x;
@@ -808,34 +810,37 @@ float f32_down(double x) {
     const float f = (float)x;
     return (double)f > x ? std::nextafter(f, -HUGE_VALF) : f;
 }
-WRay wray_of(const Ray& r) {
+WRay wray_of(const Ray& r, double M) {
     WRay w;
     const V3 inv = 1.0 / r.dir;
     const double o[3] = {r.origin.x, r.origin.y, r.origin.z}, iv[3] = {inv.x, inv.y, inv.z};
     for (int a = 0; a < 3; ++a) {
-        w.o[a] = (float)o[a];
-        if (std::fabs(iv[a]) <= 1e30) {
+        const double e = (M + std::fabs(o[a])) * std::fabs(iv[a]);
+        if (e <= 1e36) {
             w.inv[a] = (float)iv[a];
-            w.e[a] = f32_up(std::fabs(o[a] - (double)w.o[a]) * std::fabs(iv[a]) * (1.0 + 0x1p-20));
+            const double c = -(o[a] * iv[a]), E = e * 0x1p-23;
+            const float lo = f32_down(c - E), hi = f32_up(c + E);
+            w.clo[a] = iv[a] >= 0.0 ? lo : hi;
+            w.chi[a] = iv[a] >= 0.0 ? hi : lo;
         } else {
             w.inv[a] = 0.0f;
-            w.e[a] = HUGE_VALF;
+            w.clo[a] = -HUGE_VALF;
+            w.chi[a] = HUGE_VALF;
         }
     }
     return w;
 }
 bool wide_box(const wbvh::Node& nd, int i, const WRay& w, float tmin, float tmax, float* k) {
-    float ts = -HUGE_VALF, te = HUGE_VALF;
+    float ts = 0.0f, te = 0.0f;
     for (int a = 0; a < 3; ++a) {
-        const float t0 = (nd.lo[a][i] - w.o[a]) * w.inv[a];
-        const float t1 = (nd.hi[a][i] - w.o[a]) * w.inv[a];
-        ts = std::fmax(ts, std::fmin(t0, t1) - w.e[a]);
-        te = std::fmin(te, std::fmax(t0, t1) + w.e[a]);
+        const float t0 = std::fma(nd.lo[a][i], w.inv[a], w.clo[a]);
+        const float t1 = std::fma(nd.hi[a][i], w.inv[a], w.chi[a]);
+        const float lo = std::fmin(t0, t1), hi = std::fmax(t0, t1);
+        ts = a == 0 ? lo : std::fmax(ts, lo);
+        te = a == 0 ? hi : std::fmin(te, hi);
     }
-    ts = ts - std::fabs(ts) * 0x1p-21f;
-    te = te + std::fabs(te) * 0x1p-21f;
-    *k = std::fmax(ts, tmin);
-    return *k <= std::fmin(te, tmax);
+    *k = std::fmax(ts * (1.0f - 0x1p-21f), tmin);
+    return *k <= std::fmin(te * (1.0f + 0x1p-21f), tmax);
 }
 // hits first, then (by_t) hits by entry t; a swap only when strictly out of order.  Closest walks
 // sort by entry; any-hit walks only move the hits ahead (their order is irrelevant to the answer).
@@ -853,7 +858,8 @@ WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std
     } st[wbvh::STACK];
     int sp = 0;
     Ray r = rw;
-    WRay w = wray_of(r);
+    const double wM = (double)W.max_abs;
+    WRay w = wray_of(r, wM);
     const float tmin32 = f32_down(t_min);
     float tmax32 = f32_up(t_max);
     int inst = -1;
@@ -863,7 +869,7 @@ WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std
             const Entry e = st[--sp];
             if (e.ref == wbvh::MARK) {
                 r = rw;
-                w = wray_of(r);
+                w = wray_of(r, wM);
                 inst = -1;
                 continue;
             }
@@ -911,7 +917,7 @@ WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std
             } else {
                 st[sp++] = Entry{wbvh::MARK, -HUGE_VALF};
                 r = ray_to_local(xform_of(sc.d->transforms[ob.xform]), rw, false);
-                w = wray_of(r);
+                w = wray_of(r, wM);
                 inst = first;
                 cur = blas[first];
                 continue;
