@@ -557,10 +557,13 @@ __device__ bool bdpt_visible(const DScene& sc, const BVtx& a, const BVtx& b, Cou
     if constexpr (STK == 0) {
         // wide accel: Scene::hit_t as the closest hit_t (lumo's any-hit walk returns the first object
         // its BVH order finds, which has no counterpart in another structure).  Hits
-        // beyond dist + 2 EPSILON fail the test either way, so the walks are capped there.
+        // beyond dist + 2 EPSILON fail the test either way, so the walks are capped there; a hit
+        // below dist - 2 EPSILON decides it too (the closest t is below it), so the walks stop there.
         const double dist = sqrt(rmax(distance_squared(xo, xi), 0.0));
-        t = wide_walk<false, FX, TOP>(sc, sc.w_oroot, sc.tobjs, sc.w_oblas, rx, 0.0, dist + 2.0 * EPSILON, C).t;
-        t = rmin(t, wide_walk<false, FX, TOP>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, rx, 0.0, t, C).t);
+        const double stop = dist - 2.0 * EPSILON;
+        t = wide_walk<false, FX, TOP>(sc, sc.w_oroot, sc.tobjs, sc.w_oblas, rx, 0.0, dist + 2.0 * EPSILON, C, stop).t;
+        if (t < stop) return false;
+        t = rmin(t, wide_walk<false, FX, TOP>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, rx, 0.0, t, C, stop).t);
         return fabs(dist - t) < EPSILON;
     } else {
     t = rmin(t, bvh_hit_t<STK, FX, TOP>(sc, sc.onodes, sc.n_onodes, sc.oitems, sc.tobjs, rx, 0.0, t, C, sc.onodes_lds,

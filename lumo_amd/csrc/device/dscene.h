@@ -1156,9 +1156,20 @@ __device__ __forceinline__ void wcx(float& ka, int32_t& ra, bool& ha, float& kb,
 // marker and walks its BLAS with the ray in the instance's space (Ray::transform, ray.rs:24-31: the
 // same t parametrises both), the marker's pop restores the world ray.
 // Counters: aabb = child boxes tested, kd = nodes visited, tri = triangles tested.
+#ifndef LUMO_WIDE_NOINLINE  // the walk as a call (its own register budget) or inlined into each kernel
+#define LUMO_WIDE_NOINLINE 0
+#endif
+#if LUMO_WIDE_NOINLINE
+#define WIDE_INLINE __noinline__
+#else
+#define WIDE_INLINE
+#endif
+// t_stop (closest walks): return as soon as an accepted hit below it is found (BDPT visibility: any
+// hit well before the target decides the answer, bdpt_visible).
 template <bool ANY, int FX, bool TOP>
-__device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, const int32_t* blas, const RayX& rw,
-                          double t_min, double t_max, Counters& C) {
+__device__ WIDE_INLINE WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, const int32_t* blas,
+                                      const RayX& rw, double t_min, double t_max, Counters& C,
+                                      double t_stop = -DINF) {
     WHit h{t_max, -1, -1};
     if (root == wbvh::NONE) return h;
     int32_t st_ref[wbvh::STACK];
@@ -1255,7 +1266,7 @@ __device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, cons
                 DHit g;
                 if (sphere_hit<false>(ob, rl, t_min, h.t, g) && g.t < h.t) {
                     h = WHit{g.t, PRIM_SPHERE, first};
-                    if (ANY) return h;
+                    if (ANY || h.t < t_stop) return h;
                     tmax32 = f32_up(h.t);
                 }
             } else {
@@ -1274,7 +1285,7 @@ __device__ WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, cons
                 if (tri_hit_geo_at<false>(sc, tv, -1, r, t_min, h.t, g) && g.t < h.t) {
                     const int32_t* ids = reinterpret_cast<const int32_t*>(tv + 9);
                     h = WHit{g.t, ids[0], inst >= 0 ? inst : ids[1]};
-                    if (ANY) return h;
+                    if (ANY || h.t < t_stop) return h;
                     tmax32 = f32_up(h.t);
                 }
             }

@@ -847,8 +847,9 @@ bool wide_box(const wbvh::Node& nd, int i, const WRay& w, float tmin, float tmax
 void wide_cx(WChild& a, WChild& b, bool by_t) {
     if (b.hit && (!a.hit || (by_t && a.k > b.k))) std::swap(a, b);
 }
+// t_stop (closest walks): return at the first accepted hit below it (bdpt_visible's early answer)
 WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std::vector<int32_t>& blas,
-               const Ray& rw, double t_min, double t_max, bool any, Counters& C) {
+               const Ray& rw, double t_min, double t_max, bool any, Counters& C, double t_stop = -INF) {
     const wbvh::Accel& W = *sc.w;
     WRes h{t_max, -1, -1};
     if (root == wbvh::NONE) return h;
@@ -911,7 +912,7 @@ WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std
                 Hit g;
                 if (sphere_hit(ob, rl, t_min, h.t, &g) && g.t < h.t) {
                     h = WRes{g.t, PRIM_SPHERE_O, first};
-                    if (any) return h;
+                    if (any || h.t < t_stop) return h;
                     tmax32 = f32_up(h.t);
                 }
             } else {
@@ -930,7 +931,7 @@ WRes wide_walk(const Scene& sc, int32_t root, const lumo_object* objs, const std
                 const double t = triangle_hit(sc, ids[0], r, t_min, h.t, true, &g, C);
                 if (t < h.t) {
                     h = WRes{t, ids[0], inst >= 0 ? inst : ids[1]};
-                    if (any) return h;
+                    if (any || h.t < t_stop) return h;
                     tmax32 = f32_up(h.t);
                 }
             }
@@ -2144,8 +2145,10 @@ bool bdpt_visible(const Scene& sc, const Hit& h1, const Hit& h2, Counters& C) { 
     double t = INF;
     if (sc.w) {  // wide accel: Scene::hit_t as the closest hit_t, capped at dist + 2 EPSILON
         const double dist = std::sqrt(rmax(distance_squared(xo, xi), 0.0));
-        t = wide_walk(sc, sc.w->obj_root, sc.d->objects, sc.w->obj_blas, ri, 0.0, dist + 2.0 * EPSILON, false, C).t;
-        t = rmin(t, wide_walk(sc, sc.w->light_root, sc.d->lights, sc.w->light_blas, ri, 0.0, t, false, C).t);
+        const double stop = dist - 2.0 * EPSILON;  // a hit below it decides the answer: stop there
+        t = wide_walk(sc, sc.w->obj_root, sc.d->objects, sc.w->obj_blas, ri, 0.0, dist + 2.0 * EPSILON, false, C, stop).t;
+        if (t < stop) return false;
+        t = rmin(t, wide_walk(sc, sc.w->light_root, sc.d->lights, sc.w->light_blas, ri, 0.0, t, false, C, stop).t);
         return fabs(dist - t) < EPSILON;
     }
     // Scene::hit_t (scene.rs:150-162): any-hit-first over objects, then lights
