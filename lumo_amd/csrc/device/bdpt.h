@@ -1186,7 +1186,7 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_BDTRACE_WAVES) v
                 const V3 xi{X.lp.D(0, s - 1, si), X.lp.D(1, s - 1, si), X.lp.D(2, s - 1, si)};
                 Ray ri;
                 if (cam_sample_towards(cam, xi, V2{X.Dr(0, s - 2, si), X.Dr(1, s - 2, si)}, &ri))
-                    hr = scene_hit<STK, FX, LDS == 2>(sc, rayx(ri), C);
+                    hr = scene_hit<STK, FX, LDS == 2, true>(sc, rayx(ri), C);
             }
         } else if (j > (uint32_t)(Sl - 1)) {
             const int t = (int)j - Sl + 2;
@@ -1194,7 +1194,7 @@ __global__ __launch_bounds__(LDS == 2 ? TOP_BLOCK : BLOCK, LUMO_BDTRACE_WAVES) v
             if (!(cl.del || cl.light >= 0)) {
                 const int li = sample_light(sc, X.Dr(2, t - 2, si));
                 const V3 wi = light_sample_towards<FX>(sc, sc.lights[li], cl.p, V2{X.Dr(3, t - 2, si), X.Dr(4, t - 2, si)});
-                hr.tri = scene_hit_light_tri<STK, FX, LDS == 2>(sc, rayx(spawn(vtx_hit(cl), wi)), li, C);
+                hr.tri = scene_hit_light_tri<STK, FX, LDS == 2, true>(sc, rayx(spawn(vtx_hit(cl), wi)), li, C);
             }
         }
         I.a_t[q] = hr.t;

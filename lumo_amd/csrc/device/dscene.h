@@ -1156,6 +1156,29 @@ __device__ __forceinline__ void wcx(float& ka, int32_t& ra, bool& ha, float& kb,
 // marker and walks its BLAS with the ray in the instance's space (Ray::transform, ray.rs:24-31: the
 // same t parametrises both), the marker's pop restores the world ray.
 // Counters: aabb = child boxes tested, kd = nodes visited, tri = triangles tested.
+// Object leaves (spheres, instance entries) are rare next to triangle leaves.  With OC (object
+// calls) their code runs as calls, so the walk's registers are sized for its triangle loop: in
+// k_bdpt_trace_a, whose kernel holds four walks, the inlined EFloat sphere test cost 957 spilled
+// VGPRs (C4 8-spp: 112 -> 57 ms busy as calls).  The other kernels keep them inlined (as calls,
+// k_bdpt_vis 81 -> 120 ms, C3 447 -> 488 ms).
+// the sphere's accepted t (sphere.rs:27-78 with its instance transform), DINF when missed
+template <class OB>
+__device__ __forceinline__ double wide_sphere_t(const OB& ob, const lumo_transform* xforms, RayX rw, double t_min,
+                                                double t_max) {
+    const RayX rl = ob.xform() >= 0 ? ray_local(xforms[ob.xform()], rw) : rw;
+    DHit g;
+    return sphere_hit<false>(ob, rl, t_min, t_max, g) ? g.t : DINF;
+}
+template <class OB>
+__device__ __noinline__ double wide_sphere_t_call(const OB& ob, const lumo_transform* xforms, RayX rw, double t_min,
+                                                  double t_max) {
+    return wide_sphere_t(ob, xforms, rw, t_min, t_max);
+}
+// the ray in an instance's space (Ray::transform, ray.rs:24-31)
+__device__ __noinline__ RayX wide_inst_ray_call(const lumo_transform* xforms, int x, RayX rw) {
+    return ray_local(xforms[x], rw);
+}
+
 #ifndef LUMO_WIDE_NOINLINE  // the walk as a call (its own register budget) or inlined into each kernel
 #define LUMO_WIDE_NOINLINE 0
 #endif
@@ -1166,7 +1189,7 @@ __device__ __forceinline__ void wcx(float& ka, int32_t& ra, bool& ha, float& kb,
 #endif
 // t_stop (closest walks): return as soon as an accepted hit below it is found (BDPT visibility: any
 // hit well before the target decides the answer, bdpt_visible).
-template <bool ANY, int FX, bool TOP>
+template <bool ANY, int FX, bool TOP, bool OC = false>
 __device__ WIDE_INLINE WHit wide_walk(const DScene& sc, int32_t root, const DObj* objs, const int32_t* blas,
                                       const RayX& rw, double t_min, double t_max, Counters& C,
                                       double t_stop = -DINF) {
@@ -1262,16 +1285,16 @@ __device__ WIDE_INLINE WHit wide_walk(const DScene& sc, int32_t root, const DObj
         if (FX && cnt == 0) {  // object leaf: a sphere, or an instance's BLAS
             const DObj& ob = objs[first];
             if (ob.type() == LUMO_OBJ_SPHERE) {
-                const RayX rl = ob.xform() >= 0 ? ray_local(sc.xforms[ob.xform()], rw) : rw;
-                DHit g;
-                if (sphere_hit<false>(ob, rl, t_min, h.t, g) && g.t < h.t) {
-                    h = WHit{g.t, PRIM_SPHERE, first};
+                const double gt = OC ? wide_sphere_t_call(ob, sc.xforms, rw, t_min, h.t)
+                                     : wide_sphere_t(ob, sc.xforms, rw, t_min, h.t);
+                if (gt < h.t) {
+                    h = WHit{gt, PRIM_SPHERE, first};
                     if (ANY || h.t < t_stop) return h;
                     tmax32 = f32_up(h.t);
                 }
             } else {
                 push(wbvh::MARK, -__builtin_huge_valf());
-                r = ray_local(sc.xforms[ob.xform()], rw);
+                r = OC ? wide_inst_ray_call(sc.xforms, ob.xform(), rw) : ray_local(sc.xforms[ob.xform()], rw);
                 w = rayw(r, wM);
                 inst = first;
                 cur = blas[first];
@@ -1296,27 +1319,28 @@ __device__ WIDE_INLINE WHit wide_walk(const DScene& sc, int32_t root, const DObj
 
 // Scene::hit (scene.rs:119-147) on the wide trees: the objects' closest accepted hit, then the
 // lights' closest accepted hit below it.
-template <int FX, bool TOP>
+template <int FX, bool TOP, bool OC = false>
 __device__ HitRef wide_scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     HitRef h{DINF, 0, -1, -1};
-    const WHit o = wide_walk<false, FX, TOP>(sc, sc.w_oroot, sc.tobjs, sc.w_oblas, r, 0.0, DINF, C);
+    const WHit o = wide_walk<false, FX, TOP, OC>(sc, sc.w_oroot, sc.tobjs, sc.w_oblas, r, 0.0, DINF, C);
     if (o.obj >= 0) h = HitRef{o.t, 1, o.obj, o.tri};
-    const WHit l = wide_walk<false, FX, TOP>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, r, 0.0, h.t, C);
+    const WHit l = wide_walk<false, FX, TOP, OC>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, r, 0.0, h.t, C);
     if (l.obj >= 0) h = HitRef{l.t, 2, l.obj, l.tri};
     return h;
 }
 
 // Scene::hit_light's occlusion part (scene.rs:171-189) on the wide trees: any object, then any
 // light, hit below t_max.
-template <int FX, bool TOP>
+template <int FX, bool TOP, bool OC = false>
 __device__ __forceinline__ bool wide_occluded(const DScene& sc, const RayX& r, double t_max, Counters& C) {
-    if (wide_walk<true, FX, TOP>(sc, sc.w_oroot, sc.tobjs, sc.w_oblas, r, 0.0, t_max, C).t < t_max) return true;
-    return wide_walk<true, FX, TOP>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, r, 0.0, t_max, C).t < t_max;
+    if (wide_walk<true, FX, TOP, OC>(sc, sc.w_oroot, sc.tobjs, sc.w_oblas, r, 0.0, t_max, C).t < t_max) return true;
+    return wide_walk<true, FX, TOP, OC>(sc, sc.w_lroot, sc.tlights, sc.w_lblas, r, 0.0, t_max, C).t < t_max;
 }
-template <int STK, int FX, bool TOP = false>
+// OC: the wide walks' object leaves as calls (wide_sphere_t_call); no effect on lumo's walks
+template <int STK, int FX, bool TOP = false, bool OC = false>
 __device__ HitRef scene_hit(const DScene& sc, const RayX& r, Counters& C) {
     if constexpr (STK == 0) {
-        return wide_scene_hit<FX, TOP>(sc, r, C);
+        return wide_scene_hit<FX, TOP, OC>(sc, r, C);
     } else {
     HitRef h{DINF, 0, -1, -1};
     double t_max = DINF;
@@ -1373,12 +1397,12 @@ __device__ bool scene_hit_light(const DScene& sc, const RayX& r, int light, DHit
 
 // Scene::hit_light without the record: the light triangle (or PRIM_SPHERE) when visible, else -1;
 // object_record rebuilds the record (the same GEO test).
-template <int STK, int FX, bool TOP = false>
+template <int STK, int FX, bool TOP = false, bool OC = false>
 __device__ int scene_hit_light_tri(const DScene& sc, const RayX& r, int light, Counters& C) {
     DHit lh;
     if constexpr (STK == 0) {
         const int tri = object_hit_tri<kd_stk<STK>(), FX, false>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);
-        if (tri == -1 || wide_occluded<FX, TOP>(sc, r, lh.t - EPSILON, C)) return -1;
+        if (tri == -1 || wide_occluded<FX, TOP, OC>(sc, r, lh.t - EPSILON, C)) return -1;
         return tri;
     } else {
     const int tri = object_hit_tri<STK, FX, TOP>(sc, sc.tlights[light], r, 0.0, DINF, C, lh);

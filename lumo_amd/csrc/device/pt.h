@@ -335,6 +335,31 @@ __global__ __launch_bounds__(BLOCK, FX == 0 ? LUMO_SHADE_WAVES_LEAN : LUMO_SHADE
     }
 }
 
+// the record's ray (planes b .. b + 5)
+__device__ __forceinline__ RayX shadow_ray(const ShadowQ& Q, int b, size_t r) {
+    return rayx(Ray{V3{Q.D(b, r), Q.D(b + 1, r), Q.D(b + 2, r)}, V3{Q.D(b + 3, r), Q.D(b + 4, r), Q.D(b + 5, r)}});
+}
+// mis_sample (integrator.rs:139-184) of a record whose light hit hi is visible
+template <int FX>
+__device__ __forceinline__ DColor shadow_mis(const DScene& sc, const ShadowQ& Q, int b, size_t r, bool li_mode,
+                                             uint32_t p, const RayX& ri, int li, const DHit& hi) {
+    DColor out = cfill(0.0);
+    const lumo_object& Lo = sc.lights[li];
+    const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
+    const double p_sct = Q.D(b + 10, r);
+    if (!(p_lig == 0.0 || p_sct == 0.0)) {
+        double L[NS];
+        for (int k = 0; k < NS; ++k) L[k] = Q.HD(SH_L + k, p);
+        const double denom = p_lig * p_lig + p_sct * p_sct;
+        const double weight = li_mode ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
+        const double p_denom = li_mode ? p_lig : p_sct;
+        const lumo_material hm = sc.mats[hi.material];
+        const DColor f{{Q.D(b + 6, r), Q.D(b + 7, r), Q.D(b + 8, r), Q.D(b + 9, r)}};
+        out = f * cfill(1.0) * emit<FX>(sc, hm, L, hi.backface, hi.uv) * Q.D(b + 11, r) * weight / p_denom;
+    }
+    return out;
+}
+
 // Scene::hit_light + mis_sample of one NEE record (integrator.rs:100-184); plane base b.  The
 // path's wavelengths (header p) are read only after a visible hit, so they are not live across
 // the traversal.
@@ -349,25 +374,13 @@ __device__ __forceinline__ DColor shadow_record_q(const DScene& sc, const Shadow
         return cfill(0.0);
     }
 #endif
-    const RayX ri = rayx(Ray{V3{Q.D(b, r), Q.D(b + 1, r), Q.D(b + 2, r)}, V3{Q.D(b + 3, r), Q.D(b + 4, r), Q.D(b + 5, r)}});
+    const RayX ri = shadow_ray(Q, b, r);
     const int li = Q.I(SI_LIGHT, r);
     DHit hi;
     DColor out = cfill(0.0);
     if (scene_hit_light<STK, FX, TOP>(sc, ri, li, hi, C)) {
         if (visible) *visible = true;
-        const lumo_object& Lo = sc.lights[li];
-        const double p_lig = light_pdf<FX>(sc, Lo, ri, hi.p, hi.ng);
-        const double p_sct = Q.D(b + 10, r);
-        if (!(p_lig == 0.0 || p_sct == 0.0)) {  // mis_sample (integrator.rs:139-184)
-            double L[NS];
-            for (int k = 0; k < NS; ++k) L[k] = Q.HD(SH_L + k, p);
-            const double denom = p_lig * p_lig + p_sct * p_sct;
-            const double weight = li_mode ? (p_lig * p_lig) / denom : (p_sct * p_sct) / denom;
-            const double p_denom = li_mode ? p_lig : p_sct;
-            const lumo_material hm = sc.mats[hi.material];
-            const DColor f{{Q.D(b + 6, r), Q.D(b + 7, r), Q.D(b + 8, r), Q.D(b + 9, r)}};
-            out = f * cfill(1.0) * emit<FX>(sc, hm, L, hi.backface, hi.uv) * Q.D(b + 11, r) * weight / p_denom;
-        }
+        out = shadow_mis<FX>(sc, Q, b, r, li_mode, p, ri, li, hi);
     }
     return out;
 }

@@ -33,10 +33,11 @@ for k, v in summary.items():
     if k.startswith("k_") and "hbm_bytes_per_launch" in v:
         out[k] = {kk: v[kk] for kk in KEYS if kk in v}
 if "k_bdpt_trace_a" in out and "k_bdpt_vis" in out:  # bench.py's BDPT connection unit: both kernels
-    # per bench.py launch: its stage timers count one trace launch (round 5: two k_bdpt_trace_a
-    # dispatches, one per trace list) and one visibility launch per pass and task group
+    # per bench.py launch: its stage timers count one trace launch (two k_bdpt_trace_a dispatches,
+    # one per trace list) and one visibility launch per pass and task group.  k_bdpt_vis is skipped
+    # in a pass without (b) items, so the pass count is the larger of the two estimates.
     a, b = out["k_bdpt_trace_a"], out["k_bdpt_vis"]
-    n = 2 * b["launches"]
+    n = 2 * max(b["launches"], (a["launches"] + 1) // 2)
     out["k_bdpt_trace_a+k_bdpt_vis"] = {
         kk: (a[kk] * a["launches"] + b[kk] * b["launches"]) / n
         for kk in ("hbm_bytes_per_launch", "hbm_bytes_per_launch_raw", "avg_us")}
