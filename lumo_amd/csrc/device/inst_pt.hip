@@ -1,5 +1,8 @@
 // Path-tracing traversal kernels of one kd stack class (compiled once per class with
 // -DLUMO_STK=<class>, see Makefile STK_CLASSES): k_closest, k_shadow, k_trace and their launchers.
+#include <cstdio>
+#include <cstdlib>
+
 #include "launch.h"
 #include "pt.h"
 
@@ -69,24 +72,35 @@ void launch_bounce_q(const TravLaunch& l, const DScene& sc, const Paths& S, cons
     const int grid = l.grid * (BLOCK / nt);
     const size_t rec = tail_only ? 0 : (size_t)PARK_DOUBLES * sizeof(double) * nt;
     const size_t scene = l.lds ? (l.shm + 15) / 16 * 16 : 0;
+#if LUMO_BOUNCE_ARGPTR
+    if (!l.args) {  // every stream of a context has its block (launch_trav)
+        std::fprintf(stderr, "lumo_amd: k_bounce_q launched on a stream without an argument block\n");
+        std::abort();
+    }
+    k_put_args<STK><<<1, 64, 0, l.sm>>>(BounceArgs{sc, S, T, cur, nxt}, l.args);
+#define LUMO_BQ_ARGS (l.args, tail_below, dyn)
+#else
+#define LUMO_BQ_ARGS (sc, S, T, cur, nxt, tail_below, dyn)
+#endif
     auto go = [&](auto TL) {
         constexpr bool TAIL = decltype(TL)::value;
         if (l.fx == 2) {  // textured scenes: no LDS staging variant (as k_shadow_q)
-            k_bounce_q<STK, false, 2, TAIL><<<grid, nt, rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn);
+            k_bounce_q<STK, false, 2, TAIL><<<grid, nt, rec, l.sm>>>LUMO_BQ_ARGS;
         } else if (l.lds) {
             if (l.fx)
-                k_bounce_q<STK, true, 1, TAIL><<<grid, nt, scene + rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn);
+                k_bounce_q<STK, true, 1, TAIL><<<grid, nt, scene + rec, l.sm>>>LUMO_BQ_ARGS;
             else
-                k_bounce_q<STK, true, 0, TAIL><<<grid, nt, scene + rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn);
+                k_bounce_q<STK, true, 0, TAIL><<<grid, nt, scene + rec, l.sm>>>LUMO_BQ_ARGS;
         } else {
-            if (l.fx) k_bounce_q<STK, false, 1, TAIL><<<grid, nt, rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn);
-            else k_bounce_q<STK, false, 0, TAIL><<<grid, nt, rec, l.sm>>>(sc, S, T, cur, nxt, tail_below, dyn);
+            if (l.fx) k_bounce_q<STK, false, 1, TAIL><<<grid, nt, rec, l.sm>>>LUMO_BQ_ARGS;
+            else k_bounce_q<STK, false, 0, TAIL><<<grid, nt, rec, l.sm>>>LUMO_BQ_ARGS;
         }
     };
     if (tail_only)
         go(std::true_type{});
     else
         go(std::false_type{});
+#undef LUMO_BQ_ARGS
 }
 
 template <int STK>

@@ -887,6 +887,7 @@ struct Opts {
 };
 
 struct Ctx {
+    BounceArgs* bargs = nullptr;  // one k_bounce_q argument block per stream (stream, stream2, 3, 4)
     int device = 0;
     size_t lds_cu = 160 * 1024;     // LDS per CU (hipDeviceProp_t::maxSharedMemoryPerMultiProcessor)
     size_t lds_block = 160 * 1024;  // LDS one block may allocate (sharedMemPerBlock)
@@ -1115,6 +1116,9 @@ void launch_trav(Ctx& c, uint64_t count, F&& f, hipStream_t stream = nullptr, bo
     const int grid_full = ceil_div(count, BLOCK);
     TravLaunch l{lds ? std::min(grid_full, c.o.lds_grid) : grid_full, lds ? (size_t)c.sc.hot_bytes : 0, lds,
                  c.sc.full, stream ? stream : c.stream};
+    const hipStream_t ss[4] = {c.stream, c.stream2, c.stream3, c.stream4};
+    for (int i = 0; i < 4; ++i)
+        if (l.sm == ss[i]) l.args = c.bargs + i;
     if (top) {
         l.top = true;
         l.grid = std::min(ceil_div(count, TOP_BLOCK), c.o.top_grid);
@@ -3006,6 +3010,11 @@ lumo_status lumo_create(int device, void** ctx_out) {
         delete c;
         return LUMO_ERR_OOM;
     }
+    if (hipMalloc(reinterpret_cast<void**>(&c->bargs), 4 * sizeof(BounceArgs)) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return LUMO_ERR_OOM;
+    }
     // the environment's overrides of the defaults: integers; the 0 / 1 switches also take
     // on / off, true / false, yes / no.  A value that does not parse is ignored and an
     // out-of-range one clamped, each with a one-line warning on stderr
@@ -3057,6 +3066,7 @@ void lumo_destroy(void* ctx) {
         if (b.p) (void)hipFree(b.p);
     for (int i = 0; i < Ctx::SNAP_RING; ++i) (void)hipEventDestroy(c->snap_ev[i]);
     if (c->snap) (void)hipHostFree(c->snap);
+    if (c->bargs) (void)hipFree(c->bargs);
     if (c->bd_totals_h) (void)hipHostFree(c->bd_totals_h);
     for (int i = 0; i < 4; ++i) (void)hipEventDestroy(c->bd_ev[i]);
     for (int i = 0; i < 4; ++i) {

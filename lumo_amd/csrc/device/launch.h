@@ -23,6 +23,7 @@ struct TravLaunch {
     // TOP staging (k_closest_q / k_shadow_q of scenes too large for `lds`): TOP_BLOCK threads per
     // block, `shm` bytes of LDS (DScene::top_bytes), grid `grid`
     bool top = false;
+    BounceArgs* args = nullptr;  // this stream's BounceArgs block (k_bounce_q, LUMO_BOUNCE_ARGPTR)
 };
 
 template <int STK>

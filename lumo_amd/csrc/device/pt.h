@@ -825,10 +825,29 @@ __device__ __forceinline__ void store_final(const Paths& S, const PathReg& P) { 
 // final radiance (as k_shadow_q).  Neither hits nor records go through HBM.
 // The pipeline's merged passes run their tails pass by pass (each needs its previous pass's ring
 // for Russian roulette): k_split_passes first cuts the unit's queue into one segment per pass.
+// LUMO_BOUNCE_ARGPTR = 1: the arguments through the per-stream BounceArgs block (state.h).  It
+// took k_bounce_q<4, true, 0, false> from 170 to 43 spilled SGPRs (VGPR spills 29 and scratch 112 B
+// unchanged) but not the frame: C1 64-spp 168-172 ms by value, 172-177 ms by pointer; 1/8 share
+// 309-314 / 308-311 ms.  Off by default.
+#ifndef LUMO_BOUNCE_ARGPTR
+#define LUMO_BOUNCE_ARGPTR 0
+#endif
+template <int STK>
+__global__ void k_put_args(BounceArgs a, BounceArgs* out) {
+    if (threadIdx.x == 0) *out = a;
+}
 template <int STK, bool LDS, int FX, bool TAIL>
-__global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_q(DScene sc0, Paths S, Tasks T,
-                                                                                  QState cur, QState nxt,
-                                                                                  uint32_t tail_below, int dyn) {
+__global__ __launch_bounds__(BLOCK, TAIL ? 2 : LUMO_BOUNCE_WAVES) void k_bounce_q(
+#if LUMO_BOUNCE_ARGPTR
+    const BounceArgs* __restrict__ A, uint32_t tail_below, int dyn) {
+    const DScene& sc0 = A->sc;
+    const Paths& S = A->S;
+    const Tasks& T = A->T;
+    const QState& cur = A->cur;
+    const QState& nxt = A->nxt;
+#else
+    DScene sc0, Paths S, Tasks T, QState cur, QState nxt, uint32_t tail_below, int dyn) {
+#endif
     extern __shared__ __attribute__((aligned(16))) char lds_scene[];
     const uint32_t count = S.counts[CNT_CUR];
     if ((count < tail_below) != TAIL) return;      // the other kernel takes this bounce

@@ -188,6 +188,18 @@ struct Tasks {
     int sampler;  // LUMO_SAMPLER_* of the call (samplers.rs:6-17)
 };
 
+// The fused bounce kernel's arguments (pt.h k_bounce_q), read through one pointer to a per-stream
+// device block (LUMO_BOUNCE_ARGPTR) instead of the kernarg segment: by value, the scene, path,
+// task and two queue structs kept about 170 SGPRs live across the bounce loop, which spilled.
+// k_put_args, launched ahead of each k_bounce_q on the same stream, writes the block (stream order:
+// after the previous bounce kernel of that stream has read it).
+struct BounceArgs {
+    DScene sc;
+    Paths S;
+    Tasks T;
+    QState cur, nxt;
+};
+
 struct Dump {
     double *rad, *lam, *raster, *delta;
     unsigned long long* depth;
