@@ -231,3 +231,27 @@ def test_device_exclusive_scan(n):
         d.close()
     want = np.concatenate([[0], np.cumsum(a, dtype=np.uint64)[:-1]]).astype(np.uint32)
     np.testing.assert_array_equal(out, want)
+
+
+def test_wide_lights_only_scene(dev):
+    """A scene of lights only: the objects' tree is empty (root NONE), so every closest hit and
+    visibility walk goes straight to the lights' tree; PT and BDPT tiles equal the oracle's."""
+    from lumo_amd import Material, Spectrum
+    sc = L.Scene()
+    v, f = torus_knot_tube(100, 8)
+    sc.add_mesh(v, f, Material.light(Spectrum.from_rgb(1.0, 0.8, 0.6), scale=0.5), light=True)
+    sc.build()
+    cam = L.Camera.builder().origin(0.0, 0.0, 3.0).towards(0.0, 0.0, 0.0).resolution((32, 32)).build()
+    dev.upload(sc, cam)
+    assert dev.scene_info().accel == 1
+    assert O.wide_export(sc.desc())["obj_root"] == -(1 << 31)
+    tasks = L.make_tasks(32, 32, 4, SEED)
+    bufs, res = dev.render_tasks(tasks)
+    obufs, ores, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, oracle_threads(), accel=1)
+    _tiles_cmp(bufs, res, obufs, ores)
+    assert sum(float(b.sum()) for b in bufs) > 0.0
+    sp, osp = [], []
+    bufs, rr = dev.render_tasks(tasks, integrator=BDPT, splats_out=sp)
+    obufs, orr, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8, integrator=BDPT, splats_out=osp,
+                                   accel=1)
+    _tiles_cmp(bufs, rr, obufs, orr, sp=sp, osp=osp)

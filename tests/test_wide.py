@@ -43,11 +43,17 @@ def _scene(name):
         return light_scene("instanced_rect"), (0.0, 0.5, 4.0)
     if name == "spheres":
         return sphere_scene(env=True), (0.0, 0.3, 4.0)
+    if name == "lights_only":  # the objects' tree is empty (root NONE)
+        sc = L.Scene()
+        v, f = torus_knot_tube(100, 8)
+        sc.add_mesh(v, f, L.Material.light(L.Spectrum.from_rgb(1.0, 0.8, 0.6), scale=0.5), light=True)
+        return sc, (0.0, 0.0, 3.0)
     from lumo_amd.procedural import bistro_standin
     return scenes.bistro(bistro_standin(groups=40, lamps=64, n=4)), (-16.0, 5.0, -1.0)
 
 
-NAMES = ["cornell", "caustics", "zoo", "small_dragon", "tri_lights", "instanced_rect", "spheres", "bistro_small"]
+NAMES = ["cornell", "caustics", "zoo", "small_dragon", "tri_lights", "instanced_rect", "spheres", "bistro_small",
+         "lights_only"]
 
 
 def _leaves(acc, root):
@@ -83,7 +89,7 @@ def test_wide_structure(name):
     d = sc.build().desc()
     acc = O.wide_export(d)
     assert acc["ok"] and 0 <= acc["stack"] <= 64
-    objs = np.ctypeslib.as_array(d.objects, shape=(d.num_objects,))
+    objs = np.ctypeslib.as_array(d.objects, shape=(d.num_objects,)) if d.num_objects else []
     lights = np.ctypeslib.as_array(d.lights, shape=(d.num_lights,))
     tv = acc["tv"]
     reached = set()
