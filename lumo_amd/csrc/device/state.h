@@ -17,7 +17,10 @@ constexpr int BLOCK = 256;
 // Minimum waves per SIMD (register budget) per kernel, tuned by A/B on MI355X.
 // Threads per block of the TOP-staged traversal kernels (dscene.h stage_top_lds): one block holds
 // the LDS of a CU, so it must bring the CU's whole wave budget (16 waves at 4 per SIMD).
-constexpr int TOP_BLOCK = 1024;
+#ifndef LUMO_TOP_BLOCK
+#define LUMO_TOP_BLOCK 1024
+#endif
+constexpr int TOP_BLOCK = LUMO_TOP_BLOCK;
 #ifndef LUMO_CLOSEST_WAVES
 #define LUMO_CLOSEST_WAVES 4
 #endif
