@@ -8,7 +8,8 @@ uniform point of a uniform lamp triangle.  For every ray this walks the exported
 * plain: the objects' tree from the root, any hit, children that pass in node order;
 * hint K: first the subtree of the origin leaf's K-th ancestor; if it holds no occluder, the plain
   walk (the subtree's nodes are counted twice then).
-Nodes visited per ray are reported.  Triangle tests use Moller-Trumbore in f64 (an estimate, not
+Nodes visited per ray are reported, and for an 8-wide tree made by opening each node's
+largest interior children (up to 8 entries) the nodes and child boxes per ray.  Triangle tests use Moller-Trumbore in f64 (an estimate, not
 lumo's watertight test).  Usage: python tools/hint_estimate.py [n_rays]"""
 import os
 import sys
@@ -123,6 +124,60 @@ def main():
                             return True, nv
         return False, nv
 
+    # 8-wide estimate: each 8-wide node = a 4-wide node with its largest-area interior children
+    # opened until 8 entries; walk counts 8-wide nodes and child boxes tested
+    def area(i, k):
+        e = hi[i, :, k] - lo[i, :, k]
+        return e[0] * e[1] + e[1] * e[2] + e[2] * e[0]
+    wide8 = {}
+
+    def entries8(i):
+        if i in wide8:
+            return wide8[i]
+        ent = [(i, k) for k in range(cnt[i])]
+        while True:
+            inner = [e for e in ent if int(ref[e[0], e[1]]) >= 0]
+            if not inner:
+                break
+            e = max(inner, key=lambda e: area(*e))
+            c = int(ref[e[0], e[1]])
+            if len(ent) - 1 + cnt[c] > 8:
+                break
+            ent.remove(e)
+            ent += [(c, k) for k in range(cnt[c])]
+        wide8[i] = ent
+        return ent
+
+    def walk8(root, ro, rd, tmax):
+        inv = 1.0 / np.where(rd == 0, 1e-300, rd)
+        st, nv, nb = [root], 0, 0
+        while st:
+            i = st.pop()
+            nv += 1
+            ent = entries8(i)
+            nb += len(ent)
+            for (nd, k) in reversed(ent):
+                t0 = (lo[nd, :, k] - ro) * inv
+                t1 = (hi[nd, :, k] - ro) * inv
+                tn, tf = np.minimum(t0, t1).max(), np.maximum(t0, t1).min()
+                if not (tn <= tf and tf >= 0 and tn <= tmax):
+                    continue
+                r = int(ref[nd, k])
+                if r >= 0:
+                    st.append(r)
+                else:
+                    x = ~r
+                    for j in range((x >> 4), (x >> 4) + (x & 15)):
+                        if tri_hit(j, ro, rd, tmax):
+                            return True, nv, nb
+        return False, nv, nb
+
+    n8, b8 = [], []
+    for r in range(min(len(origin), 600)):
+        _, nv, nb = walk8(acc["obj_root"], origin[r], sd[r], dist[r] * (1 - 1e-6))
+        n8.append(nv)
+        b8.append(nb)
+
     K = (1, 2, 3)
     plain, hint = [], {k: [] for k in K}
     found = {k: 0 for k in K}
@@ -141,6 +196,8 @@ def main():
             hint[k].append(n1 if h else n1 + nv)
     n = len(plain)
     print(f"rays {n}, occluded {occl / n:.3f}, plain nodes per ray {np.mean(plain):.2f}")
+    print(f"8-wide (first {len(n8)} rays): nodes per ray {np.mean(n8):.2f} against {np.mean(plain[:len(n8)]):.2f}, "
+          f"child boxes per ray {np.mean(b8):.1f}")
     for k in K:
         print(f"hint K={k}: nodes per ray {np.mean(hint[k]):.2f} ({np.mean(hint[k]) / np.mean(plain) - 1:+.1%}), "
               f"occluder found in the subtree for {found[k] / max(occl, 1):.3f} of the occluded rays")
