@@ -255,3 +255,25 @@ def test_wide_lights_only_scene(dev):
     obufs, orr, _ = O.render_tasks(sc.desc(), cam.desc, tasks, O.WAVEFRONT, 8, integrator=BDPT, splats_out=osp,
                                    accel=1)
     _tiles_cmp(bufs, rr, obufs, orr, sp=sp, osp=osp)
+
+
+def test_wide_texture_zoo(dev):
+    """The texture feature class (image / procedural textures, bump map, textured light, HDR
+    environment map) on the wide walks: PT tiles, BDPT tiles and splats equal the oracle's."""
+    from scenes import texture_zoo
+    zoo = texture_zoo().build()
+    cam = default_camera((48, 32))
+    dev.upload(zoo, cam)
+    info = dev.scene_info()
+    assert info.accel == 1 and info.full_kernels == 2
+    tasks = L.make_tasks(48, 32, 8, SEED)
+    bufs, res = dev.render_tasks(tasks)
+    obufs, ores, _ = O.render_tasks(zoo.desc(), cam.desc, tasks, O.WAVEFRONT, oracle_threads(), accel=1)
+    _tiles_cmp(bufs, res, obufs, ores)
+    tasks = L.make_tasks(48, 32, 4, SEED)
+    sp, osp = [], []
+    bufs, rr = dev.render_tasks(tasks, integrator=BDPT, splats_out=sp)
+    obufs, orr, _ = O.render_tasks(zoo.desc(), cam.desc, tasks, O.WAVEFRONT, 8, integrator=BDPT, splats_out=osp,
+                                   accel=1)
+    assert sum(len(s) for s in osp) > 0
+    _tiles_cmp(bufs, rr, obufs, orr, sp=sp, osp=osp)
